@@ -1,0 +1,243 @@
+// ref_dump.cpp -- TEST INFRASTRUCTURE.  Harness that links the *unmodified* reference sources
+// (compiled in place from /root/reference/src by oracle/Makefile target `ref`) and dumps golden
+// vectors for the parity tests.  Nothing here ships: the binary lands in oracle/_ref/ (gitignored)
+// and only the text fixtures it writes are committed under tests/golden/.
+//
+// The reference reads XMLBIF through tinyxml2, which is absent from this image, so the network
+// is populated here through the reference's own public model API in exactly the order
+// XMLBIFParser does it (src/XMLBIFParser.cpp:33-179): nodes in <VARIABLE> order,
+// AddParent/AddChild in <GIVEN> order, TABLE read node-major with NaryCount
+// (src/common.cpp:193-232) and AddCount(query, parents, p*10000) (src/XMLBIFParser.cpp:176).
+//
+// Modes
+//   jt  <net.xml> <libsvm test set> <pt file|-> <out prefix> [max_cases]
+//       writes <prefix>.plan (junction-tree plan after ReorganizeTableStorage),
+//              <prefix>.init (initial clique potentials, %.17g),
+//              <prefix>.marg (per case: label + all node marginals, %.17g)
+//   ci  <csv> <tests file> <out>
+//       counts N_xyz for every (x, y, Z) line of <tests file> with the reference Counts2D/Counts3D
+//       (src/CellTable.cpp:174-291,430-455) and writes them with the dataset's domains.
+#include <cstdio>
+#include <fstream>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "CellTable.h"
+#include "Dataset.h"
+#include "DiscreteNode.h"
+#include "JunctionTree.h"
+#include "Network.h"
+#include "Timer.h"
+#include "common.h"
+
+#include "../mini_xml.h"
+
+// ---------------------------------------------------------------------------------------------
+// network population through the reference API
+static Network *LoadXmlbifIntoReference(const std::string &path) {
+    auto doc = mini_xml::parse_file(path);
+    const mini_xml::Element *net = doc->first("BIF")->first("NETWORK");
+    std::vector<Node *> nodes;
+    for (const mini_xml::Element *xv : net->all("VARIABLE")) {
+        if (Trim(const_cast<std::string &>(xv->first("TYPE")->text)) != "discrete") continue;
+        auto *n = new DiscreteNode((int)nodes.size());
+        std::string nm = xv->first("NAME")->text;
+        n->node_name = Trim(nm);
+        for (const mini_xml::Element *val : xv->all("VALUE")) {
+            std::string v = val->text;
+            n->vec_str_potential_vals.push_back(Trim(v));
+        }
+        n->SetDomainSize((int)n->vec_str_potential_vals.size());
+        nodes.push_back(n);
+    }
+    auto find = [&](std::string name) -> Node * {
+        name = Trim(name);
+        for (Node *p : nodes)
+            if (p->node_name == name) return p;
+        fprintf(stderr, "unknown variable %s\n", name.c_str());
+        exit(1);
+    };
+    for (const mini_xml::Element *xp : net->all("PROBABILITY")) {
+        auto *for_np = dynamic_cast<DiscreteNode *>(find(xp->first("FOR")->text));
+        std::vector<Node *> given;
+        for (const mini_xml::Element *g : xp->all("GIVEN")) given.push_back(find(g->text));
+        for (Node *g : given) {
+            for_np->AddParent(g);
+            g->AddChild(for_np);
+        }
+        std::string table = xp->first("TABLE")->text;
+        table = Trim(table);
+        std::vector<std::string> toks = Split(table, " ");
+        std::vector<double> entries;
+        for (auto &t : toks) entries.push_back(stod(t));
+        std::vector<int> range;
+        range.push_back(for_np->GetDomainSize());
+        for (Node *g : given) range.push_back(dynamic_cast<DiscreteNode *>(g)->GetDomainSize());
+        std::vector<std::vector<int>> counts = NaryCount(range);
+        if (counts.size() != entries.size()) {
+            fprintf(stderr, "table size mismatch for %s\n", for_np->node_name.c_str());
+            exit(1);
+        }
+        for (size_t i = 0; i < counts.size(); ++i) {
+            DiscreteConfig comb;
+            for (size_t j = 1; j < counts[i].size(); ++j)
+                comb.insert(std::pair<int, int>(given[j - 1]->GetNodeIndex(), counts[i][j]));
+            for_np->AddCount(counts[i][0], comb, entries.at(i) * 10000);
+        }
+    }
+    Network *network = new Network(nodes, "xmlbif");
+    network->GetTopoOrd();
+    return network;
+}
+
+// ---------------------------------------------------------------------------------------------
+class JTHarness : public JunctionTree {
+public:
+    JTHarness(Network *net, Dataset *dts) : JunctionTree(net, dts, false) {}
+
+    void DumpPlan(const std::string &path_plan, const std::string &path_init) {
+        std::map<const Clique *, int> cid, sid;
+        auto &C = tree->vector_clique_ptr_container;
+        auto &S = tree->vector_separator_ptr_container;
+        for (size_t i = 0; i < C.size(); ++i) cid[C[i]] = (int)i;
+        for (size_t i = 0; i < S.size(); ++i) sid[S[i]] = (int)i;
+        FILE *f = fopen(path_plan.c_str(), "w");
+        fprintf(f, "cliques %zu\n", C.size());
+        for (size_t i = 0; i < C.size(); ++i) {
+            const PotentialTable &t = clique_backup[i].p_table;
+            fprintf(f, "c %zu %d %d", i, t.num_variables, t.table_size);
+            for (int v : t.vec_related_variables) fprintf(f, " %d", v);
+            fprintf(f, " | up %d | down", C[i]->ptr_upstream_clique ? sid[C[i]->ptr_upstream_clique] : -1);
+            for (auto *d : C[i]->ptr_downstream_cliques) fprintf(f, " %d", sid[d]);
+            fprintf(f, "\n");
+        }
+        fprintf(f, "seps %zu\n", S.size());
+        for (size_t i = 0; i < S.size(); ++i) {
+            const PotentialTable &t = separator_backup[i].p_table;
+            fprintf(f, "s %zu %d %d", i, t.num_variables, t.table_size);
+            for (int v : t.vec_related_variables) fprintf(f, " %d", v);
+            fprintf(f, " | up %d | down", cid[S[i]->ptr_upstream_clique]);
+            for (auto *d : S[i]->ptr_downstream_cliques) fprintf(f, " %d", cid[d]);
+            fprintf(f, "\n");
+        }
+        fprintf(f, "root %d\n", cid[jt_root]);
+        fprintf(f, "levels %d\n", max_level);
+        for (int l = 0; l < max_level; ++l) {
+            fprintf(f, "level %d %c", l, (l % 2) ? 's' : 'c');
+            for (auto *n : nodes_by_level[l]) fprintf(f, " %d", (l % 2) ? sid[n] : cid[n]);
+            fprintf(f, "\n");
+        }
+        fclose(f);
+        f = fopen(path_init.c_str(), "w");
+        for (size_t i = 0; i < C.size(); ++i) {
+            const PotentialTable &t = clique_backup[i].p_table;
+            fprintf(f, "c %zu %d", i, t.table_size);
+            for (double p : t.potentials) fprintf(f, " %.17g", p);
+            fprintf(f, "\n");
+        }
+        fclose(f);
+    }
+
+    void DumpCases(const std::string &pt_path, const std::string &out_path, int max_cases) {
+        if (pt_path != "-") {
+            LoadGroundTruthProbabilityTable(pt_path);
+        } else {
+            ground_truth_probability_tables.assign(num_instances, std::vector<std::vector<double>>());
+            for (auto &c : ground_truth_probability_tables) {
+                c.resize(network->num_nodes);
+                for (int j = 0; j < network->num_nodes; ++j)
+                    c[j].assign(dynamic_cast<DiscreteNode *>(network->FindNodePtrByIndex(j))->GetDomainSize(), 0.0);
+            }
+        }
+        int n = num_instances;
+        if (max_cases > 0 && max_cases < n) n = max_cases;
+        Timer timer;
+        double mse = 0.0, hd = 0.0;
+        FILE *f = fopen(out_path.c_str(), "w");
+        for (int i = 0; i < n; ++i) {
+            int label = PredictUseJTInfer(evidences.at(i), i, mse, hd, 1, &timer);
+            fprintf(f, "case %d label %d\n", i, label);
+            for (int v = 0; v < network->num_nodes; ++v) {
+                for (size_t d = 0; d < probs_one_sample[v].size(); ++d)
+                    fprintf(f, "%s%.17g", d ? " " : "", probs_one_sample[v][d]);
+                fprintf(f, "\n");
+            }
+        }
+        fprintf(f, "mse_sum %.17g hd_sum %.17g\n", mse, hd);
+        fclose(f);
+    }
+};
+
+static int RunJT(int argc, char **argv) {
+    if (argc < 6) return 2;
+    Network *net = LoadXmlbifIntoReference(argv[2]);
+    auto *tester = new Dataset();
+    tester->LoadLIBSVMDataKnownNetwork(argv[3], net->num_nodes);
+    JTHarness jt(net, tester);
+    std::string prefix = argv[5];
+    jt.DumpPlan(prefix + ".plan", prefix + ".init");
+    jt.DumpCases(argv[4], prefix + ".marg", argc > 6 ? atoi(argv[6]) : 0);
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+static unsigned long long Fnv1a(const int *col, int n) {
+    unsigned long long h = 1469598103934665603ull;
+    for (int i = 0; i < n; ++i) {
+        h ^= (unsigned long long)(unsigned)col[i];
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+
+static int RunCI(int argc, char **argv) {
+    if (argc < 5) return 2;
+    auto *dts = new Dataset();
+    dts->LoadCSVData(argv[2], true, true, 0);
+    std::ifstream tin(argv[3]);
+    FILE *f = fopen(argv[4], "w");
+    fprintf(f, "vars %d samples %d\n", dts->num_vars, dts->num_instance);
+    fprintf(f, "dims");
+    for (int v = 0; v < dts->num_vars; ++v) fprintf(f, " %d", dts->num_of_possible_values_of_disc_vars[v]);
+    fprintf(f, "\n");
+    for (int v = 0; v < dts->num_vars; ++v)
+        fprintf(f, "colhash %d %llu\n", v, Fnv1a(dts->dataset_columns[v], dts->num_instance));
+    std::string line;
+    Timer timer;
+    while (std::getline(tin, line)) {
+        line = Trim(line);
+        if (line.empty()) continue;
+        std::vector<std::string> tok = Split(line, " ");
+        int x = stoi(tok[0]), y = stoi(tok[1]);
+        std::vector<int> z;
+        for (size_t i = 2; i < tok.size(); ++i) z.push_back(stoi(tok[i]));
+        int dx = dts->num_of_possible_values_of_disc_vars[x];
+        int dy = dts->num_of_possible_values_of_disc_vars[y];
+        fprintf(f, "test %d %d %zu", x, y, z.size());
+        for (int zz : z) fprintf(f, " %d", zz);
+        if (z.empty()) {
+            Counts2D t(dx, dy, x, y);
+            t.FillTable(dts, &timer);
+            fprintf(f, " cells %d :", dx * dy);
+            for (int i = 0; i < dx * dy; ++i) fprintf(f, " %d", t.n[i]);
+        } else {
+            std::vector<int> cd;
+            for (int zz : z) cd.push_back(dts->num_of_possible_values_of_disc_vars[zz]);
+            Counts3D t(dx, dy, x, y, cd, z);
+            t.FillTable(dts, &timer);
+            fprintf(f, " cells %d :", t.dimz * dx * dy);
+            for (int i = 0; i < t.dimz * dx * dy; ++i) fprintf(f, " %d", t.n[i]);
+        }
+        fprintf(f, "\n");
+    }
+    fclose(f);
+    return 0;
+}
+
+int main(int argc, char **argv) {
+    if (argc >= 2 && std::string(argv[1]) == "jt") return RunJT(argc, argv);
+    if (argc >= 2 && std::string(argv[1]) == "ci") return RunCI(argc, argv);
+    fprintf(stderr, "usage: ref_dump jt|ci ...\n");
+    return 2;
+}
