@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""Benchmark of the two FastBN hot paths on MI355X (BASELINE.json metric).
+
+Headline `value` = junction-tree test cases / s on ALARM (BASELINE config 2: 100k synthetic cases
+per GPU per step, 7 evidence variables per case, inputs resident in HBM, labels + all marginals
+written back to HBM).  A "step" is one pass of the batched JT kernel over the 100k cases.  With
+--gpus N (torchrun, one process per GPU) every rank processes its own 100k-case shard (seed +
+rank, no data-path collective) -> weak scaling; `value` = all cases / max-over-ranks time.
+
+Also reported (rank 0, N = 1): PC-stable CI-tests / s on alarm_s5000.txt (BASELINE config 3,
+reference-equivalent test count), the dominant kernel's HBM roofline (algorithmic bytes per case =
+16*(sum clique + separator entries) + 8*sum dom + V = 22,877 B) and the CPU baseline
+(the unmodified reference's per-case loop, oracle/_ref, timed on this host on a bounded sample).
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+ALARM = os.path.join(REPO, "tests", "golden", "alarm")
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+CASES_PER_GPU = 100_000
+EVIDENCE_PER_CASE = 7
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline_jt(budget_cases=40_000):
+    """Reference per-case loop (oracle/_ref/ref_dump jtbench, t = 1) on a bounded sample."""
+    from fastbn_amd import synth
+    net = synth.read_xmlbif(os.path.join(ALARM, "alarm.xml"))
+    ev = synth.evidence_cases(net, budget_cases, EVIDENCE_PER_CASE, seed=20250131)
+    ref = os.path.join(REPO, "oracle", "_ref", "ref_dump")
+    if os.path.exists(ref):
+        with tempfile.TemporaryDirectory() as td:
+            path = os.path.join(td, "ev.libsvm")
+            with open(path, "w") as f:
+                for r in ev:
+                    f.write("0 " + " ".join(f"{v}:{r[v]}" for v in range(r.size) if r[v] >= 0) + " \n")
+            out = subprocess.run([ref, "jtbench", os.path.join(ALARM, "alarm.xml"),
+                                  os.path.join(ALARM, "testing_alarm_1k_p20"), path, str(budget_cases)],
+                                 check=True, capture_output=True, text=True).stdout
+            secs = float(out.split()[3])
+            kind = "reference"
+    else:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle as O
+        o = O.OracleJT(os.path.join(ALARM, "alarm.xml"))
+        t0 = time.perf_counter()
+        o.infer(ev)
+        secs = time.perf_counter() - t0
+        kind = "port"
+    return {"value": budget_cases / secs, "unit": "cases/s", "cores": 1, "kind": kind,
+            "sample": f"{budget_cases} ALARM cases (7 evidence vars, seed 20250131), per-case loop at t=1 "
+                      f"(the reference is fastest at 1 thread on ALARM), {secs:.2f} s"}
+
+
+def cpu_baseline_pc(reps=40):
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    ds = O.OracleDataset(csv=os.path.join(ALARM, "alarm_s5000.txt"))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        r = ds.pc_stable(0.05, 1000, 1)
+    secs = (time.perf_counter() - t0) / reps
+    return {"value": r["num_ci_test"] / secs, "unit": "CI-tests/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} full PC-stable skeleton runs on alarm_s5000 (5206 tests each), "
+                      f"{secs * 1e3:.1f} ms/run"}
+
+
+def bench_pc(steps, warmup):
+    import fastbn_amd as F
+    ds = F.Dataset(os.path.join(ALARM, "alarm_s5000.txt"))
+    pc = F.PCStable(0.05, 1000)
+    for _ in range(max(1, warmup)):
+        pc.StructLearnCompData(ds)
+    t = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        pc.StructLearnCompData(ds)
+        t.append(time.perf_counter() - t0)
+    ms = 1e3 * float(np.median(t))
+    return {"metric": "PC-stable CI-tests/sec (alarm_s5000, levels 0-4)", "value": pc.num_ci_test / (ms * 1e-3),
+            "unit": "CI-tests/s", "tests": pc.num_ci_test, "tests_per_level": pc.tests_per_level.tolist(),
+            "launched_per_level": pc.launched_per_level.tolist(), "ms_per_run": ms,
+            "kernel_ms_per_run": 1e3 * pc.kernel_s, "edges": len(pc.edges)}
+
+
+def load_traffic(per_case_bytes):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if present."""
+    path = os.path.join(REPO, "profiles", "jt_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        t = json.load(f)
+    return t.get("hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--cases", type=int, default=CASES_PER_GPU)
+    ap.add_argument("--waves-per-cu", type=int, default=0)
+    ap.add_argument("--no-baseline", action="store_true")
+    ap.add_argument("--no-pc", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+
+    import fastbn_amd as F
+    from fastbn_amd import synth
+
+    net_py = synth.read_xmlbif(os.path.join(ALARM, "alarm.xml"))
+    ev = synth.evidence_cases(net_py, args.cases, EVIDENCE_PER_CASE, seed=20250131 + rank)
+    jt = F.JunctionTree(F.Network(os.path.join(ALARM, "alarm.xml")), device=local)
+    if args.waves_per_cu:
+        jt.set_waves_per_cu(args.waves_per_cu)
+    info = jt.info
+    dev = torch.device("cuda", local)
+    d_ev = torch.from_numpy(ev).to(dev)
+    d_lab = torch.empty(args.cases, dtype=torch.int32, device=dev)
+    d_marg = torch.empty((args.cases, info["sum_dom"]), dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        jt.run_device(d_ev.data_ptr(), args.cases, d_lab.data_ptr(), d_marg.data_ptr(), stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    ev_pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev_pairs[i][0].record(stream)
+        step()
+        ev_pairs[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_pairs]))
+
+    # sanity: labels of the last step agree with a CPU recomputation on a few cases (not timed)
+    if rank == 0:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle as O
+        olab, omarg = O.OracleJT(os.path.join(ALARM, "alarm.xml")).infer(ev[:256])
+        ok = (d_lab[:256].cpu().numpy() == olab).all() and (d_marg[:256].cpu().numpy() == omarg).all()
+        if not ok:
+            log("ERROR: GPU results differ from the oracle")
+            sys.exit(1)
+
+    total_cases = args.cases * args.steps * world
+    value = total_cases / elapsed
+    bpc = info["algorithmic_bytes_per_case"]
+    achieved = bpc * args.cases / (kernel_ms * 1e-3) / 1e9
+    traffic = load_traffic(bpc)
+    out = {
+        "metric": "JT test-cases/sec (ALARM, Munin) + PC-stable CI-tests/sec, 1/2/4/8 GPU",
+        "value": value,
+        "unit": "cases/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (ALARM forward samples, seed 20250131+rank)",
+        "config": {"workload": "ALARM (37 vars) JT inference, 100k synthetic cases per GPU @ 7 evidence vars "
+                               "(BASELINE config 2)", "cases_per_gpu": args.cases,
+                   "evidence_per_case": EVIDENCE_PER_CASE, "parallelism": f"case-sharded x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel_ms": kernel_ms, "algorithmic_bytes_per_case": bpc},
+    }
+    if rank == 0 and world == 1:
+        if not args.no_pc:
+            out["pc_stable"] = bench_pc(max(5, args.steps // 2), args.warmup)
+        if not args.no_baseline:
+            out["cpu_baseline"] = cpu_baseline_jt()
+            if "pc_stable" in out:
+                out["pc_stable"]["cpu_baseline"] = cpu_baseline_pc()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

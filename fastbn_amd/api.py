@@ -1,0 +1,320 @@
+"""ctypes binding of include/fastbn.h and the reference-shaped Python classes."""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfastbn.so")
+
+_vp, _i32, _i64, _dbl, _cstr = C.c_void_p, C.c_int32, C.c_int64, C.c_double, C.c_char_p
+_pp = C.POINTER(C.c_void_p)
+
+# name -> argtypes (all functions return int status except fbn_last_error)
+_SIGS = {
+    "fbn_version": [_vp, _vp],
+    "fbn_device_count": [_vp],
+    "fbn_network_load_xmlbif": [_cstr, _pp],
+    "fbn_network_num_nodes": [_vp, _vp],
+    "fbn_network_dims": [_vp, _vp],
+    "fbn_network_name": [_vp, C.c_int, C.c_char_p, C.c_int],
+    "fbn_network_destroy": [_vp],
+    "fbn_evidence_load_libsvm": [_cstr, C.c_int, _vp, _vp, _i64, _vp],
+    "fbn_dataset_load_csv": [_cstr, _pp],
+    "fbn_dataset_shape": [_vp, _vp, _vp],
+    "fbn_dataset_dims": [_vp, _vp],
+    "fbn_dataset_columns": [_vp, _vp],
+    "fbn_dataset_var_name": [_vp, C.c_int, C.c_char_p, C.c_int],
+    "fbn_dataset_destroy": [_vp],
+    "fbn_jt_plan_create": [_vp, C.c_int, _pp],
+    "fbn_jt_plan_info_get": [_vp, _vp],
+    "fbn_jt_plan_dump": [_vp, _cstr, _cstr],
+    "fbn_jt_run": [_vp, _vp, _i64, _vp, _vp, _vp],
+    "fbn_jt_run_device": [_vp, _vp, _i64, _vp, _vp, _vp],
+    "fbn_jt_score": [_vp, _vp, _vp, _i64, _vp, _vp],
+    "fbn_jt_last_kernel_ms": [_vp, _vp],
+    "fbn_jt_set_waves_per_cu": [_vp, C.c_int],
+    "fbn_jt_plan_destroy": [_vp],
+    "fbn_ci_dataset_upload": [_vp, C.c_int, _i64, _vp, C.c_int, _pp],
+    "fbn_ci_run": [_vp, _vp, _i64, C.c_int, _dbl, _vp, _vp, _vp, _vp, _vp],
+    "fbn_ci_counts": [_vp, C.c_int, C.c_int, _vp, C.c_int, _vp, _i64, _vp],
+    "fbn_ci_last_kernel_ms": [_vp, _vp],
+    "fbn_ci_ctx_destroy": [_vp],
+    "fbn_pc_stable": [_vp, _dbl, C.c_int, C.c_int, _pp],
+    "fbn_pc_num_levels": [_vp, _vp],
+    "fbn_pc_level_tests": [_vp, _vp],
+    "fbn_pc_level_launched": [_vp, _vp],
+    "fbn_pc_num_edges": [_vp, _vp],
+    "fbn_pc_edges": [_vp, _vp],
+    "fbn_pc_sepsets": [_vp, _vp, _i64, _vp],
+    "fbn_pc_timing": [_vp, _vp, _vp],
+    "fbn_pc_result_destroy": [_vp],
+}
+
+
+class FastBNError(RuntimeError):
+    pass
+
+
+class _Lib:
+    """Lazily loaded libfastbn.so.  Missing library => every call raises (no CPU fallback)."""
+
+    def __init__(self):
+        self._h = None
+
+    def load(self):
+        if self._h is None:
+            if not os.path.exists(LIB_PATH):
+                raise FastBNError(f"{LIB_PATH} is missing: run __graft_entry__.build() (no CPU fallback)")
+            h = C.CDLL(LIB_PATH)
+            for name, args in _SIGS.items():
+                f = getattr(h, name)
+                f.argtypes = args
+                f.restype = C.c_int
+            h.fbn_last_error.restype = C.c_char_p
+            h.fbn_last_error.argtypes = []
+            self._h = h
+        return self._h
+
+    def __getattr__(self, name):
+        h = self.load()
+        f = getattr(h, name)
+        if name == "fbn_last_error":
+            return f
+
+        def call(*args):
+            rc = f(*args)
+            if rc != 0:
+                raise FastBNError(f"{name}: {h.fbn_last_error().decode()} (code {rc})")
+            return rc
+
+        return call
+
+
+lib = _Lib()
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+def device_count():
+    n = C.c_int(0)
+    lib.fbn_device_count(C.byref(n))
+    return n.value
+
+
+class _PlanInfo(C.Structure):
+    _fields_ = [("num_nodes", C.c_int32), ("num_cliques", C.c_int32), ("num_separators", C.c_int32),
+                ("num_levels", C.c_int32), ("root", C.c_int32), ("sum_dom", C.c_int32),
+                ("clique_entries", C.c_int64), ("separator_entries", C.c_int64),
+                ("algorithmic_bytes_per_case", C.c_int64), ("num_ops", C.c_int32),
+                ("max_vars_per_table", C.c_int32)]
+
+
+class Network:
+    """Discrete BN loaded from XMLBIF (CustomNetwork::GetNetFromXMLBIFFile)."""
+
+    def __init__(self, path):
+        h = C.c_void_p()
+        lib.fbn_network_load_xmlbif(os.fsencode(path), C.byref(h))
+        self._h = h
+        n = C.c_int()
+        lib.fbn_network_num_nodes(h, C.byref(n))
+        self.num_nodes = n.value
+        self.dims = np.zeros(self.num_nodes, np.int32)
+        lib.fbn_network_dims(h, _p(self.dims))
+
+    def name(self, i):
+        buf = C.create_string_buffer(256)
+        lib.fbn_network_name(self._h, i, buf, 256)
+        return buf.value.decode()
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib.fbn_network_destroy(self._h)
+            self._h = None
+
+
+def load_libsvm(path, num_nodes):
+    """Dataset::LoadLIBSVMDataKnownNetwork + Inference evidence extraction -> (evidence, labels)."""
+    n = C.c_int64()
+    lib.fbn_evidence_load_libsvm(os.fsencode(path), num_nodes, None, None, 0, C.byref(n))
+    ev = np.zeros((n.value, num_nodes), np.int8)
+    lab = np.zeros(n.value, np.int32)
+    lib.fbn_evidence_load_libsvm(os.fsencode(path), num_nodes, _p(ev), _p(lab), n.value, C.byref(n))
+    return ev, lab
+
+
+class Dataset:
+    """CSV training set with first-appearance value coding (Dataset::LoadCSVData)."""
+
+    def __init__(self, path=None, columns=None, dims=None):
+        if path is not None:
+            h = C.c_void_p()
+            lib.fbn_dataset_load_csv(os.fsencode(path), C.byref(h))
+            nv, ns = C.c_int(), C.c_int64()
+            lib.fbn_dataset_shape(h, C.byref(nv), C.byref(ns))
+            self.dims = np.zeros(nv.value, np.int32)
+            self.columns = np.zeros((nv.value, ns.value), np.uint8)
+            lib.fbn_dataset_dims(h, _p(self.dims))
+            lib.fbn_dataset_columns(h, _p(self.columns))
+            self.names = []
+            buf = C.create_string_buffer(256)
+            for v in range(nv.value):
+                lib.fbn_dataset_var_name(h, v, buf, 256)
+                self.names.append(buf.value.decode())
+            lib.fbn_dataset_destroy(h)
+        else:
+            self.columns = np.ascontiguousarray(columns, dtype=np.uint8)
+            self.dims = np.ascontiguousarray(dims, dtype=np.int32)
+            self.names = [str(i) for i in range(self.columns.shape[0])]
+
+    @property
+    def num_vars(self):
+        return self.columns.shape[0]
+
+    @property
+    def num_instance(self):
+        return self.columns.shape[1]
+
+
+class JunctionTree:
+    """Batched JT inference on one device (JunctionTree ctor + PredictUseJTInfer over all cases)."""
+
+    def __init__(self, network, device=0):
+        self.network = network
+        h = C.c_void_p()
+        lib.fbn_jt_plan_create(network._h, device, C.byref(h))
+        self._h = h
+        info = _PlanInfo()
+        lib.fbn_jt_plan_info_get(h, C.byref(info))
+        self.info = {k: getattr(info, k) for k, _ in _PlanInfo._fields_}
+
+    def dump_plan(self, plan_path, init_path):
+        lib.fbn_jt_plan_dump(self._h, os.fsencode(plan_path), os.fsencode(init_path))
+
+    def set_waves_per_cu(self, w):
+        lib.fbn_jt_set_waves_per_cu(self._h, w)
+
+    def infer(self, evidence, marginals=True):
+        """evidence [ncases][num_nodes] int8 (-1 unobserved) -> (labels, marginals or None)."""
+        ev = np.ascontiguousarray(evidence, dtype=np.int8)
+        n = ev.shape[0]
+        labels = np.zeros(n, np.int32)
+        marg = np.zeros((n, self.info["sum_dom"]), np.float64) if marginals else None
+        lib.fbn_jt_run(self._h, _p(ev), n, _p(labels), _p(marg), None)
+        return labels, marg
+
+    def run_device(self, d_evidence_ptr, ncases, d_labels_ptr, d_marg_ptr, stream_ptr=None):
+        lib.fbn_jt_run_device(self._h, d_evidence_ptr, ncases, d_labels_ptr, d_marg_ptr, stream_ptr)
+
+    def last_kernel_ms(self):
+        ms = C.c_float()
+        lib.fbn_jt_last_kernel_ms(self._h, C.byref(ms))
+        return ms.value
+
+    def score(self, marginals, golden):
+        mse, hd = C.c_double(), C.c_double()
+        m = np.ascontiguousarray(marginals, np.float64)
+        g = np.ascontiguousarray(golden, np.float64)
+        lib.fbn_jt_score(self._h, _p(m), _p(g), m.shape[0], C.byref(mse), C.byref(hd))
+        return mse.value, hd.value
+
+    def EvaluateAccuracy(self, evidence, ground_truths, golden=None):
+        """Accuracy of the query-variable arg-max (+ average MSE/HD vs golden if given)."""
+        labels, marg = self.infer(evidence)
+        acc = float(np.mean(labels == np.asarray(ground_truths)))
+        if golden is None:
+            return acc
+        mse, hd = self.score(marg, golden)
+        return acc, mse / len(labels), hd / len(labels)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib.fbn_jt_plan_destroy(self._h)
+            self._h = None
+
+
+class IndependenceTest:
+    """G^2 tests on the device (IndependenceTest::IndependenceResult, batched)."""
+
+    def __init__(self, dataset, alpha=0.05, device=0):
+        self.alpha = alpha
+        h = C.c_void_p()
+        lib.fbn_ci_dataset_upload(_p(dataset.columns), dataset.num_vars, dataset.num_instance,
+                                  _p(dataset.dims), device, C.byref(h))
+        self._h = h
+
+    def run(self, items, d):
+        items = np.ascontiguousarray(items, dtype=np.int32).reshape(-1, 2 + d)
+        n = items.shape[0]
+        g2 = np.zeros(n)
+        df = np.zeros(n, np.int32)
+        p = np.zeros(n)
+        ind = np.zeros(n, np.uint8)
+        lib.fbn_ci_run(self._h, _p(items), n, d, self.alpha, _p(g2), _p(df), _p(p), _p(ind), None)
+        return g2, df, p, ind.astype(bool)
+
+    def IndependenceResult(self, x, y, z=()):
+        g2, df, p, ind = self.run(np.array([[x, y, *z]], np.int32), len(z))
+        return {"g2": g2[0], "df": int(df[0]), "p_value": p[0], "is_independent": bool(ind[0])}
+
+    def counts(self, x, y, z=()):
+        zz = np.array(z, np.int32)
+        cells = C.c_int64()
+        lib.fbn_ci_counts(self._h, x, y, _p(zz) if len(z) else None, len(z), None, 0, C.byref(cells))
+        out = np.zeros(cells.value, np.int32)
+        lib.fbn_ci_counts(self._h, x, y, _p(zz) if len(z) else None, len(z), _p(out), cells.value,
+                          C.byref(cells))
+        return out
+
+    def last_kernel_ms(self):
+        ms = C.c_float()
+        lib.fbn_ci_last_kernel_ms(self._h, C.byref(ms))
+        return ms.value
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib.fbn_ci_ctx_destroy(self._h)
+            self._h = None
+
+
+class PCStable:
+    """PC-stable skeleton search (PCStable(net, alpha, depth).StructLearnCompData)."""
+
+    def __init__(self, alpha=0.05, depth=1000, device=0):
+        self.alpha, self.depth, self.device = alpha, depth, device
+
+    def StructLearnCompData(self, dataset, group_size=1, num_threads=1, print_struct=False, verbose=False):
+        ci = IndependenceTest(dataset, self.alpha, self.device)
+        r = C.c_void_p()
+        lib.fbn_pc_stable(ci._h, self.alpha, self.depth, group_size, C.byref(r))
+        try:
+            nl, ne = C.c_int(), C.c_int()
+            lib.fbn_pc_num_levels(r, C.byref(nl))
+            self.tests_per_level = np.zeros(nl.value, np.int64)
+            self.launched_per_level = np.zeros(nl.value, np.int64)
+            lib.fbn_pc_level_tests(r, _p(self.tests_per_level))
+            lib.fbn_pc_level_launched(r, _p(self.launched_per_level))
+            lib.fbn_pc_num_edges(r, C.byref(ne))
+            e = np.zeros((ne.value, 2), np.int32)
+            if ne.value:
+                lib.fbn_pc_edges(r, _p(e))
+            self.edges = [tuple(map(int, x)) for x in e]
+            ln = C.c_int64()
+            lib.fbn_pc_sepsets(r, None, 0, C.byref(ln))
+            buf = np.zeros(max(ln.value, 1), np.int32)
+            lib.fbn_pc_sepsets(r, _p(buf), ln.value, C.byref(ln))
+            self.sepset, k = {}, 0
+            while k < ln.value:
+                x, y, m = map(int, buf[k:k + 3])
+                self.sepset[(x, y)] = tuple(int(v) for v in buf[k + 3:k + 3 + m])
+                k += 3 + m
+            tot, ker = C.c_double(), C.c_double()
+            lib.fbn_pc_timing(r, C.byref(tot), C.byref(ker))
+            self.total_s, self.kernel_s = tot.value, ker.value
+            self.num_ci_test = int(self.tests_per_level.sum())
+        finally:
+            lib.fbn_pc_result_destroy(r)
+        return self

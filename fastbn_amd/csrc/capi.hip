@@ -1,0 +1,624 @@
+// capi.hip -- the extern "C" boundary (include/fastbn.h): handles, device memory, uploads, launches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+
+#include "fbn_internal.h"
+#include "pc_internal.h"
+
+extern "C" hipError_t fbn_jt_launch(const JtOp *ops, int nops, const int32_t *aux, const double *initv,
+                                    const uint64_t *dig, const int8_t *evid, int V, long long ncases, int SD,
+                                    double *marg, int32_t *labels, double *ws, int32_t *wsi, long long NE, int nc,
+                                    int grid, hipStream_t stream);
+extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, const int32_t *items, long long N,
+                                    long long n, int d, double alpha, double *g2, int32_t *df, double *p,
+                                    uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
+                                    hipStream_t stream);
+extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy);
+
+namespace fbn {
+const char *LastError();
+}
+using fbn::SetError;
+
+#define FBN_HIP(call)                                                                              \
+    do {                                                                                           \
+        hipError_t e_ = (call);                                                                    \
+        if (e_ != hipSuccess) return SetError(FBN_ERR_HIP, "%s: %s", #call, hipGetErrorString(e_)); \
+    } while (0)
+
+namespace {
+
+// growable device buffer
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    int ensure(size_t b) {
+        if (b <= bytes) return FBN_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        if (b == 0) return FBN_OK;
+        hipError_t e = hipMalloc(&p, b);
+        if (e != hipSuccess) return SetError(FBN_ERR_NOMEM, "hipMalloc(%zu): %s", b, hipGetErrorString(e));
+        bytes = b;
+        return FBN_OK;
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    template <class T>
+    T *as() const {
+        return static_cast<T *>(p);
+    }
+};
+
+int CheckDevice(int device, int *num_cu) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return SetError(FBN_ERR_NODEV, "no HIP device visible");
+    if (device < 0 || device >= n) return SetError(FBN_ERR_NODEV, "device %d out of range (%d visible)", device, n);
+    FBN_HIP(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    FBN_HIP(hipGetDeviceProperties(&prop, device));
+    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+        return SetError(FBN_ERR_NODEV, "device %d is %s; libfastbn is built for gfx950 only", device, prop.gcnArchName);
+    if (num_cu) *num_cu = prop.multiProcessorCount;
+    return FBN_OK;
+}
+
+}  // namespace
+
+// =============================================================================================
+struct fbn_network {
+    fbn::Network net;
+};
+struct fbn_dataset {
+    fbn::Dataset ds;
+};
+
+struct fbn_jt_plan {
+    fbn::JTPlanHost host;
+    fbn::JTProgram prog;
+    int device = 0, num_cu = 0, waves_per_cu = 4;
+    DevBuf ops, aux, initv, dig;
+    DevBuf evid, labels, marg, ws;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    ~fbn_jt_plan() {
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+    }
+};
+
+struct fbn_ci_ctx {
+    int device = 0, num_cu = 0, nvars = 0;
+    int64_t N = 0;
+    std::vector<int32_t> dims;
+    DevBuf cols, ddims, items, g2, df, p, indep, counts;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float last_ms = 0.f;
+    ~fbn_ci_ctx() {
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+    }
+};
+
+struct fbn_pc_result {
+    fbn::PCResultHost r;
+};
+
+// =============================================================================================
+extern "C" {
+
+const char *fbn_last_error(void) { return fbn::LastError(); }
+
+int fbn_version(int *major, int *minor) {
+    if (major) *major = 0;
+    if (minor) *minor = 1;
+    return FBN_OK;
+}
+
+int fbn_device_count(int *n) {
+    if (!n) return SetError(FBN_ERR_ARG, "null pointer");
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *n = c;
+    return FBN_OK;
+}
+
+// ------------------------------------------------------------------ networks & data
+int fbn_network_load_xmlbif(const char *path, fbn_network **out) {
+    if (!path || !out) return SetError(FBN_ERR_ARG, "null pointer");
+    auto h = std::unique_ptr<fbn_network>(new (std::nothrow) fbn_network());
+    if (!h) return SetError(FBN_ERR_NOMEM, "out of memory");
+    int rc = fbn::LoadXmlbif(path, h->net);
+    if (rc) return rc;
+    *out = h.release();
+    return FBN_OK;
+}
+int fbn_network_num_nodes(const fbn_network *net, int *n) {
+    if (!net || !n) return SetError(FBN_ERR_ARG, "null pointer");
+    *n = net->net.n();
+    return FBN_OK;
+}
+int fbn_network_dims(const fbn_network *net, int32_t *dims) {
+    if (!net || !dims) return SetError(FBN_ERR_ARG, "null pointer");
+    for (int i = 0; i < net->net.n(); ++i) dims[i] = net->net.dom[i];
+    return FBN_OK;
+}
+int fbn_network_name(const fbn_network *net, int node, char *buf, int cap) {
+    if (!net || !buf || cap <= 0 || node < 0 || node >= net->net.n()) return SetError(FBN_ERR_ARG, "bad argument");
+    snprintf(buf, cap, "%s", net->net.names[node].c_str());
+    return FBN_OK;
+}
+int fbn_network_destroy(fbn_network *net) {
+    delete net;
+    return FBN_OK;
+}
+
+int fbn_evidence_load_libsvm(const char *path, int num_nodes, int8_t *evidence, int32_t *labels, int64_t cap,
+                             int64_t *ncases) {
+    if (!path || num_nodes <= 0) return SetError(FBN_ERR_ARG, "bad argument");
+    std::vector<int8_t> ev;
+    std::vector<int32_t> lab;
+    int rc = fbn::LoadLibsvm(path, num_nodes, ev, lab);
+    if (rc) return rc;
+    int64_t n = (int64_t)lab.size();
+    if (ncases) *ncases = n;
+    int64_t m = std::min(n, cap);
+    if (evidence && m > 0) memcpy(evidence, ev.data(), (size_t)m * num_nodes);
+    if (labels && m > 0) memcpy(labels, lab.data(), (size_t)m * 4);
+    return FBN_OK;
+}
+
+int fbn_dataset_load_csv(const char *path, fbn_dataset **out) {
+    if (!path || !out) return SetError(FBN_ERR_ARG, "null pointer");
+    auto h = std::unique_ptr<fbn_dataset>(new (std::nothrow) fbn_dataset());
+    if (!h) return SetError(FBN_ERR_NOMEM, "out of memory");
+    int rc = fbn::LoadCsv(path, h->ds);
+    if (rc) return rc;
+    *out = h.release();
+    return FBN_OK;
+}
+int fbn_dataset_shape(const fbn_dataset *ds, int *nvars, int64_t *nsamples) {
+    if (!ds) return SetError(FBN_ERR_ARG, "null pointer");
+    if (nvars) *nvars = ds->ds.nvars;
+    if (nsamples) *nsamples = ds->ds.nsamples;
+    return FBN_OK;
+}
+int fbn_dataset_dims(const fbn_dataset *ds, int32_t *dims) {
+    if (!ds || !dims) return SetError(FBN_ERR_ARG, "null pointer");
+    std::copy(ds->ds.dims.begin(), ds->ds.dims.end(), dims);
+    return FBN_OK;
+}
+int fbn_dataset_columns(const fbn_dataset *ds, uint8_t *cols) {
+    if (!ds || !cols) return SetError(FBN_ERR_ARG, "null pointer");
+    std::copy(ds->ds.cols.begin(), ds->ds.cols.end(), cols);
+    return FBN_OK;
+}
+int fbn_dataset_var_name(const fbn_dataset *ds, int v, char *buf, int cap) {
+    if (!ds || !buf || cap <= 0 || v < 0 || v >= ds->ds.nvars) return SetError(FBN_ERR_ARG, "bad argument");
+    snprintf(buf, cap, "%s", ds->ds.names[v].c_str());
+    return FBN_OK;
+}
+int fbn_dataset_destroy(fbn_dataset *ds) {
+    delete ds;
+    return FBN_OK;
+}
+
+// ------------------------------------------------------------------ junction tree
+static int JtUpload(fbn_jt_plan *p) {
+    auto up = [](DevBuf &b, const void *src, size_t bytes) -> int {
+        int rc = b.ensure(std::max<size_t>(bytes, 8));
+        if (rc) return rc;
+        if (bytes) FBN_HIP(hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice));
+        return FBN_OK;
+    };
+    const auto &g = p->prog;
+    int rc;
+    if ((rc = up(p->ops, g.ops.data(), g.ops.size() * sizeof(JtOp)))) return rc;
+    if ((rc = up(p->aux, g.aux.data(), g.aux.size() * 4))) return rc;
+    if ((rc = up(p->initv, g.initv.data(), g.initv.size() * 8))) return rc;
+    if ((rc = up(p->dig, g.dig.data(), g.dig.size() * 8))) return rc;
+    return FBN_OK;
+}
+
+int fbn_jt_plan_create(const fbn_network *net, int device, fbn_jt_plan **out) {
+    if (!net || !out) return SetError(FBN_ERR_ARG, "null pointer");
+    auto p = std::unique_ptr<fbn_jt_plan>(new (std::nothrow) fbn_jt_plan());
+    if (!p) return SetError(FBN_ERR_NOMEM, "out of memory");
+    int rc = fbn::BuildJTPlan(net->net, p->host);
+    if (rc) return rc;
+    rc = fbn::CompileJTProgram(p->host, p->prog);
+    if (rc) return rc;
+    p->device = device;
+    if (device >= 0) {  // device < 0: host-only plan (info / dump), runs fail with FBN_ERR_NODEV
+        rc = CheckDevice(device, &p->num_cu);
+        if (rc) return rc;
+        rc = JtUpload(p.get());
+        if (rc) return rc;
+        FBN_HIP(hipEventCreate(&p->ev0));
+        FBN_HIP(hipEventCreate(&p->ev1));
+    }
+    *out = p.release();
+    return FBN_OK;
+}
+
+int fbn_jt_plan_info_get(const fbn_jt_plan *p, fbn_jt_plan_info *info) {
+    if (!p || !info) return SetError(FBN_ERR_ARG, "null pointer");
+    memset(info, 0, sizeof *info);
+    info->num_nodes = p->host.num_nodes;
+    info->num_cliques = (int32_t)p->host.cliques.size();
+    info->num_separators = (int32_t)p->host.seps.size();
+    info->num_levels = (int32_t)p->host.levels.size();
+    info->root = p->host.root;
+    info->sum_dom = p->prog.sum_dom;
+    for (auto &t : p->host.cliques) info->clique_entries += t.size();
+    for (auto &t : p->host.seps) info->separator_entries += t.size();
+    info->algorithmic_bytes_per_case =
+        16 * (info->clique_entries + info->separator_entries) + 8 * (int64_t)info->sum_dom + info->num_nodes;
+    info->num_ops = (int32_t)p->prog.ops.size();
+    info->max_vars_per_table = p->prog.max_vars;
+    return FBN_OK;
+}
+
+int fbn_jt_plan_dump(const fbn_jt_plan *p, const char *plan_path, const char *init_path) {
+    if (!p || !plan_path || !init_path) return SetError(FBN_ERR_ARG, "null pointer");
+    const auto &h = p->host;
+    FILE *f = fopen(plan_path, "w");
+    if (!f) return SetError(FBN_ERR_IO, "cannot write %s", plan_path);
+    fprintf(f, "cliques %zu\n", h.cliques.size());
+    for (size_t i = 0; i < h.cliques.size(); ++i) {
+        const auto &t = h.cliques[i];
+        fprintf(f, "c %zu %zu %lld", i, t.vars.size(), (long long)t.size());
+        for (int v : t.vars) fprintf(f, " %d", v);
+        fprintf(f, " | up %d | down", h.clique_up[i]);
+        for (int d : h.clique_down[i]) fprintf(f, " %d", d);
+        fprintf(f, "\n");
+    }
+    fprintf(f, "seps %zu\n", h.seps.size());
+    for (size_t i = 0; i < h.seps.size(); ++i) {
+        const auto &t = h.seps[i];
+        fprintf(f, "s %zu %zu %lld", i, t.vars.size(), (long long)t.size());
+        for (int v : t.vars) fprintf(f, " %d", v);
+        fprintf(f, " | up %d | down %d\n", h.sep_up[i], h.sep_down[i]);
+    }
+    fprintf(f, "root %d\n", h.root);
+    fprintf(f, "levels %zu\n", h.levels.size());
+    for (size_t l = 0; l < h.levels.size(); ++l) {
+        fprintf(f, "level %zu %c", l, (l % 2) ? 's' : 'c');
+        for (int x : h.levels[l]) fprintf(f, " %d", x);
+        fprintf(f, "\n");
+    }
+    fclose(f);
+    f = fopen(init_path, "w");
+    if (!f) return SetError(FBN_ERR_IO, "cannot write %s", init_path);
+    for (size_t i = 0; i < h.cliques.size(); ++i) {
+        fprintf(f, "c %zu %lld", i, (long long)h.cliques[i].size());
+        for (double v : h.cliques[i].pot) fprintf(f, " %.17g", v);
+        fprintf(f, "\n");
+    }
+    fclose(f);
+    return FBN_OK;
+}
+
+int fbn_jt_set_waves_per_cu(fbn_jt_plan *p, int waves) {
+    if (!p || waves < 0 || waves > 32) return SetError(FBN_ERR_ARG, "waves per CU must be 0..32");
+    p->waves_per_cu = waves ? waves : 4;
+    return FBN_OK;
+}
+
+int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, int32_t *d_labels,
+                      double *d_marginals, void *hip_stream) {
+    if (!p || (!d_evidence && ncases > 0) || ncases < 0) return SetError(FBN_ERR_ARG, "bad argument");
+    if (ncases == 0) return FBN_OK;
+    if (p->device < 0) return SetError(FBN_ERR_NODEV, "host-only plan (created with device < 0)");
+    FBN_HIP(hipSetDevice(p->device));
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    const auto &g = p->prog;
+    const int V = p->host.num_nodes, SD = g.sum_dom, nc = g.num_cliques;
+    const int64_t nblk = (ncases + 63) / 64;
+    const int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * p->waves_per_cu);
+    int rc;
+    const size_t ws_d = (size_t)grid * g.state_entries * 64 * 8;
+    const size_t ws_i = (size_t)grid * nc * 64 * 4;
+    if ((rc = p->ws.ensure(ws_d + ws_i))) return rc;
+    double *marg = d_marginals;
+    if (!marg) {
+        if ((rc = p->marg.ensure((size_t)ncases * SD * 8))) return rc;
+        marg = p->marg.as<double>();
+    }
+    int32_t *labels = d_labels;
+    if (!labels) {
+        if ((rc = p->labels.ensure((size_t)ncases * 4))) return rc;
+        labels = p->labels.as<int32_t>();
+    }
+    FBN_HIP(hipEventRecord(p->ev0, s));
+    hipError_t e = fbn_jt_launch(p->ops.as<JtOp>(), (int)g.ops.size(), p->aux.as<int32_t>(), p->initv.as<double>(),
+                                 p->dig.as<uint64_t>(), d_evidence, V, ncases, SD, marg, labels, p->ws.as<double>(),
+                                 reinterpret_cast<int32_t *>(p->ws.as<char>() + ws_d), g.state_entries, nc, grid, s);
+    if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt kernel launch: %s", hipGetErrorString(e));
+    FBN_HIP(hipEventRecord(p->ev1, s));
+    p->timed = true;
+    return FBN_OK;
+}
+
+int fbn_jt_run(fbn_jt_plan *p, const int8_t *evidence, int64_t ncases, int32_t *labels_out, double *marginals_out,
+               void *hip_stream) {
+    if (!p || (!evidence && ncases > 0) || ncases < 0 || (!labels_out && ncases > 0))
+        return SetError(FBN_ERR_ARG, "bad argument");
+    if (ncases == 0) return FBN_OK;
+    if (p->device < 0) return SetError(FBN_ERR_NODEV, "host-only plan (created with device < 0)");
+    const int V = p->host.num_nodes, SD = p->prog.sum_dom;
+    for (int64_t c = 0; c < ncases; ++c)  // out-of-domain evidence has no reference meaning
+        for (int v = 0; v < V; ++v) {
+            int x = evidence[c * V + v];
+            if (x < -1 || x >= p->host.dom[v])
+                return SetError(FBN_ERR_ARG, "case %lld: evidence %d for node %d (domain %d)", (long long)c, x, v,
+                                p->host.dom[v]);
+        }
+    FBN_HIP(hipSetDevice(p->device));
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    int rc;
+    if ((rc = p->evid.ensure((size_t)ncases * V))) return rc;
+    if ((rc = p->labels.ensure((size_t)ncases * 4))) return rc;
+    if ((rc = p->marg.ensure((size_t)ncases * SD * 8))) return rc;
+    FBN_HIP(hipMemcpyAsync(p->evid.p, evidence, (size_t)ncases * V, hipMemcpyHostToDevice, s));
+    rc = fbn_jt_run_device(p, p->evid.as<int8_t>(), ncases, p->labels.as<int32_t>(), p->marg.as<double>(), s);
+    if (rc) return rc;
+    FBN_HIP(hipMemcpyAsync(labels_out, p->labels.p, (size_t)ncases * 4, hipMemcpyDeviceToHost, s));
+    if (marginals_out)
+        FBN_HIP(hipMemcpyAsync(marginals_out, p->marg.p, (size_t)ncases * SD * 8, hipMemcpyDeviceToHost, s));
+    FBN_HIP(hipStreamSynchronize(s));
+    return FBN_OK;
+}
+
+int fbn_jt_score(const fbn_jt_plan *p, const double *marginals, const double *golden, int64_t ncases, double *mse_sum,
+                 double *hd_sum) {
+    if (!p || !marginals || !golden || !mse_sum || !hd_sum) return SetError(FBN_ERR_ARG, "null pointer");
+    const auto &dom = p->host.dom;
+    const int SD = p->prog.sum_dom;
+    auto round7 = [](double number) {  // Round(x, 7), src/Inference.cpp:195-206
+        long long integerpart = (long long)number;
+        number -= integerpart;
+        for (int i = 0; i < 7; ++i) number *= 10;
+        number = (double)(long long)(number + 0.5);
+        for (int i = 0; i < 7; ++i) number /= 10;
+        return integerpart + number;
+    };
+    double mse = 0.0, hd = 0.0;
+    for (int64_t c = 0; c < ncases; ++c) {  // CalculateMSE / CalculateHellingerDistance (:153-193)
+        const double *a = marginals + c * SD, *x = golden + c * SD;
+        int num = 0, off = 0;
+        double e1 = 0.0, e2 = 0.0;
+        for (size_t v = 0; v < dom.size(); ++v) {
+            if (x[off] > 0) {
+                num += dom[v];
+                for (int j = 0; j < dom[v]; ++j) {
+                    double r = round7(a[off + j]);
+                    e1 += pow(r - x[off + j], 2);
+                    e2 += pow(sqrt(r) - sqrt(x[off + j]), 2);
+                }
+            }
+            off += dom[v];
+        }
+        mse += sqrt(e1 / num);
+        hd += sqrt(e2 / num);
+    }
+    *mse_sum = mse;
+    *hd_sum = hd;
+    return FBN_OK;
+}
+
+int fbn_jt_last_kernel_ms(const fbn_jt_plan *p, float *ms) {
+    if (!p || !ms || !p->timed) return SetError(FBN_ERR_ARG, "no timed launch");
+    FBN_HIP(hipEventSynchronize(p->ev1));
+    FBN_HIP(hipEventElapsedTime(ms, p->ev0, p->ev1));
+    return FBN_OK;
+}
+
+int fbn_jt_plan_destroy(fbn_jt_plan *p) {
+    if (p && p->device >= 0) (void)hipSetDevice(p->device);
+    delete p;
+    return FBN_OK;
+}
+
+// ------------------------------------------------------------------ CI tests
+int fbn_ci_dataset_upload(const uint8_t *cols, int nvars, int64_t nsamples, const int32_t *dims, int device,
+                          fbn_ci_ctx **out) {
+    if (!cols || !dims || !out || nvars <= 0 || nsamples <= 0) return SetError(FBN_ERR_ARG, "bad argument");
+    for (int v = 0; v < nvars; ++v)
+        if (dims[v] < 1 || dims[v] > 256) return SetError(FBN_ERR_ARG, "dims[%d] = %d out of 1..256", v, dims[v]);
+    auto c = std::unique_ptr<fbn_ci_ctx>(new (std::nothrow) fbn_ci_ctx());
+    if (!c) return SetError(FBN_ERR_NOMEM, "out of memory");
+    int rc = CheckDevice(device, &c->num_cu);
+    if (rc) return rc;
+    c->device = device;
+    c->nvars = nvars;
+    c->N = nsamples;
+    c->dims.assign(dims, dims + nvars);
+    if ((rc = c->cols.ensure((size_t)nvars * nsamples))) return rc;
+    if ((rc = c->ddims.ensure((size_t)nvars * 4))) return rc;
+    FBN_HIP(hipMemcpy(c->cols.p, cols, (size_t)nvars * nsamples, hipMemcpyHostToDevice));
+    FBN_HIP(hipMemcpy(c->ddims.p, dims, (size_t)nvars * 4, hipMemcpyHostToDevice));
+    FBN_HIP(hipEventCreate(&c->ev0));
+    FBN_HIP(hipEventCreate(&c->ev1));
+    *out = c.release();
+    return FBN_OK;
+}
+
+static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alpha, bool want_g2p,
+                          int32_t *counts_dev, hipStream_t s) {
+    if (d < 0 || d > 8) return SetError(FBN_ERR_LIMIT, "conditioning set size %d (supported 0..8)", d);
+    const int w = 2 + d;
+    size_t lds = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int32_t *it = items + i * w;
+        for (int j = 0; j < w; ++j)
+            if (it[j] < 0 || it[j] >= c->nvars) return SetError(FBN_ERR_ARG, "test %lld: variable %d out of range", (long long)i, it[j]);
+        int64_t dimz = 1;
+        for (int j = 0; j < d; ++j) dimz *= c->dims[it[2 + j]];
+        if (dimz > (1 << 24)) return SetError(FBN_ERR_LIMIT, "test %lld: conditioning table too large", (long long)i);
+        lds = std::max(lds, fbn_ci_lds_bytes((int)dimz, c->dims[it[0]], c->dims[it[1]]));
+    }
+    if (lds > 160 * 1024)
+        return SetError(FBN_ERR_LIMIT, "contingency table needs %zu B of LDS (> 160 KiB): not supported yet", lds);
+    int rc;
+    if ((rc = c->items.ensure((size_t)n * w * 4))) return rc;
+    if ((rc = c->indep.ensure((size_t)n))) return rc;
+    if ((rc = c->df.ensure((size_t)n * 4))) return rc;
+    if (want_g2p) {
+        if ((rc = c->g2.ensure((size_t)n * 8))) return rc;
+        if ((rc = c->p.ensure((size_t)n * 8))) return rc;
+    }
+    FBN_HIP(hipMemcpyAsync(c->items.p, items, (size_t)n * w * 4, hipMemcpyHostToDevice, s));
+    const int grid = (int)std::min<int64_t>(n, (int64_t)c->num_cu * 8);
+    FBN_HIP(hipEventRecord(c->ev0, s));
+    hipError_t e = fbn_ci_launch(c->cols.as<uint8_t>(), c->ddims.as<int32_t>(), c->items.as<int32_t>(), c->N, n, d,
+                                 alpha, want_g2p ? c->g2.as<double>() : nullptr, c->df.as<int32_t>(),
+                                 want_g2p ? c->p.as<double>() : nullptr, c->indep.as<uint8_t>(), counts_dev, lds, grid,
+                                 s);
+    if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci kernel launch: %s", hipGetErrorString(e));
+    FBN_HIP(hipEventRecord(c->ev1, s));
+    return FBN_OK;
+}
+
+int fbn_ci_run(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alpha, double *g2, int32_t *df, double *p,
+               uint8_t *indep, void *hip_stream) {
+    if (!c || (!items && n > 0) || n < 0) return SetError(FBN_ERR_ARG, "bad argument");
+    if (n == 0) return FBN_OK;
+    FBN_HIP(hipSetDevice(c->device));
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    int rc = CiLaunchDevice(c, items, n, d, alpha, g2 || p, nullptr, s);
+    if (rc) return rc;
+    if (g2) FBN_HIP(hipMemcpyAsync(g2, c->g2.p, (size_t)n * 8, hipMemcpyDeviceToHost, s));
+    if (p) FBN_HIP(hipMemcpyAsync(p, c->p.p, (size_t)n * 8, hipMemcpyDeviceToHost, s));
+    if (df) FBN_HIP(hipMemcpyAsync(df, c->df.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    if (indep) FBN_HIP(hipMemcpyAsync(indep, c->indep.p, (size_t)n, hipMemcpyDeviceToHost, s));
+    FBN_HIP(hipStreamSynchronize(s));
+    FBN_HIP(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+    return FBN_OK;
+}
+
+int fbn_ci_counts(fbn_ci_ctx *c, int x, int y, const int32_t *z, int d, int32_t *counts, int64_t cap, int64_t *cells) {
+    if (!c || (!z && d > 0) || d < 0 || d > 8) return SetError(FBN_ERR_ARG, "bad argument");
+    std::vector<int32_t> item{x, y};
+    for (int j = 0; j < d; ++j) item.push_back(z[j]);
+    for (int32_t v : item)
+        if (v < 0 || v >= c->nvars) return SetError(FBN_ERR_ARG, "variable out of range");
+    int64_t nc = (int64_t)c->dims[x] * c->dims[y];
+    for (int j = 0; j < d; ++j) nc *= c->dims[z[j]];
+    if (cells) *cells = nc;
+    FBN_HIP(hipSetDevice(c->device));
+    int rc;
+    if ((rc = c->counts.ensure((size_t)nc * 4))) return rc;
+    rc = CiLaunchDevice(c, item.data(), 1, d, 0.05, false, c->counts.as<int32_t>(), nullptr);
+    if (rc) return rc;
+    if (counts) FBN_HIP(hipMemcpy(counts, c->counts.p, (size_t)std::min(nc, cap) * 4, hipMemcpyDeviceToHost));
+    FBN_HIP(hipDeviceSynchronize());
+    return FBN_OK;
+}
+
+int fbn_ci_last_kernel_ms(const fbn_ci_ctx *c, float *ms) {
+    if (!c || !ms) return SetError(FBN_ERR_ARG, "null pointer");
+    *ms = c->last_ms;
+    return FBN_OK;
+}
+
+int fbn_ci_ctx_destroy(fbn_ci_ctx *c) {
+    if (c) (void)hipSetDevice(c->device);
+    delete c;
+    return FBN_OK;
+}
+
+// ------------------------------------------------------------------ PC-stable
+int fbn_pc_stable(fbn_ci_ctx *c, double alpha, int depth, int group_size, fbn_pc_result **out) {
+    if (!c || !out || depth < 1 || !(alpha >= 0.0 && alpha <= 1.0)) return SetError(FBN_ERR_ARG, "bad argument");
+    auto r = std::unique_ptr<fbn_pc_result>(new (std::nothrow) fbn_pc_result());
+    if (!r) return SetError(FBN_ERR_NOMEM, "out of memory");
+    FBN_HIP(hipSetDevice(c->device));
+    int rc = fbn::RunPCStable(c, alpha, depth, group_size, r->r);
+    if (rc) return rc;
+    *out = r.release();
+    return FBN_OK;
+}
+int fbn_pc_num_levels(const fbn_pc_result *r, int *n) {
+    if (!r || !n) return SetError(FBN_ERR_ARG, "null pointer");
+    *n = (int)r->r.tests_per_level.size();
+    return FBN_OK;
+}
+int fbn_pc_level_tests(const fbn_pc_result *r, int64_t *tests) {
+    if (!r || !tests) return SetError(FBN_ERR_ARG, "null pointer");
+    std::copy(r->r.tests_per_level.begin(), r->r.tests_per_level.end(), tests);
+    return FBN_OK;
+}
+int fbn_pc_level_launched(const fbn_pc_result *r, int64_t *tests) {
+    if (!r || !tests) return SetError(FBN_ERR_ARG, "null pointer");
+    std::copy(r->r.launched_per_level.begin(), r->r.launched_per_level.end(), tests);
+    return FBN_OK;
+}
+int fbn_pc_num_edges(const fbn_pc_result *r, int *n) {
+    if (!r || !n) return SetError(FBN_ERR_ARG, "null pointer");
+    *n = (int)r->r.edges.size();
+    return FBN_OK;
+}
+int fbn_pc_edges(const fbn_pc_result *r, int32_t *pairs) {
+    if (!r || !pairs) return SetError(FBN_ERR_ARG, "null pointer");
+    for (size_t i = 0; i < r->r.edges.size(); ++i) pairs[2 * i] = r->r.edges[i].first, pairs[2 * i + 1] = r->r.edges[i].second;
+    return FBN_OK;
+}
+int fbn_pc_sepsets(const fbn_pc_result *r, int32_t *buf, int64_t cap, int64_t *len) {
+    if (!r) return SetError(FBN_ERR_ARG, "null pointer");
+    int64_t k = 0;
+    auto put = [&](int32_t v) {
+        if (buf && k < cap) buf[k] = v;
+        ++k;
+    };
+    for (auto &kv : r->r.sepset) {
+        put(kv.first.first);
+        put(kv.first.second);
+        put((int32_t)kv.second.size());
+        for (int z : kv.second) put(z);
+    }
+    if (len) *len = k;
+    return FBN_OK;
+}
+int fbn_pc_timing(const fbn_pc_result *r, double *total_s, double *kernel_s) {
+    if (!r) return SetError(FBN_ERR_ARG, "null pointer");
+    if (total_s) *total_s = r->r.total_s;
+    if (kernel_s) *kernel_s = r->r.kernel_s;
+    return FBN_OK;
+}
+int fbn_pc_result_destroy(fbn_pc_result *r) {
+    delete r;
+    return FBN_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ driver seam
+namespace fbn {
+void CiCtxShape(const fbn_ci_ctx *c, int *nvars, int64_t *nsamples) {
+    *nvars = c->nvars;
+    *nsamples = c->N;
+}
+int CiRunBatch(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alpha, uint8_t *indep, int32_t *df,
+               PCResultHost &res) {
+    if (n == 0) return FBN_OK;
+    int rc = CiLaunchDevice(c, items, n, d, alpha, false, nullptr, nullptr);
+    if (rc) return rc;
+    FBN_HIP(hipMemcpyAsync(indep, c->indep.p, (size_t)n, hipMemcpyDeviceToHost, nullptr));
+    if (df) FBN_HIP(hipMemcpyAsync(df, c->df.p, (size_t)n * 4, hipMemcpyDeviceToHost, nullptr));
+    FBN_HIP(hipStreamSynchronize(nullptr));
+    float ms = 0.f;
+    FBN_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    res.kernel_s += ms * 1e-3;
+    return FBN_OK;
+}
+}  // namespace fbn

@@ -1,0 +1,33 @@
+// PCStable.h -- host-side mirror of the reference's PC-stable API (include/PCStable.h:23-59,
+// include/StructureLearning.h:13-25) on top of the C-ABI: PCStable(alpha, depth) +
+// StructLearnCompData(dataset, group_size, num_threads, print_struct, verbose).  The skeleton
+// (level-k CI sweep) runs on the GPU; results are exposed in the reference's shapes.
+#ifndef FBN_CLI_PCSTABLE_H
+#define FBN_CLI_PCSTABLE_H
+
+#include <map>
+#include <set>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "fastbn.h"
+
+class PCStable {
+public:
+    PCStable(double alpha, int depth = 1000, int device = 0) : alpha(alpha), depth(depth), device_(device) {}
+    void StructLearnCompData(fbn_dataset *dts, int group_size, int num_threads, bool print_struct, bool verbose);
+
+    double alpha;
+    int depth;
+    int64_t num_ci_test = 0;
+    int64_t num_dependence_judgement = 0;
+    std::vector<std::pair<int, int>> edges;         // skeleton, vec_edges order
+    std::map<std::pair<int, int>, std::set<int>> sepset;
+    std::vector<int64_t> tests_per_level;
+
+private:
+    int device_;
+};
+
+#endif

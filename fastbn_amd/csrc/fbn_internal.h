@@ -1,0 +1,79 @@
+// fbn_internal.h -- internal types of libfastbn (host side).  Not part of the ABI.
+#ifndef FBN_INTERNAL_H
+#define FBN_INTERNAL_H
+
+#include <cstdint>
+#include <map>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "../../include/fastbn.h"
+#include "jt_program.h"
+
+namespace fbn {
+
+// thread-local error channel behind fbn_last_error()
+int SetError(int code, const char *fmt, ...);
+
+// ---------------------------------------------------------------------------------------------
+// discrete Bayesian network (CustomNetwork + DiscreteNode state the hot paths read)
+struct Network {
+    std::vector<std::string> names;
+    std::vector<int> dom;
+    std::vector<std::vector<int>> given;        // parents in <GIVEN> order
+    std::vector<std::vector<int>> parents_asc;  // parents in ascending index order
+    std::vector<std::vector<int64_t>> counts;   // [v][q * npc + pc]
+    std::vector<std::vector<int64_t>> totals;   // [v][pc], pc over parents_asc, last fastest
+    int n() const { return (int)dom.size(); }
+    double Prob(int v, int q, const int *parent_vals_asc) const;
+};
+int LoadXmlbif(const std::string &path, Network &net);
+
+struct Dataset {
+    int nvars = 0;
+    int64_t nsamples = 0;
+    std::vector<std::string> names;
+    std::vector<int32_t> dims;
+    std::vector<uint8_t> cols;  // [var][sample]
+};
+int LoadCsv(const std::string &path, Dataset &ds);
+int LoadLibsvm(const std::string &path, int num_nodes, std::vector<int8_t> &ev, std::vector<int32_t> &labels);
+
+// ---------------------------------------------------------------------------------------------
+// junction-tree static plan (host), container order as in JunctionTreeStructure
+struct Table {
+    std::vector<int> vars, dims, cum;  // row-major, left-most var most significant
+    std::vector<double> pot;
+    int64_t size() const { return (int64_t)pot.size(); }
+    void Rebuild();
+};
+
+struct JTPlanHost {
+    int num_nodes = 0;
+    std::vector<int> dom;
+    std::vector<Table> cliques, seps;  // initial potentials after ReorganizeTableStorage
+    std::vector<int> clique_up;                 // upstream separator, -1 for the root
+    std::vector<std::vector<int>> clique_down;  // downstream separators (MarkLevel order)
+    std::vector<int> sep_up, sep_down;          // parent clique, child clique
+    int root = -1;
+    std::vector<std::vector<int>> levels;       // even levels: cliques, odd levels: separators
+};
+int BuildJTPlan(const Network &net, JTPlanHost &plan);
+
+// device program (see jt_program.h) compiled from the host plan
+struct JTProgram {
+    std::vector<JtOp> ops;
+    std::vector<int32_t> aux;
+    std::vector<double> initv;
+    std::vector<uint64_t> dig;
+    int64_t state_entries = 0;  // NE: table entries + one pending denominator per clique
+    int num_cliques = 0;
+    int sum_dom = 0;
+    int max_vars = 0;
+};
+int CompileJTProgram(const JTPlanHost &plan, JTProgram &prog);
+
+}  // namespace fbn
+
+#endif

@@ -1,0 +1,233 @@
+// pc_driver.cpp -- PC-stable skeleton search driven from the host, CI tests on the device.
+//
+// Semantics are the reference's sequential (t = 1) ones (src/PCStable.cpp:49-563):
+//   * level 0 tests every edge of the complete graph marginally;
+//   * level d >= 1 works on a snapshot of the adjacencies; for edge (x, y) (x < y) the candidate
+//     conditioning sets are the size-d subsets of adj(x)\{y} in ChoiceGenerator order, then those
+//     of adj(y)\{x}; the first independent one removes the edge and becomes its sepset;
+//   * with -g gs > 1, sets are evaluated in groups of gs per side (NextN), the whole group counts,
+//     and a df == 0 result inside a group of size > 1 is a dependence (src/IndependenceTest.cpp:262-271);
+//   * removals are applied after the level in vec_edges order; the search continues while
+//     FreeDegree > d.
+// Instead of the reference's 128-edge work pool, every unresolved edge contributes its next
+// chunk of candidate sets to one device batch per round (chunk 32 -> 128 -> 512 ... sets), and the
+// host resolves each edge's prefix in order.  Tests beyond an edge's first independent set are
+// speculative: they are run but not counted, so the reported counts equal the reference's.
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <map>
+#include <set>
+
+#include "fbn_internal.h"
+#include "pc_internal.h"
+
+namespace fbn {
+
+namespace {
+
+struct EdgeState {
+    int x, y;
+    int side = 0;                // 0: adj(x)\{y}, 1: adj(y)\{x}, 2: exhausted
+    std::vector<int> A;          // current side's adjacency (sorted)
+    std::vector<int> ch;         // next combination (positions in A)
+    bool has_next = false;
+    int64_t pos_in_side = 0;     // index of the next combination within the side
+    bool resolved = false, removed = false;
+    std::vector<int> sep;
+};
+
+void StartSide(EdgeState &e, const std::vector<std::vector<int>> &adj, int d) {
+    while (e.side < 2) {
+        int a = e.side ? e.y : e.x, b = e.side ? e.x : e.y;
+        e.A.clear();
+        for (int u : adj[a])
+            if (u != b) e.A.push_back(u);
+        if ((int)e.A.size() >= d) {
+            e.ch.resize(d);
+            for (int i = 0; i < d; ++i) e.ch[i] = i;
+            e.has_next = true;
+            e.pos_in_side = 0;
+            return;
+        }
+        ++e.side;
+    }
+    e.has_next = false;
+}
+
+void Advance(EdgeState &e, int d) {  // ChoiceGenerator::Next (src/ChoiceGenerator.cpp:55-85)
+    const int m = (int)e.A.size();
+    int i = d - 1;
+    while (i >= 0 && e.ch[i] == m - d + i) --i;
+    if (i < 0) {
+        e.has_next = false;
+        return;
+    }
+    ++e.ch[i];
+    for (int k = i + 1; k < d; ++k) e.ch[k] = e.ch[k - 1] + 1;
+    ++e.pos_in_side;
+}
+
+struct Pending {  // one generated test
+    int edge;
+    int side;
+    int64_t pos;  // position within the side
+    int64_t group_end;  // first position after this test's group (within the side)
+};
+
+}  // namespace
+
+int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResultHost &res) {
+    if (group_size < 1 || group_size > 8) return SetError(FBN_ERR_ARG, "group_size must be 1..8 (reference cap, src/IndependenceTest.cpp:170)");
+    auto t0 = std::chrono::steady_clock::now();
+    res = PCResultHost();
+    int nvars = 0;
+    int64_t nsamples = 0;
+    CiCtxShape(ctx, &nvars, &nsamples);
+    const int n = nvars;
+    std::vector<std::pair<int, int>> edges;
+    for (int i = 0; i < n; ++i)
+        for (int j = i + 1; j < n; ++j) edges.push_back({i, j});
+    std::vector<std::vector<int>> adj(n);
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j)
+            if (i != j) adj[i].push_back(j);
+
+    std::vector<int32_t> items;
+    std::vector<uint8_t> indep;
+    std::vector<int32_t> dfv;
+
+    auto apply_removals = [&](const std::vector<char> &rm) {
+        std::vector<std::pair<int, int>> keep;
+        keep.reserve(edges.size());
+        for (size_t e = 0; e < edges.size(); ++e) {
+            if (!rm[e]) {
+                keep.push_back(edges[e]);
+                continue;
+            }
+            auto &ax = adj[edges[e].first], &ay = adj[edges[e].second];
+            ax.erase(std::lower_bound(ax.begin(), ax.end(), edges[e].second));
+            ay.erase(std::lower_bound(ay.begin(), ay.end(), edges[e].first));
+        }
+        edges.swap(keep);
+    };
+
+    // ---- level 0 (src/PCStable.cpp:73-157)
+    {
+        items.resize(edges.size() * 2);
+        for (size_t e = 0; e < edges.size(); ++e) items[2 * e] = edges[e].first, items[2 * e + 1] = edges[e].second;
+        indep.resize(edges.size());
+        int rc = CiRunBatch(ctx, items.data(), (int64_t)edges.size(), 0, alpha, indep.data(), nullptr, res);
+        if (rc) return rc;
+        std::vector<char> rm(edges.size(), 0);
+        for (size_t e = 0; e < edges.size(); ++e)
+            if (indep[e]) {
+                rm[e] = 1;
+                res.sepset[{edges[e].first, edges[e].second}] = {};
+            }
+        res.tests_per_level.push_back((int64_t)edges.size());
+        res.launched_per_level.push_back((int64_t)edges.size());
+        apply_removals(rm);
+    }
+
+    // ---- levels d >= 1 (SearchAtDepth :209-328, CheckEdge :339-433, Testing :465-551)
+    for (int d = 1; d < depth; ++d) {
+        const std::vector<std::vector<int>> snap = adj;
+        std::vector<EdgeState> st(edges.size());
+        for (size_t e = 0; e < edges.size(); ++e) {
+            st[e].x = edges[e].first;
+            st[e].y = edges[e].second;
+            StartSide(st[e], snap, d);
+            if (!st[e].has_next) st[e].resolved = true;  // both sides too small: kept
+        }
+        int64_t counted = 0, launched = 0;
+        int64_t chunk = 32;
+        std::vector<Pending> pend;
+        while (true) {
+            items.clear();
+            pend.clear();
+            for (size_t e = 0; e < st.size(); ++e) {
+                EdgeState &s = st[e];
+                if (s.resolved) continue;
+                // next chunk: whole groups only, never across a side boundary
+                int64_t want = ((chunk + group_size - 1) / group_size) * group_size;
+                while (want > 0 && s.has_next) {
+                    const int64_t gstart = (s.pos_in_side / group_size) * group_size;
+                    Pending p{(int)e, s.side, s.pos_in_side, gstart + group_size};
+                    pend.push_back(p);
+                    items.push_back(s.x);
+                    items.push_back(s.y);
+                    for (int i = 0; i < d; ++i) items.push_back(s.A[s.ch[i]]);
+                    --want;
+                    Advance(s, d);
+                    if (!s.has_next) {
+                        // side exhausted: next side starts fresh (its groups restart at 0)
+                        if (s.side == 0) {
+                            s.side = 1;
+                            StartSide(s, snap, d);
+                        } else {
+                            s.side = 2;
+                        }
+                        break;  // keep groups aligned: finish this chunk at the side boundary
+                    }
+                }
+            }
+            if (pend.empty()) break;
+            const int64_t nt = (int64_t)pend.size();
+            indep.resize(nt);
+            dfv.resize(nt);
+            int rc = CiRunBatch(ctx, items.data(), nt, d, alpha, indep.data(), dfv.data(), res);
+            if (rc) return rc;
+            launched += nt;
+            // resolve in order per edge
+            size_t i = 0;
+            while (i < pend.size()) {
+                const int e = pend[i].edge;
+                size_t j = i;
+                while (j < pend.size() && pend[j].edge == e) ++j;  // tests of this edge: [i, j)
+                EdgeState &s = st[e];
+                size_t k = i;
+                while (k < j && !s.removed) {
+                    // one group: tests with the same side and group_end
+                    size_t g = k;
+                    while (g < j && pend[g].side == pend[k].side && pend[g].group_end == pend[k].group_end) ++g;
+                    const int gsz = (int)(g - k);
+                    counted += gsz;
+                    for (size_t t = k; t < g; ++t) {
+                        bool ind = indep[t] != 0;
+                        if (gsz > 1 && dfv[t] == 0) ind = false;  // group quirk (see file header)
+                        if (ind) {
+                            s.removed = true;
+                            s.resolved = true;
+                            std::vector<int> z(items.begin() + (2 + d) * t + 2, items.begin() + (2 + d) * (t + 1));
+                            std::sort(z.begin(), z.end());
+                            s.sep = z;
+                            break;
+                        }
+                    }
+                    k = g;
+                }
+                if (!s.removed && !s.has_next) s.resolved = true;  // exhausted: dependent, kept
+                i = j;
+            }
+            chunk = std::min<int64_t>(chunk * 4, 1 << 16);
+        }
+        std::vector<char> rm(edges.size(), 0);
+        for (size_t e = 0; e < st.size(); ++e)
+            if (st[e].removed) {
+                rm[e] = 1;
+                res.sepset[{st[e].x, st[e].y}] = st[e].sep;
+            }
+        res.tests_per_level.push_back(counted);
+        res.launched_per_level.push_back(launched);
+        apply_removals(rm);
+        size_t maxdeg = 0;  // FreeDegree (:557-563)
+        for (int v = 0; v < n; ++v) maxdeg = std::max(maxdeg, adj[v].size());
+        if (!((int64_t)maxdeg - 1 > d)) break;
+    }
+    res.edges = edges;
+    res.total_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return FBN_OK;
+}
+
+}  // namespace fbn

@@ -1,0 +1,31 @@
+// pc_internal.h -- host <-> device seam of the PC-stable driver (internal to libfastbn).
+#ifndef FBN_PC_INTERNAL_H
+#define FBN_PC_INTERNAL_H
+
+#include <cstdint>
+#include <map>
+#include <utility>
+#include <vector>
+
+#include "../../include/fastbn.h"
+
+namespace fbn {
+
+struct PCResultHost {
+    std::vector<std::pair<int, int>> edges;
+    std::map<std::pair<int, int>, std::vector<int>> sepset;
+    std::vector<int64_t> tests_per_level;     // reference (t = 1) counts
+    std::vector<int64_t> launched_per_level;  // device tests incl. speculation
+    double total_s = 0.0, kernel_s = 0.0;
+};
+
+void CiCtxShape(const fbn_ci_ctx *c, int *nvars, int64_t *nsamples);
+// run n tests of size d on the device; indep[n] (and df[n] if non-null) come back to the host;
+// accumulates kernel time into res.kernel_s
+int CiRunBatch(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alpha, uint8_t *indep, int32_t *df,
+               PCResultHost &res);
+int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResultHost &res);
+
+}  // namespace fbn
+
+#endif

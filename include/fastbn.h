@@ -1,0 +1,152 @@
+/* fastbn.h -- C-ABI of the MI355X-native FastBN hot paths (libfastbn.so).
+ *
+ * Drop-in boundary for the two data-parallel paths of the reference:
+ *   * JT: batched junction-tree sum-product.  Replaces the per-case loop of
+ *         JunctionTree::PredictUseJTInfer (src/JunctionTree.cpp:1473-1534) behind
+ *         Inference::EvaluateAccuracy (include/Inference.h:44).
+ *   * PC: the PC-stable skeleton CI sweep.  Replaces IndependenceTest::IndependenceResult
+ *         (include/IndependenceTest.h:56, src/IndependenceTest.cpp:35-364) and the level loop of
+ *         PCStable::StructLearnByPCStable / SearchAtDepth (src/PCStable.cpp:49-563) behind
+ *         StructureLearning::StructLearnCompData (include/StructureLearning.h:22).
+ *
+ * Conventions: every function returns 0 (FBN_OK) or a negative fbn_err_t; fbn_last_error()
+ * gives the message of the last failure on the calling thread.  No exceptions cross the ABI.
+ * Plain pointers and sizes only.  Host arrays are caller-owned and only touched during the call;
+ * device buffers are owned by the handle.  A handle is bound to one device and is not
+ * thread-safe; multi-GPU = one handle per device (one process per GPU).
+ */
+#ifndef FASTBN_H
+#define FASTBN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    FBN_OK = 0,
+    FBN_ERR_ARG = -1,     /* bad argument / shape */
+    FBN_ERR_IO = -2,      /* file missing or malformed (the reference exit(1)s here) */
+    FBN_ERR_HIP = -3,     /* HIP runtime / kernel failure */
+    FBN_ERR_NOMEM = -4,   /* host or device allocation failed */
+    FBN_ERR_NODEV = -5,   /* no usable gfx950 device */
+    FBN_ERR_LIMIT = -6    /* plan exceeds a kernel limit (e.g. variables per clique) */
+} fbn_err_t;
+
+const char *fbn_last_error(void);
+int fbn_version(int *major, int *minor);
+int fbn_device_count(int *n);
+
+/* ------------------------------------------------------------------ networks & data (host) */
+typedef struct fbn_network fbn_network;
+
+/* XMLBIF -> discrete network with the reference's CPT convention ((int(p*1e4)+1)/(sum+|dom|),
+ * node-major TABLE).  Replaces CustomNetwork::GetNetFromXMLBIFFile (src/CustomNetwork.cpp:20-41)
+ * + XMLBIFParser (src/XMLBIFParser.cpp:3-218). */
+int fbn_network_load_xmlbif(const char *path, fbn_network **out);
+int fbn_network_num_nodes(const fbn_network *net, int *n);
+int fbn_network_dims(const fbn_network *net, int32_t *dims /* [n] */);
+int fbn_network_name(const fbn_network *net, int node, char *buf, int cap);
+int fbn_network_destroy(fbn_network *net);
+
+/* LIBSVM test set -> evidence rows.  Replaces Dataset::LoadLIBSVMDataKnownNetwork
+ * (src/Dataset.cpp:162-262) + the evidence extraction of Inference::Inference
+ * (src/Inference.cpp:13-42).  evidence: [ncases][num_nodes] int8, -1 = unobserved.
+ * Call with evidence == NULL to get the case count. */
+int fbn_evidence_load_libsvm(const char *path, int num_nodes, int8_t *evidence, int32_t *labels,
+                             int64_t cap, int64_t *ncases);
+
+typedef struct fbn_dataset fbn_dataset;
+/* CSV with header and string values coded by first appearance; column store uint8 [var][sample].
+ * Replaces Dataset::LoadCSVData + RowMajor2ColumnMajor (src/Dataset.cpp:267-414,568-580). */
+int fbn_dataset_load_csv(const char *path, fbn_dataset **out);
+int fbn_dataset_shape(const fbn_dataset *ds, int *nvars, int64_t *nsamples);
+int fbn_dataset_dims(const fbn_dataset *ds, int32_t *dims);
+int fbn_dataset_columns(const fbn_dataset *ds, uint8_t *cols /* [nvars][nsamples] */);
+int fbn_dataset_var_name(const fbn_dataset *ds, int v, char *buf, int cap);
+int fbn_dataset_destroy(fbn_dataset *ds);
+
+/* ------------------------------------------------------------------ junction tree */
+typedef struct fbn_jt_plan fbn_jt_plan;
+
+typedef struct {
+    int32_t num_nodes, num_cliques, num_separators, num_levels;
+    int32_t root, sum_dom;
+    int64_t clique_entries;     /* sum of clique table sizes */
+    int64_t separator_entries;  /* sum of separator table sizes */
+    int64_t algorithmic_bytes_per_case; /* 16*(clique+sep entries) + 8*sum_dom + num_nodes */
+    int32_t num_ops;            /* device program length */
+    int32_t max_vars_per_table;
+} fbn_jt_plan_info;
+
+/* Build the case-independent schedule (JunctionTree ctor, src/JunctionTree.cpp:3-46:
+ * JunctionTreeStructure src/JunctionTreeStructure.cpp:12-348, root/levels/reorganization
+ * :137-281), compile it to a device program and upload it to `device`.  device < 0 builds a
+ * host-only plan (info / dump; runs return FBN_ERR_NODEV). */
+int fbn_jt_plan_create(const fbn_network *net, int device, fbn_jt_plan **out);
+int fbn_jt_plan_info_get(const fbn_jt_plan *p, fbn_jt_plan_info *info);
+/* Text dump in the same format as the reference harness (tests/golden/alarm_1k.plan/.init). */
+int fbn_jt_plan_dump(const fbn_jt_plan *p, const char *plan_path, const char *init_path);
+/* Evidence cases on the host: evidence [ncases][num_nodes] int8; labels_out [ncases] (arg-max
+ * of the query variable 0, InferenceUsingJT src/JunctionTree.cpp:1459-1467); marginals_out
+ * [ncases][sum_dom] fp64 or NULL (GetProbabilitiesAllNodes :1385-1454, evidence nodes = 0).
+ * Copies in/out over PCIe; synchronous. */
+int fbn_jt_run(fbn_jt_plan *p, const int8_t *evidence, int64_t ncases, int32_t *labels_out,
+               double *marginals_out, void *hip_stream);
+/* Same with device-resident buffers (inputs already in HBM); asynchronous on hip_stream. */
+int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, int32_t *d_labels,
+                      double *d_marginals, void *hip_stream);
+/* Per-case MSE and Hellinger distance vs a golden table (CalculateMSE / CalculateHellingerDistance
+ * with Round(.,7), src/Inference.cpp:153-206); golden [ncases][sum_dom], evidence nodes marked by
+ * golden[.][first state] <= 0.  Host arrays; sums accumulated in case order. */
+int fbn_jt_score(const fbn_jt_plan *p, const double *marginals, const double *golden, int64_t ncases,
+                 double *mse_sum, double *hd_sum);
+/* Device kernel time (ms, hipEvent) of the last fbn_jt_run*; launches of the main kernel. */
+int fbn_jt_last_kernel_ms(const fbn_jt_plan *p, float *ms);
+/* Tuning: persistent waves per CU (0 = default). */
+int fbn_jt_set_waves_per_cu(fbn_jt_plan *p, int waves);
+int fbn_jt_plan_destroy(fbn_jt_plan *p);
+
+/* ------------------------------------------------------------------ CI tests (G^2) */
+typedef struct fbn_ci_ctx fbn_ci_ctx;
+
+/* Upload the column store (uint8 [nvars][nsamples], codes < dims[v] <= 255) to `device`. */
+int fbn_ci_dataset_upload(const uint8_t *cols, int nvars, int64_t nsamples, const int32_t *dims,
+                          int device, fbn_ci_ctx **out);
+/* n tests of one conditioning size d: items [n][2+d] = (x, y, z_0..z_{d-1}).  Outputs per test
+ * (any may be NULL): G^2, adjusted df, p = 1 - pchisq(G^2, df), indep = (df == 0 || p > alpha).
+ * ComputeGSquareXY / ComputeGSquareXYZ semantics (src/IndependenceTest.cpp:65-155,295-364).
+ * Host arrays, synchronous. */
+int fbn_ci_run(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alpha, double *g2,
+               int32_t *df, double *p, uint8_t *indep, void *hip_stream);
+/* Debug/parity: the contingency table N[z][x][y] of one test (int32, cells = dimz*dx*dy). */
+int fbn_ci_counts(fbn_ci_ctx *c, int x, int y, const int32_t *z, int d, int32_t *counts, int64_t cap,
+                  int64_t *cells);
+int fbn_ci_last_kernel_ms(const fbn_ci_ctx *c, float *ms);
+int fbn_ci_ctx_destroy(fbn_ci_ctx *c);
+
+/* ------------------------------------------------------------------ PC-stable skeleton */
+typedef struct fbn_pc_result fbn_pc_result;
+
+/* Skeleton phase of PC-stable (levels 0 .. depth-1, stop when FreeDegree <= level) with the
+ * reference's sequential semantics: per edge the conditioning sets of adj(x)\{y} then adj(y)\{x}
+ * in ChoiceGenerator order, first independent set wins, removals applied after each level.
+ * group_size as the reference's -g.  CI tests run on the device in speculative batches; the
+ * reported counts are the reference's (t = 1) counts. */
+int fbn_pc_stable(fbn_ci_ctx *c, double alpha, int depth, int group_size, fbn_pc_result **out);
+int fbn_pc_num_levels(const fbn_pc_result *r, int *n);
+int fbn_pc_level_tests(const fbn_pc_result *r, int64_t *tests /* [n_levels] */);
+int fbn_pc_level_launched(const fbn_pc_result *r, int64_t *tests /* device tests incl. speculation */);
+int fbn_pc_num_edges(const fbn_pc_result *r, int *n);
+int fbn_pc_edges(const fbn_pc_result *r, int32_t *pairs /* [n][2], vec_edges order */);
+/* sepsets flattened as (x, y, k, z_0..z_{k-1})*, key x < y; returns total int count in *len */
+int fbn_pc_sepsets(const fbn_pc_result *r, int32_t *buf, int64_t cap, int64_t *len);
+int fbn_pc_timing(const fbn_pc_result *r, double *total_s, double *kernel_s);
+int fbn_pc_result_destroy(fbn_pc_result *r);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FASTBN_H */

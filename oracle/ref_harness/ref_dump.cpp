@@ -10,7 +10,7 @@
 // (src/common.cpp:193-232) and AddCount(query, parents, p*10000) (src/XMLBIFParser.cpp:176).
 //
 // Modes
-//   jt  <net.xml> <libsvm test set> <pt file|-> <out prefix> [max_cases]
+//   jt  <net.xml> <libsvm test set> <pt file|-> <out prefix> [max_cases] [eval set]
 //       writes <prefix>.plan (junction-tree plan after ReorganizeTableStorage),
 //              <prefix>.init (initial clique potentials, %.17g),
 //              <prefix>.marg (per case: label + all node marginals, %.17g)
@@ -19,6 +19,7 @@
 //       (src/CellTable.cpp:174-291,430-455) and writes them with the dataset's domains.
 #include <cstdio>
 #include <fstream>
+#include <iostream>
 #include <map>
 #include <string>
 #include <vector>
@@ -167,6 +168,36 @@ public:
         fprintf(f, "mse_sum %.17g hd_sum %.17g\n", mse, hd);
         fclose(f);
     }
+
+    // evaluate a different case list on the same tree: the reference's tree shape depends on the
+    // heap addresses of its cliques/separators (pointer-ordered std::set, src/JunctionTreeStructure.cpp:231,
+    // include/Clique.h:22), so the tree is always built after loading the same test set
+    double TimeCases(int n) {
+        if (n > num_instances) n = num_instances;
+        ground_truth_probability_tables.assign(num_instances, std::vector<std::vector<double>>());
+        for (auto &c : ground_truth_probability_tables) {
+            c.resize(network->num_nodes);
+            for (int j = 0; j < network->num_nodes; ++j)
+                c[j].assign(dynamic_cast<DiscreteNode *>(network->FindNodePtrByIndex(j))->GetDomainSize(), 0.0);
+        }
+        Timer timer;
+        double mse = 0.0, hd = 0.0, t0 = omp_get_wtime();
+        long sink = 0;
+        for (int i = 0; i < n; ++i) sink += PredictUseJTInfer(evidences.at(i), i, mse, hd, 1, &timer);
+        double t = omp_get_wtime() - t0;
+        if (sink < 0) printf("%ld", sink);
+        return t;
+    }
+    struct CaseList : Inference {  // the reference's own evidence extraction (src/Inference.cpp:13-42)
+        CaseList(Network *n, Dataset *d) : Inference(n, d, false) {}
+        double EvaluateAccuracy(string, int) override { return 0; }
+    };
+    void SwapCases(Dataset *other) {
+        CaseList tmp(network, other);
+        evidences = tmp.evidences;
+        ground_truths = tmp.ground_truths;
+        num_instances = tmp.num_instances;
+    }
 };
 
 static int RunJT(int argc, char **argv) {
@@ -177,6 +208,11 @@ static int RunJT(int argc, char **argv) {
     JTHarness jt(net, tester);
     std::string prefix = argv[5];
     jt.DumpPlan(prefix + ".plan", prefix + ".init");
+    if (argc > 7) {
+        auto *other = new Dataset();
+        other->LoadLIBSVMDataKnownNetwork(argv[7], net->num_nodes);
+        jt.SwapCases(other);
+    }
     jt.DumpCases(argv[4], prefix + ".marg", argc > 6 ? atoi(argv[6]) : 0);
     return 0;
 }
@@ -235,7 +271,27 @@ static int RunCI(int argc, char **argv) {
     return 0;
 }
 
+// jtbench <net.xml> <tree set> <eval set> <max_cases>: wall time of the reference's per-case loop
+// (PredictUseJTInfer, t = 1, as EvaluateAccuracy runs it) -- bench.py's cpu_baseline "reference"
+static int RunJTBench(int argc, char **argv) {
+    if (argc < 6) return 2;
+    std::streambuf *old = std::cout.rdbuf(nullptr);  // silence the reference's progress output
+    Network *net = LoadXmlbifIntoReference(argv[2]);
+    auto *tester = new Dataset();
+    tester->LoadLIBSVMDataKnownNetwork(argv[3], net->num_nodes);
+    JTHarness jt(net, tester);
+    auto *other = new Dataset();
+    other->LoadLIBSVMDataKnownNetwork(argv[4], net->num_nodes);
+    jt.SwapCases(other);
+    std::cout.rdbuf(old);
+    int n = atoi(argv[5]);
+    double s = jt.TimeCases(n);
+    printf("cases %d seconds %.6f\n", n, s);
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc >= 2 && std::string(argv[1]) == "jtbench") return RunJTBench(argc, argv);
     if (argc >= 2 && std::string(argv[1]) == "jt") return RunJT(argc, argv);
     if (argc >= 2 && std::string(argv[1]) == "ci") return RunCI(argc, argv);
     fprintf(stderr, "usage: ref_dump jt|ci ...\n");

@@ -68,11 +68,16 @@ def main():
     rand_set = os.path.join(OUT, "rand_evidence.libsvm")
     with open(rand_set, "w") as f:
         f.writelines(lines)
+    # the tree is built after loading testing_alarm_1k_p20 (same heap history as run 1, hence the
+    # same pointer-ordered tree), then the synthetic cases are evaluated on it
     pre = os.path.join(HERE, "alarm_rand")
-    run([ref_dump, "jt", os.path.join(OUT, "alarm.xml"), rand_set, "-", pre])
+    run([ref_dump, "jt", os.path.join(OUT, "alarm.xml"), os.path.join(OUT, "testing_alarm_1k_p20"), "-", pre,
+         "0", rand_set])
     gz(pre + ".marg", pre + ".marg.gz")
-    os.remove(pre + ".plan")
-    os.remove(pre + ".init")
+    for ext in (".plan", ".init"):
+        same = open(pre + ext).read() == open(os.path.join(OUT, "alarm_1k" + ext)).read()
+        assert same, "reference tree differs between runs (heap-address order)"
+        os.remove(pre + ext)
     for ext in (".plan", ".init"):
         shutil.move(os.path.join(OUT, "alarm_1k" + ext), os.path.join(HERE, "alarm_1k" + ext))
     shutil.move(os.path.join(OUT, "alarm_1k.marg.gz"), os.path.join(HERE, "alarm_1k.marg.gz"))

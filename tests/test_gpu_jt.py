@@ -1,0 +1,119 @@
+"""Junction-tree HIP path vs the oracle and the reference's own outputs (bit-exact fp64)."""
+import os
+
+import numpy as np
+import pytest
+from conftest import GOLD, read_pt_file, read_ref_marg
+
+import fastbn_amd as F
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def jt(alarm_paths):
+    return F.JunctionTree(F.Network(alarm_paths["xml"]), device=0)
+
+
+@pytest.fixture(scope="module")
+def ojt(alarm_paths):
+    return O.OracleJT(alarm_paths["xml"])
+
+
+@pytest.mark.parametrize("which", ["alarm_1k", "alarm_rand"])
+def test_bit_exact_vs_reference_fixture(jt, alarm_paths, which):
+    path = alarm_paths["test"] if which == "alarm_1k" else alarm_paths["rand"]
+    ev, _ = F.load_libsvm(path, 37)
+    lab, marg = jt.infer(ev)
+    rlab, rmarg, _, _ = read_ref_marg(os.path.join(GOLD, which + ".marg.gz"), jt.network.dims)
+    np.testing.assert_array_equal(lab, rlab)
+    np.testing.assert_array_equal(marg, rmarg)
+
+
+def test_accuracy_and_mse_alarm_1k(jt, alarm_paths):
+    ev, gt = F.load_libsvm(alarm_paths["test"], 37)
+    gold = read_pt_file(alarm_paths["pt"], jt.network.dims, len(gt))
+    acc, mse, hd = jt.EvaluateAccuracy(ev, gt, gold)
+    _, _, ref_mse, ref_hd = read_ref_marg(os.path.join(GOLD, "alarm_1k.marg.gz"), jt.network.dims)
+    assert acc == 1.0
+    assert mse * len(gt) == ref_mse and hd * len(gt) == ref_hd
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1000])
+def test_ragged_batches_match_oracle(jt, ojt, n):
+    from fastbn_amd import synth
+    ev = synth.evidence_cases(synth.read_xmlbif(os.path.join(GOLD, "alarm", "alarm.xml")), n, 7, seed=n)
+    lab, marg = jt.infer(ev)
+    olab, omarg = ojt.infer(ev)
+    np.testing.assert_array_equal(lab, olab)
+    np.testing.assert_array_equal(marg, omarg)
+
+
+def test_evidence_extremes(jt, ojt):
+    rng = np.random.default_rng(3)
+    dims = jt.network.dims
+    ev = np.full((4, 37), -1, np.int8)
+    ev[1, 1:] = [rng.integers(0, d) for d in dims[1:]]  # everything but the query observed
+    ev[2, 1::2] = [rng.integers(0, d) for d in dims[1::2]]
+    ev[3, 36] = 0
+    lab, marg = jt.infer(ev)
+    olab, omarg = ojt.infer(ev)
+    np.testing.assert_array_equal(lab, olab)
+    np.testing.assert_array_equal(marg, omarg)
+    off = np.concatenate([[0], np.cumsum(dims)])
+    for v in range(37):  # evidence nodes -> zeros; others -> a distribution
+        s = marg[:, off[v]:off[v + 1]].sum(1)
+        obs = ev[:, v] >= 0
+        assert np.all(s[obs] == 0) and np.allclose(s[~obs], 1.0, atol=1e-12)
+
+
+def test_large_batch_vs_oracle_and_waves(jt, ojt):
+    from fastbn_amd import synth
+    net = synth.read_xmlbif(os.path.join(GOLD, "alarm", "alarm.xml"))
+    ev = synth.evidence_cases(net, 20000, 7, seed=20250131)
+    lab, marg = jt.infer(ev)
+    olab, omarg = ojt.infer(ev)
+    np.testing.assert_array_equal(lab, olab)
+    np.testing.assert_array_equal(marg, omarg)
+    for w in (1, 2, 8):
+        jt.set_waves_per_cu(w)
+        lab2, marg2 = jt.infer(ev)
+        np.testing.assert_array_equal(lab2, lab)
+        np.testing.assert_array_equal(marg2, marg)
+    jt.set_waves_per_cu(0)
+
+
+def test_synthetic_network(tmp_path):
+    from fastbn_amd import synth
+    p = str(tmp_path / "syn.xml")
+    synth.random_network(200, seed=11, window=10, path=p)
+    net = synth.read_xmlbif(p)
+    ev = synth.evidence_cases(net, 300, 40, seed=5)
+    jt = F.JunctionTree(F.Network(p), device=0)
+    lab, marg = jt.infer(ev)
+    olab, omarg = O.OracleJT(p).infer(ev)
+    np.testing.assert_array_equal(lab, olab)
+    np.testing.assert_array_equal(marg, omarg)
+
+
+def test_device_resident_path(jt, ojt):
+    torch = pytest.importorskip("torch")
+    from fastbn_amd import synth
+    ev = synth.evidence_cases(synth.read_xmlbif(os.path.join(GOLD, "alarm", "alarm.xml")), 4096, 7, seed=9)
+    d_ev = torch.from_numpy(ev).to("cuda")
+    d_lab = torch.zeros(4096, dtype=torch.int32, device="cuda")
+    d_marg = torch.zeros((4096, jt.info["sum_dom"]), dtype=torch.float64, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    jt.run_device(d_ev.data_ptr(), 4096, d_lab.data_ptr(), d_marg.data_ptr(), stream)
+    torch.cuda.synchronize()
+    olab, omarg = ojt.infer(ev)
+    np.testing.assert_array_equal(d_lab.cpu().numpy(), olab)
+    np.testing.assert_array_equal(d_marg.cpu().numpy(), omarg)
+
+
+def test_bad_evidence_rejected(jt):
+    ev = np.full((2, 37), -1, np.int8)
+    ev[1, 5] = 9
+    with pytest.raises(F.FastBNError, match="domain"):
+        jt.infer(ev)

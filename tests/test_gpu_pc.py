@@ -1,0 +1,78 @@
+"""CI-test kernel and PC-stable driver vs the reference's counts and the oracle."""
+import os
+
+import numpy as np
+import pytest
+from conftest import GOLD, read_ci_fixture
+
+import fastbn_amd as F
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def alarm_ds(alarm_paths):
+    return F.Dataset(alarm_paths["csv"])
+
+
+@pytest.fixture(scope="module")
+def ci(alarm_ds):
+    return F.IndependenceTest(alarm_ds, 0.05, device=0)
+
+
+def test_counts_bit_exact_vs_reference(ci):
+    _, _, tests = read_ci_fixture(os.path.join(GOLD, "alarm_s5000.ci.gz"))
+    for x, y, z, counts in tests:
+        np.testing.assert_array_equal(ci.counts(x, y, z), counts)
+
+
+def test_g2_df_p_vs_oracle(ci, alarm_paths):
+    od = O.OracleDataset(csv=alarm_paths["csv"])
+    _, _, tests = read_ci_fixture(os.path.join(GOLD, "alarm_s5000.ci.gz"))
+    by_d = {}
+    for x, y, z, _ in tests:
+        by_d.setdefault(len(z), []).append([x, y] + z)
+    for d, items in by_d.items():
+        g2, df, p, ind = ci.run(np.array(items, np.int32), d)
+        for k, it in enumerate(items):
+            r = od.ci_test(it[0], it[1], it[2:])
+            assert df[k] == r["df"]
+            assert abs(g2[k] - r["g2"]) <= 1e-12 * max(1.0, abs(r["g2"]))  # north star: 1e-6 rel
+            assert abs(p[k] - r["p_value"]) <= 1e-12
+            assert ind[k] == r["is_independent"]
+
+
+@pytest.mark.parametrize("gs", [1, 4])
+def test_pc_stable_alarm5000(alarm_ds, alarm_paths, gs):
+    od = O.OracleDataset(csv=alarm_paths["csv"])
+    ref = od.pc_stable(0.05, 1000, gs)
+    pc = F.PCStable(0.05, 1000).StructLearnCompData(alarm_ds, group_size=gs)
+    assert pc.tests_per_level.tolist() == ref["tests_per_level"]
+    assert pc.edges == ref["edges"]
+    assert pc.sepset == ref["sepset"]
+    if gs == 1:
+        assert pc.num_ci_test == 5206 and len(pc.edges) == 44
+
+
+def test_pc_stable_synthetic_and_ragged_samples(tmp_path):
+    from fastbn_amd import synth
+    p = str(tmp_path / "syn.xml")
+    synth.random_network(40, seed=3, window=6, path=p)
+    cols = synth.forward_sample(synth.read_xmlbif(p), 4999, seed=4)  # N % 4 != 0 -> scalar path
+    dims = cols.max(axis=1).astype(np.int32) + 1
+    ds = F.Dataset(columns=cols, dims=dims)
+    od = O.OracleDataset(columns=cols, dims=dims)
+    ref = od.pc_stable(0.05, 1000, 1)
+    pc = F.PCStable(0.05, 1000).StructLearnCompData(ds)
+    assert pc.tests_per_level.tolist() == ref["tests_per_level"]
+    assert pc.edges == ref["edges"] and pc.sepset == ref["sepset"]
+
+
+def test_constant_column_df0(tmp_path):
+    cols = np.zeros((3, 1000), np.uint8)
+    cols[1] = np.arange(1000) % 3
+    cols[2] = (np.arange(1000) // 7) % 2
+    ds = F.Dataset(columns=cols, dims=np.array([1, 3, 2], np.int32))
+    r = F.IndependenceTest(ds).IndependenceResult(0, 1, (2,))
+    assert r["df"] == 0 and r["is_independent"] and r["p_value"] == 1.0

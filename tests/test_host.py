@@ -1,0 +1,107 @@
+"""Product host code without a GPU: the C-ABI library, loaders and the junction-tree plan builder."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+from conftest import GOLD, REPO, read_ci_fixture, read_pt_file, read_ref_marg, fnv1a
+
+import fastbn_amd as F
+import oracle as O
+
+
+def header_symbols():
+    txt = open(os.path.join(REPO, "include", "fastbn.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(fbn_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = ctypes.CDLL(F.api.LIB_PATH)
+    syms = header_symbols()
+    assert len(syms) >= 35
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    # and the Python binding declares every one of them
+    assert set(syms) - {"fbn_last_error"} <= set(F.api._SIGS)
+
+
+def test_xmlbif_loader(alarm_paths):
+    net = F.Network(alarm_paths["xml"])
+    o = O.OracleJT(alarm_paths["xml"])
+    assert net.num_nodes == 37
+    np.testing.assert_array_equal(net.dims, o.dims)
+    assert net.name(0) == "HISTORY" and net.name(36) == "BP"
+
+
+def test_host_only_plan_matches_reference_dump(alarm_paths, tmp_path):
+    net = F.Network(alarm_paths["xml"])
+    jt = F.JunctionTree(net, device=-1)
+    jt.dump_plan(str(tmp_path / "p"), str(tmp_path / "i"))
+    assert open(tmp_path / "p").read() == open(os.path.join(GOLD, "alarm_1k.plan")).read()
+    assert open(tmp_path / "i").read() == open(os.path.join(GOLD, "alarm_1k.init")).read()
+    info = jt.info
+    assert info["num_cliques"] == 27 and info["num_separators"] == 26 and info["num_levels"] == 15
+    assert info["clique_entries"] == 1110 and info["separator_entries"] == 265
+    assert info["algorithmic_bytes_per_case"] == 22877
+    with pytest.raises(F.FastBNError, match="host-only"):
+        jt.infer(np.full((1, 37), -1, np.int8))
+
+
+def test_synthetic_network_plan_matches_oracle(tmp_path):
+    from fastbn_amd import synth
+    p = str(tmp_path / "syn.xml")
+    synth.random_network(120, seed=7, window=8, path=p)
+    jt = F.JunctionTree(F.Network(p), device=-1)
+    o = O.OracleJT(p)
+    jt.dump_plan(str(tmp_path / "a"), str(tmp_path / "b"))
+    o.dump_plan(str(tmp_path / "c"), str(tmp_path / "d"))
+    assert open(tmp_path / "a").read() == open(tmp_path / "c").read()
+    assert open(tmp_path / "b").read() == open(tmp_path / "d").read()
+
+
+def test_loaders_match_oracle_and_reference(alarm_paths):
+    ds = F.Dataset(alarm_paths["csv"])
+    od = O.OracleDataset(csv=alarm_paths["csv"])
+    np.testing.assert_array_equal(ds.dims, od.dims)
+    np.testing.assert_array_equal(ds.columns, od.columns)
+    dims, colhash, _ = read_ci_fixture(os.path.join(GOLD, "alarm_s5000.ci.gz"))
+    assert ds.dims.tolist() == dims
+    assert all(fnv1a(ds.columns[v]) == h for v, h in colhash.items())
+    assert ds.names[0] == "HISTORY"
+    for key in ("test", "rand"):
+        ev, lab = F.load_libsvm(alarm_paths[key], 37)
+        oev, olab = O.load_libsvm(alarm_paths[key], 37)
+        np.testing.assert_array_equal(ev, oev)
+        np.testing.assert_array_equal(lab, olab)
+
+
+def test_libsvm_unterminated_last_line_is_skipped(tmp_path):
+    p = tmp_path / "t.libsvm"
+    p.write_text("1 3:1 \n0 4:0")  # reference getline/eof loop never reads the last line
+    ev, lab = F.load_libsvm(str(p), 37)
+    assert ev.shape == (1, 37) and lab.tolist() == [1] and ev[0, 3] == 1
+
+
+def test_score_matches_reference_mse(alarm_paths):
+    """fbn_jt_score on the reference's own marginals reproduces its MSE/HD sums exactly."""
+    net = F.Network(alarm_paths["xml"])
+    jt = F.JunctionTree(net, device=-1)
+    _, rmarg, mse_ref, hd_ref = read_ref_marg(os.path.join(GOLD, "alarm_1k.marg.gz"), net.dims)
+    gold = read_pt_file(alarm_paths["pt"], net.dims, rmarg.shape[0])
+    mse, hd = jt.score(rmarg, gold)
+    assert mse == mse_ref and hd == hd_ref
+
+
+def test_errors_are_reported_not_fatal(tmp_path):
+    with pytest.raises(F.FastBNError, match="cannot open"):
+        F.Network(str(tmp_path / "missing.xml"))
+    bad = tmp_path / "bad.xml"
+    bad.write_text("<BIF><NETWORK><VARIABLE><NAME>A</NAME><TYPE>discrete</TYPE><VALUE>x</VALUE>"
+                   "<VALUE>y</VALUE></VARIABLE><PROBABILITY><FOR>A</FOR><TABLE>0.5 0.2 0.3 </TABLE>"
+                   "</PROBABILITY></NETWORK></BIF>")
+    with pytest.raises(F.FastBNError, match="too long"):
+        F.Network(str(bad))
+    with pytest.raises(F.FastBNError, match="cannot open"):
+        F.Dataset(str(tmp_path / "missing.csv"))
