@@ -34,6 +34,7 @@ _SIGS = {
     "fbn_jt_score": [_vp, _vp, _vp, _i64, _vp, _vp],
     "fbn_jt_last_kernel_ms": [_vp, _vp],
     "fbn_jt_set_waves_per_cu": [_vp, C.c_int],
+    "fbn_jt_set_variant": [_vp, C.c_int],
     "fbn_jt_plan_destroy": [_vp],
     "fbn_ci_dataset_upload": [_vp, C.c_int, _i64, _vp, C.c_int, _pp],
     "fbn_ci_run": [_vp, _vp, _i64, C.c_int, _dbl, _vp, _vp, _vp, _vp, _vp],
@@ -66,6 +67,12 @@ class _Lib:
         if self._h is None:
             if not os.path.exists(LIB_PATH):
                 raise FastBNError(f"{LIB_PATH} is missing: run __graft_entry__.build() (no CPU fallback)")
+            try:
+                # torch bundles its own libamdhip64.so.7 (same soname as /opt/rocm's): load it first
+                # so that one HIP runtime serves both when they share a process
+                import torch  # noqa: F401
+            except ImportError:
+                pass
             h = C.CDLL(LIB_PATH)
             for name, args in _SIGS.items():
                 f = getattr(h, name)
@@ -196,6 +203,10 @@ class JunctionTree:
 
     def set_waves_per_cu(self, w):
         lib.fbn_jt_set_waves_per_cu(self._h, w)
+
+    def set_variant(self, v):
+        """0 = clique-in-LDS kernel (default), 1 = global-workspace kernel."""
+        lib.fbn_jt_set_variant(self._h, v)
 
     def infer(self, evidence, marginals=True):
         """evidence [ncases][num_nodes] int8 (-1 unobserved) -> (labels, marginals or None)."""

@@ -21,6 +21,12 @@ extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, co
                                     uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
                                     hipStream_t stream);
 extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy);
+extern "C" hipError_t fbn_jt_lds_launch(const JtOp *ops, int nops, const int32_t *aux, const double *initv,
+                                        const uint64_t *dig, const int8_t *evid, int V, long long ncases, int SD,
+                                        double *marg, int32_t *labels, double *ws, int32_t *wsi, long long wave_entries,
+                                        long long store_off, long long den_off, long long sep_off,
+                                        long long spill_off, int nc, int cap, bool spill, int grid,
+                                        hipStream_t stream);
 
 namespace fbn {
 const char *LastError();
@@ -84,9 +90,11 @@ struct fbn_dataset {
 
 struct fbn_jt_plan {
     fbn::JTPlanHost host;
-    fbn::JTProgram prog;
-    int device = 0, num_cu = 0, waves_per_cu = 4;
+    fbn::JTProgram prog;      // variant 1: whole case state in a global workspace
+    fbn::JTProgramLDS lprog;  // variant 0 (default): clique in flight resident in LDS
+    int device = 0, num_cu = 0, waves_per_cu = 0, variant = 0;
     DevBuf ops, aux, initv, dig;
+    DevBuf lops, laux, linitv, ldig;
     DevBuf evid, labels, marg, ws;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
@@ -226,6 +234,11 @@ static int JtUpload(fbn_jt_plan *p) {
     if ((rc = up(p->aux, g.aux.data(), g.aux.size() * 4))) return rc;
     if ((rc = up(p->initv, g.initv.data(), g.initv.size() * 8))) return rc;
     if ((rc = up(p->dig, g.dig.data(), g.dig.size() * 8))) return rc;
+    const auto &l = p->lprog;
+    if ((rc = up(p->lops, l.ops.data(), l.ops.size() * sizeof(JtOp)))) return rc;
+    if ((rc = up(p->laux, l.aux.data(), l.aux.size() * 4))) return rc;
+    if ((rc = up(p->linitv, l.initv.data(), l.initv.size() * 8))) return rc;
+    if ((rc = up(p->ldig, l.dig.data(), l.dig.size() * 8))) return rc;
     return FBN_OK;
 }
 
@@ -236,6 +249,8 @@ int fbn_jt_plan_create(const fbn_network *net, int device, fbn_jt_plan **out) {
     int rc = fbn::BuildJTPlan(net->net, p->host);
     if (rc) return rc;
     rc = fbn::CompileJTProgram(p->host, p->prog);
+    if (rc) return rc;
+    rc = fbn::CompileJTProgramLDS(p->host, p->lprog);
     if (rc) return rc;
     p->device = device;
     if (device >= 0) {  // device < 0: host-only plan (info / dump), runs fail with FBN_ERR_NODEV
@@ -310,8 +325,26 @@ int fbn_jt_plan_dump(const fbn_jt_plan *p, const char *plan_path, const char *in
 
 int fbn_jt_set_waves_per_cu(fbn_jt_plan *p, int waves) {
     if (!p || waves < 0 || waves > 32) return SetError(FBN_ERR_ARG, "waves per CU must be 0..32");
-    p->waves_per_cu = waves ? waves : 4;
+    p->waves_per_cu = waves;
     return FBN_OK;
+}
+
+int fbn_jt_set_variant(fbn_jt_plan *p, int variant) {
+    if (!p || variant < 0 || variant > 1) return SetError(FBN_ERR_ARG, "variant must be 0 (LDS) or 1 (global)");
+    p->variant = variant;
+    return FBN_OK;
+}
+
+static const size_t kLdsBytes = 160 * 1024;
+
+// LDS variant geometry: waves per CU and the number of LDS table rows (64 lanes x 8 B each)
+static void LdsGeometry(const fbn_jt_plan *p, int *waves, int *cap) {
+    const int64_t row = 64 * 8, tmax = std::max<int64_t>(1, p->lprog.max_table);
+    int w = p->waves_per_cu;
+    if (w <= 0) w = (int)std::max<int64_t>(1, std::min<int64_t>(8, (int64_t)kLdsBytes / (tmax * row)));
+    int64_t c = std::min<int64_t>(tmax, (int64_t)(kLdsBytes / w) / row);
+    *waves = w;
+    *cap = (int)std::max<int64_t>(1, c);
 }
 
 int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, int32_t *d_labels,
@@ -324,11 +357,7 @@ int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, 
     const auto &g = p->prog;
     const int V = p->host.num_nodes, SD = g.sum_dom, nc = g.num_cliques;
     const int64_t nblk = (ncases + 63) / 64;
-    const int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * p->waves_per_cu);
     int rc;
-    const size_t ws_d = (size_t)grid * g.state_entries * 64 * 8;
-    const size_t ws_i = (size_t)grid * nc * 64 * 4;
-    if ((rc = p->ws.ensure(ws_d + ws_i))) return rc;
     double *marg = d_marginals;
     if (!marg) {
         if ((rc = p->marg.ensure((size_t)ncases * SD * 8))) return rc;
@@ -339,10 +368,35 @@ int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, 
         if ((rc = p->labels.ensure((size_t)ncases * 4))) return rc;
         labels = p->labels.as<int32_t>();
     }
-    FBN_HIP(hipEventRecord(p->ev0, s));
-    hipError_t e = fbn_jt_launch(p->ops.as<JtOp>(), (int)g.ops.size(), p->aux.as<int32_t>(), p->initv.as<double>(),
-                                 p->dig.as<uint64_t>(), d_evidence, V, ncases, SD, marg, labels, p->ws.as<double>(),
-                                 reinterpret_cast<int32_t *>(p->ws.as<char>() + ws_d), g.state_entries, nc, grid, s);
+    hipError_t e;
+    if (p->variant == 1) {
+        const int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 8;
+        const int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * wpc);
+        const size_t ws_d = (size_t)grid * g.state_entries * 64 * 8;
+        const size_t ws_i = (size_t)grid * nc * 64 * 4;
+        if ((rc = p->ws.ensure(ws_d + ws_i))) return rc;
+        FBN_HIP(hipEventRecord(p->ev0, s));
+        e = fbn_jt_launch(p->ops.as<JtOp>(), (int)g.ops.size(), p->aux.as<int32_t>(), p->initv.as<double>(),
+                          p->dig.as<uint64_t>(), d_evidence, V, ncases, SD, marg, labels, p->ws.as<double>(),
+                          reinterpret_cast<int32_t *>(p->ws.as<char>() + ws_d), g.state_entries, nc, grid, s);
+    } else {
+        const auto &l = p->lprog;
+        int wpc, cap;
+        LdsGeometry(p, &wpc, &cap);
+        const bool spill = cap < l.max_table;
+        const int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * wpc);
+        const int64_t store_off = 0, den_off = l.store_entries, sep_off = den_off + nc,
+                      spill_off = sep_off + l.sep_entries;
+        const int64_t wave_entries = spill_off + (spill ? l.max_table - cap : 0);
+        const size_t ws_d = (size_t)grid * wave_entries * 64 * 8;
+        const size_t ws_i = (size_t)grid * nc * 64 * 4;
+        if ((rc = p->ws.ensure(ws_d + ws_i))) return rc;
+        FBN_HIP(hipEventRecord(p->ev0, s));
+        e = fbn_jt_lds_launch(p->lops.as<JtOp>(), (int)l.ops.size(), p->laux.as<int32_t>(), p->linitv.as<double>(),
+                              p->ldig.as<uint64_t>(), d_evidence, V, ncases, SD, marg, labels, p->ws.as<double>(),
+                              reinterpret_cast<int32_t *>(p->ws.as<char>() + ws_d), wave_entries, store_off, den_off,
+                              sep_off, spill_off, nc, cap, spill, grid, s);
+    }
     if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt kernel launch: %s", hipGetErrorString(e));
     FBN_HIP(hipEventRecord(p->ev1, s));
     p->timed = true;

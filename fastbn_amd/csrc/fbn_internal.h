@@ -74,6 +74,20 @@ struct JTProgram {
 };
 int CompileJTProgram(const JTPlanHost &plan, JTProgram &prog);
 
+// LDS-resident variant: per-wave global regions (entries of 64 lanes x fp64)
+struct JTProgramLDS {
+    std::vector<JtOp> ops;
+    std::vector<int32_t> aux;
+    std::vector<double> initv;
+    std::vector<uint64_t> dig;
+    int64_t store_entries = 0;  // parked collect tables (all cliques but the root)
+    int64_t sep_entries = 0;    // separator messages
+    int64_t max_table = 0;      // largest clique table (LDS rows needed for no spill)
+    int num_cliques = 0;
+    int sum_dom = 0;
+};
+int CompileJTProgramLDS(const JTPlanHost &plan, JTProgramLDS &prog);
+
 }  // namespace fbn
 
 #endif

@@ -419,3 +419,127 @@ int CompileJTProgram(const JTPlanHost &plan, JTProgram &prog) {
 }
 
 }  // namespace fbn
+
+// ---------------------------------------------------------------------------------------------
+// LDS-resident program: cliques one at a time (see jt_program.h)
+namespace fbn {
+
+int CompileJTProgramLDS(const JTPlanHost &plan, JTProgramLDS &prog) {
+    prog = JTProgramLDS();
+    const int nc = (int)plan.cliques.size(), ns = (int)plan.seps.size();
+    prog.num_cliques = nc;
+    for (int d : plan.dom) prog.sum_dom += d;
+    std::vector<int64_t> store_off(nc, -1), sep_off(ns);
+    for (int c = 0; c < nc; ++c) {
+        prog.max_table = std::max<int64_t>(prog.max_table, plan.cliques[c].size());
+        if (c == plan.root) continue;  // the root never leaves LDS between the two phases
+        store_off[c] = prog.store_entries;
+        prog.store_entries += plan.cliques[c].size();
+    }
+    for (int s = 0; s < ns; ++s) sep_off[s] = prog.sep_entries, prog.sep_entries += plan.seps[s].size();
+    if (prog.store_entries + prog.sep_entries + prog.max_table > INT32_MAX / 64)
+        return SetError(FBN_ERR_LIMIT, "junction tree too large for the LDS program");
+
+    auto op = [&](int32_t type, int64_t a, int64_t b, int64_t c, int64_t d, int64_t e, int64_t f = 0, int64_t g = 0,
+                  int64_t h = 0, int64_t pad = 0) {
+        prog.ops.push_back(JtOp{type, (int32_t)a, (int32_t)b, (int32_t)c, (int32_t)d, (int32_t)e, (int32_t)f,
+                                (int32_t)g, (int32_t)h, (int32_t)pad});
+    };
+    auto sub_index = [&](const Table &t, const Table &sub, int64_t e) {
+        int64_t r = e, idx = 0;
+        for (size_t j = 0; j < t.vars.size(); ++j) {
+            int64_t digit = r / t.cum[j];
+            r %= t.cum[j];
+            int l = LocOf(sub, t.vars[j]);
+            if (l >= 0) idx += digit * sub.cum[l];
+        }
+        return idx;
+    };
+    auto emit_init = [&](int c) -> int {
+        const Table &t = plan.cliques[c];
+        const int nv = (int)t.vars.size();
+        if (nv > 8 * JT_MAX_DIG_WORDS) return SetError(FBN_ERR_LIMIT, "clique with %d variables (max %d)", nv, 8 * JT_MAX_DIG_WORDS);
+        const int nw = std::max(1, (nv + 7) / 8);
+        int64_t vars_off = (int64_t)prog.aux.size();
+        for (int v : t.vars) prog.aux.push_back(v);
+        int64_t dig_off = (int64_t)prog.dig.size();
+        for (int64_t e = 0; e < t.size(); ++e) {
+            uint64_t w[JT_MAX_DIG_WORDS] = {0, 0, 0, 0};
+            int64_t r = e;
+            for (int j = 0; j < nv; ++j) {
+                w[j / 8] |= (uint64_t)(r / t.cum[j]) << (8 * (j % 8));
+                r %= t.cum[j];
+            }
+            for (int k = 0; k < nw; ++k) prog.dig.push_back(w[k]);
+        }
+        int64_t init_off = (int64_t)prog.initv.size();
+        prog.initv.insert(prog.initv.end(), t.pot.begin(), t.pot.end());
+        op(JT_L_INIT, 0, t.size(), vars_off, nv, dig_off, 0, c, init_off);
+        return FBN_OK;
+    };
+    // candidate cliques per variable, container order (GetProbabilitiesOneNode's scan)
+    std::vector<std::vector<int>> cand(plan.num_nodes);
+    for (int c = 0; c < nc; ++c)
+        for (int v : plan.cliques[c].vars) cand[v].push_back(c);
+    std::vector<int64_t> cand_off(plan.num_nodes), out_off(plan.num_nodes);
+    int64_t oo = 0;
+    for (int v = 0; v < plan.num_nodes; ++v) {
+        if (cand[v].empty()) return SetError(FBN_ERR_ARG, "variable %d appears in no clique", v);
+        cand_off[v] = (int64_t)prog.aux.size();
+        prog.aux.insert(prog.aux.end(), cand[v].begin(), cand[v].end());
+        out_off[v] = oo;
+        oo += plan.dom[v];
+    }
+
+    const int L = (int)plan.levels.size();
+    // Collect: clique levels deepest first (src/JunctionTree.cpp:1240-1306)
+    for (int i = ((L - 1) / 2) * 2; i >= 0; i -= 2) {
+        for (int c : plan.levels[i]) {
+            const Table &t = plan.cliques[c];
+            int rc = emit_init(c);
+            if (rc) return rc;
+            for (int s : plan.clique_down[c]) {
+                int64_t map_off = (int64_t)prog.aux.size();
+                for (int64_t e = 0; e < t.size(); ++e) prog.aux.push_back((int32_t)sub_index(t, plan.seps[s], e));
+                op(JT_L_MUL, 0, t.size(), 0, sep_off[s], map_off);
+            }
+            if (c != plan.root) {
+                int s = plan.clique_up[c];
+                op(JT_L_SEPCOL, sep_off[s], plan.seps[s].size(), t.size(), 0, 0);
+                op(JT_L_STORE, store_off[c], t.size(), c, 0, 0);
+            }
+        }
+    }
+    // Distribute: clique levels root first (src/JunctionTree.cpp:1308-1333) + outputs
+    for (int i = 0; i < L; i += 2) {
+        for (int c : plan.levels[i]) {
+            const Table &t = plan.cliques[c];
+            if (c != plan.root) {
+                int s = plan.clique_up[c];
+                op(JT_L_LOAD, store_off[c], t.size(), c, 0, 0);
+                op(JT_L_DMUL, 0, t.size(), 0, sep_off[s], plan.seps[s].size());
+            }
+            for (int s : plan.clique_down[c]) {
+                const int64_t Ts = plan.seps[s].size(), per = t.size() / Ts;
+                std::vector<std::vector<int32_t>> lists(Ts);
+                for (int64_t e = 0; e < t.size(); ++e) lists[sub_index(t, plan.seps[s], e)].push_back((int32_t)e);
+                int64_t list_off = (int64_t)prog.aux.size();
+                for (auto &l : lists) {
+                    if ((int64_t)l.size() != per) return SetError(FBN_ERR_ARG, "internal: ragged separator map");
+                    prog.aux.insert(prog.aux.end(), l.begin(), l.end());
+                }
+                op(JT_L_SEPDIS, sep_off[s], Ts, 0, 0, list_off, per);
+            }
+            for (size_t j = 0; j < t.vars.size(); ++j) {
+                int v = t.vars[j];
+                op(JT_L_MARG, out_off[v], plan.dom[v], cand_off[v], (int64_t)cand[v].size(), v, v == 0 ? 1 : 0, c,
+                   t.cum[j], t.size());
+            }
+        }
+    }
+    for (int v = 0; v < plan.num_nodes; ++v) op(JT_L_EVZERO, out_off[v], plan.dom[v], 0, 0, v);
+    if (prog.aux.size() > (size_t)INT32_MAX) return SetError(FBN_ERR_LIMIT, "device program too large");
+    return FBN_OK;
+}
+
+}  // namespace fbn

@@ -36,6 +36,24 @@ enum JtOpType : int32_t {
     JT_OP_MARG = 6
 };
 
+// ---- LDS-resident variant (jt_lds_kernel): the clique being worked on lives in LDS (lane = case,
+// [entry][64] layout), its pending normalization denominator in a register; finished collect
+// tables are parked in a per-wave global store and read back once in Distribute, separator
+// messages live in a per-wave global store.  Cliques are processed one at a time, children before
+// parents in Collect and parents before children in Distribute (the reference's level order).
+enum JtLOpType : int32_t {
+    JT_L_INIT = 11,    // b=T, c=aux off of var list, d=nv, e=dig word off, g=clique id, h=initv off
+    JT_L_MUL = 12,     // b=T, d=sep store off, e=aux off of map[T]          (CliqueLevelCollection)
+    JT_L_SEPCOL = 13,  // a=sep store off, b=Ts, c=T                          (SeparatorLevelCollection)
+    JT_L_STORE = 14,   // a=store off, b=T, c=clique id (den slot)
+    JT_L_LOAD = 15,    // a=store off, b=T, c=clique id
+    JT_L_DMUL = 16,    // b=T, d=sep store off, e=Ts                          (CliqueLevelDistribution)
+    JT_L_SEPDIS = 17,  // a=sep store off, b=Ts, e=aux off of lists[Ts][f], f=T/Ts (SeparatorLevelDistribution)
+    JT_L_MARG = 18,    // a=out off, b=dim, c=aux off of candidate clique ids, d=#candidates, e=var,
+                       // f=is query, g=this clique id, h=cum of var in this clique, pad=T
+    JT_L_EVZERO = 19   // a=out off, b=dim, e=var
+};
+
 struct JtOp {
     int32_t type, a, b, c, d, e, f, g, h, pad;
 };

@@ -104,8 +104,10 @@ int fbn_jt_score(const fbn_jt_plan *p, const double *marginals, const double *go
                  double *mse_sum, double *hd_sum);
 /* Device kernel time (ms, hipEvent) of the last fbn_jt_run*; launches of the main kernel. */
 int fbn_jt_last_kernel_ms(const fbn_jt_plan *p, float *ms);
-/* Tuning: persistent waves per CU (0 = default). */
+/* Tuning: persistent waves per CU (0 = default: as many as keep the largest clique in LDS). */
 int fbn_jt_set_waves_per_cu(fbn_jt_plan *p, int waves);
+/* Kernel variant: 0 = clique-in-LDS (default), 1 = whole case state in a global workspace. */
+int fbn_jt_set_variant(fbn_jt_plan *p, int variant);
 int fbn_jt_plan_destroy(fbn_jt_plan *p);
 
 /* ------------------------------------------------------------------ CI tests (G^2) */

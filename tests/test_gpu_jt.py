@@ -76,11 +76,14 @@ def test_large_batch_vs_oracle_and_waves(jt, ojt):
     olab, omarg = ojt.infer(ev)
     np.testing.assert_array_equal(lab, olab)
     np.testing.assert_array_equal(marg, omarg)
-    for w in (1, 2, 8):
-        jt.set_waves_per_cu(w)
+    # both kernel variants; LDS variant with and without spilled rows (w=4 -> 80 LDS rows < 144)
+    for variant, waves in ((0, 1), (0, 2), (0, 4), (0, 8), (1, 2), (1, 8)):
+        jt.set_variant(variant)
+        jt.set_waves_per_cu(waves)
         lab2, marg2 = jt.infer(ev)
         np.testing.assert_array_equal(lab2, lab)
         np.testing.assert_array_equal(marg2, marg)
+    jt.set_variant(0)
     jt.set_waves_per_cu(0)
 
 
@@ -91,10 +94,12 @@ def test_synthetic_network(tmp_path):
     net = synth.read_xmlbif(p)
     ev = synth.evidence_cases(net, 300, 40, seed=5)
     jt = F.JunctionTree(F.Network(p), device=0)
-    lab, marg = jt.infer(ev)
     olab, omarg = O.OracleJT(p).infer(ev)
-    np.testing.assert_array_equal(lab, olab)
-    np.testing.assert_array_equal(marg, omarg)
+    for variant in (0, 1):
+        jt.set_variant(variant)
+        lab, marg = jt.infer(ev)
+        np.testing.assert_array_equal(lab, olab)
+        np.testing.assert_array_equal(marg, omarg)
 
 
 def test_device_resident_path(jt, ojt):
