@@ -35,6 +35,7 @@ _SIGS = {
     "fbn_jt_last_kernel_ms": [_vp, _vp],
     "fbn_jt_set_waves_per_cu": [_vp, C.c_int],
     "fbn_jt_set_variant": [_vp, C.c_int],
+    "fbn_jt_debug_op_cycles": [_vp, C.c_int, _vp],
     "fbn_jt_plan_destroy": [_vp],
     "fbn_ci_dataset_upload": [_vp, C.c_int, _i64, _vp, C.c_int, _pp],
     "fbn_ci_run": [_vp, _vp, _i64, C.c_int, _dbl, _vp, _vp, _vp, _vp, _vp],
@@ -203,6 +204,13 @@ class JunctionTree:
 
     def set_waves_per_cu(self, w):
         lib.fbn_jt_set_waves_per_cu(self._h, w)
+
+    def op_cycles(self, enable, read=True):
+        """Diagnostic per-op-type cycles of the last run (LDS variant)."""
+        buf = np.zeros(10, np.uint64)
+        lib.fbn_jt_debug_op_cycles(self._h, int(enable), _p(buf) if read else None)
+        names = ["INIT", "MUL", "SEPCOL", "STORE", "LOAD", "DMUL", "SEPDIS", "MARG", "EVZERO", "-"]
+        return dict(zip(names, buf.tolist()))
 
     def set_variant(self, v):
         """0 = clique-in-LDS kernel (default), 1 = global-workspace kernel."""

@@ -25,8 +25,8 @@ extern "C" hipError_t fbn_jt_lds_launch(const JtOp *ops, int nops, const int32_t
                                         const uint64_t *dig, const int8_t *evid, int V, long long ncases, int SD,
                                         double *marg, int32_t *labels, double *ws, int32_t *wsi, long long wave_entries,
                                         long long store_off, long long den_off, long long sep_off,
-                                        long long spill_off, int nc, int cap, bool spill, int grid,
-                                        hipStream_t stream);
+                                        long long spill_off, int nc, int cap, bool spill, int force_exact,
+                                        int grid, unsigned long long *prof, hipStream_t stream);
 
 namespace fbn {
 const char *LastError();
@@ -95,6 +95,9 @@ struct fbn_jt_plan {
     int device = 0, num_cu = 0, waves_per_cu = 0, variant = 0;
     DevBuf ops, aux, initv, dig;
     DevBuf lops, laux, linitv, ldig;
+    DevBuf prof;       // diagnostic per-op-type cycle counters
+    bool prof_on = false;
+    int last_grid = 0;
     DevBuf evid, labels, marg, ws;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
@@ -330,8 +333,24 @@ int fbn_jt_set_waves_per_cu(fbn_jt_plan *p, int waves) {
 }
 
 int fbn_jt_set_variant(fbn_jt_plan *p, int variant) {
-    if (!p || variant < 0 || variant > 1) return SetError(FBN_ERR_ARG, "variant must be 0 (LDS) or 1 (global)");
+    if (!p || variant < 0 || variant > 2) return SetError(FBN_ERR_ARG, "variant must be 0 (LDS), 1 (global) or 2 (LDS, IEEE division)");
     p->variant = variant;
+    return FBN_OK;
+}
+
+// diagnostic: per-op-type cycle totals of the LDS variant (s_memtime, summed over waves)
+int fbn_jt_debug_op_cycles(fbn_jt_plan *p, int enable, unsigned long long *cycles /* [10] or NULL */) {
+    if (!p) return SetError(FBN_ERR_ARG, "null pointer");
+    if (cycles && p->prof_on && p->last_grid > 0) {
+        std::vector<unsigned long long> h((size_t)p->last_grid * 16);
+        FBN_HIP(hipDeviceSynchronize());
+        FBN_HIP(hipMemcpy(h.data(), p->prof.p, h.size() * 8, hipMemcpyDeviceToHost));
+        for (int k = 0; k < 10; ++k) {
+            cycles[k] = 0;
+            for (int w = 0; w < p->last_grid; ++w) cycles[k] += h[(size_t)w * 16 + k];
+        }
+    }
+    p->prof_on = enable != 0;
     return FBN_OK;
 }
 
@@ -391,11 +410,17 @@ int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, 
         const size_t ws_d = (size_t)grid * wave_entries * 64 * 8;
         const size_t ws_i = (size_t)grid * nc * 64 * 4;
         if ((rc = p->ws.ensure(ws_d + ws_i))) return rc;
+        if (p->prof_on) {
+            if ((rc = p->prof.ensure((size_t)grid * 16 * 8))) return rc;
+            FBN_HIP(hipMemsetAsync(p->prof.p, 0, (size_t)grid * 16 * 8, s));
+        }
+        p->last_grid = grid;
         FBN_HIP(hipEventRecord(p->ev0, s));
         e = fbn_jt_lds_launch(p->lops.as<JtOp>(), (int)l.ops.size(), p->laux.as<int32_t>(), p->linitv.as<double>(),
                               p->ldig.as<uint64_t>(), d_evidence, V, ncases, SD, marg, labels, p->ws.as<double>(),
                               reinterpret_cast<int32_t *>(p->ws.as<char>() + ws_d), wave_entries, store_off, den_off,
-                              sep_off, spill_off, nc, cap, spill, grid, s);
+                              sep_off, spill_off, nc, cap, spill, p->variant == 2, grid,
+                              p->prof_on ? p->prof.as<unsigned long long>() : nullptr, s);
     }
     if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt kernel launch: %s", hipGetErrorString(e));
     FBN_HIP(hipEventRecord(p->ev1, s));

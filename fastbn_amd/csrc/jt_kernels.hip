@@ -198,49 +198,164 @@ __global__ __launch_bounds__(64) void jt_interp_kernel(JtArgs A) {
 // LDS-resident variant: the clique in flight is held in LDS ([entry][64 lanes], rows >= cap spill
 // to a per-wave global buffer), its pending denominator in a register.  HBM sees each clique table
 // once when parked after Collect and once when reloaded in Distribute, plus the separator messages.
-struct JtLArgs {
-    const JtOp *ops;
-    const int32_t *aux;
-    const double *initv;
-    const uint64_t *dig;
-    const int8_t *evid;
-    double *marg;
-    int32_t *labels;
-    double *ws;     // per wave: [store][dens nc][sep][spill] x 64
-    int32_t *wsi;   // per wave: [nc] x 64 (reduced variable counts)
+struct JtLParams {
     long long ncases;
     long long wave_entries;  // store + nc + sep + spill
     long long store_off, den_off, sep_off, spill_off;
     int nops, V, SD, nc, cap;
+    int force_exact;  // ablation/testing: always take the IEEE division path
 };
 
+// Pointers are separate __restrict__ kernel arguments (not a struct): the compiler can then prove
+// that the program arrays are never written and turns their wave-uniform reads into SMEM loads.
+// Division by the pending denominator.  Markstein: with y = RN(1/den) and q = RN(x*y) within one
+// ulp of x/den, q + RN(x - den*q)*y (two fmas) is the correctly rounded quotient -- the same bits as
+// the reference's `potentials[i] /= denominator` -- as long as nothing under/overflows.  The fast form
+// is used when den lies in [2^-600, 2^600] for every lane of the wave (then any table value >= 2^-400
+// keeps every intermediate normal); otherwise the op runs with the IEEE division sequence.
+struct Den {
+    double den, y;
+};
+template <bool EXACT>
+__device__ __forceinline__ double dv(double x, const Den &d) {
+    if (EXACT) return x / d.den;
+    const double q = x * d.y;
+    const double r = __builtin_fma(-d.den, q, x);
+    return __builtin_fma(r, d.y, q);
+}
+__device__ __forceinline__ bool den_fast_all(double den) {
+    return __ballot(!(den >= 0x1p-600 && den <= 0x1p+600)) == 0ull;
+}
+
+// the clique in flight: LDS rows [0, cap), spilled rows in per-wave global memory
 template <bool SPILL>
-__global__ __launch_bounds__(64) void jt_lds_kernel(JtLArgs A) {
+struct Tab {
+    double *__restrict__ lds;
+    double *__restrict__ spill;
+    int cap;
+    __device__ __forceinline__ double &operator[](int e) const {
+        return (!SPILL || e < cap) ? lds[(size_t)e * 64] : spill[(size_t)(e - cap) * 64];
+    }
+};
+
+// parent *= extended child message, then the normalization sum in entry order (:829-941).
+// By separator entry: one message load per separator entry, parent entries from the inverse map.
+template <bool SPILL, bool EXACT>
+__device__ void op_mul(const Tab<SPILL> &T, Den &D, const double *__restrict__ sp, const int32_t *__restrict__ ls,
+                       int Ts, int Tn) {
+    const int per = Tn / Ts;
+    for (int j = 0; j < Ts; ++j) {
+        const double m = sp[(size_t)j * 64];
+        const int32_t *__restrict__ l = ls + j * per;
+#pragma unroll 8
+        for (int q = 0; q < per; ++q) {
+            const int e = l[q];
+            T[e] = dv<EXACT>(T[e], D) * m;
+        }
+    }
+    double sum = 0.0;
+#pragma unroll 8
+    for (int e = 0; e < Tn; ++e) sum += T[e];
+    D.den = sum;
+    D.y = 1.0 / sum;
+}
+
+// child *= parent message broadcast over k % Ts, then Normalize (:1150-1238)
+template <bool SPILL, bool EXACT>
+__device__ void op_dmul(const Tab<SPILL> &T, Den &D, const double *__restrict__ sp, int Ts, int Tn) {
+    const int Q = Tn / Ts;
+    for (int j = 0; j < Ts; ++j) {
+        const double m = sp[(size_t)j * 64];
+#pragma unroll 8
+        for (int q = 0; q < Q; ++q) {
+            const int e = q * Ts + j;
+            T[e] = dv<EXACT>(T[e], D) * m;
+        }
+    }
+    double sum = 0.0;
+#pragma unroll 8
+    for (int e = 0; e < Tn; ++e) sum += T[e];
+    D.den = sum;
+    D.y = 1.0 / sum;
+}
+
+// message to the parent: tmp[k % Ts] += child[k]; the separator's old value is its masked all-ones
+// table (x / 1.0 == x; its zero entries face child entries that are masked to zero) (:1056-1148)
+template <bool SPILL, bool EXACT>
+__device__ void op_sepcol(const Tab<SPILL> &T, const Den &D, double *__restrict__ sp, int Ts, int Tn) {
+    const int Q = Tn / Ts;
+    for (int j = 0; j < Ts; ++j) {
+        double acc = 0.0;
+#pragma unroll 8
+        for (int q = 0; q < Q; ++q) acc += dv<EXACT>(T[q * Ts + j], D);
+        sp[(size_t)j * 64] = acc;
+    }
+}
+
+// tmp[map(k)] += parent[k]; sep = tmp / old, zero-guarded (:700-816)
+template <bool SPILL, bool EXACT>
+__device__ void op_sepdis(const Tab<SPILL> &T, const Den &D, double *__restrict__ sp, const int32_t *__restrict__ ls,
+                          int Ts, int per) {
+    for (int j = 0; j < Ts; ++j) {
+        const int32_t *__restrict__ l = ls + j * per;
+        double acc = 0.0;
+#pragma unroll 8
+        for (int q = 0; q < per; ++q) acc += dv<EXACT>(T[l[q]], D);
+        const double old = sp[(size_t)j * 64];
+        sp[(size_t)j * 64] = (old == 0.0) ? 0.0 : acc / old;
+    }
+}
+
+// marginal of one variable from the clique (TableMarginalization in entry order), un-normalized
+template <bool SPILL, bool EXACT>
+__device__ void op_marg(const Tab<SPILL> &T, const Den &D, double *__restrict__ o, bool act, int dim, int cum,
+                        int Tn, double &tot) {
+    const int bw = dim * cum, nhi = Tn / bw;
+    tot = 0.0;
+    for (int d = 0; d < dim; ++d) {
+        double acc = 0.0;
+        for (int hi = 0; hi < nhi; ++hi) {
+            const int base = hi * bw + d * cum;
+#pragma unroll 8
+            for (int lo = 0; lo < cum; ++lo) acc += dv<EXACT>(T[base + lo], D);
+        }
+        if (act) o[d] = acc;
+        tot += acc;
+    }
+}
+
+// PROF: diagnostic build that accumulates s_memtime cycles per op type (prof[wave][32])
+template <bool SPILL, bool PROF = false>
+__global__ __launch_bounds__(64) void jt_lds_kernel(const JtOp *__restrict__ ops, const int32_t *__restrict__ aux,
+                                                   const double *__restrict__ initv,
+                                                   const uint64_t *__restrict__ dig,
+                                                   const int8_t *__restrict__ evid, double *__restrict__ marg,
+                                                   int32_t *__restrict__ labels, double *__restrict__ ws,
+                                                   int32_t *__restrict__ wsi, const JtLParams A,
+                                                   unsigned long long *__restrict__ prof = nullptr) {
+    unsigned long long pc[24] = {0};
     extern __shared__ double lds[];
     const int lane = threadIdx.x;
-    double *__restrict__ W = A.ws + (size_t)blockIdx.x * (size_t)A.wave_entries * 64 + lane;
+    double *__restrict__ W = ws + (size_t)blockIdx.x * (size_t)A.wave_entries * 64 + lane;
     double *__restrict__ store = W + (size_t)A.store_off * 64;
     double *__restrict__ dens = W + (size_t)A.den_off * 64;
     double *__restrict__ sep = W + (size_t)A.sep_off * 64;
-    double *__restrict__ spill = W + (size_t)A.spill_off * 64;
-    int32_t *__restrict__ red = A.wsi + (size_t)blockIdx.x * (size_t)A.nc * 64 + lane;
-    double *__restrict__ T = lds + lane;
-    const JtOp *__restrict__ ops = A.ops;
-    const int32_t *__restrict__ aux = A.aux;
-    const int cap = A.cap;
-#define TT(e) (*((!SPILL || (e) < cap) ? &T[(size_t)(e) * 64] : &spill[(size_t)((e) - cap) * 64]))
-#define SP(e) sep[(size_t)(e) * 64]
+    int32_t *__restrict__ red = wsi + (size_t)blockIdx.x * (size_t)A.nc * 64 + lane;
+    const Tab<SPILL> T{lds + lane, W + (size_t)A.spill_off * 64, A.cap};
 
     for (long long blk = blockIdx.x; blk * 64 < A.ncases; blk += gridDim.x) {
         const long long cs = blk * 64 + lane;
         const bool act = cs < A.ncases;
         const long long csr = act ? cs : A.ncases - 1;
-        const int8_t *__restrict__ ev = A.evid + csr * A.V;
-        double *__restrict__ out = A.marg + csr * A.SD;
-        double den = 1.0;  // pending normalization denominator of the clique in LDS
+        const int8_t *__restrict__ ev = evid + csr * A.V;
+        double *__restrict__ out = marg + csr * A.SD;
+        Den D{1.0, 1.0};  // the clique in LDS is T[e] / D.den
+        bool fast = true;
 
         for (int i = 0; i < A.nops; ++i) {
             const JtOp op = ops[i];
+            unsigned long long t0 = 0;
+            if (PROF) t0 = __builtin_amdgcn_s_memtime();
             switch (op.type) {
             case JT_L_INIT: {  // masked initial potential + post-evidence Normalize (:1479-1483)
                 const int nv = op.d;
@@ -257,10 +372,10 @@ __global__ __launch_bounds__(64) void jt_lds_kernel(JtLArgs A) {
                     else M3 |= m, W3 |= w;
                 }
                 const int nw = nv > 8 ? (nv + 7) / 8 : 1;
-                const uint64_t *__restrict__ dg = A.dig + op.e;
-                const double *__restrict__ iv = A.initv + op.h;
+                const uint64_t *__restrict__ dg = dig + op.e;
+                const double *__restrict__ iv = initv + op.h;
                 double sum = 0.0;
-#pragma unroll 4
+#pragma unroll 8
                 for (int e = 0; e < op.b; ++e) {
                     const uint64_t *d = dg + (size_t)e * nw;
                     bool cons = (d[0] & M0) == W0;
@@ -268,78 +383,55 @@ __global__ __launch_bounds__(64) void jt_lds_kernel(JtLArgs A) {
                     if (nw > 2) cons = cons && ((d[2] & M2) == W2);
                     if (nw > 3) cons = cons && ((d[3] & M3) == W3);
                     const double val = cons ? iv[e] : 0.0;
-                    TT(e) = val;
+                    T[e] = val;
                     sum += val;
                 }
-                den = sum;
+                D.den = sum;
+                D.y = 1.0 / sum;
+                fast = !A.force_exact && den_fast_all(sum);
                 red[(size_t)op.g * 64] = nv - nobs;
                 break;
             }
-            case JT_L_MUL: {  // parent *= extended child message; Normalize (:829-941)
-                const int32_t *__restrict__ mp = aux + op.e;
-                const double *__restrict__ sp = sep + (size_t)op.d * 64;
-                double sum = 0.0;
-#pragma unroll 4
-                for (int e = 0; e < op.b; ++e) {
-                    const double v = (TT(e) / den) * sp[(size_t)mp[e] * 64];
-                    TT(e) = v;
-                    sum += v;
-                }
-                den = sum;
+            case JT_L_MUL: {
+                const double *sp = sep + (size_t)op.d * 64;
+                if (fast) op_mul<SPILL, false>(T, D, sp, aux + op.e, op.c, op.b);
+                else op_mul<SPILL, true>(T, D, sp, aux + op.e, op.c, op.b);
+                fast = !A.force_exact && den_fast_all(D.den);
                 break;
             }
-            case JT_L_SEPCOL: {  // message to the parent: tmp[k % Ts] += child[k] (:1056-1148)
-                // the separator's old value is its masked all-ones table, and x / 1.0 == x, while
-                // its zero entries face child entries that are themselves masked to zero
-                const int Ts = op.b, Q = op.c / op.b;
-                for (int j = 0; j < Ts; ++j) {
-                    double acc = 0.0;
-#pragma unroll 4
-                    for (int q = 0; q < Q; ++q) acc += TT(q * Ts + j) / den;
-                    SP(op.a + j) = acc;
-                }
+            case JT_L_SEPCOL: {
+                double *sp = sep + (size_t)op.a * 64;
+                if (fast) op_sepcol<SPILL, false>(T, D, sp, op.b, op.c);
+                else op_sepcol<SPILL, true>(T, D, sp, op.b, op.c);
                 break;
             }
             case JT_L_STORE: {
                 double *__restrict__ st = store + (size_t)op.a * 64;
 #pragma unroll 8
-                for (int e = 0; e < op.b; ++e) st[(size_t)e * 64] = TT(e);
-                dens[(size_t)op.c * 64] = den;
+                for (int e = 0; e < op.b; ++e) st[(size_t)e * 64] = T[e];
+                dens[(size_t)op.c * 64] = D.den;
                 break;
             }
             case JT_L_LOAD: {
                 const double *__restrict__ st = store + (size_t)op.a * 64;
 #pragma unroll 8
-                for (int e = 0; e < op.b; ++e) TT(e) = st[(size_t)e * 64];
-                den = dens[(size_t)op.c * 64];
+                for (int e = 0; e < op.b; ++e) T[e] = st[(size_t)e * 64];
+                D.den = dens[(size_t)op.c * 64];
+                D.y = 1.0 / D.den;
+                fast = !A.force_exact && den_fast_all(D.den);
                 break;
             }
-            case JT_L_DMUL: {  // child *= parent message (k % Ts); Normalize (:1150-1238)
-                const double *__restrict__ sp = sep + (size_t)op.d * 64;
-                const int Ts = op.e, Q = op.b / op.e;
-                double sum = 0.0;
-                for (int q = 0; q < Q; ++q) {
-#pragma unroll 4
-                    for (int j = 0; j < Ts; ++j) {
-                        const int e = q * Ts + j;
-                        const double v = (TT(e) / den) * sp[(size_t)j * 64];
-                        TT(e) = v;
-                        sum += v;
-                    }
-                }
-                den = sum;
+            case JT_L_DMUL: {
+                const double *sp = sep + (size_t)op.d * 64;
+                if (fast) op_dmul<SPILL, false>(T, D, sp, op.e, op.b);
+                else op_dmul<SPILL, true>(T, D, sp, op.e, op.b);
+                fast = !A.force_exact && den_fast_all(D.den);
                 break;
             }
-            case JT_L_SEPDIS: {  // tmp[map(k)] += parent[k]; sep = tmp / old, zero-guarded (:700-816)
-                const int32_t *__restrict__ ls = aux + op.e;
-                const int per = op.f;
-                for (int j = 0; j < op.b; ++j) {
-                    double acc = 0.0;
-#pragma unroll 4
-                    for (int q = 0; q < per; ++q) acc += TT(ls[j * per + q]) / den;
-                    const double old = SP(op.a + j);
-                    SP(op.a + j) = (old == 0.0) ? 0.0 : acc / old;
-                }
+            case JT_L_SEPDIS: {
+                double *sp = sep + (size_t)op.a * 64;
+                if (fast) op_sepdis<SPILL, false>(T, D, sp, aux + op.e, op.b, op.f);
+                else op_sepdis<SPILL, true>(T, D, sp, aux + op.e, op.b, op.f);
                 break;
             }
             case JT_L_MARG: {  // GetProbabilitiesOneNode / InferenceUsingJT (:1339-1454)
@@ -351,28 +443,21 @@ __global__ __launch_bounds__(64) void jt_lds_kernel(JtLArgs A) {
                     if (r < best) best = r, sel = cd[k];
                 }
                 if (sel != op.g) break;
-                const int dim = op.b, cum = op.h, bw = dim * cum, nhi = op.pad / bw;
                 double *__restrict__ o = out + op.a;
-                double tot = 0.0;
-                for (int d = 0; d < dim; ++d) {
-                    double acc = 0.0;
-                    for (int hi = 0; hi < nhi; ++hi)
-#pragma unroll 4
-                        for (int lo = 0; lo < cum; ++lo) acc += TT(hi * bw + d * cum + lo) / den;
-                    if (act) o[d] = acc;
-                    tot += acc;
-                }
+                double tot;
+                if (fast) op_marg<SPILL, false>(T, D, o, act, op.b, op.h, op.pad, tot);
+                else op_marg<SPILL, true>(T, D, o, act, op.b, op.h, op.pad, tot);
                 if (act) {
                     if (op.f) {  // label: ArgMax, strict '>' from 0 (src/Inference.cpp:92-102)
                         int lab = 0;
                         double mp = 0.0;
-                        for (int d = 0; d < dim; ++d) {
+                        for (int d = 0; d < op.b; ++d) {
                             const double v = (best == 1) ? o[d] : o[d] / tot;
                             if (v > mp) mp = v, lab = d;
                         }
-                        A.labels[cs] = lab;
+                        labels[cs] = lab;
                     }
-                    for (int d = 0; d < dim; ++d) o[d] = o[d] / tot;
+                    for (int d = 0; d < op.b; ++d) o[d] = o[d] / tot;
                 }
                 break;
             }
@@ -384,10 +469,17 @@ __global__ __launch_bounds__(64) void jt_lds_kernel(JtLArgs A) {
             default:
                 break;
             }
+            if (PROF) {
+                __builtin_amdgcn_s_waitcnt(0);
+                const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+#pragma unroll
+                for (int k = 0; k < 10; ++k)
+                    if (op.type == 11 + k) pc[k] += t1 - t0;
+            }
         }
     }
-#undef TT
-#undef SP
+    if (PROF && lane == 0)
+        for (int k = 0; k < 10; ++k) prof[(size_t)blockIdx.x * 16 + k] = pc[k];
 }
 
 }  // namespace
@@ -396,18 +488,10 @@ extern "C" hipError_t fbn_jt_lds_launch(const JtOp *ops, int nops, const int32_t
                                         const uint64_t *dig, const int8_t *evid, int V, long long ncases, int SD,
                                         double *marg, int32_t *labels, double *ws, int32_t *wsi, long long wave_entries,
                                         long long store_off, long long den_off, long long sep_off,
-                                        long long spill_off, int nc, int cap, bool spill, int grid,
-                                        hipStream_t stream) {
-    JtLArgs a;
-    a.ops = ops;
-    a.aux = aux;
-    a.initv = initv;
-    a.dig = dig;
-    a.evid = evid;
-    a.marg = marg;
-    a.labels = labels;
-    a.ws = ws;
-    a.wsi = wsi;
+                                        long long spill_off, int nc, int cap, bool spill, int force_exact,
+                                        int grid, unsigned long long *prof, hipStream_t stream) {
+    JtLParams a;
+    a.force_exact = force_exact;
     a.ncases = ncases;
     a.wave_entries = wave_entries;
     a.store_off = store_off;
@@ -420,10 +504,20 @@ extern "C" hipError_t fbn_jt_lds_launch(const JtOp *ops, int nops, const int32_t
     a.nc = nc;
     a.cap = cap;
     const size_t lds = (size_t)cap * 64 * sizeof(double);
-    if (spill)
-        hipLaunchKernelGGL(jt_lds_kernel<true>, dim3(grid), dim3(64), lds, stream, a);
-    else
-        hipLaunchKernelGGL(jt_lds_kernel<false>, dim3(grid), dim3(64), lds, stream, a);
+    if (prof) {
+        if (spill)
+            hipLaunchKernelGGL((jt_lds_kernel<true, true>), dim3(grid), dim3(64), lds, stream, ops, aux, initv, dig,
+                               evid, marg, labels, ws, wsi, a, prof);
+        else
+            hipLaunchKernelGGL((jt_lds_kernel<false, true>), dim3(grid), dim3(64), lds, stream, ops, aux, initv, dig,
+                               evid, marg, labels, ws, wsi, a, prof);
+    } else if (spill) {
+        hipLaunchKernelGGL((jt_lds_kernel<true, false>), dim3(grid), dim3(64), lds, stream, ops, aux, initv, dig,
+                           evid, marg, labels, ws, wsi, a, nullptr);
+    } else {
+        hipLaunchKernelGGL((jt_lds_kernel<false, false>), dim3(grid), dim3(64), lds, stream, ops, aux, initv, dig,
+                           evid, marg, labels, ws, wsi, a, nullptr);
+    }
     return hipGetLastError();
 }
 

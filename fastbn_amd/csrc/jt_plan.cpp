@@ -499,9 +499,15 @@ int CompileJTProgramLDS(const JTPlanHost &plan, JTProgramLDS &prog) {
             int rc = emit_init(c);
             if (rc) return rc;
             for (int s : plan.clique_down[c]) {
-                int64_t map_off = (int64_t)prog.aux.size();
-                for (int64_t e = 0; e < t.size(); ++e) prog.aux.push_back((int32_t)sub_index(t, plan.seps[s], e));
-                op(JT_L_MUL, 0, t.size(), 0, sep_off[s], map_off);
+                const int64_t Ts = plan.seps[s].size(), per = t.size() / Ts;
+                std::vector<std::vector<int32_t>> lists(Ts);
+                for (int64_t e = 0; e < t.size(); ++e) lists[sub_index(t, plan.seps[s], e)].push_back((int32_t)e);
+                int64_t list_off = (int64_t)prog.aux.size();
+                for (auto &l : lists) {
+                    if ((int64_t)l.size() != per) return SetError(FBN_ERR_ARG, "internal: ragged separator map");
+                    prog.aux.insert(prog.aux.end(), l.begin(), l.end());
+                }
+                op(JT_L_MUL, 0, t.size(), Ts, sep_off[s], list_off);
             }
             if (c != plan.root) {
                 int s = plan.clique_up[c];

@@ -43,7 +43,7 @@ enum JtOpType : int32_t {
 // parents in Collect and parents before children in Distribute (the reference's level order).
 enum JtLOpType : int32_t {
     JT_L_INIT = 11,    // b=T, c=aux off of var list, d=nv, e=dig word off, g=clique id, h=initv off
-    JT_L_MUL = 12,     // b=T, d=sep store off, e=aux off of map[T]          (CliqueLevelCollection)
+    JT_L_MUL = 12,     // b=T, c=Ts, d=sep store off, e=aux off of lists[Ts][T/Ts] (CliqueLevelCollection)
     JT_L_SEPCOL = 13,  // a=sep store off, b=Ts, c=T                          (SeparatorLevelCollection)
     JT_L_STORE = 14,   // a=store off, b=T, c=clique id (den slot)
     JT_L_LOAD = 15,    // a=store off, b=T, c=clique id

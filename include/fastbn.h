@@ -106,8 +106,12 @@ int fbn_jt_score(const fbn_jt_plan *p, const double *marginals, const double *go
 int fbn_jt_last_kernel_ms(const fbn_jt_plan *p, float *ms);
 /* Tuning: persistent waves per CU (0 = default: as many as keep the largest clique in LDS). */
 int fbn_jt_set_waves_per_cu(fbn_jt_plan *p, int waves);
-/* Kernel variant: 0 = clique-in-LDS (default), 1 = whole case state in a global workspace. */
+/* Kernel variant: 0 = clique-in-LDS (default), 1 = whole case state in a global workspace,
+ * 2 = variant 0 with the IEEE division sequence forced (ablation / testing). */
 int fbn_jt_set_variant(fbn_jt_plan *p, int variant);
+/* Diagnostics (LDS variant): enable per-op-type s_memtime accounting for subsequent runs and/or
+ * read the totals of the last run (cycles[10], op types JT_L_INIT..JT_L_EVZERO, summed over waves). */
+int fbn_jt_debug_op_cycles(fbn_jt_plan *p, int enable, unsigned long long *cycles);
 int fbn_jt_plan_destroy(fbn_jt_plan *p);
 
 /* ------------------------------------------------------------------ CI tests (G^2) */

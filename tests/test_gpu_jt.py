@@ -77,7 +77,7 @@ def test_large_batch_vs_oracle_and_waves(jt, ojt):
     np.testing.assert_array_equal(lab, olab)
     np.testing.assert_array_equal(marg, omarg)
     # both kernel variants; LDS variant with and without spilled rows (w=4 -> 80 LDS rows < 144)
-    for variant, waves in ((0, 1), (0, 2), (0, 4), (0, 8), (1, 2), (1, 8)):
+    for variant, waves in ((0, 1), (0, 2), (0, 4), (0, 8), (1, 2), (1, 8), (2, 2), (2, 4)):
         jt.set_variant(variant)
         jt.set_waves_per_cu(waves)
         lab2, marg2 = jt.infer(ev)
@@ -95,7 +95,7 @@ def test_synthetic_network(tmp_path):
     ev = synth.evidence_cases(net, 300, 40, seed=5)
     jt = F.JunctionTree(F.Network(p), device=0)
     olab, omarg = O.OracleJT(p).infer(ev)
-    for variant in (0, 1):
+    for variant in (0, 1, 2):
         jt.set_variant(variant)
         lab, marg = jt.infer(ev)
         np.testing.assert_array_equal(lab, olab)

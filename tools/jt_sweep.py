@@ -15,7 +15,7 @@ xml = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "tests", "golden"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 100000
 k = int(sys.argv[3]) if len(sys.argv) > 3 else 7
 configs = [tuple(int(y) for y in x.split(":")) for x in
-           (sys.argv[4] if len(sys.argv) > 4 else "0:1,0:2,0:3,0:4,0:6,0:8,1:8").split(",")]  # variant:waves
+           (sys.argv[4] if len(sys.argv) > 4 else "0:1,0:2,0:3,0:4,0:6,0:8,2:2,1:8").split(",")]  # variant:waves
 net = synth.read_xmlbif(xml)
 ev = synth.evidence_cases(net, n, k, seed=1)
 jt = F.JunctionTree(F.Network(xml), device=0)
