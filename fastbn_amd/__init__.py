@@ -23,7 +23,8 @@ from .api import (  # noqa: F401
     lib,
     load_libsvm,
     device_count,
+    kernel_options,
 )
 
 __all__ = ["FastBNError", "Network", "Dataset", "JunctionTree", "IndependenceTest", "PCStable",
-           "lib", "load_libsvm", "device_count"]
+           "lib", "load_libsvm", "device_count", "kernel_options"]

@@ -36,6 +36,11 @@ _SIGS = {
     "fbn_jt_set_waves_per_cu": [_vp, C.c_int],
     "fbn_jt_set_variant": [_vp, C.c_int],
     "fbn_jt_debug_op_cycles": [_vp, C.c_int, _vp],
+    "fbn_jt_kernel_source": [_vp, C.c_char_p, C.c_int64, _vp],
+    "fbn_jt_kernel_cache_path": [_vp, C.c_char_p, C.c_int64],
+    "fbn_jt_kernel_options": [C.c_char_p, C.c_int64],
+    "fbn_jt_kernel_build": [_vp],
+    "fbn_jt_debug_force_fixup": [_vp, C.c_int],
     "fbn_jt_plan_destroy": [_vp],
     "fbn_ci_dataset_upload": [_vp, C.c_int, _i64, _vp, C.c_int, _pp],
     "fbn_ci_run": [_vp, _vp, _i64, C.c_int, _dbl, _vp, _vp, _vp, _vp, _vp],
@@ -117,7 +122,8 @@ class _PlanInfo(C.Structure):
                 ("num_levels", C.c_int32), ("root", C.c_int32), ("sum_dom", C.c_int32),
                 ("clique_entries", C.c_int64), ("separator_entries", C.c_int64),
                 ("algorithmic_bytes_per_case", C.c_int64), ("num_ops", C.c_int32),
-                ("max_vars_per_table", C.c_int32)]
+                ("max_vars_per_table", C.c_int32), ("specialized_eligible", C.c_int32),
+                ("variant", C.c_int32)]
 
 
 class Network:
@@ -142,6 +148,13 @@ class Network:
         if getattr(self, "_h", None):
             lib.fbn_network_destroy(self._h)
             self._h = None
+
+
+def kernel_options():
+    """Compile options of the plan-specialized JT kernel (list of str)."""
+    buf = C.create_string_buffer(1024)
+    lib.fbn_jt_kernel_options(buf, 1024)
+    return [x for x in buf.value.decode().split("\n") if x]
 
 
 def load_libsvm(path, num_nodes):
@@ -212,8 +225,36 @@ class JunctionTree:
         names = ["INIT", "MUL", "SEPCOL", "STORE", "LOAD", "DMUL", "SEPDIS", "MARG", "EVZERO", "-"]
         return dict(zip(names, buf.tolist()))
 
+    def kernel_source(self):
+        """Source of the plan-specialized kernel (variant 3)."""
+        n = C.c_int64()
+        lib.fbn_jt_kernel_source(self._h, None, 0, C.byref(n))
+        buf = C.create_string_buffer(n.value)
+        lib.fbn_jt_kernel_source(self._h, buf, n.value, C.byref(n))
+        return buf.value.decode()
+
+    def kernel_cache_path(self):
+        buf = C.create_string_buffer(4096)
+        lib.fbn_jt_kernel_cache_path(self._h, buf, 4096)
+        return buf.value.decode()
+
+    def debug_force_fixup(self, enable):
+        lib.fbn_jt_debug_force_fixup(self._h, int(enable))
+
+    def build_kernel(self):
+        """Compile the plan-specialized kernel into the on-disk cache (no GPU needed)."""
+        lib.fbn_jt_kernel_build(self._h)
+        return self.kernel_cache_path()
+
+    def refresh_info(self):
+        info = _PlanInfo()
+        lib.fbn_jt_plan_info_get(self._h, C.byref(info))
+        self.info = {k: getattr(info, k) for k, _ in _PlanInfo._fields_}
+        return self.info
+
     def set_variant(self, v):
-        """0 = clique-in-LDS kernel (default), 1 = global-workspace kernel."""
+        """-1 auto, 0 = clique-in-LDS interpreter, 1 = global-workspace interpreter,
+        2 = LDS interpreter with IEEE division, 3 = plan-specialized kernel."""
         lib.fbn_jt_set_variant(self._h, v)
 
     def infer(self, evidence, marginals=True):

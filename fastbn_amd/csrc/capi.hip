@@ -26,10 +26,14 @@ extern "C" hipError_t fbn_jt_lds_launch(const JtOp *ops, int nops, const int32_t
                                         double *marg, int32_t *labels, double *ws, int32_t *wsi, long long wave_entries,
                                         long long store_off, long long den_off, long long sep_off,
                                         long long spill_off, int nc, int cap, bool spill, int force_exact,
-                                        int grid, unsigned long long *prof, hipStream_t stream);
+                                        const int *flags, int grid, unsigned long long *prof, hipStream_t stream);
 
 namespace fbn {
 const char *LastError();
+extern const char *kJitOptions[];
+extern const int kJitNumOptions;
+std::string JitCachePath(const std::string &src);
+int JitCodeObject(const std::string &src, std::vector<char> &code);
 }
 using fbn::SetError;
 
@@ -92,7 +96,15 @@ struct fbn_jt_plan {
     fbn::JTPlanHost host;
     fbn::JTProgram prog;      // variant 1: whole case state in a global workspace
     fbn::JTProgramLDS lprog;  // variant 0 (default): clique in flight resident in LDS
-    int device = 0, num_cu = 0, waves_per_cu = 0, variant = 0;
+    int device = 0, num_cu = 0, waves_per_cu = 0, variant = -1;
+    // plan-specialized kernel (variant 3)
+    bool gen_eligible = false;
+    int gen_state = 0;  // 0 not tried, 1 loaded, -1 failed
+    hipModule_t gen_mod = nullptr;
+    hipFunction_t gen_fn = nullptr;
+    int64_t gen_we = 0;
+    DevBuf flags, ws_fix;
+    bool force_fixup = false;
     DevBuf ops, aux, initv, dig;
     DevBuf lops, laux, linitv, ldig;
     DevBuf prof;       // diagnostic per-op-type cycle counters
@@ -102,6 +114,7 @@ struct fbn_jt_plan {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     ~fbn_jt_plan() {
+        if (gen_mod) (void)hipModuleUnload(gen_mod);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
     }
@@ -255,6 +268,7 @@ int fbn_jt_plan_create(const fbn_network *net, int device, fbn_jt_plan **out) {
     if (rc) return rc;
     rc = fbn::CompileJTProgramLDS(p->host, p->lprog);
     if (rc) return rc;
+    p->gen_eligible = fbn::JTCodegenEligible(p->host, nullptr);
     p->device = device;
     if (device >= 0) {  // device < 0: host-only plan (info / dump), runs fail with FBN_ERR_NODEV
         rc = CheckDevice(device, &p->num_cu);
@@ -283,6 +297,8 @@ int fbn_jt_plan_info_get(const fbn_jt_plan *p, fbn_jt_plan_info *info) {
         16 * (info->clique_entries + info->separator_entries) + 8 * (int64_t)info->sum_dom + info->num_nodes;
     info->num_ops = (int32_t)p->prog.ops.size();
     info->max_vars_per_table = p->prog.max_vars;
+    info->specialized_eligible = p->gen_eligible ? 1 : 0;
+    info->variant = p->variant >= 0 ? p->variant : (p->gen_state == 1 ? 3 : p->gen_state == -1 ? 0 : -1);
     return FBN_OK;
 }
 
@@ -333,8 +349,26 @@ int fbn_jt_set_waves_per_cu(fbn_jt_plan *p, int waves) {
 }
 
 int fbn_jt_set_variant(fbn_jt_plan *p, int variant) {
-    if (!p || variant < 0 || variant > 2) return SetError(FBN_ERR_ARG, "variant must be 0 (LDS), 1 (global) or 2 (LDS, IEEE division)");
+    if (!p || variant < -1 || variant > 3)
+        return SetError(FBN_ERR_ARG, "variant must be -1 (auto), 0 (LDS), 1 (global), 2 (LDS, IEEE division) or 3 (specialized)");
+    if (variant == 3 && !p->gen_eligible) return SetError(FBN_ERR_ARG, "plan not eligible for the specialized kernel");
     p->variant = variant;
+    return FBN_OK;
+}
+
+// load (cache) or compile (hiprtc) the plan-specialized kernel once per plan
+static int GenEnsure(fbn_jt_plan *p) {
+    if (p->gen_state == 1) return FBN_OK;
+    if (p->gen_state == -1) return FBN_ERR_HIP;
+    p->gen_state = -1;
+    std::string src;
+    int rc = fbn::GenerateJTKernel(p->host, src, &p->gen_we);
+    if (rc) return rc;
+    std::vector<char> code;
+    if ((rc = fbn::JitCodeObject(src, code))) return rc;
+    FBN_HIP(hipModuleLoadData(&p->gen_mod, code.data()));
+    FBN_HIP(hipModuleGetFunction(&p->gen_fn, p->gen_mod, "fbn_jt_gen"));
+    p->gen_state = 1;
     return FBN_OK;
 }
 
@@ -354,6 +388,58 @@ int fbn_jt_debug_op_cycles(fbn_jt_plan *p, int enable, unsigned long long *cycle
     return FBN_OK;
 }
 
+int fbn_jt_kernel_source(const fbn_jt_plan *p, char *buf, int64_t cap, int64_t *len) {
+    if (!p) return SetError(FBN_ERR_ARG, "null pointer");
+    if (!p->gen_eligible) return SetError(FBN_ERR_ARG, "plan not eligible for codegen");
+    std::string src;
+    int64_t we = 0;
+    int rc = fbn::GenerateJTKernel(p->host, src, &we);
+    if (rc) return rc;
+    if (len) *len = (int64_t)src.size() + 1;
+    if (buf && cap > 0) {
+        const size_t n = std::min<size_t>((size_t)cap - 1, src.size());
+        memcpy(buf, src.data(), n);
+        buf[n] = 0;
+    }
+    return FBN_OK;
+}
+
+int fbn_jt_kernel_cache_path(const fbn_jt_plan *p, char *buf, int64_t cap) {
+    if (!p || !buf || cap <= 0) return SetError(FBN_ERR_ARG, "bad argument");
+    if (!p->gen_eligible) return SetError(FBN_ERR_ARG, "plan not eligible for codegen");
+    std::string src;
+    int64_t we = 0;
+    int rc = fbn::GenerateJTKernel(p->host, src, &we);
+    if (rc) return rc;
+    snprintf(buf, (size_t)cap, "%s", fbn::JitCachePath(src).c_str());
+    return FBN_OK;
+}
+
+int fbn_jt_debug_force_fixup(fbn_jt_plan *p, int enable) {
+    if (!p) return SetError(FBN_ERR_ARG, "null pointer");
+    p->force_fixup = enable != 0;
+    return FBN_OK;
+}
+
+int fbn_jt_kernel_build(const fbn_jt_plan *p) {
+    if (!p) return SetError(FBN_ERR_ARG, "null pointer");
+    if (!p->gen_eligible) return SetError(FBN_ERR_ARG, "plan not eligible for codegen");
+    std::string src;
+    int64_t we = 0;
+    int rc = fbn::GenerateJTKernel(p->host, src, &we);
+    if (rc) return rc;
+    std::vector<char> code;
+    return fbn::JitCodeObject(src, code);
+}
+
+int fbn_jt_kernel_options(char *buf, int64_t cap) {
+    if (!buf || cap <= 0) return SetError(FBN_ERR_ARG, "bad argument");
+    std::string o;
+    for (int i = 0; i < fbn::kJitNumOptions; ++i) o += std::string(fbn::kJitOptions[i]) + "\n";
+    snprintf(buf, (size_t)cap, "%s", o.c_str());
+    return FBN_OK;
+}
+
 static const size_t kLdsBytes = 160 * 1024;
 
 // LDS variant geometry: waves per CU and the number of LDS table rows (64 lanes x 8 B each)
@@ -364,6 +450,36 @@ static void LdsGeometry(const fbn_jt_plan *p, int *waves, int *cap) {
     int64_t c = std::min<int64_t>(tmax, (int64_t)(kLdsBytes / w) / row);
     *waves = w;
     *cap = (int)std::max<int64_t>(1, c);
+}
+
+// LDS interpreter launch (variants 0/2, and the exact fixup of variant 3 when flags != NULL)
+static int LaunchLds(fbn_jt_plan *p, DevBuf &ws, const int8_t *d_evidence, int64_t ncases, int32_t *labels,
+                     double *marg, const int *flags, bool force_exact, hipStream_t s) {
+    const auto &l = p->lprog;
+    const int V = p->host.num_nodes, SD = l.sum_dom, nc = l.num_cliques;
+    const int64_t nblk = (ncases + 63) / 64;
+    int wpc, cap, rc;
+    LdsGeometry(p, &wpc, &cap);
+    const bool spill = cap < l.max_table;
+    const int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * wpc);
+    const int64_t store_off = 0, den_off = l.store_entries, sep_off = den_off + nc, spill_off = sep_off + l.sep_entries;
+    const int64_t wave_entries = spill_off + (spill ? l.max_table - cap : 0);
+    const size_t ws_d = (size_t)grid * wave_entries * 64 * 8;
+    const size_t ws_i = (size_t)grid * nc * 64 * 4;
+    if ((rc = ws.ensure(ws_d + ws_i))) return rc;
+    const bool prof = p->prof_on && !flags;
+    if (prof) {
+        if ((rc = p->prof.ensure((size_t)grid * 16 * 8))) return rc;
+        FBN_HIP(hipMemsetAsync(p->prof.p, 0, (size_t)grid * 16 * 8, s));
+        p->last_grid = grid;
+    }
+    hipError_t e = fbn_jt_lds_launch(p->lops.as<JtOp>(), (int)l.ops.size(), p->laux.as<int32_t>(),
+                                     p->linitv.as<double>(), p->ldig.as<uint64_t>(), d_evidence, V, ncases, SD, marg,
+                                     labels, ws.as<double>(), reinterpret_cast<int32_t *>(ws.as<char>() + ws_d),
+                                     wave_entries, store_off, den_off, sep_off, spill_off, nc, cap, spill, force_exact,
+                                     flags, grid, prof ? p->prof.as<unsigned long long>() : nullptr, s);
+    if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt kernel launch: %s", hipGetErrorString(e));
+    return FBN_OK;
 }
 
 int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, int32_t *d_labels,
@@ -387,42 +503,43 @@ int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, 
         if ((rc = p->labels.ensure((size_t)ncases * 4))) return rc;
         labels = p->labels.as<int32_t>();
     }
-    hipError_t e;
-    if (p->variant == 1) {
+    int variant = p->variant;
+    if (variant == -1) variant = (p->gen_eligible && GenEnsure(p) == FBN_OK) ? 3 : 0;
+    else if (variant == 3 && (rc = GenEnsure(p))) return rc;
+
+    if (variant == 1) {
         const int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 8;
         const int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * wpc);
         const size_t ws_d = (size_t)grid * g.state_entries * 64 * 8;
         const size_t ws_i = (size_t)grid * nc * 64 * 4;
         if ((rc = p->ws.ensure(ws_d + ws_i))) return rc;
         FBN_HIP(hipEventRecord(p->ev0, s));
-        e = fbn_jt_launch(p->ops.as<JtOp>(), (int)g.ops.size(), p->aux.as<int32_t>(), p->initv.as<double>(),
-                          p->dig.as<uint64_t>(), d_evidence, V, ncases, SD, marg, labels, p->ws.as<double>(),
-                          reinterpret_cast<int32_t *>(p->ws.as<char>() + ws_d), g.state_entries, nc, grid, s);
-    } else {
-        const auto &l = p->lprog;
-        int wpc, cap;
-        LdsGeometry(p, &wpc, &cap);
-        const bool spill = cap < l.max_table;
+        hipError_t e = fbn_jt_launch(p->ops.as<JtOp>(), (int)g.ops.size(), p->aux.as<int32_t>(), p->initv.as<double>(),
+                                     p->dig.as<uint64_t>(), d_evidence, V, ncases, SD, marg, labels,
+                                     p->ws.as<double>(), reinterpret_cast<int32_t *>(p->ws.as<char>() + ws_d),
+                                     g.state_entries, nc, grid, s);
+        if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt kernel launch: %s", hipGetErrorString(e));
+    } else if (variant == 3) {
+        // one wave (64 cases) per SIMD: the clique in flight occupies the register file
+        const int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 4;
         const int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * wpc);
-        const int64_t store_off = 0, den_off = l.store_entries, sep_off = den_off + nc,
-                      spill_off = sep_off + l.sep_entries;
-        const int64_t wave_entries = spill_off + (spill ? l.max_table - cap : 0);
-        const size_t ws_d = (size_t)grid * wave_entries * 64 * 8;
-        const size_t ws_i = (size_t)grid * nc * 64 * 4;
-        if ((rc = p->ws.ensure(ws_d + ws_i))) return rc;
-        if (p->prof_on) {
-            if ((rc = p->prof.ensure((size_t)grid * 16 * 8))) return rc;
-            FBN_HIP(hipMemsetAsync(p->prof.p, 0, (size_t)grid * 16 * 8, s));
-        }
-        p->last_grid = grid;
+        if ((rc = p->ws.ensure((size_t)grid * p->gen_we * 64 * 8))) return rc;
+        if ((rc = p->flags.ensure((size_t)nblk * 4))) return rc;
         FBN_HIP(hipEventRecord(p->ev0, s));
-        e = fbn_jt_lds_launch(p->lops.as<JtOp>(), (int)l.ops.size(), p->laux.as<int32_t>(), p->linitv.as<double>(),
-                              p->ldig.as<uint64_t>(), d_evidence, V, ncases, SD, marg, labels, p->ws.as<double>(),
-                              reinterpret_cast<int32_t *>(p->ws.as<char>() + ws_d), wave_entries, store_off, den_off,
-                              sep_off, spill_off, nc, cap, spill, p->variant == 2, grid,
-                              p->prof_on ? p->prof.as<unsigned long long>() : nullptr, s);
+        FBN_HIP(hipMemsetAsync(p->flags.p, p->force_fixup ? 1 : 0, (size_t)nblk * 4, s));
+        const int8_t *a_ev = d_evidence;
+        double *a_marg = marg, *a_ws = p->ws.as<double>();
+        int32_t *a_lab = labels;
+        int *a_flags = p->flags.as<int>();
+        long long a_n = ncases;
+        void *args[] = {&a_ev, &a_marg, &a_lab, &a_ws, &a_flags, &a_n};
+        FBN_HIP(hipModuleLaunchKernel(p->gen_fn, grid, 1, 1, 64, 1, 1, 0, s, args, nullptr));
+        // exact recomputation of the blocks whose denominators left the fast-division range
+        if ((rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s))) return rc;
+    } else {
+        FBN_HIP(hipEventRecord(p->ev0, s));
+        if ((rc = LaunchLds(p, p->ws, d_evidence, ncases, labels, marg, nullptr, variant == 2, s))) return rc;
     }
-    if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt kernel launch: %s", hipGetErrorString(e));
     FBN_HIP(hipEventRecord(p->ev1, s));
     p->timed = true;
     return FBN_OK;

@@ -88,6 +88,11 @@ struct JTProgramLDS {
 };
 int CompileJTProgramLDS(const JTPlanHost &plan, JTProgramLDS &prog);
 
+// plan-specialized kernel source (jt_codegen.cpp): eligibility and generation.  The generated
+// kernel's per-wave workspace holds wave_entries rows of 64 fp64 lanes.
+bool JTCodegenEligible(const JTPlanHost &plan, int64_t *entry_ops);
+int GenerateJTKernel(const JTPlanHost &plan, std::string &src, int64_t *wave_entries);
+
 }  // namespace fbn
 
 #endif

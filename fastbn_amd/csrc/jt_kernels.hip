@@ -204,6 +204,7 @@ struct JtLParams {
     long long store_off, den_off, sep_off, spill_off;
     int nops, V, SD, nc, cap;
     int force_exact;  // ablation/testing: always take the IEEE division path
+    const int *flags;  // fixup mode (non-null): only the blocks the specialized kernel flagged
 };
 
 // Pointers are separate __restrict__ kernel arguments (not a struct): the compiler can then prove
@@ -344,6 +345,7 @@ __global__ __launch_bounds__(64) void jt_lds_kernel(const JtOp *__restrict__ ops
     const Tab<SPILL> T{lds + lane, W + (size_t)A.spill_off * 64, A.cap};
 
     for (long long blk = blockIdx.x; blk * 64 < A.ncases; blk += gridDim.x) {
+        if (A.flags && A.flags[blk] == 0) continue;
         const long long cs = blk * 64 + lane;
         const bool act = cs < A.ncases;
         const long long csr = act ? cs : A.ncases - 1;
@@ -489,9 +491,10 @@ extern "C" hipError_t fbn_jt_lds_launch(const JtOp *ops, int nops, const int32_t
                                         double *marg, int32_t *labels, double *ws, int32_t *wsi, long long wave_entries,
                                         long long store_off, long long den_off, long long sep_off,
                                         long long spill_off, int nc, int cap, bool spill, int force_exact,
-                                        int grid, unsigned long long *prof, hipStream_t stream) {
+                                        const int *flags, int grid, unsigned long long *prof, hipStream_t stream) {
     JtLParams a;
     a.force_exact = force_exact;
+    a.flags = flags;
     a.ncases = ncases;
     a.wave_entries = wave_entries;
     a.store_off = store_off;

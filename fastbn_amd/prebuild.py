@@ -1,0 +1,35 @@
+"""Prebuild plan-specialized JT kernels into the in-tree code-object cache (fastbn_amd/kcache).
+
+The cache key is a hash of the generated source and the compile options, so a kernel built here
+is found by any process that plans the same network (jt_jit.hip); a miss compiles with hiprtc at
+first run instead.
+"""
+import os
+import tempfile
+
+from . import api, synth
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ALARM_XML = os.path.join(REPO, "tests", "golden", "alarm", "alarm.xml")
+# eligible synthetic network used by the GPU parity tests (tests/test_gpu_jt.py)
+SYNTH_SMALL = dict(n=60, seed=5, window=6)
+
+
+def synth_small_xml(dirname):
+    path = os.path.join(dirname, "synth60.xml")
+    synth.random_network(SYNTH_SMALL["n"], seed=SYNTH_SMALL["seed"], window=SYNTH_SMALL["window"], path=path)
+    return path
+
+
+def prebuild(xml_paths):
+    out = []
+    for xml in xml_paths:
+        jt = api.JunctionTree(api.Network(xml), device=-1)
+        if jt.info["specialized_eligible"]:
+            out.append(jt.build_kernel())
+    return out
+
+
+def prebuild_default():
+    with tempfile.TemporaryDirectory() as d:
+        return prebuild([ALARM_XML, synth_small_xml(d)])

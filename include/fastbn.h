@@ -78,6 +78,8 @@ typedef struct {
     int64_t algorithmic_bytes_per_case; /* 16*(clique+sep entries) + 8*sum_dom + num_nodes */
     int32_t num_ops;            /* device program length */
     int32_t max_vars_per_table;
+    int32_t specialized_eligible; /* cliques small enough for the plan-specialized kernel */
+    int32_t variant;              /* kernel variant runs use (-1 auto before the first run) */
 } fbn_jt_plan_info;
 
 /* Build the case-independent schedule (JunctionTree ctor, src/JunctionTree.cpp:3-46:
@@ -106,12 +108,27 @@ int fbn_jt_score(const fbn_jt_plan *p, const double *marginals, const double *go
 int fbn_jt_last_kernel_ms(const fbn_jt_plan *p, float *ms);
 /* Tuning: persistent waves per CU (0 = default: as many as keep the largest clique in LDS). */
 int fbn_jt_set_waves_per_cu(fbn_jt_plan *p, int waves);
-/* Kernel variant: 0 = clique-in-LDS (default), 1 = whole case state in a global workspace,
- * 2 = variant 0 with the IEEE division sequence forced (ablation / testing). */
+/* Kernel variant: -1 = auto (default: 3 when eligible and its code object loads, else 0),
+ * 0 = clique-in-LDS interpreter, 1 = whole case state in a global workspace interpreter,
+ * 2 = variant 0 with the IEEE division sequence forced (ablation / testing),
+ * 3 = plan-specialized kernel (jt_codegen.cpp; hiprtc or the on-disk code-object cache) followed
+ *     by an exact-path fixup of the blocks it flags.  Selecting 3 fails if the plan is not eligible. */
 int fbn_jt_set_variant(fbn_jt_plan *p, int variant);
 /* Diagnostics (LDS variant): enable per-op-type s_memtime accounting for subsequent runs and/or
  * read the totals of the last run (cycles[10], op types JT_L_INIT..JT_L_EVZERO, summed over waves). */
 int fbn_jt_debug_op_cycles(fbn_jt_plan *p, int enable, unsigned long long *cycles);
+/* Source of the plan-specialized kernel (variant 3); *len = bytes incl. NUL.  FBN_ERR_ARG if the
+ * plan is not eligible (cliques too large for the register-resident form). */
+int fbn_jt_kernel_source(const fbn_jt_plan *p, char *buf, int64_t cap, int64_t *len);
+/* Testing: variant 3 marks every block for the exact fixup pass (exercises the fixup path). */
+int fbn_jt_debug_force_fixup(fbn_jt_plan *p, int enable);
+/* Path of the specialized kernel's code object in the on-disk cache (whether or not it exists);
+ * a build step may compile fbn_jt_kernel_source() there with the options of fbn_jt_kernel_options. */
+int fbn_jt_kernel_cache_path(const fbn_jt_plan *p, char *buf, int64_t cap);
+/* Compile the specialized kernel into the on-disk cache now (no device needed); FBN_OK if cached. */
+int fbn_jt_kernel_build(const fbn_jt_plan *p);
+/* Compile options of the specialized kernel, '\n'-separated. */
+int fbn_jt_kernel_options(char *buf, int64_t cap);
 int fbn_jt_plan_destroy(fbn_jt_plan *p);
 
 /* ------------------------------------------------------------------ CI tests (G^2) */

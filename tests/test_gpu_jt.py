@@ -77,14 +77,48 @@ def test_large_batch_vs_oracle_and_waves(jt, ojt):
     np.testing.assert_array_equal(lab, olab)
     np.testing.assert_array_equal(marg, omarg)
     # both kernel variants; LDS variant with and without spilled rows (w=4 -> 80 LDS rows < 144)
-    for variant, waves in ((0, 1), (0, 2), (0, 4), (0, 8), (1, 2), (1, 8), (2, 2), (2, 4)):
+    for variant, waves in ((0, 1), (0, 2), (0, 4), (0, 8), (1, 2), (1, 8), (2, 2), (2, 4), (3, 4), (3, 2),
+                           (-1, 0)):
         jt.set_variant(variant)
         jt.set_waves_per_cu(waves)
         lab2, marg2 = jt.infer(ev)
         np.testing.assert_array_equal(lab2, lab)
         np.testing.assert_array_equal(marg2, marg)
-    jt.set_variant(0)
+    jt.set_variant(-1)
     jt.set_waves_per_cu(0)
+
+
+def test_specialized_kernel_selected_and_fixup(jt, ojt):
+    """ALARM is eligible: auto mode runs the plan-specialized kernel (prebuilt code object)."""
+    from fastbn_amd import synth
+    assert jt.info["specialized_eligible"] == 1
+    ev = synth.evidence_cases(synth.read_xmlbif(os.path.join(GOLD, "alarm", "alarm.xml")), 3000, 12, seed=3)
+    jt.set_variant(-1)
+    lab, marg = jt.infer(ev)
+    assert jt.refresh_info()["variant"] == 3
+    olab, omarg = ojt.infer(ev)
+    np.testing.assert_array_equal(lab, olab)
+    np.testing.assert_array_equal(marg, omarg)
+    jt.debug_force_fixup(True)  # every block recomputed by the exact interpreter pass
+    lab2, marg2 = jt.infer(ev)
+    jt.debug_force_fixup(False)
+    np.testing.assert_array_equal(lab2, olab)
+    np.testing.assert_array_equal(marg2, omarg)
+
+
+def test_specialized_synthetic(tmp_path):
+    from fastbn_amd import prebuild, synth
+    p = prebuild.synth_small_xml(str(tmp_path))
+    net = synth.read_xmlbif(p)
+    ev = synth.evidence_cases(net, 777, 15, seed=8)
+    jt = F.JunctionTree(F.Network(p), device=0)
+    assert jt.info["specialized_eligible"] == 1
+    olab, omarg = O.OracleJT(p).infer(ev)
+    for variant in (3, 0):
+        jt.set_variant(variant)
+        lab, marg = jt.infer(ev)
+        np.testing.assert_array_equal(lab, olab)
+        np.testing.assert_array_equal(marg, omarg)
 
 
 def test_synthetic_network(tmp_path):
