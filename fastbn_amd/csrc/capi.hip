@@ -103,7 +103,7 @@ struct fbn_jt_plan {
     hipModule_t gen_mod = nullptr;
     hipFunction_t gen_fn = nullptr;
     int64_t gen_we = 0;
-    DevBuf flags, ws_fix;
+    DevBuf flags, ws_fix, gen_iv;
     bool force_fixup = false;
     DevBuf ops, aux, initv, dig;
     DevBuf lops, laux, linitv, ldig;
@@ -362,12 +362,15 @@ static int GenEnsure(fbn_jt_plan *p) {
     if (p->gen_state == -1) return FBN_ERR_HIP;
     p->gen_state = -1;
     std::string src;
-    int rc = fbn::GenerateJTKernel(p->host, src, &p->gen_we);
+    std::vector<double> iv;
+    int rc = fbn::GenerateJTKernel(p->host, src, &p->gen_we, iv);
     if (rc) return rc;
     std::vector<char> code;
     if ((rc = fbn::JitCodeObject(src, code))) return rc;
     FBN_HIP(hipModuleLoadData(&p->gen_mod, code.data()));
     FBN_HIP(hipModuleGetFunction(&p->gen_fn, p->gen_mod, "fbn_jt_gen"));
+    if ((rc = p->gen_iv.ensure(std::max<size_t>(iv.size() * 8, 8)))) return rc;
+    FBN_HIP(hipMemcpy(p->gen_iv.p, iv.data(), iv.size() * 8, hipMemcpyHostToDevice));
     p->gen_state = 1;
     return FBN_OK;
 }
@@ -392,8 +395,9 @@ int fbn_jt_kernel_source(const fbn_jt_plan *p, char *buf, int64_t cap, int64_t *
     if (!p) return SetError(FBN_ERR_ARG, "null pointer");
     if (!p->gen_eligible) return SetError(FBN_ERR_ARG, "plan not eligible for codegen");
     std::string src;
+    std::vector<double> iv;
     int64_t we = 0;
-    int rc = fbn::GenerateJTKernel(p->host, src, &we);
+    int rc = fbn::GenerateJTKernel(p->host, src, &we, iv);
     if (rc) return rc;
     if (len) *len = (int64_t)src.size() + 1;
     if (buf && cap > 0) {
@@ -408,8 +412,9 @@ int fbn_jt_kernel_cache_path(const fbn_jt_plan *p, char *buf, int64_t cap) {
     if (!p || !buf || cap <= 0) return SetError(FBN_ERR_ARG, "bad argument");
     if (!p->gen_eligible) return SetError(FBN_ERR_ARG, "plan not eligible for codegen");
     std::string src;
+    std::vector<double> iv;
     int64_t we = 0;
-    int rc = fbn::GenerateJTKernel(p->host, src, &we);
+    int rc = fbn::GenerateJTKernel(p->host, src, &we, iv);
     if (rc) return rc;
     snprintf(buf, (size_t)cap, "%s", fbn::JitCachePath(src).c_str());
     return FBN_OK;
@@ -425,8 +430,9 @@ int fbn_jt_kernel_build(const fbn_jt_plan *p) {
     if (!p) return SetError(FBN_ERR_ARG, "null pointer");
     if (!p->gen_eligible) return SetError(FBN_ERR_ARG, "plan not eligible for codegen");
     std::string src;
+    std::vector<double> iv;
     int64_t we = 0;
-    int rc = fbn::GenerateJTKernel(p->host, src, &we);
+    int rc = fbn::GenerateJTKernel(p->host, src, &we, iv);
     if (rc) return rc;
     std::vector<char> code;
     return fbn::JitCodeObject(src, code);
@@ -531,8 +537,9 @@ int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, 
         double *a_marg = marg, *a_ws = p->ws.as<double>();
         int32_t *a_lab = labels;
         int *a_flags = p->flags.as<int>();
+        const double *a_iv = p->gen_iv.as<double>();
         long long a_n = ncases;
-        void *args[] = {&a_ev, &a_marg, &a_lab, &a_ws, &a_flags, &a_n};
+        void *args[] = {&a_ev, &a_marg, &a_lab, &a_ws, &a_flags, &a_iv, &a_n};
         FBN_HIP(hipModuleLaunchKernel(p->gen_fn, grid, 1, 1, 64, 1, 1, 0, s, args, nullptr));
         // exact recomputation of the blocks whose denominators left the fast-division range
         if ((rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s))) return rc;

@@ -2,15 +2,29 @@
 //
 // For trees whose cliques are small (ALARM-class), the case-independent schedule is emitted as
 // straight-line code: every table entry of the clique in flight is a named fp64 register value
-// (lane = evidence case), every index map / digit / stride is a compile-time constant, and the
-// initial potentials are read with constant offsets.  No op dispatch, no index arrays, no LDS:
-// the only memory traffic is the evidence, the parked Collect tables, the separator messages and
-// the outputs.  Operation order per entry is exactly the interpreter's (= the reference's), so
-// results are bit-identical; a lane whose normalization denominator leaves [2^-600, 2^600] flags
-// its block, which the exact interpreter then recomputes (see capi.hip).
+// (lane = evidence case), every index map / digit / stride and every initial potential is a
+// compile-time constant; the initial potentials come from a constant buffer through scalar loads.
+// No op dispatch, no index arrays, no LDS.
+//
+// Schedule (values identical to the reference's level order -- a clique's Collect result depends
+// only on its subtree and the fixed order of its child messages, its Distribute result only on its
+// parent's -- so any children-first / parent-first traversal gives the same bits):
+//  * Collect in DFS post-order: the last child's message stays in registers for its parent; other
+//    messages go to the per-wave separator rows in global memory (they are needed again anyway as
+//    the "old" separator of Distribute).
+//  * Distribute in DFS pre-order: a clique's Collect table is not parked and reloaded but
+//    recomputed from its initial potential and its children's stored messages (which Distribute
+//    loads anyway) -- ALU is cheap here, HBM round trips are not.  The message to the first child
+//    stays in registers; the others overwrite their (now dead) Collect message rows.
+//  * Loads for the next clique are issued at the start of the current one (register budget
+//    permitting) so their latency hides behind its arithmetic.
+// Operation order per entry is exactly the interpreter's (= the reference's), so results are
+// bit-identical; a lane whose normalization denominator leaves [2^-600, 2^600] flags its block,
+// which the exact interpreter then recomputes (see capi.hip).
 #include <algorithm>
 #include <map>
 #include <cstdio>
+#include <cstdlib>
 #include <sstream>
 #include <string>
 
@@ -43,34 +57,236 @@ bool JTCodegenEligible(const JTPlanHost &plan, int64_t *entry_ops) {
         ops += t.size() * (4 + (int64_t)t.vars.size());
     }
     if (entry_ops) *entry_ops = ops;
+    for (int d : plan.dom)
+        if (d > 32) return false;  // evidence bit packing
     return tmax <= 256 && ops <= 40000;
 }
 
-// layout of the per-wave workspace (fp64 rows of 64 lanes): [store][dens nc][sep]
-int GenerateJTKernel(const JTPlanHost &plan, std::string &src, int64_t *wave_entries) {
-    const int nc = (int)plan.cliques.size(), ns = (int)plan.seps.size(), V = plan.num_nodes;
-    std::vector<int64_t> store_off(nc, -1), sep_off(ns);
-    int64_t store = 0, sep = 0;
-    for (int c = 0; c < nc; ++c) {
-        if (c == plan.root) continue;
-        store_off[c] = store;
-        store += plan.cliques[c].size();
+namespace {
+
+class JTGen {
+  public:
+    explicit JTGen(const JTPlanHost &p) : plan(p) {}
+    int Run(std::string &src, int64_t *wave_entries, std::vector<double> &initv);
+
+  private:
+    const JTPlanHost &plan;
+    std::ostringstream o;
+    std::vector<int> okw_word, okw_pos, out_off;
+    std::vector<int64_t> sep_row, init_off;
+    std::vector<std::vector<int>> cand;
+    int nobs = 0;
+    const char *SB = "        FBN_OP_BOUNDARY();\n";
+
+    std::string R(int c) const {  // number of unobserved variables of clique c
+        std::vector<unsigned> m(nobs, 0u);
+        for (int v : plan.cliques[c].vars) m[v / 32] |= 1u << (v % 32);
+        std::ostringstream t;
+        t << "(" << plan.cliques[c].vars.size();
+        for (int k = 0; k < nobs; ++k)
+            if (m[k]) t << " - __builtin_popcount(obs" << k << " & " << m[k] << "u)";
+        t << ")";
+        return t.str();
     }
-    for (int s = 0; s < ns; ++s) sep_off[s] = sep, sep += plan.seps[s].size();
-    const int64_t den_base = store, sep_base = store + nc;
-    *wave_entries = sep_base + sep;
+    std::string observed(int v) const {
+        std::ostringstream t;
+        t << "((obs" << v / 32 << " >> " << v % 32 << ") & 1u)";
+        return t.str();
+    }
+    int child(int s) const { return plan.sep_down[s]; }
+    // separator index of clique entry e (the clique's digits of the separator's variables)
+    int64_t SepIndex(const Table &t, const Table &sp, int64_t e) const {
+        int64_t r = e, idx = 0;
+        for (size_t j = 0; j < t.vars.size(); ++j) {
+            const int64_t dgt = r / t.cum[j];
+            r %= t.cum[j];
+            const int l = LocOfT(sp, t.vars[j]);
+            if (l >= 0) idx += dgt * sp.cum[l];
+        }
+        return idx;
+    }
+    std::string EntryCond(const Table &t, int64_t e) const;
+    void Init(const std::string &P, int c);
+    void Mul(const std::string &P, int c, int s, const std::string &M);
+    void SepCol(const std::string &P, int c, int s, bool store);
+    void DMul(const std::string &P, int c, int s, const std::string &M);
+    void SepDis(const std::string &P, int c, int s, const std::string &old, bool store);
+    void Marg(const std::string &P, int c);
+    void Load(const std::string &name, int s) {
+        for (int64_t j = 0; j < plan.seps[s].size(); ++j)
+            o << "        const double " << name << s << "_" << j << " = W(" << sep_row[s] + j << "LL);\n";
+    }
+    static std::string N(const std::string &P, int c, int64_t e) { return P + std::to_string(c) + "_" + std::to_string(e); }
+};
+
+std::string JTGen::EntryCond(const Table &t, int64_t e) const {
+    std::map<int, unsigned> need;
+    int64_t r = e;
+    for (size_t j = 0; j < t.vars.size(); ++j) {
+        const int64_t dgt = r / t.cum[j];
+        r %= t.cum[j];
+        need[okw_word[t.vars[j]]] |= 1u << (okw_pos[t.vars[j]] + dgt);
+    }
+    std::ostringstream c;
+    bool first = true;
+    for (auto &kv : need) {
+        c << (first ? "" : " && ") << "((okw" << kv.first << " & " << kv.second << "u) == " << kv.second << "u)";
+        first = false;
+    }
+    return c.str();
+}
+
+// masked initial potential + Normalize (lazy: values raw, den/y pending)
+void JTGen::Init(const std::string &P, int c) {
+    const Table &t = plan.cliques[c];
+    o << "        double s_" << P << c << " = 0.0;\n";
+    for (int64_t e = 0; e < t.size(); ++e)
+        o << "        double " << N(P, c, e) << " = (" << EntryCond(t, e) << ") ? iv[" << init_off[c] + e << "] : 0.0; s_"
+          << P << c << " += " << N(P, c, e) << ";\n";
+    o << "        den = s_" << P << c << "; y = 1.0 / den; bad |= den_bad(den);\n" << SB;
+}
+
+// CliqueLevelCollection: table *= extended child message (by separator entry), then Normalize
+void JTGen::Mul(const std::string &P, int c, int s, const std::string &M) {
+    const Table &t = plan.cliques[c], &sp = plan.seps[s];
+    std::vector<std::vector<int64_t>> inv(sp.size());
+    for (int64_t e = 0; e < t.size(); ++e) inv[SepIndex(t, sp, e)].push_back(e);
+    for (int64_t j = 0; j < sp.size(); ++j) {
+        o << "       ";
+        for (int64_t e : inv[j]) o << " " << N(P, c, e) << " = dv(" << N(P, c, e) << ", den, y) * " << M << s << "_" << j << ";";
+        o << "\n";
+    }
+    o << "        { double sm = 0.0;";
+    for (int64_t e = 0; e < t.size(); ++e) o << " sm += " << N(P, c, e) << ";";
+    o << " den = sm; y = 1.0 / den; bad |= den_bad(den); }\n" << SB;
+}
+
+// SeparatorLevelCollection: message[k % Ts] += table[k] / den  -> registers mc<s>_j (+ store)
+void JTGen::SepCol(const std::string &P, int c, int s, bool store) {
+    const Table &t = plan.cliques[c];
+    const int64_t Ts = plan.seps[s].size(), Q = t.size() / Ts;
+    for (int64_t j = 0; j < Ts; ++j) {
+        o << "        const double mc" << s << "_" << j << " = dv(" << N(P, c, j) << ", den, y)";
+        for (int64_t q = 1; q < Q; ++q) o << " + dv(" << N(P, c, q * Ts + j) << ", den, y)";
+        o << ";";
+        if (store) o << " W(" << sep_row[s] + j << "LL) = mc" << s << "_" << j << ";";
+        o << "\n";
+    }
+    o << SB;
+}
+
+// CliqueLevelDistribution: table *= parent message broadcast over k % Ts, then Normalize
+void JTGen::DMul(const std::string &P, int c, int s, const std::string &M) {
+    const Table &t = plan.cliques[c];
+    const int64_t Ts = plan.seps[s].size();
+    for (int64_t j = 0; j < Ts; ++j) {
+        o << "       ";
+        for (int64_t e = j; e < t.size(); e += Ts)
+            o << " " << N(P, c, e) << " = dv(" << N(P, c, e) << ", den, y) * " << M << s << "_" << j << ";";
+        o << "\n";
+    }
+    o << "        { double sm = 0.0;";
+    for (int64_t e = 0; e < t.size(); ++e) o << " sm += " << N(P, c, e) << ";";
+    o << " den = sm; y = 1.0 / den; bad |= den_bad(den); }\n" << SB;
+}
+
+// SeparatorLevelDistribution: tmp[map(k)] += table[k] / den; message = tmp / old (zero-guarded)
+void JTGen::SepDis(const std::string &P, int c, int s, const std::string &old, bool store) {
+    const Table &t = plan.cliques[c], &sp = plan.seps[s];
+    std::vector<std::vector<int64_t>> lists(sp.size());
+    for (int64_t e = 0; e < t.size(); ++e) lists[SepIndex(t, sp, e)].push_back(e);
+    for (int64_t j = 0; j < sp.size(); ++j) {
+        o << "        double md" << s << "_" << j << ";";
+        o << " { double a = dv(" << N(P, c, lists[j][0]) << ", den, y);";
+        for (size_t q = 1; q < lists[j].size(); ++q) o << " a += dv(" << N(P, c, lists[j][q]) << ", den, y);";
+        o << " const double od = " << old << s << "_" << j << "; md" << s << "_" << j << " = (od == 0.0) ? 0.0 : a / od; }";
+        if (store) o << " W(" << sep_row[s] + j << "LL) = md" << s << "_" << j << ";";
+        o << "\n";
+    }
+    o << SB;
+}
+
+// GetProbabilitiesOneNode for every variable whose selected clique (first with the fewest reduced
+// variables) is c, and the label (ArgMax, strict '>' from 0; un-normalized if c reduces to one var)
+void JTGen::Marg(const std::string &P, int c) {
+    const Table &t = plan.cliques[c];
+    for (size_t j = 0; j < t.vars.size(); ++j) {
+        const int v = t.vars[j];
+        const int dim = plan.dom[v];
+        const int64_t cum = t.cum[j], bw = dim * cum, nhi = t.size() / bw;
+        // selection: first candidate clique with the fewest reduced variables (recomputed here)
+        o << "        { int b = " << R(cand[v][0]) << ", sl = " << cand[v][0] << ";";
+        for (size_t k = 1; k < cand[v].size(); ++k)
+            o << " { const int r = " << R(cand[v][k]) << "; if (r < b) { b = r; sl = " << cand[v][k] << "; } }";
+        o << "\n        if (sl == " << c << " && !" << observed(v) << ") { // marginal of var " << v << "\n";
+        o << "          double tot = 0.0;";
+        for (int d = 0; d < dim; ++d) o << " double p" << d << ";";
+        o << "\n";
+        for (int d = 0; d < dim; ++d) {
+            bool first = true;
+            o << "          { double a = ";
+            for (int64_t hi = 0; hi < nhi; ++hi)
+                for (int64_t l = 0; l < cum; ++l) {
+                    const int64_t e = hi * bw + d * cum + l;
+                    o << (first ? "" : " a += ") << "dv(" << N(P, c, e) << ", den, y);";
+                    first = false;
+                }
+            o << " p" << d << " = a; tot += a; }\n";
+        }
+        if (v == 0) {
+            o << "          if (act) { int lab = 0; double mp = 0.0;";
+            for (int d = 0; d < dim; ++d)
+                o << " { const double q = (b == 1) ? p" << d << " : p" << d << " / tot; if (q > mp) { mp = q; lab = " << d
+                  << "; } }";
+            o << " labels[cs] = lab; }\n";
+        }
+        o << "          if (act) {";
+        for (int d = 0; d < dim; ++d) o << " out[" << out_off[v] + d << "] = p" << d << " / tot;";
+        o << " }\n        } }\n" << SB;
+    }
+}
+
+int JTGen::Run(std::string &src, int64_t *wave_entries, std::vector<double> &initv) {
+    const int nc = (int)plan.cliques.size(), ns = (int)plan.seps.size(), V = plan.num_nodes;
+    // initial potentials: one constant buffer, read with wave-uniform (scalar) loads
+    initv.clear();
+    init_off.assign(nc, 0);
+    for (int c = 0; c < nc; ++c) {
+        init_off[c] = (int64_t)initv.size();
+        initv.insert(initv.end(), plan.cliques[c].pot.begin(), plan.cliques[c].pot.end());
+    }
+    // per-wave workspace: one row (64 lanes x fp64) per separator entry
+    sep_row.assign(ns, 0);
+    int64_t rows = 0;
+    for (int s = 0; s < ns; ++s) sep_row[s] = rows, rows += plan.seps[s].size();
+    *wave_entries = std::max<int64_t>(rows, 1);
     int SD = 0;
-    std::vector<int> out_off(V);
+    out_off.assign(V, 0);
     for (int v = 0; v < V; ++v) out_off[v] = SD, SD += plan.dom[v];
-    std::vector<std::vector<int>> cand(V);
+    cand.assign(V, {});
     for (int c = 0; c < nc; ++c)
         for (int v : plan.cliques[c].vars) cand[v].push_back(c);
+    // traversal orders
+    std::vector<int> post, pre;
+    std::vector<std::pair<int, size_t>> st{{plan.root, 0}};
+    while (!st.empty()) {  // iterative DFS
+        auto &top = st.back();
+        const int c = top.first;
+        if (top.second == 0) pre.push_back(c);
+        if (top.second < plan.clique_down[c].size()) {
+            const int ch = child(plan.clique_down[c][top.second++]);
+            st.push_back({ch, 0});
+        } else {
+            post.push_back(c);
+            st.pop_back();
+        }
+    }
+    if ((int)post.size() != nc) return SetError(FBN_ERR_LIMIT, "codegen: tree traversal covers %zu of %d cliques", post.size(), nc);
 
-    std::ostringstream o;
     o << "// generated by libfastbn (jt_codegen.cpp): " << nc << " cliques, " << ns << " separators\n";
     o << "#define FBN_V " << V << "\n#define FBN_SD " << SD << "\n#define FBN_WE " << *wave_entries << "LL\n";
     o << R"(typedef signed char i8;
-__device__ __forceinline__ double dv(double x, double den, double y) {
+__device__ __forceinline__ double dv(double x, double den, double y) {  // x / den (Markstein, see jt_kernels.hip)
     const double q = x * y;
     const double r = __builtin_fma(-den, q, x);
     return __builtin_fma(r, y, q);
@@ -79,11 +295,10 @@ __device__ __forceinline__ double dv(double x, double den, double y) {
 typedef __attribute__((address_space(1))) double gdouble;
 typedef __attribute__((address_space(1))) char gchar;
 #define W(row) (*(gdouble *)((gchar *)(Wb + (row) * 64) + (unsigned long long)lo))
-#define FBN_OP_BOUNDARY() do { __asm__ volatile("" : "+s"(Wb), "+v"(lo) :: "memory"); __builtin_amdgcn_sched_barrier(0); } while (0)
 __device__ __forceinline__ bool den_bad(double d) { return !(d >= 0x1p-600 && d <= 0x1p+600); }
 extern "C" __global__ void __launch_bounds__(64, 1)
 fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restrict__ labels,
-           double *__restrict__ ws, int *__restrict__ flags, long long ncases) {
+           double *__restrict__ ws, int *__restrict__ flags, const double *iv, long long ncases) {
     const int lane = threadIdx.x;
     gdouble *Wb = (gdouble *)ws + (unsigned long long)blockIdx.x * FBN_WE * 64;
     unsigned lo = (unsigned)lane * 8;
@@ -96,9 +311,10 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
         bool bad = false;
         double den, y;
 )";
-    // evidence: allowed-value bits of every variable packed into 32-bit words (okw), observed flags
-    // (obs); var v owns bits [pos, pos + dom) of word wd
-    std::vector<int> okw_word(V), okw_pos(V);
+    // evidence: allowed-value bits of every variable packed into 32-bit words (okw<k>), observed
+    // flags (obs<k>); var v owns bits [pos, pos + dom) of its word
+    okw_word.assign(V, 0);
+    okw_pos.assign(V, 0);
     int nokw = 0;
     {
         int pos = 32;
@@ -107,7 +323,22 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
             okw_word[v] = nokw - 1, okw_pos[v] = pos, pos += plan.dom[v];
         }
     }
-    const int nobs = (V + 31) / 32;
+    nobs = (V + 31) / 32;
+    // op boundary: no store->load forwarding, no hoisting of addresses, no scheduling across it,
+    // and the evidence words are opaque per segment, so a Distribute recomputation is not merged
+    // with (and kept live from) its Collect twin
+    {
+        std::vector<std::string> regs;
+        for (int k = 0; k < nokw; ++k) regs.push_back("okw" + std::to_string(k));
+        for (int k = 0; k < nobs; ++k) regs.push_back("obs" + std::to_string(k));
+        o << "#define FBN_OP_BOUNDARY() do { __asm__ volatile(\"\" : \"+s\"(Wb), \"+s\"(iv), \"+v\"(lo) :: \"memory\");";
+        for (size_t i = 0; i < regs.size(); i += 16) {
+            o << " __asm__ volatile(\"\" :";
+            for (size_t k = i; k < std::min(regs.size(), i + 16); ++k) o << (k > i ? ", " : " ") << "\"+v\"(" << regs[k] << ")";
+            o << ");";
+        }
+        o << " __builtin_amdgcn_sched_barrier(0); } while (0)\n";
+    }
     for (int k = 0; k < nokw; ++k) o << "        unsigned okw" << k << " = 0u;\n";
     for (int k = 0; k < nobs; ++k) o << "        unsigned obs" << k << " = 0u;\n";
     for (int v = 0; v < V; ++v) {
@@ -115,185 +346,112 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
         o << "        { const int x = ev[" << v << "]; okw" << okw_word[v] << " |= (x < 0 ? " << full << "u : (1u << x)) << "
           << okw_pos[v] << "; obs" << v / 32 << " |= (x >= 0 ? 1u : 0u) << " << v % 32 << "; }\n";
     }
-    auto observed = [&](int v) {
-        std::ostringstream t;
-        t << "((obs" << v / 32 << " >> " << v % 32 << ") & 1u)";
-        return t.str();
+    o << SB;
+
+    // fp64 values per lane: table in flight + prefetched rows (FBN_JT_PREFETCH_BUDGET: tuning)
+    const int64_t kBudget = getenv("FBN_JT_PREFETCH_BUDGET") ? atoll(getenv("FBN_JT_PREFETCH_BUDGET")) : 200;
+    auto tsize = [&](int c) { return plan.cliques[c].size(); };
+    // ---------------- Collect, DFS post-order
+    // loads of clique post[k]: its children's messages except a last child that is post[k-1]
+    auto collect_loads = [&](size_t k, std::vector<int> &ls) {
+        ls.clear();
+        const int c = post[k];
+        const auto &down = plan.clique_down[c];
+        for (size_t i = 0; i < down.size(); ++i)
+            if (!(i + 1 == down.size() && k > 0 && child(down[i]) == post[k - 1])) ls.push_back(down[i]);
     };
-    auto entry_cond = [&](const Table &t, int64_t e) {  // evidence consistency of entry e
-        std::map<int, unsigned> need;
-        int64_t r = e;
-        for (size_t j = 0; j < t.vars.size(); ++j) {
-            const int64_t dgt = r / t.cum[j];
-            r %= t.cum[j];
-            need[okw_word[t.vars[j]]] |= 1u << (okw_pos[t.vars[j]] + dgt);
-        }
-        std::ostringstream c;
-        bool first = true;
-        for (auto &kv : need) {
-            c << (first ? "" : " && ") << "((okw" << kv.first << " & " << kv.second << "u) == " << kv.second << "u)";
-            first = false;
-        }
-        return c.str();
+    auto rows_of = [&](const std::vector<int> &ls) {
+        int64_t r = 0;
+        for (int s : ls) r += plan.seps[s].size();
+        return r;
     };
-    // op boundary: no store->load forwarding, no hoisting of addresses / scheduling across it
-    const char *SB = "        FBN_OP_BOUNDARY();\n";
-    // ---------------- Collect
-    const int L = (int)plan.levels.size();
-    std::vector<std::string> red(nc);
-    for (int i = ((L - 1) / 2) * 2; i >= 0; i -= 2) {
-        for (int c : plan.levels[i]) {
-            const Table &t = plan.cliques[c];
-            const int64_t T = t.size();
-            const int nv = (int)t.vars.size();
-            o << "        // ---- collect clique " << c << " (" << T << " entries)\n";
-            {
-                std::vector<unsigned> m(nobs, 0u);
-                for (int v : t.vars) m[v / 32] |= 1u << (v % 32);
-                o << "        const int r" << c << " = " << nv;
-                for (int k = 0; k < nobs; ++k)
-                    if (m[k]) o << " - __builtin_popcount(obs" << k << " & " << m[k] << "u)";
-                o << ";\n";
-            }
-            o << "        double";  // one named register value per entry
-            for (int64_t e = 0; e < T; ++e) o << (e ? ", c" : " c") << c << "_" << e;
-            o << ";\n";
-            // INIT: consistency from constant digits
-            o << "        { double s = 0.0;\n";
-            for (int64_t e = 0; e < T; ++e)
-                o << "          c" << c << "_" << e << " = (" << entry_cond(t, e) << ") ? " << Lit(t.pot[e])
-                  << " : 0.0; s += c" << c << "_" << e << ";\n";
-            o << "          den = s; y = 1.0 / s; bad |= den_bad(den); }\n" << SB;
-            // child messages
-            for (int s : plan.clique_down[c]) {
-                const Table &sp = plan.seps[s];
-                o << "        { // x message of separator " << s << "\n";
-                std::vector<std::vector<int64_t>> inv(sp.size());
-                for (int64_t e = 0; e < T; ++e) {
-                    int64_t r = e, idx = 0;
-                    for (int j = 0; j < nv; ++j) {
-                        int64_t dgt = r / t.cum[j];
-                        r %= t.cum[j];
-                        int l = LocOfT(sp, t.vars[j]);
-                        if (l >= 0) idx += dgt * sp.cum[l];
-                    }
-                    inv[idx].push_back(e);
-                }
-                for (int64_t j = 0; j < sp.size(); ++j) {
-                    o << "          { const double m = W(" << (sep_base + sep_off[s] + j) << "LL);";
-                    for (int64_t e : inv[j]) o << " c" << c << "_" << e << " = dv(c" << c << "_" << e << ", den, y) * m;";
-                    o << " }\n";
-                }
-                o << "          double s = 0.0;\n";
-                for (int64_t e = 0; e < T; ++e) o << "          s += c" << c << "_" << e << ";\n";
-                o << "          den = s; y = 1.0 / s; bad |= den_bad(den); }\n" << SB;
-            }
-            if (c != plan.root) {
-                const int s = plan.clique_up[c];
-                const int64_t Ts = plan.seps[s].size();
-                o << "        { // message to separator " << s << "\n";
-                for (int64_t j = 0; j < Ts; ++j) {
-                    o << "          { double a = dv(c" << c << "_" << j << ", den, y);";
-                    for (int64_t q = 1; q < T / Ts; ++q) o << " a += dv(c" << c << "_" << q * Ts + j << ", den, y);";
-                    o << " W(" << (sep_base + sep_off[s] + j) << "LL) = a; }\n";
-                }
-                o << "        }\n" << SB;
-                for (int64_t e = 0; e < T; ++e)
-                    o << "        W(" << (store_off[c] + e) << "LL) = c" << c << "_" << e << ";\n";
-                o << "        W(" << (den_base + c) << "LL) = den;\n" << SB;
-            }
-            if (c == plan.root) o << "        // root stays in registers\n";
+    std::vector<bool> loaded_a(ns, false);
+    for (size_t k = 0; k < post.size(); ++k) {
+        const int c = post[k];
+        std::vector<int> mine, next;
+        collect_loads(k, mine);
+        o << "        // ---- collect clique " << c << " (" << tsize(c) << " entries)\n";
+        for (int s : mine)
+            if (!loaded_a[s]) Load("la", s), loaded_a[s] = true;
+        if (k + 1 < post.size()) {  // prefetch for the next clique
+            collect_loads(k + 1, next);
+            int64_t pend = 0;
+            for (int s : mine) pend += plan.seps[s].size();
+            if (tsize(c) + pend + rows_of(next) <= kBudget)
+                for (int s : next)
+                    if (!loaded_a[s]) Load("la", s), loaded_a[s] = true;
         }
-    }
-    // selections for the marginals: first candidate clique with the fewest reduced variables
-    for (int v = 0; v < V; ++v) {
-        o << "        int sel" << v << " = " << cand[v][0] << "; { int b = r" << cand[v][0] << ";";
-        for (size_t k = 1; k < cand[v].size(); ++k)
-            o << " if (r" << cand[v][k] << " < b) { b = r" << cand[v][k] << "; sel" << v << " = " << cand[v][k] << "; }";
-        o << " }\n";
-    }
-    // ---------------- Distribute + outputs
-    for (int i = 0; i < L; i += 2) {
-        for (int c : plan.levels[i]) {
-            const Table &t = plan.cliques[c];
-            const int64_t T = t.size();
-            const int nv = (int)t.vars.size();
-            o << "        // ---- distribute clique " << c << "\n";
-            if (c != plan.root) {
-                o << "        double";
-                for (int64_t e = 0; e < T; ++e) o << (e ? ", c" : " c") << c << "d_" << e;
-                o << ";\n";
-                for (int64_t e = 0; e < T; ++e)
-                    o << "        c" << c << "d_" << e << " = W(" << (store_off[c] + e) << "LL);\n";
-                o << "        den = W(" << (den_base + c) << "LL); y = 1.0 / den; bad |= den_bad(den);\n" << SB;
-                const int s = plan.clique_up[c];
-                const int64_t Ts = plan.seps[s].size();
-                o << "        {\n";
-                for (int64_t j = 0; j < Ts; ++j) {
-                    o << "          { const double m = W(" << (sep_base + sep_off[s] + j) << "LL);";
-                    for (int64_t e = j; e < T; e += Ts) o << " c" << c << "d_" << e << " = dv(c" << c << "d_" << e << ", den, y) * m;";
-                    o << " }\n";
-                }
-                o << "          double s = 0.0;\n";
-                for (int64_t e = 0; e < T; ++e) o << "          s += c" << c << "d_" << e << ";\n";
-                o << "          den = s; y = 1.0 / s; bad |= den_bad(den); }\n" << SB;
-            }
-            const std::string A = (c == plan.root) ? ("c" + std::to_string(c) + "_") : ("c" + std::to_string(c) + "d_");
-            for (int s : plan.clique_down[c]) {
-                const Table &sp = plan.seps[s];
-                std::vector<std::vector<int64_t>> lists(sp.size());
-                for (int64_t e = 0; e < T; ++e) {
-                    int64_t r = e, idx = 0;
-                    for (int j = 0; j < nv; ++j) {
-                        int64_t dgt = r / t.cum[j];
-                        r %= t.cum[j];
-                        int l = LocOfT(sp, t.vars[j]);
-                        if (l >= 0) idx += dgt * sp.cum[l];
-                    }
-                    lists[idx].push_back(e);
-                }
-                o << "        { // message to separator " << s << " (distribute)\n";
-                for (int64_t j = 0; j < sp.size(); ++j) {
-                    o << "          { double a = dv(" << A << lists[j][0] << ", den, y);";
-                    for (size_t q = 1; q < lists[j].size(); ++q) o << " a += dv(" << A << lists[j][q] << ", den, y);";
-                    const int64_t row = sep_base + sep_off[s] + j;
-                    o << " const double old = W(" << row << "LL); W(" << row << "LL) = (old == 0.0) ? 0.0 : a / old; }\n";
-                }
-                o << "        }\n" << SB;
-            }
-            for (int j = 0; j < nv; ++j) {
-                const int v = t.vars[j];
-                const int dim = plan.dom[v];
-                const int64_t cum = t.cum[j], bw = dim * cum, nhi = T / bw;
-                o << "        if (sel" << v << " == " << c << " && !" << observed(v) << ") { // marginal of var " << v << "\n";
-                o << "          double tot = 0.0; double p[" << dim << "];\n";
-                for (int d = 0; d < dim; ++d) {
-                    bool first = true;
-                    o << "          { double a = ";
-                    for (int64_t hi = 0; hi < nhi; ++hi)
-                        for (int64_t lo = 0; lo < cum; ++lo) {
-                            int64_t e = hi * bw + d * cum + lo;
-                            if (first) {
-                                o << "dv(" << A << e << ", den, y);";
-                                first = false;
-                            } else {
-                                o << " a += dv(" << A << e << ", den, y);";
-                            }
-                        }
-                    o << " p[" << d << "] = a; tot += a; }\n";
-                }
-                if (v == 0) {
-                    o << "          if (act) { int lab = 0; double mp = 0.0;";
-                    for (int d = 0; d < dim; ++d)
-                        o << " { const double q = (r" << c << " == 1) ? p[" << d << "] : p[" << d << "] / tot; if (q > mp) { mp = q; lab = "
-                          << d << "; } }";
-                    o << " labels[cs] = lab; }\n";
-                }
-                o << "          if (act) {";
-                for (int d = 0; d < dim; ++d) o << " out[" << out_off[v] + d << "] = p[" << d << "] / tot;";
-                o << " }\n        }\n" << SB;
-            }
+        o << SB;
+        Init("t", c);
+        const auto &down = plan.clique_down[c];
+        for (size_t i = 0; i < down.size(); ++i) {
+            const int s = down[i];
+            Mul("t", c, s, loaded_a[s] ? "la" : "mc");
         }
+        if (c != plan.root) SepCol("t", c, plan.clique_up[c], true);
+    }
+    // ---------------- Distribute, DFS pre-order (root continues from its Collect registers)
+    // Register policy (kBudget fp64 values per lane):
+    //  * the message to a first child stays in registers if that child's table, the message and
+    //    its largest child message fit; otherwise it is stored and loaded ("ld") right before DMul
+    //  * a clique's children's Collect messages ("lb") are loaded at its start (or prefetched by
+    //    the previous clique) if they fit next to its table; otherwise each is loaded right before
+    //    its Mul and loaded again ("lc") right before its SepDis
+    auto kids_rows = [&](int c) {
+        int64_t r = 0;
+        for (int s : plan.clique_down[c]) r += plan.seps[s].size();
+        return r;
+    };
+    auto max_kid = [&](int c) {
+        int64_t r = 0;
+        for (int s : plan.clique_down[c]) r = std::max<int64_t>(r, plan.seps[s].size());
+        return r;
+    };
+    std::vector<bool> md_reg(ns, false);
+    for (int c : pre)
+        if (!plan.clique_down[c].empty()) {
+            const int s = plan.clique_down[c][0], q = child(s);
+            md_reg[s] = tsize(q) + plan.seps[s].size() + max_kid(q) <= kBudget;
+        }
+    auto early_lb = [&](int c) {
+        const int up = plan.clique_up[c];
+        const int64_t held = (c != plan.root) ? plan.seps[up].size() : 0;  // in registers at DMul either way
+        return tsize(c) + kids_rows(c) + held <= kBudget;
+    };
+    std::vector<bool> loaded_b(ns, false);
+    for (size_t k = 0; k < pre.size(); ++k) {
+        const int c = pre[k];
+        const int up = plan.clique_up[c];
+        const bool early = early_lb(c);
+        o << "        // ---- distribute clique " << c << " (" << tsize(c) << " entries)\n";
+        int64_t pend = 0;
+        if (early)
+            for (int s : plan.clique_down[c]) {
+                if (!loaded_b[s]) Load("lb", s), loaded_b[s] = true;
+                pend += plan.seps[s].size();
+            }
+        if (c != plan.root && md_reg[up]) pend += plan.seps[up].size();
+        if (k + 1 < pre.size() && early_lb(pre[k + 1]) && tsize(c) + pend + kids_rows(pre[k + 1]) <= kBudget)
+            for (int s : plan.clique_down[pre[k + 1]])  // prefetch for the next clique
+                if (!loaded_b[s]) Load("lb", s), loaded_b[s] = true;
+        o << SB;
+        std::string P = "t";
+        if (c != plan.root) {
+            P = "u";  // recompute the Collect table (same ops, same order -> same bits)
+            Init(P, c);
+            for (int s : plan.clique_down[c]) {
+                if (!early) Load("lb", s), o << SB;
+                Mul(P, c, s, "lb");
+            }
+            if (!md_reg[up]) Load("ld", up), o << SB;
+            DMul(P, c, up, md_reg[up] ? "md" : "ld");
+        }
+        const auto &down = plan.clique_down[c];
+        for (size_t i = 0; i < down.size(); ++i) {
+            if (!early) Load("lc", down[i]), o << SB;
+            SepDis(P, c, down[i], early ? "lb" : "lc", !md_reg[down[i]]);
+        }
+        Marg(P, c);
     }
     for (int v = 0; v < V; ++v) {
         o << "        if (act && " << observed(v) << ") {";
@@ -306,6 +464,13 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
 )";
     src = o.str();
     return FBN_OK;
+}
+
+}  // namespace
+
+int GenerateJTKernel(const JTPlanHost &plan, std::string &src, int64_t *wave_entries, std::vector<double> &initv) {
+    JTGen g(plan);
+    return g.Run(src, wave_entries, initv);
 }
 
 }  // namespace fbn
