@@ -117,6 +117,18 @@ class JTGen {
             o << "        const double " << name << s << "_" << j << " = W(" << sep_row[s] + j << "LL);\n";
     }
     static std::string N(const std::string &P, int c, int64_t e) { return P + std::to_string(c) + "_" + std::to_string(e); }
+    // value of entry e as the reference holds it: divided by the pending denominator unless the
+    // table has been normalized eagerly (Normalize) since its last update
+    bool normed = false;
+    std::string Val(const std::string &P, int c, int64_t e) const {
+        return normed ? N(P, c, e) : "dv(" + N(P, c, e) + ", den, y)";
+    }
+    void Normalize(const std::string &P, int c) {
+        const Table &t = plan.cliques[c];
+        for (int64_t e = 0; e < t.size(); ++e) o << (e % 8 ? " " : (e ? "\n        " : "        ")) << N(P, c, e) << " = dv(" << N(P, c, e) << ", den, y);";
+        o << "\n" << SB;
+        normed = true;
+    }
 };
 
 std::string JTGen::EntryCond(const Table &t, int64_t e) const {
@@ -141,9 +153,10 @@ void JTGen::Init(const std::string &P, int c) {
     const Table &t = plan.cliques[c];
     o << "        double s_" << P << c << " = 0.0;\n";
     for (int64_t e = 0; e < t.size(); ++e)
-        o << "        double " << N(P, c, e) << " = (" << EntryCond(t, e) << ") ? iv[" << init_off[c] + e << "] : 0.0; s_"
-          << P << c << " += " << N(P, c, e) << ";\n";
+        o << "        double " << N(P, c, e) << " = sel(" << EntryCond(t, e) << ", iv[" << init_off[c] + e << "]); s_" << P
+          << c << " += " << N(P, c, e) << ";\n";
     o << "        den = s_" << P << c << "; y = 1.0 / den; bad |= den_bad(den);\n" << SB;
+    normed = false;
 }
 
 // CliqueLevelCollection: table *= extended child message (by separator entry), then Normalize
@@ -153,12 +166,13 @@ void JTGen::Mul(const std::string &P, int c, int s, const std::string &M) {
     for (int64_t e = 0; e < t.size(); ++e) inv[SepIndex(t, sp, e)].push_back(e);
     for (int64_t j = 0; j < sp.size(); ++j) {
         o << "       ";
-        for (int64_t e : inv[j]) o << " " << N(P, c, e) << " = dv(" << N(P, c, e) << ", den, y) * " << M << s << "_" << j << ";";
+        for (int64_t e : inv[j]) o << " " << N(P, c, e) << " = " << Val(P, c, e) << " * " << M << s << "_" << j << ";";
         o << "\n";
     }
     o << "        { double sm = 0.0;";
     for (int64_t e = 0; e < t.size(); ++e) o << " sm += " << N(P, c, e) << ";";
     o << " den = sm; y = 1.0 / den; bad |= den_bad(den); }\n" << SB;
+    normed = false;
 }
 
 // SeparatorLevelCollection: message[k % Ts] += table[k] / den  -> registers mc<s>_j (+ store)
@@ -166,8 +180,8 @@ void JTGen::SepCol(const std::string &P, int c, int s, bool store) {
     const Table &t = plan.cliques[c];
     const int64_t Ts = plan.seps[s].size(), Q = t.size() / Ts;
     for (int64_t j = 0; j < Ts; ++j) {
-        o << "        const double mc" << s << "_" << j << " = dv(" << N(P, c, j) << ", den, y)";
-        for (int64_t q = 1; q < Q; ++q) o << " + dv(" << N(P, c, q * Ts + j) << ", den, y)";
+        o << "        const double mc" << s << "_" << j << " = " << Val(P, c, j);
+        for (int64_t q = 1; q < Q; ++q) o << " + " << Val(P, c, q * Ts + j);
         o << ";";
         if (store) o << " W(" << sep_row[s] + j << "LL) = mc" << s << "_" << j << ";";
         o << "\n";
@@ -182,12 +196,13 @@ void JTGen::DMul(const std::string &P, int c, int s, const std::string &M) {
     for (int64_t j = 0; j < Ts; ++j) {
         o << "       ";
         for (int64_t e = j; e < t.size(); e += Ts)
-            o << " " << N(P, c, e) << " = dv(" << N(P, c, e) << ", den, y) * " << M << s << "_" << j << ";";
+            o << " " << N(P, c, e) << " = " << Val(P, c, e) << " * " << M << s << "_" << j << ";";
         o << "\n";
     }
     o << "        { double sm = 0.0;";
     for (int64_t e = 0; e < t.size(); ++e) o << " sm += " << N(P, c, e) << ";";
     o << " den = sm; y = 1.0 / den; bad |= den_bad(den); }\n" << SB;
+    normed = false;
 }
 
 // SeparatorLevelDistribution: tmp[map(k)] += table[k] / den; message = tmp / old (zero-guarded)
@@ -197,8 +212,8 @@ void JTGen::SepDis(const std::string &P, int c, int s, const std::string &old, b
     for (int64_t e = 0; e < t.size(); ++e) lists[SepIndex(t, sp, e)].push_back(e);
     for (int64_t j = 0; j < sp.size(); ++j) {
         o << "        double md" << s << "_" << j << ";";
-        o << " { double a = dv(" << N(P, c, lists[j][0]) << ", den, y);";
-        for (size_t q = 1; q < lists[j].size(); ++q) o << " a += dv(" << N(P, c, lists[j][q]) << ", den, y);";
+        o << " { double a = " << Val(P, c, lists[j][0]) << ";";
+        for (size_t q = 1; q < lists[j].size(); ++q) o << " a += " << Val(P, c, lists[j][q]) << ";";
         o << " const double od = " << old << s << "_" << j << "; md" << s << "_" << j << " = (od == 0.0) ? 0.0 : a / od; }";
         if (store) o << " W(" << sep_row[s] + j << "LL) = md" << s << "_" << j << ";";
         o << "\n";
@@ -228,20 +243,21 @@ void JTGen::Marg(const std::string &P, int c) {
             for (int64_t hi = 0; hi < nhi; ++hi)
                 for (int64_t l = 0; l < cum; ++l) {
                     const int64_t e = hi * bw + d * cum + l;
-                    o << (first ? "" : " a += ") << "dv(" << N(P, c, e) << ", den, y);";
+                    o << (first ? "" : " a += ") << Val(P, c, e) << ";";
                     first = false;
                 }
             o << " p" << d << " = a; tot += a; }\n";
         }
+        o << "          const double yt = 1.0 / tot; bad |= den_bad(tot);\n";
         if (v == 0) {
             o << "          if (act) { int lab = 0; double mp = 0.0;";
             for (int d = 0; d < dim; ++d)
-                o << " { const double q = (b == 1) ? p" << d << " : p" << d << " / tot; if (q > mp) { mp = q; lab = " << d
+                o << " { const double q = (b == 1) ? p" << d << " : dv(p" << d << ", tot, yt); if (q > mp) { mp = q; lab = " << d
                   << "; } }";
             o << " labels[cs] = lab; }\n";
         }
         o << "          if (act) {";
-        for (int d = 0; d < dim; ++d) o << " out[" << out_off[v] + d << "] = p" << d << " / tot;";
+        for (int d = 0; d < dim; ++d) o << " out[" << out_off[v] + d << "] = dv(p" << d << ", tot, yt);";
         o << " }\n        } }\n" << SB;
     }
 }
@@ -294,11 +310,15 @@ __device__ __forceinline__ double dv(double x, double den, double y) {  // x / d
 // row r of the per-wave workspace, this lane: uniform row base (SGPRs) + lane byte offset (VGPR)
 typedef __attribute__((address_space(1))) double gdouble;
 typedef __attribute__((address_space(1))) char gchar;
+typedef __attribute__((address_space(4))) const double cdouble;
 #define W(row) (*(gdouble *)((gchar *)(Wb + (row) * 64) + (unsigned long long)lo))
+// unconditional (scalar) load + select: no branch per table entry
+__device__ __forceinline__ double sel(bool c, double v) { return c ? v : 0.0; }
 __device__ __forceinline__ bool den_bad(double d) { return !(d >= 0x1p-600 && d <= 0x1p+600); }
 extern "C" __global__ void __launch_bounds__(64, 1)
 fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restrict__ labels,
-           double *__restrict__ ws, int *__restrict__ flags, const double *iv, long long ncases) {
+           double *__restrict__ ws, int *__restrict__ flags, const double *ivp, long long ncases) {
+    const cdouble *iv = (const cdouble *)ivp;  // constant address space: scalar loads
     const int lane = threadIdx.x;
     gdouble *Wb = (gdouble *)ws + (unsigned long long)blockIdx.x * FBN_WE * 64;
     unsigned lo = (unsigned)lane * 8;
@@ -447,6 +467,8 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
             DMul(P, c, up, md_reg[up] ? "md" : "ld");
         }
         const auto &down = plan.clique_down[c];
+        // consumers of the normalized table: one SepDis per child, one marginal per variable
+        if (down.size() + plan.cliques[c].vars.size() >= 2) Normalize(P, c);
         for (size_t i = 0; i < down.size(); ++i) {
             if (!early) Load("lc", down[i]), o << SB;
             SepDis(P, c, down[i], early ? "lb" : "lc", !md_reg[down[i]]);
