@@ -102,7 +102,7 @@ struct fbn_jt_plan {
     int gen_state = 0;  // 0 not tried, 1 loaded, -1 failed
     hipModule_t gen_mod = nullptr;
     hipFunction_t gen_fn = nullptr;
-    int64_t gen_we = 0;
+    int64_t gen_we = 0, gen_lds = 0;
     DevBuf flags, ws_fix, gen_iv;
     bool force_fixup = false;
     DevBuf ops, aux, initv, dig;
@@ -363,7 +363,7 @@ static int GenEnsure(fbn_jt_plan *p) {
     p->gen_state = -1;
     std::string src;
     std::vector<double> iv;
-    int rc = fbn::GenerateJTKernel(p->host, src, &p->gen_we, iv);
+    int rc = fbn::GenerateJTKernel(p->host, src, &p->gen_we, iv, &p->gen_lds);
     if (rc) return rc;
     std::vector<char> code;
     if ((rc = fbn::JitCodeObject(src, code))) return rc;
@@ -526,8 +526,9 @@ int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, 
                                      g.state_entries, nc, grid, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt kernel launch: %s", hipGetErrorString(e));
     } else if (variant == 3) {
-        // one wave (64 cases) per SIMD: the clique in flight occupies the register file
-        const int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 4;
+        // one wave (64 cases) per SIMD: the clique in flight occupies the register file (+ LDS tail)
+        int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 4;
+        if (p->gen_lds > 0) wpc = std::max<int>(1, std::min<int64_t>(wpc, (int64_t)kLdsBytes / p->gen_lds));
         const int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * wpc);
         if ((rc = p->ws.ensure((size_t)grid * p->gen_we * 64 * 8))) return rc;
         if ((rc = p->flags.ensure((size_t)nblk * 4))) return rc;
@@ -539,8 +540,15 @@ int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, 
         int *a_flags = p->flags.as<int>();
         const double *a_iv = p->gen_iv.as<double>();
         long long a_n = ncases;
-        void *args[] = {&a_ev, &a_marg, &a_lab, &a_ws, &a_flags, &a_iv, &a_n};
-        FBN_HIP(hipModuleLaunchKernel(p->gen_fn, grid, 1, 1, 64, 1, 1, 0, s, args, nullptr));
+        unsigned long long *a_prof = nullptr;
+        if (p->prof_on) {  // diagnostic: only kernels generated with FBN_JT_PROFILE=1 write it
+            if ((rc = p->prof.ensure((size_t)grid * 16 * 8))) return rc;
+            FBN_HIP(hipMemsetAsync(p->prof.p, 0, (size_t)grid * 16 * 8, s));
+            p->last_grid = grid;
+            a_prof = p->prof.as<unsigned long long>();
+        }
+        void *args[] = {&a_ev, &a_marg, &a_lab, &a_ws, &a_flags, &a_iv, &a_n, &a_prof};
+        FBN_HIP(hipModuleLaunchKernel(p->gen_fn, grid, 1, 1, 64, 1, 1, (unsigned)p->gen_lds, s, args, nullptr));
         // exact recomputation of the blocks whose denominators left the fast-division range
         if ((rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s))) return rc;
     } else {

@@ -91,7 +91,8 @@ int CompileJTProgramLDS(const JTPlanHost &plan, JTProgramLDS &prog);
 // plan-specialized kernel source (jt_codegen.cpp): eligibility and generation.  The generated
 // kernel's per-wave workspace holds wave_entries rows of 64 fp64 lanes; initv is its constant input.
 bool JTCodegenEligible(const JTPlanHost &plan, int64_t *entry_ops);
-int GenerateJTKernel(const JTPlanHost &plan, std::string &src, int64_t *wave_entries, std::vector<double> &initv);
+int GenerateJTKernel(const JTPlanHost &plan, std::string &src, int64_t *wave_entries, std::vector<double> &initv,
+                     int64_t *lds_bytes = nullptr);
 
 }  // namespace fbn
 

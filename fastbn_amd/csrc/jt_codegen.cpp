@@ -3,7 +3,8 @@
 // For trees whose cliques are small (ALARM-class), the case-independent schedule is emitted as
 // straight-line code: every table entry of the clique in flight is a named fp64 register value
 // (lane = evidence case), every index map / digit / stride and every initial potential is a
-// compile-time constant; the initial potentials come from a constant buffer through scalar loads.
+// compile-time constant; the initial potentials are copied into LDS once per wave and read with
+// wave-uniform (broadcast) addresses.
 // No op dispatch, no index arrays, no LDS.
 //
 // Schedule (values identical to the reference's level order -- a clique's Collect result depends
@@ -59,7 +60,7 @@ bool JTCodegenEligible(const JTPlanHost &plan, int64_t *entry_ops) {
     if (entry_ops) *entry_ops = ops;
     for (int d : plan.dom)
         if (d > 32) return false;  // evidence bit packing
-    return tmax <= 256 && ops <= 40000;
+    return tmax <= 256 && ops <= 40000;  // tails beyond 96 entries in LDS: <= 80 KB per wave
 }
 
 namespace {
@@ -68,6 +69,7 @@ class JTGen {
   public:
     explicit JTGen(const JTPlanHost &p) : plan(p) {}
     int Run(std::string &src, int64_t *wave_entries, std::vector<double> &initv);
+    int64_t lds_rows = 0;  // LDS rows (64 lanes x fp64) per wave
 
   private:
     const JTPlanHost &plan;
@@ -76,7 +78,11 @@ class JTGen {
     std::vector<int64_t> sep_row, init_off;
     std::vector<std::vector<int>> cand;
     int nobs = 0;
-    const char *SB = "        FBN_OP_BOUNDARY();\n";
+    // op boundary (+ diagnostic cycle stamp of op category k when FBN_JT_PROFILE is set)
+    bool profile = false;
+    std::string B(int k) const {
+        return profile ? "        FBN_OP_BOUNDARY(); FBN_STAMP(" + std::to_string(k) + ");\n" : "        FBN_OP_BOUNDARY();\n";
+    }
 
     std::string R(int c) const {  // number of unobserved variables of clique c
         std::vector<unsigned> m(nobs, 0u);
@@ -105,7 +111,6 @@ class JTGen {
         }
         return idx;
     }
-    std::string EntryCond(const Table &t, int64_t e) const;
     void Init(const std::string &P, int c);
     void Mul(const std::string &P, int c, int s, const std::string &M);
     void SepCol(const std::string &P, int c, int s, bool store);
@@ -116,7 +121,13 @@ class JTGen {
         for (int64_t j = 0; j < plan.seps[s].size(); ++j)
             o << "        const double " << name << s << "_" << j << " = W(" << sep_row[s] + j << "LL);\n";
     }
-    static std::string N(const std::string &P, int c, int64_t e) { return P + std::to_string(c) + "_" + std::to_string(e); }
+    // entry e of clique c's table: a register value, or (entries >= kRegEntries of a large table)
+    // an LDS row [row][64 lanes] -- only one clique is in flight, so every table starts at row 0
+    int64_t kRegEntries = 96;
+    std::string N(const std::string &P, int c, int64_t e) const {
+        if (e >= kRegEntries) return "L(" + std::to_string(e - kRegEntries) + ")";
+        return P + std::to_string(c) + "_" + std::to_string(e);
+    }
     // value of entry e as the reference holds it: divided by the pending denominator unless the
     // table has been normalized eagerly (Normalize) since its last update
     bool normed = false;
@@ -126,36 +137,50 @@ class JTGen {
     void Normalize(const std::string &P, int c) {
         const Table &t = plan.cliques[c];
         for (int64_t e = 0; e < t.size(); ++e) o << (e % 8 ? " " : (e ? "\n        " : "        ")) << N(P, c, e) << " = dv(" << N(P, c, e) << ", den, y);";
-        o << "\n" << SB;
+        o << "\n" << B(6);
         normed = true;
     }
 };
 
-std::string JTGen::EntryCond(const Table &t, int64_t e) const {
-    std::map<int, unsigned> need;
-    int64_t r = e;
-    for (size_t j = 0; j < t.vars.size(); ++j) {
-        const int64_t dgt = r / t.cum[j];
-        r %= t.cum[j];
-        need[okw_word[t.vars[j]]] |= 1u << (okw_pos[t.vars[j]] + dgt);
-    }
-    std::ostringstream c;
-    bool first = true;
-    for (auto &kv : need) {
-        c << (first ? "" : " && ") << "((okw" << kv.first << " & " << kv.second << "u) == " << kv.second << "u)";
-        first = false;
-    }
-    return c.str();
-}
-
 // masked initial potential + Normalize (lazy: values raw, den/y pending)
 void JTGen::Init(const std::string &P, int c) {
     const Table &t = plan.cliques[c];
+    const int nv = (int)t.vars.size();
+    // per (variable, value) "allowed by the evidence" lane masks, then one AND chain per entry
+    for (int j = 0; j < nv; ++j) {
+        const int v = t.vars[j];
+        for (int d = 0; d < plan.dom[v]; ++d)
+            o << (d ? " " : "        ") << "const bool k" << P << c << "_" << j << "_" << d << " = (okw" << okw_word[v] << " >> "
+              << okw_pos[v] + d << ") & 1u;";
+        o << "\n";
+    }
     o << "        double s_" << P << c << " = 0.0;\n";
-    for (int64_t e = 0; e < t.size(); ++e)
-        o << "        double " << N(P, c, e) << " = sel(" << EntryCond(t, e) << ", iv[" << init_off[c] + e << "]); s_" << P
-          << c << " += " << N(P, c, e) << ";\n";
-    o << "        den = s_" << P << c << "; y = 1.0 / den; bad |= den_bad(den);\n" << SB;
+    // software-pipelined in batches: the LDS reads of batch b+1 are issued before batch b computes
+    const int64_t kB = 16, T = t.size();
+    auto loads = [&](int64_t b0) {
+        if (b0 >= T) return;
+        o << "       ";
+        for (int64_t e = b0; e < std::min(T, b0 + kB); ++e)
+            o << " const double w" << P << c << "_" << e << " = IV(" << init_off[c] + e << ");";
+        o << "\n        __builtin_amdgcn_sched_barrier(0);\n";
+    };
+    loads(0);
+    for (int64_t b0 = 0; b0 < T; b0 += kB) {
+        loads(b0 + kB);
+        for (int64_t e = b0; e < std::min(T, b0 + kB); ++e) {
+            std::ostringstream cond;
+            int64_t r = e;
+            for (int j = 0; j < nv; ++j) {
+                const int64_t dgt = r / t.cum[j];
+                r %= t.cum[j];
+                cond << (j ? " && " : "") << "k" << P << c << "_" << j << "_" << dgt;
+            }
+            o << "        " << (e < kRegEntries ? "double " : "") << N(P, c, e) << " = sel(" << cond.str() << ", w" << P
+              << c << "_" << e << "); s_" << P << c << " += " << N(P, c, e) << ";\n";
+        }
+        o << "        __builtin_amdgcn_sched_barrier(0);\n";
+    }
+    o << "        den = s_" << P << c << "; y = 1.0 / den; bad |= den_bad(den);\n" << B(2);
     normed = false;
 }
 
@@ -171,7 +196,7 @@ void JTGen::Mul(const std::string &P, int c, int s, const std::string &M) {
     }
     o << "        { double sm = 0.0;";
     for (int64_t e = 0; e < t.size(); ++e) o << " sm += " << N(P, c, e) << ";";
-    o << " den = sm; y = 1.0 / den; bad |= den_bad(den); }\n" << SB;
+    o << " den = sm; y = 1.0 / den; bad |= den_bad(den); }\n" << B(3);
     normed = false;
 }
 
@@ -186,7 +211,7 @@ void JTGen::SepCol(const std::string &P, int c, int s, bool store) {
         if (store) o << " W(" << sep_row[s] + j << "LL) = mc" << s << "_" << j << ";";
         o << "\n";
     }
-    o << SB;
+    o << B(4);
 }
 
 // CliqueLevelDistribution: table *= parent message broadcast over k % Ts, then Normalize
@@ -201,7 +226,7 @@ void JTGen::DMul(const std::string &P, int c, int s, const std::string &M) {
     }
     o << "        { double sm = 0.0;";
     for (int64_t e = 0; e < t.size(); ++e) o << " sm += " << N(P, c, e) << ";";
-    o << " den = sm; y = 1.0 / den; bad |= den_bad(den); }\n" << SB;
+    o << " den = sm; y = 1.0 / den; bad |= den_bad(den); }\n" << B(5);
     normed = false;
 }
 
@@ -218,7 +243,7 @@ void JTGen::SepDis(const std::string &P, int c, int s, const std::string &old, b
         if (store) o << " W(" << sep_row[s] + j << "LL) = md" << s << "_" << j << ";";
         o << "\n";
     }
-    o << SB;
+    o << B(7);
 }
 
 // GetProbabilitiesOneNode for every variable whose selected clique (first with the fewest reduced
@@ -250,20 +275,24 @@ void JTGen::Marg(const std::string &P, int c) {
         }
         o << "          const double yt = 1.0 / tot; bad |= den_bad(tot);\n";
         if (v == 0) {
-            o << "          if (act) { int lab = 0; double mp = 0.0;";
+            o << "          if (ACT) { int lab = 0; double mp = 0.0;";
             for (int d = 0; d < dim; ++d)
                 o << " { const double q = (b == 1) ? p" << d << " : dv(p" << d << ", tot, yt); if (q > mp) { mp = q; lab = " << d
                   << "; } }";
-            o << " labels[cs] = lab; }\n";
+            o << " labels[CS] = lab; }\n";
         }
-        o << "          if (act) {";
-        for (int d = 0; d < dim; ++d) o << " out[" << out_off[v] + d << "] = dv(p" << d << ", tot, yt);";
-        o << " }\n        } }\n" << SB;
+        o << "          if (ACT) {";
+        for (int d = 0; d < dim; ++d) o << " OUT(" << out_off[v] + d << ") = dv(p" << d << ", tot, yt);";
+        o << " }\n        } }\n" << B(8);
     }
 }
 
 int JTGen::Run(std::string &src, int64_t *wave_entries, std::vector<double> &initv) {
     const int nc = (int)plan.cliques.size(), ns = (int)plan.seps.size(), V = plan.num_nodes;
+    if (const char *e = getenv("FBN_JT_REG_ENTRIES")) kRegEntries = std::max<int64_t>(1, atoll(e));  // tuning
+    profile = getenv("FBN_JT_PROFILE") && atoi(getenv("FBN_JT_PROFILE")) != 0;  // diagnostic build
+    lds_rows = 0;
+    for (const auto &t : plan.cliques) lds_rows = std::max<int64_t>(lds_rows, t.size() - kRegEntries);
     // initial potentials: one constant buffer, read with wave-uniform (scalar) loads
     initv.clear();
     init_off.assign(nc, 0);
@@ -301,7 +330,8 @@ int JTGen::Run(std::string &src, int64_t *wave_entries, std::vector<double> &ini
 
     o << "// generated by libfastbn (jt_codegen.cpp): " << nc << " cliques, " << ns << " separators\n";
     o << "#define FBN_V " << V << "\n#define FBN_SD " << SD << "\n#define FBN_WE " << *wave_entries << "LL\n";
-    o << R"(typedef signed char i8;
+    o << "#define FBN_IV_BASE " << lds_rows * 64 << "\n#define FBN_NIV " << initv.size() << "\n";
+    o << R"FBN(typedef signed char i8;
 __device__ __forceinline__ double dv(double x, double den, double y) {  // x / den (Markstein, see jt_kernels.hip)
     const double q = x * y;
     const double r = __builtin_fma(-den, q, x);
@@ -312,25 +342,42 @@ typedef __attribute__((address_space(1))) double gdouble;
 typedef __attribute__((address_space(1))) char gchar;
 typedef __attribute__((address_space(4))) const double cdouble;
 #define W(row) (*(gdouble *)((gchar *)(Wb + (row) * 64) + (unsigned long long)lo))
-// unconditional (scalar) load + select: no branch per table entry
+// LDS row of the clique in flight (entries beyond the register-resident part of large tables)
+typedef __attribute__((address_space(3))) double ldouble;
+extern __shared__ double fbn_lds[];
+#define L(row) (ltail[(row) * 64])
+// initial potentials, copied into LDS once per wave (wave-uniform address: broadcast reads)
+#define IV(k) (ivl[k])
+// unconditional (LDS broadcast) load + select: no branch per table entry
 __device__ __forceinline__ double sel(bool c, double v) { return c ? v : 0.0; }
-__device__ __forceinline__ bool den_bad(double d) { return !(d >= 0x1p-600 && d <= 0x1p+600); }
+#define FBN_STAMP(k) do { unsigned long long t_; __asm__ volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_) :: "memory"); pacc[k] += t_ - tprev; tprev = t_; } while (0)
+__device__ __forceinline__ unsigned den_bad(double d) { return (d >= 0x1p-600 && d <= 0x1p+600) ? 0u : 1u; }
+// this lane's case / output row, recomputed per segment from the (laundered) block index
+#define CS (blkl * 64 + lane)
+#define ACT (CS < ncases)
+#define OUT(k) (marg[CS * FBN_SD + (k)])
 extern "C" __global__ void __launch_bounds__(64, 1)
 fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restrict__ labels,
-           double *__restrict__ ws, int *__restrict__ flags, const double *ivp, long long ncases) {
-    const cdouble *iv = (const cdouble *)ivp;  // constant address space: scalar loads
+           double *__restrict__ ws, int *__restrict__ flags, const double *ivp, long long ncases,
+           unsigned long long *__restrict__ prof) {
     const int lane = threadIdx.x;
+    // LDS bases are laundered at every op boundary (so addresses fold into ds_* offsets instead of
+    // being hoisted as loop-invariant constants)
+    ldouble *ltail = (ldouble *)fbn_lds + lane;
+    ldouble *ivl = (ldouble *)fbn_lds + FBN_IV_BASE;
+    for (int k = lane; k < FBN_NIV; k += 64) IV(k) = ivp[k];
+    __syncthreads();
+    unsigned long long pacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tprev = __builtin_amdgcn_s_memtime();
     gdouble *Wb = (gdouble *)ws + (unsigned long long)blockIdx.x * FBN_WE * 64;
     unsigned lo = (unsigned)lane * 8;
     for (long long blk = blockIdx.x; blk * 64 < ncases; blk += gridDim.x) {
+        long long blkl = blk;
         const long long cs = blk * 64 + lane;
-        const bool act = cs < ncases;
-        const long long csr = act ? cs : ncases - 1;
+        const long long csr = cs < ncases ? cs : ncases - 1;
         const i8 *__restrict__ ev = evid + csr * FBN_V;
-        double *__restrict__ out = marg + csr * FBN_SD;
-        bool bad = false;
+        unsigned bad = 0u;  // laundered at op boundaries: checked where computed, never deferred
         double den, y;
-)";
+)FBN";
     // evidence: allowed-value bits of every variable packed into 32-bit words (okw<k>), observed
     // flags (obs<k>); var v owns bits [pos, pos + dom) of its word
     okw_word.assign(V, 0);
@@ -351,7 +398,7 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
         std::vector<std::string> regs;
         for (int k = 0; k < nokw; ++k) regs.push_back("okw" + std::to_string(k));
         for (int k = 0; k < nobs; ++k) regs.push_back("obs" + std::to_string(k));
-        o << "#define FBN_OP_BOUNDARY() do { __asm__ volatile(\"\" : \"+s\"(Wb), \"+s\"(iv), \"+v\"(lo) :: \"memory\");";
+        o << "#define FBN_OP_BOUNDARY() do { __asm__ volatile(\"\" : \"+s\"(Wb), \"+v\"(lo), \"+v\"(ltail), \"+v\"(ivl), \"+v\"(bad), \"+s\"(blkl) :: \"memory\");";
         for (size_t i = 0; i < regs.size(); i += 16) {
             o << " __asm__ volatile(\"\" :";
             for (size_t k = i; k < std::min(regs.size(), i + 16); ++k) o << (k > i ? ", " : " ") << "\"+v\"(" << regs[k] << ")";
@@ -366,7 +413,7 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
         o << "        { const int x = ev[" << v << "]; okw" << okw_word[v] << " |= (x < 0 ? " << full << "u : (1u << x)) << "
           << okw_pos[v] << "; obs" << v / 32 << " |= (x >= 0 ? 1u : 0u) << " << v % 32 << "; }\n";
     }
-    o << SB;
+    o << B(0);
 
     // fp64 values per lane: table in flight + prefetched rows (FBN_JT_PREFETCH_BUDGET: tuning)
     const int64_t kBudget = getenv("FBN_JT_PREFETCH_BUDGET") ? atoll(getenv("FBN_JT_PREFETCH_BUDGET")) : 200;
@@ -401,7 +448,7 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
                 for (int s : next)
                     if (!loaded_a[s]) Load("la", s), loaded_a[s] = true;
         }
-        o << SB;
+        o << B(1);
         Init("t", c);
         const auto &down = plan.clique_down[c];
         for (size_t i = 0; i < down.size(); ++i) {
@@ -438,7 +485,7 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
         const int64_t held = (c != plan.root) ? plan.seps[up].size() : 0;  // in registers at DMul either way
         return tsize(c) + kids_rows(c) + held <= kBudget;
     };
-    std::vector<bool> loaded_b(ns, false);
+    std::vector<bool> loaded_b(ns, false), loaded_d(ns, false);
     for (size_t k = 0; k < pre.size(); ++k) {
         const int c = pre[k];
         const int up = plan.clique_up[c];
@@ -451,37 +498,48 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
                 pend += plan.seps[s].size();
             }
         if (c != plan.root && md_reg[up]) pend += plan.seps[up].size();
-        if (k + 1 < pre.size() && early_lb(pre[k + 1]) && tsize(c) + pend + kids_rows(pre[k + 1]) <= kBudget)
-            for (int s : plan.clique_down[pre[k + 1]])  // prefetch for the next clique
-                if (!loaded_b[s]) Load("lb", s), loaded_b[s] = true;
-        o << SB;
+        if (k + 1 < pre.size()) {  // prefetch for the next clique (before this clique's stores)
+            const int nx = pre[k + 1], nup = plan.clique_up[nx];
+            // its parent message, unless still in registers or produced by this clique
+            const bool ld_next = !md_reg[nup] && plan.sep_up[nup] != c;
+            const int64_t nrows = (early_lb(nx) ? kids_rows(nx) : 0) + (ld_next ? plan.seps[nup].size() : 0);
+            if (tsize(c) + pend + nrows <= kBudget) {
+                if (early_lb(nx))
+                    for (int s : plan.clique_down[nx])
+                        if (!loaded_b[s]) Load("lb", s), loaded_b[s] = true;
+                if (ld_next && !loaded_d[nup]) Load("ld", nup), loaded_d[nup] = true;
+            }
+        }
+        o << B(1);
         std::string P = "t";
         if (c != plan.root) {
             P = "u";  // recompute the Collect table (same ops, same order -> same bits)
             Init(P, c);
             for (int s : plan.clique_down[c]) {
-                if (!early) Load("lb", s), o << SB;
+                if (!early) Load("lb", s), o << B(1);
                 Mul(P, c, s, "lb");
             }
-            if (!md_reg[up]) Load("ld", up), o << SB;
+            if (!md_reg[up] && !loaded_d[up]) Load("ld", up), loaded_d[up] = true, o << B(1);
             DMul(P, c, up, md_reg[up] ? "md" : "ld");
         }
         const auto &down = plan.clique_down[c];
         // consumers of the normalized table: one SepDis per child, one marginal per variable
         if (down.size() + plan.cliques[c].vars.size() >= 2) Normalize(P, c);
         for (size_t i = 0; i < down.size(); ++i) {
-            if (!early) Load("lc", down[i]), o << SB;
+            if (!early) Load("lc", down[i]), o << B(1);
             SepDis(P, c, down[i], early ? "lb" : "lc", !md_reg[down[i]]);
         }
         Marg(P, c);
     }
     for (int v = 0; v < V; ++v) {
-        o << "        if (act && " << observed(v) << ") {";
-        for (int d = 0; d < plan.dom[v]; ++d) o << " out[" << out_off[v] + d << "] = 0.0;";
+        o << "        if (ACT && " << observed(v) << ") {";
+        for (int d = 0; d < plan.dom[v]; ++d) o << " OUT(" << out_off[v] + d << ") = 0.0;";
         o << " }\n";
     }
-    o << R"(        if (__builtin_amdgcn_ballot_w64(bad) != 0ull && lane == 0) flags[blk] = 1;
+    o << R"(        if (__builtin_amdgcn_ballot_w64(bad != 0u) != 0ull && lane == 0) flags[blk] = 1;
     }
+    if (prof && lane == 0)
+        for (int k = 0; k < 10; ++k) prof[(unsigned long long)blockIdx.x * 16 + k] = pacc[k];
 }
 )";
     src = o.str();
@@ -490,9 +548,12 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
 
 }  // namespace
 
-int GenerateJTKernel(const JTPlanHost &plan, std::string &src, int64_t *wave_entries, std::vector<double> &initv) {
+int GenerateJTKernel(const JTPlanHost &plan, std::string &src, int64_t *wave_entries, std::vector<double> &initv,
+                     int64_t *lds_bytes) {
     JTGen g(plan);
-    return g.Run(src, wave_entries, initv);
+    int rc = g.Run(src, wave_entries, initv);
+    if (lds_bytes) *lds_bytes = (g.lds_rows * 64 + (int64_t)initv.size()) * 8;
+    return rc;
 }
 
 }  // namespace fbn
