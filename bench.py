@@ -95,14 +95,16 @@ def bench_pc(steps, warmup):
             "kernel_ms_per_run": 1e3 * pc.kernel_s, "edges": len(pc.edges)}
 
 
-def load_traffic(per_case_bytes):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if present."""
+def load_traffic(cases):
+    """Measured HBM bytes per launch (rocprofv3 FETCH_SIZE + WRITE_SIZE, calibrated; committed
+    summary profiles/jt_traffic.json from tools/pmc_traffic.sh), scaled to this launch's cases."""
     path = os.path.join(REPO, "profiles", "jt_traffic.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
         t = json.load(f)
-    return t.get("hbm_bytes_per_launch")
+    b = t.get("hbm_bytes_per_launch")
+    return None if b is None else b * cases / t.get("cases_per_launch", CASES_PER_GPU)
 
 
 def main():
@@ -184,7 +186,7 @@ def main():
     value = total_cases / elapsed
     bpc = info["algorithmic_bytes_per_case"]
     achieved = bpc * args.cases / (kernel_ms * 1e-3) / 1e9
-    traffic = load_traffic(bpc)
+    traffic = load_traffic(args.cases)
     out = {
         "metric": "JT test-cases/sec (ALARM, Munin) + PC-stable CI-tests/sec, 1/2/4/8 GPU",
         "value": value,
@@ -203,7 +205,12 @@ def main():
                    "evidence_per_case": EVIDENCE_PER_CASE, "parallelism": f"case-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel_ms": kernel_ms, "algorithmic_bytes_per_case": bpc},
+                     "kernel_ms": kernel_ms, "algorithmic_bytes_per_case": bpc,
+                     "kernel_variant": jt.refresh_info()["variant"],
+                     "note": "achieved = materialized-table algorithmic bytes (SURVEY 8(d)) / kernel time; the "
+                             "specialized kernel keeps tables in registers/LDS and recomputes instead of "
+                             "parking them, so measured traffic is below the algorithmic bytes and the "
+                             "kernel is fp64-VALU/latency bound (DESIGN.md)"},
     }
     if rank == 0 and world == 1:
         if not args.no_pc:
