@@ -135,7 +135,8 @@ def main():
     from fastbn_amd import synth
 
     net_py = synth.read_xmlbif(os.path.join(ALARM, "alarm.xml"))
-    ev = synth.evidence_cases(net_py, args.cases, EVIDENCE_PER_CASE, seed=20250131 + rank)
+    from fastbn_amd import shard
+    ev = synth.evidence_cases(net_py, args.cases, EVIDENCE_PER_CASE, seed=shard.synthetic_seed(20250131, rank))
     jt = F.JunctionTree(F.Network(os.path.join(ALARM, "alarm.xml")), device=local)
     if args.waves_per_cu:
         jt.set_waves_per_cu(args.waves_per_cu)
@@ -166,10 +167,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = shard.max_over_ranks(elapsed, dev)  # identity at N = 1
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_pairs]))
 
     # sanity: labels of the last step agree with a CPU recomputation on a few cases (not timed)

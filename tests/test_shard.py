@@ -1,0 +1,72 @@
+"""N>1 path of the JT bench / evaluation on CPU: world_size-2 gloo process group, each rank computes
+its contiguous shard (here with the CPU oracle standing in for the GPU kernel), results gathered and
+compared with a single-process run; max-over-ranks timing reduction."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+from fastbn_amd import shard  # noqa: E402
+
+
+def test_case_shard_partition():
+    for total in (0, 1, 63, 100000, 100003):
+        for world in (1, 2, 3, 8):
+            parts = [shard.case_shard(total, r, world) for r in range(world)]
+            assert sum(c for _, c in parts) == total
+            assert parts[0][0] == 0
+            for (s0, c0), (s1, _) in zip(parts, parts[1:]):
+                assert s0 + c0 == s1
+            assert max(c for _, c in parts) - min(c for _, c in parts) <= 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, xml, ev_path, out_path):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import oracle as O
+    ev = np.load(ev_path)
+    start, count = shard.case_shard(ev.shape[0], rank, world)
+    lab, marg = O.OracleJT(xml).infer(ev[start:start + count])
+    labels = shard.gather_shards(lab, ev.shape[0])
+    margs = shard.gather_shards(marg, ev.shape[0])
+    tmax = shard.max_over_ranks(float(rank + 1))
+    sums = shard.sum_over_ranks([float(count), float((lab == 0).sum())])
+    if rank == 0:
+        np.savez(out_path, labels=labels, margs=margs, tmax=tmax, sums=sums)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_shards_match_single_process(tmp_path):
+    mp = pytest.importorskip("torch.multiprocessing")
+    import oracle as O
+    from fastbn_amd import synth
+    xml = os.path.join(REPO, "tests", "golden", "alarm", "alarm.xml")
+    ev = synth.evidence_cases(synth.read_xmlbif(xml), 301, 7, seed=shard.synthetic_seed(20250131, 0))
+    ev_path = str(tmp_path / "ev.npy")
+    np.save(ev_path, ev)
+    out = str(tmp_path / "out.npz")
+    mp.start_processes(_worker, args=(2, _free_port(), xml, ev_path, out), nprocs=2, join=True,
+                       start_method="spawn")
+    r = np.load(out)
+    lab, marg = O.OracleJT(xml).infer(ev)
+    np.testing.assert_array_equal(r["labels"], lab)
+    np.testing.assert_array_equal(r["margs"], marg)
+    assert float(r["tmax"]) == 2.0
+    assert r["sums"][0] == 301 and r["sums"][1] == (lab == 0).sum()
