@@ -467,7 +467,8 @@ static int LaunchLds(fbn_jt_plan *p, DevBuf &ws, const int8_t *d_evidence, int64
     int wpc, cap, rc;
     LdsGeometry(p, &wpc, &cap);
     const bool spill = cap < l.max_table;
-    const int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * wpc);
+    // fixup mode: flagged blocks are rare, one wave per CU scans the flags
+    const int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * (flags ? 1 : wpc));
     const int64_t store_off = 0, den_off = l.store_entries, sep_off = den_off + nc, spill_off = sep_off + l.sep_entries;
     const int64_t wave_entries = spill_off + (spill ? l.max_table - cap : 0);
     const size_t ws_d = (size_t)grid * wave_entries * 64 * 8;
@@ -533,7 +534,7 @@ int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, 
         if ((rc = p->ws.ensure((size_t)grid * p->gen_we * 64 * 8))) return rc;
         if ((rc = p->flags.ensure((size_t)nblk * 4))) return rc;
         FBN_HIP(hipEventRecord(p->ev0, s));
-        FBN_HIP(hipMemsetAsync(p->flags.p, p->force_fixup ? 1 : 0, (size_t)nblk * 4, s));
+
         const int8_t *a_ev = d_evidence;
         double *a_marg = marg, *a_ws = p->ws.as<double>();
         int32_t *a_lab = labels;
@@ -549,6 +550,7 @@ int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, 
         }
         void *args[] = {&a_ev, &a_marg, &a_lab, &a_ws, &a_flags, &a_iv, &a_n, &a_prof};
         FBN_HIP(hipModuleLaunchKernel(p->gen_fn, grid, 1, 1, 64, 1, 1, (unsigned)p->gen_lds, s, args, nullptr));
+        if (p->force_fixup) FBN_HIP(hipMemsetAsync(p->flags.p, 1, (size_t)nblk * 4, s));  // testing only
         // exact recomputation of the blocks whose denominators left the fast-division range
         if ((rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s))) return rc;
     } else {

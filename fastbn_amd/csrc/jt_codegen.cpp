@@ -536,7 +536,8 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
         for (int d = 0; d < plan.dom[v]; ++d) o << " OUT(" << out_off[v] + d << ") = 0.0;";
         o << " }\n";
     }
-    o << R"(        if (__builtin_amdgcn_ballot_w64(bad != 0u) != 0ull && lane == 0) flags[blk] = 1;
+    o << R"(        const bool any_bad = __builtin_amdgcn_ballot_w64(bad != 0u) != 0ull;
+        if (lane == 0) flags[blk] = any_bad ? 1 : 0;  // every block writes its flag: no clearing pass
     }
     if (prof && lane == 0)
         for (int k = 0; k < 10; ++k) prof[(unsigned long long)blockIdx.x * 16 + k] = pacc[k];
