@@ -96,7 +96,7 @@ struct fbn_jt_plan {
     fbn::JTPlanHost host;
     fbn::JTProgram prog;      // variant 1: whole case state in a global workspace
     fbn::JTProgramLDS lprog;  // variant 0 (default): clique in flight resident in LDS
-    int device = 0, num_cu = 0, waves_per_cu = 0, variant = -1;
+    int device = 0, num_cu = 0, waves_per_cu = 0, variant = -1, last_variant = -1;
     // plan-specialized kernel (variant 3)
     bool gen_eligible = false;
     int gen_state = 0;  // 0 not tried, 1 loaded, -1 failed
@@ -298,7 +298,7 @@ int fbn_jt_plan_info_get(const fbn_jt_plan *p, fbn_jt_plan_info *info) {
     info->num_ops = (int32_t)p->prog.ops.size();
     info->max_vars_per_table = p->prog.max_vars;
     info->specialized_eligible = p->gen_eligible ? 1 : 0;
-    info->variant = p->variant >= 0 ? p->variant : (p->gen_state == 1 ? 3 : p->gen_state == -1 ? 0 : -1);
+    info->variant = p->variant >= 0 ? p->variant : p->last_variant;
     return FBN_OK;
 }
 
@@ -511,12 +511,25 @@ int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, 
         labels = p->labels.as<int32_t>();
     }
     int variant = p->variant;
-    if (variant == -1) variant = (p->gen_eligible && GenEnsure(p) == FBN_OK) ? 3 : 0;
+    if (variant == -1) {
+        // specialized kernel when eligible; else the LDS interpreter while the largest clique fits
+        // LDS at >= 2 waves per CU, the global-workspace interpreter for spill-heavy (Munin-class) plans
+        if (p->gen_eligible && GenEnsure(p) == FBN_OK) variant = 3;
+        else variant = (p->lprog.max_table * 64 * 8 * 2 <= (int64_t)kLdsBytes) ? 0 : 1;
+    }
     else if (variant == 3 && (rc = GenEnsure(p))) return rc;
+    p->last_variant = variant;
 
     if (variant == 1) {
         const int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 8;
-        const int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * wpc);
+        int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * wpc);
+        // persistent waves: cap the per-wave workspaces at half of the free HBM
+        const size_t per_wave = (size_t)g.state_entries * 64 * 8 + (size_t)nc * 64 * 4;
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && per_wave > 0) {
+            const size_t have = free_b / 2 + (p->ws.bytes);
+            grid = (int)std::max<int64_t>(1, std::min<int64_t>(grid, (int64_t)(have / per_wave)));
+        }
         const size_t ws_d = (size_t)grid * g.state_entries * 64 * 8;
         const size_t ws_i = (size_t)grid * nc * 64 * 4;
         if ((rc = p->ws.ensure(ws_d + ws_i))) return rc;
