@@ -20,11 +20,14 @@ from .api import (  # noqa: F401
     JunctionTree,
     IndependenceTest,
     PCStable,
+    PCResult,
+    orient_skeleton,
+    shd_bif,
     lib,
     load_libsvm,
     device_count,
     kernel_options,
 )
 
-__all__ = ["FastBNError", "Network", "Dataset", "JunctionTree", "IndependenceTest", "PCStable",
+__all__ = ["FastBNError", "Network", "Dataset", "JunctionTree", "IndependenceTest", "PCStable", "PCResult", "orient_skeleton", "shd_bif",
            "lib", "load_libsvm", "device_count", "kernel_options"]

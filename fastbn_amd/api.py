@@ -55,6 +55,11 @@ _SIGS = {
     "fbn_pc_edges": [_vp, _vp],
     "fbn_pc_sepsets": [_vp, _vp, _i64, _vp],
     "fbn_pc_timing": [_vp, _vp, _vp],
+    "fbn_pc_orient_skeleton": [C.c_int, _vp, C.c_int, _vp, C.c_int64, _vp],
+    "fbn_pc_num_oriented_edges": [_vp, _vp],
+    "fbn_pc_oriented_edges": [_vp, _vp],
+    "fbn_pc_shd_bif": [_vp, C.c_char_p, _vp],
+    "fbn_shd_bif": [C.c_char_p, C.c_int, _vp, C.c_int, _vp],
     "fbn_pc_result_destroy": [_vp],
 }
 
@@ -340,41 +345,90 @@ class IndependenceTest:
             self._h = None
 
 
+class PCResult:
+    """A PC-stable result handle: skeleton, sepsets, orientation, SHD (fbn_pc_*)."""
+
+    def __init__(self, handle):
+        self._h = handle
+        ne, no = C.c_int(), C.c_int()
+        lib.fbn_pc_num_edges(handle, C.byref(ne))
+        e = np.zeros((max(ne.value, 1), 2), np.int32)
+        if ne.value:
+            lib.fbn_pc_edges(handle, _p(e))
+        self.edges = [tuple(map(int, x)) for x in e[:ne.value]]
+        ln = C.c_int64()
+        lib.fbn_pc_sepsets(handle, None, 0, C.byref(ln))
+        buf = np.zeros(max(ln.value, 1), np.int32)
+        lib.fbn_pc_sepsets(handle, _p(buf), ln.value, C.byref(ln))
+        self.sepset, k = {}, 0
+        while k < ln.value:
+            x, y, m = map(int, buf[k:k + 3])
+            self.sepset[(x, y)] = tuple(int(v) for v in buf[k + 3:k + 3 + m])
+            k += 3 + m
+        lib.fbn_pc_num_oriented_edges(handle, C.byref(no))
+        t = np.zeros((max(no.value, 1), 3), np.int32)
+        if no.value:
+            lib.fbn_pc_oriented_edges(handle, _p(t))
+        # (from, to, 1) arcs and (min, max, 0) undirected edges, in vec_edges order
+        self.oriented = [tuple(map(int, x)) for x in t[:no.value]]
+
+    def GetSHD(self, bif_path):
+        """BNSLComparison(ref_net, network).GetSHD() with ref_net loaded from a BIF file."""
+        shd = C.c_int()
+        lib.fbn_pc_shd_bif(self._h, os.fsencode(bif_path), C.byref(shd))
+        return shd.value
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib.fbn_pc_result_destroy(self._h)
+            self._h = None
+
+
+def shd_bif(bif_path, nvars, oriented):
+    """SHD of a learned graph [(from, to, 1) | (a, b, 0)] vs the CPDAG of a BIF DAG."""
+    t = np.ascontiguousarray(np.asarray(oriented if oriented else [(0, 0, 0)], np.int32).reshape(-1, 3))
+    shd = C.c_int()
+    lib.fbn_shd_bif(os.fsencode(bif_path), int(nvars), _p(t), len(oriented), C.byref(shd))
+    return shd.value
+
+
+def orient_skeleton(nvars, edges, sepset):
+    """Host-only orientation of a given skeleton (PCStable steps 2-3) -> PCResult."""
+    pairs = np.ascontiguousarray(np.asarray(edges, np.int32).reshape(-1, 2))
+    rec = []
+    for (x, y), z in sorted(sepset.items()):
+        rec += [x, y, len(z)] + list(z)
+    rec = np.ascontiguousarray(np.asarray(rec if rec else [0], np.int32))
+    r = C.c_void_p()
+    lib.fbn_pc_orient_skeleton(int(nvars), _p(pairs), int(pairs.shape[0]), _p(rec), len(rec) if sepset else 0,
+                               C.byref(r))
+    return PCResult(r)
+
+
 class PCStable:
-    """PC-stable skeleton search (PCStable(net, alpha, depth).StructLearnCompData)."""
+    """PC-stable (PCStable(net, alpha, depth).StructLearnCompData): device skeleton + host orientation."""
 
     def __init__(self, alpha=0.05, depth=1000, device=0):
         self.alpha, self.depth, self.device = alpha, depth, device
+        self.result = None
 
     def StructLearnCompData(self, dataset, group_size=1, num_threads=1, print_struct=False, verbose=False):
         ci = IndependenceTest(dataset, self.alpha, self.device)
         r = C.c_void_p()
         lib.fbn_pc_stable(ci._h, self.alpha, self.depth, group_size, C.byref(r))
-        try:
-            nl, ne = C.c_int(), C.c_int()
-            lib.fbn_pc_num_levels(r, C.byref(nl))
-            self.tests_per_level = np.zeros(nl.value, np.int64)
-            self.launched_per_level = np.zeros(nl.value, np.int64)
-            lib.fbn_pc_level_tests(r, _p(self.tests_per_level))
-            lib.fbn_pc_level_launched(r, _p(self.launched_per_level))
-            lib.fbn_pc_num_edges(r, C.byref(ne))
-            e = np.zeros((ne.value, 2), np.int32)
-            if ne.value:
-                lib.fbn_pc_edges(r, _p(e))
-            self.edges = [tuple(map(int, x)) for x in e]
-            ln = C.c_int64()
-            lib.fbn_pc_sepsets(r, None, 0, C.byref(ln))
-            buf = np.zeros(max(ln.value, 1), np.int32)
-            lib.fbn_pc_sepsets(r, _p(buf), ln.value, C.byref(ln))
-            self.sepset, k = {}, 0
-            while k < ln.value:
-                x, y, m = map(int, buf[k:k + 3])
-                self.sepset[(x, y)] = tuple(int(v) for v in buf[k + 3:k + 3 + m])
-                k += 3 + m
-            tot, ker = C.c_double(), C.c_double()
-            lib.fbn_pc_timing(r, C.byref(tot), C.byref(ker))
-            self.total_s, self.kernel_s = tot.value, ker.value
-            self.num_ci_test = int(self.tests_per_level.sum())
-        finally:
-            lib.fbn_pc_result_destroy(r)
+        self.result = PCResult(r)
+        nl = C.c_int()
+        lib.fbn_pc_num_levels(r, C.byref(nl))
+        self.tests_per_level = np.zeros(nl.value, np.int64)
+        self.launched_per_level = np.zeros(nl.value, np.int64)
+        lib.fbn_pc_level_tests(r, _p(self.tests_per_level))
+        lib.fbn_pc_level_launched(r, _p(self.launched_per_level))
+        self.edges, self.sepset, self.oriented = self.result.edges, self.result.sepset, self.result.oriented
+        tot, ker = C.c_double(), C.c_double()
+        lib.fbn_pc_timing(r, C.byref(tot), C.byref(ker))
+        self.total_s, self.kernel_s = tot.value, ker.value
+        self.num_ci_test = int(self.tests_per_level.sum())
         return self
+
+    def GetSHD(self, bif_path):
+        return self.result.GetSHD(bif_path)

@@ -771,6 +771,7 @@ int fbn_pc_stable(fbn_ci_ctx *c, double alpha, int depth, int group_size, fbn_pc
     FBN_HIP(hipSetDevice(c->device));
     int rc = fbn::RunPCStable(c, alpha, depth, group_size, r->r);
     if (rc) return rc;
+    if ((rc = fbn::OrientPC(c->nvars, r->r))) return rc;  // StructLearnByPCStable steps 2-3
     *out = r.release();
     return FBN_OK;
 }
@@ -814,6 +815,63 @@ int fbn_pc_sepsets(const fbn_pc_result *r, int32_t *buf, int64_t cap, int64_t *l
     }
     if (len) *len = k;
     return FBN_OK;
+}
+int fbn_pc_orient_skeleton(int nvars, const int32_t *pairs, int nedges, const int32_t *sepsets, int64_t len,
+                           fbn_pc_result **out) {
+    if (nvars <= 0 || nedges < 0 || (nedges && !pairs) || (len && !sepsets) || !out)
+        return SetError(FBN_ERR_ARG, "bad argument");
+    auto r = std::unique_ptr<fbn_pc_result>(new (std::nothrow) fbn_pc_result());
+    if (!r) return SetError(FBN_ERR_NOMEM, "out of memory");
+    for (int i = 0; i < nedges; ++i) {
+        const int a = pairs[2 * i], b = pairs[2 * i + 1];
+        if (a < 0 || b < 0 || a >= nvars || b >= nvars || a == b) return SetError(FBN_ERR_ARG, "bad edge %d", i);
+        r->r.edges.push_back({std::min(a, b), std::max(a, b)});
+    }
+    for (int64_t k = 0; k < len;) {  // (x, y, m, z_0..z_{m-1}) records, as fbn_pc_sepsets writes them
+        if (k + 3 > len || k + 3 + sepsets[k + 2] > len || sepsets[k + 2] < 0) return SetError(FBN_ERR_ARG, "bad sepset list");
+        const int x = sepsets[k], y = sepsets[k + 1], m = sepsets[k + 2];
+        r->r.sepset[{std::min(x, y), std::max(x, y)}] = std::vector<int>(sepsets + k + 3, sepsets + k + 3 + m);
+        k += 3 + m;
+    }
+    int rc = fbn::OrientPC(nvars, r->r);
+    if (rc) return rc;
+    *out = r.release();
+    return FBN_OK;
+}
+int fbn_pc_num_oriented_edges(const fbn_pc_result *r, int *n) {
+    if (!r || !n) return SetError(FBN_ERR_ARG, "null pointer");
+    *n = (int)r->r.oriented.size();
+    return FBN_OK;
+}
+int fbn_pc_oriented_edges(const fbn_pc_result *r, int32_t *triples) {
+    if (!r || !triples) return SetError(FBN_ERR_ARG, "null pointer");
+    for (size_t i = 0; i < r->r.oriented.size(); ++i)
+        for (int k = 0; k < 3; ++k) triples[3 * i + k] = r->r.oriented[i][k];
+    return FBN_OK;
+}
+int fbn_shd_bif(const char *bif_path, int nvars, const int32_t *triples, int n, int *shd) {
+    if (!bif_path || !shd || n < 0 || (n && !triples)) return SetError(FBN_ERR_ARG, "bad argument");
+    std::vector<std::string> names;
+    std::vector<std::pair<int, int>> arcs;
+    int rc = fbn::LoadBifGraph(bif_path, names, arcs);
+    if (rc) return rc;
+    if ((int)names.size() != nvars)
+        return SetError(FBN_ERR_ARG, "%s has %zu variables, the learned graph %d", bif_path, names.size(), nvars);
+    std::vector<std::array<int, 3>> learned(n);
+    for (int i = 0; i < n; ++i) {
+        learned[i] = {triples[3 * i], triples[3 * i + 1], triples[3 * i + 2] ? 1 : 0};
+        if (learned[i][0] < 0 || learned[i][0] >= nvars || learned[i][1] < 0 || learned[i][1] >= nvars)
+            return SetError(FBN_ERR_ARG, "edge %d out of range", i);
+    }
+    int unl = 0;
+    return fbn::ComputeSHD(nvars, arcs, learned, shd, &unl);
+}
+int fbn_pc_shd_bif(const fbn_pc_result *r, const char *bif_path, int *shd) {
+    if (!r || !bif_path || !shd) return SetError(FBN_ERR_ARG, "null pointer");
+    std::vector<int32_t> t(3 * r->r.oriented.size() + 3);
+    for (size_t i = 0; i < r->r.oriented.size(); ++i)
+        for (int k = 0; k < 3; ++k) t[3 * i + k] = r->r.oriented[i][k];
+    return fbn_shd_bif(bif_path, r->r.num_nodes, t.data(), (int)r->r.oriented.size(), shd);
 }
 int fbn_pc_timing(const fbn_pc_result *r, double *total_s, double *kernel_s) {
     if (!r) return SetError(FBN_ERR_ARG, "null pointer");

@@ -1,6 +1,7 @@
 // PCStable.cpp -- see PCStable.h
 #include "PCStable.h"
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -14,6 +15,7 @@ void PCStable::StructLearnCompData(fbn_dataset *dts, int group_size, int /*num_t
     int nvars = 0;
     int64_t nsamples = 0;
     fbn_dataset_shape(dts, &nvars, &nsamples);
+    nvars_ = nvars;
     std::vector<int32_t> dims(nvars);
     std::vector<uint8_t> cols((size_t)nvars * nsamples);
     fbn_dataset_dims(dts, dims.data());
@@ -62,14 +64,33 @@ void PCStable::StructLearnCompData(fbn_dataset *dts, int group_size, int /*num_t
     std::cout << "# remaining edges = " << edges.size() << std::endl;
     std::cout << "pc-stable: " << s << " s pc-stable step 1: " << total_s << " s (device kernels " << kernel_s
               << " s)" << std::endl;
-    if (print_struct) {
+    int no = 0;
+    fbn_pc_num_oriented_edges(res, &no);
+    std::vector<int32_t> tri(3 * (size_t)no + 3);
+    fbn_pc_oriented_edges(res, tri.data());
+    oriented.clear();
+    for (int i = 0; i < no; ++i) oriented.push_back({tri[3 * i], tri[3 * i + 1], tri[3 * i + 2]});
+    if (print_struct) {  // Network::PrintEachEdgeWithName
         char a[256], b[256];
-        for (auto &e : edges) {
-            fbn_dataset_var_name(dts, e.first, a, sizeof a);
-            fbn_dataset_var_name(dts, e.second, b, sizeof b);
-            std::cout << a << " -- " << b << std::endl;
+        for (auto &e : oriented) {
+            fbn_dataset_var_name(dts, e[0], a, sizeof a);
+            fbn_dataset_var_name(dts, e[1], b, sizeof b);
+            std::cout << a << (e[2] ? " -> " : " -- ") << b << std::endl;
         }
     }
     fbn_pc_result_destroy(res);
     fbn_ci_ctx_destroy(ctx);
+}
+
+int PCStable::GetSHD(const std::string &bif_path) const {
+    std::vector<int32_t> tri;
+    for (auto &e : oriented) tri.insert(tri.end(), e.begin(), e.end());
+    tri.resize(tri.size() + 3);
+    int shd = -1, nvars = 0;
+    for (auto &e : oriented) nvars = std::max(nvars, std::max(e[0], e[1]) + 1);
+    if (fbn_shd_bif(bif_path.c_str(), nvars_ > 0 ? nvars_ : nvars, tri.data(), (int)oriented.size(), &shd)) {
+        fprintf(stderr, "Error in GetSHD: %s\n", fbn_last_error());
+        exit(1);
+    }
+    return shd;
 }

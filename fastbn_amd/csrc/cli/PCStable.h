@@ -5,6 +5,7 @@
 #ifndef FBN_CLI_PCSTABLE_H
 #define FBN_CLI_PCSTABLE_H
 
+#include <array>
 #include <map>
 #include <set>
 #include <string>
@@ -25,9 +26,13 @@ public:
     std::vector<std::pair<int, int>> edges;         // skeleton, vec_edges order
     std::map<std::pair<int, int>, std::set<int>> sepset;
     std::vector<int64_t> tests_per_level;
+    std::vector<std::array<int, 3>> oriented;  // after steps 2-3: (from, to, 1) / (a, b, 0)
+    // BNSLComparison(ref_net, network).GetSHD() with ref_net loaded from a BIF file (src/main.cpp:39-44)
+    int GetSHD(const std::string &bif_path) const;
 
 private:
     int device_;
+    int nvars_ = 0;
 };
 
 #endif

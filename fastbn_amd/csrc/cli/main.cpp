@@ -66,6 +66,7 @@ int main(int argc, char **argv) {
         PCStable pc(0.05, depth, device);
         pc.StructLearnCompData(ds, group_size, num_threads, false, false);
         fbn_dataset_destroy(ds);
+        std::cout << "SHD = " << pc.GetSHD(ref_net_file) << std::endl;
     } else if (algorithm == 2) {
         std::cout << "===============================" << std::endl
                   << "Algorithm: junction tree (JT) for exact inference, #threads = " << num_threads << std::endl

@@ -2,8 +2,10 @@
 #ifndef FBN_PC_INTERNAL_H
 #define FBN_PC_INTERNAL_H
 
+#include <array>
 #include <cstdint>
 #include <map>
+#include <string>
 #include <utility>
 #include <vector>
 
@@ -17,6 +19,9 @@ struct PCResultHost {
     std::vector<int64_t> tests_per_level;     // reference (t = 1) counts
     std::vector<int64_t> launched_per_level;  // device tests incl. speculation
     double total_s = 0.0, kernel_s = 0.0;
+    // after orientation: (from, to, 1) arcs and (min, max, 0) undirected edges, vec_edges order
+    std::vector<std::array<int, 3>> oriented;
+    int num_nodes = 0;
 };
 
 void CiCtxShape(const fbn_ci_ctx *c, int *nvars, int64_t *nsamples);
@@ -25,6 +30,11 @@ void CiCtxShape(const fbn_ci_ctx *c, int *nvars, int64_t *nsamples);
 int CiRunBatch(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alpha, uint8_t *indep, int32_t *df,
                PCResultHost &res);
 int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResultHost &res);
+// orientation (pc_orient.cpp): v-structures + Meek rules 1-3 on res.edges / res.sepset
+int OrientPC(int nvars, PCResultHost &res);
+int LoadBifGraph(const std::string &path, std::vector<std::string> &names, std::vector<std::pair<int, int>> &arcs);
+int ComputeSHD(int n, const std::vector<std::pair<int, int>> &arcs, const std::vector<std::array<int, 3>> &learned,
+               int *shd, int *unlabelled);
 
 }  // namespace fbn
 

@@ -1,0 +1,381 @@
+// pc_orient.cpp -- PC-stable orientation (v-structures + Meek rules 1-3) and the SHD against a
+// reference BIF graph, host side.  Mirrors the reference's graph-edit semantics exactly, including
+// the order-dependent details that decide the final DAG/CPDAG:
+//   * OrientVStructure (src/PCStable.cpp:576-668): nodes b ascending, pairs of b's (skeleton)
+//     neighbours in ChoiceGenerator order; conflicting directions are overwritten, and an edit that
+//     would close a cycle is rolled back to the edge it replaced;
+//   * OrientImplied (src/PCStable.cpp:679-703): sweeps over vec_edges by position until a sweep
+//     orients nothing; an oriented edge is erased at its position and re-appended, and a rejected
+//     Direct() re-appends the undirected edge -- the sweep then advances past the element that slid
+//     into the current position (the reference's iterator arithmetic, reproduced);
+//   * Rule3 (src/PCStable.cpp:812-843) indexes nodes by *position* in the common-neighbour set,
+//     not by node id -- reproduced;
+//   * cycle checks: Kahn's algorithm over the directed part (Network::ContainCircle, src/Network.cpp:670);
+//   * SHD (src/BNSLComparison.cpp:12-121): true DAG from BIF (CustomNetwork::LoadBIFFile,
+//     src/CustomNetwork.cpp:49-160) -> Chickering edge ordering + compelled/reversible labelling
+//     (src/Network.cpp:731-869) -> reversible edges undirected -> one error per node pair whose
+//     first matching edge (undirected, x->y, y->x) differs.
+#include <algorithm>
+#include <array>
+#include <cstdio>
+#include <fstream>
+#include <map>
+#include <queue>
+#include <set>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "fbn_internal.h"
+#include "pc_internal.h"
+
+namespace fbn {
+
+namespace {
+
+enum { ARROW = 0, TAIL = 1 };
+
+struct GEdge {
+    int n1, n2, ep1, ep2;
+    bool operator==(const GEdge &o) const { return n1 == o.n1 && n2 == o.n2 && ep1 == o.ep1 && ep2 == o.ep2; }
+    bool directed() const { return (ep1 == ARROW && ep2 == TAIL) || (ep2 == ARROW && ep1 == TAIL); }
+};
+
+GEdge Undirected(int a, int b) { return GEdge{std::min(a, b), std::max(a, b), TAIL, TAIL}; }
+GEdge Directed(int p, int c) { return GEdge{p, c, TAIL, ARROW}; }
+
+// the reference's Network state used by orientation: edge list + parent/child sets
+struct Graph {
+    int n = 0;
+    std::vector<GEdge> edges;
+    std::vector<std::set<int>> parents, children;
+    explicit Graph(int nn) : n(nn), parents(nn), children(nn) {}
+
+    int Find(const GEdge &e) const {
+        auto it = std::find(edges.begin(), edges.end(), e);
+        return it == edges.end() ? -1 : (int)(it - edges.begin());
+    }
+    bool ContainCircle() const {
+        std::vector<int> indeg(n, 0);
+        for (int i = 0; i < n; ++i)
+            for (int c : children[i]) ++indeg[c];
+        std::queue<int> q;
+        for (int i = 0; i < n; ++i)
+            if (!indeg[i]) q.push(i);
+        int visited = 0;
+        while (!q.empty()) {
+            const int u = q.front();
+            q.pop();
+            ++visited;
+            for (int c : children[u])
+                if (--indeg[c] == 0) q.push(c);
+        }
+        return visited != n;
+    }
+    bool AddDirected(int p, int c) {
+        parents[c].insert(p);
+        children[p].insert(c);
+        edges.push_back(Directed(p, c));
+        const bool cyc = ContainCircle();
+        if (cyc) DeleteDirected(p, c);
+        return !cyc;
+    }
+    bool DeleteDirected(int p, int c) {
+        const int pos = Find(Directed(p, c));
+        if (pos < 0) return false;
+        parents[c].erase(p);
+        children[p].erase(c);
+        edges.erase(edges.begin() + pos);
+        return true;
+    }
+    void AddUndirected(int a, int b) { edges.push_back(Undirected(a, b)); }
+    bool DeleteUndirected(int a, int b) {
+        const int pos = Find(Undirected(a, b));
+        if (pos < 0) return false;
+        edges.erase(edges.begin() + pos);
+        return true;
+    }
+    bool IsDirectedFromTo(int a, int b) const { return parents[b].count(a) != 0; }
+    // first matching edge for the SHD: undirected, a->b, b->a
+    int GetEdge(int a, int b) const {
+        int pos = Find(Undirected(a, b));
+        if (pos < 0) pos = Find(Directed(a, b));
+        if (pos < 0) pos = Find(Directed(b, a));
+        return pos;
+    }
+};
+
+struct Orienter {
+    Graph g;
+    std::vector<std::set<int>> adj;  // skeleton adjacencies (fixed during orientation)
+    const std::map<std::pair<int, int>, std::vector<int>> &sepset;
+
+    Orienter(int n, const std::vector<std::pair<int, int>> &skeleton,
+             const std::map<std::pair<int, int>, std::vector<int>> &ss)
+        : g(n), adj(n), sepset(ss) {
+        for (auto &e : skeleton) {
+            g.edges.push_back(Undirected(e.first, e.second));
+            adj[e.first].insert(e.second);
+            adj[e.second].insert(e.first);
+        }
+    }
+    bool IsAdjacentTo(int a, int b) const { return a >= 0 && a < g.n && adj[a].count(b) != 0; }
+    bool IsUndirectedFromTo(int a, int b) const {
+        return IsAdjacentTo(a, b) && !g.IsDirectedFromTo(a, b) && !g.IsDirectedFromTo(b, a);
+    }
+    bool InSepset(int a, int c, int b) const {
+        auto it = sepset.find({a, c});
+        if (it == sepset.end()) return false;
+        return std::find(it->second.begin(), it->second.end(), b) != it->second.end();
+    }
+
+    void VStructures() {
+        for (int b = 0; b < g.n; ++b) {
+            if (adj[b].size() < 2) continue;
+            std::vector<int> nb(adj[b].begin(), adj[b].end());
+            for (size_t i = 0; i < nb.size(); ++i)
+                for (size_t j = i + 1; j < nb.size(); ++j) {  // ChoiceGenerator(k, 2) order
+                    const int a = nb[i], c = nb[j];
+                    if (IsAdjacentTo(a, c) || InSepset(a, c, b)) continue;
+                    const bool dd1 = g.DeleteDirected(b, a);
+                    const bool du1 = dd1 ? false : g.DeleteUndirected(a, b);
+                    const bool add1 = dd1 || du1;
+                    const bool dd2 = g.DeleteDirected(b, c);
+                    const bool du2 = dd2 ? false : g.DeleteUndirected(c, b);
+                    const bool add2 = dd2 || du2;
+                    const bool ok1 = add1 ? g.AddDirected(a, b) : false;
+                    const bool ok2 = add2 ? g.AddDirected(c, b) : false;
+                    if (add1 && !ok1) {
+                        if (dd1) g.AddDirected(b, a);
+                        else g.AddUndirected(a, b);
+                    }
+                    if (add2 && !ok2) {
+                        if (dd2) g.AddDirected(b, c);
+                        else g.AddUndirected(c, b);
+                    }
+                }
+        }
+    }
+    bool Direct(int a, int c) {
+        g.DeleteUndirected(a, c);
+        const bool added = g.AddDirected(a, c);
+        if (!added) g.AddUndirected(a, c);
+        return added;
+    }
+    std::vector<int> Common(int x, int y) const {
+        std::vector<int> r;
+        std::set_intersection(adj[x].begin(), adj[x].end(), adj[y].begin(), adj[y].end(), std::back_inserter(r));
+        return r;
+    }
+    bool Rule1(int b, int c) {
+        const std::set<int> par = g.parents[b];  // node-pointer order == index order
+        for (int a : par) {
+            if (IsAdjacentTo(c, a)) continue;
+            if (Direct(b, c)) return true;
+        }
+        return false;
+    }
+    bool Rule2(int a, int c) {
+        for (int b : Common(a, c))
+            if (g.IsDirectedFromTo(a, b) && g.IsDirectedFromTo(b, c) && Direct(a, c)) return true;
+        return false;
+    }
+    bool Rule3(int d, int a) {
+        const std::vector<int> common = Common(a, d);
+        if (common.size() < 2) return false;
+        // positions in the common set used as node ids, as in the reference
+        for (int b = 0; b < (int)common.size(); ++b)
+            for (int c = b + 1; c < (int)common.size(); ++c)
+                if (!IsAdjacentTo(b, c) && IsUndirectedFromTo(d, b) && IsUndirectedFromTo(d, c) &&
+                    g.IsDirectedFromTo(b, a) && g.IsDirectedFromTo(c, a) && Direct(d, a))
+                    return true;
+        return false;
+    }
+    void Implied() {
+        bool oriented = true;
+        while (oriented) {
+            oriented = false;
+            for (size_t i = 0; i < g.edges.size();) {
+                const int x = g.edges[i].n1, y = g.edges[i].n2;
+                if (IsUndirectedFromTo(x, y)) {
+                    if (Rule1(x, y) || Rule1(y, x) || Rule2(x, y) || Rule2(y, x) || Rule3(x, y) || Rule3(y, x))
+                        oriented = true;  // edge at i erased: i now holds the next one
+                    else
+                        ++i;
+                } else {
+                    ++i;
+                }
+            }
+        }
+    }
+};
+
+std::string Trim(const std::string &s) {
+    size_t a = s.find_first_not_of(" \t\r\n"), b = s.find_last_not_of(" \t\r\n");
+    return a == std::string::npos ? std::string() : s.substr(a, b - a + 1);
+}
+
+}  // namespace
+
+int OrientPC(int nvars, PCResultHost &r) {
+    Orienter o(nvars, r.edges, r.sepset);
+    o.VStructures();
+    o.Implied();
+    r.oriented.clear();
+    for (auto &e : o.g.edges) {
+        if (!e.directed()) r.oriented.push_back({e.n1, e.n2, 0});
+        else if (e.ep1 == TAIL) r.oriented.push_back({e.n1, e.n2, 1});
+        else r.oriented.push_back({e.n2, e.n1, 1});
+    }
+    r.num_nodes = nvars;
+    return FBN_OK;
+}
+
+// true DAG from a BIF file: node ids in `variable` declaration order, arcs from `probability` lines
+int LoadBifGraph(const std::string &path, std::vector<std::string> &names, std::vector<std::pair<int, int>> &arcs) {
+    std::ifstream in(path);
+    if (!in) return SetError(FBN_ERR_IO, "cannot open %s", path.c_str());
+    std::map<std::string, int> id;
+    std::string line;
+    names.clear();
+    arcs.clear();
+    while (std::getline(in, line)) {
+        line = Trim(line);
+        if (line.compare(0, 9, "variable ") == 0) {
+            std::istringstream ss(line.substr(9));
+            std::string name;
+            ss >> name;
+            id[name] = (int)names.size();
+            names.push_back(name);
+        } else if (line.compare(0, 11, "probability") == 0) {
+            const size_t lp = line.find('('), rp = line.find(')');
+            if (lp == std::string::npos || rp == std::string::npos) return SetError(FBN_ERR_IO, "%s: bad line '%s'", path.c_str(), line.c_str());
+            std::string inner = line.substr(lp + 1, rp - lp - 1);
+            const size_t bar = inner.find('|');
+            const std::string child = Trim(inner.substr(0, bar));
+            if (!id.count(child)) return SetError(FBN_ERR_IO, "%s: unknown variable %s", path.c_str(), child.c_str());
+            if (bar == std::string::npos) continue;
+            std::string rest = inner.substr(bar + 1);
+            std::istringstream ps(rest);
+            std::string tok;
+            while (std::getline(ps, tok, ',')) {
+                const std::string p = Trim(tok);
+                if (p.empty()) continue;
+                if (!id.count(p)) return SetError(FBN_ERR_IO, "%s: unknown variable %s", path.c_str(), p.c_str());
+                arcs.push_back({id[p], id[child]});
+            }
+        }
+    }
+    if (names.empty()) return SetError(FBN_ERR_IO, "%s: no variables", path.c_str());
+    return FBN_OK;
+}
+
+// SHD between the learned (oriented) graph and the CPDAG of a true DAG
+int ComputeSHD(int n, const std::vector<std::pair<int, int>> &arcs, const std::vector<std::array<int, 3>> &learned,
+               int *shd, int *unlabelled) {
+    int r_unlabelled = 0;
+    Graph t(n);
+    for (auto &a : arcs) {
+        t.parents[a.second].insert(a.first);
+        t.children[a.first].insert(a.second);
+        t.edges.push_back(Directed(a.first, a.second));
+    }
+    if (t.ContainCircle()) return SetError(FBN_ERR_ARG, "true graph is not a DAG");
+    // topological order: Kahn, queue, children scanned by ascending index (TopoSortOfDAGZeroInDegreeFirst)
+    std::vector<int> indeg(n, 0), topo;
+    for (int i = 0; i < n; ++i)
+        for (int c : t.children[i]) ++indeg[c];
+    std::queue<int> q;
+    for (int i = 0; i < n; ++i)
+        if (!indeg[i]) q.push(i);
+    while (!q.empty()) {
+        const int u = q.front();
+        q.pop();
+        topo.push_back(u);
+        for (int c : t.children[u])
+            if (--indeg[c] == 0) q.push(c);
+    }
+    // OrderEdge: for y in topo order, parents x from the highest-ordered down
+    std::vector<GEdge> order;
+    std::vector<bool> ordered(t.edges.size(), false);
+    for (size_t j = 0; j < topo.size(); ++j) {
+        const int y = topo[j];
+        for (int k = (int)j - 1; k >= 0; --k) {
+            const int x = topo[k];
+            if (!t.parents[y].count(x)) continue;
+            const int pos = t.Find(Directed(x, y));
+            if (!ordered[pos]) ordered[pos] = true, order.push_back(t.edges[pos]);
+        }
+    }
+    if (order.size() != t.edges.size()) return SetError(FBN_ERR_ARG, "true graph has duplicate arcs");
+    // FindCompelled (Chickering 1995)
+    enum { UNKNOWN = 0, COMPELLED = 1, REVERSIBLE = 2 };
+    std::vector<int> label(t.edges.size(), UNKNOWN);
+    auto in_order = [&](int p, int c) {
+        auto it = std::find(order.begin(), order.end(), Directed(p, c));
+        return it == order.end() ? -1 : (int)(it - order.begin());
+    };
+    auto lab = [&](int p, int c) -> int & { return label[t.Find(Directed(p, c))]; };
+    while (!order.empty()) {
+        const int x = order[0].n1, y = order[0].n2;
+        bool done = false;
+        for (int w : t.parents[x]) {
+            if (lab(w, x) != COMPELLED) continue;
+            if (!t.parents[y].count(w)) {
+                done = true;
+                lab(x, y) = COMPELLED;
+                order.erase(order.begin());
+                for (int py : t.parents[y]) {
+                    const int po = in_order(py, y);
+                    lab(py, y) = COMPELLED;
+                    if (po >= 0) order.erase(order.begin() + po);
+                }
+                break;
+            } else {
+                const int po = in_order(w, y);
+                if (po >= 0) lab(w, y) = COMPELLED, order.erase(order.begin() + po);
+            }
+        }
+        if (done) continue;
+        bool found = false;
+        const std::set<int> py_set = t.parents[y];
+        for (int z : py_set) {
+            if (z == x || t.parents[x].count(z)) continue;
+            // as in the reference (src/Network.cpp:828-845): x->y is labelled and the *front* of the
+            // order is erased on every hit; a second hit drops an unrelated edge unlabelled
+            if (found && !order.empty()) ++r_unlabelled;
+            found = true;
+            lab(x, y) = COMPELLED;
+            if (!order.empty()) order.erase(order.begin());
+            for (int py : t.parents[y]) {
+                const int po = in_order(py, y);
+                if (po >= 0) lab(py, y) = COMPELLED, order.erase(order.begin() + po);
+            }
+        }
+        if (!found) {
+            lab(x, y) = REVERSIBLE;
+            order.erase(order.begin());
+            for (int py : t.parents[y]) {
+                const int po = in_order(py, y);
+                if (po >= 0) lab(py, y) = REVERSIBLE, order.erase(order.begin() + po);
+            }
+        }
+    }
+    for (size_t i = 0; i < t.edges.size(); ++i)
+        if (label[i] == REVERSIBLE) t.edges[i] = Undirected(t.edges[i].n1, t.edges[i].n2);
+    Graph l(n);
+    for (auto &e : learned) l.edges.push_back(e[2] ? Directed(e[0], e[1]) : Undirected(e[0], e[1]));
+    int err = 0;
+    for (int a = 0; a < n; ++a)
+        for (int b = a + 1; b < n; ++b) {
+            const int p1 = t.GetEdge(a, b), p2 = l.GetEdge(a, b);
+            if (p1 < 0 && p2 < 0) continue;
+            if (p1 >= 0 && p2 >= 0 && t.edges[p1] == l.edges[p2]) continue;
+            ++err;
+        }
+    *shd = err;
+    if (unlabelled) *unlabelled = r_unlabelled;
+    return FBN_OK;
+}
+
+}  // namespace fbn

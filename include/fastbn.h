@@ -165,6 +165,20 @@ int fbn_pc_num_edges(const fbn_pc_result *r, int *n);
 int fbn_pc_edges(const fbn_pc_result *r, int32_t *pairs /* [n][2], vec_edges order */);
 /* sepsets flattened as (x, y, k, z_0..z_{k-1})*, key x < y; returns total int count in *len */
 int fbn_pc_sepsets(const fbn_pc_result *r, int32_t *buf, int64_t cap, int64_t *len);
+/* After the skeleton, fbn_pc_stable orients like StructLearnByPCStable steps 2-3
+ * (OrientVStructure / OrientImplied, src/PCStable.cpp:576-843): triples [n][3] =
+ * (from, to, 1) for arcs, (min, max, 0) for undirected edges, in the reference's vec_edges order. */
+/* Host-only: orient a given skeleton (pairs [nedges][2] in vec_edges order) with its sepsets
+ * (records (x, y, m, z_0..z_{m-1}) as fbn_pc_sepsets writes them) into a new result. */
+int fbn_pc_orient_skeleton(int nvars, const int32_t *pairs, int nedges, const int32_t *sepsets, int64_t len,
+                           fbn_pc_result **out);
+int fbn_pc_num_oriented_edges(const fbn_pc_result *r, int *n);
+int fbn_pc_oriented_edges(const fbn_pc_result *r, int32_t *triples);
+/* SHD against the CPDAG of the DAG in a BIF file (BNSLComparison::GetSHD, src/BNSLComparison.cpp:12-121,
+ * true graph via CustomNetwork::LoadBIFFile, src/CustomNetwork.cpp:49-160). */
+int fbn_pc_shd_bif(const fbn_pc_result *r, const char *bif_path, int *shd);
+/* Same for any learned graph given as triples [n][3] (from, to, 1) / (a, b, 0). */
+int fbn_shd_bif(const char *bif_path, int nvars, const int32_t *triples, int n, int *shd);
 int fbn_pc_timing(const fbn_pc_result *r, double *total_s, double *kernel_s);
 int fbn_pc_result_destroy(fbn_pc_result *r);
 

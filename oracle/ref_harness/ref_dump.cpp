@@ -24,6 +24,7 @@
 #include <string>
 #include <vector>
 
+#include "BNSLComparison.h"
 #include "CellTable.h"
 #include "Dataset.h"
 #include "DiscreteNode.h"
@@ -290,7 +291,83 @@ static int RunJTBench(int argc, char **argv) {
     return 0;
 }
 
+// ---------------------------------------------------------------------------------------------
+// shd <bif> <learned>: the reference's own BNSLComparison::GetSHD (src/BNSLComparison.cpp:12-121).
+// The true DAG is built from the BIF through the public Network API in CustomNetwork::LoadBIFFile's
+// order (variables in declaration order, arcs per `probability` line, parents as listed) -- that
+// loader itself needs tinyxml2 and is not compiled; <learned> lines are "from to directed".
+static Network *NewNet(int n) {
+    auto *net = new Network(true);
+    for (int i = 0; i < n; ++i) {
+        auto *node = new DiscreteNode(i);
+        net->map_idx_node_ptr[i] = node;
+    }
+    net->num_nodes = n;
+    return net;
+}
+
+static int RunSHD(int argc, char **argv) {
+    if (argc < 4) return 2;
+    std::ifstream bif(argv[2]);
+    std::map<std::string, int> id;
+    std::vector<std::pair<int, int>> arcs;
+    std::string line;
+    auto trim = [](std::string t) {
+        size_t a = t.find_first_not_of(" \t\r"), b = t.find_last_not_of(" \t\r,");
+        return a == std::string::npos ? std::string() : t.substr(a, b - a + 1);
+    };
+    while (std::getline(bif, line)) {
+        line = trim(line);
+        if (line.rfind("variable ", 0) == 0) {
+            std::string name = line.substr(9);
+            name = name.substr(0, name.find(' '));
+            int k = (int)id.size();
+            id[name] = k;
+        } else if (line.rfind("probability", 0) == 0) {
+            std::string in = line.substr(line.find('(') + 1);
+            in = in.substr(0, in.find(')'));
+            size_t bar = in.find('|');
+            std::string child = trim(in.substr(0, bar));
+            if (bar == std::string::npos) continue;
+            std::string rest = in.substr(bar + 1);
+            size_t pos = 0;
+            while (pos < rest.size()) {
+                size_t q = rest.find(',', pos);
+                if (q == std::string::npos) q = rest.size();
+                std::string p = trim(rest.substr(pos, q - pos));
+                if (!p.empty()) arcs.push_back({id.at(p), id.at(child)});
+                pos = q + 1;
+            }
+        }
+    }
+    const int n = (int)id.size();
+    Network *truth = NewNet(n), *learned = NewNet(n);
+    for (auto &a : arcs) {
+        truth->SetParentChild(a.first, a.second);
+        truth->vec_edges.push_back(Edge(truth->FindNodePtrByIndex(a.first), truth->FindNodePtrByIndex(a.second), TAIL, ARROW));
+        ++truth->num_edges;
+    }
+    std::ifstream le(argv[3]);
+    int a, b, d;
+    while (le >> a >> b >> d) {
+        if (d) {
+            learned->SetParentChild(a, b);
+            learned->vec_edges.push_back(Edge(learned->FindNodePtrByIndex(a), learned->FindNodePtrByIndex(b), TAIL, ARROW));
+        } else {
+            learned->vec_edges.push_back(Edge(learned->FindNodePtrByIndex(a), learned->FindNodePtrByIndex(b)));
+        }
+        ++learned->num_edges;
+    }
+    std::streambuf *old = std::cout.rdbuf(nullptr);
+    BNSLComparison comp(truth, learned);
+    int shd = comp.GetSHD();
+    std::cout.rdbuf(old);
+    printf("SHD %d\n", shd);
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc >= 2 && std::string(argv[1]) == "shd") return RunSHD(argc, argv);
     if (argc >= 2 && std::string(argv[1]) == "jtbench") return RunJTBench(argc, argv);
     if (argc >= 2 && std::string(argv[1]) == "jt") return RunJT(argc, argv);
     if (argc >= 2 && std::string(argv[1]) == "ci") return RunCI(argc, argv);

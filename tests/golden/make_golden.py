@@ -12,6 +12,9 @@ TEST INFRASTRUCTURE -- runs only in the build container, where /root/reference e
        alarm_1k.marg.gz           per-case label + marginals for the 1000 shipped test cases
        alarm_rand.marg.gz         the same for the synthetic evidence set
        alarm_s5000.ci.gz          reference Counts2D/Counts3D tables for the CI test list
+       alarm_shd.json             reference BNSLComparison::GetSHD for seeded learned graphs
+                                  (perturbations of ALARM's DAG: undirected / reversed / dropped /
+                                  added edges) against alarm.bif
 No reference source text is copied; only data files and the reference's outputs.
 """
 import gzip
@@ -97,6 +100,43 @@ def main():
     run([ref_dump, "ci", os.path.join(OUT, "alarm_s5000.txt"), tfile, ci])
     gz(ci, ci + ".gz")
     os.remove(tfile)
+
+    # 4) SHD: seeded learned graphs scored by the reference's own GetSHD
+    import json
+    names, arcs = [], []
+    for line in open(os.path.join(OUT, "alarm.bif")):
+        t = line.strip()
+        if t.startswith("variable "):
+            names.append(t.split()[1])
+        elif t.startswith("probability") and "|" in t:
+            inner = t[t.index("(") + 1:t.index(")")]
+            child, parents = inner.split("|")
+            for p in parents.split(","):
+                arcs.append((names.index(p.strip()), names.index(child.strip())))
+    cases = []
+    lfile = os.path.join(HERE, "learned.tmp")
+    for k in range(40):
+        g = {}
+        for a, b in arcs:
+            u = rng.random()
+            if u < 0.1:
+                continue  # dropped
+            g[(min(a, b), max(a, b))] = (b, a, 1) if u < 0.25 else (min(a, b), max(a, b), 0) if u < 0.5 else (a, b, 1)
+        for _ in range(rng.randint(0, 6)):  # spurious edges
+            a, b = sorted(rng.sample(range(37), 2))
+            if (a, b) not in g:
+                g[(a, b)] = (a, b, 0) if rng.random() < 0.5 else ((a, b, 1) if rng.random() < 0.5 else (b, a, 1))
+        edges = list(g.values())
+        rng.shuffle(edges)
+        with open(lfile, "w") as f:
+            for e in edges:
+                f.write("%d %d %d\n" % e)
+        out = subprocess.run([ref_dump, "shd", os.path.join(OUT, "alarm.bif"), lfile], check=True,
+                             capture_output=True, text=True).stdout
+        cases.append({"edges": edges, "shd": int(out.split()[1])})
+    os.remove(lfile)
+    with open(os.path.join(HERE, "alarm_shd.json"), "w") as f:
+        json.dump(cases, f, separators=(",", ":"))
     print("fixtures written to", HERE)
 
 

@@ -53,6 +53,10 @@ def test_pc_stable_alarm5000(alarm_ds, alarm_paths, gs):
     assert pc.sepset == ref["sepset"]
     if gs == 1:
         assert pc.num_ci_test == 5206 and len(pc.edges) == 44
+        # orientation (host) on the device skeleton: restatement edge for edge, SHD known answer
+        import orient
+        assert pc.oriented == orient.orient(37, pc.edges, pc.sepset)
+        assert pc.GetSHD(alarm_paths["bif"]) == 5
 
 
 def test_pc_stable_synthetic_and_ragged_samples(tmp_path):
@@ -67,6 +71,8 @@ def test_pc_stable_synthetic_and_ragged_samples(tmp_path):
     pc = F.PCStable(0.05, 1000).StructLearnCompData(ds)
     assert pc.tests_per_level.tolist() == ref["tests_per_level"]
     assert pc.edges == ref["edges"] and pc.sepset == ref["sepset"]
+    import orient
+    assert pc.oriented == orient.orient(40, pc.edges, pc.sepset)
 
 
 def test_constant_column_df0(tmp_path):

@@ -105,3 +105,42 @@ def test_errors_are_reported_not_fatal(tmp_path):
         F.Network(str(bad))
     with pytest.raises(F.FastBNError, match="cannot open"):
         F.Dataset(str(tmp_path / "missing.csv"))
+
+
+# ---------------------------------------------------------------- PC orientation + SHD (host side)
+def test_shd_matches_reference_fixture(alarm_paths):
+    """fbn_shd_bif vs the reference's own BNSLComparison::GetSHD on 40 seeded learned graphs."""
+    import json
+    cases = json.load(open(os.path.join(GOLD, "alarm_shd.json")))
+    bif = os.path.join(GOLD, "alarm", "alarm.bif")
+    for c in cases:
+        assert F.shd_bif(bif, 37, [tuple(e) for e in c["edges"]]) == c["shd"]
+
+
+def test_orientation_alarm_known_answer():
+    """PC-stable on alarm_s5000 (oracle skeleton): orientation == restatement, SHD == 5."""
+    import oracle as O
+    import orient
+    od = O.OracleDataset(csv=os.path.join(GOLD, "alarm", "alarm_s5000.txt"))
+    r = od.pc_stable(0.05, 1000, 1)
+    res = F.orient_skeleton(37, r["edges"], r["sepset"])
+    assert res.oriented == orient.orient(37, r["edges"], {k: tuple(v) for k, v in r["sepset"].items()})
+    assert res.GetSHD(os.path.join(GOLD, "alarm", "alarm.bif")) == 5
+
+
+def test_orientation_random_skeletons():
+    """Random skeletons and sepsets (cycles, conflicting v-structures, Rule 3's position indexing)."""
+    import random
+    import orient
+    rng = random.Random(7)
+    for trial in range(60):
+        n = rng.randint(4, 14)
+        pairs = [(a, b) for a in range(n) for b in range(a + 1, n)]
+        edges = [p for p in pairs if rng.random() < 0.35]
+        sep = {}
+        for p in pairs:
+            if p not in edges:
+                others = [v for v in range(n) if v not in p]
+                sep[p] = tuple(sorted(rng.sample(others, rng.randint(0, min(3, len(others))))))
+        res = F.orient_skeleton(n, edges, sep)
+        assert res.oriented == orient.orient(n, edges, sep), trial
