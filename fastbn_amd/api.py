@@ -413,7 +413,9 @@ class PCStable:
         self.result = None
 
     def StructLearnCompData(self, dataset, group_size=1, num_threads=1, print_struct=False, verbose=False):
-        ci = IndependenceTest(dataset, self.alpha, self.device)
+        """`dataset`: a Dataset (uploaded for this call) or an IndependenceTest whose column store is
+        already resident on the device (reused across calls)."""
+        ci = dataset if isinstance(dataset, IndependenceTest) else IndependenceTest(dataset, self.alpha, self.device)
         r = C.c_void_p()
         lib.fbn_pc_stable(ci._h, self.alpha, self.depth, group_size, C.byref(r))
         self.result = PCResult(r)

@@ -126,12 +126,31 @@ struct fbn_ci_ctx {
     std::vector<int32_t> dims;
     DevBuf cols, ddims, items, g2, df, p, indep, counts;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipStream_t stream = nullptr;  // the PC driver's rounds (pinned staging, one sync per round)
     float last_ms = 0.f;
+    // pinned host staging for the driver's batches
+    void *h_items = nullptr, *h_res = nullptr;
+    size_t h_items_bytes = 0, h_res_bytes = 0;
     ~fbn_ci_ctx() {
+        if (h_items) (void)hipHostFree(h_items);
+        if (h_res) (void)hipHostFree(h_res);
+        if (stream) (void)hipStreamDestroy(stream);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
     }
 };
+
+static int PinnedEnsure(void *&ptr, size_t &have, size_t want) {
+    if (want <= have) return FBN_OK;
+    if (ptr) (void)hipHostFree(ptr);
+    ptr = nullptr;
+    have = 0;
+    want = std::max<size_t>(want, 1 << 16) * 2;
+    hipError_t e = hipHostMalloc(&ptr, want, hipHostMallocDefault);
+    if (e != hipSuccess) return SetError(FBN_ERR_NOMEM, "hipHostMalloc(%zu): %s", want, hipGetErrorString(e));
+    have = want;
+    return FBN_OK;
+}
 
 struct fbn_pc_result {
     fbn::PCResultHost r;
@@ -675,6 +694,7 @@ int fbn_ci_dataset_upload(const uint8_t *cols, int nvars, int64_t nsamples, cons
     FBN_HIP(hipMemcpy(c->ddims.p, dims, (size_t)nvars * 4, hipMemcpyHostToDevice));
     FBN_HIP(hipEventCreate(&c->ev0));
     FBN_HIP(hipEventCreate(&c->ev1));
+    FBN_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     *out = c.release();
     return FBN_OK;
 }
@@ -895,11 +915,21 @@ void CiCtxShape(const fbn_ci_ctx *c, int *nvars, int64_t *nsamples) {
 int CiRunBatch(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alpha, uint8_t *indep, int32_t *df,
                PCResultHost &res) {
     if (n == 0) return FBN_OK;
-    int rc = CiLaunchDevice(c, items, n, d, alpha, false, nullptr, nullptr);
+    // pinned staging: the copies are true DMA on the ctx stream, one host sync per round
+    const size_t ib = (size_t)n * (2 + d) * 4, rb = (size_t)n * 5 + 8;
+    int rc;
+    if ((rc = PinnedEnsure(c->h_items, c->h_items_bytes, ib))) return rc;
+    if ((rc = PinnedEnsure(c->h_res, c->h_res_bytes, rb))) return rc;
+    memcpy(c->h_items, items, ib);
+    rc = CiLaunchDevice(c, static_cast<const int32_t *>(c->h_items), n, d, alpha, false, nullptr, c->stream);
     if (rc) return rc;
-    FBN_HIP(hipMemcpyAsync(indep, c->indep.p, (size_t)n, hipMemcpyDeviceToHost, nullptr));
-    if (df) FBN_HIP(hipMemcpyAsync(df, c->df.p, (size_t)n * 4, hipMemcpyDeviceToHost, nullptr));
-    FBN_HIP(hipStreamSynchronize(nullptr));
+    uint8_t *h_ind = static_cast<uint8_t *>(c->h_res);
+    int32_t *h_df = reinterpret_cast<int32_t *>(h_ind + (((size_t)n + 3) & ~(size_t)3));
+    FBN_HIP(hipMemcpyAsync(h_ind, c->indep.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    if (df) FBN_HIP(hipMemcpyAsync(h_df, c->df.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    FBN_HIP(hipStreamSynchronize(c->stream));
+    memcpy(indep, h_ind, (size_t)n);
+    if (df) memcpy(df, h_df, (size_t)n * 4);
     float ms = 0.f;
     FBN_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     res.kernel_s += ms * 1e-3;

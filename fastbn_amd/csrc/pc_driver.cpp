@@ -10,8 +10,9 @@
 //   * removals are applied after the level in vec_edges order; the search continues while
 //     FreeDegree > d.
 // Instead of the reference's 128-edge work pool, every unresolved edge contributes its next
-// chunk of candidate sets to one device batch per round (chunk 32 -> 128 -> 512 ... sets), and the
-// host resolves each edge's prefix in order.  Tests beyond an edge's first independent set are
+// chunk of candidate sets to one device batch per round (first chunk sized so one round holds
+// ~8k tests, at most 32 per edge; then x4 per round), and the host resolves each edge's prefix in
+// order.  Tests beyond an edge's first independent set are
 // speculative: they are run but not counted, so the reported counts equal the reference's.
 #include <algorithm>
 #include <chrono>
@@ -141,7 +142,11 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
             if (!st[e].has_next) st[e].resolved = true;  // both sides too small: kept
         }
         int64_t counted = 0, launched = 0;
-        int64_t chunk = 32;
+        // first round: enough tests to fill the device (~8k) without speculating deep into edges
+        // that usually resolve early; later rounds grow 4x per round
+        int64_t open_edges = 0;
+        for (auto &s : st) open_edges += !s.resolved;
+        int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(32, 8192 / std::max<int64_t>(1, open_edges)));
         std::vector<Pending> pend;
         while (true) {
             items.clear();
