@@ -1,9 +1,10 @@
 // ci_kernels.hip -- batched G^2 conditional-independence tests on gfx950.
 //
 // One 256-thread workgroup per test (grid-stride over the batch).  The column store is uint8
-// [var][sample]; each thread streams 4 samples per load (one dword per column) and bins them into
-// the contingency table N[z][x][y] held in LDS with LDS atomics (small tables are first reduced
-// inside the wave with ballots, which avoids 64-way same-address conflicts).  Marginals, the
+// [var][sample]; each thread streams 4 samples per load (one dword per column).  Tables of <= 16
+// cells are counted in per-lane packed 16-bit counters held in registers (4 x u64, no LDS traffic
+// in the sample loop) and wave-reduced once per test; larger tables N[z][x][y] use per-wave LDS
+// sub-histograms (LDS atomics without cross-wave contention), merged once per test.  Marginals, the
 // adjusted degrees of freedom and the G^2 terms are then evaluated per z-configuration by
 // parallel threads, summed in z order, and one lane evaluates p = Q(df/2, G^2/2).
 //
@@ -80,15 +81,25 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
         }
         const int dxy = dx * dy;
         const int cells = dimz * dxy;
+        // small tables (<= 16 cells): per-lane packed 16-bit counters in registers, no LDS traffic
+        // in the sample loop; larger tables: per-wave LDS sub-histograms (no cross-wave contention)
+        const bool packed = cells <= 16 && A.N <= (1ll << 24);
+        const int nsub = (cells > 16 && cells * 16 <= 64 * 1024) ? 4 : 1;  // = fbn_ci_lds_bytes
+        // LDS layout (ints): hist[cells] | sub[nsub][cells] | ni | nj | nk | dfp | (even) part[dimz] f64
         int32_t *hist = smem;
-        int32_t *ni = hist + cells;
+        int32_t *sub = hist + ((cells + 3) & ~3);
+        int32_t *ni = sub + (nsub > 1 ? nsub * cells : 0);
         int32_t *nj = ni + dimz * dx;
         int32_t *nk = nj + dimz * dy;
         int32_t *dfp = nk + dimz;
-        double *part = reinterpret_cast<double *>(smem + ((cells + dimz * (dx + dy + 2) + 1) & ~1));
+        const int part_off = (int)((dfp + dimz) - smem + 1) & ~1;
+        double *part = reinterpret_cast<double *>(smem + part_off);
 
         for (int c = tid; c < cells; c += 256) hist[c] = 0;
+        if (nsub > 1)
+            for (int c = tid; c < nsub * cells; c += 256) sub[c] = 0;
         __syncthreads();
+        int32_t *myhist = nsub > 1 ? sub + (tid >> 6) * cells : hist;
 
         const uint8_t *cx = A.cols + (size_t)x * A.N;
         const uint8_t *cy = A.cols + (size_t)y * A.N;
@@ -96,20 +107,17 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
 #pragma unroll
         for (int j = 0; j < D; ++j) cz[j] = A.cols + (size_t)zv[j] * A.N;
 
-        const bool small = cells <= 32;
+        unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;  // cell c: a[c >> 2] bits [16 (c & 3), +16)
         auto bin = [&](int cell, bool valid) {
-            if (small) {
-                // wave-aggregated: one LDS add per distinct cell present in the wave
-                unsigned long long todo = __ballot(valid);
-                while (todo) {
-                    const int leader = __ffsll(todo) - 1;
-                    const int lc = __shfl(cell, leader);
-                    const unsigned long long same = __ballot(valid && cell == lc);
-                    if (lane == leader) atomicAdd(&hist[lc], __popcll(same));
-                    todo &= ~same;
-                }
+            if (packed) {
+                const unsigned long long inc = valid ? (1ull << ((cell & 3) << 4)) : 0ull;
+                const int q = cell >> 2;
+                a0 += q == 0 ? inc : 0ull;
+                a1 += q == 1 ? inc : 0ull;
+                a2 += q == 2 ? inc : 0ull;
+                a3 += q == 3 ? inc : 0ull;
             } else if (valid) {
-                atomicAdd(&hist[cell], 1);
+                atomicAdd(&myhist[cell], 1);
             }
         };
         const long long N4 = (A.N % 4 == 0) ? A.N / 4 : 0;
@@ -142,7 +150,24 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
             }
             bin(cell, v);
         }
+        if (packed) {  // wave reduction of the packed counters, one LDS add per cell per wave
+            for (int c = 0; c < cells; ++c) {
+                const unsigned long long w = (c >> 2) == 0 ? a0 : (c >> 2) == 1 ? a1 : (c >> 2) == 2 ? a2 : a3;
+                int v = (int)((w >> ((c & 3) << 4)) & 0xFFFFull);
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+                if (lane == 0 && v) atomicAdd(&hist[c], v);
+            }
+        }
         __syncthreads();
+        if (nsub > 1) {
+            for (int c = tid; c < cells; c += 256) {
+                int v = 0;
+                for (int w = 0; w < nsub; ++w) v += sub[w * cells + c];
+                hist[c] = v;
+            }
+            __syncthreads();
+        }
         if (A.counts && it == 0)
             for (int c = tid; c < cells; c += 256) A.counts[c] = hist[c];
 
@@ -212,7 +237,10 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
 
 // LDS bytes needed for a test with `cells` = dimz*dx*dy
 extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy) {
-    size_t ints = (size_t)dimz * dx * dy + (size_t)dimz * (dx + dy + 2) + 1;
+    // must match the kernel's layout
+    const size_t cells = (size_t)dimz * dx * dy;
+    const size_t nsub = (cells > 16 && cells * 16 <= 64 * 1024) ? 4 : 0;
+    size_t ints = ((cells + 3) & ~(size_t)3) + nsub * cells + (size_t)dimz * (dx + dy + 2);
     ints = (ints + 1) & ~(size_t)1;
     return ints * 4 + (size_t)dimz * 8;
 }

@@ -98,19 +98,17 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
     std::vector<uint8_t> indep;
     std::vector<int32_t> dfv;
 
+    // removals after a level, in vec_edges order (src/PCStable.cpp:310-326); the adjacency lists
+    // are rebuilt from the kept edges in O(E) (edges stay in (i < j) lexicographic order, so every
+    // list comes out sorted) instead of erasing element by element (the reference's O(E^2) hot spot)
     auto apply_removals = [&](const std::vector<char> &rm) {
         std::vector<std::pair<int, int>> keep;
         keep.reserve(edges.size());
-        for (size_t e = 0; e < edges.size(); ++e) {
-            if (!rm[e]) {
-                keep.push_back(edges[e]);
-                continue;
-            }
-            auto &ax = adj[edges[e].first], &ay = adj[edges[e].second];
-            ax.erase(std::lower_bound(ax.begin(), ax.end(), edges[e].second));
-            ay.erase(std::lower_bound(ay.begin(), ay.end(), edges[e].first));
-        }
+        for (size_t e = 0; e < edges.size(); ++e)
+            if (!rm[e]) keep.push_back(edges[e]);
         edges.swap(keep);
+        for (auto &a : adj) a.clear();
+        for (auto &e : edges) adj[e.first].push_back(e.second), adj[e.second].push_back(e.first);
     };
 
     // ---- level 0 (src/PCStable.cpp:73-157)
