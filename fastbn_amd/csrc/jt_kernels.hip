@@ -35,6 +35,97 @@ struct JtArgs {
 
 #define AT(e) S[(size_t)(e) * 64]
 
+// Division by the pending denominator.  Markstein: with y = RN(1/den) and q = RN(x*y) within one
+// ulp of x/den, q + RN(x - den*q)*y (two fmas) is the correctly rounded quotient -- the same bits as
+// the reference's `potentials[i] /= denominator` -- as long as nothing under/overflows.  The fast form
+// is used when den lies in [2^-600, 2^600] for every lane of the wave (then any table value >= 2^-400
+// keeps every intermediate normal); otherwise the op runs with the IEEE division sequence.
+struct Den {
+    double den, y;
+};
+template <bool EXACT>
+__device__ __forceinline__ double dv(double x, const Den &d) {
+    if (EXACT) return x / d.den;
+    const double q = x * d.y;
+    const double r = __builtin_fma(-d.den, q, x);
+    return __builtin_fma(r, d.y, q);
+}
+__device__ __forceinline__ bool den_fast_all(double den) {
+    return __ballot(!(den >= 0x1p-600 && den <= 0x1p+600)) == 0ull;
+}
+
+
+
+#ifndef FBN_G_UNROLL
+#define FBN_G_UNROLL 8
+#endif
+// global-variant op bodies, instantiated for the fast (Markstein) and the exact division
+template <bool EXACT>
+__device__ __forceinline__ void g_sepcol(double *__restrict__ S, const JtOp &op, const Den &D) {
+    const int Ts = op.b, Q = op.d / op.b;
+    for (int j = 0; j < Ts; ++j) {
+        double acc = 0.0;
+#pragma unroll FBN_G_UNROLL
+        for (int q = 0; q < Q; ++q) acc += dv<EXACT>(AT(op.c + q * Ts + j), D);
+        const double old = AT(op.a + j);
+        AT(op.a + j) = (old == 0.0) ? 0.0 : acc / old;
+    }
+}
+template <bool EXACT>
+__device__ __forceinline__ double g_clqmul(double *__restrict__ S, const JtOp &op, const int32_t *__restrict__ mp,
+                                           const Den &D) {
+    double sum = 0.0;
+#pragma unroll FBN_G_UNROLL
+    for (int e = 0; e < op.b; ++e) {
+        const double v = dv<EXACT>(AT(op.a + e), D) * AT(op.d + mp[e]);
+        AT(op.a + e) = v;
+        sum += v;
+    }
+    return sum;
+}
+template <bool EXACT>
+__device__ __forceinline__ void g_sepdis(double *__restrict__ S, const JtOp &op, const int32_t *__restrict__ ls,
+                                         const Den &D) {
+    const int per = op.f;
+    for (int j = 0; j < op.b; ++j) {
+        double acc = 0.0;
+#pragma unroll FBN_G_UNROLL
+        for (int q = 0; q < per; ++q) acc += dv<EXACT>(AT(op.c + ls[j * per + q]), D);
+        const double old = AT(op.a + j);
+        AT(op.a + j) = (old == 0.0) ? 0.0 : acc / old;
+    }
+}
+template <bool EXACT>
+__device__ __forceinline__ double g_clqdis(double *__restrict__ S, const JtOp &op, const Den &D) {
+    const int Ts = op.e, Q = op.b / op.e;
+    double sum = 0.0;
+    for (int q = 0; q < Q; ++q) {
+#pragma unroll FBN_G_UNROLL
+        for (int j = 0; j < Ts; ++j) {
+            const int e = q * Ts + j;
+            const double v = dv<EXACT>(AT(op.a + e), D) * AT(op.d + j);
+            AT(op.a + e) = v;
+            sum += v;
+        }
+    }
+    return sum;
+}
+template <bool EXACT>
+__device__ __forceinline__ double g_marg(double *__restrict__ S, int toff, int dim, int cum, int T, const Den &D,
+                                         double *__restrict__ o, bool act) {
+    const int bw = dim * cum, nhi = T / bw;
+    double tot = 0.0;
+    for (int d = 0; d < dim; ++d) {
+        double acc = 0.0;
+        for (int hi = 0; hi < nhi; ++hi)
+#pragma unroll FBN_G_UNROLL
+            for (int lo = 0; lo < cum; ++lo) acc += dv<EXACT>(AT(toff + hi * bw + d * cum + lo), D);
+        if (act) o[d] = acc;
+        tot += acc;
+    }
+    return tot;
+}
+
 __global__ __launch_bounds__(64) void jt_interp_kernel(JtArgs A) {
     const int lane = threadIdx.x;
     double *__restrict__ S = A.ws + (size_t)blockIdx.x * (size_t)A.NE * 64 + lane;
@@ -92,56 +183,30 @@ __global__ __launch_bounds__(64) void jt_interp_kernel(JtArgs A) {
             }
             case JT_OP_SEPCOL: {  // src/JunctionTree.cpp:1056-1148
                 const double den = AT(op.e);
-                const int Ts = op.b, Q = op.d / op.b;
-                for (int j = 0; j < Ts; ++j) {
-                    double acc = 0.0;
-#pragma unroll 4
-                    for (int q = 0; q < Q; ++q) acc += AT(op.c + q * Ts + j) / den;
-                    const double old = AT(op.a + j);
-                    AT(op.a + j) = (old == 0.0) ? 0.0 : acc / old;
-                }
+                const Den D{den, 1.0 / den};
+                if (den_fast_all(den)) g_sepcol<false>(S, op, D);
+                else g_sepcol<true>(S, op, D);
                 break;
             }
             case JT_OP_CLQMUL: {  // src/JunctionTree.cpp:829-941 (extension + multiply + Normalize)
                 const double den = AT(op.c);
+                const Den D{den, 1.0 / den};
                 const int32_t *__restrict__ mp = aux + op.e;
-                double sum = 0.0;
-#pragma unroll 4
-                for (int e = 0; e < op.b; ++e) {
-                    const double v = (AT(op.a + e) / den) * AT(op.d + mp[e]);
-                    AT(op.a + e) = v;
-                    sum += v;
-                }
-                AT(op.c) = sum;
+                AT(op.c) = den_fast_all(den) ? g_clqmul<false>(S, op, mp, D) : g_clqmul<true>(S, op, mp, D);
                 break;
             }
             case JT_OP_SEPDIS: {  // src/JunctionTree.cpp:700-816
                 const double den = AT(op.d);
+                const Den D{den, 1.0 / den};
                 const int32_t *__restrict__ ls = aux + op.e;
-                const int per = op.f;
-                for (int j = 0; j < op.b; ++j) {
-                    double acc = 0.0;
-#pragma unroll 4
-                    for (int q = 0; q < per; ++q) acc += AT(op.c + ls[j * per + q]) / den;
-                    const double old = AT(op.a + j);
-                    AT(op.a + j) = (old == 0.0) ? 0.0 : acc / old;
-                }
+                if (den_fast_all(den)) g_sepdis<false>(S, op, ls, D);
+                else g_sepdis<true>(S, op, ls, D);
                 break;
             }
             case JT_OP_CLQDIS: {  // src/JunctionTree.cpp:1150-1238
                 const double den = AT(op.c);
-                const int Ts = op.e, Q = op.b / op.e;
-                double sum = 0.0;
-                for (int q = 0; q < Q; ++q) {
-#pragma unroll 4
-                    for (int j = 0; j < Ts; ++j) {
-                        const int e = q * Ts + j;
-                        const double v = (AT(op.a + e) / den) * AT(op.d + j);
-                        AT(op.a + e) = v;
-                        sum += v;
-                    }
-                }
-                AT(op.c) = sum;
+                const Den D{den, 1.0 / den};
+                AT(op.c) = den_fast_all(den) ? g_clqdis<false>(S, op, D) : g_clqdis<true>(S, op, D);
                 break;
             }
             case JT_OP_MARG: {  // src/JunctionTree.cpp:1339-1454, src/Inference.cpp:92-102
@@ -162,16 +227,9 @@ __global__ __launch_bounds__(64) void jt_interp_kernel(JtArgs A) {
                     if (k != sel) continue;
                     const int toff = cd[6 * k + 1], cum = cd[6 * k + 4], T = cd[6 * k + 5];
                     const double den = AT(cd[6 * k + 2]);
-                    const int bw = dim * cum, nhi = T / bw;
-                    double tot = 0.0;
-                    for (int d = 0; d < dim; ++d) {
-                        double acc = 0.0;
-                        for (int hi = 0; hi < nhi; ++hi)
-#pragma unroll 4
-                            for (int lo = 0; lo < cum; ++lo) acc += AT(toff + hi * bw + d * cum + lo) / den;
-                        if (act) o[d] = acc;
-                        tot += acc;
-                    }
+                    const Den D{den, 1.0 / den};
+                    const double tot = den_fast_all(den) ? g_marg<false>(S, toff, dim, cum, T, D, o, act)
+                                                         : g_marg<true>(S, toff, dim, cum, T, D, o, act);
                     if (act) {
                         if (op.f) {  // label: ArgMax, strict '>' from 0
                             int lab = 0;
@@ -209,25 +267,6 @@ struct JtLParams {
 
 // Pointers are separate __restrict__ kernel arguments (not a struct): the compiler can then prove
 // that the program arrays are never written and turns their wave-uniform reads into SMEM loads.
-// Division by the pending denominator.  Markstein: with y = RN(1/den) and q = RN(x*y) within one
-// ulp of x/den, q + RN(x - den*q)*y (two fmas) is the correctly rounded quotient -- the same bits as
-// the reference's `potentials[i] /= denominator` -- as long as nothing under/overflows.  The fast form
-// is used when den lies in [2^-600, 2^600] for every lane of the wave (then any table value >= 2^-400
-// keeps every intermediate normal); otherwise the op runs with the IEEE division sequence.
-struct Den {
-    double den, y;
-};
-template <bool EXACT>
-__device__ __forceinline__ double dv(double x, const Den &d) {
-    if (EXACT) return x / d.den;
-    const double q = x * d.y;
-    const double r = __builtin_fma(-d.den, q, x);
-    return __builtin_fma(r, d.y, q);
-}
-__device__ __forceinline__ bool den_fast_all(double den) {
-    return __ballot(!(den >= 0x1p-600 && den <= 0x1p+600)) == 0ull;
-}
-
 // the clique in flight: LDS rows [0, cap), spilled rows in per-wave global memory
 template <bool SPILL>
 struct Tab {
