@@ -99,6 +99,46 @@ def bench_pc(steps, warmup):
             "kernel_ms_per_run": 1e3 * pc.kernel_s, "edges": len(pc.edges)}
 
 
+def bench_munin(steps, warmup, cases=125_000):
+    """SURVEY §8(d) config 4 on one GPU: the seeded Munin-like 1041-variable network, 125k cases
+    (the per-GPU shard of 1M cases on 8 GPUs) at 20 % evidence (208 variables per case)."""
+    import tempfile
+    import torch
+    import fastbn_amd as F
+    from fastbn_amd import synth
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "munin_like.xml")
+        synth.random_network(1041, seed=1041, window=12, path=path, name="munin_like")
+        net = synth.read_xmlbif(path)
+        ev = synth.evidence_cases(net, cases, 208, seed=20250131)
+        t0 = time.perf_counter()
+        jt = F.JunctionTree(F.Network(path), device=0)
+        plan_s = time.perf_counter() - t0
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle as O
+        olab, omarg = O.OracleJT(path).infer(ev[:16])
+    d_ev = torch.from_numpy(ev).cuda()
+    d_lab = torch.empty(cases, dtype=torch.int32, device="cuda")
+    d_marg = torch.empty((cases, jt.info["sum_dom"]), dtype=torch.float64, device="cuda")
+    for _ in range(max(1, warmup)):
+        jt.run_device(d_ev.data_ptr(), cases, d_lab.data_ptr(), d_marg.data_ptr(), None)
+    torch.cuda.synchronize()
+    ok = (d_lab[:16].cpu().numpy() == olab).all() and (d_marg[:16].cpu().numpy() == omarg).all()
+    ms = []
+    for _ in range(steps):
+        jt.run_device(d_ev.data_ptr(), cases, d_lab.data_ptr(), d_marg.data_ptr(), None)
+        ms.append(jt.last_kernel_ms())
+    k = float(np.median(ms))
+    bpc = jt.info["algorithmic_bytes_per_case"]
+    return {"metric": "JT test-cases/sec (Munin-like 1041 vars, 20 % evidence)", "value": cases / (k * 1e-3),
+            "unit": "cases/s", "cases": cases, "kernel_ms": k, "plan_s": plan_s,
+            "kernel_variant": jt.refresh_info()["variant"], "bit_exact_vs_oracle_16_cases": bool(ok),
+            "cliques": jt.info["num_cliques"], "clique_entries": jt.info["clique_entries"],
+            "roofline": {"bound": "hbm", "achieved": bpc * cases / (k * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": bpc * cases / (k * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "algorithmic_bytes_per_case": bpc}}
+
+
 def load_traffic(cases):
     """Measured HBM bytes per launch (rocprofv3 FETCH_SIZE + WRITE_SIZE, calibrated; committed
     summary profiles/jt_traffic.json from tools/pmc_traffic.sh), scaled to this launch's cases."""
@@ -120,6 +160,7 @@ def main():
     ap.add_argument("--waves-per-cu", type=int, default=0)
     ap.add_argument("--no-baseline", action="store_true")
     ap.add_argument("--no-pc", action="store_true")
+    ap.add_argument("--no-munin", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -217,6 +258,8 @@ def main():
     if rank == 0 and world == 1:
         if not args.no_pc:
             out["pc_stable"] = bench_pc(max(5, args.steps // 2), args.warmup)
+        if not args.no_munin:
+            out["munin_like"] = bench_munin(3, 1)
         if not args.no_baseline:
             out["cpu_baseline"] = cpu_baseline_jt()
             if "pc_stable" in out:

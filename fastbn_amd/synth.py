@@ -92,7 +92,8 @@ def evidence_cases(net, n, k, seed, query=0):
     rng = np.random.Generator(np.random.PCG64(seed + 1))
     cand = np.array([v for v in range(V) if v != query])
     keys = rng.random((n, cand.size))
-    pick = cand[np.argsort(keys, axis=1)[:, :k]]  # k distinct candidates per case
+    # k distinct candidates per case: the k smallest keys (argpartition: same set as a full sort)
+    pick = cand[np.argpartition(keys, k - 1, axis=1)[:, :k]] if 0 < k < cand.size else cand[np.argsort(keys, axis=1)[:, :k]]
     ev = np.full((n, V), -1, np.int8)
     rows = np.repeat(np.arange(n), k)
     cols = pick.reshape(-1)
