@@ -56,6 +56,7 @@ _SIGS = {
     "fbn_pc_sepsets": [_vp, _vp, _i64, _vp],
     "fbn_pc_timing": [_vp, _vp, _vp],
     "fbn_pc_orient_skeleton": [C.c_int, _vp, C.c_int, _vp, C.c_int64, _vp],
+    "fbn_pc_level": [_vp, C.c_double, C.c_int, C.c_int, _vp, C.c_int64, C.c_int64, C.c_int64, _vp, _vp, _vp, _vp],
     "fbn_pc_num_oriented_edges": [_vp, _vp],
     "fbn_pc_oriented_edges": [_vp, _vp],
     "fbn_pc_shd_bif": [_vp, C.c_char_p, _vp],
@@ -310,6 +311,20 @@ class IndependenceTest:
         lib.fbn_ci_dataset_upload(_p(dataset.columns), dataset.num_vars, dataset.num_instance,
                                   _p(dataset.dims), device, C.byref(h))
         self._h = h
+
+    def level(self, d, edges, e_begin, e_end, group_size=1):
+        """One skeleton level for edges[e_begin:e_end] of the current skeleton (fbn_pc_level) ->
+        (removed[bool], sepsets[list of tuples or None], counted, launched)."""
+        ev = np.ascontiguousarray(np.asarray(edges, np.int32).reshape(-1, 2))
+        n = e_end - e_begin
+        rm = np.zeros(max(n, 1), np.uint8)
+        sp = np.zeros((max(n, 1), max(d, 1)), np.int32)
+        cnt, lau = C.c_int64(), C.c_int64()
+        lib.fbn_pc_level(self._h, self.alpha, d, group_size, _p(ev), ev.shape[0], e_begin, e_end, _p(rm), _p(sp),
+                         C.byref(cnt), C.byref(lau))
+        rm = rm[:n].astype(bool)
+        seps = [tuple(int(v) for v in sp[i, :d]) if rm[i] else None for i in range(n)]
+        return rm, seps, cnt.value, lau.value
 
     def run(self, items, d):
         items = np.ascontiguousarray(items, dtype=np.int32).reshape(-1, 2 + d)

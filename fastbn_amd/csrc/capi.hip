@@ -836,6 +836,37 @@ int fbn_pc_sepsets(const fbn_pc_result *r, int32_t *buf, int64_t cap, int64_t *l
     if (len) *len = k;
     return FBN_OK;
 }
+int fbn_pc_level(fbn_ci_ctx *c, double alpha, int d, int group_size, const int32_t *edges, int64_t nedges,
+                 int64_t e_begin, int64_t e_end, uint8_t *removed, int32_t *sepsets, int64_t *counted,
+                 int64_t *launched) {
+    if (!c || d < 0 || d > 8 || group_size < 1 || group_size > 8 || nedges < 0 || (nedges && !edges) ||
+        e_begin < 0 || e_end < e_begin || e_end > nedges || (e_end > e_begin && !removed))
+        return SetError(FBN_ERR_ARG, "bad argument");
+    std::vector<std::pair<int, int>> ev((size_t)nedges);
+    std::vector<std::vector<int>> adj(c->nvars);
+    for (int64_t i = 0; i < nedges; ++i) {
+        const int a = edges[2 * i], b = edges[2 * i + 1];
+        if (a < 0 || b <= a || b >= c->nvars) return SetError(FBN_ERR_ARG, "edge %lld must be (x < y) in range", (long long)i);
+        if (i && !(ev[i - 1] < std::make_pair(a, b))) return SetError(FBN_ERR_ARG, "edges must be in (x, y) lexicographic order");
+        ev[i] = {a, b};
+        adj[a].push_back(b);
+        adj[b].push_back(a);
+    }
+    for (auto &a : adj) std::sort(a.begin(), a.end());
+    FBN_HIP(hipSetDevice(c->device));
+    fbn::PCResultHost scratch;
+    fbn::LevelOut out;
+    int rc = fbn::RunLevel(c, alpha, d, group_size, adj, ev, (size_t)e_begin, (size_t)e_end, out, scratch);
+    if (rc) return rc;
+    for (int64_t e = 0; e < e_end - e_begin; ++e) {
+        removed[e] = out.removed[e] ? 1 : 0;
+        if (sepsets)
+            for (int j = 0; j < d; ++j) sepsets[e * d + j] = out.removed[e] ? out.sep[e][j] : -1;
+    }
+    if (counted) *counted = out.counted;
+    if (launched) *launched = out.launched;
+    return FBN_OK;
+}
 int fbn_pc_orient_skeleton(int nvars, const int32_t *pairs, int nedges, const int32_t *sepsets, int64_t len,
                            fbn_pc_result **out) {
     if (nvars <= 0 || nedges < 0 || (nedges && !pairs) || (len && !sepsets) || !out)

@@ -78,6 +78,137 @@ struct Pending {  // one generated test
 
 }  // namespace
 
+// One level of the skeleton search for the edges [e_begin, e_end) of `edges` (vec_edges order),
+// against the adjacency snapshot `adj` (sorted lists).  Level 0: one marginal test per edge
+// (src/PCStable.cpp:73-157); level d >= 1: SearchAtDepth / CheckEdge semantics (see file header).
+// Outputs per edge of the range: removed flag and, if removed, its sepset (sorted).
+int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::vector<std::vector<int>> &adj,
+             const std::vector<std::pair<int, int>> &edges, size_t e_begin, size_t e_end, LevelOut &out,
+             PCResultHost &res) {
+    const size_t E = e_end - e_begin;
+    out.removed.assign(E, 0);
+    out.sep.assign(E, {});
+    out.counted = out.launched = 0;
+    std::vector<int32_t> items;
+    std::vector<uint8_t> indep;
+    std::vector<int32_t> dfv;
+    if (d == 0) {
+        items.resize(E * 2);
+        for (size_t e = 0; e < E; ++e) items[2 * e] = edges[e_begin + e].first, items[2 * e + 1] = edges[e_begin + e].second;
+        indep.resize(E);
+        int rc = CiRunBatch(ctx, items.data(), (int64_t)E, 0, alpha, indep.data(), nullptr, res);
+        if (rc) return rc;
+        for (size_t e = 0; e < E; ++e) out.removed[e] = indep[e] ? 1 : 0;
+        out.counted = out.launched = (int64_t)E;
+        return FBN_OK;
+    }
+    std::vector<EdgeState> st(E);
+    for (size_t e = 0; e < E; ++e) {
+        st[e].x = edges[e_begin + e].first;
+        st[e].y = edges[e_begin + e].second;
+        StartSide(st[e], adj, d);
+        if (!st[e].has_next) st[e].resolved = true;  // both sides too small: kept
+    }
+    // first round: enough tests to fill the device (~8k) without speculating deep into edges
+    // that usually resolve early; later rounds grow 4x per round
+    int64_t open_edges = 0;
+    for (auto &s : st) open_edges += !s.resolved;
+    int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(32, 8192 / std::max<int64_t>(1, open_edges)));
+    std::vector<Pending> pend;
+    while (true) {
+        items.clear();
+        pend.clear();
+        for (size_t e = 0; e < st.size(); ++e) {
+            EdgeState &s = st[e];
+            if (s.resolved) continue;
+            // next chunk: whole groups only, never across a side boundary
+            int64_t want = ((chunk + group_size - 1) / group_size) * group_size;
+            while (want > 0 && s.has_next) {
+                const int64_t gstart = (s.pos_in_side / group_size) * group_size;
+                Pending p{(int)e, s.side, s.pos_in_side, gstart + group_size};
+                pend.push_back(p);
+                items.push_back(s.x);
+                items.push_back(s.y);
+                for (int i = 0; i < d; ++i) items.push_back(s.A[s.ch[i]]);
+                --want;
+                Advance(s, d);
+                if (!s.has_next) {
+                    // side exhausted: next side starts fresh (its groups restart at 0)
+                    if (s.side == 0) {
+                        s.side = 1;
+                        StartSide(s, adj, d);
+                    } else {
+                        s.side = 2;
+                    }
+                    break;  // keep groups aligned: finish this chunk at the side boundary
+                }
+            }
+        }
+        if (pend.empty()) break;
+        const int64_t nt = (int64_t)pend.size();
+        indep.resize(nt);
+        dfv.resize(nt);
+        int rc = CiRunBatch(ctx, items.data(), nt, d, alpha, indep.data(), dfv.data(), res);
+        if (rc) return rc;
+        out.launched += nt;
+        // resolve in order per edge
+        size_t i = 0;
+        while (i < pend.size()) {
+            const int e = pend[i].edge;
+            size_t j = i;
+            while (j < pend.size() && pend[j].edge == e) ++j;  // tests of this edge: [i, j)
+            EdgeState &s = st[e];
+            size_t k = i;
+            while (k < j && !s.removed) {
+                // one group: tests with the same side and group_end
+                size_t g = k;
+                while (g < j && pend[g].side == pend[k].side && pend[g].group_end == pend[k].group_end) ++g;
+                const int gsz = (int)(g - k);
+                out.counted += gsz;
+                for (size_t t = k; t < g; ++t) {
+                    bool ind = indep[t] != 0;
+                    if (gsz > 1 && dfv[t] == 0) ind = false;  // group quirk (see file header)
+                    if (ind) {
+                        s.removed = true;
+                        s.resolved = true;
+                        std::vector<int> z(items.begin() + (2 + d) * t + 2, items.begin() + (2 + d) * (t + 1));
+                        std::sort(z.begin(), z.end());
+                        s.sep = z;
+                        break;
+                    }
+                }
+                k = g;
+            }
+            if (!s.removed && !s.has_next) s.resolved = true;  // exhausted: dependent, kept
+            i = j;
+        }
+        chunk = std::min<int64_t>(chunk * 4, 1 << 16);
+    }
+    for (size_t e = 0; e < E; ++e)
+        if (st[e].removed) out.removed[e] = 1, out.sep[e] = st[e].sep;
+    return FBN_OK;
+}
+
+void ApplyRemovals(const std::vector<char> &rm, std::vector<std::pair<int, int>> &edges,
+                   std::vector<std::vector<int>> &adj) {
+    // removals after a level, in vec_edges order (src/PCStable.cpp:310-326); the adjacency lists
+    // are rebuilt from the kept edges in O(E) (edges stay in (i < j) lexicographic order, so every
+    // list comes out sorted) instead of erasing element by element (the reference's O(E^2) hot spot)
+    std::vector<std::pair<int, int>> keep;
+    keep.reserve(edges.size());
+    for (size_t e = 0; e < edges.size(); ++e)
+        if (!rm[e]) keep.push_back(edges[e]);
+    edges.swap(keep);
+    for (auto &a : adj) a.clear();
+    for (auto &e : edges) adj[e.first].push_back(e.second), adj[e.second].push_back(e.first);
+}
+
+bool ContinueAfter(const std::vector<std::vector<int>> &adj, int d) {  // FreeDegree (:557-563)
+    size_t maxdeg = 0;
+    for (auto &a : adj) maxdeg = std::max(maxdeg, a.size());
+    return (int64_t)maxdeg - 1 > d;
+}
+
 int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResultHost &res) {
     if (group_size < 1 || group_size > 8) return SetError(FBN_ERR_ARG, "group_size must be 1..8 (reference cap, src/IndependenceTest.cpp:170)");
     auto t0 = std::chrono::steady_clock::now();
@@ -93,140 +224,16 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
     for (int i = 0; i < n; ++i)
         for (int j = 0; j < n; ++j)
             if (i != j) adj[i].push_back(j);
-
-    std::vector<int32_t> items;
-    std::vector<uint8_t> indep;
-    std::vector<int32_t> dfv;
-
-    // removals after a level, in vec_edges order (src/PCStable.cpp:310-326); the adjacency lists
-    // are rebuilt from the kept edges in O(E) (edges stay in (i < j) lexicographic order, so every
-    // list comes out sorted) instead of erasing element by element (the reference's O(E^2) hot spot)
-    auto apply_removals = [&](const std::vector<char> &rm) {
-        std::vector<std::pair<int, int>> keep;
-        keep.reserve(edges.size());
-        for (size_t e = 0; e < edges.size(); ++e)
-            if (!rm[e]) keep.push_back(edges[e]);
-        edges.swap(keep);
-        for (auto &a : adj) a.clear();
-        for (auto &e : edges) adj[e.first].push_back(e.second), adj[e.second].push_back(e.first);
-    };
-
-    // ---- level 0 (src/PCStable.cpp:73-157)
-    {
-        items.resize(edges.size() * 2);
-        for (size_t e = 0; e < edges.size(); ++e) items[2 * e] = edges[e].first, items[2 * e + 1] = edges[e].second;
-        indep.resize(edges.size());
-        int rc = CiRunBatch(ctx, items.data(), (int64_t)edges.size(), 0, alpha, indep.data(), nullptr, res);
+    for (int d = 0; d == 0 || d < depth; ++d) {
+        LevelOut out;
+        int rc = RunLevel(ctx, alpha, d, group_size, adj, edges, 0, edges.size(), out, res);
         if (rc) return rc;
-        std::vector<char> rm(edges.size(), 0);
         for (size_t e = 0; e < edges.size(); ++e)
-            if (indep[e]) {
-                rm[e] = 1;
-                res.sepset[{edges[e].first, edges[e].second}] = {};
-            }
-        res.tests_per_level.push_back((int64_t)edges.size());
-        res.launched_per_level.push_back((int64_t)edges.size());
-        apply_removals(rm);
-    }
-
-    // ---- levels d >= 1 (SearchAtDepth :209-328, CheckEdge :339-433, Testing :465-551)
-    for (int d = 1; d < depth; ++d) {
-        const std::vector<std::vector<int>> snap = adj;
-        std::vector<EdgeState> st(edges.size());
-        for (size_t e = 0; e < edges.size(); ++e) {
-            st[e].x = edges[e].first;
-            st[e].y = edges[e].second;
-            StartSide(st[e], snap, d);
-            if (!st[e].has_next) st[e].resolved = true;  // both sides too small: kept
-        }
-        int64_t counted = 0, launched = 0;
-        // first round: enough tests to fill the device (~8k) without speculating deep into edges
-        // that usually resolve early; later rounds grow 4x per round
-        int64_t open_edges = 0;
-        for (auto &s : st) open_edges += !s.resolved;
-        int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(32, 8192 / std::max<int64_t>(1, open_edges)));
-        std::vector<Pending> pend;
-        while (true) {
-            items.clear();
-            pend.clear();
-            for (size_t e = 0; e < st.size(); ++e) {
-                EdgeState &s = st[e];
-                if (s.resolved) continue;
-                // next chunk: whole groups only, never across a side boundary
-                int64_t want = ((chunk + group_size - 1) / group_size) * group_size;
-                while (want > 0 && s.has_next) {
-                    const int64_t gstart = (s.pos_in_side / group_size) * group_size;
-                    Pending p{(int)e, s.side, s.pos_in_side, gstart + group_size};
-                    pend.push_back(p);
-                    items.push_back(s.x);
-                    items.push_back(s.y);
-                    for (int i = 0; i < d; ++i) items.push_back(s.A[s.ch[i]]);
-                    --want;
-                    Advance(s, d);
-                    if (!s.has_next) {
-                        // side exhausted: next side starts fresh (its groups restart at 0)
-                        if (s.side == 0) {
-                            s.side = 1;
-                            StartSide(s, snap, d);
-                        } else {
-                            s.side = 2;
-                        }
-                        break;  // keep groups aligned: finish this chunk at the side boundary
-                    }
-                }
-            }
-            if (pend.empty()) break;
-            const int64_t nt = (int64_t)pend.size();
-            indep.resize(nt);
-            dfv.resize(nt);
-            int rc = CiRunBatch(ctx, items.data(), nt, d, alpha, indep.data(), dfv.data(), res);
-            if (rc) return rc;
-            launched += nt;
-            // resolve in order per edge
-            size_t i = 0;
-            while (i < pend.size()) {
-                const int e = pend[i].edge;
-                size_t j = i;
-                while (j < pend.size() && pend[j].edge == e) ++j;  // tests of this edge: [i, j)
-                EdgeState &s = st[e];
-                size_t k = i;
-                while (k < j && !s.removed) {
-                    // one group: tests with the same side and group_end
-                    size_t g = k;
-                    while (g < j && pend[g].side == pend[k].side && pend[g].group_end == pend[k].group_end) ++g;
-                    const int gsz = (int)(g - k);
-                    counted += gsz;
-                    for (size_t t = k; t < g; ++t) {
-                        bool ind = indep[t] != 0;
-                        if (gsz > 1 && dfv[t] == 0) ind = false;  // group quirk (see file header)
-                        if (ind) {
-                            s.removed = true;
-                            s.resolved = true;
-                            std::vector<int> z(items.begin() + (2 + d) * t + 2, items.begin() + (2 + d) * (t + 1));
-                            std::sort(z.begin(), z.end());
-                            s.sep = z;
-                            break;
-                        }
-                    }
-                    k = g;
-                }
-                if (!s.removed && !s.has_next) s.resolved = true;  // exhausted: dependent, kept
-                i = j;
-            }
-            chunk = std::min<int64_t>(chunk * 4, 1 << 16);
-        }
-        std::vector<char> rm(edges.size(), 0);
-        for (size_t e = 0; e < st.size(); ++e)
-            if (st[e].removed) {
-                rm[e] = 1;
-                res.sepset[{st[e].x, st[e].y}] = st[e].sep;
-            }
-        res.tests_per_level.push_back(counted);
-        res.launched_per_level.push_back(launched);
-        apply_removals(rm);
-        size_t maxdeg = 0;  // FreeDegree (:557-563)
-        for (int v = 0; v < n; ++v) maxdeg = std::max(maxdeg, adj[v].size());
-        if (!((int64_t)maxdeg - 1 > d)) break;
+            if (out.removed[e]) res.sepset[edges[e]] = out.sep[e];
+        res.tests_per_level.push_back(out.counted);
+        res.launched_per_level.push_back(out.launched);
+        ApplyRemovals(out.removed, edges, adj);
+        if (d >= 1 && !ContinueAfter(adj, d)) break;
     }
     res.edges = edges;
     res.total_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

@@ -30,6 +30,15 @@ void CiCtxShape(const fbn_ci_ctx *c, int *nvars, int64_t *nsamples);
 int CiRunBatch(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alpha, uint8_t *indep, int32_t *df,
                PCResultHost &res);
 int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResultHost &res);
+// one level for an edge range (the unit a multi-GPU driver partitions), see pc_driver.cpp
+struct LevelOut {
+    std::vector<char> removed;
+    std::vector<std::vector<int>> sep;
+    int64_t counted = 0, launched = 0;
+};
+int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::vector<std::vector<int>> &adj,
+             const std::vector<std::pair<int, int>> &edges, size_t e_begin, size_t e_end, LevelOut &out,
+             PCResultHost &res);
 // orientation (pc_orient.cpp): v-structures + Meek rules 1-3 on res.edges / res.sepset
 int OrientPC(int nvars, PCResultHost &res);
 int LoadBifGraph(const std::string &path, std::vector<std::string> &names, std::vector<std::pair<int, int>> &arcs);

@@ -56,3 +56,24 @@ def gather_shards(local, total, device=None):
     outs = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(outs, t)
     return np.concatenate([o.cpu().numpy()[:c] for o, c in zip(outs, counts)], axis=0)
+
+
+def gather_var(local, device=None):
+    """Concatenate variable-length row blocks of all ranks in rank order (same trailing shape)."""
+    import torch
+    import torch.distributed as dist
+    local = np.ascontiguousarray(local)
+    if not (dist.is_available() and dist.is_initialized()):
+        return local
+    world = dist.get_world_size()
+    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=device)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    counts = [int(x.item()) for x in ns]
+    cap = max(max(counts), 1)
+    buf = np.zeros((cap,) + local.shape[1:], dtype=local.dtype)
+    buf[:local.shape[0]] = local
+    t = torch.from_numpy(buf).to(device) if device is not None else torch.from_numpy(buf)
+    outs = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(outs, t)
+    return np.concatenate([o.cpu().numpy()[:c] for o, c in zip(outs, counts)], axis=0)

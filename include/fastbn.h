@@ -168,6 +168,16 @@ int fbn_pc_sepsets(const fbn_pc_result *r, int32_t *buf, int64_t cap, int64_t *l
 /* After the skeleton, fbn_pc_stable orients like StructLearnByPCStable steps 2-3
  * (OrientVStructure / OrientImplied, src/PCStable.cpp:576-843): triples [n][3] =
  * (from, to, 1) for arcs, (min, max, 0) for undirected edges, in the reference's vec_edges order. */
+/* One skeleton level for the edge range [e_begin, e_end) of the current skeleton `edges`
+ * ([nedges][2], x < y, lexicographic = the reference's vec_edges order): level 0 = one marginal test
+ * per edge (src/PCStable.cpp:73-157), level d >= 1 = SearchAtDepth/CheckEdge over the adjacency
+ * snapshot implied by `edges` (:209-551).  removed[e - e_begin] = 1 if the edge goes; sepsets
+ * [(e_end - e_begin)][d] (or NULL) holds the removing set (sorted, -1 if kept); counted = tests the
+ * reference would run, launched = device tests incl. speculation.  The unit a multi-GPU driver
+ * partitions (fastbn_amd/pc_dist.py): ranges are independent within a level. */
+int fbn_pc_level(fbn_ci_ctx *c, double alpha, int d, int group_size, const int32_t *edges, int64_t nedges,
+                 int64_t e_begin, int64_t e_end, uint8_t *removed, int32_t *sepsets, int64_t *counted,
+                 int64_t *launched);
 /* Host-only: orient a given skeleton (pairs [nedges][2] in vec_edges order) with its sepsets
  * (records (x, y, m, z_0..z_{m-1}) as fbn_pc_sepsets writes them) into a new result. */
 int fbn_pc_orient_skeleton(int nvars, const int32_t *pairs, int nedges, const int32_t *sepsets, int64_t len,

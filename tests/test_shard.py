@@ -70,3 +70,76 @@ def test_two_rank_gloo_shards_match_single_process(tmp_path):
     np.testing.assert_array_equal(r["margs"], marg)
     assert float(r["tmax"]) == 2.0
     assert r["sums"][0] == 301 and r["sums"][1] == (lab == 0).sum()
+
+
+# ---------------------------------------------------------------- multi-GPU PC-stable orchestration
+def _oracle_level_fn(od):
+    """Per-edge CheckEdge restated over the oracle's CI test (group size 1): the CPU stand-in for
+    fbn_pc_level in the orchestration tests."""
+    from itertools import combinations
+
+    def level_fn(d, edges, b, e):
+        adj = {}
+        for x, y in edges:
+            adj.setdefault(x, []).append(y)
+            adj.setdefault(y, []).append(x)
+        rm, seps, cnt = [], [], 0
+        for x, y in edges[b:e]:
+            if d == 0:
+                cnt += 1
+                ind = od.ci_test(x, y)["is_independent"]
+                rm.append(ind)
+                seps.append(() if ind else None)
+                continue
+            found = None
+            for a, other in ((x, y), (y, x)):
+                cand = sorted(v for v in adj[a] if v != other)
+                for z in combinations(cand, d):
+                    cnt += 1
+                    if od.ci_test(x, y, list(z))["is_independent"]:
+                        found = tuple(sorted(z))
+                        break
+                if found is not None:
+                    break
+            rm.append(found is not None)
+            seps.append(found)
+        return rm, seps, cnt, cnt
+    return level_fn
+
+
+def _pc_worker(rank, world, port, csv, out_path):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import oracle as O
+    from fastbn_amd import pc_dist
+    od = O.OracleDataset(csv=csv)
+    edges, sepset, tests, launched = pc_dist.pc_skeleton_distributed(_oracle_level_fn(od), 37)
+    if rank == 0:
+        np.save(out_path, np.array([edges, sorted(sepset.items()), tests], dtype=object), allow_pickle=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_partition_balances_cost():
+    from fastbn_amd import pc_dist
+    costs = [1, 5, 1, 1, 9, 1, 1, 1, 3, 2]
+    for world in (1, 2, 3, 4):
+        parts = pc_dist.partition(costs, world)
+        assert parts[0][0] == 0 and parts[-1][1] == len(costs)
+        assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+
+
+def test_two_rank_gloo_pc_skeleton_matches_oracle(tmp_path):
+    """world_size 2: per-level edge partition + one all-gather == the single-process reference order."""
+    mp = pytest.importorskip("torch.multiprocessing")
+    import oracle as O
+    csv = os.path.join(REPO, "tests", "golden", "alarm", "alarm_s5000.txt")
+    out = str(tmp_path / "pc.npy")
+    mp.start_processes(_pc_worker, args=(2, _free_port(), csv, out), nprocs=2, join=True, start_method="spawn")
+    edges, sep, tests = np.load(out, allow_pickle=True)  # written by this test's own worker
+    ref = O.OracleDataset(csv=csv).pc_stable(0.05, 1000, 1)
+    assert [tuple(e) for e in edges] == [tuple(e) for e in ref["edges"]]
+    assert dict(sep) == {k: tuple(v) for k, v in ref["sepset"].items()}
+    assert list(tests) == list(ref["tests_per_level"])
