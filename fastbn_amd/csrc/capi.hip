@@ -542,11 +542,12 @@ int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, 
     if (variant == 1) {
         const int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 8;
         int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * wpc);
-        // persistent waves: cap the per-wave workspaces at half of the free HBM
+        // persistent waves: cap the per-wave workspaces at 80 % of the free HBM (more resident waves
+        // = more memory-level parallelism: this variant is latency bound on large plans)
         const size_t per_wave = (size_t)g.state_entries * 64 * 8 + (size_t)nc * 64 * 4;
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && per_wave > 0) {
-            const size_t have = free_b / 2 + (p->ws.bytes);
+            const size_t have = free_b / 10 * 8 + (p->ws.bytes);
             grid = (int)std::max<int64_t>(1, std::min<int64_t>(grid, (int64_t)(have / per_wave)));
         }
         const size_t ws_d = (size_t)grid * g.state_entries * 64 * 8;

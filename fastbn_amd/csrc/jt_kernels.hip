@@ -60,23 +60,63 @@ __device__ __forceinline__ bool den_fast_all(double den) {
 #define FBN_G_UNROLL 8
 #endif
 // global-variant op bodies, instantiated for the fast (Markstein) and the exact division
+// Separator sweeps keep up to kGJ results in registers and store them together, so the loads of a
+// chunk of separator entries are not serialized behind per-entry stores (vmcnt is in issue order).
+constexpr int kGJ = 32;
 template <bool EXACT>
 __device__ __forceinline__ void g_sepcol(double *__restrict__ S, const JtOp &op, const Den &D) {
     const int Ts = op.b, Q = op.d / op.b;
-    for (int j = 0; j < Ts; ++j) {
-        double acc = 0.0;
+    for (int j0 = 0; j0 < Ts; j0 += kGJ) {
+        const int nj = Ts - j0 < kGJ ? Ts - j0 : kGJ;
+        double res[kGJ];
+#pragma unroll
+        for (int jj = 0; jj < kGJ; ++jj) {
+            res[jj] = 0.0;
+            if (jj >= nj) continue;
+            const int j = j0 + jj;
+            double acc = 0.0;
 #pragma unroll FBN_G_UNROLL
-        for (int q = 0; q < Q; ++q) acc += dv<EXACT>(AT(op.c + q * Ts + j), D);
-        const double old = AT(op.a + j);
-        AT(op.a + j) = (old == 0.0) ? 0.0 : acc / old;
+            for (int q = 0; q < Q; ++q) acc += dv<EXACT>(AT(op.c + q * Ts + j), D);
+            const double old = AT(op.a + j);
+            res[jj] = (old == 0.0) ? 0.0 : acc / old;
+        }
+#pragma unroll
+        for (int jj = 0; jj < kGJ; ++jj)
+            if (jj < nj) AT(op.a + j0 + jj) = res[jj];
     }
 }
+// Read-modify-write sweeps are software-pipelined: the loads of chunk k+1 are issued before the
+// stores of chunk k, so a wait for loaded data never includes this sweep's own stores (vmcnt
+// counts loads and stores together, in issue order).  Element order and the sum order are the
+// reference's.
+constexpr int kGChunk = 16;
 template <bool EXACT>
 __device__ __forceinline__ double g_clqmul(double *__restrict__ S, const JtOp &op, const int32_t *__restrict__ mp,
                                            const Den &D) {
+    const int T = op.b, nfull = T / kGChunk;
     double sum = 0.0;
-#pragma unroll FBN_G_UNROLL
-    for (int e = 0; e < op.b; ++e) {
+    double ta[kGChunk], ma[kGChunk];
+    if (nfull > 0) {
+#pragma unroll
+        for (int k = 0; k < kGChunk; ++k) ta[k] = AT(op.a + k), ma[k] = AT(op.d + mp[k]);
+    }
+    for (int c = 0; c < nfull; ++c) {
+        const int e0 = c * kGChunk, e1 = e0 + kGChunk;
+        double tb[kGChunk], mb[kGChunk];
+        if (c + 1 < nfull) {
+#pragma unroll
+            for (int k = 0; k < kGChunk; ++k) tb[k] = AT(op.a + e1 + k), mb[k] = AT(op.d + mp[e1 + k]);
+        }
+#pragma unroll
+        for (int k = 0; k < kGChunk; ++k) {
+            const double v = dv<EXACT>(ta[k], D) * ma[k];
+            AT(op.a + e0 + k) = v;
+            sum += v;
+        }
+#pragma unroll
+        for (int k = 0; k < kGChunk; ++k) ta[k] = tb[k], ma[k] = mb[k];
+    }
+    for (int e = nfull * kGChunk; e < T; ++e) {
         const double v = dv<EXACT>(AT(op.a + e), D) * AT(op.d + mp[e]);
         AT(op.a + e) = v;
         sum += v;
@@ -86,27 +126,55 @@ __device__ __forceinline__ double g_clqmul(double *__restrict__ S, const JtOp &o
 template <bool EXACT>
 __device__ __forceinline__ void g_sepdis(double *__restrict__ S, const JtOp &op, const int32_t *__restrict__ ls,
                                          const Den &D) {
-    const int per = op.f;
-    for (int j = 0; j < op.b; ++j) {
-        double acc = 0.0;
+    const int per = op.f, Ts = op.b;
+    for (int j0 = 0; j0 < Ts; j0 += kGJ) {
+        const int nj = Ts - j0 < kGJ ? Ts - j0 : kGJ;
+        double res[kGJ];
+#pragma unroll
+        for (int jj = 0; jj < kGJ; ++jj) {
+            res[jj] = 0.0;
+            if (jj >= nj) continue;
+            const int j = j0 + jj;
+            double acc = 0.0;
 #pragma unroll FBN_G_UNROLL
-        for (int q = 0; q < per; ++q) acc += dv<EXACT>(AT(op.c + ls[j * per + q]), D);
-        const double old = AT(op.a + j);
-        AT(op.a + j) = (old == 0.0) ? 0.0 : acc / old;
+            for (int q = 0; q < per; ++q) acc += dv<EXACT>(AT(op.c + ls[j * per + q]), D);
+            const double old = AT(op.a + j);
+            res[jj] = (old == 0.0) ? 0.0 : acc / old;
+        }
+#pragma unroll
+        for (int jj = 0; jj < kGJ; ++jj)
+            if (jj < nj) AT(op.a + j0 + jj) = res[jj];
     }
 }
 template <bool EXACT>
 __device__ __forceinline__ double g_clqdis(double *__restrict__ S, const JtOp &op, const Den &D) {
-    const int Ts = op.e, Q = op.b / op.e;
+    const int T = op.b, Ts = op.e, nfull = T / kGChunk;
     double sum = 0.0;
-    for (int q = 0; q < Q; ++q) {
-#pragma unroll FBN_G_UNROLL
-        for (int j = 0; j < Ts; ++j) {
-            const int e = q * Ts + j;
-            const double v = dv<EXACT>(AT(op.a + e), D) * AT(op.d + j);
-            AT(op.a + e) = v;
+    double ta[kGChunk], ma[kGChunk];
+    if (nfull > 0) {
+#pragma unroll
+        for (int k = 0; k < kGChunk; ++k) ta[k] = AT(op.a + k), ma[k] = AT(op.d + k % Ts);
+    }
+    for (int c = 0; c < nfull; ++c) {
+        const int e0 = c * kGChunk, e1 = e0 + kGChunk;
+        double tb[kGChunk], mb[kGChunk];
+        if (c + 1 < nfull) {
+#pragma unroll
+            for (int k = 0; k < kGChunk; ++k) tb[k] = AT(op.a + e1 + k), mb[k] = AT(op.d + (e1 + k) % Ts);
+        }
+#pragma unroll
+        for (int k = 0; k < kGChunk; ++k) {
+            const double v = dv<EXACT>(ta[k], D) * ma[k];
+            AT(op.a + e0 + k) = v;
             sum += v;
         }
+#pragma unroll
+        for (int k = 0; k < kGChunk; ++k) ta[k] = tb[k], ma[k] = mb[k];
+    }
+    for (int e = nfull * kGChunk; e < T; ++e) {
+        const double v = dv<EXACT>(AT(op.a + e), D) * AT(op.d + e % Ts);
+        AT(op.a + e) = v;
+        sum += v;
     }
     return sum;
 }
