@@ -19,7 +19,7 @@ extern "C" hipError_t fbn_jt_launch(const JtOp *ops, int nops, const int32_t *au
 extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, const int32_t *items, long long N,
                                     long long n, int d, double alpha, double *g2, int32_t *df, double *p,
                                     uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
-                                    hipStream_t stream);
+                                    int32_t *gscratch, hipStream_t stream);
 extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy);
 extern "C" hipError_t fbn_jt_lds_launch(const JtOp *ops, int nops, const int32_t *aux, const double *initv,
                                         const uint64_t *dig, const int8_t *evid, int V, long long ncases, int SD,
@@ -124,7 +124,7 @@ struct fbn_ci_ctx {
     int device = 0, num_cu = 0, nvars = 0;
     int64_t N = 0;
     std::vector<int32_t> dims;
-    DevBuf cols, ddims, items, g2, df, p, indep, counts;
+    DevBuf cols, ddims, items, g2, df, p, indep, counts, scratch;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipStream_t stream = nullptr;  // the PC driver's rounds (pinned staging, one sync per round)
     float last_ms = 0.f;
@@ -714,8 +714,8 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         if (dimz > (1 << 24)) return SetError(FBN_ERR_LIMIT, "test %lld: conditioning table too large", (long long)i);
         lds = std::max(lds, fbn_ci_lds_bytes((int)dimz, c->dims[it[0]], c->dims[it[1]]));
     }
-    if (lds > 160 * 1024)
-        return SetError(FBN_ERR_LIMIT, "contingency table needs %zu B of LDS (> 160 KiB): not supported yet", lds);
+    // tables beyond the LDS budget: the same layout in a per-workgroup global scratch region
+    const bool global_tables = lds > 160 * 1024;
     int rc;
     if ((rc = c->items.ensure((size_t)n * w * 4))) return rc;
     if ((rc = c->indep.ensure((size_t)n))) return rc;
@@ -725,12 +725,21 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         if ((rc = c->p.ensure((size_t)n * 8))) return rc;
     }
     FBN_HIP(hipMemcpyAsync(c->items.p, items, (size_t)n * w * 4, hipMemcpyHostToDevice, s));
-    const int grid = (int)std::min<int64_t>(n, (int64_t)c->num_cu * 8);
+    int grid = (int)std::min<int64_t>(n, (int64_t)c->num_cu * 8);
+    int32_t *gscratch = nullptr;
+    if (global_tables) {
+        // one table region per workgroup, at most 4 GiB of scratch in total (fewer, longer-lived
+        // workgroups for very large tables; each loops over its tests)
+        const size_t stride = ((lds / 4 + 1) & ~(size_t)1) * 4;
+        grid = (int)std::max<size_t>(1, std::min<size_t>((size_t)grid, ((size_t)4 << 30) / stride));
+        if ((rc = c->scratch.ensure((size_t)grid * stride))) return rc;
+        gscratch = c->scratch.as<int32_t>();
+    }
     FBN_HIP(hipEventRecord(c->ev0, s));
     hipError_t e = fbn_ci_launch(c->cols.as<uint8_t>(), c->ddims.as<int32_t>(), c->items.as<int32_t>(), c->N, n, d,
                                  alpha, want_g2p ? c->g2.as<double>() : nullptr, c->df.as<int32_t>(),
                                  want_g2p ? c->p.as<double>() : nullptr, c->indep.as<uint8_t>(), counts_dev, lds, grid,
-                                 s);
+                                 gscratch, s);
     if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci kernel launch: %s", hipGetErrorString(e));
     FBN_HIP(hipEventRecord(c->ev1, s));
     return FBN_OK;

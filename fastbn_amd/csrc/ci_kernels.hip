@@ -28,6 +28,8 @@ struct CiArgs {
     double *p;
     uint8_t *indep;
     int32_t *counts;  // optional: histogram of item 0
+    int32_t *gscratch;  // non-null: tables too large for LDS live in global memory, one region per
+    long long gstride;  // workgroup of gstride ints (same layout as the LDS one)
 };
 
 // regularized upper incomplete gamma Q(a, x): series / modified Lentz continued fraction; the
@@ -64,7 +66,8 @@ __device__ double gamma_q(double a, double x) {
 
 template <int D>
 __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
-    extern __shared__ __align__(16) int32_t smem[];
+    extern __shared__ __align__(16) int32_t lds_base[];
+    int32_t *smem = A.gscratch ? A.gscratch + (size_t)blockIdx.x * A.gstride : lds_base;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     for (long long it = blockIdx.x; it < A.n; it += gridDim.x) {
@@ -248,8 +251,9 @@ extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy) {
 extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, const int32_t *items, long long N,
                                     long long n, int d, double alpha, double *g2, int32_t *df, double *p,
                                     uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
-                                    hipStream_t stream) {
-    CiArgs a{cols, dims, items, N, n, alpha, g2, df, p, indep, counts};
+                                    int32_t *gscratch, hipStream_t stream) {
+    CiArgs a{cols, dims, items, N, n, alpha, g2, df, p, indep, counts, gscratch, (long long)(lds_bytes / 4 + 1) & ~1ll};
+    if (gscratch) lds_bytes = 0;
     switch (d) {
 #define FBN_CI_CASE(DD)                                                                              \
     case DD:                                                                                         \

@@ -82,3 +82,24 @@ def test_constant_column_df0(tmp_path):
     ds = F.Dataset(columns=cols, dims=np.array([1, 3, 2], np.int32))
     r = F.IndependenceTest(ds).IndependenceResult(0, 1, (2,))
     assert r["df"] == 0 and r["is_independent"] and r["p_value"] == 1.0
+
+
+def test_large_contingency_table_global_fallback():
+    """|Z| = 7 over 4-state variables: 4^7 * 16 cells (1 MiB) exceed LDS -> global-memory tables;
+    counts, df, G^2 and p must still match the restatement."""
+    rng = np.random.default_rng(5)
+    cols = rng.integers(0, 4, size=(10, 3001), dtype=np.uint8)
+    cols[1] = (cols[0] + rng.integers(0, 2, size=3001)) % 4  # some dependence
+    dims = np.full(10, 4, np.int32)
+    ds = F.Dataset(columns=cols, dims=dims)
+    od = O.OracleDataset(columns=cols, dims=dims)
+    ci = F.IndependenceTest(ds)
+    items = np.array([[0, 1, 2, 3, 4, 5, 6, 7, 8], [2, 9, 0, 1, 3, 4, 5, 6, 7]], np.int32)
+    g2, df, p, ind = ci.run(items, 7)
+    for k, it in enumerate(items):
+        r = od.ci_test(int(it[0]), int(it[1]), [int(v) for v in it[2:]])
+        assert df[k] == r["df"] and bool(ind[k]) == r["is_independent"]
+        assert abs(g2[k] - r["g2"]) <= 1e-12 * max(1.0, abs(r["g2"]))
+        assert abs(p[k] - r["p_value"]) <= 1e-12
+    np.testing.assert_array_equal(ci.counts(0, 1, tuple(range(2, 9))),
+                                  od.ci_test(0, 1, list(range(2, 9)), counts=True)["counts"])
