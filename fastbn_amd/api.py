@@ -46,6 +46,8 @@ _SIGS = {
     "fbn_ci_run": [_vp, _vp, _i64, C.c_int, _dbl, _vp, _vp, _vp, _vp, _vp],
     "fbn_ci_counts": [_vp, C.c_int, C.c_int, _vp, C.c_int, _vp, _i64, _vp],
     "fbn_ci_last_kernel_ms": [_vp, _vp],
+    "fbn_ci_decision_margin": [_vp, _vp, _vp, C.c_int],
+    "fbn_pc_decision_margin": [_vp, _vp, _vp],
     "fbn_ci_ctx_destroy": [_vp],
     "fbn_pc_stable": [_vp, _dbl, C.c_int, C.c_int, _pp],
     "fbn_pc_num_levels": [_vp, _vp],
@@ -275,6 +277,12 @@ class JunctionTree:
     def run_device(self, d_evidence_ptr, ncases, d_labels_ptr, d_marg_ptr, stream_ptr=None):
         lib.fbn_jt_run_device(self._h, d_evidence_ptr, ncases, d_labels_ptr, d_marg_ptr, stream_ptr)
 
+    def decision_margin(self, reset=False):
+        """(min |p - alpha|, #tests with |p - alpha| < 1e-9) over the tests run since the last reset."""
+        m, near = C.c_double(), C.c_int64()
+        lib.fbn_ci_decision_margin(self._h, C.byref(m), C.byref(near), int(bool(reset)))
+        return m.value, near.value
+
     def last_kernel_ms(self):
         ms = C.c_float()
         lib.fbn_jt_last_kernel_ms(self._h, C.byref(ms))
@@ -349,6 +357,12 @@ class IndependenceTest:
                           C.byref(cells))
         return out
 
+    def decision_margin(self, reset=False):
+        """(min |p - alpha|, #tests with |p - alpha| < 1e-9) over the tests run since the last reset."""
+        m, near = C.c_double(), C.c_int64()
+        lib.fbn_ci_decision_margin(self._h, C.byref(m), C.byref(near), int(bool(reset)))
+        return m.value, near.value
+
     def last_kernel_ms(self):
         ms = C.c_float()
         lib.fbn_ci_last_kernel_ms(self._h, C.byref(ms))
@@ -386,6 +400,10 @@ class PCResult:
             lib.fbn_pc_oriented_edges(handle, _p(t))
         # (from, to, 1) arcs and (min, max, 0) undirected edges, in vec_edges order
         self.oriented = [tuple(map(int, x)) for x in t[:no.value]]
+        m, near = C.c_double(), C.c_int64()
+        lib.fbn_pc_decision_margin(handle, C.byref(m), C.byref(near))
+        # p-values are parity-unpinned; decisions this close to alpha are flagged
+        self.min_margin, self.near_alpha = m.value, near.value
 
     def GetSHD(self, bif_path):
         """BNSLComparison(ref_net, network).GetSHD() with ref_net loaded from a BIF file."""
@@ -445,6 +463,7 @@ class PCStable:
         lib.fbn_pc_timing(r, C.byref(tot), C.byref(ker))
         self.total_s, self.kernel_s = tot.value, ker.value
         self.num_ci_test = int(self.tests_per_level.sum())
+        self.min_margin, self.near_alpha = self.result.min_margin, self.result.near_alpha
         return self
 
     def GetSHD(self, bif_path):

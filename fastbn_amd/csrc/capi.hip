@@ -19,7 +19,7 @@ extern "C" hipError_t fbn_jt_launch(const JtOp *ops, int nops, const int32_t *au
 extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, const int32_t *items, long long N,
                                     long long n, int d, double alpha, double *g2, int32_t *df, double *p,
                                     uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
-                                    int32_t *gscratch, hipStream_t stream);
+                                    int32_t *gscratch, unsigned long long *stats, hipStream_t stream);
 extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy);
 extern "C" hipError_t fbn_jt_lds_launch(const JtOp *ops, int nops, const int32_t *aux, const double *initv,
                                         const uint64_t *dig, const int8_t *evid, int V, long long ncases, int SD,
@@ -125,6 +125,7 @@ struct fbn_ci_ctx {
     int64_t N = 0;
     std::vector<int32_t> dims;
     DevBuf cols, ddims, items, g2, df, p, indep, counts, scratch;
+    DevBuf stats;  // decision-margin log: {min |p - alpha| bits, #tests within 1e-9 of alpha}
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipStream_t stream = nullptr;  // the PC driver's rounds (pinned staging, one sync per round)
     float last_ms = 0.f;
@@ -155,6 +156,24 @@ static int PinnedEnsure(void *&ptr, size_t &have, size_t want) {
 struct fbn_pc_result {
     fbn::PCResultHost r;
 };
+
+static int CiResetMargin(fbn_ci_ctx *c) {
+    const unsigned long long init[2] = {0x7FF0000000000000ull /* +inf */, 0};
+    FBN_HIP(hipDeviceSynchronize());
+    FBN_HIP(hipMemcpy(c->stats.p, init, 16, hipMemcpyHostToDevice));
+    return FBN_OK;
+}
+
+static int CiReadMargin(fbn_ci_ctx *c, double *min_margin, int64_t *near_alpha) {
+    unsigned long long h[2];
+    FBN_HIP(hipDeviceSynchronize());
+    FBN_HIP(hipMemcpy(h, c->stats.p, 16, hipMemcpyDeviceToHost));
+    double m;
+    memcpy(&m, &h[0], 8);
+    if (min_margin) *min_margin = m;
+    if (near_alpha) *near_alpha = (int64_t)h[1];
+    return FBN_OK;
+}
 
 // =============================================================================================
 extern "C" {
@@ -696,6 +715,8 @@ int fbn_ci_dataset_upload(const uint8_t *cols, int nvars, int64_t nsamples, cons
     FBN_HIP(hipEventCreate(&c->ev0));
     FBN_HIP(hipEventCreate(&c->ev1));
     FBN_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    if ((rc = c->stats.ensure(16))) return rc;
+    if ((rc = CiResetMargin(c.get()))) return rc;
     *out = c.release();
     return FBN_OK;
 }
@@ -739,7 +760,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
     hipError_t e = fbn_ci_launch(c->cols.as<uint8_t>(), c->ddims.as<int32_t>(), c->items.as<int32_t>(), c->N, n, d,
                                  alpha, want_g2p ? c->g2.as<double>() : nullptr, c->df.as<int32_t>(),
                                  want_g2p ? c->p.as<double>() : nullptr, c->indep.as<uint8_t>(), counts_dev, lds, grid,
-                                 gscratch, s);
+                                 gscratch, c->stats.as<unsigned long long>(), s);
     if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci kernel launch: %s", hipGetErrorString(e));
     FBN_HIP(hipEventRecord(c->ev1, s));
     return FBN_OK;
@@ -781,6 +802,21 @@ int fbn_ci_counts(fbn_ci_ctx *c, int x, int y, const int32_t *z, int d, int32_t 
     return FBN_OK;
 }
 
+int fbn_ci_decision_margin(fbn_ci_ctx *c, double *min_margin, int64_t *near_alpha, int reset) {
+    if (!c) return SetError(FBN_ERR_ARG, "null pointer");
+    FBN_HIP(hipSetDevice(c->device));
+    int rc = CiReadMargin(c, min_margin, near_alpha);
+    if (rc == FBN_OK && reset) rc = CiResetMargin(c);
+    return rc;
+}
+
+int fbn_pc_decision_margin(const fbn_pc_result *r, double *min_margin, int64_t *near_alpha) {
+    if (!r) return SetError(FBN_ERR_ARG, "null pointer");
+    if (min_margin) *min_margin = r->r.min_margin;
+    if (near_alpha) *near_alpha = r->r.near_alpha;
+    return FBN_OK;
+}
+
 int fbn_ci_last_kernel_ms(const fbn_ci_ctx *c, float *ms) {
     if (!c || !ms) return SetError(FBN_ERR_ARG, "null pointer");
     *ms = c->last_ms;
@@ -799,8 +835,10 @@ int fbn_pc_stable(fbn_ci_ctx *c, double alpha, int depth, int group_size, fbn_pc
     auto r = std::unique_ptr<fbn_pc_result>(new (std::nothrow) fbn_pc_result());
     if (!r) return SetError(FBN_ERR_NOMEM, "out of memory");
     FBN_HIP(hipSetDevice(c->device));
-    int rc = fbn::RunPCStable(c, alpha, depth, group_size, r->r);
+    int rc = CiResetMargin(c);
     if (rc) return rc;
+    if ((rc = fbn::RunPCStable(c, alpha, depth, group_size, r->r))) return rc;
+    if ((rc = CiReadMargin(c, &r->r.min_margin, &r->r.near_alpha))) return rc;
     if ((rc = fbn::OrientPC(c->nvars, r->r))) return rc;  // StructLearnByPCStable steps 2-3
     *out = r.release();
     return FBN_OK;

@@ -30,6 +30,9 @@ struct CiArgs {
     int32_t *counts;  // optional: histogram of item 0
     int32_t *gscratch;  // non-null: tables too large for LDS live in global memory, one region per
     long long gstride;  // workgroup of gstride ints (same layout as the LDS one)
+    // decision-margin log: [0] = min over tests of |p - alpha| as IEEE bits
+    // (non-negative doubles order like their bit patterns), [1] = #tests with |p - alpha| < 1e-9
+    unsigned long long *stats;
 };
 
 // regularized upper incomplete gamma Q(a, x): series / modified Lentz continued fraction; the
@@ -231,6 +234,11 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
             if (A.df) A.df[it] = df;
             if (A.p) A.p[it] = p;
             if (A.indep) A.indep[it] = ind;
+            if (A.stats) {
+                const double m = fabs(p - A.alpha);
+                atomicMin(A.stats, (unsigned long long)__double_as_longlong(m));
+                if (m < 1e-9) atomicAdd(A.stats + 1, 1ull);
+            }
         }
         __syncthreads();
     }
@@ -251,8 +259,9 @@ extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy) {
 extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, const int32_t *items, long long N,
                                     long long n, int d, double alpha, double *g2, int32_t *df, double *p,
                                     uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
-                                    int32_t *gscratch, hipStream_t stream) {
-    CiArgs a{cols, dims, items, N, n, alpha, g2, df, p, indep, counts, gscratch, (long long)(lds_bytes / 4 + 1) & ~1ll};
+                                    int32_t *gscratch, unsigned long long *stats, hipStream_t stream) {
+    CiArgs a{cols, dims, items, N, n, alpha, g2, df, p, indep, counts, gscratch, (long long)(lds_bytes / 4 + 1) & ~1ll,
+             stats};
     if (gscratch) lds_bytes = 0;
     switch (d) {
 #define FBN_CI_CASE(DD)                                                                              \

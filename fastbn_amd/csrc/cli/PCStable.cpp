@@ -64,6 +64,9 @@ void PCStable::StructLearnCompData(fbn_dataset *dts, int group_size, int /*num_t
     std::cout << "# remaining edges = " << edges.size() << std::endl;
     std::cout << "pc-stable: " << s << " s pc-stable step 1: " << total_s << " s (device kernels " << kernel_s
               << " s)" << std::endl;
+    // decision-margin log (p-values are parity-unpinned)
+    fbn_pc_decision_margin(res, &min_margin, &near_alpha);
+    std::cout << "min |p - alpha| = " << min_margin << " (" << near_alpha << " decisions within 1e-9)" << std::endl;
     int no = 0;
     fbn_pc_num_oriented_edges(res, &no);
     std::vector<int32_t> tri(3 * (size_t)no + 3);

@@ -26,6 +26,8 @@ public:
     std::vector<std::pair<int, int>> edges;         // skeleton, vec_edges order
     std::map<std::pair<int, int>, std::set<int>> sepset;
     std::vector<int64_t> tests_per_level;
+    double min_margin = 0.0;  // min |p - alpha| over the run's tests
+    int64_t near_alpha = 0;   // tests with |p - alpha| < 1e-9
     std::vector<std::array<int, 3>> oriented;  // after steps 2-3: (from, to, 1) / (a, b, 0)
     // BNSLComparison(ref_net, network).GetSHD() with ref_net loaded from a BIF file (src/main.cpp:39-44)
     int GetSHD(const std::string &bif_path) const;

@@ -22,6 +22,9 @@ struct PCResultHost {
     // after orientation: (from, to, 1) arcs and (min, max, 0) undirected edges, vec_edges order
     std::vector<std::array<int, 3>> oriented;
     int num_nodes = 0;
+    // SURVEY §8(c) decision-margin log over every test evaluated (speculative ones included)
+    double min_margin = 0.0;
+    int64_t near_alpha = 0;
 };
 
 void CiCtxShape(const fbn_ci_ctx *c, int *nvars, int64_t *nsamples);

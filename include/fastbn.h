@@ -147,6 +147,11 @@ int fbn_ci_run(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alp
 int fbn_ci_counts(fbn_ci_ctx *c, int x, int y, const int32_t *z, int d, int32_t *counts, int64_t cap,
                   int64_t *cells);
 int fbn_ci_last_kernel_ms(const fbn_ci_ctx *c, float *ms);
+/* Decision-margin log: the p-value CDF (stats::pchisq, src/IndependenceTest.cpp:146,
+ * 268,355) is not pinned by any reference fixture, so every test records min |p - alpha| and counts
+ * tests with |p - alpha| < 1e-9 (a decision a different-but-accurate CDF could flip).  Covers every
+ * test run on `c` since the last reset (creation resets; `reset` != 0 resets after reading). */
+int fbn_ci_decision_margin(fbn_ci_ctx *c, double *min_margin, int64_t *near_alpha, int reset);
 int fbn_ci_ctx_destroy(fbn_ci_ctx *c);
 
 /* ------------------------------------------------------------------ PC-stable skeleton */
@@ -159,6 +164,8 @@ typedef struct fbn_pc_result fbn_pc_result;
  * reported counts are the reference's (t = 1) counts. */
 int fbn_pc_stable(fbn_ci_ctx *c, double alpha, int depth, int group_size, fbn_pc_result **out);
 int fbn_pc_num_levels(const fbn_pc_result *r, int *n);
+/* The run's decision-margin log (see fbn_ci_decision_margin): over every test of the skeleton phase. */
+int fbn_pc_decision_margin(const fbn_pc_result *r, double *min_margin, int64_t *near_alpha);
 int fbn_pc_level_tests(const fbn_pc_result *r, int64_t *tests /* [n_levels] */);
 int fbn_pc_level_launched(const fbn_pc_result *r, int64_t *tests /* device tests incl. speculation */);
 int fbn_pc_num_edges(const fbn_pc_result *r, int *n);

@@ -25,4 +25,5 @@ def test_cli_jt_alarm():
 def test_cli_pc_alarm_shd():
     out = run(["-a", "0", "-f1", "alarm/alarm.bif", "-f2", "alarm/alarm_s5000.txt"])
     assert "# of CI-tests is 5206" in out, out
+    assert "(0 decisions within 1e-9)" in out, out  # decision-margin log, SURVEY §8(c)
     assert "SHD = 5" in out, out

@@ -103,3 +103,22 @@ def test_large_contingency_table_global_fallback():
         assert abs(p[k] - r["p_value"]) <= 1e-12
     np.testing.assert_array_equal(ci.counts(0, 1, tuple(range(2, 9))),
                                   od.ci_test(0, 1, list(range(2, 9)), counts=True)["counts"])
+
+
+def test_decision_margin_log(alarm_ds, alarm_paths):
+    """every run logs min |p - alpha| (p-values are parity-unpinned).  The device
+    evaluates a superset of the reference's tests (speculation), so its minimum is <= the
+    reference-order minimum; ALARM-5000 has no decision within 1e-9 of alpha."""
+    od = O.OracleDataset(csv=alarm_paths["csv"])
+    ref = od.pc_stable(0.05, 1000, 1, keep_log=True)
+    ref_min = min(abs(t[6] - 0.05) for t in ref["log"] if t[5] != 0)
+    pc = F.PCStable(0.05, 1000).StructLearnCompData(alarm_ds)
+    assert pc.near_alpha == 0
+    assert 1e-9 < pc.min_margin <= ref_min * (1 + 1e-9)
+    # the ctx-level log over an explicit batch equals the minimum over the returned p-values
+    ci = F.IndependenceTest(alarm_ds)
+    items = np.array([[t[1], t[2]] + list(t[3]) for t in ref["log"] if len(t[3]) == 1], np.int32)
+    ci.decision_margin(reset=True)
+    _, _, p, _ = ci.run(items, 1)
+    m, near = ci.decision_margin()
+    assert m == np.min(np.abs(p - 0.05)) and near == 0
