@@ -21,6 +21,11 @@ extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, co
                                     uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
                                     int32_t *gscratch, unsigned long long *stats, hipStream_t stream);
 extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy);
+extern "C" hipError_t fbn_jt_virt_launch(const JtVClique *cls, const int32_t *aux, const double *initv,
+                                         const uint64_t *dig, const int32_t *order, const int32_t *vsel,
+                                         const int8_t *evid, double *marg, int32_t *labels, double *ws, int32_t *wsi,
+                                         int *flags, long long ncases, long long store_rows, int nc, int V, int SD,
+                                         int grid, hipStream_t stream);
 extern "C" hipError_t fbn_jt_lds_launch(const JtOp *ops, int nops, const int32_t *aux, const double *initv,
                                         const uint64_t *dig, const int8_t *evid, int V, long long ncases, int SD,
                                         double *marg, int32_t *labels, double *ws, int32_t *wsi, long long wave_entries,
@@ -96,6 +101,9 @@ struct fbn_jt_plan {
     fbn::JTPlanHost host;
     fbn::JTProgram prog;      // variant 1: whole case state in a global workspace
     fbn::JTProgramLDS lprog;  // variant 0 (default): clique in flight resident in LDS
+    fbn::JTProgramV vprog;    // variant 4: streamed (virtual) tables, large trees
+    bool v_ok = false;
+    DevBuf vcl, vaux, viv, vdig, vorder, vsel;
     int device = 0, num_cu = 0, waves_per_cu = 0, variant = -1, last_variant = -1;
     // plan-specialized kernel (variant 3)
     bool gen_eligible = false;
@@ -293,6 +301,15 @@ static int JtUpload(fbn_jt_plan *p) {
     if ((rc = up(p->laux, l.aux.data(), l.aux.size() * 4))) return rc;
     if ((rc = up(p->linitv, l.initv.data(), l.initv.size() * 8))) return rc;
     if ((rc = up(p->ldig, l.dig.data(), l.dig.size() * 8))) return rc;
+    if (p->v_ok) {
+        const auto &v = p->vprog;
+        if ((rc = up(p->vcl, v.cl.data(), v.cl.size() * sizeof(JtVClique)))) return rc;
+        if ((rc = up(p->vaux, v.aux.data(), v.aux.size() * 4))) return rc;
+        if ((rc = up(p->viv, v.initv.data(), v.initv.size() * 8))) return rc;
+        if ((rc = up(p->vdig, v.dig.data(), v.dig.size() * 8))) return rc;
+        if ((rc = up(p->vorder, v.order.data(), v.order.size() * 4))) return rc;
+        if ((rc = up(p->vsel, v.vsel.data(), v.vsel.size() * 4))) return rc;
+    }
     return FBN_OK;
 }
 
@@ -306,6 +323,10 @@ int fbn_jt_plan_create(const fbn_network *net, int device, fbn_jt_plan **out) {
     if (rc) return rc;
     rc = fbn::CompileJTProgramLDS(p->host, p->lprog);
     if (rc) return rc;
+    rc = fbn::CompileJTProgramV(p->host, p->vprog);
+    if (rc && rc != FBN_ERR_LIMIT) return rc;
+    p->v_ok = rc == FBN_OK;
+    if (!p->v_ok) p->vprog = fbn::JTProgramV();
     p->gen_eligible = fbn::JTCodegenEligible(p->host, nullptr);
     p->device = device;
     if (device >= 0) {  // device < 0: host-only plan (info / dump), runs fail with FBN_ERR_NODEV
@@ -387,9 +408,11 @@ int fbn_jt_set_waves_per_cu(fbn_jt_plan *p, int waves) {
 }
 
 int fbn_jt_set_variant(fbn_jt_plan *p, int variant) {
-    if (!p || variant < -1 || variant > 3)
-        return SetError(FBN_ERR_ARG, "variant must be -1 (auto), 0 (LDS), 1 (global), 2 (LDS, IEEE division) or 3 (specialized)");
+    if (!p || variant < -1 || variant > 4)
+        return SetError(FBN_ERR_ARG, "variant must be -1 (auto), 0 (LDS), 1 (global), 2 (LDS, IEEE division), "
+                                     "3 (specialized) or 4 (streamed)");
     if (variant == 3 && !p->gen_eligible) return SetError(FBN_ERR_ARG, "plan not eligible for the specialized kernel");
+    if (variant == 4 && !p->v_ok) return SetError(FBN_ERR_ARG, "plan not eligible for the streamed kernel");
     p->variant = variant;
     return FBN_OK;
 }
@@ -506,9 +529,11 @@ static int LaunchLds(fbn_jt_plan *p, DevBuf &ws, const int8_t *d_evidence, int64
     LdsGeometry(p, &wpc, &cap);
     const bool spill = cap < l.max_table;
     // fixup mode: flagged blocks are rare, one wave per CU scans the flags
-    const int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * (flags ? 1 : wpc));
+    int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * (flags ? 1 : wpc));
     const int64_t store_off = 0, den_off = l.store_entries, sep_off = den_off + nc, spill_off = sep_off + l.sep_entries;
     const int64_t wave_entries = spill_off + (spill ? l.max_table - cap : 0);
+    if (flags)  // fixup mode: at most ~2 GiB of workspace (large trees need ~100 MB per wave)
+        grid = (int)std::max<int64_t>(1, std::min<int64_t>(grid, ((int64_t)2 << 30) / (wave_entries * 64 * 8 + nc * 64 * 4)));
     const size_t ws_d = (size_t)grid * wave_entries * 64 * 8;
     const size_t ws_i = (size_t)grid * nc * 64 * 4;
     if ((rc = ws.ensure(ws_d + ws_i))) return rc;
@@ -578,6 +603,31 @@ int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, 
                                      p->ws.as<double>(), reinterpret_cast<int32_t *>(p->ws.as<char>() + ws_d),
                                      g.state_entries, nc, grid, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt kernel launch: %s", hipGetErrorString(e));
+    } else if (variant == 4) {
+        // streamed tables: small register footprint, many resident waves; the per-wave store holds
+        // only separator messages and denominators
+        const int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 8;
+        int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * wpc);
+        const auto &v = p->vprog;
+        const size_t per_wave_d = (size_t)v.store_rows * 64 * 8, per_wave_i = (size_t)(nc + V) * 64 * 4;
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+            const size_t have = free_b / 10 * 8 + p->ws.bytes;
+            grid = (int)std::max<int64_t>(1, std::min<int64_t>(grid, (int64_t)(have / (per_wave_d + per_wave_i))));
+        }
+        const size_t ws_d = (size_t)grid * per_wave_d;
+        if ((rc = p->ws.ensure(ws_d + (size_t)grid * per_wave_i))) return rc;
+        if ((rc = p->flags.ensure((size_t)nblk * 4))) return rc;
+        FBN_HIP(hipEventRecord(p->ev0, s));
+        hipError_t e = fbn_jt_virt_launch(p->vcl.as<JtVClique>(), p->vaux.as<int32_t>(), p->viv.as<double>(),
+                                          p->vdig.as<uint64_t>(), p->vorder.as<int32_t>(), p->vsel.as<int32_t>(),
+                                          d_evidence, marg, labels, p->ws.as<double>(),
+                                          reinterpret_cast<int32_t *>(p->ws.as<char>() + ws_d), p->flags.as<int>(),
+                                          ncases, v.store_rows, nc, V, SD, grid, s);
+        if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt kernel launch: %s", hipGetErrorString(e));
+        if (p->force_fixup) FBN_HIP(hipMemsetAsync(p->flags.p, 1, (size_t)nblk * 4, s));  // testing only
+        // exact recomputation of the blocks whose denominators left the fast-division range
+        if ((rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s))) return rc;
     } else if (variant == 3) {
         // one wave (64 cases) per SIMD: the clique in flight occupies the register file (+ LDS tail)
         int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 4;

@@ -88,6 +88,22 @@ struct JTProgramLDS {
 };
 int CompileJTProgramLDS(const JTPlanHost &plan, JTProgramLDS &prog);
 
+// streamed ("virtual table") variant, see jt_program.h
+struct JTProgramV {
+    std::vector<JtVClique> cl;
+    std::vector<int32_t> aux;
+    std::vector<double> initv;
+    std::vector<uint64_t> dig;
+    std::vector<int32_t> order;  // Collect (DFS post-order) then Distribute (DFS pre-order) clique ids
+    std::vector<int32_t> vsel;   // per variable {cand_off, ncand, out_off, dim} (candidates in aux)
+    int64_t store_rows = 0;      // per-wave fp64 rows: Collect messages, Distribute messages, denominators
+    int num_cliques = 0;
+    int sum_dom = 0;
+};
+// FBN_ERR_LIMIT when the plan does not fit the variant (a clique with > JT_V_MAX_CHILDREN children,
+// more than 8 * JT_MAX_DIG_WORDS variables, or tables beyond int32 indexing)
+int CompileJTProgramV(const JTPlanHost &plan, JTProgramV &prog);
+
 // plan-specialized kernel source (jt_codegen.cpp): eligibility and generation.  The generated
 // kernel's per-wave workspace holds wave_entries rows of 64 fp64 lanes; initv is its constant input.
 bool JTCodegenEligible(const JTPlanHost &plan, int64_t *entry_ops);

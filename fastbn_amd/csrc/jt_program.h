@@ -60,4 +60,25 @@ struct JtOp {
 
 #define JT_MAX_DIG_WORDS 4  // 8 variables per 64-bit word -> at most 32 variables per table
 
+// ---- streamed ("virtual table") variant, jt_virt.hip: clique tables are never stored.  Every
+// pass over a clique recomputes each entry from its initial potential, the case's evidence mask,
+// the messages already received and the normalization denominators of the earlier steps:
+//     c_0(e) = mask(e) ? init(e) : 0,   c_j(e) = (c_{j-1}(e) / D_{j-1}) * M_j(e),   D_j = sum_e c_j(e)
+// (M_1..M_k = child Collect messages in multiplication order, M_{k+1} = the parent's Distribute
+// message), i.e. exactly the values the reference stores after each multiply + Normalize.  Only
+// separator messages (and the per-step denominators) live in the per-wave global store.
+struct JtVClique {
+    int32_t T, nv, k, root;         // entries, variables, children, is the root
+    int32_t iv_off, dig_off, nw;    // initial potentials; digit words (nw uint64 per entry)
+    int32_t vars_off;               // aux: the clique's variable ids
+    int32_t map_off;                // aux: for each message j < k (+1 for the parent message unless
+                                    //      root) T int32 absolute store rows M_j(e)
+    int32_t den_row;                // store rows den_row + j hold D_j (j = 0 .. k+1)
+    int32_t up_Ts, up_col_row;      // upstream separator size, its Collect message rows
+    int32_t child_off;              // aux: k records {Ts, per, list_off, col_row, dis_row}
+    int32_t marg_off, nmarg;        // aux: nmarg records {out_off, dim, var, cum}
+    int32_t id;
+};
+#define JT_V_MAX_CHILDREN 6
+
 #endif

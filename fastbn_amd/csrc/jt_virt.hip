@@ -1,0 +1,343 @@
+// jt_virt.hip -- streamed ("virtual table") junction-tree kernel for large trees (Munin class).
+//
+// One lane = one evidence case, 64 cases per wave, persistent waves (as jt_kernels.hip).  No
+// clique table is ever stored: every pass over a clique recomputes each entry it needs as
+//     c_0(e) = mask(e) ? init(e) : 0,     c_j(e) = (c_{j-1}(e) / D_{j-1}) * M_j(e)
+// from the constant initial potentials (scalar loads shared by the 64 cases), the lane's evidence
+// mask, the messages received so far (M_1..M_k: child Collect messages in multiplication order,
+// M_{k+1}: the parent's Distribute message) and the per-step normalization sums D_j.  Those are the
+// values the reference stores after each `parent *= ext; Normalize()` (src/JunctionTree.cpp:829-941,
+// 1150-1238): the recomputation repeats the same IEEE operations on the same operands, so every
+// value is bit-identical, while HBM only sees separator messages (written once per case and
+// phase) instead of whole tables read and written once per operation.
+//
+// Passes per clique (entry order inside every bin = the reference's summation order):
+//   Collect:     SUM(L) for L = 0..k -> D_L  (post-evidence Normalize, then one per child round)
+//                SEPCOL: message to the parent, bins = upstream separator entries, e = q*Ts + j
+//                (SeparatorLevelCollectionOptimized, :1056-1148; the old separator is all ones)
+//   Distribute:  SUM(k+1) -> D_{k+1} after the parent's message (CliqueLevelDistributionOptimized)
+//                SEPDIS per child: bins = that separator's entries, divided by its Collect message
+//                with the reference's zero guard (SeparatorLevelDistribution, :700-816)
+//                MARG per variable and case whose chosen clique this is (GetProbabilitiesOneNode,
+//                :1392-1454; ArgMax, src/Inference.cpp:92-102)
+// Division by D_j uses Markstein's correctly rounded sequence (see jt_kernels.hip); a block any of
+// whose denominators leaves [2^-600, 2^600] is flagged and recomputed by the exact interpreter.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "jt_program.h"
+
+namespace {
+
+typedef __attribute__((address_space(1))) double gdouble;
+typedef __attribute__((address_space(1))) char gchar;
+typedef __attribute__((address_space(1))) int gint;
+
+struct Den {
+    double den, y;
+};
+__device__ __forceinline__ double mdiv(double x, const Den &d) {
+    const double q = x * d.y;
+    const double r = __builtin_fma(-d.den, q, x);
+    return __builtin_fma(r, d.y, q);
+}
+__device__ __forceinline__ bool den_ok(double d) { return d >= 0x1p-600 && d <= 0x1p+600; }
+
+// this wave's store: uniform row base (SGPRs) + this lane's byte offset (VGPR)
+#define ROW(r) (*(gdouble *)((gchar *)(Wb + (long long)(r) * 64) + lo))
+#define IROW(r) (*(gint *)((gchar *)(Ib + (long long)(r) * 64) + lo4))
+
+enum { K_SUM = 0, K_SEPCOL = 1, K_SEPDIS = 2, K_MARG = 3 };
+
+// uniform entry-sequence generators: entries bin by bin, each bin in increasing entry order
+struct SeqSum {
+    int n;
+    __device__ __forceinline__ int next() { return n++; }
+};
+struct SeqCol {  // bin j = upstream separator entry, e = q * Ts + j
+    int e, q, j, Ts, per;
+    __device__ __forceinline__ int next() {
+        const int r = e;
+        if (++q == per) q = 0, ++j, e = j;
+        else e += Ts;
+        return r;
+    }
+};
+struct SeqList {  // bins of `per` entries listed in aux
+    const int32_t *__restrict__ l;
+    int n;
+    __device__ __forceinline__ int next() { return l[n++]; }
+};
+struct SeqMarg {  // bin d = value of the variable: e = hi * bw + d * cum + lo
+    int e, lo, hi, d, cum, bw, nhi;
+    __device__ __forceinline__ int next() {
+        const int r = e;
+        if (++lo == cum) {
+            lo = 0;
+            if (++hi == nhi) hi = 0, ++d, e = d * cum;
+            else e += bw - cum + 1;
+        } else {
+            ++e;
+        }
+        return r;
+    }
+};
+
+struct Clq {
+    const double *__restrict__ iv;
+    const uint64_t *__restrict__ dg;
+    const int32_t *__restrict__ mp;
+    int T, nw;
+    uint64_t M[JT_MAX_DIG_WORDS], W[JT_MAX_DIG_WORDS];  // this lane's evidence pattern
+};
+
+constexpr int kU = 8;  // entries evaluated together (their message loads are in flight together)
+
+// one pass: chain of L message multiplies (+ final division by D_L when FINAL), accumulated bin
+// by bin; `flush(bin, acc)` consumes a finished bin.  Returns the last bin's sum (SUM passes).
+template <int L, bool FINAL, class Seq, class Flush>
+__device__ __forceinline__ double vpass(gdouble *Wb, unsigned lo, const Clq &C, const Den (&D)[JT_V_MAX_CHILDREN + 2],
+                                        Seq seq, int total, int per, Flush flush) {
+    double acc = 0.0;
+    int q = 0, bin = 0;
+    for (int n0 = 0; n0 < total; n0 += kU) {
+        const int cnt = total - n0 < kU ? total - n0 : kU;
+        int e[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) e[u] = (u < cnt) ? seq.next() : e[u > 0 ? u - 1 : 0];
+        double val[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int ee = e[u];
+            double w = C.iv[ee];
+            const uint64_t *d = C.dg + (size_t)ee * C.nw;
+            bool ok = (d[0] & C.M[0]) == C.W[0];
+            if (C.nw > 1) {
+#pragma unroll
+                for (int i = 1; i < JT_MAX_DIG_WORDS; ++i)
+                    if (i < C.nw) ok = ok && ((d[i] & C.M[i]) == C.W[i]);
+            }
+#pragma unroll
+            for (int j = 0; j < L; ++j) w = mdiv(w, D[j]) * ROW(C.mp[(size_t)j * C.T + ee]);
+            if (FINAL) w = mdiv(w, D[L]);
+            val[u] = ok ? w : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            if (u < cnt) {
+                acc += val[u];
+                if (++q == per) {
+                    flush(bin, acc);
+                    ++bin;
+                    q = 0;
+                    if (n0 + u + 1 < total) acc = 0.0;
+                }
+            }
+        }
+    }
+    return acc;
+}
+
+// dispatch on the (wave-uniform) chain length
+#define FBN_VDISPATCH(Lv, FINALv, CALL)         \
+    switch (Lv) {                               \
+    case 0: CALL(0, FINALv); break;             \
+    case 1: CALL(1, FINALv); break;             \
+    case 2: CALL(2, FINALv); break;             \
+    case 3: CALL(3, FINALv); break;             \
+    case 4: CALL(4, FINALv); break;             \
+    case 5: CALL(5, FINALv); break;             \
+    case 6: CALL(6, FINALv); break;             \
+    default: CALL(7, FINALv); break;            \
+    }
+
+__global__ __launch_bounds__(64) void jt_virt_kernel(
+    const JtVClique *__restrict__ cls, const int32_t *__restrict__ aux, const double *__restrict__ initv,
+    const uint64_t *__restrict__ dig, const int32_t *__restrict__ order, const int32_t *__restrict__ vsel,
+    const int8_t *__restrict__ evid, double *__restrict__ marg, int32_t *__restrict__ labels,
+    double *__restrict__ ws, int32_t *__restrict__ wsi, int *__restrict__ flags, long long ncases,
+    long long store_rows, int nc, int V, int SD) {
+    const int lane = threadIdx.x;
+    gdouble *Wb = (gdouble *)ws + (size_t)blockIdx.x * (size_t)store_rows * 64;
+    gint *Ib = (gint *)wsi + (size_t)blockIdx.x * (size_t)(nc + V) * 64;  // rows: red[c], then sel[v]
+    const unsigned lo = (unsigned)lane * 8u, lo4 = (unsigned)lane * 4u;
+
+    for (long long blk = blockIdx.x; blk * 64 < ncases; blk += gridDim.x) {
+        const long long cs = blk * 64 + lane;
+        const bool act = cs < ncases;
+        const long long csr = act ? cs : ncases - 1;
+        const int8_t *__restrict__ ev = evid + csr * V;
+        double *__restrict__ out = marg + csr * SD;
+        bool bad = false;
+
+        auto setup = [&](const JtVClique &q, Clq &C, int &nobs) {
+            C.iv = initv + q.iv_off;
+            C.dg = dig + q.dig_off;
+            C.mp = aux + q.map_off;
+            C.T = q.T;
+            C.nw = q.nw;
+#pragma unroll
+            for (int i = 0; i < JT_MAX_DIG_WORDS; ++i) C.M[i] = 0ull, C.W[i] = 0ull;
+            nobs = 0;
+            const int32_t *__restrict__ vars = aux + q.vars_off;
+            for (int j = 0; j < q.nv; ++j) {
+                const int x = ev[vars[j]];
+                const uint64_t m = x >= 0 ? (0xFFull << (8 * (j & 7))) : 0ull;
+                const uint64_t w = x >= 0 ? ((uint64_t)x << (8 * (j & 7))) : 0ull;
+                nobs += x >= 0;
+                const int wi = j >> 3;
+                if (wi == 0) C.M[0] |= m, C.W[0] |= w;
+                else if (wi == 1) C.M[1] |= m, C.W[1] |= w;
+                else if (wi == 2) C.M[2] |= m, C.W[2] |= w;
+                else C.M[3] |= m, C.W[3] |= w;
+            }
+        };
+
+        // ---------------- Collect, DFS post-order
+        for (int i = 0; i < nc; ++i) {
+            const JtVClique q = cls[order[i]];
+            Clq C;
+            int nobs;
+            setup(q, C, nobs);
+            IROW(q.id) = q.nv - nobs;  // variables left after the reference's table reduction
+            Den D[JT_V_MAX_CHILDREN + 2];
+#pragma unroll
+            for (int j = 0; j < JT_V_MAX_CHILDREN + 2; ++j) D[j] = Den{1.0, 1.0};
+            for (int L = 0; L <= q.k; ++L) {
+                double s = 0.0;
+                auto none = [](int, double) {};
+#define FBN_SUMCALL(Lc, F) s = vpass<Lc, F>(Wb, lo, C, D, SeqSum{0}, q.T, q.T, none)
+                FBN_VDISPATCH(L, false, FBN_SUMCALL);
+#undef FBN_SUMCALL
+                bad |= !den_ok(s);
+                ROW(q.den_row + L) = s;
+                // D is indexed by the uniform L: write every slot under a uniform compare so the
+                // array stays in registers
+#pragma unroll
+                for (int j = 0; j < JT_V_MAX_CHILDREN + 2; ++j)
+                    if (j == L) D[j] = Den{s, 1.0 / s};
+            }
+            if (!q.root) {
+                const int Ts = q.up_Ts, per = q.T / Ts, dst = q.up_col_row;
+                auto fl = [&](int j, double acc) { ROW(dst + j) = acc; };
+#define FBN_COLCALL(Lc, F) vpass<Lc, F>(Wb, lo, C, D, SeqCol{0, 0, 0, Ts, per}, q.T, per, fl)
+                FBN_VDISPATCH(q.k, true, FBN_COLCALL);
+#undef FBN_COLCALL
+            }
+        }
+
+        // ---------------- per variable: the clique GetProbabilitiesOneNode would use for this case
+        // (first candidate with the fewest remaining variables, src/JunctionTree.cpp:1412-1434)
+        for (int v = 0; v < V; ++v) {
+            const int32_t *__restrict__ cd = aux + vsel[4 * v];
+            const int ncand = vsel[4 * v + 1];
+            int sel = 0, best = 0x7fffffff;
+            for (int k = 0; k < ncand; ++k) {
+                const int r = IROW(cd[k]);
+                if (r < best) best = r, sel = cd[k];
+            }
+            IROW(nc + v) = sel | (best << 24);
+        }
+
+        // ---------------- Distribute, DFS pre-order, and the outputs
+        for (int i = 0; i < nc; ++i) {
+            const JtVClique q = cls[order[nc + i]];
+            Clq C;
+            int nobs;
+            setup(q, C, nobs);
+            Den D[JT_V_MAX_CHILDREN + 2];
+#pragma unroll
+            for (int j = 0; j < JT_V_MAX_CHILDREN + 2; ++j) {
+                D[j] = Den{1.0, 1.0};
+                if (j <= q.k) {
+                    const double s = ROW(q.den_row + j);
+                    D[j] = Den{s, 1.0 / s};
+                }
+            }
+            int Lf = q.k;
+            if (!q.root) {
+                double s = 0.0;
+                auto none = [](int, double) {};
+#define FBN_SUMCALL(Lc, F) s = vpass<Lc, F>(Wb, lo, C, D, SeqSum{0}, q.T, q.T, none)
+                FBN_VDISPATCH(q.k + 1, false, FBN_SUMCALL);
+#undef FBN_SUMCALL
+                bad |= !den_ok(s);
+                Lf = q.k + 1;
+#pragma unroll
+                for (int j = 0; j < JT_V_MAX_CHILDREN + 2; ++j)
+                    if (j == Lf) D[j] = Den{s, 1.0 / s};
+            }
+            // messages to the children
+            for (int ci = 0; ci < q.k; ++ci) {
+                const int32_t *__restrict__ rec = aux + q.child_off + 5 * ci;
+                const int Ts = rec[0], per = rec[1], col = rec[3], dis = rec[4];
+                const int32_t *__restrict__ lst = aux + rec[2];
+                auto fl = [&](int j, double acc) {
+                    const double old = ROW(col + j);
+                    ROW(dis + j) = (old == 0.0) ? 0.0 : acc / old;
+                };
+#define FBN_DISCALL(Lc, F) vpass<Lc, F>(Wb, lo, C, D, SeqList{lst, 0}, q.T, per, fl)
+                FBN_VDISPATCH(Lf, true, FBN_DISCALL);
+#undef FBN_DISCALL
+                (void)Ts;
+            }
+            // marginals of the variables whose chosen clique (for this case) is this one
+            for (int mi = 0; mi < q.nmarg; ++mi) {
+                const int32_t *__restrict__ rec = aux + q.marg_off + 4 * mi;
+                const int off = rec[0], dim = rec[1], var = rec[2], cum = rec[3];
+                const int sb = IROW(nc + var);
+                const bool mine = ((sb & 0xFFFFFF) == q.id) && ev[var] < 0;
+                if (__ballot(mine) == 0ull) continue;
+                const int best = sb >> 24;
+                double *__restrict__ o = out + off;
+                const bool wr = mine && act;
+                auto fl = [&](int d, double acc) {
+                    if (wr) o[d] = acc;
+                };
+                const int bw = dim * cum;
+                double tot = 0.0;
+                // bins = values of the variable, each in entry order; tot = sum of the bins in order
+                auto flt = [&](int d, double acc) {
+                    fl(d, acc);
+                    tot += acc;
+                };
+#define FBN_MARGCALL(Lc, F) vpass<Lc, F>(Wb, lo, C, D, SeqMarg{0, 0, 0, 0, cum, bw, q.T / bw}, q.T, q.T / dim, flt)
+                FBN_VDISPATCH(Lf, true, FBN_MARGCALL);
+#undef FBN_MARGCALL
+                if (wr) {
+                    if (var == 0) {  // label: ArgMax, strict '>' from 0 (src/Inference.cpp:92-102)
+                        int lab = 0;
+                        double mx = 0.0;
+                        for (int d = 0; d < dim; ++d) {
+                            const double p = (best == 1) ? o[d] : o[d] / tot;
+                            if (p > mx) mx = p, lab = d;
+                        }
+                        labels[cs] = lab;
+                    }
+                    for (int d = 0; d < dim; ++d) o[d] = o[d] / tot;
+                }
+            }
+        }
+        // evidence variables: probabilities stay 0 (their first slot is compared with -1 by the scorer)
+        if (act)
+            for (int v = 0; v < V; ++v)
+                if (ev[v] >= 0) {
+                    const int off = vsel[4 * v + 2], dim = vsel[4 * v + 3];
+                    for (int d = 0; d < dim; ++d) out[off + d] = 0.0;
+                }
+        const unsigned long long b = __ballot(bad);
+        if (lane == 0) flags[blk] = b != 0ull;
+    }
+}
+
+}  // namespace
+
+extern "C" hipError_t fbn_jt_virt_launch(const JtVClique *cls, const int32_t *aux, const double *initv,
+                                         const uint64_t *dig, const int32_t *order, const int32_t *vsel,
+                                         const int8_t *evid, double *marg, int32_t *labels, double *ws, int32_t *wsi,
+                                         int *flags, long long ncases, long long store_rows, int nc, int V, int SD,
+                                         int grid, hipStream_t stream) {
+    hipLaunchKernelGGL(jt_virt_kernel, dim3(grid), dim3(64), 0, stream, cls, aux, initv, dig, order, vsel, evid, marg,
+                       labels, ws, wsi, flags, ncases, store_rows, nc, V, SD);
+    return hipGetLastError();
+}

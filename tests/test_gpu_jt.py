@@ -78,7 +78,7 @@ def test_large_batch_vs_oracle_and_waves(jt, ojt):
     np.testing.assert_array_equal(marg, omarg)
     # both kernel variants; LDS variant with and without spilled rows (w=4 -> 80 LDS rows < 144)
     for variant, waves in ((0, 1), (0, 2), (0, 4), (0, 8), (1, 2), (1, 8), (2, 2), (2, 4), (3, 4), (3, 2),
-                           (-1, 0)):
+                           (4, 1), (4, 8), (-1, 0)):
         jt.set_variant(variant)
         jt.set_waves_per_cu(waves)
         lab2, marg2 = jt.infer(ev)
@@ -129,7 +129,44 @@ def test_synthetic_network(tmp_path):
     ev = synth.evidence_cases(net, 300, 40, seed=5)
     jt = F.JunctionTree(F.Network(p), device=0)
     olab, omarg = O.OracleJT(p).infer(ev)
-    for variant in (0, 1, 2):
+    for variant in (0, 1, 2, 4):
+        jt.set_variant(variant)
+        lab, marg = jt.infer(ev)
+        np.testing.assert_array_equal(lab, olab)
+        np.testing.assert_array_equal(marg, omarg)
+
+
+@pytest.mark.parametrize("which", ["alarm_1k", "alarm_rand"])
+def test_streamed_variant_vs_reference_fixture(jt, alarm_paths, which):
+    """Variant 4 (streamed tables) reproduces the reference's own dump bit for bit, also when every
+    block goes through the exact fixup pass."""
+    path = alarm_paths["test"] if which == "alarm_1k" else alarm_paths["rand"]
+    ev, _ = F.load_libsvm(path, 37)
+    rlab, rmarg, _, _ = read_ref_marg(os.path.join(GOLD, which + ".marg.gz"), jt.network.dims)
+    jt.set_variant(4)
+    try:
+        for force in (False, True):
+            jt.debug_force_fixup(force)
+            lab, marg = jt.infer(ev)
+            np.testing.assert_array_equal(lab, rlab)
+            np.testing.assert_array_equal(marg, rmarg)
+    finally:
+        jt.debug_force_fixup(False)
+        jt.set_variant(-1)
+
+
+def test_streamed_variant_munin_like(tmp_path):
+    """SURVEY 8(d) config 4 network (seeded Munin-like, 1041 variables, 20 % evidence): the streamed
+    kernel and the global interpreter agree with the oracle bit for bit on a ragged batch."""
+    from fastbn_amd import synth
+    p = str(tmp_path / "munin_like.xml")
+    synth.random_network(1041, seed=1041, window=12, path=p, name="munin_like")
+    net = synth.read_xmlbif(p)
+    ev = synth.evidence_cases(net, 136, 208, seed=20250131)
+    ev[0, :] = -1  # no evidence at all
+    olab, omarg = O.OracleJT(p).infer(ev)
+    jt = F.JunctionTree(F.Network(p), device=0)
+    for variant in (4, 1):
         jt.set_variant(variant)
         lab, marg = jt.infer(ev)
         np.testing.assert_array_equal(lab, olab)
