@@ -69,10 +69,12 @@ struct JtOp {
 // separator messages (and the per-step denominators) live in the per-wave global store.
 struct JtVClique {
     int32_t T, nv, k, root;         // entries, variables, children, is the root
-    int32_t iv_off, dig_off, nw;    // initial potentials; digit words (nw uint64 per entry)
-    int32_t vars_off;               // aux: the clique's variable ids
+    int32_t iv_off, dig_off, nw;    // initial potentials; entry digits: nw = 0 -> one packed 32-bit
+                                    // word per entry (uint32 index 2 * dig_off + e), else 8-bit
+                                    // digits in nw uint64 words per entry
+    int32_t vars_off;               // aux: per variable {id, digit shift, digit field mask}
     int32_t map_off;                // aux: for each message j < k (+1 for the parent message unless
-                                    //      root) T int32 absolute store rows M_j(e)
+                                    //      root) T int32 byte offsets (store row * 512) of M_j(e)
     int32_t den_row;                // store rows den_row + j hold D_j (j = 0 .. k+1)
     int32_t up_Ts, up_col_row;      // upstream separator size, its Collect message rows
     int32_t child_off;              // aux: k records {Ts, per, list_off, col_row, dis_row}

@@ -43,17 +43,23 @@ __device__ __forceinline__ double mdiv(double x, const Den &d) {
 }
 __device__ __forceinline__ bool den_ok(double d) { return d >= 0x1p-600 && d <= 0x1p+600; }
 
-// this wave's store: uniform row base (SGPRs) + this lane's byte offset (VGPR)
-#define ROW(r) (*(gdouble *)((gchar *)(Wb + (long long)(r) * 64) + lo))
+// The wave's store is addressed through a buffer resource: row offsets are the loads' scalar
+// soffset (no per-load 64-bit address arithmetic), the lane's byte offset the VGPR offset.
+struct Store {
+    __amdgpu_buffer_rsrc_t r;
+    unsigned lo;
+    __device__ __forceinline__ double ld(int byte_off) const {
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, lo, byte_off, 0));
+    }
+    __device__ __forceinline__ double row(int row) const { return ld(row * 512); }
+    __device__ __forceinline__ void st_row(int row, double v) const {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), r,
+                                              lo, row * 512, 0);
+    }
+};
 #define IROW(r) (*(gint *)((gchar *)(Ib + (long long)(r) * 64) + lo4))
 
-enum { K_SUM = 0, K_SEPCOL = 1, K_SEPDIS = 2, K_MARG = 3 };
-
 // uniform entry-sequence generators: entries bin by bin, each bin in increasing entry order
-struct SeqSum {
-    int n;
-    __device__ __forceinline__ int next() { return n++; }
-};
 struct SeqCol {  // bin j = upstream separator entry, e = q * Ts + j
     int e, q, j, Ts, per;
     __device__ __forceinline__ int next() {
@@ -85,71 +91,117 @@ struct SeqMarg {  // bin d = value of the variable: e = hi * bw + d * cum + lo
 
 struct Clq {
     const double *__restrict__ iv;
-    const uint64_t *__restrict__ dg;
+    const uint32_t *__restrict__ dg32;
+    const uint64_t *__restrict__ dg64;
     const int32_t *__restrict__ mp;
     int T, nw;
-    uint64_t M[JT_MAX_DIG_WORDS], W[JT_MAX_DIG_WORDS];  // this lane's evidence pattern
+    uint32_t M32, W32;                                  // this lane's evidence pattern (packed digits)
+    uint64_t M[JT_MAX_DIG_WORDS], W[JT_MAX_DIG_WORDS];  // (8-bit digits)
+};
+typedef Den Dens[JT_V_MAX_CHILDREN + 2];
+
+// entry e of the clique after L message multiplies (divided by D_L when FINAL), 0 if the entry
+// contradicts this lane's evidence
+template <int L, bool FINAL, bool P32>
+__device__ __forceinline__ double entry(const Store &S, const Clq &C, const Dens &D, int e) {
+    double w = C.iv[e];
+    bool ok;
+    if (P32) {
+        ok = (C.dg32[e] & C.M32) == C.W32;
+    } else {
+        const uint64_t *d = C.dg64 + (size_t)e * C.nw;
+        ok = (d[0] & C.M[0]) == C.W[0];
+#pragma unroll
+        for (int i = 1; i < JT_MAX_DIG_WORDS; ++i)
+            if (i < C.nw) ok = ok && ((d[i] & C.M[i]) == C.W[i]);
+    }
+#pragma unroll
+    for (int j = 0; j < L; ++j) w = mdiv(w, D[j]) * S.ld(C.mp[(size_t)j * C.T + e]);
+    if (FINAL) w = mdiv(w, D[L]);
+    return ok ? w : 0.0;
+}
+
+template <int L>
+struct Unroll {
+    static constexpr int U = L <= 3 ? 8 : 4;  // entries in flight together (SGPR budget)
 };
 
-constexpr int kU = 8;  // entries evaluated together (their message loads are in flight together)
+// normalization sum D_L = sum_e c_L(e), entry order (Normalize, src/PotentialTableBase.cpp:433-445)
+template <int L, bool P32>
+__device__ __forceinline__ double vsum(const Store &S, const Clq &C, const Dens &D) {
+    constexpr int U = Unroll<L>::U;
+    double acc = 0.0;
+    const int T = C.T;
+    int n0 = 0;
+    for (; n0 + U <= T; n0 += U) {
+        double val[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) val[u] = entry<L, false, P32>(S, C, D, n0 + u);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += val[u];
+    }
+    for (; n0 < T; ++n0) acc += entry<L, false, P32>(S, C, D, n0);
+    return acc;
+}
 
-// one pass: chain of L message multiplies (+ final division by D_L when FINAL), accumulated bin
-// by bin; `flush(bin, acc)` consumes a finished bin.  Returns the last bin's sum (SUM passes).
-template <int L, bool FINAL, class Seq, class Flush>
-__device__ __forceinline__ double vpass(gdouble *Wb, unsigned lo, const Clq &C, const Den (&D)[JT_V_MAX_CHILDREN + 2],
-                                        Seq seq, int total, int per, Flush flush) {
+// binned pass over the final table (after L multiplies, divided by D_L): bins of `per`
+// consecutive sequence entries; flush(bin, sum) consumes each finished bin
+template <int L, bool P32, class Seq, class Flush>
+__device__ __forceinline__ void vbins(const Store &S, const Clq &C, const Dens &D, Seq seq, int per, Flush flush) {
+    constexpr int U = Unroll<L>::U;
+    const int total = C.T;
     double acc = 0.0;
     int q = 0, bin = 0;
-    for (int n0 = 0; n0 < total; n0 += kU) {
-        const int cnt = total - n0 < kU ? total - n0 : kU;
-        int e[kU];
+    for (int n0 = 0; n0 < total; n0 += U) {
+        const int cnt = total - n0 < U ? total - n0 : U;
+        int e[U];
 #pragma unroll
-        for (int u = 0; u < kU; ++u) e[u] = (u < cnt) ? seq.next() : e[u > 0 ? u - 1 : 0];
-        double val[kU];
+        for (int u = 0; u < U; ++u) e[u] = (u < cnt) ? seq.next() : 0;
+        double val[U];
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const int ee = e[u];
-            double w = C.iv[ee];
-            const uint64_t *d = C.dg + (size_t)ee * C.nw;
-            bool ok = (d[0] & C.M[0]) == C.W[0];
-            if (C.nw > 1) {
+        for (int u = 0; u < U; ++u) val[u] = entry<L, true, P32>(S, C, D, e[u]);
 #pragma unroll
-                for (int i = 1; i < JT_MAX_DIG_WORDS; ++i)
-                    if (i < C.nw) ok = ok && ((d[i] & C.M[i]) == C.W[i]);
-            }
-#pragma unroll
-            for (int j = 0; j < L; ++j) w = mdiv(w, D[j]) * ROW(C.mp[(size_t)j * C.T + ee]);
-            if (FINAL) w = mdiv(w, D[L]);
-            val[u] = ok ? w : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
+        for (int u = 0; u < U; ++u) {
             if (u < cnt) {
                 acc += val[u];
                 if (++q == per) {
                     flush(bin, acc);
                     ++bin;
                     q = 0;
-                    if (n0 + u + 1 < total) acc = 0.0;
+                    acc = 0.0;
                 }
             }
         }
     }
-    return acc;
 }
 
-// dispatch on the (wave-uniform) chain length
-#define FBN_VDISPATCH(Lv, FINALv, CALL)         \
-    switch (Lv) {                               \
-    case 0: CALL(0, FINALv); break;             \
-    case 1: CALL(1, FINALv); break;             \
-    case 2: CALL(2, FINALv); break;             \
-    case 3: CALL(3, FINALv); break;             \
-    case 4: CALL(4, FINALv); break;             \
-    case 5: CALL(5, FINALv); break;             \
-    case 6: CALL(6, FINALv); break;             \
-    default: CALL(7, FINALv); break;            \
-    }
+// dispatch on the (wave-uniform) chain length and digit packing
+#define FBN_VDISPATCH(Lv, P32v, CALL)                                  \
+    do {                                                               \
+        if (P32v) {                                                    \
+            switch (Lv) {                                              \
+            case 0: CALL(0, true); break;                              \
+            case 1: CALL(1, true); break;                              \
+            case 2: CALL(2, true); break;                              \
+            case 3: CALL(3, true); break;                              \
+            case 4: CALL(4, true); break;                              \
+            case 5: CALL(5, true); break;                              \
+            case 6: CALL(6, true); break;                              \
+            default: CALL(7, true); break;                             \
+            }                                                          \
+        } else {                                                       \
+            switch (Lv) {                                              \
+            case 0: CALL(0, false); break;                             \
+            case 1: CALL(1, false); break;                             \
+            case 2: CALL(2, false); break;                             \
+            case 3: CALL(3, false); break;                             \
+            case 4: CALL(4, false); break;                             \
+            case 5: CALL(5, false); break;                             \
+            case 6: CALL(6, false); break;                             \
+            default: CALL(7, false); break;                            \
+            }                                                          \
+        }                                                              \
+    } while (0)
 
 __global__ __launch_bounds__(64) void jt_virt_kernel(
     const JtVClique *__restrict__ cls, const int32_t *__restrict__ aux, const double *__restrict__ initv,
@@ -158,9 +210,12 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
     double *__restrict__ ws, int32_t *__restrict__ wsi, int *__restrict__ flags, long long ncases,
     long long store_rows, int nc, int V, int SD) {
     const int lane = threadIdx.x;
-    gdouble *Wb = (gdouble *)ws + (size_t)blockIdx.x * (size_t)store_rows * 64;
+    Store S;
+    S.r = __builtin_amdgcn_make_buffer_rsrc((double *)ws + (size_t)blockIdx.x * (size_t)store_rows * 64, 0,
+                                            (int)(store_rows * 512), 0x00020000);
+    S.lo = (unsigned)lane * 8u;
     gint *Ib = (gint *)wsi + (size_t)blockIdx.x * (size_t)(nc + V) * 64;  // rows: red[c], then sel[v]
-    const unsigned lo = (unsigned)lane * 8u, lo4 = (unsigned)lane * 4u;
+    const unsigned lo4 = (unsigned)lane * 4u;
 
     for (long long blk = blockIdx.x; blk * 64 < ncases; blk += gridDim.x) {
         const long long cs = blk * 64 + lane;
@@ -172,24 +227,33 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
 
         auto setup = [&](const JtVClique &q, Clq &C, int &nobs) {
             C.iv = initv + q.iv_off;
-            C.dg = dig + q.dig_off;
+            C.dg32 = reinterpret_cast<const uint32_t *>(dig + q.dig_off);
+            C.dg64 = dig + q.dig_off;
             C.mp = aux + q.map_off;
             C.T = q.T;
             C.nw = q.nw;
+            C.M32 = 0u, C.W32 = 0u;
 #pragma unroll
             for (int i = 0; i < JT_MAX_DIG_WORDS; ++i) C.M[i] = 0ull, C.W[i] = 0ull;
             nobs = 0;
-            const int32_t *__restrict__ vars = aux + q.vars_off;
+            const int32_t *__restrict__ vr = aux + q.vars_off;
             for (int j = 0; j < q.nv; ++j) {
-                const int x = ev[vars[j]];
-                const uint64_t m = x >= 0 ? (0xFFull << (8 * (j & 7))) : 0ull;
-                const uint64_t w = x >= 0 ? ((uint64_t)x << (8 * (j & 7))) : 0ull;
+                const int x = ev[vr[3 * j]];
+                const int sh = vr[3 * j + 1];
+                const uint32_t fm = (uint32_t)vr[3 * j + 2];
                 nobs += x >= 0;
-                const int wi = j >> 3;
-                if (wi == 0) C.M[0] |= m, C.W[0] |= w;
-                else if (wi == 1) C.M[1] |= m, C.W[1] |= w;
-                else if (wi == 2) C.M[2] |= m, C.W[2] |= w;
-                else C.M[3] |= m, C.W[3] |= w;
+                if (q.nw == 0) {
+                    C.M32 |= x >= 0 ? fm << sh : 0u;
+                    C.W32 |= x >= 0 ? (uint32_t)x << sh : 0u;
+                } else {
+                    const uint64_t m = x >= 0 ? ((uint64_t)fm << sh) : 0ull;
+                    const uint64_t w = x >= 0 ? ((uint64_t)x << sh) : 0ull;
+                    const int wi = j >> 3;
+                    if (wi == 0) C.M[0] |= m, C.W[0] |= w;
+                    else if (wi == 1) C.M[1] |= m, C.W[1] |= w;
+                    else if (wi == 2) C.M[2] |= m, C.W[2] |= w;
+                    else C.M[3] |= m, C.W[3] |= w;
+                }
             }
         };
 
@@ -200,17 +264,17 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
             int nobs;
             setup(q, C, nobs);
             IROW(q.id) = q.nv - nobs;  // variables left after the reference's table reduction
-            Den D[JT_V_MAX_CHILDREN + 2];
+            const bool p32 = q.nw == 0;
+            Dens D;
 #pragma unroll
             for (int j = 0; j < JT_V_MAX_CHILDREN + 2; ++j) D[j] = Den{1.0, 1.0};
             for (int L = 0; L <= q.k; ++L) {
                 double s = 0.0;
-                auto none = [](int, double) {};
-#define FBN_SUMCALL(Lc, F) s = vpass<Lc, F>(Wb, lo, C, D, SeqSum{0}, q.T, q.T, none)
-                FBN_VDISPATCH(L, false, FBN_SUMCALL);
+#define FBN_SUMCALL(Lc, P) s = vsum<Lc, P>(S, C, D)
+                FBN_VDISPATCH(L, p32, FBN_SUMCALL);
 #undef FBN_SUMCALL
                 bad |= !den_ok(s);
-                ROW(q.den_row + L) = s;
+                S.st_row(q.den_row + L, s);
                 // D is indexed by the uniform L: write every slot under a uniform compare so the
                 // array stays in registers
 #pragma unroll
@@ -219,9 +283,9 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
             }
             if (!q.root) {
                 const int Ts = q.up_Ts, per = q.T / Ts, dst = q.up_col_row;
-                auto fl = [&](int j, double acc) { ROW(dst + j) = acc; };
-#define FBN_COLCALL(Lc, F) vpass<Lc, F>(Wb, lo, C, D, SeqCol{0, 0, 0, Ts, per}, q.T, per, fl)
-                FBN_VDISPATCH(q.k, true, FBN_COLCALL);
+                auto fl = [&](int j, double acc) { S.st_row(dst + j, acc); };
+#define FBN_COLCALL(Lc, P) vbins<Lc, P>(S, C, D, SeqCol{0, 0, 0, Ts, per}, per, fl)
+                FBN_VDISPATCH(q.k, p32, FBN_COLCALL);
 #undef FBN_COLCALL
             }
         }
@@ -245,21 +309,21 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
             Clq C;
             int nobs;
             setup(q, C, nobs);
-            Den D[JT_V_MAX_CHILDREN + 2];
+            const bool p32 = q.nw == 0;
+            Dens D;
 #pragma unroll
             for (int j = 0; j < JT_V_MAX_CHILDREN + 2; ++j) {
                 D[j] = Den{1.0, 1.0};
                 if (j <= q.k) {
-                    const double s = ROW(q.den_row + j);
+                    const double s = S.row(q.den_row + j);
                     D[j] = Den{s, 1.0 / s};
                 }
             }
             int Lf = q.k;
             if (!q.root) {
                 double s = 0.0;
-                auto none = [](int, double) {};
-#define FBN_SUMCALL(Lc, F) s = vpass<Lc, F>(Wb, lo, C, D, SeqSum{0}, q.T, q.T, none)
-                FBN_VDISPATCH(q.k + 1, false, FBN_SUMCALL);
+#define FBN_SUMCALL(Lc, P) s = vsum<Lc, P>(S, C, D)
+                FBN_VDISPATCH(q.k + 1, p32, FBN_SUMCALL);
 #undef FBN_SUMCALL
                 bad |= !den_ok(s);
                 Lf = q.k + 1;
@@ -270,16 +334,15 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
             // messages to the children
             for (int ci = 0; ci < q.k; ++ci) {
                 const int32_t *__restrict__ rec = aux + q.child_off + 5 * ci;
-                const int Ts = rec[0], per = rec[1], col = rec[3], dis = rec[4];
+                const int per = rec[1], col = rec[3], dis = rec[4];
                 const int32_t *__restrict__ lst = aux + rec[2];
                 auto fl = [&](int j, double acc) {
-                    const double old = ROW(col + j);
-                    ROW(dis + j) = (old == 0.0) ? 0.0 : acc / old;
+                    const double old = S.row(col + j);
+                    S.st_row(dis + j, (old == 0.0) ? 0.0 : acc / old);
                 };
-#define FBN_DISCALL(Lc, F) vpass<Lc, F>(Wb, lo, C, D, SeqList{lst, 0}, q.T, per, fl)
-                FBN_VDISPATCH(Lf, true, FBN_DISCALL);
+#define FBN_DISCALL(Lc, P) vbins<Lc, P>(S, C, D, SeqList{lst, 0}, per, fl)
+                FBN_VDISPATCH(Lf, p32, FBN_DISCALL);
 #undef FBN_DISCALL
-                (void)Ts;
             }
             // marginals of the variables whose chosen clique (for this case) is this one
             for (int mi = 0; mi < q.nmarg; ++mi) {
@@ -291,18 +354,15 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
                 const int best = sb >> 24;
                 double *__restrict__ o = out + off;
                 const bool wr = mine && act;
-                auto fl = [&](int d, double acc) {
-                    if (wr) o[d] = acc;
-                };
                 const int bw = dim * cum;
                 double tot = 0.0;
                 // bins = values of the variable, each in entry order; tot = sum of the bins in order
-                auto flt = [&](int d, double acc) {
-                    fl(d, acc);
+                auto fl = [&](int d, double acc) {
+                    if (wr) o[d] = acc;
                     tot += acc;
                 };
-#define FBN_MARGCALL(Lc, F) vpass<Lc, F>(Wb, lo, C, D, SeqMarg{0, 0, 0, 0, cum, bw, q.T / bw}, q.T, q.T / dim, flt)
-                FBN_VDISPATCH(Lf, true, FBN_MARGCALL);
+#define FBN_MARGCALL(Lc, P) vbins<Lc, P>(S, C, D, SeqMarg{0, 0, 0, 0, cum, bw, q.T / bw}, q.T / dim, fl)
+                FBN_VDISPATCH(Lf, p32, FBN_MARGCALL);
 #undef FBN_MARGCALL
                 if (wr) {
                     if (var == 0) {  // label: ArgMax, strict '>' from 0 (src/Inference.cpp:92-102)

@@ -56,7 +56,8 @@ int CompileJTProgramV(const JTPlanHost &plan, JTProgramV &prog) {
     for (int s = 0; s < ns; ++s) col_row[s] = rows, rows += plan.seps[s].size();
     for (int s = 0; s < ns; ++s) dis_row[s] = rows, rows += plan.seps[s].size();
     for (int c = 0; c < nc; ++c) den_row[c] = rows, rows += (int64_t)plan.clique_down[c].size() + 2;
-    if (rows > INT32_MAX / 64) return SetError(FBN_ERR_LIMIT, "junction tree too large for the streamed variant");
+    // message maps hold byte offsets into the per-wave store (buffer-load soffset)
+    if (rows > INT32_MAX / 512) return SetError(FBN_ERR_LIMIT, "junction tree too large for the streamed variant");
     prog.store_rows = rows;
 
     // DFS orders (iterative)
@@ -114,25 +115,58 @@ int CompileJTProgramV(const JTPlanHost &plan, JTProgramV &prog) {
         q.id = c;
         q.iv_off = (int32_t)prog.initv.size();
         prog.initv.insert(prog.initv.end(), t.pot.begin(), t.pot.end());
-        q.nw = std::max(1, (nv + 7) / 8);
-        q.dig_off = (int32_t)prog.dig.size();
-        for (int64_t e = 0; e < T; ++e) {
-            uint64_t w[JT_MAX_DIG_WORDS] = {0, 0, 0, 0};
-            int64_t r = e;
-            for (int j = 0; j < nv; ++j) {
-                w[j / 8] |= (uint64_t)(r / t.cum[j]) << (8 * (j % 8));
-                r %= t.cum[j];
-            }
-            for (int i = 0; i < q.nw; ++i) prog.dig.push_back(w[i]);
+        // digits of every entry for the evidence test: packed into one 32-bit word with the
+        // narrowest fields when they fit (nw = 0), else 8 bits per digit in nw 64-bit words
+        std::vector<int> sh(nv), fm(nv);
+        int bits = 0;
+        for (int j = 0; j < nv; ++j) {
+            int w = 1;
+            while ((1 << w) < t.dims[j]) ++w;
+            sh[j] = bits, fm[j] = (1 << w) - 1, bits += w;
         }
-        q.vars_off = (int32_t)prog.aux.size();
-        prog.aux.insert(prog.aux.end(), t.vars.begin(), t.vars.end());
+        const bool packed = bits <= 32 && nv <= 32;
+        q.nw = packed ? 0 : std::max(1, (nv + 7) / 8);
+        if (!packed) {
+            for (int j = 0; j < nv; ++j) sh[j] = 8 * (j % 8), fm[j] = 0xFF;
+            if (nv > 8 * JT_MAX_DIG_WORDS) return SetError(FBN_ERR_LIMIT, "clique with %d variables", nv);
+        }
+        q.dig_off = (int32_t)prog.dig.size();
+        if (packed) {  // two entries per uint64 slot: entry e at 32-bit word dig_off * 2 + e
+            std::vector<uint32_t> w32(T);
+            for (int64_t e = 0; e < T; ++e) {
+                uint32_t w = 0;
+                int64_t r = e;
+                for (int j = 0; j < nv; ++j) {
+                    w |= (uint32_t)(r / t.cum[j]) << sh[j];
+                    r %= t.cum[j];
+                }
+                w32[e] = w;
+            }
+            for (int64_t e = 0; e < T; e += 2)
+                prog.dig.push_back((uint64_t)w32[e] | ((e + 1 < T ? (uint64_t)w32[e + 1] : 0ull) << 32));
+        } else {
+            for (int64_t e = 0; e < T; ++e) {
+                uint64_t w[JT_MAX_DIG_WORDS] = {0, 0, 0, 0};
+                int64_t r = e;
+                for (int j = 0; j < nv; ++j) {
+                    w[j / 8] |= (uint64_t)(r / t.cum[j]) << sh[j];
+                    r %= t.cum[j];
+                }
+                for (int i = 0; i < q.nw; ++i) prog.dig.push_back(w[i]);
+            }
+        }
+        q.vars_off = (int32_t)prog.aux.size();  // records {var, shift, field mask}
+        for (int j = 0; j < nv; ++j) {
+            prog.aux.push_back(t.vars[j]);
+            prog.aux.push_back(sh[j]);
+            prog.aux.push_back(fm[j]);
+        }
         q.den_row = (int32_t)den_row[c];
         // message maps: child Collect messages in multiplication order, then the parent's message
         q.map_off = (int32_t)prog.aux.size();
         for (int s : plan.clique_down[c])
             for (int64_t e = 0; e < T; ++e)
-                prog.aux.push_back((int32_t)(col_row[s] + SubIndex(t, plan.seps[s], e)));
+                prog.aux.push_back((int32_t)((col_row[s] + SubIndex(t, plan.seps[s], e)) * 512));
         if (!root) {
             const int s = plan.clique_up[c];
             const int64_t Ts = plan.seps[s].size();
@@ -141,7 +175,7 @@ int CompileJTProgramV(const JTPlanHost &plan, JTProgramV &prog) {
             for (int64_t e = 0; e < T; ++e) {
                 if (SubIndex(t, plan.seps[s], e) != e % Ts)
                     return SetError(FBN_ERR_ARG, "internal: upstream separator of clique %d is not trailing", c);
-                prog.aux.push_back((int32_t)(dis_row[s] + e % Ts));
+                prog.aux.push_back((int32_t)((dis_row[s] + e % Ts) * 512));
             }
             q.up_Ts = (int32_t)Ts;
             q.up_col_row = (int32_t)col_row[s];
