@@ -24,8 +24,8 @@ extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy);
 extern "C" hipError_t fbn_jt_virt_launch(const JtVClique *cls, const int32_t *aux, const double *initv,
                                          const uint64_t *dig, const int32_t *order, const int32_t *vsel,
                                          const int8_t *evid, double *marg, int32_t *labels, double *ws, int32_t *wsi,
-                                         int *flags, long long ncases, long long store_rows, int nc, int V, int SD,
-                                         int grid, hipStream_t stream);
+                                         int *flags, long long ncases, long long store_rows, long long scratch_row,
+                                         int nc, int V, int SD, int grid, int dbg, hipStream_t stream);
 extern "C" hipError_t fbn_jt_lds_launch(const JtOp *ops, int nops, const int32_t *aux, const double *initv,
                                         const uint64_t *dig, const int8_t *evid, int V, long long ncases, int SD,
                                         double *marg, int32_t *labels, double *ws, int32_t *wsi, long long wave_entries,
@@ -623,11 +623,15 @@ int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, 
                                           p->vdig.as<uint64_t>(), p->vorder.as<int32_t>(), p->vsel.as<int32_t>(),
                                           d_evidence, marg, labels, p->ws.as<double>(),
                                           reinterpret_cast<int32_t *>(p->ws.as<char>() + ws_d), p->flags.as<int>(),
-                                          ncases, v.store_rows, nc, V, SD, grid, s);
+                                          ncases, v.store_rows, v.scratch_row, nc, V, SD, grid,
+                                          // diagnostic ablation only (tools/): skip pass types, wrong results
+                                          getenv("FBN_JT_VDEBUG") ? atoi(getenv("FBN_JT_VDEBUG")) : 0, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt kernel launch: %s", hipGetErrorString(e));
         if (p->force_fixup) FBN_HIP(hipMemsetAsync(p->flags.p, 1, (size_t)nblk * 4, s));  // testing only
         // exact recomputation of the blocks whose denominators left the fast-division range
-        if ((rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s))) return rc;
+        if (!getenv("FBN_JT_VDEBUG") &&
+            (rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s)))
+            return rc;
     } else if (variant == 3) {
         // one wave (64 cases) per SIMD: the clique in flight occupies the register file (+ LDS tail)
         int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 4;

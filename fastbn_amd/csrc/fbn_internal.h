@@ -96,7 +96,8 @@ struct JTProgramV {
     std::vector<uint64_t> dig;
     std::vector<int32_t> order;  // Collect (DFS post-order) then Distribute (DFS pre-order) clique ids
     std::vector<int32_t> vsel;   // per variable {cand_off, ncand, out_off, dim} (candidates in aux)
-    int64_t store_rows = 0;      // per-wave fp64 rows: Collect messages, Distribute messages, denominators
+    int64_t store_rows = 0;      // per-wave fp64 rows: Collect messages, Distribute messages, denominators,
+    int64_t scratch_row = 0;     // then the scratch table (rows scratch_row .. store_rows)
     int num_cliques = 0;
     int sum_dom = 0;
 };

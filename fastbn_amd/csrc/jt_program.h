@@ -80,6 +80,9 @@ struct JtVClique {
     int32_t child_off;              // aux: k records {Ts, per, list_off, col_row, dis_row}
     int32_t marg_off, nmarg;        // aux: nmarg records {out_off, dim, var, cum}
     int32_t id;
+    int32_t mat;                    // Distribute: the final table is written to the per-wave scratch
+                                    // rows once (fused into its normalization pass) and the separator
+                                    // and marginal passes read it instead of recomputing the chain
 };
 #define JT_V_MAX_CHILDREN 6
 

@@ -52,10 +52,11 @@ struct Store {
         return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, lo, byte_off, 0));
     }
     __device__ __forceinline__ double row(int row) const { return ld(row * 512); }
-    __device__ __forceinline__ void st_row(int row, double v) const {
+    __device__ __forceinline__ void st(int byte_off, double v) const {
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), r,
-                                              lo, row * 512, 0);
+                                              lo, byte_off, 0);
     }
+    __device__ __forceinline__ void st_row(int row, double v) const { st(row * 512, v); }
 };
 #define IROW(r) (*(gint *)((gchar *)(Ib + (long long)(r) * 64) + lo4))
 
@@ -126,9 +127,10 @@ struct Unroll {
     static constexpr int U = L <= 3 ? 8 : 4;  // entries in flight together (SGPR budget)
 };
 
-// normalization sum D_L = sum_e c_L(e), entry order (Normalize, src/PotentialTableBase.cpp:433-445)
-template <int L, bool P32>
-__device__ __forceinline__ double vsum(const Store &S, const Clq &C, const Dens &D) {
+// normalization sum D_L = sum_e c_L(e), entry order (Normalize, src/PotentialTableBase.cpp:433-445);
+// STORE: c_L(e) is also written to the scratch rows starting at byte offset scr
+template <int L, bool P32, bool STORE = false>
+__device__ __forceinline__ double vsum(const Store &S, const Clq &C, const Dens &D, int scr = 0) {
     constexpr int U = Unroll<L>::U;
     double acc = 0.0;
     const int T = C.T;
@@ -138,10 +140,44 @@ __device__ __forceinline__ double vsum(const Store &S, const Clq &C, const Dens 
 #pragma unroll
         for (int u = 0; u < U; ++u) val[u] = entry<L, false, P32>(S, C, D, n0 + u);
 #pragma unroll
-        for (int u = 0; u < U; ++u) acc += val[u];
+        for (int u = 0; u < U; ++u) {
+            acc += val[u];
+            if (STORE) S.st(scr + (n0 + u) * 512, val[u]);
+        }
     }
-    for (; n0 < T; ++n0) acc += entry<L, false, P32>(S, C, D, n0);
+    for (; n0 < T; ++n0) {
+        const double v = entry<L, false, P32>(S, C, D, n0);
+        acc += v;
+        if (STORE) S.st(scr + n0 * 512, v);
+    }
     return acc;
+}
+
+// binned pass over the stored table (scratch rows at byte offset scr), divided by Df
+template <class Seq, class Flush>
+__device__ __forceinline__ void vbins_scr(const Store &S, int scr, const Den &Df, int total, Seq seq, int per,
+                                          Flush flush) {
+    constexpr int U = 16;
+    double acc = 0.0;
+    int q = 0, bin = 0;
+    for (int n0 = 0; n0 < total; n0 += U) {
+        const int cnt = total - n0 < U ? total - n0 : U;
+        double val[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) val[u] = mdiv(S.ld(scr + ((u < cnt) ? seq.next() : 0) * 512), Df);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (u < cnt) {
+                acc += val[u];
+                if (++q == per) {
+                    flush(bin, acc);
+                    ++bin;
+                    q = 0;
+                    acc = 0.0;
+                }
+            }
+        }
+    }
 }
 
 // binned pass over the final table (after L multiplies, divided by D_L): bins of `per`
@@ -208,7 +244,7 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
     const uint64_t *__restrict__ dig, const int32_t *__restrict__ order, const int32_t *__restrict__ vsel,
     const int8_t *__restrict__ evid, double *__restrict__ marg, int32_t *__restrict__ labels,
     double *__restrict__ ws, int32_t *__restrict__ wsi, int *__restrict__ flags, long long ncases,
-    long long store_rows, int nc, int V, int SD) {
+    long long store_rows, long long scratch_row, int nc, int V, int SD, int dbg) {
     const int lane = threadIdx.x;
     Store S;
     S.r = __builtin_amdgcn_make_buffer_rsrc((double *)ws + (size_t)blockIdx.x * (size_t)store_rows * 64, 0,
@@ -216,6 +252,7 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
     S.lo = (unsigned)lane * 8u;
     gint *Ib = (gint *)wsi + (size_t)blockIdx.x * (size_t)(nc + V) * 64;  // rows: red[c], then sel[v]
     const unsigned lo4 = (unsigned)lane * 4u;
+    const int scr = (int)(scratch_row * 512);
 
     for (long long blk = blockIdx.x; blk * 64 < ncases; blk += gridDim.x) {
         const long long cs = blk * 64 + lane;
@@ -268,11 +305,19 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
             Dens D;
 #pragma unroll
             for (int j = 0; j < JT_V_MAX_CHILDREN + 2; ++j) D[j] = Den{1.0, 1.0};
+            // the last normalization pass of a clique with children also stores the table for SEPCOL
+            const bool cmat = !q.root && q.k > 0;
             for (int L = 0; L <= q.k; ++L) {
                 double s = 0.0;
-#define FBN_SUMCALL(Lc, P) s = vsum<Lc, P>(S, C, D)
-                FBN_VDISPATCH(L, p32, FBN_SUMCALL);
+                if (cmat && L == q.k) {
+#define FBN_SUMCALL(Lc, P) s = vsum<Lc, P, true>(S, C, D, scr)
+                    FBN_VDISPATCH(L, p32, FBN_SUMCALL);
 #undef FBN_SUMCALL
+                } else {
+#define FBN_SUMCALL(Lc, P) s = vsum<Lc, P>(S, C, D)
+                    FBN_VDISPATCH(L, p32, FBN_SUMCALL);
+#undef FBN_SUMCALL
+                }
                 bad |= !den_ok(s);
                 S.st_row(q.den_row + L, s);
                 // D is indexed by the uniform L: write every slot under a uniform compare so the
@@ -281,12 +326,16 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
                 for (int j = 0; j < JT_V_MAX_CHILDREN + 2; ++j)
                     if (j == L) D[j] = Den{s, 1.0 / s};
             }
-            if (!q.root) {
+            if (!q.root && !(dbg & 1)) {
                 const int Ts = q.up_Ts, per = q.T / Ts, dst = q.up_col_row;
                 auto fl = [&](int j, double acc) { S.st_row(dst + j, acc); };
+                if (cmat) {
+                    vbins_scr(S, scr, D[q.k], q.T, SeqCol{0, 0, 0, Ts, per}, per, fl);
+                } else {
 #define FBN_COLCALL(Lc, P) vbins<Lc, P>(S, C, D, SeqCol{0, 0, 0, Ts, per}, per, fl)
-                FBN_VDISPATCH(q.k, p32, FBN_COLCALL);
+                    FBN_VDISPATCH(q.k, p32, FBN_COLCALL);
 #undef FBN_COLCALL
+                }
             }
         }
 
@@ -304,7 +353,7 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
         }
 
         // ---------------- Distribute, DFS pre-order, and the outputs
-        for (int i = 0; i < nc; ++i) {
+        for (int i = 0; i < ((dbg & 16) ? 0 : nc); ++i) {
             const JtVClique q = cls[order[nc + i]];
             Clq C;
             int nobs;
@@ -320,11 +369,17 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
                 }
             }
             int Lf = q.k;
-            if (!q.root) {
+            if (!q.root && !(dbg & 8)) {
                 double s = 0.0;
-#define FBN_SUMCALL(Lc, P) s = vsum<Lc, P>(S, C, D)
-                FBN_VDISPATCH(q.k + 1, p32, FBN_SUMCALL);
+                if (q.mat) {
+#define FBN_SUMCALL(Lc, P) s = vsum<Lc, P, true>(S, C, D, scr)
+                    FBN_VDISPATCH(q.k + 1, p32, FBN_SUMCALL);
 #undef FBN_SUMCALL
+                } else {
+#define FBN_SUMCALL(Lc, P) s = vsum<Lc, P>(S, C, D)
+                    FBN_VDISPATCH(q.k + 1, p32, FBN_SUMCALL);
+#undef FBN_SUMCALL
+                }
                 bad |= !den_ok(s);
                 Lf = q.k + 1;
 #pragma unroll
@@ -332,20 +387,35 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
                     if (j == Lf) D[j] = Den{s, 1.0 / s};
             }
             // messages to the children
-            for (int ci = 0; ci < q.k; ++ci) {
+            for (int ci = 0; ci < ((dbg & 2) ? 0 : q.k); ++ci) {
                 const int32_t *__restrict__ rec = aux + q.child_off + 5 * ci;
-                const int per = rec[1], col = rec[3], dis = rec[4];
+                const int Ts = rec[0], per = rec[1], col = rec[3], dis = rec[4];
                 const int32_t *__restrict__ lst = aux + rec[2];
-                auto fl = [&](int j, double acc) {
-                    const double old = S.row(col + j);
-                    S.st_row(dis + j, (old == 0.0) ? 0.0 : acc / old);
-                };
+                // bin sums first (stores only), then the division by the Collect message
+                auto fl = [&](int j, double acc) { S.st_row(dis + j, acc); };
+                if (q.mat) {
+                    vbins_scr(S, scr, D[Lf], q.T, SeqList{lst, 0}, per, fl);
+                } else {
 #define FBN_DISCALL(Lc, P) vbins<Lc, P>(S, C, D, SeqList{lst, 0}, per, fl)
-                FBN_VDISPATCH(Lf, p32, FBN_DISCALL);
+                    FBN_VDISPATCH(Lf, p32, FBN_DISCALL);
 #undef FBN_DISCALL
+                }
+                // sep = tmp / old, zero-guarded (src/JunctionTree.cpp:700-816)
+                for (int j0 = 0; j0 < Ts; j0 += 8) {
+                    double a[8], o[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int j = j0 + u < Ts ? j0 + u : Ts - 1;
+                        a[u] = S.row(dis + j);
+                        o[u] = S.row(col + j);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u)
+                        if (j0 + u < Ts) S.st_row(dis + j0 + u, (o[u] == 0.0) ? 0.0 : a[u] / o[u]);
+                }
             }
             // marginals of the variables whose chosen clique (for this case) is this one
-            for (int mi = 0; mi < q.nmarg; ++mi) {
+            for (int mi = 0; mi < ((dbg & 4) ? 0 : q.nmarg); ++mi) {
                 const int32_t *__restrict__ rec = aux + q.marg_off + 4 * mi;
                 const int off = rec[0], dim = rec[1], var = rec[2], cum = rec[3];
                 const int sb = IROW(nc + var);
@@ -361,9 +431,13 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
                     if (wr) o[d] = acc;
                     tot += acc;
                 };
+                if (q.mat) {
+                    vbins_scr(S, scr, D[Lf], q.T, SeqMarg{0, 0, 0, 0, cum, bw, q.T / bw}, q.T / dim, fl);
+                } else {
 #define FBN_MARGCALL(Lc, P) vbins<Lc, P>(S, C, D, SeqMarg{0, 0, 0, 0, cum, bw, q.T / bw}, q.T / dim, fl)
-                FBN_VDISPATCH(Lf, p32, FBN_MARGCALL);
+                    FBN_VDISPATCH(Lf, p32, FBN_MARGCALL);
 #undef FBN_MARGCALL
+                }
                 if (wr) {
                     if (var == 0) {  // label: ArgMax, strict '>' from 0 (src/Inference.cpp:92-102)
                         int lab = 0;
@@ -395,9 +469,9 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
 extern "C" hipError_t fbn_jt_virt_launch(const JtVClique *cls, const int32_t *aux, const double *initv,
                                          const uint64_t *dig, const int32_t *order, const int32_t *vsel,
                                          const int8_t *evid, double *marg, int32_t *labels, double *ws, int32_t *wsi,
-                                         int *flags, long long ncases, long long store_rows, int nc, int V, int SD,
-                                         int grid, hipStream_t stream) {
+                                         int *flags, long long ncases, long long store_rows, long long scratch_row,
+                                         int nc, int V, int SD, int grid, int dbg, hipStream_t stream) {
     hipLaunchKernelGGL(jt_virt_kernel, dim3(grid), dim3(64), 0, stream, cls, aux, initv, dig, order, vsel, evid, marg,
-                       labels, ws, wsi, flags, ncases, store_rows, nc, V, SD);
+                       labels, ws, wsi, flags, ncases, store_rows, scratch_row, nc, V, SD, dbg);
     return hipGetLastError();
 }

@@ -56,6 +56,11 @@ int CompileJTProgramV(const JTPlanHost &plan, JTProgramV &prog) {
     for (int s = 0; s < ns; ++s) col_row[s] = rows, rows += plan.seps[s].size();
     for (int s = 0; s < ns; ++s) dis_row[s] = rows, rows += plan.seps[s].size();
     for (int c = 0; c < nc; ++c) den_row[c] = rows, rows += (int64_t)plan.clique_down[c].size() + 2;
+    // scratch table for the Distribute result of cliques with children (read by each SEPDIS pass)
+    prog.scratch_row = rows;
+    for (int c = 0; c < nc; ++c)
+        if (c != plan.root && !plan.clique_down[c].empty())
+            rows = std::max<int64_t>(rows, prog.scratch_row + plan.cliques[c].size());
     // message maps hold byte offsets into the per-wave store (buffer-load soffset)
     if (rows > INT32_MAX / 512) return SetError(FBN_ERR_LIMIT, "junction tree too large for the streamed variant");
     prog.store_rows = rows;
@@ -113,6 +118,7 @@ int CompileJTProgramV(const JTPlanHost &plan, JTProgramV &prog) {
         q.k = k;
         q.root = root ? 1 : 0;
         q.id = c;
+        q.mat = (!root && k > 0) ? 1 : 0;
         q.iv_off = (int32_t)prog.initv.size();
         prog.initv.insert(prog.initv.end(), t.pot.begin(), t.pot.end());
         // digits of every entry for the evidence test: packed into one 32-bit word with the
