@@ -262,7 +262,8 @@ class JunctionTree:
 
     def set_variant(self, v):
         """-1 auto, 0 = clique-in-LDS interpreter, 1 = global-workspace interpreter,
-        2 = LDS interpreter with IEEE division, 3 = plan-specialized kernel."""
+        2 = LDS interpreter with IEEE division, 3 = plan-specialized kernel,
+        4 = streamed (virtual-table) kernel for large trees."""
         lib.fbn_jt_set_variant(self._h, v)
 
     def infer(self, evidence, marginals=True):

@@ -21,6 +21,7 @@ extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, co
                                     uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
                                     int32_t *gscratch, unsigned long long *stats, hipStream_t stream);
 extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy);
+extern "C" int fbn_jt_virt_waves_per_group();
 extern "C" hipError_t fbn_jt_virt_launch(const JtVClique *cls, const int32_t *aux, const double *initv,
                                          const uint64_t *dig, const int32_t *order, const int32_t *vsel,
                                          const int8_t *evid, double *marg, int32_t *labels, double *ws, int32_t *wsi,
@@ -575,9 +576,10 @@ int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, 
     }
     int variant = p->variant;
     if (variant == -1) {
-        // specialized kernel when eligible; else the LDS interpreter while the largest clique fits
-        // LDS at >= 2 waves per CU, the global-workspace interpreter for spill-heavy (Munin-class) plans
+        // specialized kernel when eligible; else the streamed kernel (1.5-2x the interpreters on
+        // ALARM and the Munin-like network); the interpreters only for plans it cannot take
         if (p->gen_eligible && GenEnsure(p) == FBN_OK) variant = 3;
+        else if (p->v_ok) variant = 4;
         else variant = (p->lprog.max_table * 64 * 8 * 2 <= (int64_t)kLdsBytes) ? 0 : 1;
     }
     else if (variant == 3 && (rc = GenEnsure(p))) return rc;
@@ -606,17 +608,19 @@ int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, 
     } else if (variant == 4) {
         // streamed tables: small register footprint, many resident waves; the per-wave store holds
         // only separator messages and denominators
+        // workgroups of W lock-stepped waves, one 64-case block per wave
+        const int W = fbn_jt_virt_waves_per_group();
         const int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 8;
-        int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * wpc);
+        int grid = (int)std::min<int64_t>((nblk + W - 1) / W, std::max<int64_t>(1, (int64_t)p->num_cu * wpc / W));
         const auto &v = p->vprog;
         const size_t per_wave_d = (size_t)v.store_rows * 64 * 8, per_wave_i = (size_t)(nc + V) * 64 * 4;
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
             const size_t have = free_b / 10 * 8 + p->ws.bytes;
-            grid = (int)std::max<int64_t>(1, std::min<int64_t>(grid, (int64_t)(have / (per_wave_d + per_wave_i))));
+            grid = (int)std::max<int64_t>(1, std::min<int64_t>(grid, (int64_t)(have / (W * (per_wave_d + per_wave_i)))));
         }
-        const size_t ws_d = (size_t)grid * per_wave_d;
-        if ((rc = p->ws.ensure(ws_d + (size_t)grid * per_wave_i))) return rc;
+        const size_t ws_d = (size_t)grid * W * per_wave_d;
+        if ((rc = p->ws.ensure(ws_d + (size_t)grid * W * per_wave_i))) return rc;
         if ((rc = p->flags.ensure((size_t)nblk * 4))) return rc;
         FBN_HIP(hipEventRecord(p->ev0, s));
         hipError_t e = fbn_jt_virt_launch(p->vcl.as<JtVClique>(), p->vaux.as<int32_t>(), p->viv.as<double>(),

@@ -100,6 +100,14 @@ struct Clq {
     uint64_t M[JT_MAX_DIG_WORDS], W[JT_MAX_DIG_WORDS];  // (8-bit digits)
 };
 typedef Den Dens[JT_V_MAX_CHILDREN + 2];
+// D[j] for a wave-uniform runtime j without dynamic register indexing (which would go to scratch)
+__device__ __forceinline__ Den pick(const Dens &D, int j) {
+    Den r = D[0];
+#pragma unroll
+    for (int i = 1; i < JT_V_MAX_CHILDREN + 2; ++i)
+        if (i == j) r = D[i];
+    return r;
+}
 
 // entry e of the clique after L message multiplies (divided by D_L when FINAL), 0 if the entry
 // contradicts this lane's evidence
@@ -124,31 +132,74 @@ __device__ __forceinline__ double entry(const Store &S, const Clq &C, const Dens
 
 template <int L>
 struct Unroll {
-    static constexpr int U = L <= 3 ? 8 : 4;  // entries in flight together (SGPR budget)
+    static constexpr int U = L <= 3 ? 4 : 2;  // entries per pipeline stage (SGPR budget)
 };
 
+// one entry's operands, loaded ahead of its arithmetic: the masked initial potential and the L
+// messages (masking first is equivalent: 0 / D * m == +0 for the finite values involved)
+template <int L>
+struct Pre {
+    double w0;
+    double m[L > 0 ? L : 1];
+};
+template <int L, bool P32>
+__device__ __forceinline__ void pre_load(const Store &S, const Clq &C, int e, Pre<L> &p) {
+    const double iv = C.iv[e];
+    bool ok;
+    if (P32) {
+        ok = (C.dg32[e] & C.M32) == C.W32;
+    } else {
+        const uint64_t *d = C.dg64 + (size_t)e * C.nw;
+        ok = (d[0] & C.M[0]) == C.W[0];
+#pragma unroll
+        for (int i = 1; i < JT_MAX_DIG_WORDS; ++i)
+            if (i < C.nw) ok = ok && ((d[i] & C.M[i]) == C.W[i]);
+    }
+    p.w0 = ok ? iv : 0.0;
+#pragma unroll
+    for (int j = 0; j < L; ++j) p.m[j] = S.ld(C.mp[(size_t)j * C.T + e]);
+}
+template <int L>
+__device__ __forceinline__ double pre_eval(const Pre<L> &p, const Dens &D) {
+    double w = p.w0;
+#pragma unroll
+    for (int j = 0; j < L; ++j) w = mdiv(w, D[j]) * p.m[j];
+    return w;
+}
+
 // normalization sum D_L = sum_e c_L(e), entry order (Normalize, src/PotentialTableBase.cpp:433-445);
-// STORE: c_L(e) is also written to the scratch rows starting at byte offset scr
+// STORE: c_L(e) is also written to the scratch rows starting at byte offset scr.  Software
+// pipelined: the operands of chunk c+1 are in flight while chunk c is evaluated.
 template <int L, bool P32, bool STORE = false>
 __device__ __forceinline__ double vsum(const Store &S, const Clq &C, const Dens &D, int scr = 0) {
     constexpr int U = Unroll<L>::U;
     double acc = 0.0;
-    const int T = C.T;
-    int n0 = 0;
-    for (; n0 + U <= T; n0 += U) {
-        double val[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) val[u] = entry<L, false, P32>(S, C, D, n0 + u);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            acc += val[u];
-            if (STORE) S.st(scr + (n0 + u) * 512, val[u]);
-        }
+    const int T = C.T, npair = T / (2 * U);
+    Pre<L> A[U], B[U];
+#define FBN_LOADC(X, n0)                                                        \
+    _Pragma("unroll") for (int u = 0; u < U; ++u) pre_load<L, P32>(S, C, (n0) + u, X[u])
+#define FBN_EVALC(X, n0)                                                        \
+    _Pragma("unroll") for (int u = 0; u < U; ++u) {                             \
+        const double v = pre_eval<L>(X[u], D);                                  \
+        acc += v;                                                               \
+        if (STORE) S.st(scr + ((n0) + u) * 512, v);                             \
     }
-    for (; n0 < T; ++n0) {
-        const double v = entry<L, false, P32>(S, C, D, n0);
+    if (npair > 0) FBN_LOADC(A, 0);
+    for (int c = 0; c < npair; ++c) {
+        const int n0 = 2 * U * c;
+        FBN_LOADC(B, n0 + U);
+        FBN_EVALC(A, n0);
+        if (c + 1 < npair) FBN_LOADC(A, n0 + 2 * U);
+        FBN_EVALC(B, n0 + U);
+    }
+#undef FBN_LOADC
+#undef FBN_EVALC
+    for (int n = npair * 2 * U; n < T; ++n) {
+        Pre<L> X;
+        pre_load<L, P32>(S, C, n, X);
+        const double v = pre_eval<L>(X, D);
         acc += v;
-        if (STORE) S.st(scr + n0 * 512, v);
+        if (STORE) S.st(scr + n * 512, v);
     }
     return acc;
 }
@@ -239,22 +290,32 @@ __device__ __forceinline__ void vbins(const Store &S, const Clq &C, const Dens &
         }                                                              \
     } while (0)
 
-__global__ __launch_bounds__(64) void jt_virt_kernel(
+// A workgroup = kWaves waves, each with its own block of 64 cases and its own store; the waves
+// walk the same clique schedule in lock-step (one barrier per clique), so the constant stream of
+// the clique in flight (initial potentials, digits, message maps, entry lists) is fetched once
+// into the CU's scalar cache and shared by the group.
+constexpr int kWaves = 4;
+__global__ __launch_bounds__(64 * kWaves) void jt_virt_kernel(
     const JtVClique *__restrict__ cls, const int32_t *__restrict__ aux, const double *__restrict__ initv,
     const uint64_t *__restrict__ dig, const int32_t *__restrict__ order, const int32_t *__restrict__ vsel,
     const int8_t *__restrict__ evid, double *__restrict__ marg, int32_t *__restrict__ labels,
     double *__restrict__ ws, int32_t *__restrict__ wsi, int *__restrict__ flags, long long ncases,
     long long store_rows, long long scratch_row, int nc, int V, int SD, int dbg) {
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const long long gw = (long long)blockIdx.x * kWaves + wv;  // this wave's store
     Store S;
-    S.r = __builtin_amdgcn_make_buffer_rsrc((double *)ws + (size_t)blockIdx.x * (size_t)store_rows * 64, 0,
+    S.r = __builtin_amdgcn_make_buffer_rsrc((double *)ws + (size_t)gw * (size_t)store_rows * 64, 0,
                                             (int)(store_rows * 512), 0x00020000);
     S.lo = (unsigned)lane * 8u;
-    gint *Ib = (gint *)wsi + (size_t)blockIdx.x * (size_t)(nc + V) * 64;  // rows: red[c], then sel[v]
+    gint *Ib = (gint *)wsi + (size_t)gw * (size_t)(nc + V) * 64;  // rows: red[c], then sel[v]
     const unsigned lo4 = (unsigned)lane * 4u;
     const int scr = (int)(scratch_row * 512);
 
-    for (long long blk = blockIdx.x; blk * 64 < ncases; blk += gridDim.x) {
+    // every wave of the group runs the same number of iterations (barrier counts match); a wave
+    // past the last block recomputes the last case and writes nothing
+    for (long long grp = blockIdx.x; grp * kWaves * 64 < ncases; grp += gridDim.x) {
+        const long long blk = grp * kWaves + wv;
         const long long cs = blk * 64 + lane;
         const bool act = cs < ncases;
         const long long csr = act ? cs : ncases - 1;
@@ -306,7 +367,7 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
 #pragma unroll
             for (int j = 0; j < JT_V_MAX_CHILDREN + 2; ++j) D[j] = Den{1.0, 1.0};
             // the last normalization pass of a clique with children also stores the table for SEPCOL
-            const bool cmat = !q.root && q.k > 0;
+            const bool cmat = !q.root && q.k > 0 && !(dbg & 32);
             for (int L = 0; L <= q.k; ++L) {
                 double s = 0.0;
                 if (cmat && L == q.k) {
@@ -330,13 +391,14 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
                 const int Ts = q.up_Ts, per = q.T / Ts, dst = q.up_col_row;
                 auto fl = [&](int j, double acc) { S.st_row(dst + j, acc); };
                 if (cmat) {
-                    vbins_scr(S, scr, D[q.k], q.T, SeqCol{0, 0, 0, Ts, per}, per, fl);
+                    vbins_scr(S, scr, pick(D, q.k), q.T, SeqCol{0, 0, 0, Ts, per}, per, fl);
                 } else {
 #define FBN_COLCALL(Lc, P) vbins<Lc, P>(S, C, D, SeqCol{0, 0, 0, Ts, per}, per, fl)
                     FBN_VDISPATCH(q.k, p32, FBN_COLCALL);
 #undef FBN_COLCALL
                 }
             }
+            __syncthreads();
         }
 
         // ---------------- per variable: the clique GetProbabilitiesOneNode would use for this case
@@ -351,6 +413,7 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
             }
             IROW(nc + v) = sel | (best << 24);
         }
+        __syncthreads();
 
         // ---------------- Distribute, DFS pre-order, and the outputs
         for (int i = 0; i < ((dbg & 16) ? 0 : nc); ++i) {
@@ -371,7 +434,7 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
             int Lf = q.k;
             if (!q.root && !(dbg & 8)) {
                 double s = 0.0;
-                if (q.mat) {
+                if (q.mat && !(dbg & 64)) {
 #define FBN_SUMCALL(Lc, P) s = vsum<Lc, P, true>(S, C, D, scr)
                     FBN_VDISPATCH(q.k + 1, p32, FBN_SUMCALL);
 #undef FBN_SUMCALL
@@ -393,8 +456,8 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
                 const int32_t *__restrict__ lst = aux + rec[2];
                 // bin sums first (stores only), then the division by the Collect message
                 auto fl = [&](int j, double acc) { S.st_row(dis + j, acc); };
-                if (q.mat) {
-                    vbins_scr(S, scr, D[Lf], q.T, SeqList{lst, 0}, per, fl);
+                if (q.mat && !(dbg & 64)) {
+                    vbins_scr(S, scr, pick(D, Lf), q.T, SeqList{lst, 0}, per, fl);
                 } else {
 #define FBN_DISCALL(Lc, P) vbins<Lc, P>(S, C, D, SeqList{lst, 0}, per, fl)
                     FBN_VDISPATCH(Lf, p32, FBN_DISCALL);
@@ -431,8 +494,8 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
                     if (wr) o[d] = acc;
                     tot += acc;
                 };
-                if (q.mat) {
-                    vbins_scr(S, scr, D[Lf], q.T, SeqMarg{0, 0, 0, 0, cum, bw, q.T / bw}, q.T / dim, fl);
+                if (q.mat && !(dbg & 64)) {
+                    vbins_scr(S, scr, pick(D, Lf), q.T, SeqMarg{0, 0, 0, 0, cum, bw, q.T / bw}, q.T / dim, fl);
                 } else {
 #define FBN_MARGCALL(Lc, P) vbins<Lc, P>(S, C, D, SeqMarg{0, 0, 0, 0, cum, bw, q.T / bw}, q.T / dim, fl)
                     FBN_VDISPATCH(Lf, p32, FBN_MARGCALL);
@@ -451,6 +514,7 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
                     for (int d = 0; d < dim; ++d) o[d] = o[d] / tot;
                 }
             }
+            __syncthreads();
         }
         // evidence variables: probabilities stay 0 (their first slot is compared with -1 by the scorer)
         if (act)
@@ -460,18 +524,20 @@ __global__ __launch_bounds__(64) void jt_virt_kernel(
                     for (int d = 0; d < dim; ++d) out[off + d] = 0.0;
                 }
         const unsigned long long b = __ballot(bad);
-        if (lane == 0) flags[blk] = b != 0ull;
+        if (lane == 0 && blk * 64 < ncases) flags[blk] = b != 0ull;
     }
 }
 
 }  // namespace
+
+extern "C" int fbn_jt_virt_waves_per_group() { return kWaves; }
 
 extern "C" hipError_t fbn_jt_virt_launch(const JtVClique *cls, const int32_t *aux, const double *initv,
                                          const uint64_t *dig, const int32_t *order, const int32_t *vsel,
                                          const int8_t *evid, double *marg, int32_t *labels, double *ws, int32_t *wsi,
                                          int *flags, long long ncases, long long store_rows, long long scratch_row,
                                          int nc, int V, int SD, int grid, int dbg, hipStream_t stream) {
-    hipLaunchKernelGGL(jt_virt_kernel, dim3(grid), dim3(64), 0, stream, cls, aux, initv, dig, order, vsel, evid, marg,
+    hipLaunchKernelGGL(jt_virt_kernel, dim3(grid), dim3(64 * kWaves), 0, stream, cls, aux, initv, dig, order, vsel, evid, marg,
                        labels, ws, wsi, flags, ncases, store_rows, scratch_row, nc, V, SD, dbg);
     return hipGetLastError();
 }

@@ -108,11 +108,14 @@ int fbn_jt_score(const fbn_jt_plan *p, const double *marginals, const double *go
 int fbn_jt_last_kernel_ms(const fbn_jt_plan *p, float *ms);
 /* Tuning: persistent waves per CU (0 = default: as many as keep the largest clique in LDS). */
 int fbn_jt_set_waves_per_cu(fbn_jt_plan *p, int waves);
-/* Kernel variant: -1 = auto (default: 3 when eligible and its code object loads, else 0),
+/* Kernel variant: -1 = auto (default: 3 when eligible and its code object loads, else 4, else 0/1),
  * 0 = clique-in-LDS interpreter, 1 = whole case state in a global workspace interpreter,
  * 2 = variant 0 with the IEEE division sequence forced (ablation / testing),
  * 3 = plan-specialized kernel (jt_codegen.cpp; hiprtc or the on-disk code-object cache) followed
- *     by an exact-path fixup of the blocks it flags.  Selecting 3 fails if the plan is not eligible. */
+ *     by an exact-path fixup of the blocks it flags.  Selecting 3 fails if the plan is not eligible.
+ * 4 = streamed ("virtual table") kernel for large trees (jt_virt.hip): tables recomputed per pass
+ *     from initial potentials + received messages, only messages stored; exact-path fixup as 3.
+ *     Selecting 4 fails for plans it cannot take (a clique with more than 6 children, ...). */
 int fbn_jt_set_variant(fbn_jt_plan *p, int variant);
 /* Diagnostics (LDS variant): enable per-op-type s_memtime accounting for subsequent runs and/or
  * read the totals of the last run (cycles[10], op types JT_L_INIT..JT_L_EVZERO, summed over waves). */

@@ -9,5 +9,5 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
            "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_LDS SQ_INST_CYCLES_SMEM" \
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp -d $out/p$i -o pmc --output-format csv -- python tools/munin_once.py 32768 $v $w > $out/p$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $grp -d $out/p$i -o pmc --output-format csv -- python tools/munin_once.py ${4:-32768} $v $w > $out/p$i.log 2>&1
 done
