@@ -21,6 +21,12 @@ extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, co
                                     uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
                                     int32_t *gscratch, unsigned long long *stats, hipStream_t stream);
 extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy);
+extern "C" hipError_t fbn_ci_bits_build(const uint8_t *cols, const int32_t *dims, const int32_t *row0, long long N,
+                                        long long W, int nvars, uint32_t *bits, hipStream_t s);
+extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *dims, const int32_t *row0,
+                                         const int32_t *items, long long W, long long n, double alpha, double *g2,
+                                         int32_t *df, double *p, uint8_t *indep, int32_t *counts, int32_t *counts0,
+                                         unsigned long long *stats, int num_cu, hipStream_t s);
 extern "C" int fbn_jt_virt_waves_per_group();
 extern "C" hipError_t fbn_jt_virt_launch(const JtVClique *cls, const int32_t *aux, const double *initv,
                                          const uint64_t *dig, const int32_t *order, const int32_t *vsel,
@@ -135,6 +141,10 @@ struct fbn_ci_ctx {
     std::vector<int32_t> dims;
     DevBuf cols, ddims, items, g2, df, p, indep, counts, scratch;
     DevBuf stats;  // decision-margin log: {min |p - alpha| bits, #tests within 1e-9 of alpha}
+    // bit-sliced columns for marginal tests (ci_bits.hip), built on first use
+    DevBuf bits, brow, bcounts;
+    bool bits_ready = false;
+    int64_t bits_W = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipStream_t stream = nullptr;  // the PC driver's rounds (pinned staging, one sync per round)
     float last_ms = 0.f;
@@ -793,9 +803,48 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         if (dimz > (1 << 24)) return SetError(FBN_ERR_LIMIT, "test %lld: conditioning table too large", (long long)i);
         lds = std::max(lds, fbn_ci_lds_bytes((int)dimz, c->dims[it[0]], c->dims[it[1]]));
     }
+    int rc;
+    // marginal tests over variables with <= 4 states: popcounts of bit-sliced columns (ci_bits.hip)
+    bool bits_path = d == 0 && !getenv("FBN_CI_NO_BITS");
+    for (int64_t i = 0; bits_path && i < n; ++i)
+        bits_path = c->dims[items[2 * i]] <= 4 && c->dims[items[2 * i + 1]] <= 4;
+    if (bits_path) {
+        if (!c->bits_ready) {
+            const int64_t W = (c->N + 31) / 32;
+            std::vector<int32_t> row0(c->nvars);
+            int64_t rows = 0;
+            for (int v = 0; v < c->nvars; ++v) row0[v] = (int32_t)rows, rows += std::min(c->dims[v], 8);
+            if ((rc = c->bits.ensure((size_t)std::max<int64_t>(rows * W, 1) * 4))) return rc;
+            if ((rc = c->brow.ensure((size_t)c->nvars * 4))) return rc;
+            FBN_HIP(hipMemcpyAsync(c->brow.p, row0.data(), (size_t)c->nvars * 4, hipMemcpyHostToDevice, s));
+            hipError_t e = fbn_ci_bits_build(c->cols.as<uint8_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(), c->N,
+                                             W, c->nvars, c->bits.as<uint32_t>(), s);
+            if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci bits build: %s", hipGetErrorString(e));
+            c->bits_W = W;
+            c->bits_ready = true;
+        }
+        if ((rc = c->items.ensure((size_t)n * w * 4))) return rc;
+        if ((rc = c->indep.ensure((size_t)n))) return rc;
+        if ((rc = c->df.ensure((size_t)n * 4))) return rc;
+        if ((rc = c->bcounts.ensure((size_t)n * 16 * 4))) return rc;
+        if (want_g2p) {
+            if ((rc = c->g2.ensure((size_t)n * 8))) return rc;
+            if ((rc = c->p.ensure((size_t)n * 8))) return rc;
+        }
+        FBN_HIP(hipMemcpyAsync(c->items.p, items, (size_t)n * w * 4, hipMemcpyHostToDevice, s));
+        FBN_HIP(hipEventRecord(c->ev0, s));
+        hipError_t e = fbn_ci_bits_launch(c->bits.as<uint32_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(),
+                                          c->items.as<int32_t>(), c->bits_W, n, alpha,
+                                          want_g2p ? c->g2.as<double>() : nullptr, c->df.as<int32_t>(),
+                                          want_g2p ? c->p.as<double>() : nullptr, c->indep.as<uint8_t>(),
+                                          c->bcounts.as<int32_t>(), counts_dev, c->stats.as<unsigned long long>(),
+                                          c->num_cu, s);
+        if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci bits kernel launch: %s", hipGetErrorString(e));
+        FBN_HIP(hipEventRecord(c->ev1, s));
+        return FBN_OK;
+    }
     // tables beyond the LDS budget: the same layout in a per-workgroup global scratch region
     const bool global_tables = lds > 160 * 1024;
-    int rc;
     if ((rc = c->items.ensure((size_t)n * w * 4))) return rc;
     if ((rc = c->indep.ensure((size_t)n))) return rc;
     if ((rc = c->df.ensure((size_t)n * 4))) return rc;

@@ -1,0 +1,225 @@
+// ci_bits.hip -- marginal (level-0) G^2 tests on bit-sliced columns, gfx950.
+//
+// The level-0 sweep tests every pair of variables (499,500 tests at 1000 variables), each a
+// 2-D contingency table N[x][y] over all samples (Counts2D::FillTable, src/CellTable.cpp:430-455).
+// Instead of re-reading two byte columns and binning sample by sample, every column is stored
+// once as one bit mask per value (bit s of mask (v, a) = [sample s of v has value a], 32 samples
+// per word): N[a][b] = sum over words of popcount(mask(x, a) & mask(y, b)).  One wave per test,
+// lanes stride over the words, one v_bcnt (popcount + accumulate) per cell per 32 samples; the
+// masks are 1/8 of the byte columns per value (HBM / Infinity-cache traffic per test: (dx + dy)
+// rows of N/8 bytes), counts are exact integers.
+//
+// Phase 2 evaluates marginals, the adjusted df and G^2 with one lane per test (no idle lanes in
+// the log / incomplete-gamma code), in the reference's operation order: ComputeGSquareXY,
+// src/IndependenceTest.cpp:295-364 (same arithmetic as ci_kernels.hip, so the two kernels agree
+// bit for bit).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+// bits[(row0[v] + a) * W + w]: samples 32w .. 32w+31 of variable v equal to a
+__global__ __launch_bounds__(256) void ci_bits_build(const uint8_t *__restrict__ cols, const int32_t *__restrict__ dims,
+                                                     const int32_t *__restrict__ row0, long long N, long long W,
+                                                     int nvars, uint32_t *__restrict__ bits) {
+    const long long total = (long long)nvars * W;
+    for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+        const int v = (int)(t / W);
+        const long long w = t % W;
+        const uint8_t *c = cols + (size_t)v * N + 32 * w;
+        const int n = (int)((N - 32 * w) < 32 ? (N - 32 * w) : 32);
+        uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const int d = dims[v];
+        for (int s = 0; s < n; ++s) {
+            const int a = c[s];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) m[k] |= (a == k ? 1u : 0u) << s;
+        }
+        for (int a = 0; a < d; ++a) bits[(size_t)(row0[v] + a) * W + w] = m[a];
+    }
+}
+
+template <int DX, int DY>
+__device__ __forceinline__ void count_pair(const uint32_t *__restrict__ bx, const uint32_t *__restrict__ by, long long W,
+                                           int lane, int32_t *__restrict__ out) {
+    uint32_t cnt[DX * DY];
+#pragma unroll
+    for (int c = 0; c < DX * DY; ++c) cnt[c] = 0u;
+    long long w = lane;
+    for (; w + 64 < W; w += 128) {  // two words per lane in flight
+        uint32_t x0[DX], y0[DY], x1[DX], y1[DY];
+#pragma unroll
+        for (int a = 0; a < DX; ++a) x0[a] = bx[a * W + w], x1[a] = bx[a * W + w + 64];
+#pragma unroll
+        for (int b = 0; b < DY; ++b) y0[b] = by[b * W + w], y1[b] = by[b * W + w + 64];
+#pragma unroll
+        for (int a = 0; a < DX; ++a)
+#pragma unroll
+            for (int b = 0; b < DY; ++b)
+                cnt[a * DY + b] += __builtin_popcount(x0[a] & y0[b]) + __builtin_popcount(x1[a] & y1[b]);
+    }
+    for (; w < W; w += 64) {
+#pragma unroll
+        for (int a = 0; a < DX; ++a) {
+            const uint32_t xa = bx[a * W + w];
+#pragma unroll
+            for (int b = 0; b < DY; ++b) cnt[a * DY + b] += __builtin_popcount(xa & by[b * W + w]);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < DX * DY; ++c) {
+        uint32_t v = cnt[c];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+        cnt[c] = v;
+    }
+    if (lane < DX * DY) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int c = 0; c < DX * DY; ++c) v = lane == c ? cnt[c] : v;
+        out[lane] = (int32_t)v;
+    }
+}
+
+// phase 1: counts[t][16] (row-major dx x dy) of every test, one wave per test
+__global__ __launch_bounds__(256) void ci_bits_count(const uint32_t *__restrict__ bits, const int32_t *__restrict__ dims,
+                                                     const int32_t *__restrict__ row0, const int32_t *__restrict__ items,
+                                                     long long W, long long n, int32_t *__restrict__ counts) {
+    const int lane = threadIdx.x & 63;
+    const long long wave = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    for (long long t = wave; t < n; t += (long long)gridDim.x * 4) {
+        const int x = items[2 * t], y = items[2 * t + 1];
+        const int dx = dims[x], dy = dims[y];
+        const uint32_t *bx = bits + (size_t)row0[x] * W, *by = bits + (size_t)row0[y] * W;
+        int32_t *out = counts + t * 16;
+        switch (dx * 8 + dy) {
+#define FBN_PAIR(A, B) \
+    case A * 8 + B: count_pair<A, B>(bx, by, W, lane, out); break;
+            FBN_PAIR(1, 1) FBN_PAIR(1, 2) FBN_PAIR(1, 3) FBN_PAIR(1, 4)
+            FBN_PAIR(2, 1) FBN_PAIR(2, 2) FBN_PAIR(2, 3) FBN_PAIR(2, 4)
+            FBN_PAIR(3, 1) FBN_PAIR(3, 2) FBN_PAIR(3, 3) FBN_PAIR(3, 4)
+            FBN_PAIR(4, 1) FBN_PAIR(4, 2) FBN_PAIR(4, 3) FBN_PAIR(4, 4)
+#undef FBN_PAIR
+        default: break;  // the host only routes tests with dims <= 4 here
+        }
+    }
+}
+
+// regularized upper incomplete gamma: the same function as ci_kernels.hip's gamma_q
+__device__ double gamma_q_b(double a, double x) {
+    if (x <= 0.0) return 1.0;
+    const double lg = lgamma(a);
+    if (x < a + 1.0) {
+        double ap = a, sum = 1.0 / a, del = sum;
+        for (int n = 0; n < 2000; ++n) {
+            ap += 1.0;
+            del *= x / ap;
+            sum += del;
+            if (fabs(del) < fabs(sum) * 1e-17) break;
+        }
+        return 1.0 - sum * exp(-x + a * log(x) - lg);
+    }
+    const double tiny = 1e-300;
+    double b = x + 1.0 - a, c = 1.0 / tiny, d = 1.0 / b, h = d;
+    for (int i = 1; i < 2000; ++i) {
+        const double an = -i * (i - a);
+        b += 2.0;
+        d = an * d + b;
+        if (fabs(d) < tiny) d = tiny;
+        c = b + an / c;
+        if (fabs(c) < tiny) c = tiny;
+        d = 1.0 / d;
+        const double del = d * c;
+        h *= del;
+        if (fabs(del - 1.0) < 1e-17) break;
+    }
+    return exp(-x + a * log(x) - lg) * h;
+}
+
+// phase 2: one lane per test -- marginals, adjusted df, G^2 (reference loop order), p
+__global__ __launch_bounds__(256) void ci_bits_g2(const int32_t *__restrict__ counts, const int32_t *__restrict__ dims,
+                                                  const int32_t *__restrict__ items, long long n, double alpha,
+                                                  double *__restrict__ g2o, int32_t *__restrict__ dfo,
+                                                  double *__restrict__ po, uint8_t *__restrict__ indep,
+                                                  int32_t *__restrict__ counts0, unsigned long long *__restrict__ stats) {
+    for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t < n; t += (long long)gridDim.x * 256) {
+        const int dx = dims[items[2 * t]], dy = dims[items[2 * t + 1]];
+        const int32_t *h = counts + t * 16;
+        int ni[4], nj[4];
+        long total = 0;
+        int alx = 0, aly = 0;
+        for (int i = 0; i < dx; ++i) {
+            int s = 0;
+            for (int j = 0; j < dy; ++j) s += h[i * dy + j];
+            ni[i] = s;
+            alx += s > 0;
+            total += s;
+        }
+        for (int j = 0; j < dy; ++j) {
+            int s = 0;
+            for (int i = 0; i < dx; ++i) s += h[i * dy + j];
+            nj[j] = s;
+            aly += s > 0;
+        }
+        alx = alx >= 1 ? alx : 1;
+        aly = aly >= 1 ? aly : 1;
+        const int df = (alx - 1) * (aly - 1);
+        double g = 0.0;
+        if (total != 0) {
+            for (int i = 0; i < dx; ++i) {
+                const long sum_row = ni[i];
+                if (sum_row == 0) continue;
+                for (int j = 0; j < dy; ++j) {
+                    const long sum_col = nj[j];
+                    const long observed = h[i * dy + j];
+                    if (sum_col == 0 || observed == 0) continue;
+                    const double expected = (double)sum_col * (double)sum_row / (double)total;
+                    g += 2.0 * observed * log(observed / expected);
+                }
+            }
+        }
+        double p;
+        bool ind;
+        if (df == 0) {  // src/IndependenceTest.cpp:349-351
+            p = 1.0;
+            ind = true;
+        } else {
+            p = gamma_q_b(0.5 * df, 0.5 * g);
+            ind = p > alpha;
+        }
+        if (g2o) g2o[t] = g;
+        dfo[t] = df;
+        if (po) po[t] = p;
+        indep[t] = ind;
+        if (counts0 && t == 0)
+            for (int c = 0; c < dx * dy; ++c) counts0[c] = h[c];
+        if (stats) {
+            const double m = fabs(p - alpha);
+            atomicMin(stats, (unsigned long long)__double_as_longlong(m));
+            if (m < 1e-9) atomicAdd(stats + 1, 1ull);
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" hipError_t fbn_ci_bits_build(const uint8_t *cols, const int32_t *dims, const int32_t *row0, long long N,
+                                        long long W, int nvars, uint32_t *bits, hipStream_t s) {
+    const long long total = (long long)nvars * W;
+    const int grid = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
+    hipLaunchKernelGGL(ci_bits_build, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, cols, dims, row0, N, W, nvars, bits);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *dims, const int32_t *row0,
+                                         const int32_t *items, long long W, long long n, double alpha, double *g2,
+                                         int32_t *df, double *p, uint8_t *indep, int32_t *counts, int32_t *counts0,
+                                         unsigned long long *stats, int num_cu, hipStream_t s) {
+    const long long g1 = (n + 3) / 4, cap = (long long)num_cu * 8;
+    hipLaunchKernelGGL(ci_bits_count, dim3((int)(g1 < cap ? g1 : cap)), dim3(256), 0, s, bits, dims, row0, items, W, n,
+                       counts);
+    const long long g2g = (n + 255) / 256;
+    hipLaunchKernelGGL(ci_bits_g2, dim3((int)(g2g < cap ? g2g : cap)), dim3(256), 0, s, counts, dims, items, n, alpha,
+                       g2, df, p, indep, counts0, stats);
+    return hipGetLastError();
+}

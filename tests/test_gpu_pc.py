@@ -122,3 +122,36 @@ def test_decision_margin_log(alarm_ds, alarm_paths):
     _, _, p, _ = ci.run(items, 1)
     m, near = ci.decision_margin()
     assert m == np.min(np.abs(p - 0.05)) and near == 0
+
+
+@pytest.mark.parametrize("ns", [1, 31, 32, 33, 5000, 100003])
+def test_bit_sliced_marginal_tests_match_histogram_kernel(ns):
+    """Level-0 tests go through the bit-sliced popcount kernel (ci_bits.hip) when every variable
+    has <= 4 states; the byte-column histogram kernel (FBN_CI_NO_BITS) must give identical counts,
+    df, G^2 and p, and both must match the oracle.  Ragged sample counts, constant columns and
+    1..4-state variables."""
+    rng = np.random.default_rng(ns)
+    nv = 12
+    dims = np.array([1, 2, 3, 4, 2, 3, 4, 4, 2, 3, 1, 4], np.int32)
+    cols = np.stack([rng.integers(0, d, ns) for d in dims]).astype(np.uint8)
+    cols[5] = (cols[4] + cols[5]) % 3  # some dependence
+    items = np.array([[x, y] for x in range(nv) for y in range(x + 1, nv)], np.int32)
+    ci = F.IndependenceTest(F.Dataset(columns=cols, dims=dims), 0.05, device=0)
+    g2, df, p, ind = ci.run(items, 0)
+    cnt = ci.counts(1, 7)
+    os.environ["FBN_CI_NO_BITS"] = "1"
+    try:
+        g2h, dfh, ph, indh = ci.run(items, 0)
+        cnth = ci.counts(1, 7)
+    finally:
+        del os.environ["FBN_CI_NO_BITS"]
+    np.testing.assert_array_equal(cnt, cnth)
+    np.testing.assert_array_equal(df, dfh)
+    np.testing.assert_array_equal(g2, g2h)
+    np.testing.assert_array_equal(p, ph)
+    np.testing.assert_array_equal(ind, indh)
+    od = O.OracleDataset(columns=cols, dims=dims)
+    for k, (x, y) in enumerate(items[:20]):
+        r = od.ci_test(int(x), int(y))
+        assert df[k] == r["df"] and ind[k] == r["is_independent"]
+        assert abs(g2[k] - r["g2"]) <= 1e-12 * max(1.0, abs(r["g2"]))
