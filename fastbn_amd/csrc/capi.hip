@@ -982,7 +982,7 @@ int fbn_pc_sepsets(const fbn_pc_result *r, int32_t *buf, int64_t cap, int64_t *l
         if (buf && k < cap) buf[k] = v;
         ++k;
     };
-    for (auto &kv : r->r.sepset) {
+    for (auto &kv : r->r.sepset.entries()) {
         put(kv.first.first);
         put(kv.first.second);
         put((int32_t)kv.second.size());
@@ -1036,7 +1036,7 @@ int fbn_pc_orient_skeleton(int nvars, const int32_t *pairs, int nedges, const in
     for (int64_t k = 0; k < len;) {  // (x, y, m, z_0..z_{m-1}) records, as fbn_pc_sepsets writes them
         if (k + 3 > len || k + 3 + sepsets[k + 2] > len || sepsets[k + 2] < 0) return SetError(FBN_ERR_ARG, "bad sepset list");
         const int x = sepsets[k], y = sepsets[k + 1], m = sepsets[k + 2];
-        r->r.sepset[{std::min(x, y), std::max(x, y)}] = std::vector<int>(sepsets + k + 3, sepsets + k + 3 + m);
+        r->r.sepset.set({std::min(x, y), std::max(x, y)}, std::vector<int>(sepsets + k + 3, sepsets + k + 3 + m));
         k += 3 + m;
     }
     int rc = fbn::OrientPC(nvars, r->r);

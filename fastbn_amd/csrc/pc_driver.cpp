@@ -16,6 +16,8 @@
 // speculative: they are run but not counted, so the reported counts equal the reference's.
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <set>
@@ -224,15 +226,26 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
     for (int i = 0; i < n; ++i)
         for (int j = 0; j < n; ++j)
             if (i != j) adj[i].push_back(j);
+    const bool timing = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic: host phase times per level
     for (int d = 0; d == 0 || d < depth; ++d) {
         LevelOut out;
+        auto ta = std::chrono::steady_clock::now();
+        const double k0 = res.kernel_s;
         int rc = RunLevel(ctx, alpha, d, group_size, adj, edges, 0, edges.size(), out, res);
         if (rc) return rc;
+        auto tb = std::chrono::steady_clock::now();
         for (size_t e = 0; e < edges.size(); ++e)
-            if (out.removed[e]) res.sepset[edges[e]] = out.sep[e];
+            if (out.removed[e]) res.sepset.set(edges[e], std::move(out.sep[e]));
         res.tests_per_level.push_back(out.counted);
         res.launched_per_level.push_back(out.launched);
+        auto tc = std::chrono::steady_clock::now();
         ApplyRemovals(out.removed, edges, adj);
+        auto td = std::chrono::steady_clock::now();
+        if (timing)
+            fprintf(stderr, "pc level %d: run %.2f ms (kernels %.2f), sepsets %.2f ms, removals %.2f ms\n", d,
+                    std::chrono::duration<double, std::milli>(tb - ta).count(), (res.kernel_s - k0) * 1e3,
+                    std::chrono::duration<double, std::milli>(tc - tb).count(),
+                    std::chrono::duration<double, std::milli>(td - tc).count());
         if (d >= 1 && !ContinueAfter(adj, d)) break;
     }
     res.edges = edges;

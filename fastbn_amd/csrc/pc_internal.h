@@ -2,6 +2,7 @@
 #ifndef FBN_PC_INTERNAL_H
 #define FBN_PC_INTERNAL_H
 
+#include <algorithm>
 #include <array>
 #include <cstdint>
 #include <map>
@@ -13,9 +14,48 @@
 
 namespace fbn {
 
+// sepsets keyed by (min, max): appended per level, sorted once on first lookup / iteration (a
+// node-based map cost ~40 ms of host time for the ~500k marginal removals of a 1000-variable run)
+class SepsetMap {
+  public:
+    typedef std::pair<std::pair<int, int>, std::vector<int>> Entry;
+    void set(std::pair<int, int> key, std::vector<int> z) {
+        sorted_ = sorted_ && (v_.empty() || v_.back().first < key);
+        v_.emplace_back(key, std::move(z));
+    }
+    const std::vector<int> *find(std::pair<int, int> key) const {
+        sort();
+        auto it = std::lower_bound(v_.begin(), v_.end(), key,
+                                   [](const Entry &e, const std::pair<int, int> &k) { return e.first < k; });
+        return (it != v_.end() && it->first == key) ? &it->second : nullptr;
+    }
+    const std::vector<Entry> &entries() const {  // ascending keys
+        sort();
+        return v_;
+    }
+    size_t size() const { return v_.size(); }
+
+  private:
+    void sort() const {
+        if (sorted_) return;
+        // a key set twice keeps its last value (std::map assignment semantics)
+        std::stable_sort(v_.begin(), v_.end(), [](const Entry &a, const Entry &b) { return a.first < b.first; });
+        size_t o = 0;
+        for (size_t i = 0; i < v_.size(); ++i) {
+            if (o > 0 && v_[o - 1].first == v_[i].first) v_[o - 1] = std::move(v_[i]);
+            else if (o != i) v_[o++] = std::move(v_[i]);
+            else ++o;
+        }
+        v_.resize(o);
+        sorted_ = true;
+    }
+    mutable std::vector<Entry> v_;
+    mutable bool sorted_ = true;
+};
+
 struct PCResultHost {
     std::vector<std::pair<int, int>> edges;
-    std::map<std::pair<int, int>, std::vector<int>> sepset;
+    SepsetMap sepset;
     std::vector<int64_t> tests_per_level;     // reference (t = 1) counts
     std::vector<int64_t> launched_per_level;  // device tests incl. speculation
     double total_s = 0.0, kernel_s = 0.0;

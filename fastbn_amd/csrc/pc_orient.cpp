@@ -108,10 +108,10 @@ struct Graph {
 struct Orienter {
     Graph g;
     std::vector<std::set<int>> adj;  // skeleton adjacencies (fixed during orientation)
-    const std::map<std::pair<int, int>, std::vector<int>> &sepset;
+    const SepsetMap &sepset;
 
     Orienter(int n, const std::vector<std::pair<int, int>> &skeleton,
-             const std::map<std::pair<int, int>, std::vector<int>> &ss)
+             const SepsetMap &ss)
         : g(n), adj(n), sepset(ss) {
         for (auto &e : skeleton) {
             g.edges.push_back(Undirected(e.first, e.second));
@@ -124,9 +124,9 @@ struct Orienter {
         return IsAdjacentTo(a, b) && !g.IsDirectedFromTo(a, b) && !g.IsDirectedFromTo(b, a);
     }
     bool InSepset(int a, int c, int b) const {
-        auto it = sepset.find({a, c});
-        if (it == sepset.end()) return false;
-        return std::find(it->second.begin(), it->second.end(), b) != it->second.end();
+        const std::vector<int> *z = sepset.find({a, c});
+        if (!z) return false;
+        return std::find(z->begin(), z->end(), b) != z->end();
     }
 
     void VStructures() {
