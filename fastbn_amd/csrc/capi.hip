@@ -24,9 +24,9 @@ extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy);
 extern "C" hipError_t fbn_ci_bits_build(const uint8_t *cols, const int32_t *dims, const int32_t *row0, long long N,
                                         long long W, int nvars, uint32_t *bits, hipStream_t s);
 extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *dims, const int32_t *row0,
-                                         const int32_t *items, long long W, long long n, double alpha, double *g2,
-                                         int32_t *df, double *p, uint8_t *indep, int32_t *counts, int32_t *counts0,
-                                         unsigned long long *stats, int num_cu, hipStream_t s);
+                                         const int32_t *items, long long W, long long n, int d, double alpha,
+                                         double *g2, int32_t *df, double *p, uint8_t *indep, int32_t *counts,
+                                         int32_t *counts0, unsigned long long *stats, int num_cu, hipStream_t s);
 extern "C" int fbn_jt_virt_waves_per_group();
 extern "C" hipError_t fbn_jt_virt_launch(const JtVClique *cls, const int32_t *aux, const double *initv,
                                          const uint64_t *dig, const int32_t *order, const int32_t *vsel,
@@ -804,10 +804,11 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         lds = std::max(lds, fbn_ci_lds_bytes((int)dimz, c->dims[it[0]], c->dims[it[1]]));
     }
     int rc;
-    // marginal tests over variables with <= 4 states: popcounts of bit-sliced columns (ci_bits.hip)
-    bool bits_path = d == 0 && !getenv("FBN_CI_NO_BITS");
+    // tests with <= 1 conditioning variable over variables with <= 4 states: popcounts of
+    // bit-sliced columns (ci_bits.hip)
+    bool bits_path = d <= 1 && !getenv("FBN_CI_NO_BITS");
     for (int64_t i = 0; bits_path && i < n; ++i)
-        bits_path = c->dims[items[2 * i]] <= 4 && c->dims[items[2 * i + 1]] <= 4;
+        for (int j = 0; j < w; ++j) bits_path = bits_path && c->dims[items[w * i + j]] <= 4;
     if (bits_path) {
         if (!c->bits_ready) {
             const int64_t W = (c->N + 31) / 32;
@@ -826,7 +827,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         if ((rc = c->items.ensure((size_t)n * w * 4))) return rc;
         if ((rc = c->indep.ensure((size_t)n))) return rc;
         if ((rc = c->df.ensure((size_t)n * 4))) return rc;
-        if ((rc = c->bcounts.ensure((size_t)n * 16 * 4))) return rc;
+        if ((rc = c->bcounts.ensure((size_t)n * 64 * 4))) return rc;
         if (want_g2p) {
             if ((rc = c->g2.ensure((size_t)n * 8))) return rc;
             if ((rc = c->p.ensure((size_t)n * 8))) return rc;
@@ -834,7 +835,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         FBN_HIP(hipMemcpyAsync(c->items.p, items, (size_t)n * w * 4, hipMemcpyHostToDevice, s));
         FBN_HIP(hipEventRecord(c->ev0, s));
         hipError_t e = fbn_ci_bits_launch(c->bits.as<uint32_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(),
-                                          c->items.as<int32_t>(), c->bits_W, n, alpha,
+                                          c->items.as<int32_t>(), c->bits_W, n, d, alpha,
                                           want_g2p ? c->g2.as<double>() : nullptr, c->df.as<int32_t>(),
                                           want_g2p ? c->p.as<double>() : nullptr, c->indep.as<uint8_t>(),
                                           c->bcounts.as<int32_t>(), counts_dev, c->stats.as<unsigned long long>(),

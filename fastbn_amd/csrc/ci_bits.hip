@@ -1,4 +1,4 @@
-// ci_bits.hip -- marginal (level-0) G^2 tests on bit-sliced columns, gfx950.
+// ci_bits.hip -- G^2 tests with at most one conditioning variable on bit-sliced columns, gfx950.
 //
 // The level-0 sweep tests every pair of variables (499,500 tests at 1000 variables), each a
 // 2-D contingency table N[x][y] over all samples (Counts2D::FillTable, src/CellTable.cpp:430-455).
@@ -6,8 +6,9 @@
 // once as one bit mask per value (bit s of mask (v, a) = [sample s of v has value a], 32 samples
 // per word): N[a][b] = sum over words of popcount(mask(x, a) & mask(y, b)).  One wave per test,
 // lanes stride over the words, one v_bcnt (popcount + accumulate) per cell per 32 samples; the
-// masks are 1/8 of the byte columns per value (HBM / Infinity-cache traffic per test: (dx + dy)
-// rows of N/8 bytes), counts are exact integers.
+// masks are 1/8 of the byte columns per value (HBM / Infinity-cache traffic per test: (dx + dy
+// [+ dz]) rows of N/8 bytes), counts are exact integers.  Level 1 (one conditioning variable z)
+// adds z's masks: N[c][a][b] = sum popcount(x_a & y_b & z_c) (Counts3D, src/CellTable.cpp:226-291).
 //
 // Phase 2 evaluates marginals, the adjusted df and G^2 with one lane per test (no idle lanes in
 // the log / incomplete-gamma code), in the reference's operation order: ComputeGSquareXY,
@@ -39,62 +40,82 @@ __global__ __launch_bounds__(256) void ci_bits_build(const uint8_t *__restrict__
     }
 }
 
-template <int DX, int DY>
-__device__ __forceinline__ void count_pair(const uint32_t *__restrict__ bx, const uint32_t *__restrict__ by, long long W,
-                                           int lane, int32_t *__restrict__ out) {
-    uint32_t cnt[DX * DY];
+// counts of one test: N[z][a][b] += popcount(x_a & y_b & z_c) over this lane's words, then a
+// wave reduction; cells (c * DX + a) * DY + b (Counts3D layout, src/CellTable.cpp:277-281).
+// DZ = 1 for marginal tests; conditional tests (one conditioning variable) use DZ = 4 with the
+// masks of absent values zero (their cells stay 0 and are never read).
+template <int DX, int DY, int DZ>
+__device__ __forceinline__ void count_test(const uint32_t *__restrict__ bx, const uint32_t *__restrict__ by,
+                                           const uint32_t *__restrict__ bz, int dz, long long W, int lane,
+                                           int32_t *__restrict__ out) {
+    constexpr int NC = DX * DY * DZ;
+    uint32_t cnt[NC];
 #pragma unroll
-    for (int c = 0; c < DX * DY; ++c) cnt[c] = 0u;
+    for (int c = 0; c < NC; ++c) cnt[c] = 0u;
     long long w = lane;
-    for (; w + 64 < W; w += 128) {  // two words per lane in flight
-        uint32_t x0[DX], y0[DY], x1[DX], y1[DY];
+    auto word = [&](long long ww) {
+        uint32_t x[DX], y[DY], z[DZ];
 #pragma unroll
-        for (int a = 0; a < DX; ++a) x0[a] = bx[a * W + w], x1[a] = bx[a * W + w + 64];
+        for (int a = 0; a < DX; ++a) x[a] = bx[a * W + ww];
 #pragma unroll
-        for (int b = 0; b < DY; ++b) y0[b] = by[b * W + w], y1[b] = by[b * W + w + 64];
+        for (int b = 0; b < DY; ++b) y[b] = by[b * W + ww];
+#pragma unroll
+        for (int c = 0; c < DZ; ++c) z[c] = (DZ == 1) ? 0xFFFFFFFFu : (c < dz ? bz[c * W + ww] : 0u);
 #pragma unroll
         for (int a = 0; a < DX; ++a)
 #pragma unroll
-            for (int b = 0; b < DY; ++b)
-                cnt[a * DY + b] += __builtin_popcount(x0[a] & y0[b]) + __builtin_popcount(x1[a] & y1[b]);
+            for (int b = 0; b < DY; ++b) {
+                const uint32_t xy = x[a] & y[b];
+#pragma unroll
+                for (int c = 0; c < DZ; ++c) cnt[(c * DX + a) * DY + b] += __builtin_popcount(xy & z[c]);
+            }
+    };
+    for (; w + 64 < W; w += 128) {  // two words per lane in flight
+        word(w);
+        word(w + 64);
     }
-    for (; w < W; w += 64) {
+    for (; w < W; w += 64) word(w);
 #pragma unroll
-        for (int a = 0; a < DX; ++a) {
-            const uint32_t xa = bx[a * W + w];
-#pragma unroll
-            for (int b = 0; b < DY; ++b) cnt[a * DY + b] += __builtin_popcount(xa & by[b * W + w]);
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < DX * DY; ++c) {
+    for (int c = 0; c < NC; ++c) {
         uint32_t v = cnt[c];
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
         cnt[c] = v;
     }
-    if (lane < DX * DY) {
+    const int ncells = DX * DY * (DZ == 1 ? 1 : dz);
+    if (lane < ncells) {
         uint32_t v = 0;
 #pragma unroll
-        for (int c = 0; c < DX * DY; ++c) v = lane == c ? cnt[c] : v;
+        for (int c = 0; c < NC; ++c) v = lane == c ? cnt[c] : v;
         out[lane] = (int32_t)v;
     }
 }
 
-// phase 1: counts[t][16] (row-major dx x dy) of every test, one wave per test
+constexpr int kBitsCells = 64;  // count slots per test
+
+// phase 1: counts[t][64] of every test, one wave per test; D = 0 (x, y) or 1 (x, y, z)
+template <int D>
 __global__ __launch_bounds__(256) void ci_bits_count(const uint32_t *__restrict__ bits, const int32_t *__restrict__ dims,
                                                      const int32_t *__restrict__ row0, const int32_t *__restrict__ items,
                                                      long long W, long long n, int32_t *__restrict__ counts) {
     const int lane = threadIdx.x & 63;
     const long long wave = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
     for (long long t = wave; t < n; t += (long long)gridDim.x * 4) {
-        const int x = items[2 * t], y = items[2 * t + 1];
+        const int x = items[(2 + D) * t], y = items[(2 + D) * t + 1];
         const int dx = dims[x], dy = dims[y];
         const uint32_t *bx = bits + (size_t)row0[x] * W, *by = bits + (size_t)row0[y] * W;
-        int32_t *out = counts + t * 16;
+        const uint32_t *bz = bx;
+        int dz = 1;
+        if (D == 1) {
+            const int z = items[3 * t + 2];
+            dz = dims[z];
+            bz = bits + (size_t)row0[z] * W;
+        }
+        int32_t *out = counts + t * kBitsCells;
+        constexpr int DZ = D == 1 ? 4 : 1;
         switch (dx * 8 + dy) {
 #define FBN_PAIR(A, B) \
-    case A * 8 + B: count_pair<A, B>(bx, by, W, lane, out); break;
+    case A * 8 + B: count_test<A, B, DZ>(bx, by, bz, dz, W, lane, out); break;
             FBN_PAIR(1, 1) FBN_PAIR(1, 2) FBN_PAIR(1, 3) FBN_PAIR(1, 4)
             FBN_PAIR(2, 1) FBN_PAIR(2, 2) FBN_PAIR(2, 3) FBN_PAIR(2, 4)
             FBN_PAIR(3, 1) FBN_PAIR(3, 2) FBN_PAIR(3, 3) FBN_PAIR(3, 4)
@@ -136,63 +157,74 @@ __device__ double gamma_q_b(double a, double x) {
     return exp(-x + a * log(x) - lg) * h;
 }
 
-// phase 2: one lane per test -- marginals, adjusted df, G^2 (reference loop order), p
+// phase 2: one lane per test -- per z: marginals, adjusted df, G^2 terms in the reference's
+// i -> j order; then the sums over z in z order (ComputeGSquareXY / XYZ, src/IndependenceTest.cpp:
+// 65-155, 295-364; the same arithmetic as ci_g2_kernel), p = Q(df/2, G^2/2)
+template <int D>
 __global__ __launch_bounds__(256) void ci_bits_g2(const int32_t *__restrict__ counts, const int32_t *__restrict__ dims,
                                                   const int32_t *__restrict__ items, long long n, double alpha,
                                                   double *__restrict__ g2o, int32_t *__restrict__ dfo,
                                                   double *__restrict__ po, uint8_t *__restrict__ indep,
                                                   int32_t *__restrict__ counts0, unsigned long long *__restrict__ stats) {
     for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t < n; t += (long long)gridDim.x * 256) {
-        const int dx = dims[items[2 * t]], dy = dims[items[2 * t + 1]];
-        const int32_t *h = counts + t * 16;
-        int ni[4], nj[4];
-        long total = 0;
-        int alx = 0, aly = 0;
-        for (int i = 0; i < dx; ++i) {
-            int s = 0;
-            for (int j = 0; j < dy; ++j) s += h[i * dy + j];
-            ni[i] = s;
-            alx += s > 0;
-            total += s;
-        }
-        for (int j = 0; j < dy; ++j) {
-            int s = 0;
-            for (int i = 0; i < dx; ++i) s += h[i * dy + j];
-            nj[j] = s;
-            aly += s > 0;
-        }
-        alx = alx >= 1 ? alx : 1;
-        aly = aly >= 1 ? aly : 1;
-        const int df = (alx - 1) * (aly - 1);
-        double g = 0.0;
-        if (total != 0) {
+        const int dx = dims[items[(2 + D) * t]], dy = dims[items[(2 + D) * t + 1]];
+        const int dimz = D == 1 ? dims[items[3 * t + 2]] : 1;
+        const int dxy = dx * dy;
+        const int32_t *hz = counts + t * kBitsCells;
+        double g2 = 0.0;
+        int df = 0;
+        for (int k = 0; k < dimz; ++k) {
+            const int32_t *h = hz + k * dxy;
+            int ni[4], nj[4];
+            long total = 0;
+            int alx = 0, aly = 0;
             for (int i = 0; i < dx; ++i) {
-                const long sum_row = ni[i];
-                if (sum_row == 0) continue;
-                for (int j = 0; j < dy; ++j) {
-                    const long sum_col = nj[j];
-                    const long observed = h[i * dy + j];
-                    if (sum_col == 0 || observed == 0) continue;
-                    const double expected = (double)sum_col * (double)sum_row / (double)total;
-                    g += 2.0 * observed * log(observed / expected);
+                int s = 0;
+                for (int j = 0; j < dy; ++j) s += h[i * dy + j];
+                ni[i] = s;
+                alx += s > 0;
+                total += s;
+            }
+            for (int j = 0; j < dy; ++j) {
+                int s = 0;
+                for (int i = 0; i < dx; ++i) s += h[i * dy + j];
+                nj[j] = s;
+                aly += s > 0;
+            }
+            alx = alx >= 1 ? alx : 1;
+            aly = aly >= 1 ? aly : 1;
+            df += (alx - 1) * (aly - 1);
+            double g = 0.0;
+            if (total != 0) {
+                for (int i = 0; i < dx; ++i) {
+                    const long sum_row = ni[i];
+                    if (sum_row == 0) continue;
+                    for (int j = 0; j < dy; ++j) {
+                        const long sum_col = nj[j];
+                        const long observed = h[i * dy + j];
+                        if (sum_col == 0 || observed == 0) continue;
+                        const double expected = (double)sum_col * (double)sum_row / (double)total;
+                        g += 2.0 * observed * log(observed / expected);
+                    }
                 }
             }
+            g2 += g;
         }
         double p;
         bool ind;
-        if (df == 0) {  // src/IndependenceTest.cpp:349-351
+        if (df == 0) {  // src/IndependenceTest.cpp:149-151, 349-351
             p = 1.0;
             ind = true;
         } else {
-            p = gamma_q_b(0.5 * df, 0.5 * g);
+            p = gamma_q_b(0.5 * df, 0.5 * g2);
             ind = p > alpha;
         }
-        if (g2o) g2o[t] = g;
+        if (g2o) g2o[t] = g2;
         dfo[t] = df;
         if (po) po[t] = p;
         indep[t] = ind;
         if (counts0 && t == 0)
-            for (int c = 0; c < dx * dy; ++c) counts0[c] = h[c];
+            for (int c = 0; c < dimz * dxy; ++c) counts0[c] = hz[c];
         if (stats) {
             const double m = fabs(p - alpha);
             atomicMin(stats, (unsigned long long)__double_as_longlong(m));
@@ -212,14 +244,22 @@ extern "C" hipError_t fbn_ci_bits_build(const uint8_t *cols, const int32_t *dims
 }
 
 extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *dims, const int32_t *row0,
-                                         const int32_t *items, long long W, long long n, double alpha, double *g2,
-                                         int32_t *df, double *p, uint8_t *indep, int32_t *counts, int32_t *counts0,
-                                         unsigned long long *stats, int num_cu, hipStream_t s) {
+                                         const int32_t *items, long long W, long long n, int d, double alpha,
+                                         double *g2, int32_t *df, double *p, uint8_t *indep, int32_t *counts,
+                                         int32_t *counts0, unsigned long long *stats, int num_cu, hipStream_t s) {
     const long long g1 = (n + 3) / 4, cap = (long long)num_cu * 8;
-    hipLaunchKernelGGL(ci_bits_count, dim3((int)(g1 < cap ? g1 : cap)), dim3(256), 0, s, bits, dims, row0, items, W, n,
-                       counts);
     const long long g2g = (n + 255) / 256;
-    hipLaunchKernelGGL(ci_bits_g2, dim3((int)(g2g < cap ? g2g : cap)), dim3(256), 0, s, counts, dims, items, n, alpha,
-                       g2, df, p, indep, counts0, stats);
+    const dim3 b1((unsigned)(g1 < cap ? g1 : cap)), b2((unsigned)(g2g < cap ? g2g : cap));
+    if (d == 0) {
+        hipLaunchKernelGGL(ci_bits_count<0>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts);
+        hipLaunchKernelGGL(ci_bits_g2<0>, b2, dim3(256), 0, s, counts, dims, items, n, alpha, g2, df, p, indep,
+                           counts0, stats);
+    } else if (d == 1) {
+        hipLaunchKernelGGL(ci_bits_count<1>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts);
+        hipLaunchKernelGGL(ci_bits_g2<1>, b2, dim3(256), 0, s, counts, dims, items, n, alpha, g2, df, p, indep,
+                           counts0, stats);
+    } else {
+        return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }

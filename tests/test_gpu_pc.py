@@ -126,8 +126,8 @@ def test_decision_margin_log(alarm_ds, alarm_paths):
 
 @pytest.mark.parametrize("ns", [1, 31, 32, 33, 5000, 100003])
 def test_bit_sliced_marginal_tests_match_histogram_kernel(ns):
-    """Level-0 tests go through the bit-sliced popcount kernel (ci_bits.hip) when every variable
-    has <= 4 states; the byte-column histogram kernel (FBN_CI_NO_BITS) must give identical counts,
+    """Tests with <= 1 conditioning variable go through the bit-sliced popcount kernel (ci_bits.hip)
+    when every variable has <= 4 states; the byte-column histogram kernel (FBN_CI_NO_BITS) must give identical counts,
     df, G^2 and p, and both must match the oracle.  Ragged sample counts, constant columns and
     1..4-state variables."""
     rng = np.random.default_rng(ns)
@@ -135,23 +135,27 @@ def test_bit_sliced_marginal_tests_match_histogram_kernel(ns):
     dims = np.array([1, 2, 3, 4, 2, 3, 4, 4, 2, 3, 1, 4], np.int32)
     cols = np.stack([rng.integers(0, d, ns) for d in dims]).astype(np.uint8)
     cols[5] = (cols[4] + cols[5]) % 3  # some dependence
-    items = np.array([[x, y] for x in range(nv) for y in range(x + 1, nv)], np.int32)
+    items0 = np.array([[x, y] for x in range(nv) for y in range(x + 1, nv)], np.int32)
+    items1 = np.array([[x, y, z] for x in range(nv) for y in range(x + 1, nv) for z in range(nv)
+                       if z != x and z != y], np.int32)
     ci = F.IndependenceTest(F.Dataset(columns=cols, dims=dims), 0.05, device=0)
-    g2, df, p, ind = ci.run(items, 0)
-    cnt = ci.counts(1, 7)
-    os.environ["FBN_CI_NO_BITS"] = "1"
-    try:
-        g2h, dfh, ph, indh = ci.run(items, 0)
-        cnth = ci.counts(1, 7)
-    finally:
-        del os.environ["FBN_CI_NO_BITS"]
-    np.testing.assert_array_equal(cnt, cnth)
-    np.testing.assert_array_equal(df, dfh)
-    np.testing.assert_array_equal(g2, g2h)
-    np.testing.assert_array_equal(p, ph)
-    np.testing.assert_array_equal(ind, indh)
     od = O.OracleDataset(columns=cols, dims=dims)
-    for k, (x, y) in enumerate(items[:20]):
-        r = od.ci_test(int(x), int(y))
-        assert df[k] == r["df"] and ind[k] == r["is_independent"]
-        assert abs(g2[k] - r["g2"]) <= 1e-12 * max(1.0, abs(r["g2"]))
+    for d, items in ((0, items0), (1, items1)):
+        g2, df, p, ind = ci.run(items, d)
+        cnt = ci.counts(1, 7, [6] if d else [])
+        os.environ["FBN_CI_NO_BITS"] = "1"
+        try:
+            g2h, dfh, ph, indh = ci.run(items, d)
+            cnth = ci.counts(1, 7, [6] if d else [])
+        finally:
+            del os.environ["FBN_CI_NO_BITS"]
+        np.testing.assert_array_equal(cnt, cnth)
+        np.testing.assert_array_equal(df, dfh)
+        np.testing.assert_array_equal(g2, g2h)
+        np.testing.assert_array_equal(p, ph)
+        np.testing.assert_array_equal(ind, indh)
+        for k in range(0, len(items), max(1, len(items) // 25)):
+            it = [int(v) for v in items[k]]
+            r = od.ci_test(it[0], it[1], it[2:])
+            assert df[k] == r["df"] and ind[k] == r["is_independent"]
+            assert abs(g2[k] - r["g2"]) <= 1e-12 * max(1.0, abs(r["g2"]))
