@@ -57,6 +57,7 @@ _SIGS = {
     "fbn_pc_edges": [_vp, _vp],
     "fbn_pc_sepsets": [_vp, _vp, _i64, _vp],
     "fbn_pc_timing": [_vp, _vp, _vp],
+    "fbn_pc_device_bytes": [_vp, _vp],
     "fbn_pc_orient_skeleton": [C.c_int, _vp, C.c_int, _vp, C.c_int64, _vp],
     "fbn_pc_level": [_vp, C.c_double, C.c_int, C.c_int, _vp, C.c_int64, C.c_int64, C.c_int64, _vp, _vp, _vp, _vp],
     "fbn_pc_num_oriented_edges": [_vp, _vp],
@@ -463,6 +464,9 @@ class PCStable:
         tot, ker = C.c_double(), C.c_double()
         lib.fbn_pc_timing(r, C.byref(tot), C.byref(ker))
         self.total_s, self.kernel_s = tot.value, ker.value
+        nb = C.c_int64()
+        lib.fbn_pc_device_bytes(r, C.byref(nb))
+        self.device_bytes = nb.value
         self.num_ci_test = int(self.tests_per_level.sum())
         self.min_margin, self.near_alpha = self.result.min_margin, self.result.near_alpha
         return self

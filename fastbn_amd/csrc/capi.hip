@@ -145,6 +145,7 @@ struct fbn_ci_ctx {
     DevBuf bits, brow, bcounts;
     bool bits_ready = false;
     int64_t bits_W = 0;
+    int64_t last_bytes = 0;  // input bytes of the last launch in the kernel's own format (roofline)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipStream_t stream = nullptr;  // the PC driver's rounds (pinned staging, one sync per round)
     float last_ms = 0.f;
@@ -805,8 +806,10 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
     }
     int rc;
     // tests with <= 1 conditioning variable over variables with <= 4 states: popcounts of
-    // bit-sliced columns (ci_bits.hip)
-    bool bits_path = d <= 1 && !getenv("FBN_CI_NO_BITS");
+    // bit-sliced columns (ci_bits.hip).  Below ~32k samples the per-test fixed cost (two launches,
+    // the wave reduction of the counters) outweighs the sample loop: byte-column kernel there.
+    const int64_t kBitsMinSamples = 32768;
+    bool bits_path = d <= 1 && !getenv("FBN_CI_NO_BITS") && (c->N >= kBitsMinSamples || getenv("FBN_CI_FORCE_BITS"));
     for (int64_t i = 0; bits_path && i < n; ++i)
         for (int j = 0; j < w; ++j) bits_path = bits_path && c->dims[items[w * i + j]] <= 4;
     if (bits_path) {
@@ -833,6 +836,8 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
             if ((rc = c->p.ensure((size_t)n * 8))) return rc;
         }
         FBN_HIP(hipMemcpyAsync(c->items.p, items, (size_t)n * w * 4, hipMemcpyHostToDevice, s));
+        c->last_bytes = 0;
+        for (int64_t i = 0; i < n * w; ++i) c->last_bytes += (int64_t)c->dims[items[i]] * c->bits_W * 4;
         FBN_HIP(hipEventRecord(c->ev0, s));
         hipError_t e = fbn_ci_bits_launch(c->bits.as<uint32_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(),
                                           c->items.as<int32_t>(), c->bits_W, n, d, alpha,
@@ -864,6 +869,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         if ((rc = c->scratch.ensure((size_t)grid * stride))) return rc;
         gscratch = c->scratch.as<int32_t>();
     }
+    c->last_bytes = n * c->N * (2 + d);  // uint8 columns x, y, z_1..z_d streamed once
     FBN_HIP(hipEventRecord(c->ev0, s));
     hipError_t e = fbn_ci_launch(c->cols.as<uint8_t>(), c->ddims.as<int32_t>(), c->items.as<int32_t>(), c->N, n, d,
                                  alpha, want_g2p ? c->g2.as<double>() : nullptr, c->df.as<int32_t>(),
@@ -1080,6 +1086,11 @@ int fbn_pc_shd_bif(const fbn_pc_result *r, const char *bif_path, int *shd) {
         for (int k = 0; k < 3; ++k) t[3 * i + k] = r->r.oriented[i][k];
     return fbn_shd_bif(bif_path, r->r.num_nodes, t.data(), (int)r->r.oriented.size(), shd);
 }
+int fbn_pc_device_bytes(const fbn_pc_result *r, int64_t *bytes) {
+    if (!r || !bytes) return SetError(FBN_ERR_ARG, "null pointer");
+    *bytes = r->r.device_bytes;
+    return FBN_OK;
+}
 int fbn_pc_timing(const fbn_pc_result *r, double *total_s, double *kernel_s) {
     if (!r) return SetError(FBN_ERR_ARG, "null pointer");
     if (total_s) *total_s = r->r.total_s;
@@ -1120,6 +1131,7 @@ int CiRunBatch(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alp
     float ms = 0.f;
     FBN_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     res.kernel_s += ms * 1e-3;
+    res.device_bytes += c->last_bytes;
     return FBN_OK;
 }
 }  // namespace fbn

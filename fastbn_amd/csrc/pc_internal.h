@@ -59,6 +59,7 @@ struct PCResultHost {
     std::vector<int64_t> tests_per_level;     // reference (t = 1) counts
     std::vector<int64_t> launched_per_level;  // device tests incl. speculation
     double total_s = 0.0, kernel_s = 0.0;
+    int64_t device_bytes = 0;  // input bytes the CI kernels had to read, in their own column format
     // after orientation: (from, to, 1) arcs and (min, max, 0) undirected edges, vec_edges order
     std::vector<std::array<int, 3>> oriented;
     int num_nodes = 0;

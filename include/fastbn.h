@@ -200,6 +200,9 @@ int fbn_pc_shd_bif(const fbn_pc_result *r, const char *bif_path, int *shd);
 /* Same for any learned graph given as triples [n][3] (from, to, 1) / (a, b, 0). */
 int fbn_shd_bif(const char *bif_path, int nvars, const int32_t *triples, int n, int *shd);
 int fbn_pc_timing(const fbn_pc_result *r, double *total_s, double *kernel_s);
+/* Roofline accounting: bytes of column data the CI kernels had to read for every launched test,
+ * in the format they read (uint8 columns: N per variable; bit-sliced masks: N/8 per value). */
+int fbn_pc_device_bytes(const fbn_pc_result *r, int64_t *bytes);
 int fbn_pc_result_destroy(fbn_pc_result *r);
 
 #ifdef __cplusplus

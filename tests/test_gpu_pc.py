@@ -140,9 +140,13 @@ def test_bit_sliced_marginal_tests_match_histogram_kernel(ns):
                        if z != x and z != y], np.int32)
     ci = F.IndependenceTest(F.Dataset(columns=cols, dims=dims), 0.05, device=0)
     od = O.OracleDataset(columns=cols, dims=dims)
+    os.environ["FBN_CI_FORCE_BITS"] = "1"  # the bit-sliced path also below its sample threshold
+    try:
+        res = {d: (ci.run(items, d), ci.counts(1, 7, [6] if d else [])) for d, items in ((0, items0), (1, items1))}
+    finally:
+        del os.environ["FBN_CI_FORCE_BITS"]
     for d, items in ((0, items0), (1, items1)):
-        g2, df, p, ind = ci.run(items, d)
-        cnt = ci.counts(1, 7, [6] if d else [])
+        (g2, df, p, ind), cnt = res[d]
         os.environ["FBN_CI_NO_BITS"] = "1"
         try:
             g2h, dfh, ph, indh = ci.run(items, d)
