@@ -794,24 +794,21 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
                           int32_t *counts_dev, hipStream_t s) {
     if (d < 0 || d > 8) return SetError(FBN_ERR_LIMIT, "conditioning set size %d (supported 0..8)", d);
     const int w = 2 + d;
-    size_t lds = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        const int32_t *it = items + i * w;
-        for (int j = 0; j < w; ++j)
-            if (it[j] < 0 || it[j] >= c->nvars) return SetError(FBN_ERR_ARG, "test %lld: variable %d out of range", (long long)i, it[j]);
-        int64_t dimz = 1;
-        for (int j = 0; j < d; ++j) dimz *= c->dims[it[2 + j]];
-        if (dimz > (1 << 24)) return SetError(FBN_ERR_LIMIT, "test %lld: conditioning table too large", (long long)i);
-        lds = std::max(lds, fbn_ci_lds_bytes((int)dimz, c->dims[it[0]], c->dims[it[1]]));
+    // one validation pass: variable ranges and the largest state count (bit-sliced eligibility)
+    int maxdim = 0;
+    for (int64_t i = 0; i < n * w; ++i) {
+        const int v = items[i];
+        if (v < 0 || v >= c->nvars)
+            return SetError(FBN_ERR_ARG, "test %lld: variable %d out of range", (long long)(i / w), v);
+        maxdim = std::max(maxdim, c->dims[v]);
     }
     int rc;
     // tests with <= 1 conditioning variable over variables with <= 4 states: popcounts of
     // bit-sliced columns (ci_bits.hip).  Below ~32k samples the per-test fixed cost (two launches,
     // the wave reduction of the counters) outweighs the sample loop: byte-column kernel there.
     const int64_t kBitsMinSamples = 32768;
-    bool bits_path = d <= 1 && !getenv("FBN_CI_NO_BITS") && (c->N >= kBitsMinSamples || getenv("FBN_CI_FORCE_BITS"));
-    for (int64_t i = 0; bits_path && i < n; ++i)
-        for (int j = 0; j < w; ++j) bits_path = bits_path && c->dims[items[w * i + j]] <= 4;
+    const bool bits_path = d <= 1 && maxdim <= 4 && !getenv("FBN_CI_NO_BITS") &&
+                           (c->N >= kBitsMinSamples || getenv("FBN_CI_FORCE_BITS"));
     if (bits_path) {
         if (!c->bits_ready) {
             const int64_t W = (c->N + 31) / 32;
@@ -836,8 +833,9 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
             if ((rc = c->p.ensure((size_t)n * 8))) return rc;
         }
         FBN_HIP(hipMemcpyAsync(c->items.p, items, (size_t)n * w * 4, hipMemcpyHostToDevice, s));
-        c->last_bytes = 0;
-        for (int64_t i = 0; i < n * w; ++i) c->last_bytes += (int64_t)c->dims[items[i]] * c->bits_W * 4;
+        int64_t rows = 0;
+        for (int64_t i = 0; i < n * w; ++i) rows += c->dims[items[i]];
+        c->last_bytes = rows * c->bits_W * 4;
         FBN_HIP(hipEventRecord(c->ev0, s));
         hipError_t e = fbn_ci_bits_launch(c->bits.as<uint32_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(),
                                           c->items.as<int32_t>(), c->bits_W, n, d, alpha,
@@ -848,6 +846,14 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci bits kernel launch: %s", hipGetErrorString(e));
         FBN_HIP(hipEventRecord(c->ev1, s));
         return FBN_OK;
+    }
+    size_t lds = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int32_t *it = items + i * w;
+        int64_t dimz = 1;
+        for (int j = 0; j < d; ++j) dimz *= c->dims[it[2 + j]];
+        if (dimz > (1 << 24)) return SetError(FBN_ERR_LIMIT, "test %lld: conditioning table too large", (long long)i);
+        lds = std::max(lds, fbn_ci_lds_bytes((int)dimz, c->dims[it[0]], c->dims[it[1]]));
     }
     // tables beyond the LDS budget: the same layout in a per-workgroup global scratch region
     const bool global_tables = lds > 160 * 1024;

@@ -234,6 +234,7 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
         int rc = RunLevel(ctx, alpha, d, group_size, adj, edges, 0, edges.size(), out, res);
         if (rc) return rc;
         auto tb = std::chrono::steady_clock::now();
+        res.sepset.reserve(res.sepset.size() + edges.size());
         for (size_t e = 0; e < edges.size(); ++e)
             if (out.removed[e]) res.sepset.set(edges[e], std::move(out.sep[e]));
         res.tests_per_level.push_back(out.counted);

@@ -34,6 +34,7 @@ class SepsetMap {
         return v_;
     }
     size_t size() const { return v_.size(); }
+    void reserve(size_t n) { v_.reserve(n); }
 
   private:
     void sort() const {
