@@ -314,6 +314,16 @@ def main():
                              "kernel is fp64-VALU/latency bound (DESIGN.md)"},
     }
     if rank == 0 and world == 1:
+        # PCIe-inclusive rate (host evidence in, host labels + marginals out through fbn_jt_run):
+        # reported beside the metric, never as `value`
+        t_host = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            jt.infer(ev)
+            t_host.append(time.perf_counter() - t0)
+        out["pcie_inclusive"] = {"value": args.cases / float(np.median(t_host)), "unit": "cases/s",
+                                 "note": "fbn_jt_run from host buffers: evidence H2D, kernel, labels + "
+                                         f"{info['sum_dom']} marginals per case D2H"}
         if not args.no_pc:
             out["pc_stable"] = bench_pc(max(5, args.steps // 2), args.warmup)
         if not args.no_munin:
