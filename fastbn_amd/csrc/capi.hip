@@ -27,12 +27,12 @@ extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *di
                                          const int32_t *items, long long W, long long n, int d, double alpha,
                                          double *g2, int32_t *df, double *p, uint8_t *indep, int32_t *counts,
                                          int32_t *counts0, unsigned long long *stats, int num_cu, hipStream_t s);
-extern "C" int fbn_jt_virt_waves_per_group();
 extern "C" hipError_t fbn_jt_virt_launch(const JtVClique *cls, const int32_t *aux, const double *initv,
-                                         const uint64_t *dig, const int32_t *order, const int32_t *vsel,
-                                         const int8_t *evid, double *marg, int32_t *labels, double *ws, int32_t *wsi,
-                                         int *flags, long long ncases, long long store_rows, long long scratch_row,
-                                         int nc, int V, int SD, int grid, int dbg, hipStream_t stream);
+                                         const uint64_t *dig, const int32_t *order, const int32_t *sched,
+                                         const int32_t *vsel, const int8_t *evid, double *marg, int32_t *labels,
+                                         double *ws, int32_t *wsi, int *flags, long long ncases, long long store_rows,
+                                         long long scratch_row, long long scratch_rows, int nc, int V, int SD,
+                                         int grid, int dbg, hipStream_t stream);
 extern "C" hipError_t fbn_jt_lds_launch(const JtOp *ops, int nops, const int32_t *aux, const double *initv,
                                         const uint64_t *dig, const int8_t *evid, int V, long long ncases, int SD,
                                         double *marg, int32_t *labels, double *ws, int32_t *wsi, long long wave_entries,
@@ -110,7 +110,7 @@ struct fbn_jt_plan {
     fbn::JTProgramLDS lprog;  // variant 0 (default): clique in flight resident in LDS
     fbn::JTProgramV vprog;    // variant 4: streamed (virtual) tables, large trees
     bool v_ok = false;
-    DevBuf vcl, vaux, viv, vdig, vorder, vsel;
+    DevBuf vcl, vaux, viv, vdig, vorder, vsched, vsel;
     int device = 0, num_cu = 0, waves_per_cu = 0, variant = -1, last_variant = -1;
     // plan-specialized kernel (variant 3)
     bool gen_eligible = false;
@@ -320,6 +320,7 @@ static int JtUpload(fbn_jt_plan *p) {
         if ((rc = up(p->viv, v.initv.data(), v.initv.size() * 8))) return rc;
         if ((rc = up(p->vdig, v.dig.data(), v.dig.size() * 8))) return rc;
         if ((rc = up(p->vorder, v.order.data(), v.order.size() * 4))) return rc;
+        if ((rc = up(p->vsched, v.sched.data(), v.sched.size() * 4))) return rc;
         if ((rc = up(p->vsel, v.vsel.data(), v.vsel.size() * 4))) return rc;
     }
     return FBN_OK;
@@ -619,26 +620,26 @@ int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, 
     } else if (variant == 4) {
         // streamed tables: small register footprint, many resident waves; the per-wave store holds
         // only separator messages and denominators
-        // workgroups of W lock-stepped waves, one 64-case block per wave
-        const int W = fbn_jt_virt_waves_per_group();
-        const int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 8;
-        int grid = (int)std::min<int64_t>((nblk + W - 1) / W, std::max<int64_t>(1, (int64_t)p->num_cu * wpc / W));
+        // workgroups of JT_V_WAVES waves, one 64-case block per workgroup (persistent)
+        const int W = JT_V_WAVES;
+        const int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 16;
+        int grid = (int)std::min<int64_t>(nblk, std::max<int64_t>(1, (int64_t)p->num_cu * wpc / W));
         const auto &v = p->vprog;
-        const size_t per_wave_d = (size_t)v.store_rows * 64 * 8, per_wave_i = (size_t)(nc + V) * 64 * 4;
+        const size_t per_blk_d = (size_t)v.store_rows * 64 * 8, per_blk_i = (size_t)(nc + V) * 64 * 4;
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
             const size_t have = free_b / 10 * 8 + p->ws.bytes;
-            grid = (int)std::max<int64_t>(1, std::min<int64_t>(grid, (int64_t)(have / (W * (per_wave_d + per_wave_i)))));
+            grid = (int)std::max<int64_t>(1, std::min<int64_t>(grid, (int64_t)(have / (per_blk_d + per_blk_i))));
         }
-        const size_t ws_d = (size_t)grid * W * per_wave_d;
-        if ((rc = p->ws.ensure(ws_d + (size_t)grid * W * per_wave_i))) return rc;
+        const size_t ws_d = (size_t)grid * per_blk_d;
+        if ((rc = p->ws.ensure(ws_d + (size_t)grid * per_blk_i))) return rc;
         if ((rc = p->flags.ensure((size_t)nblk * 4))) return rc;
         FBN_HIP(hipEventRecord(p->ev0, s));
         hipError_t e = fbn_jt_virt_launch(p->vcl.as<JtVClique>(), p->vaux.as<int32_t>(), p->viv.as<double>(),
-                                          p->vdig.as<uint64_t>(), p->vorder.as<int32_t>(), p->vsel.as<int32_t>(),
-                                          d_evidence, marg, labels, p->ws.as<double>(),
+                                          p->vdig.as<uint64_t>(), p->vorder.as<int32_t>(), p->vsched.as<int32_t>(),
+                                          p->vsel.as<int32_t>(), d_evidence, marg, labels, p->ws.as<double>(),
                                           reinterpret_cast<int32_t *>(p->ws.as<char>() + ws_d), p->flags.as<int>(),
-                                          ncases, v.store_rows, v.scratch_row, nc, V, SD, grid,
+                                          ncases, v.store_rows, v.scratch_row, v.scratch_rows, nc, V, SD, grid,
                                           // diagnostic ablation only (tools/): skip pass types, wrong results
                                           getenv("FBN_JT_VDEBUG") ? atoi(getenv("FBN_JT_VDEBUG")) : 0, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt kernel launch: %s", hipGetErrorString(e));

@@ -94,10 +94,14 @@ struct JTProgramV {
     std::vector<int32_t> aux;
     std::vector<double> initv;
     std::vector<uint64_t> dig;
-    std::vector<int32_t> order;  // Collect (DFS post-order) then Distribute (DFS pre-order) clique ids
+    std::vector<int32_t> order;  // clique ids of the schedule segments (see sched)
+    std::vector<int32_t> sched;  // 2 * JT_V_WAVES + 3 segment offsets into order: Collect per wave,
+                                 // Collect top, Distribute top, Distribute per wave, end
+    double split_efficiency = 1.0;  // modelled parallel efficiency of the waves' tree split
     std::vector<int32_t> vsel;   // per variable {cand_off, ncand, out_off, dim} (candidates in aux)
     int64_t store_rows = 0;      // per-wave fp64 rows: Collect messages, Distribute messages, denominators,
-    int64_t scratch_row = 0;     // then the scratch table (rows scratch_row .. store_rows)
+    int64_t scratch_row = 0;     // then one scratch table per wave of the block
+    int64_t scratch_rows = 0;    // rows per scratch table
     int num_cliques = 0;
     int sum_dom = 0;
 };

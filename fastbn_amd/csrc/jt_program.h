@@ -85,5 +85,6 @@ struct JtVClique {
                                     // and marginal passes read it instead of recomputing the chain
 };
 #define JT_V_MAX_CHILDREN 6
+#define JT_V_WAVES 2  // waves sharing one 64-case block (disjoint subtrees in parallel)
 
 #endif

@@ -132,7 +132,7 @@ __device__ __forceinline__ double entry(const Store &S, const Clq &C, const Dens
 
 template <int L>
 struct Unroll {
-    static constexpr int U = L <= 3 ? 4 : 2;  // entries per pipeline stage (SGPR budget)
+    static constexpr int U = L <= 2 ? 4 : 2;  // entries in flight together (SGPR budget)
 };
 
 // one entry's operands, loaded ahead of its arithmetic: the masked initial potential and the L
@@ -174,32 +174,25 @@ template <int L, bool P32, bool STORE = false>
 __device__ __forceinline__ double vsum(const Store &S, const Clq &C, const Dens &D, int scr = 0) {
     constexpr int U = Unroll<L>::U;
     double acc = 0.0;
-    const int T = C.T, npair = T / (2 * U);
-    Pre<L> A[U], B[U];
-#define FBN_LOADC(X, n0)                                                        \
-    _Pragma("unroll") for (int u = 0; u < U; ++u) pre_load<L, P32>(S, C, (n0) + u, X[u])
-#define FBN_EVALC(X, n0)                                                        \
-    _Pragma("unroll") for (int u = 0; u < U; ++u) {                             \
-        const double v = pre_eval<L>(X[u], D);                                  \
-        acc += v;                                                               \
-        if (STORE) S.st(scr + ((n0) + u) * 512, v);                             \
+    const int T = C.T;
+    int n0 = 0;
+    for (; n0 + U <= T; n0 += U) {
+        Pre<L> X[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) pre_load<L, P32>(S, C, n0 + u, X[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const double v = pre_eval<L>(X[u], D);
+            acc += v;
+            if (STORE) S.st(scr + (n0 + u) * 512, v);
+        }
     }
-    if (npair > 0) FBN_LOADC(A, 0);
-    for (int c = 0; c < npair; ++c) {
-        const int n0 = 2 * U * c;
-        FBN_LOADC(B, n0 + U);
-        FBN_EVALC(A, n0);
-        if (c + 1 < npair) FBN_LOADC(A, n0 + 2 * U);
-        FBN_EVALC(B, n0 + U);
-    }
-#undef FBN_LOADC
-#undef FBN_EVALC
-    for (int n = npair * 2 * U; n < T; ++n) {
+    for (; n0 < T; ++n0) {
         Pre<L> X;
-        pre_load<L, P32>(S, C, n, X);
+        pre_load<L, P32>(S, C, n0, X);
         const double v = pre_eval<L>(X, D);
         acc += v;
-        if (STORE) S.st(scr + n * 512, v);
+        if (STORE) S.st(scr + n0 * 512, v);
     }
     return acc;
 }
@@ -290,32 +283,30 @@ __device__ __forceinline__ void vbins(const Store &S, const Clq &C, const Dens &
         }                                                              \
     } while (0)
 
-// A workgroup = kWaves waves, each with its own block of 64 cases and its own store; the waves
-// walk the same clique schedule in lock-step (one barrier per clique), so the constant stream of
-// the clique in flight (initial potentials, digits, message maps, entry lists) is fetched once
-// into the CU's scalar cache and shared by the group.
-constexpr int kWaves = 4;
-__global__ __launch_bounds__(64 * kWaves) void jt_virt_kernel(
+// A workgroup = JT_V_WAVES waves sharing one 64-case block: each runs the Collect (then the
+// Distribute) of its own disjoint subtrees in parallel, one wave runs the "top" cliques above them
+// (jt_virt_plan.cpp: order / sched segments), barriers between the stages.  More waves per block
+// = more memory-level parallelism for a kernel that is latency-bound at ~2 blocks per SIMD.
+__global__ __launch_bounds__(64 * JT_V_WAVES) __attribute__((amdgpu_waves_per_eu(4)))
+void jt_virt_kernel(
     const JtVClique *__restrict__ cls, const int32_t *__restrict__ aux, const double *__restrict__ initv,
-    const uint64_t *__restrict__ dig, const int32_t *__restrict__ order, const int32_t *__restrict__ vsel,
-    const int8_t *__restrict__ evid, double *__restrict__ marg, int32_t *__restrict__ labels,
-    double *__restrict__ ws, int32_t *__restrict__ wsi, int *__restrict__ flags, long long ncases,
-    long long store_rows, long long scratch_row, int nc, int V, int SD, int dbg) {
+    const uint64_t *__restrict__ dig, const int32_t *__restrict__ order, const int32_t *__restrict__ sched,
+    const int32_t *__restrict__ vsel, const int8_t *__restrict__ evid, double *__restrict__ marg,
+    int32_t *__restrict__ labels, double *__restrict__ ws, int32_t *__restrict__ wsi, int *__restrict__ flags,
+    long long ncases, long long store_rows, long long scratch_row, long long scratch_rows, int nc, int V, int SD,
+    int dbg) {
+    __shared__ int sbad[JT_V_WAVES];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const long long gw = (long long)blockIdx.x * kWaves + wv;  // this wave's store
-    Store S;
-    S.r = __builtin_amdgcn_make_buffer_rsrc((double *)ws + (size_t)gw * (size_t)store_rows * 64, 0,
+    Store S;  // the block's store (messages, denominators, one scratch table per wave)
+    S.r = __builtin_amdgcn_make_buffer_rsrc((double *)ws + (size_t)blockIdx.x * (size_t)store_rows * 64, 0,
                                             (int)(store_rows * 512), 0x00020000);
     S.lo = (unsigned)lane * 8u;
-    gint *Ib = (gint *)wsi + (size_t)gw * (size_t)(nc + V) * 64;  // rows: red[c], then sel[v]
+    gint *Ib = (gint *)wsi + (size_t)blockIdx.x * (size_t)(nc + V) * 64;  // rows: red[c], then sel[v]
     const unsigned lo4 = (unsigned)lane * 4u;
-    const int scr = (int)(scratch_row * 512);
+    const int scr = (int)((scratch_row + (long long)wv * scratch_rows) * 512);
 
-    // every wave of the group runs the same number of iterations (barrier counts match); a wave
-    // past the last block recomputes the last case and writes nothing
-    for (long long grp = blockIdx.x; grp * kWaves * 64 < ncases; grp += gridDim.x) {
-        const long long blk = grp * kWaves + wv;
+    for (long long blk = blockIdx.x; blk * 64 < ncases; blk += gridDim.x) {
         const long long cs = blk * 64 + lane;
         const bool act = cs < ncases;
         const long long csr = act ? cs : ncases - 1;
@@ -355,9 +346,9 @@ __global__ __launch_bounds__(64 * kWaves) void jt_virt_kernel(
             }
         };
 
-        // ---------------- Collect, DFS post-order
-        for (int i = 0; i < nc; ++i) {
-            const JtVClique q = cls[order[i]];
+        // ---------------- Collect of one clique (children first)
+        auto collect = [&](int cid) {
+            const JtVClique q = cls[cid];
             Clq C;
             int nobs;
             setup(q, C, nobs);
@@ -367,7 +358,7 @@ __global__ __launch_bounds__(64 * kWaves) void jt_virt_kernel(
 #pragma unroll
             for (int j = 0; j < JT_V_MAX_CHILDREN + 2; ++j) D[j] = Den{1.0, 1.0};
             // the last normalization pass of a clique with children also stores the table for SEPCOL
-            const bool cmat = !q.root && q.k > 0 && !(dbg & 32);
+            const bool cmat = !q.root && q.k > (dbg & 128 ? 0 : 1) && !(dbg & 32);
             for (int L = 0; L <= q.k; ++L) {
                 double s = 0.0;
                 if (cmat && L == q.k) {
@@ -398,12 +389,11 @@ __global__ __launch_bounds__(64 * kWaves) void jt_virt_kernel(
 #undef FBN_COLCALL
                 }
             }
-            __syncthreads();
-        }
+        };
 
         // ---------------- per variable: the clique GetProbabilitiesOneNode would use for this case
         // (first candidate with the fewest remaining variables, src/JunctionTree.cpp:1412-1434)
-        for (int v = 0; v < V; ++v) {
+        auto select = [&](int v) {
             const int32_t *__restrict__ cd = aux + vsel[4 * v];
             const int ncand = vsel[4 * v + 1];
             int sel = 0, best = 0x7fffffff;
@@ -412,12 +402,11 @@ __global__ __launch_bounds__(64 * kWaves) void jt_virt_kernel(
                 if (r < best) best = r, sel = cd[k];
             }
             IROW(nc + v) = sel | (best << 24);
-        }
-        __syncthreads();
+        };
 
-        // ---------------- Distribute, DFS pre-order, and the outputs
-        for (int i = 0; i < ((dbg & 16) ? 0 : nc); ++i) {
-            const JtVClique q = cls[order[nc + i]];
+        // ---------------- Distribute of one clique (parent first) and its outputs
+        auto distribute = [&](int cid) {
+            const JtVClique q = cls[cid];
             Clq C;
             int nobs;
             setup(q, C, nobs);
@@ -434,7 +423,7 @@ __global__ __launch_bounds__(64 * kWaves) void jt_virt_kernel(
             int Lf = q.k;
             if (!q.root && !(dbg & 8)) {
                 double s = 0.0;
-                if (q.mat && !(dbg & 64)) {
+                if (q.mat && !(dbg & 64) && !((dbg & 512) && q.k < 2)) {
 #define FBN_SUMCALL(Lc, P) s = vsum<Lc, P, true>(S, C, D, scr)
                     FBN_VDISPATCH(q.k + 1, p32, FBN_SUMCALL);
 #undef FBN_SUMCALL
@@ -454,9 +443,18 @@ __global__ __launch_bounds__(64 * kWaves) void jt_virt_kernel(
                 const int32_t *__restrict__ rec = aux + q.child_off + 5 * ci;
                 const int Ts = rec[0], per = rec[1], col = rec[3], dis = rec[4];
                 const int32_t *__restrict__ lst = aux + rec[2];
-                // bin sums first (stores only), then the division by the Collect message
-                auto fl = [&](int j, double acc) { S.st_row(dis + j, acc); };
-                if (q.mat && !(dbg & 64)) {
+                // sep = tmp / old at each bin's flush (diagnostic dbg & 256: bin sums first, then
+                // a separate division sweep)
+                const bool direct = !(dbg & 256);
+                auto fl = [&](int j, double acc) {
+                    if (direct) {
+                        const double old = S.row(col + j);
+                        S.st_row(dis + j, (old == 0.0) ? 0.0 : acc / old);
+                    } else {
+                        S.st_row(dis + j, acc);
+                    }
+                };
+                if (q.mat && !(dbg & 64) && !((dbg & 512) && q.k < 2)) {
                     vbins_scr(S, scr, pick(D, Lf), q.T, SeqList{lst, 0}, per, fl);
                 } else {
 #define FBN_DISCALL(Lc, P) vbins<Lc, P>(S, C, D, SeqList{lst, 0}, per, fl)
@@ -464,7 +462,7 @@ __global__ __launch_bounds__(64 * kWaves) void jt_virt_kernel(
 #undef FBN_DISCALL
                 }
                 // sep = tmp / old, zero-guarded (src/JunctionTree.cpp:700-816)
-                for (int j0 = 0; j0 < Ts; j0 += 8) {
+                for (int j0 = 0; j0 < (direct ? 0 : Ts); j0 += 8) {
                     double a[8], o[8];
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
@@ -494,7 +492,7 @@ __global__ __launch_bounds__(64 * kWaves) void jt_virt_kernel(
                     if (wr) o[d] = acc;
                     tot += acc;
                 };
-                if (q.mat && !(dbg & 64)) {
+                if (q.mat && !(dbg & 64) && !((dbg & 512) && q.k < 2)) {
                     vbins_scr(S, scr, pick(D, Lf), q.T, SeqMarg{0, 0, 0, 0, cum, bw, q.T / bw}, q.T / dim, fl);
                 } else {
 #define FBN_MARGCALL(Lc, P) vbins<Lc, P>(S, C, D, SeqMarg{0, 0, 0, 0, cum, bw, q.T / bw}, q.T / dim, fl)
@@ -514,30 +512,53 @@ __global__ __launch_bounds__(64 * kWaves) void jt_virt_kernel(
                     for (int d = 0; d < dim; ++d) o[d] = o[d] / tot;
                 }
             }
+        };
+
+        // ---------------- the schedule: subtrees in parallel, the top by wave 0
+        // (one call site per lambda, so each is inlined)
+        for (int stage = 0; stage < 2; ++stage) {
+            const int b = stage == 0 ? sched[wv] : (wv == 0 ? sched[JT_V_WAVES] : 0);
+            const int e = stage == 0 ? sched[wv + 1] : (wv == 0 ? sched[JT_V_WAVES + 1] : 0);
+            for (int i = b; i < e; ++i) collect(order[i]);
             __syncthreads();
+        }
+        for (int v = wv; v < V; v += JT_V_WAVES) select(v);
+        __syncthreads();
+        for (int stage = 0; stage < ((dbg & 16) ? 0 : 2); ++stage) {
+            const int b = stage == 0 ? (wv == 0 ? sched[JT_V_WAVES + 1] : 0) : sched[JT_V_WAVES + 2 + wv];
+            const int e = stage == 0 ? (wv == 0 ? sched[JT_V_WAVES + 2] : 0) : sched[JT_V_WAVES + 3 + wv];
+            for (int i = b; i < e; ++i) distribute(order[i]);
+            if (stage == 0) __syncthreads();
         }
         // evidence variables: probabilities stay 0 (their first slot is compared with -1 by the scorer)
         if (act)
-            for (int v = 0; v < V; ++v)
+            for (int v = wv; v < V; v += JT_V_WAVES)
                 if (ev[v] >= 0) {
                     const int off = vsel[4 * v + 2], dim = vsel[4 * v + 3];
                     for (int d = 0; d < dim; ++d) out[off + d] = 0.0;
                 }
         const unsigned long long b = __ballot(bad);
-        if (lane == 0 && blk * 64 < ncases) flags[blk] = b != 0ull;
+        if (lane == 0) sbad[wv] = b != 0ull;
+        __syncthreads();  // also: no wave starts the next block while another still reads this one
+        if (wv == 0 && lane == 0) {
+            int f = 0;
+            for (int w = 0; w < JT_V_WAVES; ++w) f |= sbad[w];
+            flags[blk] = f;
+        }
+        __syncthreads();
     }
 }
 
 }  // namespace
 
-extern "C" int fbn_jt_virt_waves_per_group() { return kWaves; }
-
 extern "C" hipError_t fbn_jt_virt_launch(const JtVClique *cls, const int32_t *aux, const double *initv,
-                                         const uint64_t *dig, const int32_t *order, const int32_t *vsel,
-                                         const int8_t *evid, double *marg, int32_t *labels, double *ws, int32_t *wsi,
-                                         int *flags, long long ncases, long long store_rows, long long scratch_row,
-                                         int nc, int V, int SD, int grid, int dbg, hipStream_t stream) {
-    hipLaunchKernelGGL(jt_virt_kernel, dim3(grid), dim3(64 * kWaves), 0, stream, cls, aux, initv, dig, order, vsel, evid, marg,
-                       labels, ws, wsi, flags, ncases, store_rows, scratch_row, nc, V, SD, dbg);
+                                         const uint64_t *dig, const int32_t *order, const int32_t *sched,
+                                         const int32_t *vsel, const int8_t *evid, double *marg, int32_t *labels,
+                                         double *ws, int32_t *wsi, int *flags, long long ncases, long long store_rows,
+                                         long long scratch_row, long long scratch_rows, int nc, int V, int SD,
+                                         int grid, int dbg, hipStream_t stream) {
+    hipLaunchKernelGGL(jt_virt_kernel, dim3(grid), dim3(64 * JT_V_WAVES), 0, stream, cls, aux, initv, dig, order,
+                       sched, vsel, evid, marg, labels, ws, wsi, flags, ncases, store_rows, scratch_row, scratch_rows,
+                       nc, V, SD, dbg);
     return hipGetLastError();
 }

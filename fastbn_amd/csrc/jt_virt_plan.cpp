@@ -56,12 +56,15 @@ int CompileJTProgramV(const JTPlanHost &plan, JTProgramV &prog) {
     for (int s = 0; s < ns; ++s) col_row[s] = rows, rows += plan.seps[s].size();
     for (int s = 0; s < ns; ++s) dis_row[s] = rows, rows += plan.seps[s].size();
     for (int c = 0; c < nc; ++c) den_row[c] = rows, rows += (int64_t)plan.clique_down[c].size() + 2;
-    // scratch table for the Distribute result of cliques with children (read by each SEPDIS pass)
+    // one scratch table per wave of the block (the Collect / Distribute table of the clique in
+    // flight, read by its SEPCOL / SEPDIS / MARG passes)
     prog.scratch_row = rows;
+    int64_t scr = 1;
     for (int c = 0; c < nc; ++c)
-        if (c != plan.root && !plan.clique_down[c].empty())
-            rows = std::max<int64_t>(rows, prog.scratch_row + plan.cliques[c].size());
-    // message maps hold byte offsets into the per-wave store (buffer-load soffset)
+        if (!plan.clique_down[c].empty()) scr = std::max<int64_t>(scr, plan.cliques[c].size());
+    prog.scratch_rows = scr;
+    rows += JT_V_WAVES * scr;
+    // message maps hold byte offsets into the block's store (buffer-load soffset)
     if (rows > INT32_MAX / 512) return SetError(FBN_ERR_LIMIT, "junction tree too large for the streamed variant");
     prog.store_rows = rows;
 
@@ -84,8 +87,72 @@ int CompileJTProgramV(const JTPlanHost &plan, JTProgramV &prog) {
     }
     if ((int)post.size() != nc)
         return SetError(FBN_ERR_LIMIT, "tree traversal covers %zu of %d cliques", post.size(), nc);
-    prog.order = std::vector<int32_t>(post.begin(), post.end());
-    prog.order.insert(prog.order.end(), pre.begin(), pre.end());
+    // the JT_V_WAVES waves of a block split the tree: disjoint subtrees (one list per wave, run in
+    // parallel) and the "top" cliques above them (one wave).  Greedy: expand the costliest subtree
+    // while it exceeds 1/W of the total, then longest-processing-time assignment to the waves.
+    {
+        std::vector<int64_t> cost(nc), sub(nc);
+        for (int c = 0; c < nc; ++c)
+            cost[c] = plan.cliques[c].size() * (2 * (int64_t)plan.clique_down[c].size() + 3);
+        for (int c : post) {
+            sub[c] = cost[c];
+            for (int s : plan.clique_down[c]) sub[c] += sub[plan.sep_down[s]];
+        }
+        const int64_t total = sub[plan.root];
+        std::vector<int> cand{plan.root};
+        std::vector<char> top(nc, 0);
+        while (JT_V_WAVES > 1) {
+            size_t bi = 0;
+            for (size_t i = 1; i < cand.size(); ++i)
+                if (sub[cand[i]] > sub[cand[bi]]) bi = i;
+            const int c = cand[bi];
+            if (sub[c] * JT_V_WAVES <= total || plan.clique_down[c].empty()) break;
+            cand.erase(cand.begin() + bi);
+            top[c] = 1;
+            for (int s : plan.clique_down[c]) cand.push_back(plan.sep_down[s]);
+        }
+        std::stable_sort(cand.begin(), cand.end(), [&](int a, int b) { return sub[a] > sub[b]; });
+        std::vector<int64_t> load(JT_V_WAVES, 0);
+        std::vector<int> owner(nc, -1);  // wave of each non-top clique
+        for (int c : cand) {
+            int w = 0;
+            for (int i = 1; i < JT_V_WAVES; ++i)
+                if (load[i] < load[w]) w = i;
+            load[w] += sub[c];
+            owner[c] = w;
+        }
+        for (int c : pre)  // propagate subtree ownership down (pre-order: parents first)
+            for (int s : plan.clique_down[c]) {
+                const int ch = plan.sep_down[s];
+                if (!top[ch] && owner[ch] < 0) owner[ch] = owner[c];
+            }
+        // segments: collect per wave | collect top | distribute top | distribute per wave
+        prog.sched.clear();
+        prog.order.clear();
+        for (int w = 0; w < JT_V_WAVES; ++w) {
+            prog.sched.push_back((int32_t)prog.order.size());
+            for (int c : post)
+                if (!top[c] && owner[c] == w) prog.order.push_back(c);
+        }
+        prog.sched.push_back((int32_t)prog.order.size());
+        for (int c : post)
+            if (top[c] || JT_V_WAVES == 1) prog.order.push_back(c);
+        prog.sched.push_back((int32_t)prog.order.size());
+        for (int c : pre)
+            if (top[c] || JT_V_WAVES == 1) prog.order.push_back(c);
+        for (int w = 0; w < JT_V_WAVES; ++w) {
+            prog.sched.push_back((int32_t)prog.order.size());
+            for (int c : pre)
+                if (!top[c] && owner[c] == w) prog.order.push_back(c);
+        }
+        prog.sched.push_back((int32_t)prog.order.size());
+        if ((int)prog.order.size() != 2 * nc) return SetError(FBN_ERR_ARG, "internal: streamed schedule covers %zu of %d", prog.order.size(), 2 * nc);
+        int64_t top_cost = 0;
+        for (int c = 0; c < nc; ++c) top_cost += top[c] ? cost[c] : 0;
+        int64_t mx = 0;
+        for (auto l : load) mx = std::max(mx, l);
+        prog.split_efficiency = (double)total / JT_V_WAVES / (double)std::max<int64_t>(1, mx + top_cost);
+    }
 
     // per variable: candidate cliques in container order (GetProbabilitiesOneNode's scan,
     // src/JunctionTree.cpp:1412-1434) and the output slot
