@@ -33,6 +33,7 @@ _SIGS = {
     "fbn_jt_run_device": [_vp, _vp, _i64, _vp, _vp, _vp],
     "fbn_jt_score": [_vp, _vp, _vp, _i64, _vp, _vp],
     "fbn_jt_last_kernel_ms": [_vp, _vp],
+    "fbn_jt_stream_schedule": [_vp, _vp, C.c_int64, _vp, C.c_int64, _vp, _vp],
     "fbn_jt_set_waves_per_cu": [_vp, C.c_int],
     "fbn_jt_set_variant": [_vp, C.c_int],
     "fbn_jt_debug_op_cycles": [_vp, C.c_int, _vp],
@@ -132,7 +133,8 @@ class _PlanInfo(C.Structure):
                 ("clique_entries", C.c_int64), ("separator_entries", C.c_int64),
                 ("algorithmic_bytes_per_case", C.c_int64), ("num_ops", C.c_int32),
                 ("max_vars_per_table", C.c_int32), ("specialized_eligible", C.c_int32),
-                ("variant", C.c_int32)]
+                ("variant", C.c_int32), ("streamed_eligible", C.c_int32), ("streamed_waves", C.c_int32),
+                ("streamed_split_efficiency", C.c_double)]
 
 
 class Network:
@@ -223,6 +225,15 @@ class JunctionTree:
 
     def dump_plan(self, plan_path, init_path):
         lib.fbn_jt_plan_dump(self._h, os.fsencode(plan_path), os.fsencode(init_path))
+
+    def stream_schedule(self):
+        """Streamed-kernel schedule: (order, sched) -- see fbn_jt_stream_schedule."""
+        no, ns = C.c_int64(), C.c_int64()
+        lib.fbn_jt_stream_schedule(self._h, None, 0, None, 0, C.byref(no), C.byref(ns))
+        order = np.zeros(no.value, np.int32)
+        sched = np.zeros(ns.value, np.int32)
+        lib.fbn_jt_stream_schedule(self._h, _p(order), no.value, _p(sched), ns.value, None, None)
+        return order, sched
 
     def set_waves_per_cu(self, w):
         lib.fbn_jt_set_waves_per_cu(self._h, w)

@@ -371,6 +371,27 @@ int fbn_jt_plan_info_get(const fbn_jt_plan *p, fbn_jt_plan_info *info) {
     info->max_vars_per_table = p->prog.max_vars;
     info->specialized_eligible = p->gen_eligible ? 1 : 0;
     info->variant = p->variant >= 0 ? p->variant : p->last_variant;
+    info->streamed_eligible = p->v_ok ? 1 : 0;
+    info->streamed_waves = JT_V_WAVES;
+    info->streamed_split_efficiency = p->v_ok ? p->vprog.split_efficiency : 0.0;
+    return FBN_OK;
+}
+
+int fbn_jt_stream_schedule(const fbn_jt_plan *p, int32_t *order, int64_t order_cap, int32_t *sched,
+                           int64_t sched_cap, int64_t *n_order, int64_t *n_sched) {
+    if (!p) return SetError(FBN_ERR_ARG, "null pointer");
+    if (!p->v_ok) return SetError(FBN_ERR_LIMIT, "plan not eligible for the streamed kernel");
+    const auto &v = p->vprog;
+    if (n_order) *n_order = (int64_t)v.order.size();
+    if (n_sched) *n_sched = (int64_t)v.sched.size();
+    if (order) {
+        if (order_cap < (int64_t)v.order.size()) return SetError(FBN_ERR_ARG, "order buffer too small");
+        std::copy(v.order.begin(), v.order.end(), order);
+    }
+    if (sched) {
+        if (sched_cap < (int64_t)v.sched.size()) return SetError(FBN_ERR_ARG, "sched buffer too small");
+        std::copy(v.sched.begin(), v.sched.end(), sched);
+    }
     return FBN_OK;
 }
 

@@ -80,6 +80,9 @@ typedef struct {
     int32_t max_vars_per_table;
     int32_t specialized_eligible; /* cliques small enough for the plan-specialized kernel */
     int32_t variant;              /* kernel variant runs use (-1 auto before the first run) */
+    int32_t streamed_eligible;    /* the streamed kernel (variant 4) can take the plan */
+    int32_t streamed_waves;       /* waves sharing one 64-case block in variant 4 */
+    double streamed_split_efficiency; /* modelled parallel efficiency of their subtree split */
 } fbn_jt_plan_info;
 
 /* Build the case-independent schedule (JunctionTree ctor, src/JunctionTree.cpp:3-46:
@@ -90,6 +93,11 @@ int fbn_jt_plan_create(const fbn_network *net, int device, fbn_jt_plan **out);
 int fbn_jt_plan_info_get(const fbn_jt_plan *p, fbn_jt_plan_info *info);
 /* Text dump in the same format as the reference harness (tests/golden/alarm_1k.plan/.init). */
 int fbn_jt_plan_dump(const fbn_jt_plan *p, const char *plan_path, const char *init_path);
+/* Diagnostics: the streamed kernel's clique schedule.  order[n_order] = clique ids of the segments
+ * sched[0..n_sched-1] delimits (waves W = streamed_waves): Collect per wave (W), Collect top,
+ * Distribute top, Distribute per wave (W), end.  Pass NULL buffers to query the sizes. */
+int fbn_jt_stream_schedule(const fbn_jt_plan *p, int32_t *order, int64_t order_cap, int32_t *sched,
+                           int64_t sched_cap, int64_t *n_order, int64_t *n_sched);
 /* Evidence cases on the host: evidence [ncases][num_nodes] int8; labels_out [ncases] (arg-max
  * of the query variable 0, InferenceUsingJT src/JunctionTree.cpp:1459-1467); marginals_out
  * [ncases][sum_dom] fp64 or NULL (GetProbabilitiesAllNodes :1385-1454, evidence nodes = 0).

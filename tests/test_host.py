@@ -144,3 +144,71 @@ def test_orientation_random_skeletons():
                 sep[p] = tuple(sorted(rng.sample(others, rng.randint(0, min(3, len(others))))))
         res = F.orient_skeleton(n, edges, sep)
         assert res.oriented == orient.orient(n, edges, sep), trial
+
+
+def _tree_from_dump(path):
+    """parent clique of every clique from a plan dump ('c id ... | up s | down ...', 's id ... | up P | down C')."""
+    sep_parent, clique_up = {}, {}
+    for ln in open(path).read().split("\n"):
+        if ln.startswith("s "):
+            sid = int(ln.split()[1])
+            sep_parent[sid] = int(ln.split("| up")[1].split("|")[0])
+        elif ln.startswith("c "):
+            cid = int(ln.split()[1])
+            up = ln.split("| up")[1].split("|")[0].split()
+            clique_up[cid] = int(up[0]) if up else -1
+    return {c: (sep_parent[s] if s in sep_parent else -1) for c, s in clique_up.items()}
+
+
+@pytest.mark.parametrize("net", ["alarm", "synth200", "munin_like"])
+def test_streamed_schedule_respects_tree_dependencies(tmp_path, net):
+    """Variant 4's block schedule (subtrees per wave in parallel, the top on one wave): every clique
+    once per phase; Collect children before parents, Distribute parents before children, across
+    the barrier-separated segments; subtrees never straddle waves."""
+    from fastbn_amd import synth
+    if net == "alarm":
+        xml = os.path.join(GOLD, "alarm", "alarm.xml")
+    else:
+        xml = str(tmp_path / f"{net}.xml")
+        if net == "synth200":
+            synth.random_network(200, seed=11, window=10, path=xml)
+        else:
+            synth.random_network(1041, seed=1041, window=12, path=xml, name="munin_like")
+    jt = F.JunctionTree(F.Network(xml), device=-1)
+    assert jt.info["streamed_eligible"] == 1
+    W = jt.info["streamed_waves"]
+    order, sched = jt.stream_schedule()
+    assert len(sched) == 2 * W + 3 and sched[-1] == len(order) == 2 * jt.info["num_cliques"]
+    jt.dump_plan(str(tmp_path / "p"), str(tmp_path / "i"))
+    parent = _tree_from_dump(str(tmp_path / "p"))
+    nc = jt.info["num_cliques"]
+    seg = [order[sched[i]:sched[i + 1]].tolist() for i in range(2 * W + 2)]
+    col_w, col_top, dis_top, dis_w = seg[:W], seg[W], seg[W + 1], seg[W + 2:]
+    assert sorted(sum(col_w, []) + col_top) == list(range(nc))
+    assert sorted(sum(dis_w, []) + dis_top) == list(range(nc))
+    assert sorted(col_top) == sorted(dis_top)
+    owner = {c: w for w in range(W) for c in col_w[w]}
+    assert owner == {c: w for w in range(W) for c in dis_w[w]}
+    for c, w in owner.items():  # a subtree clique's parent: same wave or the top
+        assert parent[c] == -1 or parent[c] in col_top or owner.get(parent[c]) == w
+    # Collect: within a wave segment children first; the top runs after every wave segment
+    for w in range(W):
+        pos = {c: i for i, c in enumerate(col_w[w])}
+        for c in col_w[w]:
+            if parent[c] in pos:
+                assert pos[parent[c]] > pos[c]
+    pos = {c: i for i, c in enumerate(col_top)}
+    for c in col_top:
+        if parent[c] in pos:
+            assert pos[parent[c]] > pos[c]
+    # Distribute: the top first (parents first), then each wave's subtrees parents first
+    pos = {c: i for i, c in enumerate(dis_top)}
+    for c in dis_top:
+        if parent[c] != -1:
+            assert parent[c] in pos and pos[parent[c]] < pos[c]
+    for w in range(W):
+        pos = {c: i for i, c in enumerate(dis_w[w])}
+        for c in dis_w[w]:
+            if parent[c] in pos:
+                assert pos[parent[c]] < pos[c]
+    assert 0.5 < jt.info["streamed_split_efficiency"] <= 1.0 or W == 1
