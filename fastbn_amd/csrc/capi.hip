@@ -1,5 +1,6 @@
 // capi.hip -- the extern "C" boundary (include/fastbn.h): handles, device memory, uploads, launches.
 #include <hip/hip_runtime.h>
+#include <chrono>
 
 #include <algorithm>
 #include <cmath>
@@ -1146,6 +1147,8 @@ int CiRunBatch(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alp
     int rc;
     if ((rc = PinnedEnsure(c->h_items, c->h_items_bytes, ib))) return rc;
     if ((rc = PinnedEnsure(c->h_res, c->h_res_bytes, rb))) return rc;
+    static const bool timing = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic
+    auto t0 = std::chrono::steady_clock::now();
     memcpy(c->h_items, items, ib);
     rc = CiLaunchDevice(c, static_cast<const int32_t *>(c->h_items), n, d, alpha, false, nullptr, c->stream);
     if (rc) return rc;
@@ -1153,9 +1156,15 @@ int CiRunBatch(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alp
     int32_t *h_df = reinterpret_cast<int32_t *>(h_ind + (((size_t)n + 3) & ~(size_t)3));
     FBN_HIP(hipMemcpyAsync(h_ind, c->indep.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
     if (df) FBN_HIP(hipMemcpyAsync(h_df, c->df.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    auto t1 = std::chrono::steady_clock::now();
     FBN_HIP(hipStreamSynchronize(c->stream));
+    auto t2 = std::chrono::steady_clock::now();
     memcpy(indep, h_ind, (size_t)n);
     if (df) memcpy(df, h_df, (size_t)n * 4);
+    if (timing)
+        fprintf(stderr, "  ci batch d=%d n=%lld: enqueue %.1f us, wait %.1f us\n", d, (long long)n,
+                std::chrono::duration<double, std::micro>(t1 - t0).count(),
+                std::chrono::duration<double, std::micro>(t2 - t1).count());
     float ms = 0.f;
     FBN_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     res.kernel_s += ms * 1e-3;

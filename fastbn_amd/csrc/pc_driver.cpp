@@ -71,6 +71,9 @@ void Advance(EdgeState &e, int d) {  // ChoiceGenerator::Next (src/ChoiceGenerat
     ++e.pos_in_side;
 }
 
+// levels whose candidate sets number at most this many run in a single round
+constexpr int64_t kFullSpeculation = 4096;
+
 struct Pending {  // one generated test
     int edge;
     int side;
@@ -116,6 +119,27 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
     int64_t open_edges = 0;
     for (auto &s : st) open_edges += !s.resolved;
     int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(32, 8192 / std::max<int64_t>(1, open_edges)));
+    bool full = false;
+    // small levels: every candidate set of every edge in one round (one host round trip per level;
+    // the extra speculative tests cost less than the round trips they save)
+    {
+        auto binom = [](int64_t m, int k) -> int64_t {
+            if (k < 0 || m < k) return 0;
+            int64_t r = 1;
+            for (int i = 1; i <= k; ++i) {
+                r = r * (m - k + i) / i;
+                if (r > (int64_t)1 << 40) return (int64_t)1 << 40;
+            }
+            return r;
+        };
+        int64_t all = 0;
+        for (auto &s : st) {
+            if (s.resolved) continue;
+            all += binom((int64_t)adj[s.x].size() - 1, d) + binom((int64_t)adj[s.y].size() - 1, d);
+            if (all > kFullSpeculation) break;
+        }
+        if (all <= kFullSpeculation) chunk = all, full = true;
+    }
     std::vector<Pending> pend;
     while (true) {
         items.clear();
@@ -142,7 +166,9 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
                     } else {
                         s.side = 2;
                     }
-                    break;  // keep groups aligned: finish this chunk at the side boundary
+                    // keep groups aligned: a partial chunk ends at the side boundary (not needed
+                    // when the round takes every candidate set: no group is ever split)
+                    if (!full) break;
                 }
             }
         }
