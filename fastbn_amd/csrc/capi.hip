@@ -813,8 +813,12 @@ int fbn_ci_dataset_upload(const uint8_t *cols, int nvars, int64_t nsamples, cons
     return FBN_OK;
 }
 
+// items: host copy (validated here).  zc_items / zc_indep / zc_df: optional device-visible
+// (pinned, mapped) host buffers the kernels read the items from and write the decisions to
+// directly -- no staging copies for the small batches of a latency-bound driver round.
 static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alpha, bool want_g2p,
-                          int32_t *counts_dev, hipStream_t s) {
+                          int32_t *counts_dev, hipStream_t s, const int32_t *zc_items = nullptr,
+                          uint8_t *zc_indep = nullptr, int32_t *zc_df = nullptr) {
     if (d < 0 || d > 8) return SetError(FBN_ERR_LIMIT, "conditioning set size %d (supported 0..8)", d);
     const int w = 2 + d;
     // one validation pass: variable ranges and the largest state count (bit-sliced eligibility)
@@ -855,15 +859,17 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
             if ((rc = c->g2.ensure((size_t)n * 8))) return rc;
             if ((rc = c->p.ensure((size_t)n * 8))) return rc;
         }
-        FBN_HIP(hipMemcpyAsync(c->items.p, items, (size_t)n * w * 4, hipMemcpyHostToDevice, s));
+        if (!zc_items) FBN_HIP(hipMemcpyAsync(c->items.p, items, (size_t)n * w * 4, hipMemcpyHostToDevice, s));
+        const int32_t *ditems = zc_items ? zc_items : c->items.as<int32_t>();
         int64_t rows = 0;
         for (int64_t i = 0; i < n * w; ++i) rows += c->dims[items[i]];
         c->last_bytes = rows * c->bits_W * 4;
         FBN_HIP(hipEventRecord(c->ev0, s));
         hipError_t e = fbn_ci_bits_launch(c->bits.as<uint32_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(),
-                                          c->items.as<int32_t>(), c->bits_W, n, d, alpha,
-                                          want_g2p ? c->g2.as<double>() : nullptr, c->df.as<int32_t>(),
-                                          want_g2p ? c->p.as<double>() : nullptr, c->indep.as<uint8_t>(),
+                                          ditems, c->bits_W, n, d, alpha,
+                                          want_g2p ? c->g2.as<double>() : nullptr, zc_df ? zc_df : c->df.as<int32_t>(),
+                                          want_g2p ? c->p.as<double>() : nullptr,
+                                          zc_indep ? zc_indep : c->indep.as<uint8_t>(),
                                           c->bcounts.as<int32_t>(), counts_dev, c->stats.as<unsigned long long>(),
                                           c->num_cu, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci bits kernel launch: %s", hipGetErrorString(e));
@@ -887,7 +893,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         if ((rc = c->g2.ensure((size_t)n * 8))) return rc;
         if ((rc = c->p.ensure((size_t)n * 8))) return rc;
     }
-    FBN_HIP(hipMemcpyAsync(c->items.p, items, (size_t)n * w * 4, hipMemcpyHostToDevice, s));
+    if (!zc_items) FBN_HIP(hipMemcpyAsync(c->items.p, items, (size_t)n * w * 4, hipMemcpyHostToDevice, s));
     int grid = (int)std::min<int64_t>(n, (int64_t)c->num_cu * 8);
     int32_t *gscratch = nullptr;
     if (global_tables) {
@@ -900,9 +906,11 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
     }
     c->last_bytes = n * c->N * (2 + d);  // uint8 columns x, y, z_1..z_d streamed once
     FBN_HIP(hipEventRecord(c->ev0, s));
-    hipError_t e = fbn_ci_launch(c->cols.as<uint8_t>(), c->ddims.as<int32_t>(), c->items.as<int32_t>(), c->N, n, d,
-                                 alpha, want_g2p ? c->g2.as<double>() : nullptr, c->df.as<int32_t>(),
-                                 want_g2p ? c->p.as<double>() : nullptr, c->indep.as<uint8_t>(), counts_dev, lds, grid,
+    hipError_t e = fbn_ci_launch(c->cols.as<uint8_t>(), c->ddims.as<int32_t>(),
+                                 zc_items ? zc_items : c->items.as<int32_t>(), c->N, n, d, alpha,
+                                 want_g2p ? c->g2.as<double>() : nullptr, zc_df ? zc_df : c->df.as<int32_t>(),
+                                 want_g2p ? c->p.as<double>() : nullptr, zc_indep ? zc_indep : c->indep.as<uint8_t>(),
+                                 counts_dev, lds, grid,
                                  gscratch, c->stats.as<unsigned long long>(), s);
     if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci kernel launch: %s", hipGetErrorString(e));
     FBN_HIP(hipEventRecord(c->ev1, s));
@@ -1139,6 +1147,8 @@ void CiCtxShape(const fbn_ci_ctx *c, int *nvars, int64_t *nsamples) {
     *nvars = c->nvars;
     *nsamples = c->N;
 }
+// batches up to this many item bytes take the zero-copy path of CiRunBatch
+constexpr size_t kZeroCopyBytes = 256 << 10;
 int CiRunBatch(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alpha, uint8_t *indep, int32_t *df,
                PCResultHost &res) {
     if (n == 0) return FBN_OK;
@@ -1150,12 +1160,22 @@ int CiRunBatch(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alp
     static const bool timing = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic
     auto t0 = std::chrono::steady_clock::now();
     memcpy(c->h_items, items, ib);
-    rc = CiLaunchDevice(c, static_cast<const int32_t *>(c->h_items), n, d, alpha, false, nullptr, c->stream);
-    if (rc) return rc;
     uint8_t *h_ind = static_cast<uint8_t *>(c->h_res);
     int32_t *h_df = reinterpret_cast<int32_t *>(h_ind + (((size_t)n + 3) & ~(size_t)3));
-    FBN_HIP(hipMemcpyAsync(h_ind, c->indep.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
-    if (df) FBN_HIP(hipMemcpyAsync(h_df, c->df.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    // small rounds (the latency-bound ones): the kernel reads the items from and writes the
+    // decisions to the pinned buffers directly (one launch + one sync per round); large rounds
+    // stage through device memory with DMA copies
+    const bool zc = ib <= kZeroCopyBytes && !getenv("FBN_CI_NO_ZEROCOPY");
+    if (zc) {
+        rc = CiLaunchDevice(c, static_cast<const int32_t *>(c->h_items), n, d, alpha, false, nullptr, c->stream,
+                            static_cast<const int32_t *>(c->h_items), h_ind, df ? h_df : nullptr);
+        if (rc) return rc;
+    } else {
+        rc = CiLaunchDevice(c, static_cast<const int32_t *>(c->h_items), n, d, alpha, false, nullptr, c->stream);
+        if (rc) return rc;
+        FBN_HIP(hipMemcpyAsync(h_ind, c->indep.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+        if (df) FBN_HIP(hipMemcpyAsync(h_df, c->df.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    }
     auto t1 = std::chrono::steady_clock::now();
     FBN_HIP(hipStreamSynchronize(c->stream));
     auto t2 = std::chrono::steady_clock::now();

@@ -24,6 +24,7 @@
 // whose denominators leaves [2^-600, 2^600] is flagged and recomputed by the exact interpreter.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "jt_program.h"
 
@@ -57,7 +58,19 @@ struct Store {
                                               lo, byte_off, 0);
     }
     __device__ __forceinline__ void st_row(int row, double v) const { st(row * 512, v); }
+    // scratch-table accesses with an explicit cache policy (aux bits: 1 sc0, 2 nt, 16 sc1)
+    template <int AUX>
+    __device__ __forceinline__ double ldp(int byte_off) const {
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, lo, byte_off, AUX));
+    }
+    template <int AUX>
+    __device__ __forceinline__ void stp(int byte_off, double v) const {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), r,
+                                              lo, byte_off, AUX);
+    }
 };
+// scratch policy SP of the kernel instance: low byte = aux of scratch stores, next byte = aux of
+// scratch loads
 #define IROW(r) (*(gint *)((gchar *)(Ib + (long long)(r) * 64) + lo4))
 
 // uniform entry-sequence generators: entries bin by bin, each bin in increasing entry order
@@ -170,7 +183,7 @@ __device__ __forceinline__ double pre_eval(const Pre<L> &p, const Dens &D) {
 // normalization sum D_L = sum_e c_L(e), entry order (Normalize, src/PotentialTableBase.cpp:433-445);
 // STORE: c_L(e) is also written to the scratch rows starting at byte offset scr.  Software
 // pipelined: the operands of chunk c+1 are in flight while chunk c is evaluated.
-template <int L, bool P32, bool STORE = false>
+template <int L, bool P32, bool STORE = false, int SP = 0>
 __device__ __forceinline__ double vsum(const Store &S, const Clq &C, const Dens &D, int scr = 0) {
     constexpr int U = Unroll<L>::U;
     double acc = 0.0;
@@ -184,7 +197,7 @@ __device__ __forceinline__ double vsum(const Store &S, const Clq &C, const Dens 
         for (int u = 0; u < U; ++u) {
             const double v = pre_eval<L>(X[u], D);
             acc += v;
-            if (STORE) S.st(scr + (n0 + u) * 512, v);
+            if (STORE) S.template stp<(SP & 255)>(scr + (n0 + u) * 512, v);
         }
     }
     for (; n0 < T; ++n0) {
@@ -192,13 +205,13 @@ __device__ __forceinline__ double vsum(const Store &S, const Clq &C, const Dens 
         pre_load<L, P32>(S, C, n0, X);
         const double v = pre_eval<L>(X, D);
         acc += v;
-        if (STORE) S.st(scr + n0 * 512, v);
+        if (STORE) S.template stp<(SP & 255)>(scr + n0 * 512, v);
     }
     return acc;
 }
 
 // binned pass over the stored table (scratch rows at byte offset scr), divided by Df
-template <class Seq, class Flush>
+template <int SP, class Seq, class Flush>
 __device__ __forceinline__ void vbins_scr(const Store &S, int scr, const Den &Df, int total, Seq seq, int per,
                                           Flush flush) {
     constexpr int U = 16;
@@ -208,7 +221,7 @@ __device__ __forceinline__ void vbins_scr(const Store &S, int scr, const Den &Df
         const int cnt = total - n0 < U ? total - n0 : U;
         double val[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) val[u] = mdiv(S.ld(scr + ((u < cnt) ? seq.next() : 0) * 512), Df);
+        for (int u = 0; u < U; ++u) val[u] = mdiv(S.template ldp<(SP >> 8)>(scr + ((u < cnt) ? seq.next() : 0) * 512), Df);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (u < cnt) {
@@ -287,6 +300,7 @@ __device__ __forceinline__ void vbins(const Store &S, const Clq &C, const Dens &
 // Distribute) of its own disjoint subtrees in parallel, one wave runs the "top" cliques above them
 // (jt_virt_plan.cpp: order / sched segments), barriers between the stages.  More waves per block
 // = more memory-level parallelism for a kernel that is latency-bound at ~2 blocks per SIMD.
+template <int SP>
 __global__ __launch_bounds__(64 * JT_V_WAVES) __attribute__((amdgpu_waves_per_eu(4)))
 void jt_virt_kernel(
     const JtVClique *__restrict__ cls, const int32_t *__restrict__ aux, const double *__restrict__ initv,
@@ -362,7 +376,7 @@ void jt_virt_kernel(
             for (int L = 0; L <= q.k; ++L) {
                 double s = 0.0;
                 if (cmat && L == q.k) {
-#define FBN_SUMCALL(Lc, P) s = vsum<Lc, P, true>(S, C, D, scr)
+#define FBN_SUMCALL(Lc, P) s = vsum<Lc, P, true, SP>(S, C, D, scr)
                     FBN_VDISPATCH(L, p32, FBN_SUMCALL);
 #undef FBN_SUMCALL
                 } else {
@@ -382,7 +396,7 @@ void jt_virt_kernel(
                 const int Ts = q.up_Ts, per = q.T / Ts, dst = q.up_col_row;
                 auto fl = [&](int j, double acc) { S.st_row(dst + j, acc); };
                 if (cmat) {
-                    vbins_scr(S, scr, pick(D, q.k), q.T, SeqCol{0, 0, 0, Ts, per}, per, fl);
+                    vbins_scr<SP>(S, scr, pick(D, q.k), q.T, SeqCol{0, 0, 0, Ts, per}, per, fl);
                 } else {
 #define FBN_COLCALL(Lc, P) vbins<Lc, P>(S, C, D, SeqCol{0, 0, 0, Ts, per}, per, fl)
                     FBN_VDISPATCH(q.k, p32, FBN_COLCALL);
@@ -424,7 +438,7 @@ void jt_virt_kernel(
             if (!q.root && !(dbg & 8)) {
                 double s = 0.0;
                 if (q.mat && !(dbg & 64) && !((dbg & 512) && q.k < 2)) {
-#define FBN_SUMCALL(Lc, P) s = vsum<Lc, P, true>(S, C, D, scr)
+#define FBN_SUMCALL(Lc, P) s = vsum<Lc, P, true, SP>(S, C, D, scr)
                     FBN_VDISPATCH(q.k + 1, p32, FBN_SUMCALL);
 #undef FBN_SUMCALL
                 } else {
@@ -455,7 +469,7 @@ void jt_virt_kernel(
                     }
                 };
                 if (q.mat && !(dbg & 64) && !((dbg & 512) && q.k < 2)) {
-                    vbins_scr(S, scr, pick(D, Lf), q.T, SeqList{lst, 0}, per, fl);
+                    vbins_scr<SP>(S, scr, pick(D, Lf), q.T, SeqList{lst, 0}, per, fl);
                 } else {
 #define FBN_DISCALL(Lc, P) vbins<Lc, P>(S, C, D, SeqList{lst, 0}, per, fl)
                     FBN_VDISPATCH(Lf, p32, FBN_DISCALL);
@@ -493,7 +507,7 @@ void jt_virt_kernel(
                     tot += acc;
                 };
                 if (q.mat && !(dbg & 64) && !((dbg & 512) && q.k < 2)) {
-                    vbins_scr(S, scr, pick(D, Lf), q.T, SeqMarg{0, 0, 0, 0, cum, bw, q.T / bw}, q.T / dim, fl);
+                    vbins_scr<SP>(S, scr, pick(D, Lf), q.T, SeqMarg{0, 0, 0, 0, cum, bw, q.T / bw}, q.T / dim, fl);
                 } else {
 #define FBN_MARGCALL(Lc, P) vbins<Lc, P>(S, C, D, SeqMarg{0, 0, 0, 0, cum, bw, q.T / bw}, q.T / dim, fl)
                     FBN_VDISPATCH(Lf, p32, FBN_MARGCALL);
@@ -557,8 +571,18 @@ extern "C" hipError_t fbn_jt_virt_launch(const JtVClique *cls, const int32_t *au
                                          double *ws, int32_t *wsi, int *flags, long long ncases, long long store_rows,
                                          long long scratch_row, long long scratch_rows, int nc, int V, int SD,
                                          int grid, int dbg, hipStream_t stream) {
-    hipLaunchKernelGGL(jt_virt_kernel, dim3(grid), dim3(64 * JT_V_WAVES), 0, stream, cls, aux, initv, dig, order,
-                       sched, vsel, evid, marg, labels, ws, wsi, flags, ncases, store_rows, scratch_row, scratch_rows,
-                       nc, V, SD, dbg);
+    // scratch-table cache policy (diagnostic override FBN_JT_VPOL; results do not depend on it)
+    static const int pol = getenv("FBN_JT_VPOL") ? atoi(getenv("FBN_JT_VPOL")) : 1;
+#define FBN_VLAUNCH(SPv)                                                                                          \
+    hipLaunchKernelGGL(jt_virt_kernel<SPv>, dim3(grid), dim3(64 * JT_V_WAVES), 0, stream, cls, aux, initv, dig, \
+                       order, sched, vsel, evid, marg, labels, ws, wsi, flags, ncases, store_rows, scratch_row,  \
+                       scratch_rows, nc, V, SD, dbg)
+    switch (pol) {
+    case 1: FBN_VLAUNCH(2 | (2 << 8)); break;     // nt stores, nt loads
+    case 2: FBN_VLAUNCH(16 | (2 << 8)); break;    // sc1 stores (line dropped from L2), nt loads
+    case 3: FBN_VLAUNCH(18 | (18 << 8)); break;   // sc1|nt both ways
+    default: FBN_VLAUNCH(0); break;
+    }
+#undef FBN_VLAUNCH
     return hipGetLastError();
 }

@@ -71,8 +71,12 @@ void Advance(EdgeState &e, int d) {  // ChoiceGenerator::Next (src/ChoiceGenerat
     ++e.pos_in_side;
 }
 
-// levels whose candidate sets number at most this many run in a single round
-constexpr int64_t kFullSpeculation = 4096;
+// levels whose candidate sets number at most this many run in a single round (FBN_PC_FULLSPEC:
+// diagnostic override)
+int64_t FullSpeculation() {
+    static const int64_t v = getenv("FBN_PC_FULLSPEC") ? atoll(getenv("FBN_PC_FULLSPEC")) : 4096;
+    return v;
+}
 
 struct Pending {  // one generated test
     int edge;
@@ -132,13 +136,14 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
             }
             return r;
         };
+        const int64_t cap = FullSpeculation();
         int64_t all = 0;
         for (auto &s : st) {
             if (s.resolved) continue;
             all += binom((int64_t)adj[s.x].size() - 1, d) + binom((int64_t)adj[s.y].size() - 1, d);
-            if (all > kFullSpeculation) break;
+            if (all > cap) break;
         }
-        if (all <= kFullSpeculation) chunk = all, full = true;
+        if (all <= cap) chunk = all, full = true;
     }
     std::vector<Pending> pend;
     while (true) {

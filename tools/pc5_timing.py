@@ -1,0 +1,27 @@
+"""Diagnostic: repeated PC-stable runs on the config-5 dataset (1000 vars x 100k samples, levels
+0-5) with per-run driver/kernel times; FBN_PC_TIMING=1 adds per-level host phase times."""
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import fastbn_amd as F  # noqa: E402
+from fastbn_amd import synth  # noqa: E402
+
+runs = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+path = "/tmp/pc_c5.xml"
+synth.random_network(1000, seed=1000, window=50, parent_probs=(1, 1, 1), dom=(2, 4), path=path, k_min=0)
+cols = synth.forward_sample(synth.read_xmlbif(path), 100000, seed=1000)
+dims = (cols.max(axis=1).astype(np.int32) + 1)
+ds = F.Dataset(columns=cols, dims=dims)
+for r in range(runs):
+    pc = F.PCStable(0.05, 6)
+    t0 = time.time()
+    pc.StructLearnCompData(ds)
+    wall = time.time() - t0
+    print(f"run {r}: wall {wall * 1e3:.1f} ms, driver {pc.total_s * 1e3:.1f} ms, kernels {pc.kernel_s * 1e3:.1f} ms, "
+          f"tests {pc.tests_per_level.tolist()} launched {pc.launched_per_level.tolist()} edges {len(pc.edges)}",
+          file=sys.stderr, flush=True)
