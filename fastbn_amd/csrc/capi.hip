@@ -823,11 +823,14 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
     const int w = 2 + d;
     // one validation pass: variable ranges and the largest state count (bit-sliced eligibility)
     int maxdim = 0;
+    int64_t dim_rows = 0;  // sum of the items' state counts (bit-sliced input bytes)
+    const int *dims = c->dims.data();
     for (int64_t i = 0; i < n * w; ++i) {
         const int v = items[i];
-        if (v < 0 || v >= c->nvars)
+        if ((unsigned)v >= (unsigned)c->nvars)
             return SetError(FBN_ERR_ARG, "test %lld: variable %d out of range", (long long)(i / w), v);
-        maxdim = std::max(maxdim, c->dims[v]);
+        maxdim = std::max(maxdim, dims[v]);
+        dim_rows += dims[v];
     }
     int rc;
     // tests with <= 1 conditioning variable over variables with <= 4 states: popcounts of
@@ -861,9 +864,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         }
         if (!zc_items) FBN_HIP(hipMemcpyAsync(c->items.p, items, (size_t)n * w * 4, hipMemcpyHostToDevice, s));
         const int32_t *ditems = zc_items ? zc_items : c->items.as<int32_t>();
-        int64_t rows = 0;
-        for (int64_t i = 0; i < n * w; ++i) rows += c->dims[items[i]];
-        c->last_bytes = rows * c->bits_W * 4;
+        c->last_bytes = dim_rows * c->bits_W * 4;
         FBN_HIP(hipEventRecord(c->ev0, s));
         hipError_t e = fbn_ci_bits_launch(c->bits.as<uint32_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(),
                                           ditems, c->bits_W, n, d, alpha,
@@ -1026,11 +1027,14 @@ int fbn_pc_sepsets(const fbn_pc_result *r, int32_t *buf, int64_t cap, int64_t *l
         if (buf && k < cap) buf[k] = v;
         ++k;
     };
-    for (auto &kv : r->r.sepset.entries()) {
-        put(kv.first.first);
-        put(kv.first.second);
-        put((int32_t)kv.second.size());
-        for (int z : kv.second) put(z);
+    const auto &sm = r->r.sepset;
+    for (size_t i = 0, n = sm.sorted_size(); i < n; ++i) {
+        const auto key = sm.key(i);
+        const auto z = sm.value(i);
+        put(key.first);
+        put(key.second);
+        put((int32_t)z.size());
+        for (int v : z) put(v);
     }
     if (len) *len = k;
     return FBN_OK;
@@ -1060,7 +1064,7 @@ int fbn_pc_level(fbn_ci_ctx *c, double alpha, int d, int group_size, const int32
     for (int64_t e = 0; e < e_end - e_begin; ++e) {
         removed[e] = out.removed[e] ? 1 : 0;
         if (sepsets)
-            for (int j = 0; j < d; ++j) sepsets[e * d + j] = out.removed[e] ? out.sep[e][j] : -1;
+            for (int j = 0; j < d; ++j) sepsets[e * d + j] = out.removed[e] ? out.sep[(size_t)e * d + j] : -1;
     }
     if (counted) *counted = out.counted;
     if (launched) *launched = out.launched;
@@ -1080,7 +1084,7 @@ int fbn_pc_orient_skeleton(int nvars, const int32_t *pairs, int nedges, const in
     for (int64_t k = 0; k < len;) {  // (x, y, m, z_0..z_{m-1}) records, as fbn_pc_sepsets writes them
         if (k + 3 > len || k + 3 + sepsets[k + 2] > len || sepsets[k + 2] < 0) return SetError(FBN_ERR_ARG, "bad sepset list");
         const int x = sepsets[k], y = sepsets[k + 1], m = sepsets[k + 2];
-        r->r.sepset.set({std::min(x, y), std::max(x, y)}, std::vector<int>(sepsets + k + 3, sepsets + k + 3 + m));
+        r->r.sepset.set({std::min(x, y), std::max(x, y)}, sepsets + k + 3, m);
         k += 3 + m;
     }
     int rc = fbn::OrientPC(nvars, r->r);

@@ -29,25 +29,33 @@ namespace fbn {
 
 namespace {
 
+constexpr int kMaxD = 8;  // CI tests take at most 8 conditioning variables (capi.hip)
+
+// one edge's search state: the current side's candidate list is adj(a) \ {b}, read in place
+// (element i = base[i + (i >= skip)]), the next combination as positions into it
 struct EdgeState {
     int x, y;
     int side = 0;                // 0: adj(x)\{y}, 1: adj(y)\{x}, 2: exhausted
-    std::vector<int> A;          // current side's adjacency (sorted)
-    std::vector<int> ch;         // next combination (positions in A)
+    const int *base = nullptr;   // adj(a), sorted
+    int m = 0;                   // |adj(a) \ {b}|
+    int skip = 0;                // position of b in adj(a) (m + 1 if absent)
+    int ch[kMaxD];               // next combination (positions in the candidate list)
     bool has_next = false;
     int64_t pos_in_side = 0;     // index of the next combination within the side
     bool resolved = false, removed = false;
-    std::vector<int> sep;
+    int A(int i) const { return base[i + (i >= skip)]; }
 };
 
 void StartSide(EdgeState &e, const std::vector<std::vector<int>> &adj, int d) {
     while (e.side < 2) {
-        int a = e.side ? e.y : e.x, b = e.side ? e.x : e.y;
-        e.A.clear();
-        for (int u : adj[a])
-            if (u != b) e.A.push_back(u);
-        if ((int)e.A.size() >= d) {
-            e.ch.resize(d);
+        const int a = e.side ? e.y : e.x, b = e.side ? e.x : e.y;
+        const std::vector<int> &L = adj[a];
+        const int pos = (int)(std::lower_bound(L.begin(), L.end(), b) - L.begin());
+        const bool has_b = pos < (int)L.size() && L[pos] == b;
+        e.base = L.data();
+        e.m = (int)L.size() - (has_b ? 1 : 0);
+        e.skip = has_b ? pos : (int)L.size() + 1;
+        if (e.m >= d) {
             for (int i = 0; i < d; ++i) e.ch[i] = i;
             e.has_next = true;
             e.pos_in_side = 0;
@@ -59,7 +67,7 @@ void StartSide(EdgeState &e, const std::vector<std::vector<int>> &adj, int d) {
 }
 
 void Advance(EdgeState &e, int d) {  // ChoiceGenerator::Next (src/ChoiceGenerator.cpp:55-85)
-    const int m = (int)e.A.size();
+    const int m = e.m;
     int i = d - 1;
     while (i >= 0 && e.ch[i] == m - d + i) --i;
     if (i < 0) {
@@ -96,7 +104,8 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
              PCResultHost &res) {
     const size_t E = e_end - e_begin;
     out.removed.assign(E, 0);
-    out.sep.assign(E, {});
+    out.d = d;
+    out.sep.assign(E * (size_t)d, -1);
     out.counted = out.launched = 0;
     std::vector<int32_t> items;
     std::vector<uint8_t> indep;
@@ -111,6 +120,7 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
         out.counted = out.launched = (int64_t)E;
         return FBN_OK;
     }
+    if (d > kMaxD) return SetError(FBN_ERR_LIMIT, "conditioning set size %d (supported 0..%d)", d, kMaxD);
     std::vector<EdgeState> st(E);
     for (size_t e = 0; e < E; ++e) {
         st[e].x = edges[e_begin + e].first;
@@ -146,7 +156,9 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
         if (all <= cap) chunk = all, full = true;
     }
     std::vector<Pending> pend;
+    static const bool timing = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic
     while (true) {
+        auto tg0 = std::chrono::steady_clock::now();
         items.clear();
         pend.clear();
         for (size_t e = 0; e < st.size(); ++e) {
@@ -160,7 +172,7 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
                 pend.push_back(p);
                 items.push_back(s.x);
                 items.push_back(s.y);
-                for (int i = 0; i < d; ++i) items.push_back(s.A[s.ch[i]]);
+                for (int i = 0; i < d; ++i) items.push_back(s.A(s.ch[i]));
                 --want;
                 Advance(s, d);
                 if (!s.has_next) {
@@ -181,8 +193,10 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
         const int64_t nt = (int64_t)pend.size();
         indep.resize(nt);
         dfv.resize(nt);
+        auto tg1 = std::chrono::steady_clock::now();
         int rc = CiRunBatch(ctx, items.data(), nt, d, alpha, indep.data(), dfv.data(), res);
         if (rc) return rc;
+        auto tg2 = std::chrono::steady_clock::now();
         out.launched += nt;
         // resolve in order per edge
         size_t i = 0;
@@ -204,9 +218,9 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
                     if (ind) {
                         s.removed = true;
                         s.resolved = true;
-                        std::vector<int> z(items.begin() + (2 + d) * t + 2, items.begin() + (2 + d) * (t + 1));
-                        std::sort(z.begin(), z.end());
-                        s.sep = z;
+                        int *z = out.sep.data() + (size_t)e * d;
+                        std::copy(items.begin() + (2 + d) * t + 2, items.begin() + (2 + d) * (t + 1), z);
+                        std::sort(z, z + d);
                         break;
                     }
                 }
@@ -215,10 +229,15 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
             if (!s.removed && !s.has_next) s.resolved = true;  // exhausted: dependent, kept
             i = j;
         }
+        if (timing)
+            fprintf(stderr, "   round d=%d: %lld tests, generate %.2f ms, batch %.2f ms, resolve %.2f ms\n", d,
+                    (long long)nt, std::chrono::duration<double, std::milli>(tg1 - tg0).count(),
+                    std::chrono::duration<double, std::milli>(tg2 - tg1).count(),
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tg2).count());
         chunk = std::min<int64_t>(chunk * 4, 1 << 16);
     }
     for (size_t e = 0; e < E; ++e)
-        if (st[e].removed) out.removed[e] = 1, out.sep[e] = st[e].sep;
+        if (st[e].removed) out.removed[e] = 1;
     return FBN_OK;
 }
 
@@ -267,7 +286,7 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
         auto tb = std::chrono::steady_clock::now();
         res.sepset.reserve(res.sepset.size() + edges.size());
         for (size_t e = 0; e < edges.size(); ++e)
-            if (out.removed[e]) res.sepset.set(edges[e], std::move(out.sep[e]));
+            if (out.removed[e]) res.sepset.set(edges[e], out.sep.data() + e * (size_t)d, d);
         res.tests_per_level.push_back(out.counted);
         res.launched_per_level.push_back(out.launched);
         auto tc = std::chrono::steady_clock::now();

@@ -14,43 +14,73 @@
 
 namespace fbn {
 
-// sepsets keyed by (min, max): appended per level, sorted once on first lookup / iteration (a
-// node-based map cost ~40 ms of host time for the ~500k marginal removals of a 1000-variable run)
+// sepsets keyed by (min, max), flat: keys, (offset, length) into one int pool.  Appended per level,
+// sorted once on first lookup / iteration (a node-based map cost ~40 ms, a vector of vectors ~3 ms,
+// of host time for the ~500k marginal removals of a 1000-variable run)
 class SepsetMap {
   public:
-    typedef std::pair<std::pair<int, int>, std::vector<int>> Entry;
-    void set(std::pair<int, int> key, std::vector<int> z) {
-        sorted_ = sorted_ && (v_.empty() || v_.back().first < key);
-        v_.emplace_back(key, std::move(z));
+    struct View {  // the sorted sepset of one key
+        const int *p;
+        int n;
+        const int *begin() const { return p; }
+        const int *end() const { return p + n; }
+        size_t size() const { return (size_t)n; }
+    };
+    void set(std::pair<int, int> key, const int *z, int n) {
+        sorted_ = sorted_ && (keys_.empty() || keys_.back() < key);
+        keys_.push_back(key);
+        off_.push_back((int64_t)pool_.size());
+        len_.push_back(n);
+        pool_.insert(pool_.end(), z, z + n);
     }
-    const std::vector<int> *find(std::pair<int, int> key) const {
+    void set(std::pair<int, int> key, const std::vector<int> &z) { set(key, z.data(), (int)z.size()); }
+    bool find(std::pair<int, int> key, View *v) const {
         sort();
-        auto it = std::lower_bound(v_.begin(), v_.end(), key,
-                                   [](const Entry &e, const std::pair<int, int> &k) { return e.first < k; });
-        return (it != v_.end() && it->first == key) ? &it->second : nullptr;
+        auto it = std::lower_bound(keys_.begin(), keys_.end(), key);
+        if (it == keys_.end() || *it != key) return false;
+        const size_t i = (size_t)(it - keys_.begin());
+        *v = View{pool_.data() + off_[i], len_[i]};
+        return true;
     }
-    const std::vector<Entry> &entries() const {  // ascending keys
+    size_t size() const { return keys_.size(); }  // entries appended (no sort)
+    // iteration in ascending key order: n = sorted_size(), then key(i) / value(i) for i < n
+    size_t sorted_size() const {
         sort();
-        return v_;
+        return keys_.size();
     }
-    size_t size() const { return v_.size(); }
-    void reserve(size_t n) { v_.reserve(n); }
+    std::pair<int, int> key(size_t i) const { return keys_[i]; }
+    View value(size_t i) const { return View{pool_.data() + off_[i], len_[i]}; }
+    void reserve(size_t n) {
+        keys_.reserve(n);
+        off_.reserve(n);
+        len_.reserve(n);
+    }
 
   private:
     void sort() const {
         if (sorted_) return;
         // a key set twice keeps its last value (std::map assignment semantics)
-        std::stable_sort(v_.begin(), v_.end(), [](const Entry &a, const Entry &b) { return a.first < b.first; });
-        size_t o = 0;
-        for (size_t i = 0; i < v_.size(); ++i) {
-            if (o > 0 && v_[o - 1].first == v_[i].first) v_[o - 1] = std::move(v_[i]);
-            else if (o != i) v_[o++] = std::move(v_[i]);
-            else ++o;
+        std::vector<int64_t> idx(keys_.size());
+        for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int64_t)i;
+        std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return keys_[a] < keys_[b]; });
+        std::vector<std::pair<int, int>> k;
+        std::vector<int64_t> o;
+        std::vector<int> l;
+        k.reserve(idx.size()), o.reserve(idx.size()), l.reserve(idx.size());
+        for (int64_t i : idx) {
+            if (!k.empty() && k.back() == keys_[i]) {
+                o.back() = off_[i], l.back() = len_[i];
+            } else {
+                k.push_back(keys_[i]), o.push_back(off_[i]), l.push_back(len_[i]);
+            }
         }
-        v_.resize(o);
+        keys_.swap(k), off_.swap(o), len_.swap(l);
         sorted_ = true;
     }
-    mutable std::vector<Entry> v_;
+    mutable std::vector<std::pair<int, int>> keys_;
+    mutable std::vector<int64_t> off_;
+    mutable std::vector<int> len_;
+    std::vector<int> pool_;
     mutable bool sorted_ = true;
 };
 
@@ -78,7 +108,8 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
 // one level for an edge range (the unit a multi-GPU driver partitions), see pc_driver.cpp
 struct LevelOut {
     std::vector<char> removed;
-    std::vector<std::vector<int>> sep;
+    int d = 0;
+    std::vector<int> sep;  // [edge][d]: the sorted sepset of each removed edge of the range
     int64_t counted = 0, launched = 0;
 };
 int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::vector<std::vector<int>> &adj,

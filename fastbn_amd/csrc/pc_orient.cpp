@@ -124,9 +124,9 @@ struct Orienter {
         return IsAdjacentTo(a, b) && !g.IsDirectedFromTo(a, b) && !g.IsDirectedFromTo(b, a);
     }
     bool InSepset(int a, int c, int b) const {
-        const std::vector<int> *z = sepset.find({a, c});
-        if (!z) return false;
-        return std::find(z->begin(), z->end(), b) != z->end();
+        SepsetMap::View z;
+        if (!sepset.find({a, c}, &z)) return false;
+        return std::find(z.begin(), z.end(), b) != z.end();
     }
 
     void VStructures() {
