@@ -136,29 +136,41 @@ struct fbn_jt_plan {
     }
 };
 
+// per-slot state of the CI launches: the PC driver keeps two batches in flight (one per half of
+// the level's edges) on the ctx stream, so every buffer a launch (re)sizes or writes is per slot
+struct CiSlot {
+    DevBuf items, indep, df, bcounts, scratch;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;  // kernel start / end, batch results ready
+    int64_t last_bytes = 0;  // input bytes of the last launch in the kernel's own format (roofline)
+    // pinned host staging of the driver's batches
+    void *h_items = nullptr, *h_res = nullptr;
+    size_t h_items_bytes = 0, h_res_bytes = 0;
+    int64_t n = 0;  // batch in flight
+    bool zc = false, want_df = false;
+    ~CiSlot() {
+        if (h_items) (void)hipHostFree(h_items);
+        if (h_res) (void)hipHostFree(h_res);
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+        if (done) (void)hipEventDestroy(done);
+    }
+};
+
 struct fbn_ci_ctx {
     int device = 0, num_cu = 0, nvars = 0;
     int64_t N = 0;
     std::vector<int32_t> dims;
-    DevBuf cols, ddims, items, g2, df, p, indep, counts, scratch;
+    DevBuf cols, ddims, g2, p, counts;
     DevBuf stats;  // decision-margin log: {min |p - alpha| bits, #tests within 1e-9 of alpha}
     // bit-sliced columns for marginal tests (ci_bits.hip), built on first use
-    DevBuf bits, brow, bcounts;
+    DevBuf bits, brow;
     bool bits_ready = false;
     int64_t bits_W = 0;
-    int64_t last_bytes = 0;  // input bytes of the last launch in the kernel's own format (roofline)
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    CiSlot slot[2];
     hipStream_t stream = nullptr;  // the PC driver's rounds (pinned staging, one sync per round)
     float last_ms = 0.f;
-    // pinned host staging for the driver's batches
-    void *h_items = nullptr, *h_res = nullptr;
-    size_t h_items_bytes = 0, h_res_bytes = 0;
     ~fbn_ci_ctx() {
-        if (h_items) (void)hipHostFree(h_items);
-        if (h_res) (void)hipHostFree(h_res);
         if (stream) (void)hipStreamDestroy(stream);
-        if (ev0) (void)hipEventDestroy(ev0);
-        if (ev1) (void)hipEventDestroy(ev1);
     }
 };
 
@@ -804,8 +816,11 @@ int fbn_ci_dataset_upload(const uint8_t *cols, int nvars, int64_t nsamples, cons
     if ((rc = c->ddims.ensure((size_t)nvars * 4))) return rc;
     FBN_HIP(hipMemcpy(c->cols.p, cols, (size_t)nvars * nsamples, hipMemcpyHostToDevice));
     FBN_HIP(hipMemcpy(c->ddims.p, dims, (size_t)nvars * 4, hipMemcpyHostToDevice));
-    FBN_HIP(hipEventCreate(&c->ev0));
-    FBN_HIP(hipEventCreate(&c->ev1));
+    for (auto &sl : c->slot) {
+        FBN_HIP(hipEventCreate(&sl.ev0));
+        FBN_HIP(hipEventCreate(&sl.ev1));
+        FBN_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    }
     FBN_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     if ((rc = c->stats.ensure(16))) return rc;
     if ((rc = CiResetMargin(c.get()))) return rc;
@@ -817,20 +832,26 @@ int fbn_ci_dataset_upload(const uint8_t *cols, int nvars, int64_t nsamples, cons
 // (pinned, mapped) host buffers the kernels read the items from and write the decisions to
 // directly -- no staging copies for the small batches of a latency-bound driver round.
 static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alpha, bool want_g2p,
-                          int32_t *counts_dev, hipStream_t s, const int32_t *zc_items = nullptr,
-                          uint8_t *zc_indep = nullptr, int32_t *zc_df = nullptr) {
+                          int32_t *counts_dev, hipStream_t s, int k = 0, const int32_t *zc_items = nullptr,
+                          uint8_t *zc_indep = nullptr, int32_t *zc_df = nullptr, const fbn::CiBatchStats *pre = nullptr) {
+    CiSlot &S = c->slot[k];
     if (d < 0 || d > 8) return SetError(FBN_ERR_LIMIT, "conditioning set size %d (supported 0..8)", d);
     const int w = 2 + d;
     // one validation pass: variable ranges and the largest state count (bit-sliced eligibility)
+    // (skipped for batches generated by the driver from the skeleton, which pass the same figures)
     int maxdim = 0;
     int64_t dim_rows = 0;  // sum of the items' state counts (bit-sliced input bytes)
     const int *dims = c->dims.data();
-    for (int64_t i = 0; i < n * w; ++i) {
-        const int v = items[i];
-        if ((unsigned)v >= (unsigned)c->nvars)
-            return SetError(FBN_ERR_ARG, "test %lld: variable %d out of range", (long long)(i / w), v);
-        maxdim = std::max(maxdim, dims[v]);
-        dim_rows += dims[v];
+    if (pre) {
+        maxdim = pre->maxdim, dim_rows = pre->dim_rows;
+    } else {
+        for (int64_t i = 0; i < n * w; ++i) {
+            const int v = items[i];
+            if ((unsigned)v >= (unsigned)c->nvars)
+                return SetError(FBN_ERR_ARG, "test %lld: variable %d out of range", (long long)(i / w), v);
+            maxdim = std::max(maxdim, dims[v]);
+            dim_rows += dims[v];
+        }
     }
     int rc;
     // tests with <= 1 conditioning variable over variables with <= 4 states: popcounts of
@@ -854,27 +875,27 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
             c->bits_W = W;
             c->bits_ready = true;
         }
-        if ((rc = c->items.ensure((size_t)n * w * 4))) return rc;
-        if ((rc = c->indep.ensure((size_t)n))) return rc;
-        if ((rc = c->df.ensure((size_t)n * 4))) return rc;
-        if ((rc = c->bcounts.ensure((size_t)n * 64 * 4))) return rc;
+        if ((rc = S.items.ensure((size_t)n * w * 4))) return rc;
+        if ((rc = S.indep.ensure((size_t)n))) return rc;
+        if ((rc = S.df.ensure((size_t)n * 4))) return rc;
+        if ((rc = S.bcounts.ensure((size_t)n * 64 * 4))) return rc;
         if (want_g2p) {
             if ((rc = c->g2.ensure((size_t)n * 8))) return rc;
             if ((rc = c->p.ensure((size_t)n * 8))) return rc;
         }
-        if (!zc_items) FBN_HIP(hipMemcpyAsync(c->items.p, items, (size_t)n * w * 4, hipMemcpyHostToDevice, s));
-        const int32_t *ditems = zc_items ? zc_items : c->items.as<int32_t>();
-        c->last_bytes = dim_rows * c->bits_W * 4;
-        FBN_HIP(hipEventRecord(c->ev0, s));
+        if (!zc_items) FBN_HIP(hipMemcpyAsync(S.items.p, items, (size_t)n * w * 4, hipMemcpyHostToDevice, s));
+        const int32_t *ditems = zc_items ? zc_items : S.items.as<int32_t>();
+        S.last_bytes = dim_rows * c->bits_W * 4;
+        FBN_HIP(hipEventRecord(S.ev0, s));
         hipError_t e = fbn_ci_bits_launch(c->bits.as<uint32_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(),
                                           ditems, c->bits_W, n, d, alpha,
-                                          want_g2p ? c->g2.as<double>() : nullptr, zc_df ? zc_df : c->df.as<int32_t>(),
+                                          want_g2p ? c->g2.as<double>() : nullptr, zc_df ? zc_df : S.df.as<int32_t>(),
                                           want_g2p ? c->p.as<double>() : nullptr,
-                                          zc_indep ? zc_indep : c->indep.as<uint8_t>(),
-                                          c->bcounts.as<int32_t>(), counts_dev, c->stats.as<unsigned long long>(),
+                                          zc_indep ? zc_indep : S.indep.as<uint8_t>(),
+                                          S.bcounts.as<int32_t>(), counts_dev, c->stats.as<unsigned long long>(),
                                           c->num_cu, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci bits kernel launch: %s", hipGetErrorString(e));
-        FBN_HIP(hipEventRecord(c->ev1, s));
+        FBN_HIP(hipEventRecord(S.ev1, s));
         return FBN_OK;
     }
     size_t lds = 0;
@@ -887,14 +908,14 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
     }
     // tables beyond the LDS budget: the same layout in a per-workgroup global scratch region
     const bool global_tables = lds > 160 * 1024;
-    if ((rc = c->items.ensure((size_t)n * w * 4))) return rc;
-    if ((rc = c->indep.ensure((size_t)n))) return rc;
-    if ((rc = c->df.ensure((size_t)n * 4))) return rc;
+    if ((rc = S.items.ensure((size_t)n * w * 4))) return rc;
+    if ((rc = S.indep.ensure((size_t)n))) return rc;
+    if ((rc = S.df.ensure((size_t)n * 4))) return rc;
     if (want_g2p) {
         if ((rc = c->g2.ensure((size_t)n * 8))) return rc;
         if ((rc = c->p.ensure((size_t)n * 8))) return rc;
     }
-    if (!zc_items) FBN_HIP(hipMemcpyAsync(c->items.p, items, (size_t)n * w * 4, hipMemcpyHostToDevice, s));
+    if (!zc_items) FBN_HIP(hipMemcpyAsync(S.items.p, items, (size_t)n * w * 4, hipMemcpyHostToDevice, s));
     int grid = (int)std::min<int64_t>(n, (int64_t)c->num_cu * 8);
     int32_t *gscratch = nullptr;
     if (global_tables) {
@@ -902,19 +923,19 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         // workgroups for very large tables; each loops over its tests)
         const size_t stride = ((lds / 4 + 1) & ~(size_t)1) * 4;
         grid = (int)std::max<size_t>(1, std::min<size_t>((size_t)grid, ((size_t)4 << 30) / stride));
-        if ((rc = c->scratch.ensure((size_t)grid * stride))) return rc;
-        gscratch = c->scratch.as<int32_t>();
+        if ((rc = S.scratch.ensure((size_t)grid * stride))) return rc;
+        gscratch = S.scratch.as<int32_t>();
     }
-    c->last_bytes = n * c->N * (2 + d);  // uint8 columns x, y, z_1..z_d streamed once
-    FBN_HIP(hipEventRecord(c->ev0, s));
+    S.last_bytes = n * c->N * (2 + d);  // uint8 columns x, y, z_1..z_d streamed once
+    FBN_HIP(hipEventRecord(S.ev0, s));
     hipError_t e = fbn_ci_launch(c->cols.as<uint8_t>(), c->ddims.as<int32_t>(),
-                                 zc_items ? zc_items : c->items.as<int32_t>(), c->N, n, d, alpha,
-                                 want_g2p ? c->g2.as<double>() : nullptr, zc_df ? zc_df : c->df.as<int32_t>(),
-                                 want_g2p ? c->p.as<double>() : nullptr, zc_indep ? zc_indep : c->indep.as<uint8_t>(),
+                                 zc_items ? zc_items : S.items.as<int32_t>(), c->N, n, d, alpha,
+                                 want_g2p ? c->g2.as<double>() : nullptr, zc_df ? zc_df : S.df.as<int32_t>(),
+                                 want_g2p ? c->p.as<double>() : nullptr, zc_indep ? zc_indep : S.indep.as<uint8_t>(),
                                  counts_dev, lds, grid,
                                  gscratch, c->stats.as<unsigned long long>(), s);
     if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci kernel launch: %s", hipGetErrorString(e));
-    FBN_HIP(hipEventRecord(c->ev1, s));
+    FBN_HIP(hipEventRecord(S.ev1, s));
     return FBN_OK;
 }
 
@@ -928,10 +949,10 @@ int fbn_ci_run(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alp
     if (rc) return rc;
     if (g2) FBN_HIP(hipMemcpyAsync(g2, c->g2.p, (size_t)n * 8, hipMemcpyDeviceToHost, s));
     if (p) FBN_HIP(hipMemcpyAsync(p, c->p.p, (size_t)n * 8, hipMemcpyDeviceToHost, s));
-    if (df) FBN_HIP(hipMemcpyAsync(df, c->df.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
-    if (indep) FBN_HIP(hipMemcpyAsync(indep, c->indep.p, (size_t)n, hipMemcpyDeviceToHost, s));
+    if (df) FBN_HIP(hipMemcpyAsync(df, c->slot[0].df.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    if (indep) FBN_HIP(hipMemcpyAsync(indep, c->slot[0].indep.p, (size_t)n, hipMemcpyDeviceToHost, s));
     FBN_HIP(hipStreamSynchronize(s));
-    FBN_HIP(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+    FBN_HIP(hipEventElapsedTime(&c->last_ms, c->slot[0].ev0, c->slot[0].ev1));
     return FBN_OK;
 }
 
@@ -1151,48 +1172,65 @@ void CiCtxShape(const fbn_ci_ctx *c, int *nvars, int64_t *nsamples) {
     *nvars = c->nvars;
     *nsamples = c->N;
 }
-// batches up to this many item bytes take the zero-copy path of CiRunBatch
+// batches up to this many item bytes take the zero-copy path of CiBatchLaunch
 constexpr size_t kZeroCopyBytes = 256 << 10;
-int CiRunBatch(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alpha, uint8_t *indep, int32_t *df,
-               PCResultHost &res) {
+const int32_t *CiCtxDims(const fbn_ci_ctx *c) { return c->dims.data(); }
+int CiBatchLaunch(fbn_ci_ctx *c, int k, const int32_t *items, int64_t n, int d, double alpha, bool want_df,
+                  const CiBatchStats *pre) {
+    CiSlot &S = c->slot[k];
+    S.n = n;
+    S.want_df = want_df;
     if (n == 0) return FBN_OK;
     // pinned staging: the copies are true DMA on the ctx stream, one host sync per round
     const size_t ib = (size_t)n * (2 + d) * 4, rb = (size_t)n * 5 + 8;
     int rc;
-    if ((rc = PinnedEnsure(c->h_items, c->h_items_bytes, ib))) return rc;
-    if ((rc = PinnedEnsure(c->h_res, c->h_res_bytes, rb))) return rc;
-    static const bool timing = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic
-    auto t0 = std::chrono::steady_clock::now();
-    memcpy(c->h_items, items, ib);
-    uint8_t *h_ind = static_cast<uint8_t *>(c->h_res);
+    if ((rc = PinnedEnsure(S.h_items, S.h_items_bytes, ib))) return rc;
+    if ((rc = PinnedEnsure(S.h_res, S.h_res_bytes, rb))) return rc;
+    memcpy(S.h_items, items, ib);
+    uint8_t *h_ind = static_cast<uint8_t *>(S.h_res);
     int32_t *h_df = reinterpret_cast<int32_t *>(h_ind + (((size_t)n + 3) & ~(size_t)3));
+    const int32_t *hi = static_cast<const int32_t *>(S.h_items);
     // small rounds (the latency-bound ones): the kernel reads the items from and writes the
     // decisions to the pinned buffers directly (one launch + one sync per round); large rounds
     // stage through device memory with DMA copies
-    const bool zc = ib <= kZeroCopyBytes && !getenv("FBN_CI_NO_ZEROCOPY");
-    if (zc) {
-        rc = CiLaunchDevice(c, static_cast<const int32_t *>(c->h_items), n, d, alpha, false, nullptr, c->stream,
-                            static_cast<const int32_t *>(c->h_items), h_ind, df ? h_df : nullptr);
+    S.zc = ib <= kZeroCopyBytes && !getenv("FBN_CI_NO_ZEROCOPY");
+    if (S.zc) {
+        rc = CiLaunchDevice(c, hi, n, d, alpha, false, nullptr, c->stream, k, hi, h_ind, want_df ? h_df : nullptr, pre);
         if (rc) return rc;
     } else {
-        rc = CiLaunchDevice(c, static_cast<const int32_t *>(c->h_items), n, d, alpha, false, nullptr, c->stream);
+        rc = CiLaunchDevice(c, hi, n, d, alpha, false, nullptr, c->stream, k, nullptr, nullptr, nullptr, pre);
         if (rc) return rc;
-        FBN_HIP(hipMemcpyAsync(h_ind, c->indep.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
-        if (df) FBN_HIP(hipMemcpyAsync(h_df, c->df.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+        FBN_HIP(hipMemcpyAsync(h_ind, S.indep.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+        if (want_df) FBN_HIP(hipMemcpyAsync(h_df, S.df.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
     }
+    FBN_HIP(hipEventRecord(S.done, c->stream));
+    return FBN_OK;
+}
+int CiBatchWait(fbn_ci_ctx *c, int k, uint8_t *indep, int32_t *df, PCResultHost &res) {
+    CiSlot &S = c->slot[k];
+    const int64_t n = S.n;
+    if (n == 0) return FBN_OK;
+    static const bool timing = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic
     auto t1 = std::chrono::steady_clock::now();
-    FBN_HIP(hipStreamSynchronize(c->stream));
+    FBN_HIP(hipEventSynchronize(S.done));
     auto t2 = std::chrono::steady_clock::now();
+    const uint8_t *h_ind = static_cast<const uint8_t *>(S.h_res);
     memcpy(indep, h_ind, (size_t)n);
-    if (df) memcpy(df, h_df, (size_t)n * 4);
+    if (df && S.want_df) memcpy(df, h_ind + (((size_t)n + 3) & ~(size_t)3), (size_t)n * 4);
     if (timing)
-        fprintf(stderr, "  ci batch d=%d n=%lld: enqueue %.1f us, wait %.1f us\n", d, (long long)n,
-                std::chrono::duration<double, std::micro>(t1 - t0).count(),
+        fprintf(stderr, "  ci batch slot %d n=%lld: wait %.1f us\n", k, (long long)n,
                 std::chrono::duration<double, std::micro>(t2 - t1).count());
     float ms = 0.f;
-    FBN_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    FBN_HIP(hipEventElapsedTime(&ms, S.ev0, S.ev1));
     res.kernel_s += ms * 1e-3;
-    res.device_bytes += c->last_bytes;
+    res.device_bytes += S.last_bytes;
+    S.n = 0;
     return FBN_OK;
+}
+int CiRunBatch(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alpha, uint8_t *indep, int32_t *df,
+               PCResultHost &res) {
+    int rc = CiBatchLaunch(c, 0, items, n, d, alpha, df != nullptr);
+    if (rc) return rc;
+    return CiBatchWait(c, 0, indep, df, res);
 }
 }  // namespace fbn

@@ -86,10 +86,19 @@ int64_t FullSpeculation() {
     return v;
 }
 
+int64_t binom(int64_t m, int k) {  // C(m, k), saturating at 2^40
+    if (k < 0 || m < k) return 0;
+    int64_t r = 1;
+    for (int i = 1; i <= k; ++i) {
+        r = r * (m - k + i) / i;
+        if (r > (int64_t)1 << 40) return (int64_t)1 << 40;
+    }
+    return r;
+}
+
 struct Pending {  // one generated test
     int edge;
     int side;
-    int64_t pos;  // position within the side
     int64_t group_end;  // first position after this test's group (within the side)
 };
 
@@ -111,10 +120,11 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
     std::vector<uint8_t> indep;
     std::vector<int32_t> dfv;
     if (d == 0) {
-        items.resize(E * 2);
-        for (size_t e = 0; e < E; ++e) items[2 * e] = edges[e_begin + e].first, items[2 * e + 1] = edges[e_begin + e].second;
+        // the (x, y) pairs of the edge range are the items, in place (pair<int, int> = two ints)
+        static_assert(sizeof(std::pair<int, int>) == 2 * sizeof(int32_t), "pair layout");
+        const int32_t *pairs = reinterpret_cast<const int32_t *>(edges.data() + e_begin);
         indep.resize(E);
-        int rc = CiRunBatch(ctx, items.data(), (int64_t)E, 0, alpha, indep.data(), nullptr, res);
+        int rc = CiRunBatch(ctx, pairs, (int64_t)E, 0, alpha, indep.data(), nullptr, res);
         if (rc) return rc;
         for (size_t e = 0; e < E; ++e) out.removed[e] = indep[e] ? 1 : 0;
         out.counted = out.launched = (int64_t)E;
@@ -137,15 +147,6 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
     // small levels: every candidate set of every edge in one round (one host round trip per level;
     // the extra speculative tests cost less than the round trips they save)
     {
-        auto binom = [](int64_t m, int k) -> int64_t {
-            if (k < 0 || m < k) return 0;
-            int64_t r = 1;
-            for (int i = 1; i <= k; ++i) {
-                r = r * (m - k + i) / i;
-                if (r > (int64_t)1 << 40) return (int64_t)1 << 40;
-            }
-            return r;
-        };
         const int64_t cap = FullSpeculation();
         int64_t all = 0;
         for (auto &s : st) {
@@ -155,24 +156,57 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
         }
         if (all <= cap) chunk = all, full = true;
     }
-    std::vector<Pending> pend;
     static const bool timing = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic
-    while (true) {
-        auto tg0 = std::chrono::steady_clock::now();
-        items.clear();
-        pend.clear();
-        for (size_t e = 0; e < st.size(); ++e) {
+    // Two halves of the edge range, each with its own rounds, alternate on the device: while one
+    // half's batch runs, the host resolves the other's results and generates its next round (the
+    // device stays busy through the host work).  One half when a single round covers the level or
+    // the level is small.
+    struct Half {
+        size_t e0, e1;
+        int64_t chunk;
+        std::vector<int32_t> items;
+        std::vector<Pending> pend;
+        std::vector<uint8_t> indep;
+        std::vector<int32_t> dfv;
+        CiBatchStats stats;
+    };
+    const int nh = (full || open_edges < 2048 || getenv("FBN_PC_NO_PIPELINE")) ? 1 : 2;
+    Half H[2];
+    for (int h = 0; h < nh; ++h) H[h].e0 = E * h / nh, H[h].e1 = E * (h + 1) / nh, H[h].chunk = chunk;
+    if (nh == 2) {  // cut where the candidate-set counts of the open edges reach half
+        std::vector<double> cost(E, 0.0);
+        double tot = 0.0;
+        for (size_t e = 0; e < E; ++e)
+            if (!st[e].resolved)
+                tot += cost[e] = (double)binom((int64_t)adj[st[e].x].size() - 1, d) +
+                                 (double)binom((int64_t)adj[st[e].y].size() - 1, d);
+        double acc = 0.0;
+        size_t cut = 0;
+        while (cut < E && acc + cost[cut] <= tot / 2) acc += cost[cut++];
+        H[0].e1 = H[1].e0 = std::max<size_t>(1, std::min(cut, E - 1));
+    }
+    const int32_t *dims = CiCtxDims(ctx);
+    auto generate = [&](Half &hf) {
+        hf.items.clear();
+        hf.pend.clear();
+        hf.stats = CiBatchStats{0, 0};
+        for (size_t e = hf.e0; e < hf.e1; ++e) {
             EdgeState &s = st[e];
             if (s.resolved) continue;
             // next chunk: whole groups only, never across a side boundary
-            int64_t want = ((chunk + group_size - 1) / group_size) * group_size;
+            int64_t want = ((hf.chunk + group_size - 1) / group_size) * group_size;
             while (want > 0 && s.has_next) {
                 const int64_t gstart = (s.pos_in_side / group_size) * group_size;
-                Pending p{(int)e, s.side, s.pos_in_side, gstart + group_size};
-                pend.push_back(p);
-                items.push_back(s.x);
-                items.push_back(s.y);
-                for (int i = 0; i < d; ++i) items.push_back(s.A(s.ch[i]));
+                hf.pend.push_back(Pending{(int)e, s.side, gstart + group_size});
+                hf.items.push_back(s.x);
+                hf.items.push_back(s.y);
+                int r = dims[s.x] + dims[s.y], mx = std::max(dims[s.x], dims[s.y]);
+                for (int i = 0; i < d; ++i) {
+                    const int z = s.A(s.ch[i]);
+                    hf.items.push_back(z);
+                    r += dims[z], mx = std::max(mx, dims[z]);
+                }
+                hf.stats.dim_rows += r, hf.stats.maxdim = std::max(hf.stats.maxdim, mx);
                 --want;
                 Advance(s, d);
                 if (!s.has_next) {
@@ -189,16 +223,10 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
                 }
             }
         }
-        if (pend.empty()) break;
-        const int64_t nt = (int64_t)pend.size();
-        indep.resize(nt);
-        dfv.resize(nt);
-        auto tg1 = std::chrono::steady_clock::now();
-        int rc = CiRunBatch(ctx, items.data(), nt, d, alpha, indep.data(), dfv.data(), res);
-        if (rc) return rc;
-        auto tg2 = std::chrono::steady_clock::now();
-        out.launched += nt;
-        // resolve in order per edge
+        hf.chunk = std::min<int64_t>(hf.chunk * 4, 1 << 16);
+    };
+    auto resolve = [&](Half &hf) {  // in order per edge
+        const auto &pend = hf.pend;
         size_t i = 0;
         while (i < pend.size()) {
             const int e = pend[i].edge;
@@ -213,13 +241,13 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
                 const int gsz = (int)(g - k);
                 out.counted += gsz;
                 for (size_t t = k; t < g; ++t) {
-                    bool ind = indep[t] != 0;
-                    if (gsz > 1 && dfv[t] == 0) ind = false;  // group quirk (see file header)
+                    bool ind = hf.indep[t] != 0;
+                    if (gsz > 1 && hf.dfv[t] == 0) ind = false;  // group quirk (see file header)
                     if (ind) {
                         s.removed = true;
                         s.resolved = true;
                         int *z = out.sep.data() + (size_t)e * d;
-                        std::copy(items.begin() + (2 + d) * t + 2, items.begin() + (2 + d) * (t + 1), z);
+                        std::copy(hf.items.begin() + (2 + d) * t + 2, hf.items.begin() + (2 + d) * (t + 1), z);
                         std::sort(z, z + d);
                         break;
                     }
@@ -229,12 +257,34 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
             if (!s.removed && !s.has_next) s.resolved = true;  // exhausted: dependent, kept
             i = j;
         }
+    };
+    auto launch = [&](int h) -> int {  // generate + launch half h's next round; 0 tests = done
+        auto t0 = std::chrono::steady_clock::now();
+        generate(H[h]);
+        const int64_t nt = (int64_t)H[h].pend.size();
+        if (nt == 0) return FBN_OK;
+        H[h].indep.resize(nt);
+        H[h].dfv.resize(nt);
+        int rc = CiBatchLaunch(ctx, h, H[h].items.data(), nt, d, alpha, true, &H[h].stats);
+        if (rc) return rc;
+        out.launched += nt;
         if (timing)
-            fprintf(stderr, "   round d=%d: %lld tests, generate %.2f ms, batch %.2f ms, resolve %.2f ms\n", d,
-                    (long long)nt, std::chrono::duration<double, std::milli>(tg1 - tg0).count(),
-                    std::chrono::duration<double, std::milli>(tg2 - tg1).count(),
-                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tg2).count());
-        chunk = std::min<int64_t>(chunk * 4, 1 << 16);
+            fprintf(stderr, "   half %d d=%d: %lld tests, generate + launch %.2f ms\n", h, d, (long long)nt,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        return FBN_OK;
+    };
+    for (int h = 0; h < nh; ++h)
+        if (int rc = launch(h)) return rc;
+    while (true) {
+        bool any = false;
+        for (int h = 0; h < nh; ++h) {
+            if (H[h].pend.empty()) continue;
+            any = true;
+            if (int rc = CiBatchWait(ctx, h, H[h].indep.data(), H[h].dfv.data(), res)) return rc;
+            resolve(H[h]);
+            if (int rc = launch(h)) return rc;
+        }
+        if (!any) break;
     }
     for (size_t e = 0; e < E; ++e)
         if (st[e].removed) out.removed[e] = 1;
@@ -284,9 +334,8 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
         int rc = RunLevel(ctx, alpha, d, group_size, adj, edges, 0, edges.size(), out, res);
         if (rc) return rc;
         auto tb = std::chrono::steady_clock::now();
-        res.sepset.reserve(res.sepset.size() + edges.size());
-        for (size_t e = 0; e < edges.size(); ++e)
-            if (out.removed[e]) res.sepset.set(edges[e], out.sep.data() + e * (size_t)d, d);
+        if (d == 0) res.sepset.set_level0(n, out.removed.data());  // edges = the complete graph
+        else res.sepset.append_level(edges.data(), out.removed.data(), out.sep.data(), edges.size(), d);
         res.tests_per_level.push_back(out.counted);
         res.launched_per_level.push_back(out.launched);
         auto tc = std::chrono::steady_clock::now();

@@ -27,60 +27,92 @@ class SepsetMap {
         size_t size() const { return (size_t)n; }
     };
     void set(std::pair<int, int> key, const int *z, int n) {
-        sorted_ = sorted_ && (keys_.empty() || keys_.back() < key);
-        keys_.push_back(key);
-        off_.push_back((int64_t)pool_.size());
-        len_.push_back(n);
+        sorted_ = sorted_ && (e_.empty() || e_.back().key < key);
+        e_.push_back(Ent{key, (int64_t)pool_.size(), n});
         pool_.insert(pool_.end(), z, z + n);
     }
     void set(std::pair<int, int> key, const std::vector<int> &z) { set(key, z.data(), (int)z.size()); }
+    // one level's removals in one go: keys[i] for every i with removed[i], sepset sep[i*d .. +d)
+    void append_level(const std::pair<int, int> *keys, const char *removed, const int *sep, size_t n, int d) {
+        size_t cnt = 0;
+        for (size_t i = 0; i < n; ++i) cnt += removed[i] != 0;
+        size_t o = e_.size();
+        e_.resize(o + cnt);
+        const int64_t p0 = (int64_t)pool_.size();
+        pool_.resize(pool_.size() + cnt * (size_t)d);
+        int64_t q = p0;
+        for (size_t i = 0; i < n; ++i) {
+            if (!removed[i]) continue;
+            sorted_ = sorted_ && (o == 0 || e_[o - 1].key < keys[i]);
+            e_[o++] = Ent{keys[i], q, d};
+            for (int j = 0; j < d; ++j) pool_[(size_t)q + j] = sep[i * (size_t)d + j];
+            q += d;
+        }
+    }
+    // level 0 of a run over n variables: removed[k] for the k-th pair (i < j) of the complete graph
+    // in lexicographic order, all with empty sepsets (a flag per pair instead of ~500k entries)
+    void set_level0(int n, const char *removed) {
+        n0_ = n;
+        l0_.assign(removed, removed + (size_t)n * (n - 1) / 2);
+    }
     bool find(std::pair<int, int> key, View *v) const {
         sort();
-        auto it = std::lower_bound(keys_.begin(), keys_.end(), key);
-        if (it == keys_.end() || *it != key) return false;
-        const size_t i = (size_t)(it - keys_.begin());
-        *v = View{pool_.data() + off_[i], len_[i]};
-        return true;
+        auto it = std::lower_bound(e_.begin(), e_.end(), key, [](const Ent &a, const std::pair<int, int> &k) {
+            return a.key < k;
+        });
+        if (it != e_.end() && it->key == key) {
+            *v = View{pool_.data() + it->off, it->len};
+            return true;
+        }
+        const int i = key.first, j = key.second;
+        if (!l0_.empty() && 0 <= i && i < j && j < n0_ &&
+            l0_[(size_t)i * n0_ - (size_t)i * (i + 1) / 2 + (size_t)(j - i - 1)]) {
+            *v = View{pool_.data(), 0};
+            return true;
+        }
+        return false;
     }
-    size_t size() const { return keys_.size(); }  // entries appended (no sort)
-    // iteration in ascending key order: n = sorted_size(), then key(i) / value(i) for i < n
+    // iteration in ascending key order: n = sorted_size(), then key(i) / value(i) for i < n (folds
+    // the level-0 flags into explicit entries first)
     size_t sorted_size() const {
+        if (!l0_.empty()) {
+            size_t k = 0;
+            for (int i = 0; i < n0_; ++i)
+                for (int j = i + 1; j < n0_; ++j, ++k)
+                    if (l0_[k]) {
+                        sorted_ = sorted_ && (e_.empty() || e_.back().key < std::make_pair(i, j));
+                        e_.push_back(Ent{{i, j}, 0, 0});
+                    }
+            l0_.clear();
+        }
         sort();
-        return keys_.size();
+        return e_.size();
     }
-    std::pair<int, int> key(size_t i) const { return keys_[i]; }
-    View value(size_t i) const { return View{pool_.data() + off_[i], len_[i]}; }
-    void reserve(size_t n) {
-        keys_.reserve(n);
-        off_.reserve(n);
-        len_.reserve(n);
-    }
+    std::pair<int, int> key(size_t i) const { return e_[i].key; }
+    View value(size_t i) const { return View{pool_.data() + e_[i].off, e_[i].len}; }
 
   private:
+    struct Ent {
+        std::pair<int, int> key;
+        int64_t off;
+        int len;
+    };
     void sort() const {
         if (sorted_) return;
         // a key set twice keeps its last value (std::map assignment semantics)
-        std::vector<int64_t> idx(keys_.size());
-        for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int64_t)i;
-        std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return keys_[a] < keys_[b]; });
-        std::vector<std::pair<int, int>> k;
-        std::vector<int64_t> o;
-        std::vector<int> l;
-        k.reserve(idx.size()), o.reserve(idx.size()), l.reserve(idx.size());
-        for (int64_t i : idx) {
-            if (!k.empty() && k.back() == keys_[i]) {
-                o.back() = off_[i], l.back() = len_[i];
-            } else {
-                k.push_back(keys_[i]), o.push_back(off_[i]), l.push_back(len_[i]);
-            }
+        std::stable_sort(e_.begin(), e_.end(), [](const Ent &a, const Ent &b) { return a.key < b.key; });
+        size_t o = 0;
+        for (size_t i = 0; i < e_.size(); ++i) {
+            if (o > 0 && e_[o - 1].key == e_[i].key) e_[o - 1] = e_[i];
+            else e_[o++] = e_[i];
         }
-        keys_.swap(k), off_.swap(o), len_.swap(l);
+        e_.resize(o);
         sorted_ = true;
     }
-    mutable std::vector<std::pair<int, int>> keys_;
-    mutable std::vector<int64_t> off_;
-    mutable std::vector<int> len_;
+    mutable std::vector<Ent> e_;
     std::vector<int> pool_;
+    mutable std::vector<char> l0_;
+    int n0_ = 0;
     mutable bool sorted_ = true;
 };
 
@@ -104,6 +136,18 @@ void CiCtxShape(const fbn_ci_ctx *c, int *nvars, int64_t *nsamples);
 // accumulates kernel time into res.kernel_s
 int CiRunBatch(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alpha, uint8_t *indep, int32_t *df,
                PCResultHost &res);
+// the same as two halves: launch a batch into slot k (0 or 1) on the ctx stream, wait for it later
+// (each slot holds one batch in flight; a slot's batch must be waited for before its next launch)
+// pre: the batch's largest state count and sum of state counts over all item variables, when the
+// caller generated the items from valid variables (skips the validation pass); nullptr: validate
+struct CiBatchStats {
+    int maxdim;
+    int64_t dim_rows;
+};
+int CiBatchLaunch(fbn_ci_ctx *c, int k, const int32_t *items, int64_t n, int d, double alpha, bool want_df,
+                  const CiBatchStats *pre = nullptr);
+const int32_t *CiCtxDims(const fbn_ci_ctx *c);  // state count per variable
+int CiBatchWait(fbn_ci_ctx *c, int k, uint8_t *indep, int32_t *df, PCResultHost &res);
 int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResultHost &res);
 // one level for an edge range (the unit a multi-GPU driver partitions), see pc_driver.cpp
 struct LevelOut {
