@@ -194,7 +194,24 @@ def bench_munin(steps, warmup, cases=125_000):
             "cliques": jt.info["num_cliques"], "clique_entries": jt.info["clique_entries"],
             "roofline": {"bound": "hbm", "achieved": bpc * cases / (k * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": bpc * cases / (k * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "algorithmic_bytes_per_case": bpc}}
+                         "algorithmic_bytes_per_case": bpc, **munin_traffic(cases, k)}}
+
+
+def munin_traffic(cases, kernel_ms):
+    """Measured L2<->fabric bytes of the streamed kernel (rocprofv3 FETCH_SIZE + WRITE_SIZE, calibrated;
+    committed summary profiles/munin_traffic.json from tools/profile_round.sh), scaled to this launch,
+    and the rate they imply at this launch's kernel time."""
+    path = os.path.join(REPO, "profiles", "munin_traffic.json")
+    if not os.path.exists(path):
+        return {"traffic": None}
+    with open(path) as f:
+        t = json.load(f)
+    b = t["hbm_bytes_per_launch"] * cases / t["cases_per_launch"]
+    return {"traffic": b, "traffic_rate_GBs": b / (kernel_ms * 1e-3) / 1e9,
+            "traffic_frac": b / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "traffic_note": "the streamed kernel recomputes clique tables from separator messages instead of "
+                            "storing them; its measured traffic (message re-reads + per-wave scratch tables) "
+                            "exceeds the materialized-table bytes and is what bounds it (DESIGN.md 5.2)"}
 
 
 def load_traffic(cases):
