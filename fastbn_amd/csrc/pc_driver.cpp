@@ -79,12 +79,15 @@ void Advance(EdgeState &e, int d) {  // ChoiceGenerator::Next (src/ChoiceGenerat
     ++e.pos_in_side;
 }
 
-// levels whose candidate sets number at most this many run in a single round (FBN_PC_FULLSPEC:
-// diagnostic override)
-int64_t FullSpeculation() {
-    static const int64_t v = getenv("FBN_PC_FULLSPEC") ? atoll(getenv("FBN_PC_FULLSPEC")) : 4096;
-    return v;
+// levels whose candidate sets number at most this many run in a single round; levels with fewer
+// open edges than kPipelineEdges run as one half (FBN_PC_FULLSPEC / FBN_PC_PIPELINE_EDGES: test and
+// diagnostic overrides, read per level)
+int64_t EnvOr(const char *name, int64_t dflt) {
+    const char *v = getenv(name);
+    return v ? atoll(v) : dflt;
 }
+int64_t FullSpeculation() { return EnvOr("FBN_PC_FULLSPEC", 4096); }
+constexpr int64_t kPipelineEdges = 2048;
 
 int64_t binom(int64_t m, int k) {  // C(m, k), saturating at 2^40
     if (k < 0 || m < k) return 0;
@@ -170,7 +173,7 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
         std::vector<int32_t> dfv;
         CiBatchStats stats;
     };
-    const int nh = (full || open_edges < 2048 || getenv("FBN_PC_NO_PIPELINE")) ? 1 : 2;
+    const int nh = (full || open_edges < EnvOr("FBN_PC_PIPELINE_EDGES", kPipelineEdges)) ? 1 : 2;
     Half H[2];
     for (int h = 0; h < nh; ++h) H[h].e0 = E * h / nh, H[h].e1 = E * (h + 1) / nh, H[h].chunk = chunk;
     if (nh == 2) {  // cut where the candidate-set counts of the open edges reach half
