@@ -44,6 +44,7 @@ _SIGS = {
     "fbn_jt_debug_force_fixup": [_vp, C.c_int],
     "fbn_jt_plan_destroy": [_vp],
     "fbn_ci_dataset_upload": [_vp, C.c_int, _i64, _vp, C.c_int, _pp],
+    "fbn_ci_dataset_from_device": [_vp, C.c_int, _i64, _vp, C.c_int, _pp],
     "fbn_ci_run": [_vp, _vp, _i64, C.c_int, _dbl, _vp, _vp, _vp, _vp, _vp],
     "fbn_ci_counts": [_vp, C.c_int, C.c_int, _vp, C.c_int, _vp, _i64, _vp],
     "fbn_ci_last_kernel_ms": [_vp, _vp],
@@ -332,6 +333,19 @@ class IndependenceTest:
         lib.fbn_ci_dataset_upload(_p(dataset.columns), dataset.num_vars, dataset.num_instance,
                                   _p(dataset.dims), device, C.byref(h))
         self._h = h
+
+    @classmethod
+    def from_device(cls, d_cols_ptr, nvars, nsamples, dims, alpha=0.05, device=0):
+        """Column store already in `device` memory (uint8 [nvars][nsamples], e.g. a tensor filled by
+        an RCCL broadcast): fbn_ci_dataset_from_device."""
+        self = cls.__new__(cls)
+        self.alpha = alpha
+        dims = np.ascontiguousarray(dims, np.int32)
+        h = C.c_void_p()
+        lib.fbn_ci_dataset_from_device(C.c_void_p(d_cols_ptr), int(nvars), int(nsamples), _p(dims), device,
+                                       C.byref(h))
+        self._h = h
+        return self
 
     def level(self, d, edges, e_begin, e_end, group_size=1):
         """One skeleton level for edges[e_begin:e_end] of the current skeleton (fbn_pc_level) ->

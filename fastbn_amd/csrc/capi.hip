@@ -22,6 +22,8 @@ extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, co
                                     uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
                                     int32_t *gscratch, unsigned long long *stats, hipStream_t stream);
 extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy);
+extern "C" hipError_t fbn_ci_cols_check(const uint8_t *cols, const int32_t *dims, int nvars, long long N, int *bad,
+                                        hipStream_t s);
 extern "C" hipError_t fbn_ci_bits_build(const uint8_t *cols, const int32_t *dims, const int32_t *row0, long long N,
                                         long long W, int nvars, uint32_t *bits, hipStream_t s);
 extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *dims, const int32_t *row0,
@@ -799,8 +801,11 @@ int fbn_jt_plan_destroy(fbn_jt_plan *p) {
 }
 
 // ------------------------------------------------------------------ CI tests
-int fbn_ci_dataset_upload(const uint8_t *cols, int nvars, int64_t nsamples, const int32_t *dims, int device,
-                          fbn_ci_ctx **out) {
+// the column store from host memory (cols_on_device = false) or from a device buffer of the same
+// device, e.g. one filled by an RCCL broadcast (true); every code is checked < dims[v] on the
+// device before any kernel bins with it
+static int CiCreate(const uint8_t *cols, bool cols_on_device, int nvars, int64_t nsamples, const int32_t *dims,
+                    int device, fbn_ci_ctx **out) {
     if (!cols || !dims || !out || nvars <= 0 || nsamples <= 0) return SetError(FBN_ERR_ARG, "bad argument");
     for (int v = 0; v < nvars; ++v)
         if (dims[v] < 1 || dims[v] > 256) return SetError(FBN_ERR_ARG, "dims[%d] = %d out of 1..256", v, dims[v]);
@@ -808,24 +813,45 @@ int fbn_ci_dataset_upload(const uint8_t *cols, int nvars, int64_t nsamples, cons
     if (!c) return SetError(FBN_ERR_NOMEM, "out of memory");
     int rc = CheckDevice(device, &c->num_cu);
     if (rc) return rc;
+    FBN_HIP(hipSetDevice(device));
     c->device = device;
     c->nvars = nvars;
     c->N = nsamples;
     c->dims.assign(dims, dims + nvars);
     if ((rc = c->cols.ensure((size_t)nvars * nsamples))) return rc;
     if ((rc = c->ddims.ensure((size_t)nvars * 4))) return rc;
-    FBN_HIP(hipMemcpy(c->cols.p, cols, (size_t)nvars * nsamples, hipMemcpyHostToDevice));
+    if ((rc = c->stats.ensure(16))) return rc;
+    FBN_HIP(hipMemcpy(c->cols.p, cols, (size_t)nvars * nsamples,
+                      cols_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
     FBN_HIP(hipMemcpy(c->ddims.p, dims, (size_t)nvars * 4, hipMemcpyHostToDevice));
+    {
+        FBN_HIP(hipMemset(c->stats.p, 0, 16));
+        hipError_t e = fbn_ci_cols_check(c->cols.as<uint8_t>(), c->ddims.as<int32_t>(), nvars, nsamples,
+                                         c->stats.as<int>(), nullptr);
+        if (e != hipSuccess) return SetError(FBN_ERR_HIP, "column check: %s", hipGetErrorString(e));
+        int bad[2] = {0, 0};
+        FBN_HIP(hipMemcpy(bad, c->stats.p, 8, hipMemcpyDeviceToHost));
+        if (bad[0])
+            return SetError(FBN_ERR_ARG, "column store: variable %d holds a code >= its state count %d", bad[1] - 1,
+                            dims[bad[1] - 1]);
+    }
     for (auto &sl : c->slot) {
         FBN_HIP(hipEventCreate(&sl.ev0));
         FBN_HIP(hipEventCreate(&sl.ev1));
         FBN_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
     }
     FBN_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    if ((rc = c->stats.ensure(16))) return rc;
     if ((rc = CiResetMargin(c.get()))) return rc;
     *out = c.release();
     return FBN_OK;
+}
+int fbn_ci_dataset_upload(const uint8_t *cols, int nvars, int64_t nsamples, const int32_t *dims, int device,
+                          fbn_ci_ctx **out) {
+    return CiCreate(cols, false, nvars, nsamples, dims, device, out);
+}
+int fbn_ci_dataset_from_device(const uint8_t *d_cols, int nvars, int64_t nsamples, const int32_t *dims, int device,
+                               fbn_ci_ctx **out) {
+    return CiCreate(d_cols, true, nvars, nsamples, dims, device, out);
 }
 
 // items: host copy (validated here).  zc_items / zc_indep / zc_df: optional device-visible

@@ -235,6 +235,30 @@ __global__ __launch_bounds__(256) void ci_bits_g2(const int32_t *__restrict__ co
 
 }  // namespace
 
+// bad[0] = 1 and bad[1] = v + 1 (some such v) if any code of variable v is >= dims[v]
+static __global__ __launch_bounds__(256) void ci_cols_check(const uint8_t *__restrict__ cols, const int32_t *__restrict__ dims,
+                                                     int nvars, long long N, int *__restrict__ bad) {
+    for (int v = blockIdx.y; v < nvars; v += gridDim.y) {
+        const uint8_t *c = cols + (size_t)v * N;
+        const int d = dims[v];
+        bool b = false;
+        for (long long k = (long long)blockIdx.x * 256 + threadIdx.x; k < N; k += (long long)gridDim.x * 256)
+            b |= c[k] >= d;
+        if (b) {
+            bad[0] = 1;
+            bad[1] = v + 1;
+        }
+    }
+}
+
+extern "C" hipError_t fbn_ci_cols_check(const uint8_t *cols, const int32_t *dims, int nvars, long long N, int *bad,
+                                        hipStream_t s) {
+    const long long bx = (N + 255) / 256;
+    const dim3 grid((unsigned)(bx < 16 ? bx : 16), (unsigned)(nvars < 4096 ? nvars : 4096));
+    hipLaunchKernelGGL(ci_cols_check, grid, dim3(256), 0, s, cols, dims, nvars, N, bad);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t fbn_ci_bits_build(const uint8_t *cols, const int32_t *dims, const int32_t *row0, long long N,
                                         long long W, int nvars, uint32_t *bits, hipStream_t s) {
     const long long total = (long long)nvars * W;

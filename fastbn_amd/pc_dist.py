@@ -81,6 +81,32 @@ def pc_skeleton_distributed(level_fn, nvars, depth=1000, device=None):
     return edges, sepset, tests, launched
 
 
+def broadcast_columns(cols, shape, device=None, src=0):
+    """The read-only column store from rank `src` to every rank in one broadcast:
+    `cols` = uint8 [nvars][nsamples] numpy array on `src` (ignored elsewhere), `shape` = (nvars,
+    nsamples) on every rank.  Returns a uint8 torch tensor on `device` (CPU for gloo) holding the
+    columns on every rank; with nccl (RCCL) it stays on the GPU for IndependenceTest.from_device."""
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cpu") if device is None else torch.device(device)
+    if dist.get_rank() == src:
+        t = torch.from_numpy(np.ascontiguousarray(cols, np.uint8)).to(dev)
+    else:
+        t = torch.empty(tuple(shape), dtype=torch.uint8, device=dev)
+    dist.broadcast(t, src)
+    return t
+
+
+def independence_test_broadcast(cols, dims, shape, alpha=0.05, device=0, src=0):
+    """Every rank's IndependenceTest over the column store loaded on rank `src`, moved by one RCCL
+    broadcast straight into device memory (no host copy on the receiving ranks)."""
+    import torch
+    from . import api
+    t = broadcast_columns(cols, shape, torch.device("cuda", device), src)
+    torch.cuda.synchronize(device)
+    return api.IndependenceTest.from_device(t.data_ptr(), shape[0], shape[1], dims, alpha, device)
+
+
 def pc_stable_distributed(ci, nvars, alpha=0.05, depth=1000, group_size=1, device=None):
     """Device skeleton on every rank's IndependenceTest `ci`, then host orientation."""
     from . import api

@@ -148,6 +148,12 @@ typedef struct fbn_ci_ctx fbn_ci_ctx;
 /* Upload the column store (uint8 [nvars][nsamples], codes < dims[v] <= 255) to `device`. */
 int fbn_ci_dataset_upload(const uint8_t *cols, int nvars, int64_t nsamples, const int32_t *dims,
                           int device, fbn_ci_ctx **out);
+/* The same from a column store already in `device`'s memory (uint8 [nvars][nsamples]), e.g. filled
+ * by one RCCL broadcast from the rank that loaded the file; copied into the handle.
+ * Replaces every rank's own Dataset::LoadCSVData (src/Dataset.cpp:267-414) in a multi-GPU run.
+ * Both entry points reject a code >= dims[v] (FBN_ERR_ARG). */
+int fbn_ci_dataset_from_device(const uint8_t *d_cols, int nvars, int64_t nsamples, const int32_t *dims,
+                               int device, fbn_ci_ctx **out);
 /* n tests of one conditioning size d: items [n][2+d] = (x, y, z_0..z_{d-1}).  Outputs per test
  * (any may be NULL): G^2, adjusted df, p = 1 - pchisq(G^2, df), indep = (df == 0 || p > alpha).
  * ComputeGSquareXY / ComputeGSquareXYZ semantics (src/IndependenceTest.cpp:65-155,295-364).

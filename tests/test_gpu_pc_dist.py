@@ -37,8 +37,18 @@ def _worker(rank, world, port, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
     from fastbn_amd import pc_dist
-    ci = F.IndependenceTest(F.Dataset(CSV), device=0)
+    # rank 0 loads the file; every rank gets the column store by one broadcast (gloo carries it on
+    # the CPU here; with RCCL it lands in device memory directly: independence_test_broadcast)
+    ds = F.Dataset(CSV) if rank == 0 else None
+    shape = [ds.num_vars, ds.num_instance] if rank == 0 else [0, 0]
+    dims = ds.dims if rank == 0 else None
+    meta = [shape, None if dims is None else [int(v) for v in dims]]
+    dist.broadcast_object_list(meta, 0)
+    t = pc_dist.broadcast_columns(ds.columns if rank == 0 else None, meta[0]).to("cuda:0")
+    torch.cuda.synchronize()
+    ci = F.IndependenceTest.from_device(t.data_ptr(), meta[0][0], meta[0][1], meta[1], device=0)
     res, tests, _ = pc_dist.pc_stable_distributed(ci, 37)
     if rank == 0:
         np.save(out, np.array([res.edges, sorted(res.sepset.items()), tests, res.oriented, res.GetSHD(BIF)],
@@ -57,3 +67,20 @@ def test_two_ranks_match_single_gpu(tmp_path):
     assert dict(sep) == pc.sepset
     assert list(tests) == pc.tests_per_level.tolist()
     assert [tuple(o) for o in oriented] == pc.oriented and shd == 5
+
+
+def test_from_device_matches_upload_and_rejects_bad_codes():
+    import torch
+    ds = F.Dataset(CSV)
+    t = torch.from_numpy(np.ascontiguousarray(ds.columns)).cuda()
+    ci_dev = F.IndependenceTest.from_device(t.data_ptr(), ds.num_vars, ds.num_instance, ds.dims)
+    a = F.PCStable(0.05, 1000).StructLearnCompData(ci_dev)
+    b = F.PCStable(0.05, 1000).StructLearnCompData(F.IndependenceTest(ds))
+    assert a.edges == b.edges and a.sepset == b.sepset and a.tests_per_level.tolist() == b.tests_per_level.tolist()
+    bad = ds.columns.copy()
+    bad[3, 17] = ds.dims[3]  # a code outside the variable's state count
+    tb = torch.from_numpy(np.ascontiguousarray(bad)).cuda()
+    with pytest.raises(F.FastBNError, match="variable 3"):
+        F.IndependenceTest.from_device(tb.data_ptr(), ds.num_vars, ds.num_instance, ds.dims)
+    with pytest.raises(F.FastBNError, match="variable 3"):
+        F.IndependenceTest(F.Dataset(columns=bad, dims=ds.dims))

@@ -143,3 +143,26 @@ def test_two_rank_gloo_pc_skeleton_matches_oracle(tmp_path):
     assert [tuple(e) for e in edges] == [tuple(e) for e in ref["edges"]]
     assert dict(sep) == {k: tuple(v) for k, v in ref["sepset"].items()}
     assert list(tests) == list(ref["tests_per_level"])
+
+
+def _bcast_worker(rank, world, port, out_path):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fastbn_amd import pc_dist
+    cols = np.random.default_rng(7).integers(0, 4, (37, 5000)).astype(np.uint8) if rank == 0 else None
+    t = pc_dist.broadcast_columns(cols, (37, 5000))
+    np.save(f"{out_path}.{rank}.npy", t.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_column_broadcast(tmp_path):
+    """The column store loaded on rank 0 reaches every rank by one broadcast."""
+    mp = pytest.importorskip("torch.multiprocessing")
+    out = str(tmp_path / "cols")
+    mp.start_processes(_bcast_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    ref = np.random.default_rng(7).integers(0, 4, (37, 5000)).astype(np.uint8)
+    for r in range(2):
+        np.testing.assert_array_equal(np.load(f"{out}.{r}.npy"), ref)
