@@ -194,7 +194,8 @@ def bench_munin(steps, warmup, cases=125_000):
             "cliques": jt.info["num_cliques"], "clique_entries": jt.info["clique_entries"],
             "roofline": {"bound": "hbm", "achieved": bpc * cases / (k * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": bpc * cases / (k * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "algorithmic_bytes_per_case": bpc, **munin_traffic(cases, k)}}
+                         "algorithmic_bytes_per_case": bpc, **munin_traffic(cases, k),
+                         "valu": valu_roofline("munin", cases, k)}}
 
 
 def munin_traffic(cases, kernel_ms):
@@ -212,6 +213,24 @@ def munin_traffic(cases, kernel_ms):
             "traffic_note": "the streamed kernel recomputes clique tables from separator messages instead of "
                             "storing them; its measured traffic (message re-reads + per-wave scratch tables) "
                             "exceeds the materialized-table bytes and is what bounds it (DESIGN.md 5.2)"}
+
+
+VALU_PEAK_LANE_OPS = 256 * 4 * 16 * 2.4e9  # MI355X: CUs x SIMDs x lanes x clock (fp64 FMA full rate)
+
+
+def valu_roofline(which, cases, kernel_ms):
+    """Second roofline of a JT kernel: measured VALU instructions per launch (rocprofv3
+    SQ_INSTS_VALU, committed summary profiles/jt_valu.json from tools/pmc_valu.sh) scaled to this
+    launch, as wave64 lane-ops per second against the fp64 vector peak."""
+    path = os.path.join(REPO, "profiles", "jt_valu.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        t = json.load(f)[which]
+    insts = t["valu_insts_per_launch"] * cases / t["cases_per_launch"]
+    ach = insts * 64 / (kernel_ms * 1e-3)
+    return {"bound": "valu", "achieved": ach / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12, "unit": "Tlane-op/s",
+            "frac": ach / VALU_PEAK_LANE_OPS, "valu_insts": insts}
 
 
 def load_traffic(cases):
@@ -333,6 +352,7 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel_ms": kernel_ms, "algorithmic_bytes_per_case": bpc,
                      "kernel_variant": jt.refresh_info()["variant"],
+                     "valu": valu_roofline("alarm", args.cases, kernel_ms),
                      "note": "achieved = materialized-table algorithmic bytes (SURVEY 8(d)) / kernel time; the "
                              "specialized kernel keeps tables in registers/LDS and recomputes instead of "
                              "parking them, so measured traffic is below the algorithmic bytes and the "
