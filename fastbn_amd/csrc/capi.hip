@@ -22,6 +22,8 @@ extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, co
                                     uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
                                     int32_t *gscratch, unsigned long long *stats, hipStream_t stream);
 extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy);
+extern "C" hipError_t fbn_jt_evidence_check(const int8_t *ev, long long n, int V, const int32_t *dom,
+                                            unsigned long long *first, hipStream_t s);
 extern "C" hipError_t fbn_ci_cols_check(const uint8_t *cols, const int32_t *dims, int nvars, long long N, int *bad,
                                         hipStream_t s);
 extern "C" hipError_t fbn_ci_bits_build(const uint8_t *cols, const int32_t *dims, const int32_t *row0, long long N,
@@ -129,6 +131,7 @@ struct fbn_jt_plan {
     bool prof_on = false;
     int last_grid = 0;
     DevBuf evid, labels, marg, ws;
+    DevBuf ddom, evcheck;  // fbn_jt_run's device-side evidence range check
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     ~fbn_jt_plan() {
@@ -727,13 +730,6 @@ int fbn_jt_run(fbn_jt_plan *p, const int8_t *evidence, int64_t ncases, int32_t *
     if (ncases == 0) return FBN_OK;
     if (p->device < 0) return SetError(FBN_ERR_NODEV, "host-only plan (created with device < 0)");
     const int V = p->host.num_nodes, SD = p->prog.sum_dom;
-    for (int64_t c = 0; c < ncases; ++c)  // out-of-domain evidence has no reference meaning
-        for (int v = 0; v < V; ++v) {
-            int x = evidence[c * V + v];
-            if (x < -1 || x >= p->host.dom[v])
-                return SetError(FBN_ERR_ARG, "case %lld: evidence %d for node %d (domain %d)", (long long)c, x, v,
-                                p->host.dom[v]);
-        }
     FBN_HIP(hipSetDevice(p->device));
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
     int rc;
@@ -741,6 +737,28 @@ int fbn_jt_run(fbn_jt_plan *p, const int8_t *evidence, int64_t ncases, int32_t *
     if ((rc = p->labels.ensure((size_t)ncases * 4))) return rc;
     if ((rc = p->marg.ensure((size_t)ncases * SD * 8))) return rc;
     FBN_HIP(hipMemcpyAsync(p->evid.p, evidence, (size_t)ncases * V, hipMemcpyHostToDevice, s));
+    // out-of-domain evidence has no reference meaning: checked on the device (the host loop cost
+    // ~1 ns per value) before any kernel indexes with it
+    if (!p->ddom.p) {
+        if ((rc = p->ddom.ensure((size_t)V * 4))) return rc;
+        if ((rc = p->evcheck.ensure(8))) return rc;
+        FBN_HIP(hipMemcpy(p->ddom.p, p->host.dom.data(), (size_t)V * 4, hipMemcpyHostToDevice));
+    }
+    {
+        FBN_HIP(hipMemsetAsync(p->evcheck.p, 0xFF, 8, s));
+        hipError_t e = fbn_jt_evidence_check(p->evid.as<int8_t>(), (long long)ncases * V, V, p->ddom.as<int32_t>(),
+                                             p->evcheck.as<unsigned long long>(), s);
+        if (e != hipSuccess) return SetError(FBN_ERR_HIP, "evidence check: %s", hipGetErrorString(e));
+        unsigned long long first = 0;
+        FBN_HIP(hipMemcpyAsync(&first, p->evcheck.p, 8, hipMemcpyDeviceToHost, s));
+        FBN_HIP(hipStreamSynchronize(s));
+        if (first != ~0ull) {
+            const long long c = (long long)(first / V);
+            const int v = (int)(first % V);
+            return SetError(FBN_ERR_ARG, "case %lld: evidence %d for node %d (domain %d)", c, (int)evidence[first], v,
+                            p->host.dom[v]);
+        }
+    }
     rc = fbn_jt_run_device(p, p->evid.as<int8_t>(), ncases, p->labels.as<int32_t>(), p->marg.as<double>(), s);
     if (rc) return rc;
     FBN_HIP(hipMemcpyAsync(labels_out, p->labels.p, (size_t)ncases * 4, hipMemcpyDeviceToHost, s));

@@ -655,3 +655,23 @@ extern "C" hipError_t fbn_jt_launch(const JtOp *ops, int nops, const int32_t *au
     hipLaunchKernelGGL(jt_interp_kernel, dim3(grid), dim3(64), 0, stream, a);
     return hipGetLastError();
 }
+
+// evidence range check of a host-supplied batch, on the device: *first = smallest flat index
+// [case * V + v] whose value is outside -1 .. dom[v] - 1 (left at INT64_MAX when all are valid)
+static __global__ __launch_bounds__(256) void jt_evidence_check(const int8_t *__restrict__ ev, long long n, int V,
+                                                                const int32_t *__restrict__ dom,
+                                                                unsigned long long *__restrict__ first) {
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+        const int x = ev[i];
+        const int v = (int)(i % V);
+        if (x < -1 || x >= dom[v]) atomicMin(first, (unsigned long long)i);
+    }
+}
+
+extern "C" hipError_t fbn_jt_evidence_check(const int8_t *ev, long long n, int V, const int32_t *dom,
+                                            unsigned long long *first, hipStream_t s) {
+    const long long b = (n + 255) / 256;
+    hipLaunchKernelGGL(jt_evidence_check, dim3((unsigned)(b < 4096 ? (b > 0 ? b : 1) : 4096)), dim3(256), 0, s, ev, n,
+                       V, dom, first);
+    return hipGetLastError();
+}

@@ -191,5 +191,14 @@ def test_device_resident_path(jt, ojt):
 def test_bad_evidence_rejected(jt):
     ev = np.full((2, 37), -1, np.int8)
     ev[1, 5] = 9
-    with pytest.raises(F.FastBNError, match="domain"):
+    with pytest.raises(F.FastBNError, match="case 1: evidence 9 for node 5"):
         jt.infer(ev)
+    ev = np.full((300, 37), -1, np.int8)
+    ev[250, 36] = -2
+    ev[299, 0] = 7
+    with pytest.raises(F.FastBNError, match="case 250: evidence -2 for node 36"):  # the first one
+        jt.infer(ev)
+    ev[250, 36] = -1
+    ev[299, 0] = -1
+    lab, _ = jt.infer(ev)  # the plan stays usable after a rejected batch
+    assert lab.shape == (300,)
