@@ -96,7 +96,14 @@ def bench_pc(steps, warmup):
     return {"metric": "PC-stable CI-tests/sec (alarm_s5000, levels 0-4)", "value": pc.num_ci_test / (ms * 1e-3),
             "unit": "CI-tests/s", "tests": pc.num_ci_test, "tests_per_level": pc.tests_per_level.tolist(),
             "launched_per_level": pc.launched_per_level.tolist(), "ms_per_run": ms,
-            "kernel_ms_per_run": 1e3 * pc.kernel_s, "edges": len(pc.edges)}
+            "kernel_ms_per_run": 1e3 * pc.kernel_s, "edges": len(pc.edges),
+            "roofline": {"bound": "hbm", "achieved": pc.device_bytes / pc.kernel_s / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": pc.device_bytes / pc.kernel_s / 1e9 / HBM_PEAK_GBS,
+                         "algorithmic_bytes": pc.device_bytes,
+                         "note": "N*(d+2) uint8 column bytes per launched test (SURVEY 8(d)) over the CI kernels' "
+                                 "time; the 185 KB column store is cache resident and each level is a few-"
+                                 "microsecond-per-test latency chain (5 dependent launches), so this is far "
+                                 "from any bandwidth bound (DESIGN.md 5.3)"}}
 
 
 def synth_c5(nvars=1000, nsamples=100_000):
