@@ -164,39 +164,57 @@ def bench_pc_synth(steps, depth=6, cpu_vars=120):
     return out
 
 
-def bench_munin(steps, warmup, cases=125_000):
-    """SURVEY §8(d) config 4 on one GPU: the seeded Munin-like 1041-variable network, 125k cases
-    (the per-GPU shard of 1M cases on 8 GPUs) at 20 % evidence (208 variables per case)."""
+def bench_munin(steps, warmup, cases=125_000, rank=0, world=1, device=0):
+    """the seeded Munin-like 1041-variable network at 20 % evidence (208
+    variables per case), 125k cases per GPU -- on 8 GPUs the 1M-case job sharded by rank (seed
+    20250131 + rank).  N = 1: kernel time (HIP events); N > 1: wall clock between barriers, max
+    over ranks, all ranks' cases."""
     import tempfile
     import torch
     import fastbn_amd as F
-    from fastbn_amd import synth
+    from fastbn_amd import shard, synth
+    dev = torch.device("cuda", device)
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "munin_like.xml")
         synth.random_network(1041, seed=1041, window=12, path=path, name="munin_like")
         net = synth.read_xmlbif(path)
-        ev = synth.evidence_cases(net, cases, 208, seed=20250131)
+        ev = synth.evidence_cases(net, cases, 208, seed=shard.synthetic_seed(20250131, rank))
         t0 = time.perf_counter()
-        jt = F.JunctionTree(F.Network(path), device=0)
+        jt = F.JunctionTree(F.Network(path), device=device)
         plan_s = time.perf_counter() - t0
-        sys.path.insert(0, os.path.join(REPO, "oracle"))
-        import oracle as O
-        olab, omarg = O.OracleJT(path).infer(ev[:16])
-    d_ev = torch.from_numpy(ev).cuda()
-    d_lab = torch.empty(cases, dtype=torch.int32, device="cuda")
-    d_marg = torch.empty((cases, jt.info["sum_dom"]), dtype=torch.float64, device="cuda")
+        if rank == 0:
+            sys.path.insert(0, os.path.join(REPO, "oracle"))
+            import oracle as O
+            olab, omarg = O.OracleJT(path).infer(ev[:16])
+    d_ev = torch.from_numpy(ev).to(dev)
+    d_lab = torch.empty(cases, dtype=torch.int32, device=dev)
+    d_marg = torch.empty((cases, jt.info["sum_dom"]), dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
     for _ in range(max(1, warmup)):
-        jt.run_device(d_ev.data_ptr(), cases, d_lab.data_ptr(), d_marg.data_ptr(), None)
-    torch.cuda.synchronize()
-    ok = (d_lab[:16].cpu().numpy() == olab).all() and (d_marg[:16].cpu().numpy() == omarg).all()
+        jt.run_device(d_ev.data_ptr(), cases, d_lab.data_ptr(), d_marg.data_ptr(), stream)
+    torch.cuda.synchronize(dev)
+    ok = True
+    if rank == 0:
+        ok = bool((d_lab[:16].cpu().numpy() == olab).all() and (d_marg[:16].cpu().numpy() == omarg).all())
     ms = []
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    w0 = time.perf_counter()
     for _ in range(steps):
-        jt.run_device(d_ev.data_ptr(), cases, d_lab.data_ptr(), d_marg.data_ptr(), None)
+        jt.run_device(d_ev.data_ptr(), cases, d_lab.data_ptr(), d_marg.data_ptr(), stream)
         ms.append(jt.last_kernel_ms())
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    wall = shard.max_over_ranks(time.perf_counter() - w0, dev)
     k = float(np.median(ms))
     bpc = jt.info["algorithmic_bytes_per_case"]
-    return {"metric": "JT test-cases/sec (Munin-like 1041 vars, 20 % evidence)", "value": cases / (k * 1e-3),
-            "unit": "cases/s", "cases": cases, "kernel_ms": k, "plan_s": plan_s,
+    value = cases / (k * 1e-3) if world == 1 else world * cases * steps / wall
+    return {"metric": "JT test-cases/sec (Munin-like 1041 vars, 20 % evidence)", "value": value,
+            "unit": "cases/s", "n_gpus": world, "cases": cases * world, "cases_per_gpu": cases, "kernel_ms": k,
+            "wall_ms_per_step": 1e3 * wall / steps, "plan_s": plan_s,
             "kernel_variant": jt.refresh_info()["variant"], "bit_exact_vs_oracle_16_cases": bool(ok),
             "cliques": jt.info["num_cliques"], "clique_entries": jt.info["clique_entries"],
             "roofline": {"bound": "hbm", "achieved": bpc * cases / (k * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
@@ -365,6 +383,9 @@ def main():
                              "parking them, so measured traffic is below the algorithmic bytes and the "
                              "kernel is fp64-VALU/latency bound (DESIGN.md)"},
     }
+    if world > 1 and not args.no_munin:
+        # BASELINE config 4 at its real scale: 125k Munin-like cases per rank (1M on 8 GPUs)
+        out["munin_like"] = bench_munin(3, 1, rank=rank, world=world, device=local)
     if rank == 0 and world == 1:
         # PCIe-inclusive rate (host evidence in, host labels + marginals out through fbn_jt_run):
         # reported beside the metric, never as `value`

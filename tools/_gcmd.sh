@@ -1,2 +1,2 @@
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_all.log 2>&1 && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && bash tools/profile_round.sh gpurun_out/r01_s3b > gpurun_out/prof.log 2>&1 && bash tools/pmc_valu.sh gpurun_out/r01_s3b/valu > gpurun_out/valu.log 2>&1
+FBN_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 > gpurun_out/b2.json 2> gpurun_out/b2.err && timeout -k 10 300 python -u bench.py --steps 5 --no-pc --no-baseline > gpurun_out/b1.json 2> gpurun_out/b1.err
