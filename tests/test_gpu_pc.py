@@ -59,15 +59,18 @@ def test_pc_stable_alarm5000(alarm_ds, alarm_paths, gs):
         assert pc.GetSHD(alarm_paths["bif"]) == 5
 
 
-@pytest.mark.parametrize("gs", [1, 3])
-def test_pc_stable_alarm5000_pipelined_rounds(alarm_ds, alarm_paths, gs, monkeypatch):
+@pytest.mark.parametrize("gs,staged", [(1, False), (3, False), (1, True)])
+def test_pc_stable_alarm5000_pipelined_rounds(alarm_ds, alarm_paths, gs, staged, monkeypatch):
     """The driver's multi-round path (no full speculation) with the level's edges in two halves
     alternating on the device (pc_driver.cpp), forced on ALARM: identical counts, skeleton and
-    sepsets to the restatement, incl. grouped tests whose groups must not straddle rounds."""
+    sepsets to the restatement, incl. grouped tests whose groups must not straddle rounds; staged:
+    every round through the per-slot device buffers and DMA copies instead of zero-copy."""
     od = O.OracleDataset(csv=alarm_paths["csv"])
     ref = od.pc_stable(0.05, 1000, gs)
     monkeypatch.setenv("FBN_PC_FULLSPEC", "0")
     monkeypatch.setenv("FBN_PC_PIPELINE_EDGES", "1")
+    if staged:
+        monkeypatch.setenv("FBN_CI_NO_ZEROCOPY", "1")
     pc = F.PCStable(0.05, 1000).StructLearnCompData(alarm_ds, group_size=gs)
     assert pc.tests_per_level.tolist() == ref["tests_per_level"]
     assert pc.edges == ref["edges"]
