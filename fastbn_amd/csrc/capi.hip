@@ -31,7 +31,10 @@ extern "C" hipError_t fbn_ci_bits_build(const uint8_t *cols, const int32_t *dims
 extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *dims, const int32_t *row0,
                                          const int32_t *items, long long W, long long n, int d, double alpha,
                                          double *g2, int32_t *df, double *p, uint8_t *indep, int32_t *counts,
-                                         int32_t *counts0, unsigned long long *stats, int num_cu, hipStream_t s);
+                                         int32_t *counts0, unsigned long long *stats, const int32_t *rowcnt,
+                                         int num_cu, hipStream_t s);
+extern "C" hipError_t fbn_ci_bits_rowcount(const uint32_t *bits, long long rows, long long W, int32_t *rowcnt,
+                                           hipStream_t s);
 extern "C" hipError_t fbn_jt_virt_launch(const JtVClique *cls, const int32_t *aux, const double *initv,
                                          const uint64_t *dig, const int32_t *order, const int32_t *sched,
                                          const int32_t *vsel, const int8_t *evid, double *marg, int32_t *labels,
@@ -168,7 +171,7 @@ struct fbn_ci_ctx {
     DevBuf cols, ddims, g2, p, counts;
     DevBuf stats;  // decision-margin log: {min |p - alpha| bits, #tests within 1e-9 of alpha}
     // bit-sliced columns for marginal tests (ci_bits.hip), built on first use
-    DevBuf bits, brow;
+    DevBuf bits, brow, browcnt;  // masks, first row of each variable, sample count per row
     bool bits_ready = false;
     int64_t bits_W = 0;
     CiSlot slot[2];
@@ -906,7 +909,8 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
                            (c->N >= kBitsMinSamples || getenv("FBN_CI_FORCE_BITS"));
     if (bits_path) {
         if (!c->bits_ready) {
-            const int64_t W = (c->N + 31) / 32;
+            // words per mask row, padded to a multiple of 4 (zero words) for 16-byte row loads
+            const int64_t W = ((c->N + 31) / 32 + 3) & ~(int64_t)3;
             std::vector<int32_t> row0(c->nvars);
             int64_t rows = 0;
             for (int v = 0; v < c->nvars; ++v) row0[v] = (int32_t)rows, rows += std::min(c->dims[v], 8);
@@ -916,6 +920,9 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
             hipError_t e = fbn_ci_bits_build(c->cols.as<uint8_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(), c->N,
                                              W, c->nvars, c->bits.as<uint32_t>(), s);
             if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci bits build: %s", hipGetErrorString(e));
+            if ((rc = c->browcnt.ensure((size_t)std::max<int64_t>(rows, 1) * 4))) return rc;
+            e = fbn_ci_bits_rowcount(c->bits.as<uint32_t>(), rows, W, c->browcnt.as<int32_t>(), s);
+            if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci bits row counts: %s", hipGetErrorString(e));
             c->bits_W = W;
             c->bits_ready = true;
         }
@@ -937,7 +944,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
                                           want_g2p ? c->p.as<double>() : nullptr,
                                           zc_indep ? zc_indep : S.indep.as<uint8_t>(),
                                           S.bcounts.as<int32_t>(), counts_dev, c->stats.as<unsigned long long>(),
-                                          c->num_cu, s);
+                                          c->browcnt.as<int32_t>(), c->num_cu, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci bits kernel launch: %s", hipGetErrorString(e));
         FBN_HIP(hipEventRecord(S.ev1, s));
         return FBN_OK;

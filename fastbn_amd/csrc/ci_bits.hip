@@ -52,29 +52,32 @@ __device__ __forceinline__ void count_test(const uint32_t *__restrict__ bx, cons
     uint32_t cnt[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) cnt[c] = 0u;
-    long long w = lane;
-    auto word = [&](long long ww) {
-        uint32_t x[DX], y[DY], z[DZ];
+    // four consecutive words per lane per step, one 16-byte load per mask row (W is a multiple
+    // of 4, padding words are zero)
+    typedef __attribute__((ext_vector_type(4))) unsigned u4;
+    auto quad = [&](long long w4) {
+        u4 x[DX], y[DY], z[DZ];
 #pragma unroll
-        for (int a = 0; a < DX; ++a) x[a] = bx[a * W + ww];
+        for (int a = 0; a < DX; ++a) x[a] = *reinterpret_cast<const u4 *>(bx + a * W + 4 * w4);
 #pragma unroll
-        for (int b = 0; b < DY; ++b) y[b] = by[b * W + ww];
+        for (int b = 0; b < DY; ++b) y[b] = *reinterpret_cast<const u4 *>(by + b * W + 4 * w4);
 #pragma unroll
-        for (int c = 0; c < DZ; ++c) z[c] = (DZ == 1) ? 0xFFFFFFFFu : (c < dz ? bz[c * W + ww] : 0u);
+        for (int c = 0; c < DZ; ++c) {
+            if (DZ == 1) z[c] = u4{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+            else z[c] = c < dz ? *reinterpret_cast<const u4 *>(bz + c * W + 4 * w4) : u4{0u, 0u, 0u, 0u};
+        }
 #pragma unroll
-        for (int a = 0; a < DX; ++a)
+        for (int k = 0; k < 4; ++k)
 #pragma unroll
-            for (int b = 0; b < DY; ++b) {
-                const uint32_t xy = x[a] & y[b];
+            for (int a = 0; a < DX; ++a)
 #pragma unroll
-                for (int c = 0; c < DZ; ++c) cnt[(c * DX + a) * DY + b] += __builtin_popcount(xy & z[c]);
-            }
+                for (int b = 0; b < DY; ++b) {
+                    const uint32_t xy = x[a][k] & y[b][k];
+#pragma unroll
+                    for (int c = 0; c < DZ; ++c) cnt[(c * DX + a) * DY + b] += __builtin_popcount(xy & z[c][k]);
+                }
     };
-    for (; w + 64 < W; w += 128) {  // two words per lane in flight
-        word(w);
-        word(w + 64);
-    }
-    for (; w < W; w += 64) word(w);
+    for (long long w4 = lane; 4 * w4 < W; w4 += 64) quad(w4);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         uint32_t v = cnt[c];
@@ -91,13 +94,74 @@ __device__ __forceinline__ void count_test(const uint32_t *__restrict__ bx, cons
     }
 }
 
+// marginal test N[a][b] (Counts2D::FillTable, src/CellTable.cpp:430-455) from (DX-1)(DY-1)
+// popcounts per word: the masks of a variable partition the samples, so the last value's row and
+// column follow exactly from the per-value sample counts nx / ny of x and y (test-independent,
+// ci_bits_rowcount) -- N[a][DY-1] = nx[a] - sum_b N[a][b], N[DX-1][b] = ny[b] - sum_a N[a][b];
+// only DX-1 and DY-1 mask rows are read
+template <int DX, int DY>
+__device__ __forceinline__ void count_pair(const uint32_t *__restrict__ bx, const uint32_t *__restrict__ by,
+                                           const int32_t *__restrict__ nx, const int32_t *__restrict__ ny,
+                                           long long W, int lane, int32_t *__restrict__ out) {
+    constexpr int MX = DX - 1, MY = DY - 1, NC = MX * MY > 0 ? MX * MY : 1;
+    uint32_t cnt[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) cnt[c] = 0u;
+    if (MX > 0 && MY > 0) {
+        typedef __attribute__((ext_vector_type(4))) unsigned u4;
+        for (long long w4 = lane; 4 * w4 < W; w4 += 64) {
+            u4 x[MX > 0 ? MX : 1], y[MY > 0 ? MY : 1];
+#pragma unroll
+            for (int a = 0; a < MX; ++a) x[a] = *reinterpret_cast<const u4 *>(bx + a * W + 4 * w4);
+#pragma unroll
+            for (int b = 0; b < MY; ++b) y[b] = *reinterpret_cast<const u4 *>(by + b * W + 4 * w4);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int a = 0; a < MX; ++a)
+#pragma unroll
+                    for (int b = 0; b < MY; ++b) cnt[a * MY + b] += __builtin_popcount(x[a][k] & y[b][k]);
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            uint32_t v = cnt[c];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+            cnt[c] = v;
+        }
+    }
+    // every lane now holds the wave totals: complete the table with the marginals
+    int32_t full[DX * DY];
+#pragma unroll
+    for (int a = 0; a < MX; ++a) {
+        int32_t r = nx[a];
+#pragma unroll
+        for (int b = 0; b < MY; ++b) full[a * DY + b] = (int32_t)cnt[a * MY + b], r -= (int32_t)cnt[a * MY + b];
+        full[a * DY + MY] = r;
+    }
+#pragma unroll
+    for (int b = 0; b < DY; ++b) {
+        int32_t r = ny[b];
+#pragma unroll
+        for (int a = 0; a < MX; ++a) r -= full[a * DY + b];
+        full[MX * DY + b] = r;
+    }
+    if (lane < DX * DY) {
+        int32_t v = 0;
+#pragma unroll
+        for (int c = 0; c < DX * DY; ++c) v = lane == c ? full[c] : v;
+        out[lane] = v;
+    }
+}
+
 constexpr int kBitsCells = 64;  // count slots per test
 
 // phase 1: counts[t][64] of every test, one wave per test; D = 0 (x, y) or 1 (x, y, z)
 template <int D>
 __global__ __launch_bounds__(256) void ci_bits_count(const uint32_t *__restrict__ bits, const int32_t *__restrict__ dims,
                                                      const int32_t *__restrict__ row0, const int32_t *__restrict__ items,
-                                                     long long W, long long n, int32_t *__restrict__ counts) {
+                                                     long long W, long long n, int32_t *__restrict__ counts,
+                                                     const int32_t *__restrict__ rowcnt) {
     const int lane = threadIdx.x & 63;
     const long long wave = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
     for (long long t = wave; t < n; t += (long long)gridDim.x * 4) {
@@ -113,9 +177,13 @@ __global__ __launch_bounds__(256) void ci_bits_count(const uint32_t *__restrict_
         }
         int32_t *out = counts + t * kBitsCells;
         constexpr int DZ = D == 1 ? 4 : 1;
+        const int32_t *nx = rowcnt + row0[x], *ny = rowcnt + row0[y];
         switch (dx * 8 + dy) {
-#define FBN_PAIR(A, B) \
-    case A * 8 + B: count_test<A, B, DZ>(bx, by, bz, dz, W, lane, out); break;
+#define FBN_PAIR(A, B)                                                             \
+    case A * 8 + B:                                                                \
+        if (D == 0) count_pair<A, B>(bx, by, nx, ny, W, lane, out);                \
+        else count_test<A, B, DZ>(bx, by, bz, dz, W, lane, out);                   \
+        break;
             FBN_PAIR(1, 1) FBN_PAIR(1, 2) FBN_PAIR(1, 3) FBN_PAIR(1, 4)
             FBN_PAIR(2, 1) FBN_PAIR(2, 2) FBN_PAIR(2, 3) FBN_PAIR(2, 4)
             FBN_PAIR(3, 1) FBN_PAIR(3, 2) FBN_PAIR(3, 3) FBN_PAIR(3, 4)
@@ -259,6 +327,27 @@ extern "C" hipError_t fbn_ci_cols_check(const uint8_t *cols, const int32_t *dims
     return hipGetLastError();
 }
 
+// sample count of every mask row (variable v, value a): one wave per row
+static __global__ __launch_bounds__(256) void ci_bits_rowcount(const uint32_t *__restrict__ bits, long long rows,
+                                                               long long W, int32_t *__restrict__ rowcnt) {
+    const int lane = threadIdx.x & 63;
+    for (long long r = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += (long long)gridDim.x * 4) {
+        uint32_t v = 0;
+        for (long long w = lane; w < W; w += 64) v += __builtin_popcount(bits[r * W + w]);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+        if (lane == 0) rowcnt[r] = (int32_t)v;
+    }
+}
+
+extern "C" hipError_t fbn_ci_bits_rowcount(const uint32_t *bits, long long rows, long long W, int32_t *rowcnt,
+                                           hipStream_t s) {
+    const long long g = (rows + 3) / 4;
+    hipLaunchKernelGGL(ci_bits_rowcount, dim3((unsigned)(g < 4096 ? (g > 0 ? g : 1) : 4096)), dim3(256), 0, s, bits,
+                       rows, W, rowcnt);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t fbn_ci_bits_build(const uint8_t *cols, const int32_t *dims, const int32_t *row0, long long N,
                                         long long W, int nvars, uint32_t *bits, hipStream_t s) {
     const long long total = (long long)nvars * W;
@@ -270,16 +359,17 @@ extern "C" hipError_t fbn_ci_bits_build(const uint8_t *cols, const int32_t *dims
 extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *dims, const int32_t *row0,
                                          const int32_t *items, long long W, long long n, int d, double alpha,
                                          double *g2, int32_t *df, double *p, uint8_t *indep, int32_t *counts,
-                                         int32_t *counts0, unsigned long long *stats, int num_cu, hipStream_t s) {
+                                         int32_t *counts0, unsigned long long *stats, const int32_t *rowcnt,
+                                         int num_cu, hipStream_t s) {
     const long long g1 = (n + 3) / 4, cap = (long long)num_cu * 8;
     const long long g2g = (n + 255) / 256;
     const dim3 b1((unsigned)(g1 < cap ? g1 : cap)), b2((unsigned)(g2g < cap ? g2g : cap));
     if (d == 0) {
-        hipLaunchKernelGGL(ci_bits_count<0>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts);
+        hipLaunchKernelGGL(ci_bits_count<0>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts, rowcnt);
         hipLaunchKernelGGL(ci_bits_g2<0>, b2, dim3(256), 0, s, counts, dims, items, n, alpha, g2, df, p, indep,
                            counts0, stats);
     } else if (d == 1) {
-        hipLaunchKernelGGL(ci_bits_count<1>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts);
+        hipLaunchKernelGGL(ci_bits_count<1>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts, rowcnt);
         hipLaunchKernelGGL(ci_bits_g2<1>, b2, dim3(256), 0, s, counts, dims, items, n, alpha, g2, df, p, indep,
                            counts0, stats);
     } else {
