@@ -32,7 +32,7 @@ extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *di
                                          const int32_t *items, long long W, long long n, int d, double alpha,
                                          double *g2, int32_t *df, double *p, uint8_t *indep, int32_t *counts,
                                          int32_t *counts0, unsigned long long *stats, const int32_t *rowcnt,
-                                         int num_cu, hipStream_t s);
+                                         int32_t *pairtab, int pmode, int nvars, int num_cu, hipStream_t s);
 extern "C" hipError_t fbn_ci_bits_rowcount(const uint32_t *bits, long long rows, long long W, int32_t *rowcnt,
                                            hipStream_t s);
 extern "C" hipError_t fbn_jt_virt_launch(const JtVClique *cls, const int32_t *aux, const double *initv,
@@ -172,6 +172,11 @@ struct fbn_ci_ctx {
     DevBuf stats;  // decision-margin log: {min |p - alpha| bits, #tests within 1e-9 of alpha}
     // bit-sliced columns for marginal tests (ci_bits.hip), built on first use
     DevBuf bits, brow, browcnt;  // masks, first row of each variable, sample count per row
+    // pair tables of every (i < j), 16 counts each, recorded by level 0 of a PC run and used by its
+    // level-1 tests (pair_mode: 0 off, 1 record at the next marginal batch, 2 use if recorded)
+    DevBuf pairtab;
+    int pair_mode = 0;
+    bool pairs_recorded = false;
     bool bits_ready = false;
     int64_t bits_W = 0;
     CiSlot slot[2];
@@ -937,6 +942,15 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         if (!zc_items) FBN_HIP(hipMemcpyAsync(S.items.p, items, (size_t)n * w * 4, hipMemcpyHostToDevice, s));
         const int32_t *ditems = zc_items ? zc_items : S.items.as<int32_t>();
         S.last_bytes = dim_rows * c->bits_W * 4;
+        int pmode = 0;
+        if (c->pair_mode == 1 && d == 0) {
+            const size_t np = (size_t)c->nvars * (c->nvars - 1) / 2;
+            if ((rc = c->pairtab.ensure(std::max<size_t>(np, 1) * 16 * 4))) return rc;
+            pmode = 1;
+            c->pairs_recorded = true;
+        } else if (c->pair_mode == 2 && d == 1 && c->pairs_recorded) {
+            pmode = 2;
+        }
         FBN_HIP(hipEventRecord(S.ev0, s));
         hipError_t e = fbn_ci_bits_launch(c->bits.as<uint32_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(),
                                           ditems, c->bits_W, n, d, alpha,
@@ -944,7 +958,8 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
                                           want_g2p ? c->p.as<double>() : nullptr,
                                           zc_indep ? zc_indep : S.indep.as<uint8_t>(),
                                           S.bcounts.as<int32_t>(), counts_dev, c->stats.as<unsigned long long>(),
-                                          c->browcnt.as<int32_t>(), c->num_cu, s);
+                                          c->browcnt.as<int32_t>(), c->pairtab.as<int32_t>(), pmode, c->nvars,
+                                          c->num_cu, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci bits kernel launch: %s", hipGetErrorString(e));
         FBN_HIP(hipEventRecord(S.ev1, s));
         return FBN_OK;
@@ -1226,6 +1241,10 @@ void CiCtxShape(const fbn_ci_ctx *c, int *nvars, int64_t *nsamples) {
 // batches up to this many item bytes take the zero-copy path of CiBatchLaunch
 constexpr size_t kZeroCopyBytes = 256 << 10;
 const int32_t *CiCtxDims(const fbn_ci_ctx *c) { return c->dims.data(); }
+void CiSetPairMode(fbn_ci_ctx *c, int mode) {
+    c->pair_mode = mode;
+    if (mode != 2) c->pairs_recorded = false;
+}
 int CiBatchLaunch(fbn_ci_ctx *c, int k, const int32_t *items, int64_t n, int d, double alpha, bool want_df,
                   const CiBatchStats *pre) {
     CiSlot &S = c->slot[k];

@@ -102,7 +102,8 @@ __device__ __forceinline__ void count_test(const uint32_t *__restrict__ bx, cons
 template <int DX, int DY>
 __device__ __forceinline__ void count_pair(const uint32_t *__restrict__ bx, const uint32_t *__restrict__ by,
                                            const int32_t *__restrict__ nx, const int32_t *__restrict__ ny,
-                                           long long W, int lane, int32_t *__restrict__ out) {
+                                           long long W, int lane, int32_t *__restrict__ out,
+                                           int32_t *__restrict__ rec) {
     constexpr int MX = DX - 1, MY = DY - 1, NC = MX * MY > 0 ? MX * MY : 1;
     uint32_t cnt[NC];
 #pragma unroll
@@ -151,6 +152,93 @@ __device__ __forceinline__ void count_pair(const uint32_t *__restrict__ bx, cons
 #pragma unroll
         for (int c = 0; c < DX * DY; ++c) v = lane == c ? full[c] : v;
         out[lane] = v;
+        if (rec) rec[lane] = v;
+    }
+}
+
+// conditional test N[c][a][b] (one conditioning variable z) from (DZ-1)(DX-1)(DY-1) popcounts per
+// word: the pair tables N_xy, N_xz, N_yz this run's level 0 recorded (every pair of the complete
+// graph, table of (u < v) stored [value of u][value of v]) give the last value of each variable
+// exactly -- N[c][a][DY-1] = N_xz[a][c] - sum_b, N[c][DX-1][b] = N_yz[b][c] - sum_a,
+// N[DZ-1][a][b] = N_xy[a][b] - sum_c; only DX-1, DY-1, DZ-1 mask rows are read
+template <int DX, int DY, int DZ>
+__device__ __forceinline__ void count_test_derived(const uint32_t *__restrict__ bx, const uint32_t *__restrict__ by,
+                                                   const uint32_t *__restrict__ bz, long long W, int lane,
+                                                   int32_t *__restrict__ out, const int32_t *__restrict__ Txy, bool txy,
+                                                   const int32_t *__restrict__ Txz, bool txz,
+                                                   const int32_t *__restrict__ Tyz, bool tyz) {
+    constexpr int MX = DX - 1, MY = DY - 1, MZ = DZ - 1, M = MX * MY * MZ, NC = M > 0 ? M : 1;
+    uint32_t cnt[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) cnt[c] = 0u;
+    if (M > 0) {
+        typedef __attribute__((ext_vector_type(4))) unsigned u4;
+        for (long long w4 = lane; 4 * w4 < W; w4 += 64) {
+            u4 x[MX > 0 ? MX : 1], y[MY > 0 ? MY : 1], z[MZ > 0 ? MZ : 1];
+#pragma unroll
+            for (int a = 0; a < MX; ++a) x[a] = *reinterpret_cast<const u4 *>(bx + a * W + 4 * w4);
+#pragma unroll
+            for (int b = 0; b < MY; ++b) y[b] = *reinterpret_cast<const u4 *>(by + b * W + 4 * w4);
+#pragma unroll
+            for (int c = 0; c < MZ; ++c) z[c] = *reinterpret_cast<const u4 *>(bz + c * W + 4 * w4);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int a = 0; a < MX; ++a)
+#pragma unroll
+                    for (int b = 0; b < MY; ++b) {
+                        const uint32_t xy = x[a][k] & y[b][k];
+#pragma unroll
+                        for (int c = 0; c < MZ; ++c) cnt[(c * MX + a) * MY + b] += __builtin_popcount(xy & z[c][k]);
+                    }
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            uint32_t v = cnt[c];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+            cnt[c] = v;
+        }
+    }
+    auto nxy = [&](int a, int b) { return txy ? Txy[b * DX + a] : Txy[a * DY + b]; };
+    auto nxz = [&](int a, int c) { return txz ? Txz[c * DX + a] : Txz[a * DZ + c]; };
+    auto nyz = [&](int b, int c) { return tyz ? Tyz[c * DY + b] : Tyz[b * DZ + c]; };
+    int32_t full[DZ * DX * DY];
+#pragma unroll
+    for (int c = 0; c < MZ; ++c) {
+#pragma unroll
+        for (int a = 0; a < MX; ++a) {
+            int32_t r = nxz(a, c);
+#pragma unroll
+            for (int b = 0; b < MY; ++b) {
+                const int32_t v = (int32_t)cnt[(c * MX + a) * MY + b];
+                full[(c * DX + a) * DY + b] = v;
+                r -= v;
+            }
+            full[(c * DX + a) * DY + MY] = r;
+        }
+#pragma unroll
+        for (int b = 0; b < DY; ++b) {
+            int32_t r = nyz(b, c);
+#pragma unroll
+            for (int a = 0; a < MX; ++a) r -= full[(c * DX + a) * DY + b];
+            full[(c * DX + MX) * DY + b] = r;
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < DX; ++a)
+#pragma unroll
+        for (int b = 0; b < DY; ++b) {
+            int32_t r = nxy(a, b);
+#pragma unroll
+            for (int c = 0; c < MZ; ++c) r -= full[(c * DX + a) * DY + b];
+            full[(MZ * DX + a) * DY + b] = r;
+        }
+    if (lane < DZ * DX * DY) {
+        int32_t v = 0;
+#pragma unroll
+        for (int c = 0; c < DZ * DX * DY; ++c) v = lane == c ? full[c] : v;
+        out[lane] = v;
     }
 }
 
@@ -161,7 +249,8 @@ template <int D>
 __global__ __launch_bounds__(256) void ci_bits_count(const uint32_t *__restrict__ bits, const int32_t *__restrict__ dims,
                                                      const int32_t *__restrict__ row0, const int32_t *__restrict__ items,
                                                      long long W, long long n, int32_t *__restrict__ counts,
-                                                     const int32_t *__restrict__ rowcnt) {
+                                                     const int32_t *__restrict__ rowcnt, int32_t *__restrict__ pairtab,
+                                                     int nvars) {
     const int lane = threadIdx.x & 63;
     const long long wave = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
     for (long long t = wave; t < n; t += (long long)gridDim.x * 4) {
@@ -178,10 +267,14 @@ __global__ __launch_bounds__(256) void ci_bits_count(const uint32_t *__restrict_
         int32_t *out = counts + t * kBitsCells;
         constexpr int DZ = D == 1 ? 4 : 1;
         const int32_t *nx = rowcnt + row0[x], *ny = rowcnt + row0[y];
+        // level 0 of a PC run records every pair's table (pair index of x < y, 16 slots)
+        int32_t *rec = (D == 0 && pairtab && x < y)
+                           ? pairtab + 16 * ((long long)x * nvars - (long long)x * (x + 1) / 2 + (y - x - 1))
+                           : nullptr;
         switch (dx * 8 + dy) {
 #define FBN_PAIR(A, B)                                                             \
     case A * 8 + B:                                                                \
-        if (D == 0) count_pair<A, B>(bx, by, nx, ny, W, lane, out);                \
+        if (D == 0) count_pair<A, B>(bx, by, nx, ny, W, lane, out, rec);           \
         else count_test<A, B, DZ>(bx, by, bz, dz, W, lane, out);                   \
         break;
             FBN_PAIR(1, 1) FBN_PAIR(1, 2) FBN_PAIR(1, 3) FBN_PAIR(1, 4)
@@ -190,6 +283,45 @@ __global__ __launch_bounds__(256) void ci_bits_count(const uint32_t *__restrict_
             FBN_PAIR(4, 1) FBN_PAIR(4, 2) FBN_PAIR(4, 3) FBN_PAIR(4, 4)
 #undef FBN_PAIR
         default: break;  // the host only routes tests with dims <= 4 here
+        }
+    }
+}
+
+// level >= 1 of a PC run, one conditioning variable, pair tables recorded: derived counting
+__device__ __forceinline__ const int32_t *pair_table(const int32_t *pairtab, int nvars, int u, int v) {
+    const int i = u < v ? u : v, j = u < v ? v : u;
+    return pairtab + 16 * ((long long)i * nvars - (long long)i * (i + 1) / 2 + (j - i - 1));
+}
+__global__ __launch_bounds__(256) void ci_bits_count_derived(const uint32_t *__restrict__ bits,
+                                                             const int32_t *__restrict__ dims,
+                                                             const int32_t *__restrict__ row0,
+                                                             const int32_t *__restrict__ items, long long W, long long n,
+                                                             int32_t *__restrict__ counts,
+                                                             const int32_t *__restrict__ pairtab, int nvars) {
+    const int lane = threadIdx.x & 63;
+    const long long wave = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    for (long long t = wave; t < n; t += (long long)gridDim.x * 4) {
+        const int x = items[3 * t], y = items[3 * t + 1], z = items[3 * t + 2];
+        const int dx = dims[x], dy = dims[y], dz = dims[z];
+        const uint32_t *bx = bits + (size_t)row0[x] * W, *by = bits + (size_t)row0[y] * W,
+                       *bz = bits + (size_t)row0[z] * W;
+        const int32_t *Txy = pair_table(pairtab, nvars, x, y), *Txz = pair_table(pairtab, nvars, x, z),
+                      *Tyz = pair_table(pairtab, nvars, y, z);
+        int32_t *out = counts + t * kBitsCells;
+        switch (dz * 64 + dx * 8 + dy) {
+#define FBN_TRIPLE(C, A, B)                                                                                  \
+    case C * 64 + A * 8 + B:                                                                                 \
+        count_test_derived<A, B, C>(bx, by, bz, W, lane, out, Txy, x > y, Txz, x > z, Tyz, y > z);          \
+        break;
+#define FBN_ROW(C)                                                                                           \
+    FBN_TRIPLE(C, 1, 1) FBN_TRIPLE(C, 1, 2) FBN_TRIPLE(C, 1, 3) FBN_TRIPLE(C, 1, 4)                          \
+    FBN_TRIPLE(C, 2, 1) FBN_TRIPLE(C, 2, 2) FBN_TRIPLE(C, 2, 3) FBN_TRIPLE(C, 2, 4)                          \
+    FBN_TRIPLE(C, 3, 1) FBN_TRIPLE(C, 3, 2) FBN_TRIPLE(C, 3, 3) FBN_TRIPLE(C, 3, 4)                          \
+    FBN_TRIPLE(C, 4, 1) FBN_TRIPLE(C, 4, 2) FBN_TRIPLE(C, 4, 3) FBN_TRIPLE(C, 4, 4)
+            FBN_ROW(1) FBN_ROW(2) FBN_ROW(3) FBN_ROW(4)
+#undef FBN_ROW
+#undef FBN_TRIPLE
+        default: break;
         }
     }
 }
@@ -360,16 +492,22 @@ extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *di
                                          const int32_t *items, long long W, long long n, int d, double alpha,
                                          double *g2, int32_t *df, double *p, uint8_t *indep, int32_t *counts,
                                          int32_t *counts0, unsigned long long *stats, const int32_t *rowcnt,
-                                         int num_cu, hipStream_t s) {
+                                         int32_t *pairtab, int pmode, int nvars, int num_cu, hipStream_t s) {
     const long long g1 = (n + 3) / 4, cap = (long long)num_cu * 8;
     const long long g2g = (n + 255) / 256;
     const dim3 b1((unsigned)(g1 < cap ? g1 : cap)), b2((unsigned)(g2g < cap ? g2g : cap));
     if (d == 0) {
-        hipLaunchKernelGGL(ci_bits_count<0>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts, rowcnt);
+        hipLaunchKernelGGL(ci_bits_count<0>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts, rowcnt,
+                           pmode == 1 ? pairtab : nullptr, nvars);
         hipLaunchKernelGGL(ci_bits_g2<0>, b2, dim3(256), 0, s, counts, dims, items, n, alpha, g2, df, p, indep,
                            counts0, stats);
     } else if (d == 1) {
-        hipLaunchKernelGGL(ci_bits_count<1>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts, rowcnt);
+        if (pmode == 2)
+            hipLaunchKernelGGL(ci_bits_count_derived, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts,
+                               (const int32_t *)pairtab, nvars);
+        else
+            hipLaunchKernelGGL(ci_bits_count<1>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts, rowcnt,
+                               nullptr, nvars);
         hipLaunchKernelGGL(ci_bits_g2<1>, b2, dim3(256), 0, s, counts, dims, items, n, alpha, g2, df, p, indep,
                            counts0, stats);
     } else {

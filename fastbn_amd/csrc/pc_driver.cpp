@@ -330,6 +330,14 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
         for (int j = 0; j < n; ++j)
             if (i != j) adj[i].push_back(j);
     const bool timing = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic: host phase times per level
+    // level 0 tests every pair: its tables are recorded for the level-1 kernel (derived counting)
+    // and dropped when this run ends, however it ends
+    struct PairModeGuard {
+        fbn_ci_ctx *c;
+        ~PairModeGuard() { CiSetPairMode(c, 0); }
+    } pair_guard{ctx};
+    const bool pairs = !getenv("FBN_CI_NO_PAIRS");
+    CiSetPairMode(ctx, pairs ? 1 : 0);
     for (int d = 0; d == 0 || d < depth; ++d) {
         LevelOut out;
         auto ta = std::chrono::steady_clock::now();
@@ -343,6 +351,7 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
         res.launched_per_level.push_back(out.launched);
         auto tc = std::chrono::steady_clock::now();
         ApplyRemovals(out.removed, edges, adj);
+        if (d == 0 && pairs) CiSetPairMode(ctx, 2);
         auto td = std::chrono::steady_clock::now();
         if (timing)
             fprintf(stderr, "pc level %d: run %.2f ms (kernels %.2f), sepsets %.2f ms, removals %.2f ms\n", d,

@@ -147,6 +147,10 @@ struct CiBatchStats {
 int CiBatchLaunch(fbn_ci_ctx *c, int k, const int32_t *items, int64_t n, int d, double alpha, bool want_df,
                   const CiBatchStats *pre = nullptr);
 const int32_t *CiCtxDims(const fbn_ci_ctx *c);  // state count per variable
+// pair tables of the bit-sliced path: 1 = the next marginal batch records every pair's table (it
+// must test all pairs i < j: a PC run's level 0), 2 = one-conditioning-variable batches derive the
+// last value of x, y and z from them, 0 = off (also drops what was recorded)
+void CiSetPairMode(fbn_ci_ctx *c, int mode);
 int CiBatchWait(fbn_ci_ctx *c, int k, uint8_t *indep, int32_t *df, PCResultHost &res);
 int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResultHost &res);
 // one level for an edge range (the unit a multi-GPU driver partitions), see pc_driver.cpp

@@ -78,6 +78,29 @@ def test_pc_stable_alarm5000_pipelined_rounds(alarm_ds, alarm_paths, gs, staged,
     assert pc.launched_per_level.tolist() != [666, 5157, 1212, 128, 15]  # not the one-round schedule
 
 
+@pytest.mark.parametrize("pairs", [True, False])
+def test_pc_stable_alarm5000_bit_sliced_pair_tables(alarm_ds, alarm_paths, pairs, monkeypatch):
+    """Levels 0-1 through the bit-sliced kernels (forced below their sample threshold): level 0
+    records every pair's table, level 1 derives the last value of x, y and z from them
+    (ci_bits_count_derived) -- identical counts, skeleton and sepsets to the restatement."""
+    od = O.OracleDataset(csv=alarm_paths["csv"])
+    ref = od.pc_stable(0.05, 1000, 1)
+    monkeypatch.setenv("FBN_CI_FORCE_BITS", "1")
+    if not pairs:
+        monkeypatch.setenv("FBN_CI_NO_PAIRS", "1")
+    ci = F.IndependenceTest(alarm_ds)
+    for _ in range(2):  # a second run on the same context re-records its own level 0
+        pc = F.PCStable(0.05, 1000).StructLearnCompData(ci)
+        assert pc.tests_per_level.tolist() == ref["tests_per_level"]
+        assert pc.edges == ref["edges"]
+        assert pc.sepset == ref["sepset"]
+    # single tests after the run use full counting again (pair tables dropped at the end of the run)
+    g2, df, p, ind = ci.run(np.array([[0, 1, 2], [5, 9, 30]], np.int32), 1)
+    for k, (x, y, z) in enumerate([(0, 1, 2), (5, 9, 30)]):
+        r = od.ci_test(x, y, [z])
+        assert df[k] == r["df"] and ind[k] == r["is_independent"]
+
+
 def test_pc_stable_synthetic_and_ragged_samples(tmp_path):
     from fastbn_amd import synth
     p = str(tmp_path / "syn.xml")
