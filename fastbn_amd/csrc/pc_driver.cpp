@@ -127,7 +127,16 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
         static_assert(sizeof(std::pair<int, int>) == 2 * sizeof(int32_t), "pair layout");
         const int32_t *pairs = reinterpret_cast<const int32_t *>(edges.data() + e_begin);
         indep.resize(E);
-        int rc = CiRunBatch(ctx, pairs, (int64_t)E, 0, alpha, indep.data(), nullptr, res);
+        // statistics of the pairs without the validation pass (they come from the skeleton)
+        const int32_t *dims = CiCtxDims(ctx);
+        CiBatchStats st0{0, 0};
+        for (size_t e = e_begin; e < e_end; ++e) {
+            const int a = dims[edges[e].first], b = dims[edges[e].second];
+            st0.dim_rows += a + b, st0.maxdim = std::max(st0.maxdim, std::max(a, b));
+        }
+        int rc = CiBatchLaunch(ctx, 0, pairs, (int64_t)E, 0, alpha, false, &st0);
+        if (rc) return rc;
+        rc = CiBatchWait(ctx, 0, indep.data(), nullptr, res);
         if (rc) return rc;
         for (size_t e = 0; e < E; ++e) out.removed[e] = indep[e] ? 1 : 0;
         out.counted = out.launched = (int64_t)E;
@@ -145,7 +154,9 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
     // that usually resolve early; later rounds grow 4x per round
     int64_t open_edges = 0;
     for (auto &s : st) open_edges += !s.resolved;
-    int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(32, 8192 / std::max<int64_t>(1, open_edges)));
+    int64_t chunk = std::max<int64_t>(
+        1, std::min<int64_t>(32, EnvOr("FBN_PC_ROUND0", 8192) / std::max<int64_t>(1, open_edges)));
+    const int64_t growth = std::max<int64_t>(2, EnvOr("FBN_PC_GROWTH", 4));  // chunk factor per round
     bool full = false;
     // small levels: every candidate set of every edge in one round (one host round trip per level;
     // the extra speculative tests cost less than the round trips they save)
@@ -226,7 +237,7 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
                 }
             }
         }
-        hf.chunk = std::min<int64_t>(hf.chunk * 4, 1 << 16);
+        hf.chunk = std::min<int64_t>(hf.chunk * growth, 1 << 16);
     };
     auto resolve = [&](Half &hf) {  // in order per edge
         const auto &pend = hf.pend;
