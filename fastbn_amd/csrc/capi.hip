@@ -907,9 +907,9 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
     }
     int rc;
     // tests with <= 1 conditioning variable over variables with <= 4 states: popcounts of
-    // bit-sliced columns (ci_bits.hip).  Below ~32k samples the per-test fixed cost (two launches,
-    // the wave reduction of the counters) outweighs the sample loop: byte-column kernel there.
-    const int64_t kBitsMinSamples = 32768;
+    // bit-sliced columns (ci_bits.hip).  From 4096 samples up (ALARM-5000 included: 0.46 -> 0.40 ms
+    // per PC run with the pair-table level 1); below, the byte-column kernel (untuned regime).
+    const int64_t kBitsMinSamples = 4096;
     const bool bits_path = d <= 1 && maxdim <= 4 && !getenv("FBN_CI_NO_BITS") &&
                            (c->N >= kBitsMinSamples || getenv("FBN_CI_FORCE_BITS"));
     if (bits_path) {

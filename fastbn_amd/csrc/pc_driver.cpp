@@ -86,7 +86,7 @@ int64_t EnvOr(const char *name, int64_t dflt) {
     const char *v = getenv(name);
     return v ? atoll(v) : dflt;
 }
-int64_t FullSpeculation() { return EnvOr("FBN_PC_FULLSPEC", 4096); }
+int64_t FullSpeculation() { return EnvOr("FBN_PC_FULLSPEC", 16384); }
 constexpr int64_t kPipelineEdges = 2048;
 
 int64_t binom(int64_t m, int k) {  // C(m, k), saturating at 2^40
