@@ -148,8 +148,9 @@ def bench_pc_synth(steps, depth=6, cpu_vars=120):
                         "frac": alg / kern_s / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": alg,
                         "byte_column_model_bytes": sum(n_d * N * (d + 2) for d, n_d in enumerate(launched)),
                         "note": "algorithmic = column data each launched test must read once, in the format "
-                                "the kernel reads: levels 0-1 bit-sliced masks ((dx+dy[+dz]) * N/8 B, "
-                                "ci_bits.hip), levels >= 2 uint8 columns (N*(d+2) B, SURVEY 8(d)); the "
+                                "the kernel reads: levels 0-1 bit-sliced mask rows ((dx-1+dy-1[+dz-1]) * N/8 B: "
+                                "the last value of each variable is derived from counts, ci_bits.hip), "
+                                "levels >= 2 uint8 columns (N*(d+2) B, SURVEY 8(d)); the "
                                 "37.5 MB mask store is Infinity-cache resident, so HBM is not the binding "
                                 "limit at this size (byte_column_model_bytes: SURVEY's model for comparison)"}}
     sys.path.insert(0, os.path.join(REPO, "oracle"))

@@ -941,7 +941,6 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         }
         if (!zc_items) FBN_HIP(hipMemcpyAsync(S.items.p, items, (size_t)n * w * 4, hipMemcpyHostToDevice, s));
         const int32_t *ditems = zc_items ? zc_items : S.items.as<int32_t>();
-        S.last_bytes = dim_rows * c->bits_W * 4;
         int pmode = 0;
         if (c->pair_mode == 1 && d == 0) {
             const size_t np = (size_t)c->nvars * (c->nvars - 1) / 2;
@@ -951,6 +950,10 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         } else if (c->pair_mode == 2 && d == 1 && c->pairs_recorded) {
             pmode = 2;
         }
+        // mask rows the count kernel reads: the last value of x and y (and z with pair tables)
+        // is derived, not read (ci_bits.hip)
+        const int64_t skipped = d == 0 ? 2 : (pmode == 2 ? 3 : 0);
+        S.last_bytes = (dim_rows - skipped * n) * c->bits_W * 4;
         FBN_HIP(hipEventRecord(S.ev0, s));
         hipError_t e = fbn_ci_bits_launch(c->bits.as<uint32_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(),
                                           ditems, c->bits_W, n, d, alpha,
