@@ -1077,11 +1077,23 @@ int fbn_pc_stable(fbn_ci_ctx *c, double alpha, int depth, int group_size, fbn_pc
     auto r = std::unique_ptr<fbn_pc_result>(new (std::nothrow) fbn_pc_result());
     if (!r) return SetError(FBN_ERR_NOMEM, "out of memory");
     FBN_HIP(hipSetDevice(c->device));
+    static const bool timing = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic
+    auto t0 = std::chrono::steady_clock::now();
     int rc = CiResetMargin(c);
     if (rc) return rc;
+    auto t1 = std::chrono::steady_clock::now();
     if ((rc = fbn::RunPCStable(c, alpha, depth, group_size, r->r))) return rc;
+    auto t2 = std::chrono::steady_clock::now();
     if ((rc = CiReadMargin(c, &r->r.min_margin, &r->r.near_alpha))) return rc;
+    auto t3 = std::chrono::steady_clock::now();
     if ((rc = fbn::OrientPC(c->nvars, r->r))) return rc;  // StructLearnByPCStable steps 2-3
+    if (timing) {
+        auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+            return std::chrono::duration<double, std::milli>(b - a).count();
+        };
+        fprintf(stderr, "pc_stable: margin reset %.2f ms, skeleton %.2f ms, margin read %.2f ms, orientation %.2f ms\n",
+                ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, std::chrono::steady_clock::now()));
+    }
     *out = r.release();
     return FBN_OK;
 }

@@ -72,11 +72,33 @@ struct Graph {
         }
         return visited != n;
     }
+    // does a directed path from `from` reach `to`?  (DFS over children, visit stamps)
+    std::vector<int> stamp, stack;
+    int epoch = 0;
+    bool Reaches(int from, int to) {
+        if (stamp.size() != (size_t)n) stamp.assign(n, 0);
+        ++epoch;
+        stack.clear();
+        stack.push_back(from);
+        stamp[from] = epoch;
+        while (!stack.empty()) {
+            const int u = stack.back();
+            stack.pop_back();
+            if (u == to) return true;
+            for (int v : children[u])
+                if (stamp[v] != epoch) stamp[v] = epoch, stack.push_back(v);
+        }
+        return false;
+    }
+    // the reference adds the edge and rolls it back if Network::ContainCircle() then holds.  Every
+    // cycle-closing add is rolled back and deletions close no cycle, so the graph is acyclic before
+    // each add, and the new edge p -> c closes a cycle iff c already reaches p: the same answer as a
+    // whole-graph Kahn pass (ContainCircle above), in time proportional to what c reaches
     bool AddDirected(int p, int c) {
+        const bool cyc = p == c || Reaches(c, p);
         parents[c].insert(p);
         children[p].insert(c);
         edges.push_back(Directed(p, c));
-        const bool cyc = ContainCircle();
         if (cyc) DeleteDirected(p, c);
         return !cyc;
     }
@@ -168,7 +190,9 @@ struct Orienter {
         return r;
     }
     bool Rule1(int b, int c) {
-        const std::set<int> par = g.parents[b];  // node-pointer order == index order
+        // node-pointer order == index order; Direct(b, c) edits parents[c] / children[b] only, so
+        // b's parent set is stable while it is walked
+        const std::set<int> &par = g.parents[b];
         for (int a : par) {
             if (IsAdjacentTo(c, a)) continue;
             if (Direct(b, c)) return true;
