@@ -334,12 +334,15 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
     CiCtxShape(ctx, &nvars, &nsamples);
     const int n = nvars;
     std::vector<std::pair<int, int>> edges;
+    edges.reserve((size_t)n * (n - 1) / 2);
     for (int i = 0; i < n; ++i)
         for (int j = i + 1; j < n; ++j) edges.push_back({i, j});
     std::vector<std::vector<int>> adj(n);
-    for (int i = 0; i < n; ++i)
+    for (int i = 0; i < n; ++i) {
+        adj[i].reserve(n - 1);
         for (int j = 0; j < n; ++j)
             if (i != j) adj[i].push_back(j);
+    }
     const bool timing = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic: host phase times per level
     // level 0 tests every pair: its tables are recorded for the level-1 kernel (derived counting)
     // and dropped when this run ends, however it ends
