@@ -101,6 +101,27 @@ def test_pc_stable_alarm5000_bit_sliced_pair_tables(alarm_ds, alarm_paths, pairs
         assert df[k] == r["df"] and ind[k] == r["is_independent"]
 
 
+@pytest.mark.parametrize("rounds", ["default", "pipelined"])
+def test_pc_stable_config5_like_vs_restatement(tmp_path, rounds, monkeypatch):
+    """SURVEY config 5's generator at 150 variables x 50k samples, levels 0-5: every level-0/1
+    test through the bit-sliced kernels (derived last values, recorded pair tables); "pipelined"
+    forces multi-round levels in two halves -- identical test counts, skeleton and sepsets to the
+    restatement."""
+    if rounds == "pipelined":
+        monkeypatch.setenv("FBN_PC_FULLSPEC", "0")
+        monkeypatch.setenv("FBN_PC_PIPELINE_EDGES", "1")
+    from fastbn_amd import synth
+    path = str(tmp_path / "c5.xml")
+    synth.random_network(150, seed=1000, window=50, parent_probs=(1, 1, 1), dom=(2, 4), path=path, k_min=0)
+    cols = synth.forward_sample(synth.read_xmlbif(path), 50000, seed=1000)
+    dims = (cols.max(axis=1).astype(np.int32) + 1)
+    ref = O.OracleDataset(columns=cols, dims=dims).pc_stable(0.05, 6, 1)
+    pc = F.PCStable(0.05, 6).StructLearnCompData(F.Dataset(columns=cols, dims=dims))
+    assert pc.tests_per_level.tolist() == ref["tests_per_level"]
+    assert pc.edges == ref["edges"]
+    assert pc.sepset == ref["sepset"]
+
+
 def test_pc_stable_synthetic_and_ragged_samples(tmp_path):
     from fastbn_amd import synth
     p = str(tmp_path / "syn.xml")

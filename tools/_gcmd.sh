@@ -1,2 +1,2 @@
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_jt.py -x -q --timeout 120 --timeout-method thread > gpurun_out/tjt.log 2>&1 && timeout -k 10 300 python -u bench.py --steps 10 --no-pc --no-munin --no-baseline > gpurun_out/b1.json 2> gpurun_out/b1.err && FBN_JT_NO_HOSTREG=1 timeout -k 10 300 python -u bench.py --steps 10 --no-pc --no-munin --no-baseline > gpurun_out/b2.json 2> gpurun_out/b2.err
+timeout -k 10 400 python -u -m pytest tests/test_gpu_pc.py -x -v --timeout 200 --timeout-method thread -k config5 > gpurun_out/tc5.log 2>&1
