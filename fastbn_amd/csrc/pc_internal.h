@@ -27,7 +27,7 @@ class SepsetMap {
         size_t size() const { return (size_t)n; }
     };
     void set(std::pair<int, int> key, const int *z, int n) {
-        sorted_ = sorted_ && (e_.empty() || e_.back().key < key);
+        if (!e_.empty() && !(e_.back().key < key)) sorted_ = false, runs_.push_back(e_.size());
         e_.push_back(Ent{key, (int64_t)pool_.size(), n});
         pool_.insert(pool_.end(), z, z + n);
     }
@@ -43,7 +43,7 @@ class SepsetMap {
         int64_t q = p0;
         for (size_t i = 0; i < n; ++i) {
             if (!removed[i]) continue;
-            sorted_ = sorted_ && (o == 0 || e_[o - 1].key < keys[i]);
+            if (o > 0 && !(e_[o - 1].key < keys[i])) sorted_ = false, runs_.push_back(o);
             e_[o++] = Ent{keys[i], q, d};
             for (int j = 0; j < d; ++j) pool_[(size_t)q + j] = sep[i * (size_t)d + j];
             q += d;
@@ -55,14 +55,19 @@ class SepsetMap {
         n0_ = n;
         l0_.assign(removed, removed + (size_t)n * (n - 1) / 2);
     }
+    // lookups need no sort: the entries are a few ascending runs (one per level), searched from the
+    // last run back (a key set twice keeps its last value)
     bool find(std::pair<int, int> key, View *v) const {
-        sort();
-        auto it = std::lower_bound(e_.begin(), e_.end(), key, [](const Ent &a, const std::pair<int, int> &k) {
-            return a.key < k;
-        });
-        if (it != e_.end() && it->key == key) {
-            *v = View{pool_.data() + it->off, it->len};
-            return true;
+        size_t end = e_.size();
+        for (size_t r = runs_.size() + 1; r-- > 0;) {
+            const size_t begin = r ? runs_[r - 1] : 0;
+            auto it = std::lower_bound(e_.begin() + begin, e_.begin() + end, key,
+                                       [](const Ent &a, const std::pair<int, int> &k) { return a.key < k; });
+            if (it != e_.begin() + end && it->key == key) {
+                *v = View{pool_.data() + it->off, it->len};
+                return true;
+            }
+            end = begin;
         }
         const int i = key.first, j = key.second;
         if (!l0_.empty() && 0 <= i && i < j && j < n0_ &&
@@ -80,7 +85,7 @@ class SepsetMap {
             for (int i = 0; i < n0_; ++i)
                 for (int j = i + 1; j < n0_; ++j, ++k)
                     if (l0_[k]) {
-                        sorted_ = sorted_ && (e_.empty() || e_.back().key < std::make_pair(i, j));
+                        if (!e_.empty() && !(e_.back().key < std::make_pair(i, j))) sorted_ = false;
                         e_.push_back(Ent{{i, j}, 0, 0});
                     }
             l0_.clear();
@@ -108,8 +113,10 @@ class SepsetMap {
         }
         e_.resize(o);
         sorted_ = true;
+        runs_.clear();
     }
     mutable std::vector<Ent> e_;
+    mutable std::vector<size_t> runs_;  // start of every ascending run after the first
     std::vector<int> pool_;
     mutable std::vector<char> l0_;
     int n0_ = 0;
