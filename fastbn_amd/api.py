@@ -45,6 +45,7 @@ _SIGS = {
     "fbn_jt_plan_destroy": [_vp],
     "fbn_ci_dataset_upload": [_vp, C.c_int, _i64, _vp, C.c_int, _pp],
     "fbn_ci_dataset_from_device": [_vp, C.c_int, _i64, _vp, C.c_int, _pp],
+    "fbn_ci_set_kernel_timing": [_vp, C.c_int],
     "fbn_ci_run": [_vp, _vp, _i64, C.c_int, _dbl, _vp, _vp, _vp, _vp, _vp],
     "fbn_ci_counts": [_vp, C.c_int, C.c_int, _vp, C.c_int, _vp, _i64, _vp],
     "fbn_ci_last_kernel_ms": [_vp, _vp],
@@ -346,6 +347,10 @@ class IndependenceTest:
                                        C.byref(h))
         self._h = h
         return self
+
+    def set_kernel_timing(self, enable):
+        """HIP-event kernel timing of every CI launch (default on; off saves the events' cost)."""
+        lib.fbn_ci_set_kernel_timing(self._h, int(bool(enable)))
 
     def level(self, d, edges, e_begin, e_end, group_size=1):
         """One skeleton level for edges[e_begin:e_end] of the current skeleton (fbn_pc_level) ->

@@ -182,6 +182,7 @@ struct fbn_ci_ctx {
     CiSlot slot[2];
     hipStream_t stream = nullptr;  // the PC driver's rounds (pinned staging, one sync per round)
     float last_ms = 0.f;
+    bool timing = true;  // HIP events around every CI kernel (fbn_ci_set_kernel_timing)
     ~fbn_ci_ctx() {
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -871,6 +872,11 @@ static int CiCreate(const uint8_t *cols, bool cols_on_device, int nvars, int64_t
     *out = c.release();
     return FBN_OK;
 }
+int fbn_ci_set_kernel_timing(fbn_ci_ctx *c, int enable) {
+    if (!c) return SetError(FBN_ERR_ARG, "null pointer");
+    c->timing = enable != 0;
+    return FBN_OK;
+}
 int fbn_ci_dataset_upload(const uint8_t *cols, int nvars, int64_t nsamples, const int32_t *dims, int device,
                           fbn_ci_ctx **out) {
     return CiCreate(cols, false, nvars, nsamples, dims, device, out);
@@ -954,7 +960,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         // is derived, not read (ci_bits.hip)
         const int64_t skipped = d == 0 ? 2 : (pmode == 2 ? 3 : 0);
         S.last_bytes = (dim_rows - skipped * n) * c->bits_W * 4;
-        FBN_HIP(hipEventRecord(S.ev0, s));
+        if (c->timing) FBN_HIP(hipEventRecord(S.ev0, s));
         hipError_t e = fbn_ci_bits_launch(c->bits.as<uint32_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(),
                                           ditems, c->bits_W, n, d, alpha,
                                           want_g2p ? c->g2.as<double>() : nullptr, zc_df ? zc_df : S.df.as<int32_t>(),
@@ -964,7 +970,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
                                           c->browcnt.as<int32_t>(), c->pairtab.as<int32_t>(), pmode, c->nvars,
                                           c->num_cu, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci bits kernel launch: %s", hipGetErrorString(e));
-        FBN_HIP(hipEventRecord(S.ev1, s));
+        if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
         return FBN_OK;
     }
     size_t lds = 0;
@@ -996,7 +1002,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         gscratch = S.scratch.as<int32_t>();
     }
     S.last_bytes = n * c->N * (2 + d);  // uint8 columns x, y, z_1..z_d streamed once
-    FBN_HIP(hipEventRecord(S.ev0, s));
+    if (c->timing) FBN_HIP(hipEventRecord(S.ev0, s));
     hipError_t e = fbn_ci_launch(c->cols.as<uint8_t>(), c->ddims.as<int32_t>(),
                                  zc_items ? zc_items : S.items.as<int32_t>(), c->N, n, d, alpha,
                                  want_g2p ? c->g2.as<double>() : nullptr, zc_df ? zc_df : S.df.as<int32_t>(),
@@ -1004,7 +1010,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
                                  counts_dev, lds, grid,
                                  gscratch, c->stats.as<unsigned long long>(), s);
     if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci kernel launch: %s", hipGetErrorString(e));
-    FBN_HIP(hipEventRecord(S.ev1, s));
+    if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
     return FBN_OK;
 }
 
@@ -1021,7 +1027,8 @@ int fbn_ci_run(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alp
     if (df) FBN_HIP(hipMemcpyAsync(df, c->slot[0].df.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
     if (indep) FBN_HIP(hipMemcpyAsync(indep, c->slot[0].indep.p, (size_t)n, hipMemcpyDeviceToHost, s));
     FBN_HIP(hipStreamSynchronize(s));
-    FBN_HIP(hipEventElapsedTime(&c->last_ms, c->slot[0].ev0, c->slot[0].ev1));
+    c->last_ms = 0.f;
+    if (c->timing) FBN_HIP(hipEventElapsedTime(&c->last_ms, c->slot[0].ev0, c->slot[0].ev1));
     return FBN_OK;
 }
 
@@ -1306,7 +1313,7 @@ int CiBatchWait(fbn_ci_ctx *c, int k, uint8_t *indep, int32_t *df, PCResultHost 
         fprintf(stderr, "  ci batch slot %d n=%lld: wait %.1f us\n", k, (long long)n,
                 std::chrono::duration<double, std::micro>(t2 - t1).count());
     float ms = 0.f;
-    FBN_HIP(hipEventElapsedTime(&ms, S.ev0, S.ev1));
+    if (c->timing) FBN_HIP(hipEventElapsedTime(&ms, S.ev0, S.ev1));
     res.kernel_s += ms * 1e-3;
     res.device_bytes += S.last_bytes;
     S.n = 0;

@@ -154,6 +154,10 @@ int fbn_ci_dataset_upload(const uint8_t *cols, int nvars, int64_t nsamples, cons
  * Both entry points reject a code >= dims[v] (FBN_ERR_ARG). */
 int fbn_ci_dataset_from_device(const uint8_t *d_cols, int nvars, int64_t nsamples, const int32_t *dims,
                                int device, fbn_ci_ctx **out);
+/* Kernel-time accounting of a context (default on): HIP events around every CI kernel, summed into
+ * fbn_ci_last_kernel_ms / fbn_pc_timing's kernel time.  Off: no events (≈30 µs less per ALARM-5000
+ * PC-stable run; the reference's Timer measures wall time only), kernel times read 0. */
+int fbn_ci_set_kernel_timing(fbn_ci_ctx *c, int enable);
 /* n tests of one conditioning size d: items [n][2+d] = (x, y, z_0..z_{d-1}).  Outputs per test
  * (any may be NULL): G^2, adjusted df, p = 1 - pchisq(G^2, df), indep = (df == 0 || p > alpha).
  * ComputeGSquareXY / ComputeGSquareXYZ semantics (src/IndependenceTest.cpp:65-155,295-364).

@@ -226,3 +226,19 @@ def test_bit_sliced_marginal_tests_match_histogram_kernel(ns):
             r = od.ci_test(it[0], it[1], it[2:])
             assert df[k] == r["df"] and ind[k] == r["is_independent"]
             assert abs(g2[k] - r["g2"]) <= 1e-12 * max(1.0, abs(r["g2"]))
+
+
+def test_kernel_timing_switch(alarm_ds):
+    """fbn_ci_set_kernel_timing: events off -> identical results, kernel times read 0; back on."""
+    ci = F.IndependenceTest(alarm_ds)
+    a = F.PCStable(0.05, 1000).StructLearnCompData(ci)
+    assert a.kernel_s > 0
+    ci.set_kernel_timing(False)
+    b = F.PCStable(0.05, 1000).StructLearnCompData(ci)
+    assert b.kernel_s == 0 and b.edges == a.edges and b.sepset == a.sepset
+    assert b.tests_per_level.tolist() == a.tests_per_level.tolist()
+    ci.run(np.array([[0, 1]], np.int32), 0)
+    assert ci.last_kernel_ms() == 0
+    ci.set_kernel_timing(True)
+    ci.run(np.array([[0, 1]], np.int32), 0)
+    assert ci.last_kernel_ms() > 0
