@@ -891,7 +891,8 @@ int fbn_ci_dataset_from_device(const uint8_t *d_cols, int nvars, int64_t nsample
 // directly -- no staging copies for the small batches of a latency-bound driver round.
 static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alpha, bool want_g2p,
                           int32_t *counts_dev, hipStream_t s, int k = 0, const int32_t *zc_items = nullptr,
-                          uint8_t *zc_indep = nullptr, int32_t *zc_df = nullptr, const fbn::CiBatchStats *pre = nullptr) {
+                          uint8_t *zc_indep = nullptr, int32_t *zc_df = nullptr, const fbn::CiBatchStats *pre = nullptr,
+                          bool all_pairs = false) {
     CiSlot &S = c->slot[k];
     if (d < 0 || d > 8) return SetError(FBN_ERR_LIMIT, "conditioning set size %d (supported 0..8)", d);
     const int w = 2 + d;
@@ -937,7 +938,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
             c->bits_W = W;
             c->bits_ready = true;
         }
-        if ((rc = S.items.ensure((size_t)n * w * 4))) return rc;
+        if (!all_pairs && (rc = S.items.ensure((size_t)n * w * 4))) return rc;
         if ((rc = S.indep.ensure((size_t)n))) return rc;
         if ((rc = S.df.ensure((size_t)n * 4))) return rc;
         if ((rc = S.bcounts.ensure((size_t)n * 64 * 4))) return rc;
@@ -945,8 +946,10 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
             if ((rc = c->g2.ensure((size_t)n * 8))) return rc;
             if ((rc = c->p.ensure((size_t)n * 8))) return rc;
         }
-        if (!zc_items) FBN_HIP(hipMemcpyAsync(S.items.p, items, (size_t)n * w * 4, hipMemcpyHostToDevice, s));
-        const int32_t *ditems = zc_items ? zc_items : S.items.as<int32_t>();
+        if (!zc_items && !all_pairs)
+            FBN_HIP(hipMemcpyAsync(S.items.p, items, (size_t)n * w * 4, hipMemcpyHostToDevice, s));
+        // all pairs of the complete graph: the kernels decode test t into its pair (no item array)
+        const int32_t *ditems = all_pairs ? nullptr : zc_items ? zc_items : S.items.as<int32_t>();
         int pmode = 0;
         if (c->pair_mode == 1 && d == 0) {
             const size_t np = (size_t)c->nvars * (c->nvars - 1) / 2;
@@ -973,6 +976,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
         return FBN_OK;
     }
+    if (all_pairs) return SetError(FBN_ERR_ARG, "implicit pair batches need the bit-sliced path");
     size_t lds = 0;
     for (int64_t i = 0; i < n; ++i) {
         const int32_t *it = items + i * w;
@@ -1295,6 +1299,24 @@ int CiBatchLaunch(fbn_ci_ctx *c, int k, const int32_t *items, int64_t n, int d, 
         FBN_HIP(hipMemcpyAsync(h_ind, S.indep.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
         if (want_df) FBN_HIP(hipMemcpyAsync(h_df, S.df.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
     }
+    FBN_HIP(hipEventRecord(S.done, c->stream));
+    return FBN_OK;
+}
+bool CiAllPairsEligible(const fbn_ci_ctx *c, const CiBatchStats &st) {
+    return st.maxdim <= 4 && !getenv("FBN_CI_NO_BITS") && (c->N >= 4096 || getenv("FBN_CI_FORCE_BITS"));
+}
+int CiBatchLaunchAllPairs(fbn_ci_ctx *c, double alpha, const CiBatchStats *pre) {
+    CiSlot &S = c->slot[0];
+    const int64_t n = (int64_t)c->nvars * (c->nvars - 1) / 2;
+    S.n = n;
+    S.want_df = false;
+    S.zc = false;
+    if (n == 0) return FBN_OK;
+    int rc;
+    if ((rc = PinnedEnsure(S.h_res, S.h_res_bytes, (size_t)n * 5 + 8))) return rc;
+    rc = CiLaunchDevice(c, nullptr, n, 0, alpha, false, nullptr, c->stream, 0, nullptr, nullptr, nullptr, pre, true);
+    if (rc) return rc;
+    FBN_HIP(hipMemcpyAsync(S.h_res, S.indep.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
     FBN_HIP(hipEventRecord(S.done, c->stream));
     return FBN_OK;
 }

@@ -242,6 +242,19 @@ __device__ __forceinline__ void count_test_derived(const uint32_t *__restrict__ 
     }
 }
 
+// items == nullptr for a marginal batch: test t is the t-th pair (x < y) of the complete graph over
+// nv variables in lexicographic order (a PC run's level 0), decoded instead of read
+__device__ __forceinline__ void pair_of(long long t, int nv, int &x, int &y) {
+    const double b = 2.0 * nv - 1.0;
+    long long i = (long long)((b - sqrt(b * b - 8.0 * (double)t)) * 0.5);
+    auto off = [&](long long r) { return r * nv - r * (r + 1) / 2; };
+    if (i < 0) i = 0;
+    while (i > 0 && off(i) > t) --i;
+    while (i + 1 < nv && off(i + 1) <= t) ++i;
+    x = (int)i;
+    y = (int)(t - off(i) + i + 1);
+}
+
 constexpr int kBitsCells = 64;  // count slots per test
 
 // phase 1: counts[t][64] of every test, one wave per test; D = 0 (x, y) or 1 (x, y, z)
@@ -254,7 +267,9 @@ __global__ __launch_bounds__(256) void ci_bits_count(const uint32_t *__restrict_
     const int lane = threadIdx.x & 63;
     const long long wave = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
     for (long long t = wave; t < n; t += (long long)gridDim.x * 4) {
-        const int x = items[(2 + D) * t], y = items[(2 + D) * t + 1];
+        int x, y;
+        if (D == 0 && !items) pair_of(t, nvars, x, y);
+        else x = items[(2 + D) * t], y = items[(2 + D) * t + 1];
         const int dx = dims[x], dy = dims[y];
         const uint32_t *bx = bits + (size_t)row0[x] * W, *by = bits + (size_t)row0[y] * W;
         const uint32_t *bz = bx;
@@ -365,9 +380,13 @@ __global__ __launch_bounds__(256) void ci_bits_g2(const int32_t *__restrict__ co
                                                   const int32_t *__restrict__ items, long long n, double alpha,
                                                   double *__restrict__ g2o, int32_t *__restrict__ dfo,
                                                   double *__restrict__ po, uint8_t *__restrict__ indep,
-                                                  int32_t *__restrict__ counts0, unsigned long long *__restrict__ stats) {
+                                                  int32_t *__restrict__ counts0, unsigned long long *__restrict__ stats,
+                                                  int nvars) {
     for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t < n; t += (long long)gridDim.x * 256) {
-        const int dx = dims[items[(2 + D) * t]], dy = dims[items[(2 + D) * t + 1]];
+        int px, py;
+        if (D == 0 && !items) pair_of(t, nvars, px, py);
+        else px = items[(2 + D) * t], py = items[(2 + D) * t + 1];
+        const int dx = dims[px], dy = dims[py];
         const int dimz = D == 1 ? dims[items[3 * t + 2]] : 1;
         const int dxy = dx * dy;
         const int32_t *hz = counts + t * kBitsCells;
@@ -500,7 +519,7 @@ extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *di
         hipLaunchKernelGGL(ci_bits_count<0>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts, rowcnt,
                            pmode == 1 ? pairtab : nullptr, nvars);
         hipLaunchKernelGGL(ci_bits_g2<0>, b2, dim3(256), 0, s, counts, dims, items, n, alpha, g2, df, p, indep,
-                           counts0, stats);
+                           counts0, stats, nvars);
     } else if (d == 1) {
         if (pmode == 2)
             hipLaunchKernelGGL(ci_bits_count_derived, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts,
@@ -509,7 +528,7 @@ extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *di
             hipLaunchKernelGGL(ci_bits_count<1>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts, rowcnt,
                                nullptr, nvars);
         hipLaunchKernelGGL(ci_bits_g2<1>, b2, dim3(256), 0, s, counts, dims, items, n, alpha, g2, df, p, indep,
-                           counts0, stats);
+                           counts0, stats, nvars);
     } else {
         return hipErrorInvalidValue;
     }

@@ -134,7 +134,13 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
             const int a = dims[edges[e].first], b = dims[edges[e].second];
             st0.dim_rows += a + b, st0.maxdim = std::max(st0.maxdim, std::max(a, b));
         }
-        int rc = CiBatchLaunch(ctx, 0, pairs, (int64_t)E, 0, alpha, false, &st0);
+        int nv = 0;
+        int64_t ns = 0;
+        CiCtxShape(ctx, &nv, &ns);
+        const bool all_pairs = e_begin == 0 && e_end == edges.size() && (int64_t)E == (int64_t)nv * (nv - 1) / 2 &&
+                               CiAllPairsEligible(ctx, st0) && !getenv("FBN_CI_NO_IMPLICIT");
+        int rc = all_pairs ? CiBatchLaunchAllPairs(ctx, alpha, &st0)
+                           : CiBatchLaunch(ctx, 0, pairs, (int64_t)E, 0, alpha, false, &st0);
         if (rc) return rc;
         rc = CiBatchWait(ctx, 0, indep.data(), nullptr, res);
         if (rc) return rc;

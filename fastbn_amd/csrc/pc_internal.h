@@ -154,6 +154,11 @@ struct CiBatchStats {
 int CiBatchLaunch(fbn_ci_ctx *c, int k, const int32_t *items, int64_t n, int d, double alpha, bool want_df,
                   const CiBatchStats *pre = nullptr);
 const int32_t *CiCtxDims(const fbn_ci_ctx *c);  // state count per variable
+// all nvars(nvars-1)/2 marginal tests of the complete graph (lexicographic pairs) as one batch in
+// slot 0 with no item array (the kernels decode the pair); only when eligible for the bit-sliced
+// path (st = the batch's statistics)
+bool CiAllPairsEligible(const fbn_ci_ctx *c, const CiBatchStats &st);
+int CiBatchLaunchAllPairs(fbn_ci_ctx *c, double alpha, const CiBatchStats *pre);
 // pair tables of the bit-sliced path: 1 = the next marginal batch records every pair's table (it
 // must test all pairs i < j: a PC run's level 0), 2 = one-conditioning-variable batches derive the
 // last value of x, y and z from them, 0 = off (also drops what was recorded)
