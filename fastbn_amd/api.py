@@ -31,6 +31,8 @@ _SIGS = {
     "fbn_jt_plan_dump": [_vp, _cstr, _cstr],
     "fbn_jt_run": [_vp, _vp, _i64, _vp, _vp, _vp],
     "fbn_jt_run_device": [_vp, _vp, _i64, _vp, _vp, _vp],
+    "fbn_jt_evidence_validate": [_vp, _vp, _i64, _vp],
+    "fbn_jt_set_evidence_check": [_vp, C.c_int],
     "fbn_jt_score": [_vp, _vp, _vp, _i64, _vp, _vp],
     "fbn_jt_last_kernel_ms": [_vp, _vp],
     "fbn_jt_stream_schedule": [_vp, _vp, C.c_int64, _vp, C.c_int64, _vp, _vp],
@@ -290,7 +292,18 @@ class JunctionTree:
         return labels, marg
 
     def run_device(self, d_evidence_ptr, ncases, d_labels_ptr, d_marg_ptr, stream_ptr=None):
+        """Device-resident run (asynchronous on the stream unless the evidence check is on)."""
         lib.fbn_jt_run_device(self._h, d_evidence_ptr, ncases, d_labels_ptr, d_marg_ptr, stream_ptr)
+
+    def validate_device(self, d_evidence_ptr, ncases, stream_ptr=None):
+        """Device-side evidence range check of a device buffer; raises FastBNError if a code is out
+        of its node's domain."""
+        lib.fbn_jt_evidence_validate(self._h, d_evidence_ptr, ncases, stream_ptr)
+
+    def set_evidence_check(self, enable):
+        """run_device's per-call evidence check (default on); off = fully asynchronous runs of a
+        buffer the caller validated (validate_device)."""
+        lib.fbn_jt_set_evidence_check(self._h, int(bool(enable)))
 
     def decision_margin(self, reset=False):
         """(min |p - alpha|, #tests with |p - alpha| < 1e-9) over the tests run since the last reset."""

@@ -134,7 +134,8 @@ struct fbn_jt_plan {
     bool prof_on = false;
     int last_grid = 0;
     DevBuf evid, labels, marg, ws;
-    DevBuf ddom, evcheck;  // fbn_jt_run's device-side evidence range check
+    DevBuf ddom, evcheck;  // device-side evidence range check (fbn_jt_run, fbn_jt_run_device)
+    bool ev_check = true;  // fbn_jt_set_evidence_check
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     ~fbn_jt_plan() {
@@ -613,13 +614,63 @@ static int LaunchLds(fbn_jt_plan *p, DevBuf &ws, const int8_t *d_evidence, int64
     return FBN_OK;
 }
 
+// out-of-domain evidence has no reference meaning (a code >= the node's state count would shift
+// bits into the neighbouring digit fields of the kernels' evidence masks): checked on the device
+// before any kernel indexes with it; one stream sync (the host loop cost ~1 ns per value)
+static int JtCheckEvidence(fbn_jt_plan *p, const int8_t *d_ev, int64_t ncases, hipStream_t s) {
+    const int V = p->host.num_nodes;
+    int rc;
+    if (!p->ddom.p) {
+        if ((rc = p->ddom.ensure((size_t)V * 4))) return rc;
+        if ((rc = p->evcheck.ensure(8))) return rc;
+        FBN_HIP(hipMemcpy(p->ddom.p, p->host.dom.data(), (size_t)V * 4, hipMemcpyHostToDevice));
+    }
+    FBN_HIP(hipMemsetAsync(p->evcheck.p, 0xFF, 8, s));
+    hipError_t e = fbn_jt_evidence_check(d_ev, (long long)ncases * V, V, p->ddom.as<int32_t>(),
+                                         p->evcheck.as<unsigned long long>(), s);
+    if (e != hipSuccess) return SetError(FBN_ERR_HIP, "evidence check: %s", hipGetErrorString(e));
+    unsigned long long first = 0;
+    FBN_HIP(hipMemcpyAsync(&first, p->evcheck.p, 8, hipMemcpyDeviceToHost, s));
+    FBN_HIP(hipStreamSynchronize(s));
+    if (first == ~0ull) return FBN_OK;
+    int8_t code = 0;
+    FBN_HIP(hipMemcpy(&code, d_ev + first, 1, hipMemcpyDeviceToHost));
+    const long long c = (long long)(first / V);
+    const int v = (int)(first % V);
+    return SetError(FBN_ERR_ARG, "case %lld: evidence %d for node %d (domain %d)", c, (int)code, v, p->host.dom[v]);
+}
+
+int fbn_jt_evidence_validate(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, void *hip_stream) {
+    if (!p || (!d_evidence && ncases > 0) || ncases < 0) return SetError(FBN_ERR_ARG, "bad argument");
+    if (ncases == 0) return FBN_OK;
+    if (p->device < 0) return SetError(FBN_ERR_NODEV, "host-only plan (created with device < 0)");
+    FBN_HIP(hipSetDevice(p->device));
+    return JtCheckEvidence(p, d_evidence, ncases, static_cast<hipStream_t>(hip_stream));
+}
+
+int fbn_jt_set_evidence_check(fbn_jt_plan *p, int enable) {
+    if (!p) return SetError(FBN_ERR_ARG, "null pointer");
+    p->ev_check = enable != 0;
+    return FBN_OK;
+}
+
+static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, int32_t *d_labels,
+                       double *d_marginals, hipStream_t s, bool check);
+
 int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, int32_t *d_labels,
                       double *d_marginals, void *hip_stream) {
     if (!p || (!d_evidence && ncases > 0) || ncases < 0) return SetError(FBN_ERR_ARG, "bad argument");
     if (ncases == 0) return FBN_OK;
     if (p->device < 0) return SetError(FBN_ERR_NODEV, "host-only plan (created with device < 0)");
     FBN_HIP(hipSetDevice(p->device));
-    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    return JtRunDevice(p, d_evidence, ncases, d_labels, d_marginals, static_cast<hipStream_t>(hip_stream),
+                       p->ev_check);
+}
+
+static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, int32_t *d_labels,
+                       double *d_marginals, hipStream_t s, bool check) {
+    if (check)
+        if (int rc = JtCheckEvidence(p, d_evidence, ncases, s)) return rc;
     const auto &g = p->prog;
     const int V = p->host.num_nodes, SD = g.sum_dom, nc = g.num_cliques;
     const int64_t nblk = (ncases + 63) / 64;
@@ -746,29 +797,7 @@ int fbn_jt_run(fbn_jt_plan *p, const int8_t *evidence, int64_t ncases, int32_t *
     if ((rc = p->labels.ensure((size_t)ncases * 4))) return rc;
     if ((rc = p->marg.ensure((size_t)ncases * SD * 8))) return rc;
     FBN_HIP(hipMemcpyAsync(p->evid.p, evidence, (size_t)ncases * V, hipMemcpyHostToDevice, s));
-    // out-of-domain evidence has no reference meaning: checked on the device (the host loop cost
-    // ~1 ns per value) before any kernel indexes with it
-    if (!p->ddom.p) {
-        if ((rc = p->ddom.ensure((size_t)V * 4))) return rc;
-        if ((rc = p->evcheck.ensure(8))) return rc;
-        FBN_HIP(hipMemcpy(p->ddom.p, p->host.dom.data(), (size_t)V * 4, hipMemcpyHostToDevice));
-    }
-    {
-        FBN_HIP(hipMemsetAsync(p->evcheck.p, 0xFF, 8, s));
-        hipError_t e = fbn_jt_evidence_check(p->evid.as<int8_t>(), (long long)ncases * V, V, p->ddom.as<int32_t>(),
-                                             p->evcheck.as<unsigned long long>(), s);
-        if (e != hipSuccess) return SetError(FBN_ERR_HIP, "evidence check: %s", hipGetErrorString(e));
-        unsigned long long first = 0;
-        FBN_HIP(hipMemcpyAsync(&first, p->evcheck.p, 8, hipMemcpyDeviceToHost, s));
-        FBN_HIP(hipStreamSynchronize(s));
-        if (first != ~0ull) {
-            const long long c = (long long)(first / V);
-            const int v = (int)(first % V);
-            return SetError(FBN_ERR_ARG, "case %lld: evidence %d for node %d (domain %d)", c, (int)evidence[first], v,
-                            p->host.dom[v]);
-        }
-    }
-    rc = fbn_jt_run_device(p, p->evid.as<int8_t>(), ncases, p->labels.as<int32_t>(), p->marg.as<double>(), s);
+    rc = JtRunDevice(p, p->evid.as<int8_t>(), ncases, p->labels.as<int32_t>(), p->marg.as<double>(), s, true);
     if (rc) return rc;
     FBN_HIP(hipMemcpyAsync(labels_out, p->labels.p, (size_t)ncases * 4, hipMemcpyDeviceToHost, s));
     if (marginals_out)

@@ -11,11 +11,14 @@
 // adds z's masks: N[c][a][b] = sum popcount(x_a & y_b & z_c) (Counts3D, src/CellTable.cpp:226-291).
 //
 // Phase 2 evaluates marginals, the adjusted df and G^2 with one lane per test (no idle lanes in
-// the log / incomplete-gamma code), in the reference's operation order: ComputeGSquareXY,
+// the log / incomplete-gamma code), in the reference's operation order (one running G^2 sum):
+// ComputeGSquareXY,
 // src/IndependenceTest.cpp:295-364 (same arithmetic as ci_kernels.hip, so the two kernels agree
 // bit for bit).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include "ci_chisq.h"
 
 namespace {
 
@@ -341,40 +344,9 @@ __global__ __launch_bounds__(256) void ci_bits_count_derived(const uint32_t *__r
     }
 }
 
-// regularized upper incomplete gamma: the same function as ci_kernels.hip's gamma_q
-__device__ double gamma_q_b(double a, double x) {
-    if (x <= 0.0) return 1.0;
-    const double lg = lgamma(a);
-    if (x < a + 1.0) {
-        double ap = a, sum = 1.0 / a, del = sum;
-        for (int n = 0; n < 2000; ++n) {
-            ap += 1.0;
-            del *= x / ap;
-            sum += del;
-            if (fabs(del) < fabs(sum) * 1e-17) break;
-        }
-        return 1.0 - sum * exp(-x + a * log(x) - lg);
-    }
-    const double tiny = 1e-300;
-    double b = x + 1.0 - a, c = 1.0 / tiny, d = 1.0 / b, h = d;
-    for (int i = 1; i < 2000; ++i) {
-        const double an = -i * (i - a);
-        b += 2.0;
-        d = an * d + b;
-        if (fabs(d) < tiny) d = tiny;
-        c = b + an / c;
-        if (fabs(c) < tiny) c = tiny;
-        d = 1.0 / d;
-        const double del = d * c;
-        h *= del;
-        if (fabs(del - 1.0) < 1e-17) break;
-    }
-    return exp(-x + a * log(x) - lg) * h;
-}
-
-// phase 2: one lane per test -- per z: marginals, adjusted df, G^2 terms in the reference's
-// i -> j order; then the sums over z in z order (ComputeGSquareXY / XYZ, src/IndependenceTest.cpp:
-// 65-155, 295-364; the same arithmetic as ci_g2_kernel), p = Q(df/2, G^2/2)
+// phase 2: one lane per test -- per z: marginals, adjusted df; G^2 as one running sum in the
+// reference's z -> x -> y order (ComputeGSquareXY / XYZ, src/IndependenceTest.cpp:65-155,
+// 295-364; the same arithmetic as ci_g2_kernel), p = 1 - P(df/2, G^2/2) (ci_chisq.h)
 template <int D>
 __global__ __launch_bounds__(256) void ci_bits_g2(const int32_t *__restrict__ counts, const int32_t *__restrict__ dims,
                                                   const int32_t *__restrict__ items, long long n, double alpha,
@@ -390,6 +362,7 @@ __global__ __launch_bounds__(256) void ci_bits_g2(const int32_t *__restrict__ co
         const int dimz = D == 1 ? dims[items[3 * t + 2]] : 1;
         const int dxy = dx * dy;
         const int32_t *hz = counts + t * kBitsCells;
+        // one running sum over z -> x -> y, exactly the reference's loop (no per-z partials)
         double g2 = 0.0;
         int df = 0;
         for (int k = 0; k < dimz; ++k) {
@@ -413,7 +386,6 @@ __global__ __launch_bounds__(256) void ci_bits_g2(const int32_t *__restrict__ co
             alx = alx >= 1 ? alx : 1;
             aly = aly >= 1 ? aly : 1;
             df += (alx - 1) * (aly - 1);
-            double g = 0.0;
             if (total != 0) {
                 for (int i = 0; i < dx; ++i) {
                     const long sum_row = ni[i];
@@ -423,11 +395,10 @@ __global__ __launch_bounds__(256) void ci_bits_g2(const int32_t *__restrict__ co
                         const long observed = h[i * dy + j];
                         if (sum_col == 0 || observed == 0) continue;
                         const double expected = (double)sum_col * (double)sum_row / (double)total;
-                        g += 2.0 * observed * log(observed / expected);
+                        g2 += 2.0 * observed * log(observed / expected);
                     }
                 }
             }
-            g2 += g;
         }
         double p;
         bool ind;
@@ -435,7 +406,7 @@ __global__ __launch_bounds__(256) void ci_bits_g2(const int32_t *__restrict__ co
             p = 1.0;
             ind = true;
         } else {
-            p = gamma_q_b(0.5 * df, 0.5 * g2);
+            p = fbn_chisq_pvalue(g2, df);
             ind = p > alpha;
         }
         if (g2o) g2o[t] = g2;

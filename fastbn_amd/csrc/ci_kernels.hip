@@ -5,16 +5,25 @@
 // cells are counted in per-lane packed 16-bit counters held in registers (4 x u64, no LDS traffic
 // in the sample loop) and wave-reduced once per test; larger tables N[z][x][y] use per-wave LDS
 // sub-histograms (LDS atomics without cross-wave contention), merged once per test.  Marginals, the
-// adjusted degrees of freedom and the G^2 terms are then evaluated per z-configuration by
-// parallel threads, summed in z order, and one lane evaluates p = Q(df/2, G^2/2).
+// adjusted degrees of freedom and the G^2 terms (one per cell: the logs) are then evaluated by
+// parallel threads; one lane adds the terms in cell order -- the reference's single running sum
+// over z -> x -> y -- and evaluates p = 1 - P(df/2, G^2/2) (ci_chisq.h).
 //
 // Reference: Counts2D/Counts3D (src/CellTable.cpp:23-91,226-291,430-455) and
-// ComputeGSquareXY/XYZ (src/IndependenceTest.cpp:65-155,295-364).  Counts and df are exact;
-// G^2 is summed per z then across z (vs one running sum in the reference): <= a few ulp apart.
+// ComputeGSquareXY/XYZ (src/IndependenceTest.cpp:65-155,295-364).  Counts and df are exact; G^2
+// is the reference's sum of the same terms in the same order (skipped cells contribute +0.0,
+// which leaves a running sum unchanged).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
+#include "ci_chisq.h"
+
 namespace {
+
+// G^2 terms buffered per chunk of cells (LDS doubles) before the in-order sum
+constexpr int kTermChunk = 1024;
 
 struct CiArgs {
     const uint8_t *cols;  // [nvars][N]
@@ -34,38 +43,6 @@ struct CiArgs {
     // (non-negative doubles order like their bit patterns), [1] = #tests with |p - alpha| < 1e-9
     unsigned long long *stats;
 };
-
-// regularized upper incomplete gamma Q(a, x): series / modified Lentz continued fraction; the
-// same algorithm as the oracle restatement of stats::pchisq (oracle/pc_oracle.cpp)
-__device__ double gamma_q(double a, double x) {
-    if (x <= 0.0) return 1.0;
-    const double lg = lgamma(a);
-    if (x < a + 1.0) {
-        double ap = a, sum = 1.0 / a, del = sum;
-        for (int n = 0; n < 2000; ++n) {
-            ap += 1.0;
-            del *= x / ap;
-            sum += del;
-            if (fabs(del) < fabs(sum) * 1e-17) break;
-        }
-        return 1.0 - sum * exp(-x + a * log(x) - lg);
-    }
-    const double tiny = 1e-300;
-    double b = x + 1.0 - a, c = 1.0 / tiny, d = 1.0 / b, h = d;
-    for (int i = 1; i < 2000; ++i) {
-        const double an = -i * (i - a);
-        b += 2.0;
-        d = an * d + b;
-        if (fabs(d) < tiny) d = tiny;
-        c = b + an / c;
-        if (fabs(c) < tiny) c = tiny;
-        d = 1.0 / d;
-        const double del = d * c;
-        h *= del;
-        if (fabs(del - 1.0) < 1e-17) break;
-    }
-    return exp(-x + a * log(x) - lg) * h;
-}
 
 template <int D>
 __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
@@ -91,15 +68,17 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
         // in the sample loop; larger tables: per-wave LDS sub-histograms (no cross-wave contention)
         const bool packed = cells <= 16 && A.N <= (1ll << 24);
         const int nsub = (cells > 16 && cells * 16 <= 64 * 1024) ? 4 : 1;  // = fbn_ci_lds_bytes
-        // LDS layout (ints): hist[cells] | sub[nsub][cells] | ni | nj | nk | dfp | (even) part[dimz] f64
+        // LDS layout (ints): hist[cells] | sub[nsub][cells] | ni | nj | nk | dfp | (even) term[tc] f64
+        // (tc = min(cells, kTermChunk): the G^2 terms of one chunk of cells)
+        const int tc = cells < kTermChunk ? cells : kTermChunk;
         int32_t *hist = smem;
         int32_t *sub = hist + ((cells + 3) & ~3);
         int32_t *ni = sub + (nsub > 1 ? nsub * cells : 0);
         int32_t *nj = ni + dimz * dx;
         int32_t *nk = nj + dimz * dy;
         int32_t *dfp = nk + dimz;
-        const int part_off = (int)((dfp + dimz) - smem + 1) & ~1;
-        double *part = reinterpret_cast<double *>(smem + part_off);
+        const int term_off = (int)((dfp + dimz) - smem + 1) & ~1;
+        double *term = reinterpret_cast<double *>(smem + term_off);
 
         for (int c = tid; c < cells; c += 256) hist[c] = 0;
         if (nsub > 1)
@@ -191,43 +170,47 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
             nj[r] = s;
         }
         __syncthreads();
-        // per z: adjusted df and G^2 terms in the reference's i -> j order
+        // N_{++z} and the adjusted df per z (src/IndependenceTest.cpp:96-112)
         for (int k = tid; k < dimz; k += 256) {
-            int alx = 0, aly = 0;
-            long total = 0;
+            int alx = 0, aly = 0, total = 0;
             for (int i = 0; i < dx; ++i) alx += ni[k * dx + i] > 0, total += ni[k * dx + i];
             for (int j = 0; j < dy; ++j) aly += nj[k * dy + j] > 0;
             alx = alx >= 1 ? alx : 1;
             aly = aly >= 1 ? aly : 1;
             dfp[k] = (alx - 1) * (aly - 1);
-            double g = 0.0;
-            if (total != 0) {
-                for (int i = 0; i < dx; ++i) {
-                    const long sum_row = ni[k * dx + i];
-                    if (sum_row == 0) continue;
-                    for (int j = 0; j < dy; ++j) {
-                        const long sum_col = nj[k * dy + j];
-                        const long observed = hist[k * dxy + i * dy + j];
-                        if (sum_col == 0 || observed == 0) continue;
-                        const double expected = (double)sum_col * (double)sum_row / (double)total;
-                        g += 2.0 * observed * log(observed / expected);
-                    }
-                }
-            }
-            part[k] = g;
+            nk[k] = total;
         }
         __syncthreads();
+        // G^2: the terms of a chunk of cells in parallel (cell c = (k * dx + i) * dy + j, the
+        // reference's loop order), then one lane adds them in order (src/IndependenceTest.cpp:112-137)
+        double g2 = 0.0;
+        for (int c0 = 0; c0 < cells; c0 += tc) {
+            const int c1 = c0 + tc < cells ? c0 + tc : cells;
+            for (int c = c0 + tid; c < c1; c += 256) {
+                const int k = c / dxy, i = (c / dy) % dx, j = c % dy;
+                const long total = nk[k], sum_row = ni[k * dx + i], sum_col = nj[k * dy + j], observed = hist[c];
+                double t = 0.0;
+                if (total != 0 && sum_row != 0 && sum_col != 0 && observed != 0) {
+                    const double expected = (double)sum_col * (double)sum_row / (double)total;
+                    t = 2.0 * observed * log(observed / expected);
+                }
+                term[c - c0] = t;
+            }
+            __syncthreads();
+            if (tid == 0)
+                for (int c = 0; c < c1 - c0; ++c) g2 += term[c];
+            __syncthreads();
+        }
         if (tid == 0) {
-            double g2 = 0.0;
             int df = 0;
-            for (int k = 0; k < dimz; ++k) g2 += part[k], df += dfp[k];
+            for (int k = 0; k < dimz; ++k) df += dfp[k];
             double p;
             bool ind;
-            if (df == 0) {  // src/IndependenceTest.cpp:149-151, 349-351
+            if (df == 0) {  // src/IndependenceTest.cpp:140-142, 349-351
                 p = 1.0;
                 ind = true;
             } else {
-                p = gamma_q(0.5 * df, 0.5 * g2);
+                p = fbn_chisq_pvalue(g2, df);
                 ind = p > A.alpha;
             }
             if (A.g2) A.g2[it] = g2;
@@ -253,7 +236,7 @@ extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy) {
     const size_t nsub = (cells > 16 && cells * 16 <= 64 * 1024) ? 4 : 0;
     size_t ints = ((cells + 3) & ~(size_t)3) + nsub * cells + (size_t)dimz * (dx + dy + 2);
     ints = (ints + 1) & ~(size_t)1;
-    return ints * 4 + (size_t)dimz * 8;
+    return ints * 4 + std::min<size_t>(cells, kTermChunk) * 8;
 }
 
 extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, const int32_t *items, long long N,

@@ -104,9 +104,20 @@ int fbn_jt_stream_schedule(const fbn_jt_plan *p, int32_t *order, int64_t order_c
  * Copies in/out over PCIe; synchronous. */
 int fbn_jt_run(fbn_jt_plan *p, const int8_t *evidence, int64_t ncases, int32_t *labels_out,
                double *marginals_out, void *hip_stream);
-/* Same with device-resident buffers (inputs already in HBM); asynchronous on hip_stream. */
+/* Same with device-resident buffers (inputs already in HBM); asynchronous on hip_stream.  Every
+ * evidence code must be -1 or < the node's state count: by default the call checks that on the
+ * device first (one stream sync) and returns FBN_ERR_ARG naming the first bad case/node; see
+ * fbn_jt_set_evidence_check. */
 int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, int32_t *d_labels,
                       double *d_marginals, void *hip_stream);
+/* The device-side evidence check alone (synchronous on hip_stream): FBN_ERR_ARG on the first
+ * out-of-domain code.  For callers that validate a buffer once and run it many times. */
+int fbn_jt_evidence_validate(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, void *hip_stream);
+/* enable = 0: fbn_jt_run_device skips its check (fully asynchronous); the caller guarantees valid
+ * evidence (e.g. fbn_jt_evidence_validate once per buffer).  An unchecked out-of-domain code gives
+ * unspecified marginals and labels for its case (never an out-of-bounds access).  Default 1.
+ * fbn_jt_run always checks. */
+int fbn_jt_set_evidence_check(fbn_jt_plan *p, int enable);
 /* Per-case MSE and Hellinger distance vs a golden table (CalculateMSE / CalculateHellingerDistance
  * with Round(.,7), src/Inference.cpp:153-206); golden [ncases][sum_dom], evidence nodes marked by
  * golden[.][first state] <= 0.  Host arrays; sums accumulated in case order. */

@@ -8,10 +8,11 @@
 
 namespace oracle {
 
-// Regularized upper incomplete gamma Q(a, x); P = 1 - Q.  Series for x < a + 1, modified Lentz
-// continued fraction otherwise -- converged to full double precision.
-static double GammaQ(double a, double x) {
-    if (x <= 0) return 1.0;
+// Regularized lower incomplete gamma P(a, x): series for x < a + 1, modified Lentz continued
+// fraction for Q = 1 - P otherwise -- converged to full double precision.  stats::pchisq (the
+// reference's p-value, src/IndependenceTest.cpp:146,268,355) is un-vendored: parity unpinned.
+static double GammaP(double a, double x) {
+    if (x <= 0) return 0.0;
     double lg = std::lgamma(a);
     if (x < a + 1.0) {
         double ap = a, sum = 1.0 / a, del = sum;
@@ -21,8 +22,7 @@ static double GammaQ(double a, double x) {
             sum += del;
             if (std::fabs(del) < std::fabs(sum) * 1e-17) break;
         }
-        double P = sum * std::exp(-x + a * std::log(x) - lg);
-        return 1.0 - P;
+        return sum * std::exp(-x + a * std::log(x) - lg);
     }
     const double tiny = 1e-300;
     double b = x + 1.0 - a, c = 1.0 / tiny, d = 1.0 / b, h = d;
@@ -38,10 +38,11 @@ static double GammaQ(double a, double x) {
         h *= del;
         if (std::fabs(del - 1.0) < 1e-17) break;
     }
-    return std::exp(-x + a * std::log(x) - lg) * h;
+    return 1.0 - std::exp(-x + a * std::log(x) - lg) * h;
 }
 
-double ChiSquarePValue(double g2, int df) { return GammaQ(0.5 * df, 0.5 * g2); }
+// p = 1.0 - pchisq(g2, df), formed as the reference forms it (a CDF that rounds to 1 gives 0)
+double ChiSquarePValue(double g2, int df) { return 1.0 - GammaP(0.5 * df, 0.5 * g2); }
 
 CIResult CITest(const CodedDataset &ds, int x, int y, const int *z, int d, double alpha,
                 std::vector<int> *counts_out) {

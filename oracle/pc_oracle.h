@@ -3,8 +3,9 @@
 // src/CellTable.cpp).  Used only as the parity checker and as bench.py's cpu_baseline "port".
 //
 // The p-value goes through stats::pchisq (third-party submodule lib/stats + lib/gcem, pinned
-// commit unknown and absent from the snapshot, `.gitmodules:10-15`).  It is restated here as the
-// regularized upper incomplete gamma Q(df/2, G^2/2) (series / Lentz continued fraction).  No
+// commit unknown and absent from the snapshot, `.gitmodules:10-15`).  It is restated here as
+// p = 1 - P(df/2, G^2/2), P the regularized lower incomplete gamma (series / Lentz continued
+// fraction), formed as the reference forms it (1.0 - pchisq).  No
 // reference test pins values at this boundary: p-values are "parity unpinned"; the counts are
 // pinned by the reference's own Counts2D/Counts3D (tests/golden/alarm_s5000.ci).
 #ifndef FBN_ORACLE_PC_H

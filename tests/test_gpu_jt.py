@@ -202,3 +202,35 @@ def test_bad_evidence_rejected(jt):
     ev[299, 0] = -1
     lab, _ = jt.infer(ev)  # the plan stays usable after a rejected batch
     assert lab.shape == (300,)
+
+
+def test_bad_evidence_rejected_on_device_path(jt, ojt):
+    """fbn_jt_run_device checks a device buffer's codes by default (FBN_ERR_ARG naming the first bad
+    case/node); fbn_jt_evidence_validate is the check alone; with the check off the run is
+    asynchronous and a valid buffer gives the oracle's results."""
+    torch = pytest.importorskip("torch")
+    from fastbn_amd import synth
+    n = 512
+    ev = synth.evidence_cases(synth.read_xmlbif(os.path.join(GOLD, "alarm", "alarm.xml")), n, 7, seed=11)
+    bad = ev.copy()
+    bad[300, 12] = 5  # node 12 has fewer states
+    bad[400, 3] = -3
+    d_bad = torch.from_numpy(bad).to("cuda")
+    d_lab = torch.zeros(n, dtype=torch.int32, device="cuda")
+    d_marg = torch.zeros((n, jt.info["sum_dom"]), dtype=torch.float64, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    with pytest.raises(F.FastBNError, match="case 300: evidence 5 for node 12"):
+        jt.run_device(d_bad.data_ptr(), n, d_lab.data_ptr(), d_marg.data_ptr(), stream)
+    with pytest.raises(F.FastBNError, match="case 300: evidence 5 for node 12"):
+        jt.validate_device(d_bad.data_ptr(), n, stream)
+    d_ev = torch.from_numpy(ev).to("cuda")
+    jt.validate_device(d_ev.data_ptr(), n, stream)
+    jt.set_evidence_check(False)
+    try:
+        jt.run_device(d_ev.data_ptr(), n, d_lab.data_ptr(), d_marg.data_ptr(), stream)
+        torch.cuda.synchronize()
+    finally:
+        jt.set_evidence_check(True)
+    olab, omarg = ojt.infer(ev)
+    np.testing.assert_array_equal(d_lab.cpu().numpy(), olab)
+    np.testing.assert_array_equal(d_marg.cpu().numpy(), omarg)
