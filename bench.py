@@ -109,14 +109,9 @@ def bench_pc(steps, warmup):
 
 
 def synth_c5(nvars=1000, nsamples=100_000):
-    """SURVEY §8(d) config 5 dataset: node i draws k ~ U{0..2} parents from the previous 50,
-    domains U{2..4}, Dirichlet(1) CPTs, forward sampling, seed 1000."""
+    """SURVEY §8(d) config 5 dataset (fastbn_amd.synth.config5_dataset)."""
     from fastbn_amd import synth
-    with tempfile.TemporaryDirectory() as td:
-        path = os.path.join(td, "pc_c5.xml")
-        synth.random_network(nvars, seed=1000, window=50, parent_probs=(1, 1, 1), dom=(2, 4), path=path, k_min=0)
-        cols = synth.forward_sample(synth.read_xmlbif(path), nsamples, seed=1000)
-    return cols, (cols.max(axis=1).astype(np.int32) + 1)
+    return synth.config5_dataset(nvars, nsamples)
 
 
 def bench_pc_synth(steps, depth=6, cpu_vars=120):

@@ -140,3 +140,16 @@ def random_network(n_nodes, seed, window=12, parent_probs=(0.8, 0.15, 0.05), dom
                 f.write("<TABLE>%s </TABLE>\n</PROBABILITY>\n" % " ".join("%.4f" % x for x in vals))
             f.write("</NETWORK>\n</BIF>\n")
     return dims, parents, cpts
+
+
+def config5_dataset(nvars=1000, nsamples=100_000, seed=1000):
+    """SURVEY §8(d) config 5 dataset: node i draws k ~ U{0..2} parents from the previous 50,
+    domains U{2..4}, Dirichlet(1) CPTs (4 decimals, XMLBIF round trip), forward sampling, seed 1000.
+    Returns (uint8 columns [nvars][nsamples], dims = observed state counts)."""
+    import os
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "pc_c5.xml")
+        random_network(nvars, seed=seed, window=50, parent_probs=(1, 1, 1), dom=(2, 4), path=path, k_min=0)
+        cols = forward_sample(read_xmlbif(path), nsamples, seed=seed)
+    return cols, (cols.max(axis=1).astype(np.int32) + 1)

@@ -81,6 +81,19 @@ def read_ci_fixture(path):
     return dims, colhash, tests
 
 
+def pc_digest(edges, sepset):
+    """Digests of a PC-stable skeleton: the edge list in vec_edges order and the sepsets as
+    (x, y, |Z|, Z...) records in ascending key order (int32), sha256 hex."""
+    import hashlib
+    e = np.asarray(edges, np.int32).reshape(-1, 2)
+    rec = []
+    for k in sorted(sepset):
+        z = sorted(sepset[k])
+        rec += [k[0], k[1], len(z)] + list(z)
+    return {"edges_sha256": hashlib.sha256(e.tobytes()).hexdigest(),
+            "sepsets_sha256": hashlib.sha256(np.asarray(rec, np.int32).tobytes()).hexdigest()}
+
+
 def fnv1a(col):
     h = 1469598103934665603
     for v in col.tolist():
@@ -102,3 +115,49 @@ def have_gpu():
         return fastbn_amd.device_count() > 0
     except Exception:
         return False
+
+
+MUNIN = os.path.join(GOLD, "munin_like")
+
+
+@pytest.fixture(scope="session")
+def munin_fixture(tmp_path_factory):
+    """BASELINE config 4 fixture (tests/golden/make_golden_synth.py): the seeded Munin-like XMLBIF,
+    32 evidence cases and the reference's own labels / marginals / plan for them."""
+    d = tmp_path_factory.mktemp("munin_like")
+    xml = str(d / "munin_like.xml")
+    with gzip.open(os.path.join(MUNIN, "munin_like.xml.gz"), "rb") as f, open(xml, "wb") as g:
+        g.write(f.read())
+    lib = str(d / "ev.libsvm")
+    with gzip.open(os.path.join(MUNIN, "ev.libsvm.gz"), "rb") as f, open(lib, "wb") as g:
+        g.write(f.read())
+    plan = str(d / "ref.plan")
+    with gzip.open(os.path.join(MUNIN, "ref.plan.gz"), "rb") as f, open(plan, "wb") as g:
+        g.write(f.read())
+    return {"xml": xml, "libsvm": lib, "plan": plan, "marg": os.path.join(MUNIN, "ref.marg.gz")}
+
+
+def parse_plan(path):
+    """A plan dump (fbn_jt_plan_dump / the reference harness) -> cliques {id: (vars, up, down)},
+    separators {id: (vars, up, down)}, root, levels."""
+    C, S, root, levels = {}, {}, None, []
+    for ln in open(path):
+        t = ln.split()
+        if t and t[0] in ("c", "s"):
+            i, nv = int(t[1]), int(t[2])
+            up = int(t[t.index("up") + 1])
+            down = [int(v) for v in t[t.index("down") + 1:]]
+            (C if t[0] == "c" else S)[i] = (tuple(int(v) for v in t[4:4 + nv]), up, down)
+        elif t and t[0] == "root":
+            root = int(t[1])
+        elif t and t[0] == "level":
+            levels.append([int(v) for v in t[3:]])
+    return C, S, root, levels
+
+
+# the reference's junction tree on the Munin-like network depends on heap addresses (Prim's ties
+# between equal-weight separators are broken by the pointer order of a std::set<Separator*>,
+# src/JunctionTreeStructure.cpp:231,264-277); ours breaks them by creation order.  Both are
+# maximum-weight spanning trees over the same cliques; message order then differs on the tied
+# branches, so the marginals agree to a few ulp (DESIGN.md §3), labels exactly.
+MUNIN_REF_RTOL = 1e-12

@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""Fixtures that pin BASELINE configs 4 and 5 at their real network / dataset sizes.
+
+TEST INFRASTRUCTURE -- runs in the build container.
+
+  munin_like/   config 4: the seeded Munin-like network (1041 variables) as
+                XMLBIF, 32 seeded evidence cases (208 observed variables each, LIBSVM), and the
+                *reference's own* outputs on them (oracle/_ref/ref_dump jt: the unmodified
+                reference JunctionTree compiled in place): per-case label + 17-digit marginals
+                (ref.marg.gz) and the reference's junction-tree plan (ref.plan.gz).
+  pc_c5.json    config 5: PC-stable (depth 6, alpha 0.05) on the seeded 1000-variable x 100k-sample
+                dataset, run by the CPU restatement (oracle/pc_oracle.cpp; the reference's
+                PCStable/IndependenceTest cannot be compiled here: stats/gcem absent): tests per
+                level, edge count and digests of the edge list and of the sepsets, plus the digest
+                of the column store so the GPU test knows it regenerated the same data.
+
+No reference source text is copied; only its outputs on our generated inputs.
+"""
+import gzip
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+sys.path.insert(0, os.path.dirname(HERE))
+
+MUNIN_CASES = 32
+
+
+def gz_write(path, data):
+    with gzip.GzipFile(path, "wb", compresslevel=9, mtime=0) as g:
+        g.write(data if isinstance(data, bytes) else data.encode())
+
+
+def munin_like():
+    from fastbn_amd import synth
+    out = os.path.join(HERE, "munin_like")
+    os.makedirs(out, exist_ok=True)
+    ref_dump = os.path.join(REPO, "oracle", "_ref", "ref_dump")
+    if not os.path.exists(ref_dump):
+        subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref"], check=True)
+    with tempfile.TemporaryDirectory() as td:
+        xml = os.path.join(td, "munin_like.xml")
+        synth.random_network(1041, seed=1041, window=12, path=xml, name="munin_like")
+        net = synth.read_xmlbif(xml)
+        ev = synth.evidence_cases(net, MUNIN_CASES, 208, seed=20250131)
+        lib = os.path.join(td, "ev.libsvm")
+        with open(lib, "w") as f:
+            for r in ev:
+                f.write("0 " + " ".join(f"{v}:{r[v]}" for v in range(r.size) if r[v] >= 0) + " \n")
+        pre = os.path.join(td, "ref")
+        subprocess.run([ref_dump, "jt", xml, lib, "-", pre, str(MUNIN_CASES)], check=True,
+                       stdout=subprocess.DEVNULL)
+        gz_write(os.path.join(out, "munin_like.xml.gz"), open(xml, "rb").read())
+        gz_write(os.path.join(out, "ev.libsvm.gz"), open(lib, "rb").read())
+        gz_write(os.path.join(out, "ref.marg.gz"), open(pre + ".marg", "rb").read())
+        gz_write(os.path.join(out, "ref.plan.gz"), open(pre + ".plan", "rb").read())
+
+
+def pc_c5():
+    import numpy as np
+    import oracle as O
+    from conftest import pc_digest
+    from fastbn_amd import synth
+    cols, dims = synth.config5_dataset()
+    t0 = time.time()
+    r = O.OracleDataset(columns=cols, dims=dims).pc_stable(0.05, 6, 1)
+    secs = time.time() - t0
+    import hashlib
+    rec = {"nvars": int(cols.shape[0]), "nsamples": int(cols.shape[1]), "depth": 6, "alpha": 0.05,
+           "columns_sha256": hashlib.sha256(np.ascontiguousarray(cols).tobytes()).hexdigest(),
+           "dims": dims.tolist(),
+           "tests_per_level": r["tests_per_level"], "num_ci_test": r["num_ci_test"],
+           "num_edges": len(r["edges"]), "num_sepsets": len(r["sepset"]),
+           **pc_digest(r["edges"], r["sepset"]),
+           "oracle_seconds": round(secs, 1)}
+    with open(os.path.join(HERE, "pc_c5.json"), "w") as f:
+        json.dump(rec, f, indent=1)
+    print("pc_c5:", {k: v for k, v in rec.items() if k != "dims"})
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["munin", "c5"]
+    if "munin" in which:
+        munin_like()
+    if "c5" in which:
+        pc_c5()

@@ -234,3 +234,22 @@ def test_bad_evidence_rejected_on_device_path(jt, ojt):
     olab, omarg = ojt.infer(ev)
     np.testing.assert_array_equal(d_lab.cpu().numpy(), olab)
     np.testing.assert_array_equal(d_marg.cpu().numpy(), omarg)
+
+
+def test_munin_like_full_network_vs_reference(munin_fixture):
+    """BASELINE config 4 at its real network size: the streamed kernel (default variant for the
+    1041-variable plan) on the reference's 32 fixture cases -- labels equal to the reference's,
+    marginals within 1e-12 relative (its heap-ordered tree breaks a few Prim ties differently,
+    conftest.MUNIN_REF_RTOL), and bit-identical to the restatement on our tree."""
+    from conftest import MUNIN_REF_RTOL, read_ref_marg
+    jt = F.JunctionTree(F.Network(munin_fixture["xml"]), device=0)
+    o = O.OracleJT(munin_fixture["xml"])
+    ev, _ = O.load_libsvm(munin_fixture["libsvm"], o.n)
+    lab, marg = jt.infer(ev)
+    assert jt.refresh_info()["variant"] == 4
+    rlab, rmarg, _, _ = read_ref_marg(munin_fixture["marg"], o.dims)
+    np.testing.assert_array_equal(lab, rlab)
+    np.testing.assert_allclose(marg, rmarg, rtol=MUNIN_REF_RTOL, atol=1e-300)
+    olab, omarg = o.infer(ev)
+    np.testing.assert_array_equal(lab, olab)
+    np.testing.assert_array_equal(marg, omarg)

@@ -270,3 +270,23 @@ def test_kernel_timing_switch(alarm_ds):
     ci.set_kernel_timing(True)
     ci.run(np.array([[0, 1]], np.int32), 0)
     assert ci.last_kernel_ms() > 0
+
+
+def test_pc_stable_config5_full_size_vs_fixture():
+    """BASELINE config 5 at full size (1000 variables x 100k samples, depth 6): the device
+    skeleton vs the restatement's committed result (tests/golden/pc_c5.json, 801,354 tests):
+    identical tests per level, edge list and sepsets (digests), on the regenerated dataset."""
+    import hashlib
+    import json
+    from conftest import pc_digest
+    from fastbn_amd import synth
+    ref = json.load(open(os.path.join(GOLD, "pc_c5.json")))
+    cols, dims = synth.config5_dataset()
+    assert hashlib.sha256(np.ascontiguousarray(cols).tobytes()).hexdigest() == ref["columns_sha256"]
+    assert dims.tolist() == ref["dims"]
+    pc = F.PCStable(ref["alpha"], ref["depth"]).StructLearnCompData(F.Dataset(columns=cols, dims=dims))
+    assert pc.tests_per_level.tolist() == ref["tests_per_level"]
+    assert pc.num_ci_test == ref["num_ci_test"] == 801354
+    assert len(pc.edges) == ref["num_edges"] and len(pc.sepset) == ref["num_sepsets"]
+    assert pc_digest(pc.edges, pc.sepset) == {k: ref[k] for k in ("edges_sha256", "sepsets_sha256")}
+    assert pc.near_alpha == 0
