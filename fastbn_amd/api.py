@@ -70,6 +70,18 @@ _SIGS = {
     "fbn_pc_shd_bif": [_vp, C.c_char_p, _vp],
     "fbn_shd_bif": [C.c_char_p, C.c_int, _vp, C.c_int, _vp],
     "fbn_pc_result_destroy": [_vp],
+    "fbn_pc_dist_create": [C.c_int, _dbl, C.c_int, C.c_int, _pp],
+    "fbn_pc_dist_level": [_vp, C.c_int, C.c_int, _vp, _vp, _vp, _vp],
+    "fbn_pc_dist_num_edges": [_vp, _vp],
+    "fbn_pc_dist_edges": [_vp, _vp, _i64],
+    "fbn_pc_dist_run": [_vp, _vp, _vp],
+    "fbn_pc_dist_pack": [_vp, _vp, _vp, _i64, _i64, _vp],
+    "fbn_pc_dist_pairs_chunk": [_vp, _vp],
+    "fbn_pc_dist_pairs_export": [_vp, _vp, C.c_int],
+    "fbn_pc_dist_pairs_import": [_vp, _vp, _vp, C.c_int],
+    "fbn_pc_dist_apply": [_vp, _vp, _vp],
+    "fbn_pc_dist_result": [_vp, _pp],
+    "fbn_pc_dist_destroy": [_vp],
 }
 
 
@@ -449,6 +461,24 @@ class PCResult:
         lib.fbn_pc_decision_margin(handle, C.byref(m), C.byref(near))
         # p-values are parity-unpinned; decisions this close to alpha are flagged
         self.min_margin, self.near_alpha = m.value, near.value
+        nl = C.c_int()
+        lib.fbn_pc_num_levels(handle, C.byref(nl))
+        self.tests_per_level = np.zeros(nl.value, np.int64)
+        self.launched_per_level = np.zeros(nl.value, np.int64)
+        if nl.value:
+            lib.fbn_pc_level_tests(handle, _p(self.tests_per_level))
+            lib.fbn_pc_level_launched(handle, _p(self.launched_per_level))
+        self.num_ci_test = int(self.tests_per_level.sum())
+        tot, ker = C.c_double(), C.c_double()
+        lib.fbn_pc_timing(handle, C.byref(tot), C.byref(ker))
+        self.total_s, self.kernel_s = tot.value, ker.value
+        nb = C.c_int64()
+        lib.fbn_pc_device_bytes(handle, C.byref(nb))
+        self.device_bytes = nb.value
+
+    @classmethod
+    def with_levels(cls, handle):
+        return cls(handle)
 
     def GetSHD(self, bif_path):
         """BNSLComparison(ref_net, network).GetSHD() with ref_net loaded from a BIF file."""
@@ -496,21 +526,11 @@ class PCStable:
         ci = dataset if isinstance(dataset, IndependenceTest) else IndependenceTest(dataset, self.alpha, self.device)
         r = C.c_void_p()
         lib.fbn_pc_stable(ci._h, self.alpha, self.depth, group_size, C.byref(r))
-        self.result = PCResult(r)
-        nl = C.c_int()
-        lib.fbn_pc_num_levels(r, C.byref(nl))
-        self.tests_per_level = np.zeros(nl.value, np.int64)
-        self.launched_per_level = np.zeros(nl.value, np.int64)
-        lib.fbn_pc_level_tests(r, _p(self.tests_per_level))
-        lib.fbn_pc_level_launched(r, _p(self.launched_per_level))
-        self.edges, self.sepset, self.oriented = self.result.edges, self.result.sepset, self.result.oriented
-        tot, ker = C.c_double(), C.c_double()
-        lib.fbn_pc_timing(r, C.byref(tot), C.byref(ker))
-        self.total_s, self.kernel_s = tot.value, ker.value
-        nb = C.c_int64()
-        lib.fbn_pc_device_bytes(r, C.byref(nb))
-        self.device_bytes = nb.value
-        self.num_ci_test = int(self.tests_per_level.sum())
+        self.result = res = PCResult(r)
+        self.tests_per_level, self.launched_per_level = res.tests_per_level, res.launched_per_level
+        self.edges, self.sepset, self.oriented = res.edges, res.sepset, res.oriented
+        self.total_s, self.kernel_s, self.device_bytes = res.total_s, res.kernel_s, res.device_bytes
+        self.num_ci_test = res.num_ci_test
         self.min_margin, self.near_alpha = self.result.min_margin, self.result.near_alpha
         return self
 

@@ -32,7 +32,8 @@ extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *di
                                          const int32_t *items, long long W, long long n, int d, double alpha,
                                          double *g2, int32_t *df, double *p, uint8_t *indep, int32_t *counts,
                                          int32_t *counts0, unsigned long long *stats, const int32_t *rowcnt,
-                                         int32_t *pairtab, int pmode, int nvars, int num_cu, hipStream_t s);
+                                         int32_t *pairtab, int pmode, int nvars, int num_cu, long long t0,
+                                         hipStream_t s);
 extern "C" hipError_t fbn_ci_bits_rowcount(const uint32_t *bits, long long rows, long long W, int32_t *rowcnt,
                                            hipStream_t s);
 extern "C" hipError_t fbn_jt_virt_launch(const JtVClique *cls, const int32_t *aux, const double *initv,
@@ -200,10 +201,6 @@ static int PinnedEnsure(void *&ptr, size_t &have, size_t want) {
     have = want;
     return FBN_OK;
 }
-
-struct fbn_pc_result {
-    fbn::PCResultHost r;
-};
 
 static int CiResetMargin(fbn_ci_ctx *c) {
     const unsigned long long init[2] = {0x7FF0000000000000ull /* +inf */, 0};
@@ -921,7 +918,7 @@ int fbn_ci_dataset_from_device(const uint8_t *d_cols, int nvars, int64_t nsample
 static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alpha, bool want_g2p,
                           int32_t *counts_dev, hipStream_t s, int k = 0, const int32_t *zc_items = nullptr,
                           uint8_t *zc_indep = nullptr, int32_t *zc_df = nullptr, const fbn::CiBatchStats *pre = nullptr,
-                          bool all_pairs = false) {
+                          bool all_pairs = false, int64_t pair0 = 0) {
     CiSlot &S = c->slot[k];
     if (d < 0 || d > 8) return SetError(FBN_ERR_LIMIT, "conditioning set size %d (supported 0..8)", d);
     const int w = 2 + d;
@@ -1000,7 +997,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
                                           zc_indep ? zc_indep : S.indep.as<uint8_t>(),
                                           S.bcounts.as<int32_t>(), counts_dev, c->stats.as<unsigned long long>(),
                                           c->browcnt.as<int32_t>(), c->pairtab.as<int32_t>(), pmode, c->nvars,
-                                          c->num_cu, s);
+                                          c->num_cu, (long long)pair0, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci bits kernel launch: %s", hipGetErrorString(e));
         if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
         return FBN_OK;
@@ -1194,10 +1191,9 @@ int fbn_pc_level(fbn_ci_ctx *c, double alpha, int d, int group_size, const int32
         if (a < 0 || b <= a || b >= c->nvars) return SetError(FBN_ERR_ARG, "edge %lld must be (x < y) in range", (long long)i);
         if (i && !(ev[i - 1] < std::make_pair(a, b))) return SetError(FBN_ERR_ARG, "edges must be in (x, y) lexicographic order");
         ev[i] = {a, b};
-        adj[a].push_back(b);
+        adj[a].push_back(b);  // lexicographic edges: every list comes out sorted (no sort pass)
         adj[b].push_back(a);
     }
-    for (auto &a : adj) std::sort(a.begin(), a.end());
     FBN_HIP(hipSetDevice(c->device));
     fbn::PCResultHost scratch;
     fbn::LevelOut out;
@@ -1334,20 +1330,49 @@ int CiBatchLaunch(fbn_ci_ctx *c, int k, const int32_t *items, int64_t n, int d, 
 bool CiAllPairsEligible(const fbn_ci_ctx *c, const CiBatchStats &st) {
     return st.maxdim <= 4 && !getenv("FBN_CI_NO_BITS") && (c->N >= 4096 || getenv("FBN_CI_FORCE_BITS"));
 }
-int CiBatchLaunchAllPairs(fbn_ci_ctx *c, double alpha, const CiBatchStats *pre) {
+int CiBatchLaunchAllPairs(fbn_ci_ctx *c, double alpha, const CiBatchStats *pre, int64_t t0, int64_t n) {
     CiSlot &S = c->slot[0];
-    const int64_t n = (int64_t)c->nvars * (c->nvars - 1) / 2;
     S.n = n;
     S.want_df = false;
     S.zc = false;
     if (n == 0) return FBN_OK;
     int rc;
     if ((rc = PinnedEnsure(S.h_res, S.h_res_bytes, (size_t)n * 5 + 8))) return rc;
-    rc = CiLaunchDevice(c, nullptr, n, 0, alpha, false, nullptr, c->stream, 0, nullptr, nullptr, nullptr, pre, true);
+    rc = CiLaunchDevice(c, nullptr, n, 0, alpha, false, nullptr, c->stream, 0, nullptr, nullptr, nullptr, pre, true,
+                        t0);
     if (rc) return rc;
     FBN_HIP(hipMemcpyAsync(S.h_res, S.indep.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
     FBN_HIP(hipEventRecord(S.done, c->stream));
     return FBN_OK;
+}
+int CiPairTablesCopy(fbn_ci_ctx *c, int64_t p0, int64_t np, void *buf, bool buf_on_device, bool to_ctx) {
+    if (np < 0 || p0 < 0) return SetError(FBN_ERR_ARG, "bad pair range");
+    const int64_t P = (int64_t)c->nvars * (c->nvars - 1) / 2;
+    if (p0 + np > P) return SetError(FBN_ERR_ARG, "pair range [%lld, %lld) beyond %lld pairs", (long long)p0,
+                                     (long long)(p0 + np), (long long)P);
+    FBN_HIP(hipSetDevice(c->device));
+    int rc;
+    if ((rc = c->pairtab.ensure(std::max<size_t>((size_t)P, 1) * 16 * 4))) return rc;
+    if (!to_ctx && !c->pairs_recorded) return SetError(FBN_ERR_ARG, "no pair tables recorded on this context");
+    char *ctx_ptr = c->pairtab.as<char>() + (size_t)p0 * 64;
+    const size_t bytes = (size_t)np * 64;
+    const hipMemcpyKind kind = to_ctx ? (buf_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice)
+                                      : (buf_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost);
+    FBN_HIP(hipStreamSynchronize(c->stream));
+    if (bytes) FBN_HIP(hipMemcpy(to_ctx ? (void *)ctx_ptr : buf, to_ctx ? (const void *)buf : ctx_ptr, bytes, kind));
+    return FBN_OK;
+}
+int CiMarginReset(fbn_ci_ctx *c) {
+    FBN_HIP(hipSetDevice(c->device));
+    return CiResetMargin(c);
+}
+int CiMarginRead(fbn_ci_ctx *c, double *min_margin, int64_t *near_alpha) {
+    FBN_HIP(hipSetDevice(c->device));
+    return CiReadMargin(c, min_margin, near_alpha);
+}
+void CiSetPairsRecorded(fbn_ci_ctx *c) {
+    c->pair_mode = 2;
+    c->pairs_recorded = true;
 }
 int CiBatchWait(fbn_ci_ctx *c, int k, uint8_t *indep, int32_t *df, PCResultHost &res) {
     CiSlot &S = c->slot[k];

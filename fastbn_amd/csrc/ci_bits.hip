@@ -245,8 +245,9 @@ __device__ __forceinline__ void count_test_derived(const uint32_t *__restrict__ 
     }
 }
 
-// items == nullptr for a marginal batch: test t is the t-th pair (x < y) of the complete graph over
-// nv variables in lexicographic order (a PC run's level 0), decoded instead of read
+// items == nullptr for a marginal batch: test t is the (t0 + t)-th pair (x < y) of the complete graph
+// over nv variables in lexicographic order (a PC run's level 0, or one rank's range of it), decoded
+// instead of read
 __device__ __forceinline__ void pair_of(long long t, int nv, int &x, int &y) {
     const double b = 2.0 * nv - 1.0;
     long long i = (long long)((b - sqrt(b * b - 8.0 * (double)t)) * 0.5);
@@ -266,12 +267,12 @@ __global__ __launch_bounds__(256) void ci_bits_count(const uint32_t *__restrict_
                                                      const int32_t *__restrict__ row0, const int32_t *__restrict__ items,
                                                      long long W, long long n, int32_t *__restrict__ counts,
                                                      const int32_t *__restrict__ rowcnt, int32_t *__restrict__ pairtab,
-                                                     int nvars) {
+                                                     int nvars, long long t0) {
     const int lane = threadIdx.x & 63;
     const long long wave = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
     for (long long t = wave; t < n; t += (long long)gridDim.x * 4) {
         int x, y;
-        if (D == 0 && !items) pair_of(t, nvars, x, y);
+        if (D == 0 && !items) pair_of(t0 + t, nvars, x, y);
         else x = items[(2 + D) * t], y = items[(2 + D) * t + 1];
         const int dx = dims[x], dy = dims[y];
         const uint32_t *bx = bits + (size_t)row0[x] * W, *by = bits + (size_t)row0[y] * W;
@@ -353,10 +354,10 @@ __global__ __launch_bounds__(256) void ci_bits_g2(const int32_t *__restrict__ co
                                                   double *__restrict__ g2o, int32_t *__restrict__ dfo,
                                                   double *__restrict__ po, uint8_t *__restrict__ indep,
                                                   int32_t *__restrict__ counts0, unsigned long long *__restrict__ stats,
-                                                  int nvars) {
+                                                  int nvars, long long t0) {
     for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t < n; t += (long long)gridDim.x * 256) {
         int px, py;
-        if (D == 0 && !items) pair_of(t, nvars, px, py);
+        if (D == 0 && !items) pair_of(t0 + t, nvars, px, py);
         else px = items[(2 + D) * t], py = items[(2 + D) * t + 1];
         const int dx = dims[px], dy = dims[py];
         const int dimz = D == 1 ? dims[items[3 * t + 2]] : 1;
@@ -482,24 +483,25 @@ extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *di
                                          const int32_t *items, long long W, long long n, int d, double alpha,
                                          double *g2, int32_t *df, double *p, uint8_t *indep, int32_t *counts,
                                          int32_t *counts0, unsigned long long *stats, const int32_t *rowcnt,
-                                         int32_t *pairtab, int pmode, int nvars, int num_cu, hipStream_t s) {
+                                         int32_t *pairtab, int pmode, int nvars, int num_cu, long long t0,
+                                         hipStream_t s) {
     const long long g1 = (n + 3) / 4, cap = (long long)num_cu * 8;
     const long long g2g = (n + 255) / 256;
     const dim3 b1((unsigned)(g1 < cap ? g1 : cap)), b2((unsigned)(g2g < cap ? g2g : cap));
     if (d == 0) {
         hipLaunchKernelGGL(ci_bits_count<0>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts, rowcnt,
-                           pmode == 1 ? pairtab : nullptr, nvars);
+                           pmode == 1 ? pairtab : nullptr, nvars, t0);
         hipLaunchKernelGGL(ci_bits_g2<0>, b2, dim3(256), 0, s, counts, dims, items, n, alpha, g2, df, p, indep,
-                           counts0, stats, nvars);
+                           counts0, stats, nvars, t0);
     } else if (d == 1) {
         if (pmode == 2)
             hipLaunchKernelGGL(ci_bits_count_derived, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts,
                                (const int32_t *)pairtab, nvars);
         else
             hipLaunchKernelGGL(ci_bits_count<1>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts, rowcnt,
-                               nullptr, nvars);
+                               nullptr, nvars, 0ll);
         hipLaunchKernelGGL(ci_bits_g2<1>, b2, dim3(256), 0, s, counts, dims, items, n, alpha, g2, df, p, indep,
-                           counts0, stats, nvars);
+                           counts0, stats, nvars, 0ll);
     } else {
         return hipErrorInvalidValue;
     }

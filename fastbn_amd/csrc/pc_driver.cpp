@@ -137,9 +137,11 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
         int nv = 0;
         int64_t ns = 0;
         CiCtxShape(ctx, &nv, &ns);
-        const bool all_pairs = e_begin == 0 && e_end == edges.size() && (int64_t)E == (int64_t)nv * (nv - 1) / 2 &&
+        // the complete graph (a PC run's level 0): edge index = pair index, the kernels decode the
+        // pairs of the range themselves
+        const bool all_pairs = (int64_t)edges.size() == (int64_t)nv * (nv - 1) / 2 &&
                                CiAllPairsEligible(ctx, st0) && !getenv("FBN_CI_NO_IMPLICIT");
-        int rc = all_pairs ? CiBatchLaunchAllPairs(ctx, alpha, &st0)
+        int rc = all_pairs ? CiBatchLaunchAllPairs(ctx, alpha, &st0, (int64_t)e_begin, (int64_t)E)
                            : CiBatchLaunch(ctx, 0, pairs, (int64_t)E, 0, alpha, false, &st0);
         if (rc) return rc;
         rc = CiBatchWait(ctx, 0, indep.data(), nullptr, res);

@@ -158,7 +158,13 @@ const int32_t *CiCtxDims(const fbn_ci_ctx *c);  // state count per variable
 // slot 0 with no item array (the kernels decode the pair); only when eligible for the bit-sliced
 // path (st = the batch's statistics)
 bool CiAllPairsEligible(const fbn_ci_ctx *c, const CiBatchStats &st);
-int CiBatchLaunchAllPairs(fbn_ci_ctx *c, double alpha, const CiBatchStats *pre);
+// pairs [t0, t0 + n) of that order (one rank's range of a distributed level 0)
+int CiBatchLaunchAllPairs(fbn_ci_ctx *c, double alpha, const CiBatchStats *pre, int64_t t0, int64_t n);
+// copy the pair tables of pairs [p0, p0 + np) (16 int32 each) out of the ctx (to_ctx = false; they
+// must have been recorded) or into it (to_ctx = true); buf in device or host memory
+int CiPairTablesCopy(fbn_ci_ctx *c, int64_t p0, int64_t np, void *buf, bool buf_on_device, bool to_ctx);
+// every pair's table is now in the ctx (imported from all ranks): level-1 batches derive from them
+void CiSetPairsRecorded(fbn_ci_ctx *c);
 // pair tables of the bit-sliced path: 1 = the next marginal batch records every pair's table (it
 // must test all pairs i < j: a PC run's level 0), 2 = one-conditioning-variable batches derive the
 // last value of x, y and z from them, 0 = off (also drops what was recorded)
@@ -175,6 +181,13 @@ struct LevelOut {
 int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::vector<std::vector<int>> &adj,
              const std::vector<std::pair<int, int>> &edges, size_t e_begin, size_t e_end, LevelOut &out,
              PCResultHost &res);
+// removals after a level in vec_edges order + adjacency rebuild; FreeDegree > d (pc_driver.cpp)
+void ApplyRemovals(const std::vector<char> &rm, std::vector<std::pair<int, int>> &edges,
+                   std::vector<std::vector<int>> &adj);
+bool ContinueAfter(const std::vector<std::vector<int>> &adj, int d);
+// decision-margin log of a ctx (capi.hip): reset / read
+int CiMarginReset(fbn_ci_ctx *c);
+int CiMarginRead(fbn_ci_ctx *c, double *min_margin, int64_t *near_alpha);
 // orientation (pc_orient.cpp): v-structures + Meek rules 1-3 on res.edges / res.sepset
 int OrientPC(int nvars, PCResultHost &res);
 int LoadBifGraph(const std::string &path, std::vector<std::string> &names, std::vector<std::pair<int, int>> &arcs);
@@ -182,5 +195,9 @@ int ComputeSHD(int n, const std::vector<std::pair<int, int>> &arcs, const std::v
                int *shd, int *unlabelled);
 
 }  // namespace fbn
+
+struct fbn_pc_result {
+    fbn::PCResultHost r;
+};
 
 #endif

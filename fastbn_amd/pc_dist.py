@@ -1,84 +1,163 @@
 """Multi-GPU PC-stable skeleton: one process per GPU, the column store resident on
 every rank, and per level one exchange step.
 
-Per level d the current skeleton's edges (vec_edges order) are split into contiguous ranges of
-roughly equal cost -- C(|adj(x)\\{y}|, d) + C(|adj(y)\\{x}|, d) candidate sets per edge, 1 at level
-0 -- each rank runs its range on its own device (`fbn_pc_level`: the edge's sequential
-first-independent-set semantics stay local), and one all-gather brings every rank the removal
-flags, sepsets and test counts; every rank then applies the removals in vec_edges order, exactly as
-the single-GPU driver (src/PCStable.cpp:310-326).  Orientation (host) runs on the gathered skeleton.
-Works with nccl (RCCL) and, for tests, with gloo."""
-from math import comb
+The level bookkeeping is native (fastbn_amd/csrc/pc_dist.cpp, `fbn_pc_dist_*`): every rank holds
+the same skeleton, cuts the level's edges into the same contiguous ranges (level 0: equal chunks of
+the complete graph; level d >= 1: equal candidate-set cost C(|adj(x)|-1, d) + C(|adj(y)|-1, d) + 1),
+runs its range on its own device (an edge's sequential first-independent-set search stays on one
+rank) into a fixed-size int32 record, and after one all-gather of the records applies all of them
+in rank order = vec_edges order, exactly as the single-GPU driver (src/PCStable.cpp:310-326).  At
+level 0 the ranks also all-gather their pair tables (16 counts per pair, device to device over
+RCCL) so that every rank keeps the derived level-1 counting.  This module only moves the records;
+no per-edge Python.  Works with nccl (RCCL) and, for tests, with gloo (records on the CPU)."""
+import ctypes as C
 
 import numpy as np
 
-from . import shard
+from . import api
 
 
-def partition(costs, world):
-    """Contiguous ranges [b, e) of near-equal total cost, one per rank (rank order)."""
-    n = len(costs)
-    if world <= 1 or n == 0:
-        return [(0, n)] + [(n, n)] * (world - 1)
-    cum = np.concatenate([[0], np.cumsum(np.asarray(costs, np.float64))])
-    total = cum[-1]
-    cuts = [0]
-    for r in range(1, world):
-        cuts.append(int(np.searchsorted(cum, total * r / world, side="left")))
-    cuts.append(n)
-    cuts = [min(max(c, 0), n) for c in cuts]
-    for i in range(1, len(cuts)):
-        cuts[i] = max(cuts[i], cuts[i - 1])
-    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+class PCDistSession:
+    """One rank's view of a distributed PC-stable skeleton search (fbn_pc_dist_*)."""
+
+    def __init__(self, nvars, alpha=0.05, depth=1000, group_size=1):
+        h = C.c_void_p()
+        api.lib.fbn_pc_dist_create(int(nvars), float(alpha), int(depth), int(group_size), C.byref(h))
+        self._h, self.nvars = h, int(nvars)
+
+    def level(self, world, rank):
+        """Partition of the current level -> (d, e_begin, e_end, record_len), or None when done."""
+        d, b, e, L = C.c_int(), C.c_int64(), C.c_int64(), C.c_int64()
+        api.lib.fbn_pc_dist_level(self._h, int(world), int(rank), C.byref(d), C.byref(b), C.byref(e), C.byref(L))
+        return None if d.value < 0 else (d.value, b.value, e.value, L.value)
+
+    def edges(self):
+        n = C.c_int64()
+        api.lib.fbn_pc_dist_num_edges(self._h, C.byref(n))
+        e = np.zeros((max(n.value, 1), 2), np.int32)
+        api.lib.fbn_pc_dist_edges(self._h, e.ctypes.data, n.value)
+        return e[:n.value]
+
+    def run(self, ci, record_len):
+        """This rank's range of the level on the device of IndependenceTest `ci` -> record."""
+        rec = np.empty(record_len, np.int32)
+        api.lib.fbn_pc_dist_run(self._h, ci._h, rec.ctypes.data)
+        return rec
+
+    def pack(self, removed, sepsets, counted, launched, record_len):
+        """A record from results computed elsewhere (removed[n] bool, sepsets [n][d] or None)."""
+        rm = np.ascontiguousarray(np.asarray(removed, np.uint8).reshape(-1))
+        sp = np.ascontiguousarray(np.asarray(sepsets, np.int32)) if sepsets is not None else None
+        rec = np.empty(record_len, np.int32)
+        api.lib.fbn_pc_dist_pack(self._h, rm.ctypes.data if rm.size else None,
+                                 sp.ctypes.data if sp is not None and sp.size else None, int(counted), int(launched),
+                                 rec.ctypes.data)
+        return rec
+
+    def pairs_chunk(self):
+        n = C.c_int64()
+        api.lib.fbn_pc_dist_pairs_chunk(self._h, C.byref(n))
+        return n.value
+
+    def pairs_export(self, ptr, on_device):
+        api.lib.fbn_pc_dist_pairs_export(self._h, C.c_void_p(ptr), int(bool(on_device)))
+
+    def pairs_import(self, ci, ptr, on_device):
+        api.lib.fbn_pc_dist_pairs_import(self._h, ci._h, C.c_void_p(ptr), int(bool(on_device)))
+
+    def apply(self, records):
+        """records [world][record_len] int32 (rank order) -> True if another level follows."""
+        recs = np.ascontiguousarray(records, np.int32)
+        more = C.c_int()
+        api.lib.fbn_pc_dist_apply(self._h, recs.ctypes.data, C.byref(more))
+        return bool(more.value)
+
+    def result(self):
+        """Skeleton + sepsets + counts + host orientation (fbn_pc_dist_result) -> api.PCResult with
+        tests_per_level / launched_per_level."""
+        r = C.c_void_p()
+        api.lib.fbn_pc_dist_result(self._h, C.byref(r))
+        return api.PCResult.with_levels(r)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            api.lib.fbn_pc_dist_destroy(self._h)
+            self._h = None
 
 
-def level_costs(edges, adj, d):
-    if d == 0:
-        return [1.0] * len(edges)
-    return [comb(len(adj[x]) - 1, d) + comb(len(adj[y]) - 1, d) + 1.0 for x, y in edges]
-
-
-def pc_skeleton_distributed(level_fn, nvars, depth=1000, device=None):
-    """level_fn(d, edges, b, e) -> (removed[bool], sepsets, counted, launched) for edges[b:e].
-    Returns (edges, sepset dict, tests_per_level, launched_per_level), identical on every rank."""
+def _world_rank():
     import torch.distributed as dist
-    world = dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1
-    rank = dist.get_rank() if world > 1 else 0
-    edges = [(i, j) for i in range(nvars) for j in range(i + 1, nvars)]
-    adj = [[j for j in range(nvars) if j != i] for i in range(nvars)]
-    sepset, tests, launched = {}, [], []
-    d = 0
-    while d == 0 or d < depth:
-        ranges = partition(level_costs(edges, adj, d), world)
-        b, e = ranges[rank]
-        rm, seps, cnt, lau = level_fn(d, edges, b, e)
-        # one exchange: removal flags + sepsets (fixed width d, -1 = kept) + counts, rank order
-        width = max(d, 1)
-        rec = np.full((e - b, 1 + width), -1, np.int32)
-        rec[:, 0] = np.asarray(rm, np.int32)
-        for i, z in enumerate(seps):
-            if z is not None and d:
-                rec[i, 1:1 + d] = z
-        allrec = shard.gather_var(rec, device)
-        cnts = shard.sum_over_ranks([cnt, lau], device)
-        assert allrec.shape[0] == len(edges)
-        keep = []
-        for (x, y), r in zip(edges, allrec):
-            if r[0]:
-                sepset[(x, y)] = tuple(int(v) for v in r[1:1 + d]) if d else ()
-            else:
-                keep.append((x, y))
-        edges = keep
-        adj = [[] for _ in range(nvars)]
-        for x, y in edges:
-            adj[x].append(y)
-            adj[y].append(x)
-        tests.append(int(cnts[0]))
-        launched.append(int(cnts[1]))
-        if d >= 1 and not (max(len(a) for a in adj) - 1 > d):
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+def _all_gather_fixed(arr, device):
+    """Every rank's equal-length int32 array, stacked in rank order -> numpy [world][len]."""
+    import torch
+    import torch.distributed as dist
+    world, _ = _world_rank()
+    if world == 1:
+        return arr[None, :]
+    t = torch.from_numpy(arr)
+    if device is not None:
+        t = t.to(device)
+        out = torch.empty((world, arr.size), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t)
+        return out.cpu().numpy()
+    outs = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(outs, t)
+    return torch.stack(outs).numpy()
+
+
+def _exchange_pair_tables(sess, ci, device):
+    """Level 0 -> 1: all-gather every rank's chunk of pair tables into every rank's context."""
+    import torch
+    import torch.distributed as dist
+    world, _ = _world_rank()
+    chunk = sess.pairs_chunk()
+    on_dev = device is not None
+    dev = torch.device(device) if on_dev else torch.device("cpu")
+    inp = torch.zeros(chunk * 16, dtype=torch.int32, device=dev)
+    sess.pairs_export(inp.data_ptr(), on_dev)
+    if on_dev:
+        out = torch.empty(world * chunk * 16, dtype=torch.int32, device=dev)
+        dist.all_gather_into_tensor(out, inp)
+        torch.cuda.synchronize(dev)
+    else:
+        outs = [torch.empty_like(inp) for _ in range(world)]
+        dist.all_gather(outs, inp)
+        out = torch.cat(outs)
+    sess.pairs_import(ci, out.data_ptr(), on_dev)
+
+
+def pc_skeleton_distributed(engine, nvars, alpha=0.05, depth=1000, group_size=1, device=None, ci=None):
+    """Run the level loop; `engine(sess, d, b, e, record_len)` -> this rank's record for edges
+    [b, e) of sess.edges() (the device engine is `sess.run(ci, record_len)`).  `device`: the torch
+    device the records / pair tables travel on (an RCCL group), None for a CPU (gloo) group.  With
+    `ci` given and world > 1, level 0's pair tables are all-gathered into it.  Returns the session
+    after the last level (identical on every rank)."""
+    world, rank = _world_rank()
+    sess = PCDistSession(nvars, alpha, depth, group_size)
+    while True:
+        lv = sess.level(world, rank)
+        if lv is None:
             break
-        d += 1
-    return edges, sepset, tests, launched
+        d, b, e, L = lv
+        rec = engine(sess, d, b, e, L)
+        if d == 0 and world > 1 and ci is not None:
+            _exchange_pair_tables(sess, ci, device)
+        if not sess.apply(_all_gather_fixed(rec, device)):
+            break
+    return sess
+
+
+def pc_stable_distributed(ci, nvars, alpha=0.05, depth=1000, group_size=1, device=None):
+    """Device skeleton on every rank's IndependenceTest `ci`, then host orientation ->
+    (PCResult, tests_per_level, launched_per_level)."""
+    sess = pc_skeleton_distributed(lambda s, d, b, e, L: s.run(ci, L), nvars, alpha, depth, group_size, device, ci)
+    res = sess.result()
+    return res, res.tests_per_level.tolist(), res.launched_per_level.tolist()
 
 
 def broadcast_columns(cols, shape, device=None, src=0):
@@ -101,18 +180,6 @@ def independence_test_broadcast(cols, dims, shape, alpha=0.05, device=0, src=0):
     """Every rank's IndependenceTest over the column store loaded on rank `src`, moved by one RCCL
     broadcast straight into device memory (no host copy on the receiving ranks)."""
     import torch
-    from . import api
     t = broadcast_columns(cols, shape, torch.device("cuda", device), src)
     torch.cuda.synchronize(device)
     return api.IndependenceTest.from_device(t.data_ptr(), shape[0], shape[1], dims, alpha, device)
-
-
-def pc_stable_distributed(ci, nvars, alpha=0.05, depth=1000, group_size=1, device=None):
-    """Device skeleton on every rank's IndependenceTest `ci`, then host orientation."""
-    from . import api
-
-    def level_fn(d, edges, b, e):
-        return ci.level(d, edges, b, e, group_size)
-
-    edges, sepset, tests, launched = pc_skeleton_distributed(level_fn, nvars, depth, device)
-    return api.orient_skeleton(nvars, edges, sepset), tests, launched

@@ -229,6 +229,42 @@ int fbn_pc_shd_bif(const fbn_pc_result *r, const char *bif_path, int *shd);
 /* Same for any learned graph given as triples [n][3] (from, to, 1) / (a, b, 0). */
 int fbn_shd_bif(const char *bif_path, int nvars, const int32_t *triples, int n, int *shd);
 int fbn_pc_timing(const fbn_pc_result *r, double *total_s, double *kernel_s);
+
+/* ------------------------------------------------------------------ multi-GPU PC-stable session
+ * One session per rank (one process per GPU); the per-level exchange is the caller's collective
+ * (RCCL all-gather), everything per edge stays native (fastbn_amd/csrc/pc_dist.cpp).  Replaces the
+ * level loop of PCStable::StructLearnByPCStable (src/PCStable.cpp:49-200) for a partitioned run:
+ *   create -> { level(world, rank) -> run (or pack) -> [level 0: pairs_export / all-gather /
+ *   pairs_import] -> all-gather the records -> apply } until apply reports no further level ->
+ *   result (orientation included).  Every rank must apply the same records in rank order. */
+typedef struct fbn_pc_dist fbn_pc_dist;
+int fbn_pc_dist_create(int nvars, double alpha, int depth, int group_size, fbn_pc_dist **out);
+/* Partition of the current level: d (-1 when finished), this rank's edge range [e_begin, e_end) of
+ * the current skeleton (vec_edges order) and the int32 length of every rank's record. */
+int fbn_pc_dist_level(fbn_pc_dist *s, int world, int rank, int *d, int64_t *e_begin, int64_t *e_end,
+                      int64_t *record_len);
+int fbn_pc_dist_num_edges(const fbn_pc_dist *s, int64_t *n);
+int fbn_pc_dist_edges(const fbn_pc_dist *s, int32_t *pairs /* [n][2] */, int64_t cap);
+/* This rank's range on the device of `c` (column store resident there) -> record [record_len]. */
+int fbn_pc_dist_run(fbn_pc_dist *s, fbn_ci_ctx *c, int32_t *record);
+/* A record from results computed elsewhere: removed [n], sepsets [n][d] (sorted; ignored where
+ * not removed), counted / launched tests.  For engines other than the device (testing). */
+int fbn_pc_dist_pack(fbn_pc_dist *s, const uint8_t *removed, const int32_t *sepsets, int64_t counted,
+                     int64_t launched, int32_t *record);
+/* Level 0 pair tables (16 int32 per pair) for the derived level-1 counting: after this rank's
+ * level-0 run, export writes its chunk (pairs_chunk pairs, the tail zero-padded by the caller) to
+ * buf; the caller all-gathers the chunks in rank order (pair index = offset / 16) and imports the
+ * gathered buffer into its context.  buf in device (buf_on_device = 1) or host memory. */
+int fbn_pc_dist_pairs_chunk(const fbn_pc_dist *s, int64_t *pairs_per_rank);
+int fbn_pc_dist_pairs_export(fbn_pc_dist *s, void *buf, int buf_on_device);
+int fbn_pc_dist_pairs_import(fbn_pc_dist *s, fbn_ci_ctx *c, const void *buf, int buf_on_device);
+/* All ranks' records [world][record_len], rank order: sepsets, counts, removals; *more = 1 if
+ * another level follows (depth and FreeDegree, src/PCStable.cpp:159-178). */
+int fbn_pc_dist_apply(fbn_pc_dist *s, const int32_t *records, int *more);
+/* After the last level: skeleton, sepsets, per-level counts (all ranks), this rank's kernel time /
+ * decision margin, orientation (as fbn_pc_stable). */
+int fbn_pc_dist_result(fbn_pc_dist *s, fbn_pc_result **out);
+int fbn_pc_dist_destroy(fbn_pc_dist *s);
 /* Roofline accounting: bytes of column data the CI kernels had to read for every launched test,
  * in the format they read (uint8 columns: N per variable; bit-sliced masks: N/8 per value). */
 int fbn_pc_device_bytes(const fbn_pc_result *r, int64_t *bytes);

@@ -84,3 +84,23 @@ def test_from_device_matches_upload_and_rejects_bad_codes():
         F.IndependenceTest.from_device(tb.data_ptr(), ds.num_vars, ds.num_instance, ds.dims)
     with pytest.raises(F.FastBNError, match="variable 3"):
         F.IndependenceTest(F.Dataset(columns=bad, dims=ds.dims))
+
+
+def test_config5_full_size_through_session_world1():
+    """BASELINE config 5 (1000 vars x 100k samples, depth 6) through the native distributed
+    session at world size 1 (the N = 1 leg of bench.py's multi-GPU PC path): the fixture's
+    counts, edges and sepsets, and pair tables kept for the derived level-1 counting."""
+    import hashlib
+    import json
+    from conftest import pc_digest
+    from fastbn_amd import pc_dist, synth
+    ref = json.load(open(os.path.join(GOLD, "pc_c5.json")))
+    cols, dims = synth.config5_dataset()
+    assert hashlib.sha256(np.ascontiguousarray(cols).tobytes()).hexdigest() == ref["columns_sha256"]
+    ci = F.IndependenceTest(F.Dataset(columns=cols, dims=dims))
+    res, tests, launched = pc_dist.pc_stable_distributed(ci, 1000, 0.05, 6)
+    assert tests == ref["tests_per_level"]
+    assert pc_digest(res.edges, res.sepset) == {k: ref[k] for k in ("edges_sha256", "sepsets_sha256")}
+    single = F.PCStable(0.05, 6).StructLearnCompData(ci)
+    assert launched == single.launched_per_level.tolist()  # same rounds: derived level 1 kept
+    assert res.oriented == single.oriented

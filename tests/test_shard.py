@@ -107,6 +107,19 @@ def _oracle_level_fn(od):
     return level_fn
 
 
+def _oracle_engine(od):
+    """The session's engine on the CPU: the oracle restatement of CheckEdge over the range."""
+    def engine(sess, d, b, e, L):
+        edges = [tuple(map(int, x)) for x in sess.edges()]
+        rm, seps, cnt, lau = _oracle_level_fn(od)(d, edges, b, e)
+        sp = np.full((len(rm), max(d, 1)), -1, np.int32)
+        for i, z in enumerate(seps):
+            if z is not None and d:
+                sp[i, :d] = z
+        return sess.pack(np.asarray(rm, np.uint8), sp if d else None, cnt, lau, L)
+    return engine
+
+
 def _pc_worker(rank, world, port, csv, out_path):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -115,20 +128,60 @@ def _pc_worker(rank, world, port, csv, out_path):
     import oracle as O
     from fastbn_amd import pc_dist
     od = O.OracleDataset(csv=csv)
-    edges, sepset, tests, launched = pc_dist.pc_skeleton_distributed(_oracle_level_fn(od), 37)
+    sess = pc_dist.pc_skeleton_distributed(_oracle_engine(od), 37)
+    res = sess.result()
     if rank == 0:
-        np.save(out_path, np.array([edges, sorted(sepset.items()), tests], dtype=object), allow_pickle=True)
+        np.save(out_path, np.array([res.edges, sorted(res.sepset.items()), res.tests_per_level.tolist(),
+                                    res.oriented], dtype=object), allow_pickle=True)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_partition_balances_cost():
+def test_session_partition_is_deterministic_and_balanced():
+    """fbn_pc_dist_level on W independent sessions (one per simulated rank): the same contiguous
+    cover of the level's edges on every rank; level 0 in equal chunks of the complete graph; after
+    applying the same records, level 1 cut by candidate-set cost."""
     from fastbn_amd import pc_dist
-    costs = [1, 5, 1, 1, 9, 1, 1, 1, 3, 2]
-    for world in (1, 2, 3, 4):
-        parts = pc_dist.partition(costs, world)
-        assert parts[0][0] == 0 and parts[-1][1] == len(costs)
-        assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+    n = 30
+    for world in (1, 2, 3, 8):
+        ss = [pc_dist.PCDistSession(n, 0.05, 3) for _ in range(world)]
+        lv = [s.level(world, r) for r, s in enumerate(ss)]
+        P = n * (n - 1) // 2
+        chunk = -(-P // world)
+        assert [x[1] for x in lv] == [min(P, r * chunk) for r in range(world)]
+        assert lv[-1][2] == P and all(a[2] == b[1] for a, b in zip(lv, lv[1:]))
+        assert len({x[3] for x in lv}) == 1  # same record length everywhere
+        rng = np.random.default_rng(world)
+        rm_all = rng.random(P) < 0.7  # drop ~70 % of the pairs at level 0
+        recs = np.stack([s.pack(rm_all[b:e], None, e - b, e - b, L) for s, (_, b, e, L) in zip(ss, lv)])
+        for s in ss:
+            assert s.apply(recs)
+        lv1 = [s.level(world, r) for r, s in enumerate(ss)]
+        E = len(ss[0].edges())
+        assert E == int((~rm_all).sum())
+        assert lv1[0][1] == 0 and lv1[-1][2] == E and all(a[2] == b[1] for a, b in zip(lv1, lv1[1:]))
+        assert all(np.array_equal(ss[0].edges(), s.edges()) for s in ss)
+        assert len({x[1:] for x in lv1}) == world or E < world
+        # balance: candidate-set cost per range within one edge's cost of the ideal share
+        edges = ss[0].edges()
+        deg = np.bincount(edges.reshape(-1), minlength=n)
+        cost = (deg[edges[:, 0]] - 1).clip(0) + (deg[edges[:, 1]] - 1).clip(0) + 1.0
+        share = cost.sum() / world
+        for _, b, e, _ in lv1:
+            assert abs(cost[b:e].sum() - share) <= cost.max() + 1e-9
+
+
+def test_session_single_rank_matches_oracle():
+    """world_size 1 through the session with the oracle as the engine: the restatement's skeleton."""
+    import oracle as O
+    from fastbn_amd import pc_dist
+    csv = os.path.join(REPO, "tests", "golden", "alarm", "alarm_s5000.txt")
+    od = O.OracleDataset(csv=csv)
+    res = pc_dist.pc_skeleton_distributed(_oracle_engine(od), 37).result()
+    ref = od.pc_stable(0.05, 1000, 1)
+    assert res.edges == [tuple(e) for e in ref["edges"]]
+    assert res.sepset == {k: tuple(v) for k, v in ref["sepset"].items()}
+    assert res.tests_per_level.tolist() == list(ref["tests_per_level"])
 
 
 def test_two_rank_gloo_pc_skeleton_matches_oracle(tmp_path):
@@ -138,11 +191,14 @@ def test_two_rank_gloo_pc_skeleton_matches_oracle(tmp_path):
     csv = os.path.join(REPO, "tests", "golden", "alarm", "alarm_s5000.txt")
     out = str(tmp_path / "pc.npy")
     mp.start_processes(_pc_worker, args=(2, _free_port(), csv, out), nprocs=2, join=True, start_method="spawn")
-    edges, sep, tests = np.load(out, allow_pickle=True)  # written by this test's own worker
+    edges, sep, tests, oriented = np.load(out, allow_pickle=True)  # written by this test's own worker
     ref = O.OracleDataset(csv=csv).pc_stable(0.05, 1000, 1)
+    ref_sep = {k: tuple(v) for k, v in ref["sepset"].items()}
     assert [tuple(e) for e in edges] == [tuple(e) for e in ref["edges"]]
-    assert dict(sep) == {k: tuple(v) for k, v in ref["sepset"].items()}
+    assert dict(sep) == ref_sep
     assert list(tests) == list(ref["tests_per_level"])
+    import orient
+    assert [tuple(o) for o in oriented] == orient.orient(37, [tuple(e) for e in ref["edges"]], ref_sep)
 
 
 def _bcast_worker(rank, world, port, out_path):
