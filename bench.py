@@ -24,6 +24,7 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
+from fastbn_amd import shard  # noqa: E402
 ALARM = os.path.join(REPO, "tests", "golden", "alarm")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 CASES_PER_GPU = 100_000
@@ -108,7 +109,10 @@ def bench_pc(steps, warmup):
                                  "from any bandwidth bound (DESIGN.md 5.3)"}}
 
 
-def synth_c5(nvars=1000, nsamples=100_000):
+N_VARS_C5 = 1000
+
+
+def synth_c5(nvars=N_VARS_C5, nsamples=100_000):
     """SURVEY §8(d) config 5 dataset (fastbn_amd.synth.config5_dataset)."""
     from fastbn_amd import synth
     return synth.config5_dataset(nvars, nsamples)
@@ -152,6 +156,20 @@ def bench_pc_synth(steps, depth=6, cpu_vars=120):
                                 "levels >= 2 uint8 columns (N*(d+2) B, SURVEY 8(d)); the "
                                 "37.5 MB mask store is Infinity-cache resident, so HBM is not the binding "
                                 "limit at this size (byte_column_model_bytes: SURVEY's model for comparison)"}}
+    # the same workload through the native multi-GPU session at world size 1 (bench.py --gpus N
+    # runs it on N ranks): the per-level partition / record / apply overhead of the N > 1 path
+    from fastbn_amd import pc_dist
+    ci.set_kernel_timing(False)
+    td = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        res, dtests, _ = pc_dist.pc_stable_distributed(ci, N_VARS_C5, 0.05, depth)
+        td.append(time.perf_counter() - t0)
+    ci.set_kernel_timing(True)
+    out["session_world1"] = {"ms_per_run": 1e3 * float(np.median(td)), "tests": int(sum(dtests)),
+                             "same_skeleton": res.edges == pc.edges and res.sepset == pc.sepset,
+                             "note": "fbn_pc_dist_* session (the N > 1 path) at world size 1, Python level "
+                                     "loop + records included"}
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     od = O.OracleDataset(columns=cols[:cpu_vars], dims=dims[:cpu_vars])
@@ -164,6 +182,56 @@ def bench_pc_synth(steps, depth=6, cpu_vars=120):
     return out
 
 
+def bench_pc_synth_dist(steps, rank, world, device, depth=6):
+    """BASELINE config 5 on N GPUs: rank 0 generates the 1000 x 100k column store and one RCCL
+    broadcast puts it in every rank's HBM; each level's edges are partitioned over the ranks
+    (fbn_pc_dist_*), one all-gather of the records per level (+ the level-0 pair tables).  Timed
+    on the wall clock between barriers, max over ranks; the skeleton is checked against the
+    committed fixture (tests/golden/pc_c5.json) on rank 0."""
+    import torch
+    import torch.distributed as dist
+    from fastbn_amd import pc_dist
+    dev = torch.device("cuda", device)
+    cols, dims = synth_c5() if rank == 0 else (None, None)
+    meta = [list(cols.shape) if rank == 0 else None, dims.tolist() if rank == 0 else None]
+    dist.broadcast_object_list(meta, 0)
+    dims = np.array(meta[1], np.int32)
+    if dist.get_backend() == "nccl":  # RCCL: broadcast straight into device memory, records on the GPU
+        ci = pc_dist.independence_test_broadcast(cols, dims, meta[0], 0.05, device)
+        coll = dev
+    else:  # gloo rehearsal (ranks sharing a GPU): collectives on the CPU
+        import fastbn_amd as F
+        t = pc_dist.broadcast_columns(cols, meta[0]).to(dev)
+        torch.cuda.synchronize(dev)
+        ci = F.IndependenceTest.from_device(t.data_ptr(), meta[0][0], meta[0][1], dims, 0.05, device)
+        coll = None
+    ci.set_kernel_timing(False)
+    res, tests, launched = pc_dist.pc_stable_distributed(ci, N_VARS_C5, 0.05, depth, device=coll)  # warm-up
+    t = []
+    for _ in range(steps):
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        res, tests, launched = pc_dist.pc_stable_distributed(ci, N_VARS_C5, 0.05, depth, device=coll)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t.append(shard.max_over_ranks(time.perf_counter() - t0, dev))
+    ms = 1e3 * float(np.median(t))
+    out = {"metric": "PC-stable CI-tests/sec (synthetic 1000 vars x 100k samples, levels 0-5, BASELINE config 5)",
+           "value": sum(tests) / (ms * 1e-3), "unit": "CI-tests/s", "n_gpus": world, "tests": int(sum(tests)),
+           "tests_per_level": tests, "launched_per_level": launched, "ms_per_run": ms,
+           "edges": len(res.edges), "parallelism": f"edge ranges per level x{world}, one all-gather per level",
+           "timing": "wall clock between barriers, max over ranks, median of runs"}
+    if rank == 0:
+        import json as _json
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        from conftest import pc_digest
+        ref = _json.load(open(os.path.join(REPO, "tests", "golden", "pc_c5.json")))
+        out["matches_fixture"] = (tests == ref["tests_per_level"] and pc_digest(res.edges, res.sepset) ==
+                                  {k: ref[k] for k in ("edges_sha256", "sepsets_sha256")})
+    return out
+
+
 def bench_munin(steps, warmup, cases=125_000, rank=0, world=1, device=0):
     """the seeded Munin-like 1041-variable network at 20 % evidence (208
     variables per case), 125k cases per GPU -- on 8 GPUs the 1M-case job sharded by rank (seed
@@ -172,7 +240,7 @@ def bench_munin(steps, warmup, cases=125_000, rank=0, world=1, device=0):
     import tempfile
     import torch
     import fastbn_amd as F
-    from fastbn_amd import shard, synth
+    from fastbn_amd import synth
     dev = torch.device("cuda", device)
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "munin_like.xml")
@@ -310,7 +378,6 @@ def main():
     from fastbn_amd import synth
 
     net_py = synth.read_xmlbif(os.path.join(ALARM, "alarm.xml"))
-    from fastbn_amd import shard
     ev = synth.evidence_cases(net_py, args.cases, EVIDENCE_PER_CASE, seed=shard.synthetic_seed(20250131, rank))
     jt = F.JunctionTree(F.Network(os.path.join(ALARM, "alarm.xml")), device=local)
     if args.waves_per_cu:
@@ -393,6 +460,9 @@ def main():
     if world > 1 and not args.no_munin:
         # BASELINE config 4 at its real scale: 125k Munin-like cases per rank (1M on 8 GPUs)
         out["munin_like"] = bench_munin(3, 1, rank=rank, world=world, device=local)
+    if world > 1 and not args.no_pc:
+        # BASELINE config 5 on N GPUs: edge ranges per level, one all-gather per level
+        out["pc_synthetic"] = bench_pc_synth_dist(5, rank, world, local)
     if rank == 0 and world == 1:
         # PCIe-inclusive rate (host evidence in, host labels + marginals out through fbn_jt_run):
         # reported beside the metric, never as `value`

@@ -436,27 +436,7 @@ class PCResult:
 
     def __init__(self, handle):
         self._h = handle
-        ne, no = C.c_int(), C.c_int()
-        lib.fbn_pc_num_edges(handle, C.byref(ne))
-        e = np.zeros((max(ne.value, 1), 2), np.int32)
-        if ne.value:
-            lib.fbn_pc_edges(handle, _p(e))
-        self.edges = [tuple(map(int, x)) for x in e[:ne.value]]
-        ln = C.c_int64()
-        lib.fbn_pc_sepsets(handle, None, 0, C.byref(ln))
-        buf = np.zeros(max(ln.value, 1), np.int32)
-        lib.fbn_pc_sepsets(handle, _p(buf), ln.value, C.byref(ln))
-        self.sepset, k = {}, 0
-        while k < ln.value:
-            x, y, m = map(int, buf[k:k + 3])
-            self.sepset[(x, y)] = tuple(int(v) for v in buf[k + 3:k + 3 + m])
-            k += 3 + m
-        lib.fbn_pc_num_oriented_edges(handle, C.byref(no))
-        t = np.zeros((max(no.value, 1), 3), np.int32)
-        if no.value:
-            lib.fbn_pc_oriented_edges(handle, _p(t))
-        # (from, to, 1) arcs and (min, max, 0) undirected edges, in vec_edges order
-        self.oriented = [tuple(map(int, x)) for x in t[:no.value]]
+        self._edges = self._sepset = self._oriented = None
         m, near = C.c_double(), C.c_int64()
         lib.fbn_pc_decision_margin(handle, C.byref(m), C.byref(near))
         # p-values are parity-unpinned; decisions this close to alpha are flagged
@@ -479,6 +459,46 @@ class PCResult:
     @classmethod
     def with_levels(cls, handle):
         return cls(handle)
+
+    # skeleton / sepsets / orientation are converted to Python objects on first access (a
+    # 1000-variable run has ~500k sepsets: the conversion costs far more than the search)
+    @property
+    def edges(self):
+        if self._edges is None:
+            ne = C.c_int()
+            lib.fbn_pc_num_edges(self._h, C.byref(ne))
+            e = np.zeros((max(ne.value, 1), 2), np.int32)
+            if ne.value:
+                lib.fbn_pc_edges(self._h, _p(e))
+            self._edges = [tuple(map(int, x)) for x in e[:ne.value]]
+        return self._edges
+
+    @property
+    def sepset(self):
+        if self._sepset is None:
+            ln = C.c_int64()
+            lib.fbn_pc_sepsets(self._h, None, 0, C.byref(ln))
+            buf = np.zeros(max(ln.value, 1), np.int32)
+            lib.fbn_pc_sepsets(self._h, _p(buf), ln.value, C.byref(ln))
+            sep, k, b = {}, 0, buf.tolist()
+            while k < ln.value:
+                x, y, m = b[k], b[k + 1], b[k + 2]
+                sep[(x, y)] = tuple(b[k + 3:k + 3 + m])
+                k += 3 + m
+            self._sepset = sep
+        return self._sepset
+
+    @property
+    def oriented(self):
+        """(from, to, 1) arcs and (min, max, 0) undirected edges, in vec_edges order."""
+        if self._oriented is None:
+            no = C.c_int()
+            lib.fbn_pc_num_oriented_edges(self._h, C.byref(no))
+            t = np.zeros((max(no.value, 1), 3), np.int32)
+            if no.value:
+                lib.fbn_pc_oriented_edges(self._h, _p(t))
+            self._oriented = [tuple(map(int, x)) for x in t[:no.value]]
+        return self._oriented
 
     def GetSHD(self, bif_path):
         """BNSLComparison(ref_net, network).GetSHD() with ref_net loaded from a BIF file."""
@@ -528,11 +548,14 @@ class PCStable:
         lib.fbn_pc_stable(ci._h, self.alpha, self.depth, group_size, C.byref(r))
         self.result = res = PCResult(r)
         self.tests_per_level, self.launched_per_level = res.tests_per_level, res.launched_per_level
-        self.edges, self.sepset, self.oriented = res.edges, res.sepset, res.oriented
         self.total_s, self.kernel_s, self.device_bytes = res.total_s, res.kernel_s, res.device_bytes
         self.num_ci_test = res.num_ci_test
         self.min_margin, self.near_alpha = self.result.min_margin, self.result.near_alpha
         return self
+
+    edges = property(lambda self: self.result.edges)
+    sepset = property(lambda self: self.result.sepset)
+    oriented = property(lambda self: self.result.oriented)
 
     def GetSHD(self, bif_path):
         return self.result.GetSHD(bif_path)
