@@ -197,8 +197,18 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
                 term[c - c0] = t;
             }
             __syncthreads();
-            if (tid == 0)
-                for (int c = 0; c < c1 - c0; ++c) g2 += term[c];
+            if (tid == 0) {  // loads batched ahead of the dependent adds (LDS latency off the chain)
+                const int m = c1 - c0;
+                int c = 0;
+                for (; c + 8 <= m; c += 8) {
+                    double t[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) t[u] = term[c + u];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) g2 += t[u];
+                }
+                for (; c < m; ++c) g2 += term[c];
+            }
             __syncthreads();
         }
         if (tid == 0) {
