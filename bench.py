@@ -341,6 +341,64 @@ def bench_pc_synth_dist(steps, rank, world, device, depth=6):
     return out
 
 
+def bench_loaders(munin_xml=None):
+    """SURVEY §8(f) rank 4 at BASELINE scale: the native seeded generators (numpy-PCG64-identical,
+    multi-threaded) against synth.py's numpy versions, and the block-streamed, threaded text
+    loaders on a 100k x 1000 CSV (config 5) and a 1M-case LIBSVM test set (config 4: Munin-like,
+    208 evidence variables per case), each checked against what was written."""
+    import fastbn_amd as F
+    from fastbn_amd import synth
+    out = {"cpu": host_info()}
+    with tempfile.TemporaryDirectory() as td:
+        t0 = time.perf_counter()
+        cols, dims = synth.config5_dataset()
+        out["config5_numpy_generate_s"] = time.perf_counter() - t0
+        xml = os.path.join(td, "pc_c5.xml")
+        synth.random_network(N_VARS_C5, seed=1000, window=50, parent_probs=(1, 1, 1), dom=(2, 4), path=xml, k_min=0)
+        t0 = time.perf_counter()
+        cols_n = F.Network(xml).forward_sample(cols.shape[1], 1000)
+        out["config5_native_generate_s"] = time.perf_counter() - t0
+        out["config5_native_equals_numpy"] = bool(np.array_equal(cols_n, cols))
+        csv = os.path.join(td, "c5.csv")
+        t0 = time.perf_counter()
+        F.write_csv(csv, cols)
+        out["csv_write_s"] = time.perf_counter() - t0
+        out["csv_bytes"] = os.path.getsize(csv)
+        t0 = time.perf_counter()
+        ds = F.Dataset(csv)
+        out["csv_load_s"] = time.perf_counter() - t0
+        out["csv_shape"] = list(ds.columns.shape)
+        out["csv_load_GBs"] = out["csv_bytes"] / out["csv_load_s"] / 1e9
+        ok = ds.columns.shape == cols.shape
+        for v in range(0, cols.shape[0], 97):  # first-appearance recoding, spot columns
+            vals, first = np.unique(cols[v], return_index=True)
+            m = np.zeros(256, np.uint8)
+            m[vals[np.argsort(first)]] = np.arange(len(vals))
+            ok = ok and bool(np.array_equal(ds.columns[v], m[cols[v]]))
+        out["csv_coding_ok"] = ok
+        del ds, cols, cols_n
+        os.remove(csv)
+        if munin_xml is None:
+            munin_xml = os.path.join(td, "munin_like.xml")
+            synth.random_network(1041, seed=1041, window=12, path=munin_xml, name="munin_like")
+        net = F.Network(munin_xml)
+        t0 = time.perf_counter()
+        ev = net.evidence_cases(1_000_000, 208, 20250131)
+        out["munin_1M_native_generate_s"] = time.perf_counter() - t0
+        lib = os.path.join(td, "m1m.libsvm")
+        t0 = time.perf_counter()
+        F.write_libsvm(lib, ev)
+        out["libsvm_write_s"] = time.perf_counter() - t0
+        out["libsvm_bytes"] = os.path.getsize(lib)
+        t0 = time.perf_counter()
+        ev2, _ = F.load_libsvm(lib, net.num_nodes)
+        out["libsvm_load_s"] = time.perf_counter() - t0
+        out["libsvm_load_GBs"] = out["libsvm_bytes"] / out["libsvm_load_s"] / 1e9
+        out["libsvm_rows"] = int(ev2.shape[0])
+        out["libsvm_roundtrip_ok"] = bool(np.array_equal(ev, ev2))
+    return out
+
+
 def bench_munin(steps, warmup, cases=125_000, rank=0, world=1, device=0, with_baseline=False):
     """the seeded Munin-like 1041-variable network at 20 % evidence (208
     variables per case), 125k cases per GPU -- on 8 GPUs the 1M-case job sharded by rank (seed
@@ -354,11 +412,12 @@ def bench_munin(steps, warmup, cases=125_000, rank=0, world=1, device=0, with_ba
     tdir = tempfile.TemporaryDirectory()  # holds the XMLBIF until the CPU baseline has run
     path = os.path.join(tdir.name, "munin_like.xml")
     synth.random_network(1041, seed=1041, window=12, path=path, name="munin_like")
-    net = synth.read_xmlbif(path)
-    ev = synth.evidence_cases(net, cases, 208, seed=shard.synthetic_seed(20250131, rank))
     t0 = time.perf_counter()
-    jt = F.JunctionTree(F.Network(path), device=device)
+    fnet = F.Network(path)
+    jt = F.JunctionTree(fnet, device=device)
     plan_s = time.perf_counter() - t0
+    # native generator (bit-identical to synth.evidence_cases, multi-threaded)
+    ev = fnet.evidence_cases(cases, 208, shard.synthetic_seed(20250131, rank))
     if rank == 0:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle as O
@@ -463,6 +522,7 @@ def main():
     ap.add_argument("--no-baseline", action="store_true")
     ap.add_argument("--no-pc", action="store_true")
     ap.add_argument("--no-munin", action="store_true")
+    ap.add_argument("--no-loaders", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -489,9 +549,10 @@ def main():
     import fastbn_amd as F
     from fastbn_amd import synth
 
-    net_py = synth.read_xmlbif(os.path.join(ALARM, "alarm.xml"))
-    ev = synth.evidence_cases(net_py, args.cases, EVIDENCE_PER_CASE, seed=shard.synthetic_seed(20250131, rank))
-    jt = F.JunctionTree(F.Network(os.path.join(ALARM, "alarm.xml")), device=local)
+    alarm_net = F.Network(os.path.join(ALARM, "alarm.xml"))
+    # native generator (bit-identical to synth.evidence_cases, multi-threaded)
+    ev = alarm_net.evidence_cases(args.cases, EVIDENCE_PER_CASE, shard.synthetic_seed(20250131, rank))
+    jt = F.JunctionTree(alarm_net, device=local)
     if args.waves_per_cu:
         jt.set_waves_per_cu(args.waves_per_cu)
     info = jt.info
@@ -592,6 +653,8 @@ def main():
             out["munin_like"] = bench_munin(3, 1, with_baseline=not args.no_baseline)
         if not args.no_pc:
             out["pc_synthetic"] = bench_pc_synth(5, with_baseline=not args.no_baseline)
+        if not args.no_loaders:
+            out["loaders"] = bench_loaders()
         if not args.no_baseline:
             out["cpu_baseline"] = cpu_baseline_jt()
             if "pc_stable" in out:

@@ -25,9 +25,11 @@ from .api import (  # noqa: F401
     shd_bif,
     lib,
     load_libsvm,
+    write_csv,
+    write_libsvm,
     device_count,
     kernel_options,
 )
 
 __all__ = ["FastBNError", "Network", "Dataset", "JunctionTree", "IndependenceTest", "PCStable", "PCResult", "orient_skeleton", "shd_bif",
-           "lib", "load_libsvm", "device_count", "kernel_options"]
+           "lib", "load_libsvm", "write_csv", "write_libsvm", "device_count", "kernel_options"]

@@ -21,6 +21,10 @@ _SIGS = {
     "fbn_network_destroy": [_vp],
     "fbn_evidence_load_libsvm": [_cstr, C.c_int, _vp, _vp, _i64, _vp],
     "fbn_dataset_load_csv": [_cstr, _pp],
+    "fbn_synth_forward_sample": [_vp, _i64, C.c_uint64, _vp],
+    "fbn_synth_evidence": [_vp, _i64, C.c_int, C.c_uint64, C.c_int, _vp],
+    "fbn_write_csv": [_cstr, _vp, C.c_int, _i64, _vp],
+    "fbn_write_libsvm": [_cstr, _vp, _i64, C.c_int, _vp],
     "fbn_dataset_shape": [_vp, _vp, _vp],
     "fbn_dataset_dims": [_vp, _vp],
     "fbn_dataset_columns": [_vp, _vp],
@@ -171,10 +175,37 @@ class Network:
         lib.fbn_network_name(self._h, i, buf, 256)
         return buf.value.decode()
 
+    def forward_sample(self, n, seed):
+        """n complete cases, uint8 [V][n] (fbn_synth_forward_sample; = synth.forward_sample)."""
+        cols = np.empty((self.num_nodes, n), np.uint8)
+        lib.fbn_synth_forward_sample(self._h, int(n), int(seed), _p(cols))
+        return cols
+
+    def evidence_cases(self, n, k, seed, query=0):
+        """n evidence cases observing k variables each, int8 [n][V] (fbn_synth_evidence; =
+        synth.evidence_cases)."""
+        ev = np.empty((n, self.num_nodes), np.int8)
+        lib.fbn_synth_evidence(self._h, int(n), int(k), int(seed), int(query), _p(ev))
+        return ev
+
     def __del__(self):
         if getattr(self, "_h", None):
             lib.fbn_network_destroy(self._h)
             self._h = None
+
+
+def write_csv(path, columns, network=None):
+    """CSV of a column store (header + "s<code>" values), the reference's LoadCSVData input."""
+    cols = np.ascontiguousarray(columns, np.uint8)
+    lib.fbn_write_csv(os.fsencode(path), _p(cols), cols.shape[0], cols.shape[1], network._h if network else None)
+
+
+def write_libsvm(path, evidence, labels=None):
+    """LIBSVM test set of evidence rows (label + observed v:x), the reference's
+    LoadLIBSVMDataKnownNetwork input."""
+    ev = np.ascontiguousarray(evidence, np.int8)
+    lab = None if labels is None else np.ascontiguousarray(labels, np.int32)
+    lib.fbn_write_libsvm(os.fsencode(path), _p(ev), ev.shape[0], ev.shape[1], None if lab is None else _p(lab))
 
 
 def kernel_options():

@@ -106,12 +106,6 @@ int CheckDevice(int device, int *num_cu) {
 }  // namespace
 
 // =============================================================================================
-struct fbn_network {
-    fbn::Network net;
-};
-struct fbn_dataset {
-    fbn::Dataset ds;
-};
 
 struct fbn_jt_plan {
     fbn::JTPlanHost host;
@@ -272,16 +266,8 @@ int fbn_network_destroy(fbn_network *net) {
 int fbn_evidence_load_libsvm(const char *path, int num_nodes, int8_t *evidence, int32_t *labels, int64_t cap,
                              int64_t *ncases) {
     if (!path || num_nodes <= 0) return SetError(FBN_ERR_ARG, "bad argument");
-    std::vector<int8_t> ev;
-    std::vector<int32_t> lab;
-    int rc = fbn::LoadLibsvm(path, num_nodes, ev, lab);
-    if (rc) return rc;
-    int64_t n = (int64_t)lab.size();
-    if (ncases) *ncases = n;
-    int64_t m = std::min(n, cap);
-    if (evidence && m > 0) memcpy(evidence, ev.data(), (size_t)m * num_nodes);
-    if (labels && m > 0) memcpy(labels, lab.data(), (size_t)m * 4);
-    return FBN_OK;
+    // streaming parse straight into the caller's rows (no intermediate copy)
+    return fbn::LoadLibsvm(path, num_nodes, evidence && cap > 0 ? evidence : nullptr, labels, cap, ncases);
 }
 
 int fbn_dataset_load_csv(const char *path, fbn_dataset **out) {

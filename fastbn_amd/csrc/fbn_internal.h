@@ -38,7 +38,16 @@ struct Dataset {
     std::vector<uint8_t> cols;  // [var][sample]
 };
 int LoadCsv(const std::string &path, Dataset &ds);
-int LoadLibsvm(const std::string &path, int num_nodes, std::vector<int8_t> &ev, std::vector<int32_t> &labels);
+// ev == nullptr: only *nrows; otherwise the first min(rows, cap) rows into ev [row][num_nodes] / labels
+int LoadLibsvm(const std::string &path, int num_nodes, int8_t *ev, int32_t *labels, int64_t cap, int64_t *nrows);
+
+// seeded generators (synth.cpp): numpy-PCG64-identical forward sampling and evidence cases, and
+// writers of the reference's text formats
+int ForwardSample(const Network &net, int64_t n, uint64_t seed, uint8_t *cols);
+int EvidenceCases(const Network &net, int64_t n, int k, uint64_t seed, int query, int8_t *ev);
+int WriteCsv(const std::string &path, const uint8_t *cols, int nvars, int64_t n, const std::vector<std::string> &names,
+             const std::vector<std::vector<std::string>> &values);
+int WriteLibsvm(const std::string &path, const int8_t *ev, int64_t n, int V, const int32_t *labels);
 
 // ---------------------------------------------------------------------------------------------
 // junction-tree static plan (host), container order as in JunctionTreeStructure
@@ -116,5 +125,13 @@ int GenerateJTKernel(const JTPlanHost &plan, std::string &src, int64_t *wave_ent
                      int64_t *lds_bytes = nullptr);
 
 }  // namespace fbn
+
+// C-ABI handles over the host model (capi.hip, synth.cpp)
+struct fbn_network {
+    fbn::Network net;
+};
+struct fbn_dataset {
+    fbn::Dataset ds;
+};
 
 #endif

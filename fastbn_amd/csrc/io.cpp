@@ -5,8 +5,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <fstream>
 #include <sstream>
+#include <thread>
 #include <unordered_map>
 
 #include "fbn_internal.h"
@@ -213,66 +215,206 @@ int LoadXmlbif(const std::string &path, Network &net) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Streaming, multi-threaded text scanning: the file is read in blocks of kBlock bytes; each block's
+// complete lines are cut into one part per thread at line boundaries and parsed in parallel; the
+// parts are then merged in file order (so every order-dependent result -- first-appearance codes,
+// row indices -- is the sequential one).  Memory: one block plus the outputs.
+namespace {
+
+constexpr size_t kBlock = 64u << 20;
+
+int NumThreads() {
+    const unsigned hc = std::thread::hardware_concurrency();
+    int t = (int)std::max(1u, std::min(16u, hc ? hc : 1u));  // the GPU box's CPU share is 16
+    if (const char *e = getenv("OMP_NUM_THREADS")) t = std::max(1, std::min(t, atoi(e)));
+    return t;
+}
+
+// calls fn(lines_begin, lines_end, is_last_block) for consecutive blocks of complete lines; the
+// final unterminated line (if any) is passed as the last block's tail
+template <class F>
+int ForEachBlock(const std::string &path, F fn) {
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) return SetError(FBN_ERR_IO, "cannot open %s", path.c_str());
+    std::vector<char> buf;
+    size_t carry = 0;
+    while (true) {
+        buf.resize(carry + kBlock);
+        const size_t got = fread(buf.data() + carry, 1, kBlock, f);
+        const size_t have = carry + got;
+        const bool eof = got < kBlock;
+        size_t end = have;
+        if (!eof) {  // cut after the last newline; the rest carries over
+            const char *p = buf.data();
+            size_t k = have;
+            while (k > 0 && p[k - 1] != '\n') --k;
+            if (k == 0) {  // one line longer than a block: read on
+                carry = have;
+                continue;
+            }
+            end = k;
+        }
+        int rc = fn(buf.data(), buf.data() + end, eof);
+        if (rc) {
+            fclose(f);
+            return rc;
+        }
+        if (eof) break;
+        carry = have - end;
+        memmove(buf.data(), buf.data() + end, carry);
+    }
+    fclose(f);
+    return FBN_OK;
+}
+
+// cut [b, e) into up to T parts at line boundaries
+std::vector<std::pair<const char *, const char *>> CutLines(const char *b, const char *e, int T) {
+    std::vector<std::pair<const char *, const char *>> parts;
+    const char *p = b;
+    for (int t = 0; t < T && p < e; ++t) {
+        const char *q = t == T - 1 ? e : std::min(e, p + (e - b) / T + 1);
+        if (q < e) {
+            const char *nl = (const char *)memchr(q, '\n', (size_t)(e - q));
+            q = nl ? nl + 1 : e;
+        }
+        parts.push_back({p, q});
+        p = q;
+    }
+    return parts;
+}
+
+template <class F>
+void Parallel(int n, F fn) {
+    std::vector<std::thread> th;
+    for (int i = 1; i < n; ++i) th.emplace_back(fn, i);
+    fn(0);
+    for (auto &t : th) t.join();
+}
+
+// one line [b, e) without its '\n', right-trimmed (chars < 33, as the reference's Trim)
+inline void TrimRight(const char *b, const char *&e) {
+    while (e > b && (unsigned char)e[-1] < 33) --e;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
 // CSV training set: header + string values coded by first appearance per column
 // (src/Dataset.cpp:267-414).  Trailing empty lines are ignored (the reference would read past the
-// end of the row vector there).
+// end of the row vector there).  A row's last variable ends at the next ',' if the row
+// has extra fields (they are ignored); a row with fewer fields is an error.
 int LoadCsv(const std::string &path, Dataset &ds) {
-    std::string s;
-    if (!ReadFile(path, s)) return SetError(FBN_ERR_IO, "cannot open %s", path.c_str());
     ds = Dataset();
-    size_t pos = 0, n = s.size();
-    auto next_line = [&](std::string &line) {
-        if (pos >= n) return false;
-        size_t e = s.find('\n', pos);
-        if (e == std::string::npos) e = n;
-        line.assign(s, pos, e - pos);
-        pos = e + 1;
-        size_t t = line.size();
-        while (t > 0 && (unsigned char)line[t - 1] < 33) --t;  // TrimRight
-        line.resize(t);
-        return true;
+    const int T = NumThreads();
+    bool header_done = false;
+    std::vector<std::vector<std::string>> gdict;     // global first-appearance dictionaries
+    std::vector<std::vector<uint8_t>> colv;          // per-column codes, file order
+    struct Part {
+        std::vector<uint8_t> rows;                   // row-major local codes
+        std::vector<std::vector<std::string>> dict;  // local dictionaries
+        int64_t nrows = 0;
+        int err = 0, err_var = 0;
+        int64_t err_row = 0;
     };
-    std::string line;
-    if (!next_line(line)) return SetError(FBN_ERR_IO, "%s: empty file", path.c_str());
-    {
-        size_t b = 0, e;
-        while ((e = line.find(',', b)) != std::string::npos) {
-            ds.names.push_back(line.substr(b, e - b));
-            b = e + 1;
-        }
-        ds.names.push_back(line.substr(b));
-    }
-    ds.nvars = (int)ds.names.size();
-    std::vector<std::unordered_map<std::string, int>> code(ds.nvars);
-    std::vector<std::vector<uint8_t>> rows(ds.nvars);
-    while (next_line(line)) {
-        if (line.empty()) continue;
-        size_t b = 0;
-        for (int v = 0; v < ds.nvars; ++v) {
-            size_t e = line.find(',', b);
-            if (e == std::string::npos) {
-                if (v != ds.nvars - 1) return SetError(FBN_ERR_IO, "%s: short row at sample %lld", path.c_str(), (long long)ds.nsamples);
-                e = line.size();
+    int rc = ForEachBlock(path, [&](const char *b, const char *e, bool) -> int {
+        if (!header_done) {
+            const char *nl = (const char *)memchr(b, '\n', (size_t)(e - b));
+            const char *he = nl ? nl : e;
+            TrimRight(b, he);
+            const char *p = b;
+            while (true) {
+                const char *c = (const char *)memchr(p, ',', (size_t)(he - p));
+                ds.names.emplace_back(p, c ? c : he);
+                if (!c) break;
+                p = c + 1;
             }
-            std::string f = line.substr(b, e - b);
-            b = e + 1;
-            auto it = code[v].find(f);
-            int c;
-            if (it == code[v].end()) {
-                c = (int)code[v].size();
-                if (c > 255) return SetError(FBN_ERR_LIMIT, "%s: column %d has more than 256 values", path.c_str(), v);
-                code[v].emplace(f, c);
-            } else {
-                c = it->second;
-            }
-            rows[v].push_back((uint8_t)c);
+            if (b == e) return SetError(FBN_ERR_IO, "%s: empty file", path.c_str());
+            ds.nvars = (int)ds.names.size();
+            gdict.assign(ds.nvars, {});
+            colv.assign(ds.nvars, {});
+            header_done = true;
+            b = nl ? nl + 1 : e;
         }
-        ds.nsamples++;
-    }
+        const int V = ds.nvars;
+        auto parts = CutLines(b, e, T);
+        std::vector<Part> P(parts.size());
+        Parallel((int)parts.size(), [&](int t) {
+            Part &pt = P[t];
+            pt.dict.assign(V, {});
+            const char *p = parts[t].first, *pe = parts[t].second;
+            while (p < pe && !pt.err) {
+                const char *nl = (const char *)memchr(p, '\n', (size_t)(pe - p));
+                const char *le = nl ? nl : pe;
+                const char *ls = p;
+                p = nl ? nl + 1 : pe;
+                TrimRight(ls, le);
+                if (ls == le) continue;  // empty line
+                const char *f = ls;
+                for (int v = 0; v < V; ++v) {
+                    const char *c = (const char *)memchr(f, ',', (size_t)(le - f));
+                    if (!c) {
+                        if (v != V - 1) {
+                            pt.err = 1, pt.err_row = pt.nrows;
+                            break;
+                        }
+                        c = le;
+                    }
+                    const size_t len = (size_t)(c - f);
+                    auto &d = pt.dict[v];
+                    size_t k = 0;
+                    while (k < d.size() && !(d[k].size() == len && memcmp(d[k].data(), f, len) == 0)) ++k;
+                    if (k == d.size()) {
+                        if (k >= 256) {
+                            pt.err = 2, pt.err_var = v;
+                            break;
+                        }
+                        d.emplace_back(f, len);
+                    }
+                    pt.rows.push_back((uint8_t)k);
+                    f = c + 1;
+                }
+                if (!pt.err) ++pt.nrows;
+            }
+        });
+        // merge in file order: local -> global codes (first appearance), append per column
+        int64_t base = ds.nsamples;
+        for (auto &pt : P) {
+            if (pt.err == 1)
+                return SetError(FBN_ERR_IO, "%s: short row at sample %lld", path.c_str(), (long long)(base + pt.err_row));
+            if (pt.err == 2) return SetError(FBN_ERR_LIMIT, "%s: column %d has more than 256 values", path.c_str(), pt.err_var);
+            base += pt.nrows;
+        }
+        std::vector<std::vector<uint8_t>> remap(P.size(), std::vector<uint8_t>((size_t)V * 256));
+        for (size_t t = 0; t < P.size(); ++t)
+            for (int v = 0; v < V; ++v)
+                for (size_t k = 0; k < P[t].dict[v].size(); ++k) {
+                    auto &g = gdict[v];
+                    size_t j = 0;
+                    while (j < g.size() && g[j] != P[t].dict[v][k]) ++j;
+                    if (j == g.size()) {
+                        if (j >= 256) return SetError(FBN_ERR_LIMIT, "%s: column %d has more than 256 values", path.c_str(), v);
+                        g.push_back(P[t].dict[v][k]);
+                    }
+                    remap[t][(size_t)v * 256 + k] = (uint8_t)j;
+                }
+        std::vector<int64_t> row0(P.size() + 1, ds.nsamples);
+        for (size_t t = 0; t < P.size(); ++t) row0[t + 1] = row0[t] + P[t].nrows;
+        for (int v = 0; v < V; ++v) colv[v].resize((size_t)row0.back());
+        Parallel((int)P.size(), [&](int t) {
+            const uint8_t *r = P[t].rows.data();
+            const uint8_t *m = remap[t].data();
+            for (int64_t i = 0; i < P[t].nrows; ++i, r += V)
+                for (int v = 0; v < V; ++v) colv[v][(size_t)(row0[t] + i)] = m[(size_t)v * 256 + r[v]];
+        });
+        ds.nsamples = row0.back();
+        return FBN_OK;
+    });
+    if (rc) return rc;
+    if (!header_done) return SetError(FBN_ERR_IO, "%s: empty file", path.c_str());
     ds.cols.resize((size_t)ds.nvars * ds.nsamples);
     for (int v = 0; v < ds.nvars; ++v) {
-        std::copy(rows[v].begin(), rows[v].end(), ds.cols.begin() + (size_t)v * ds.nsamples);
-        ds.dims.push_back((int32_t)code[v].size());
+        std::copy(colv[v].begin(), colv[v].end(), ds.cols.begin() + (size_t)v * ds.nsamples);
+        ds.dims.push_back((int32_t)gdict[v].size());
     }
     return FBN_OK;
 }
@@ -280,42 +422,72 @@ int LoadCsv(const std::string &path, Dataset &ds) {
 // ---------------------------------------------------------------------------------------------
 // LIBSVM test set -> evidence (src/Dataset.cpp:162-262, src/Inference.cpp:13-42).  The reference's
 // `getline; while(!eof)` loop skips a final line without '\n'; reproduced.  Features with an index
-// >= num_nodes are ignored (src/JunctionTree.cpp:326-331).
-int LoadLibsvm(const std::string &path, int num_nodes, std::vector<int8_t> &ev, std::vector<int32_t> &labels) {
-    std::string s;
-    if (!ReadFile(path, s)) return SetError(FBN_ERR_IO, "cannot open %s", path.c_str());
-    ev.clear();
-    labels.clear();
-    size_t pos = 0, n = s.size();
-    while (pos < n) {
-        size_t e = s.find('\n', pos);
-        if (e == std::string::npos) break;  // unterminated last line: not read by the reference
-        std::string line = s.substr(pos, e - pos);
-        pos = e + 1;
-        size_t t = line.size();
-        while (t > 0 && (unsigned char)line[t - 1] < 33) --t;
-        line.resize(t);
-        std::vector<int8_t> row(num_nodes, -1);
-        size_t b = 0;
-        bool first = true;
-        while (true) {
-            size_t sp = line.find(' ', b);
-            std::string tok = line.substr(b, sp == std::string::npos ? std::string::npos : sp - b);
-            if (first) {
-                labels.push_back(atoi(tok.c_str()));
-                first = false;
-            } else {
-                size_t c = tok.find(':');
-                if (c == std::string::npos) return SetError(FBN_ERR_IO, "%s: bad feature '%s'", path.c_str(), tok.c_str());
-                int idx = atoi(tok.substr(0, c).c_str());
-                int val = atoi(tok.substr(c + 1).c_str());
-                if (idx >= 0 && idx < num_nodes) row[idx] = (int8_t)val;
-            }
-            if (sp == std::string::npos) break;
-            b = sp + 1;
+// >= num_nodes are ignored (src/JunctionTree.cpp:326-331).  ev == nullptr: count the rows only;
+// otherwise the first min(rows, cap) rows are written to ev [row][num_nodes] / labels.
+int LoadLibsvm(const std::string &path, int num_nodes, int8_t *ev, int32_t *labels, int64_t cap, int64_t *nrows) {
+    const int T = NumThreads();
+    int64_t row = 0;
+    int rc = ForEachBlock(path, [&](const char *b, const char *e, bool last) -> int {
+        if (last) {  // drop an unterminated final line
+            const char *k = e;
+            while (k > b && k[-1] != '\n') --k;
+            e = k;
         }
-        ev.insert(ev.end(), row.begin(), row.end());
-    }
+        auto parts = CutLines(b, e, T);
+        std::vector<int64_t> cnt(parts.size(), 0);
+        Parallel((int)parts.size(), [&](int t) {
+            for (const char *p = parts[t].first; p < parts[t].second;) {
+                const char *nl = (const char *)memchr(p, '\n', (size_t)(parts[t].second - p));
+                if (!nl) break;
+                ++cnt[t];
+                p = nl + 1;
+            }
+        });
+        std::vector<int64_t> r0(parts.size() + 1, row);
+        for (size_t t = 0; t < parts.size(); ++t) r0[t + 1] = r0[t] + cnt[t];
+        if (ev && row < cap) {
+            std::vector<std::string> errs(parts.size());
+            Parallel((int)parts.size(), [&](int t) {
+                int64_t r = r0[t];
+                for (const char *p = parts[t].first; p < parts[t].second && r < cap; ++r) {
+                    const char *nl = (const char *)memchr(p, '\n', (size_t)(parts[t].second - p));
+                    const char *ls = p, *le = nl;
+                    p = nl + 1;
+                    TrimRight(ls, le);
+                    int8_t *out = ev + (size_t)r * num_nodes;
+                    memset(out, -1, (size_t)num_nodes);
+                    // tokens separated by single spaces: the label, then idx:val features
+                    const char *q = ls;
+                    bool first = true;
+                    while (true) {
+                        const char *sp = (const char *)memchr(q, ' ', (size_t)(le - q));
+                        const char *te = sp ? sp : le;
+                        if (first) {
+                            if (labels) labels[r] = atoi(std::string(q, te).c_str());
+                            first = false;
+                        } else {
+                            const char *c = (const char *)memchr(q, ':', (size_t)(te - q));
+                            if (!c) {
+                                errs[t] = std::string(q, te);
+                                return;
+                            }
+                            const int idx = atoi(std::string(q, c).c_str());
+                            const int val = atoi(std::string(c + 1, te).c_str());
+                            if (idx >= 0 && idx < num_nodes) out[idx] = (int8_t)val;
+                        }
+                        if (!sp) break;
+                        q = sp + 1;
+                    }
+                }
+            });
+            for (auto &m : errs)
+                if (!m.empty()) return SetError(FBN_ERR_IO, "%s: bad feature '%s'", path.c_str(), m.c_str());
+        }
+        row = r0.back();
+        return FBN_OK;
+    });
+    if (rc) return rc;
+    if (nrows) *nrows = row;
     return FBN_OK;
 }
 

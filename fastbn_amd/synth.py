@@ -91,6 +91,7 @@ def evidence_cases(net, n, k, seed, query=0):
     full = forward_sample(net, n, seed)
     rng = np.random.Generator(np.random.PCG64(seed + 1))
     cand = np.array([v for v in range(V) if v != query])
+    k = max(0, min(k, cand.size))
     keys = rng.random((n, cand.size))
     # k distinct candidates per case: the k smallest keys (argpartition: same set as a full sort)
     pick = cand[np.argpartition(keys, k - 1, axis=1)[:, :k]] if 0 < k < cand.size else cand[np.argsort(keys, axis=1)[:, :k]]

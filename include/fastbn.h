@@ -57,6 +57,17 @@ int fbn_network_destroy(fbn_network *net);
 int fbn_evidence_load_libsvm(const char *path, int num_nodes, int8_t *evidence, int32_t *labels,
                              int64_t cap, int64_t *ncases);
 
+/* Seeded workload generators (the reference's SampleSetGenerator is wall-clock seeded
+ * and unreachable): forward sampling of n complete cases (cols [V][n] uint8, the reference's CPT
+ * convention) and n evidence cases observing k variables each, never `query`, -1 elsewhere
+ * (evidence [n][V] int8).  Bit-identical to fastbn_amd/synth.py's numpy PCG64(seed) generators. */
+int fbn_synth_forward_sample(const fbn_network *net, int64_t n, uint64_t seed, uint8_t *cols);
+int fbn_synth_evidence(const fbn_network *net, int64_t n, int k, uint64_t seed, int query, int8_t *evidence);
+/* Writers of the reference's input formats (multi-threaded): CSV with header (network names or
+ * X<v>) and values "s<code>"; LIBSVM rows "label v:x ..." of the observed variables. */
+int fbn_write_csv(const char *path, const uint8_t *cols, int nvars, int64_t n, const fbn_network *net);
+int fbn_write_libsvm(const char *path, const int8_t *evidence, int64_t n, int num_nodes, const int32_t *labels);
+
 typedef struct fbn_dataset fbn_dataset;
 /* CSV with header and string values coded by first appearance; column store uint8 [var][sample].
  * Replaces Dataset::LoadCSVData + RowMajor2ColumnMajor (src/Dataset.cpp:267-414,568-580). */

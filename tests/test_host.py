@@ -212,3 +212,67 @@ def test_streamed_schedule_respects_tree_dependencies(tmp_path, net):
             if parent[c] in pos:
                 assert pos[parent[c]] < pos[c]
     assert 0.5 < jt.info["streamed_split_efficiency"] <= 1.0 or W == 1
+
+
+# ------------------------------------------------------------- native generators and text loaders
+def test_native_generators_match_numpy(alarm_paths, tmp_path):
+    """fbn_synth_forward_sample / fbn_synth_evidence draw exactly numpy's PCG64(seed) stream
+    (SeedSequence, XSL-RR, 53-bit doubles, jump-ahead per thread): bit-identical to synth.py."""
+    import fastbn_amd as F
+    from fastbn_amd import synth
+    net, py = F.Network(alarm_paths["xml"]), synth.read_xmlbif(alarm_paths["xml"])
+    for seed in (0, 1, 1000, 20250131, 2 ** 40 + 7):
+        np.testing.assert_array_equal(net.forward_sample(3001, seed), synth.forward_sample(py, 3001, seed))
+    for n, k in ((1, 7), (513, 7), (20000, 7), (300, 0), (50, 36), (50, 40)):
+        np.testing.assert_array_equal(net.evidence_cases(n, k, 20250131), synth.evidence_cases(py, n, k, 20250131))
+    p = str(tmp_path / "syn.xml")
+    synth.random_network(300, seed=5, window=12, path=p)
+    np.testing.assert_array_equal(F.Network(p).evidence_cases(4097, 60, 9), synth.evidence_cases(synth.read_xmlbif(p), 4097, 60, 9))
+
+
+def test_csv_writer_and_streaming_loader(tmp_path, monkeypatch):
+    """fbn_write_csv -> fbn_dataset_load_csv (block-streamed, threaded): codes in first-appearance
+    order per column (src/Dataset.cpp:334-342) across block and thread boundaries."""
+    import fastbn_amd as F
+    rng = np.random.default_rng(3)
+    cols = rng.integers(0, 4, (7, 50001)).astype(np.uint8)
+    cols[2] = 3 - cols[2] // 2  # codes whose first appearance is not 0, 1, ...
+    cols[5] = 0  # a constant column
+    p = str(tmp_path / "d.csv")
+    F.write_csv(p, cols)
+    for threads in ("1", "3", "8"):
+        monkeypatch.setenv("OMP_NUM_THREADS", threads)
+        ds = F.Dataset(p)
+        assert ds.names == [f"X{v}" for v in range(7)]
+        for v in range(7):
+            vals, first = np.unique(cols[v], return_index=True)
+            m = np.zeros(256, np.uint8)
+            m[vals[np.argsort(first)]] = np.arange(len(vals))
+            np.testing.assert_array_equal(ds.columns[v], m[cols[v]])
+            assert ds.dims[v] == len(vals)
+
+
+def test_libsvm_writer_and_streaming_loader(alarm_paths, tmp_path, monkeypatch):
+    """fbn_write_libsvm -> fbn_evidence_load_libsvm round trip (labels, -1 for unobserved), and
+    the reference's loader quirk: an unterminated last line is not read (src/Dataset.cpp:162-262)."""
+    import fastbn_amd as F
+    net = F.Network(alarm_paths["xml"])
+    ev = net.evidence_cases(20001, 7, 4)
+    lab = (np.arange(20001) % 3).astype(np.int32)
+    p = str(tmp_path / "e.libsvm")
+    F.write_libsvm(p, ev, lab)
+    for threads in ("1", "5"):
+        monkeypatch.setenv("OMP_NUM_THREADS", threads)
+        e2, l2 = F.load_libsvm(p, 37)
+        np.testing.assert_array_equal(e2, ev)
+        np.testing.assert_array_equal(l2, lab)
+    with open(p, "ab") as f:
+        f.write(b"1 3:1")  # no newline: skipped like the reference's getline/eof loop
+    e3, _ = F.load_libsvm(p, 37)
+    assert e3.shape[0] == 20001
+    # the shipped test set through the new loader = the oracle's loader
+    e4, l4 = F.load_libsvm(alarm_paths["test"], 37)
+    import oracle as O
+    oe, ol = O.load_libsvm(alarm_paths["test"], 37)
+    np.testing.assert_array_equal(e4, oe)
+    np.testing.assert_array_equal(l4, ol)
