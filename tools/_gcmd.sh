@@ -1,7 +1,6 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-export TMPDIR=/tmp
-mkdir -p gpurun_out/pcprof
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/pcprof/alarm -o run --output-format csv -- python tools/pc_alarm_timing.py > gpurun_out/pcprof/alarm.log 2>&1
-cat gpurun_out/pcprof/alarm.log | tail -2
-find gpurun_out/pcprof/alarm -name "*kernel_stats.csv" -exec cut -c1-200 {} \; | head -20
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/gpu_tests.log; exit 1; }
+tail -2 gpurun_out/gpu_tests.log
+timeout -k 10 600 python -u bench.py > gpurun_out/bench_r2b.json 2> gpurun_out/bench_r2b.err || { echo "bench failed"; tail -30 gpurun_out/bench_r2b.err; exit 1; }
+echo bench ok
