@@ -33,9 +33,14 @@ extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *di
                                          double *g2, int32_t *df, double *p, uint8_t *indep, int32_t *counts,
                                          int32_t *counts0, unsigned long long *stats, const int32_t *rowcnt,
                                          int32_t *pairtab, int pmode, int nvars, int num_cu, long long t0,
-                                         hipStream_t s);
+                                         int counted, hipStream_t s);
 extern "C" hipError_t fbn_ci_bits_rowcount(const uint32_t *bits, long long rows, long long W, int32_t *rowcnt,
                                            hipStream_t s);
+extern "C" int fbn_ci_pair_block(int d);
+extern "C" hipError_t fbn_ci_bits_pairs_tiled(const uint32_t *bits, const int32_t *row0, const int32_t *rowcnt,
+                                              long long W, const int32_t *tasks, long long ntasks, int nvars,
+                                              long long t0, long long t1, int32_t *counts, int32_t *pairtab,
+                                              int num_cu, hipStream_t s);
 extern "C" hipError_t fbn_jt_virt_launch(const JtVClique *cls, const int32_t *aux, const double *initv,
                                          const uint64_t *dig, const int32_t *order, const int32_t *sched,
                                          const int32_t *vsel, const int8_t *evid, double *marg, int32_t *labels,
@@ -171,6 +176,9 @@ struct fbn_ci_ctx {
     // pair tables of every (i < j), 16 counts each, recorded by level 0 of a PC run and used by its
     // level-1 tests (pair_mode: 0 off, 1 record at the next marginal batch, 2 use if recorded)
     DevBuf pairtab;
+    // register-blocked level-0 tasks (ci_bits_pairs_tiled) of the pair range [ptask_t0, ptask_t1)
+    DevBuf ptasks;
+    int64_t ptask_t0 = -1, ptask_t1 = -1, ptask_n = 0;
     int pair_mode = 0;
     bool pairs_recorded = false;
     bool bits_ready = false;
@@ -898,6 +906,70 @@ int fbn_ci_dataset_from_device(const uint8_t *d_cols, int nvars, int64_t nsample
     return CiCreate(d_cols, true, nvars, nsamples, dims, device, out);
 }
 
+// Tasks of the register-blocked level-0 kernel for the pairs [t0, t1) of the complete graph (pair
+// index = lexicographic (u < v) order): x-side variables = the range's rows u, y-side = all variables,
+// both cut into sorted blocks per state-count class (fbn_ci_pair_block); a task is kept if it holds
+// a pair (x < y) of the range, so every pair of the range is in exactly one task (x-side = its u).
+// Cached per range (a PC run's level 0 repeats it).
+static int CiPairTasks(fbn_ci_ctx *c, int64_t t0, int64_t t1, hipStream_t s) {
+    if (c->ptask_t0 == t0 && c->ptask_t1 == t1) return FBN_OK;
+    const int nv = c->nvars;
+    const int64_t P = (int64_t)nv * (nv - 1) / 2;
+    auto row_of = [&](int64_t t) {  // u of pair t
+        int64_t lo = 0, hi = nv - 2;
+        while (lo < hi) {
+            const int64_t m = (lo + hi + 1) / 2;
+            if (m * nv - m * (m + 1) / 2 <= t) lo = m;
+            else hi = m - 1;
+        }
+        return (int)lo;
+    };
+    auto idx = [&](int64_t u, int64_t v) { return u * nv - u * (u + 1) / 2 + (v - u - 1); };
+    const int u0 = t1 > t0 ? row_of(t0) : 0, u1 = t1 > t0 ? row_of(t1 - 1) : -1;
+    const bool full = t0 == 0 && t1 == P;
+    std::vector<int> cls[5], ucls[5];
+    for (int v = 0; v < nv; ++v) {
+        const int d = c->dims[v];
+        if (d < 1 || d > 4) return SetError(FBN_ERR_ARG, "blocked pairs: variable %d has %d states", v, d);
+        cls[d].push_back(v);
+        if (v >= u0 && v <= u1) ucls[d].push_back(v);
+    }
+    std::vector<int32_t> tasks;
+    for (int dx = 1; dx <= 4; ++dx)
+        for (int dy = 1; dy <= 4; ++dy) {
+            const int bx = fbn_ci_pair_block(dx), by = fbn_ci_pair_block(dy);
+            const std::vector<int> &X = ucls[dx], &Y = cls[dy];
+            for (size_t i = 0; i < X.size(); i += bx) {
+                const int nxs = (int)std::min<size_t>(bx, X.size() - i);
+                for (size_t j = 0; j < Y.size(); j += by) {
+                    const int nys = (int)std::min<size_t>(by, Y.size() - j);
+                    if (Y[j + nys - 1] <= X[i]) continue;  // no y above any x
+                    bool any = full;
+                    for (int a = 0; a < nxs && !any; ++a)
+                        for (int b = 0; b < nys && !any; ++b) {
+                            const int x = X[i + a], y = Y[j + b];
+                            if (x < y) {
+                                const int64_t t = idx(x, y);
+                                any = t >= t0 && t < t1;
+                            }
+                        }
+                    if (!any) continue;
+                    const size_t o = tasks.size();
+                    tasks.resize(o + 12, -1);
+                    tasks[o] = dx, tasks[o + 1] = dy, tasks[o + 2] = nxs, tasks[o + 3] = nys;
+                    for (int a = 0; a < nxs; ++a) tasks[o + 4 + a] = X[i + a];
+                    for (int b = 0; b < nys; ++b) tasks[o + 8 + b] = Y[j + b];
+                }
+            }
+        }
+    int rc;
+    if ((rc = c->ptasks.ensure(std::max<size_t>(tasks.size(), 1) * 4))) return rc;
+    if (!tasks.empty()) FBN_HIP(hipMemcpyAsync(c->ptasks.p, tasks.data(), tasks.size() * 4, hipMemcpyHostToDevice, s));
+    FBN_HIP(hipStreamSynchronize(s));  // the host vector goes out of scope
+    c->ptask_t0 = t0, c->ptask_t1 = t1, c->ptask_n = (int64_t)tasks.size() / 12;
+    return FBN_OK;
+}
+
 // items: host copy (validated here).  zc_items / zc_indep / zc_df: optional device-visible
 // (pinned, mapped) host buffers the kernels read the items from and write the decisions to
 // directly -- no staging copies for the small batches of a latency-bound driver round.
@@ -976,14 +1048,25 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         const int64_t skipped = d == 0 ? 2 : (pmode == 2 ? 3 : 0);
         S.last_bytes = (dim_rows - skipped * n) * c->bits_W * 4;
         if (c->timing) FBN_HIP(hipEventRecord(S.ev0, s));
-        hipError_t e = fbn_ci_bits_launch(c->bits.as<uint32_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(),
+        // all pairs of a range: register-blocked count kernel (ci_bits_pairs_tiled), then phase 2
+        const bool tiled = all_pairs && d == 0 && !getenv("FBN_CI_NO_TILED");
+        if (tiled && (rc = CiPairTasks(c, pair0, pair0 + n, s))) return rc;
+        hipError_t e = hipSuccess;
+        if (tiled) {
+            e = fbn_ci_bits_pairs_tiled(c->bits.as<uint32_t>(), c->brow.as<int32_t>(), c->browcnt.as<int32_t>(),
+                                        c->bits_W, c->ptasks.as<int32_t>(), c->ptask_n, c->nvars, pair0, pair0 + n,
+                                        S.bcounts.as<int32_t>(), pmode == 1 ? c->pairtab.as<int32_t>() : nullptr,
+                                        c->num_cu, s);
+            if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci tiled pairs launch: %s", hipGetErrorString(e));
+        }
+        e = fbn_ci_bits_launch(c->bits.as<uint32_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(),
                                           ditems, c->bits_W, n, d, alpha,
                                           want_g2p ? c->g2.as<double>() : nullptr, zc_df ? zc_df : S.df.as<int32_t>(),
                                           want_g2p ? c->p.as<double>() : nullptr,
                                           zc_indep ? zc_indep : S.indep.as<uint8_t>(),
                                           S.bcounts.as<int32_t>(), counts_dev, c->stats.as<unsigned long long>(),
                                           c->browcnt.as<int32_t>(), c->pairtab.as<int32_t>(), pmode, c->nvars,
-                                          c->num_cu, (long long)pair0, s);
+                                          c->num_cu, (long long)pair0, tiled ? 1 : 0, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci bits kernel launch: %s", hipGetErrorString(e));
         if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
         return FBN_OK;

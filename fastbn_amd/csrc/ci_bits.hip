@@ -17,6 +17,7 @@
 // bit for bit).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "ci_chisq.h"
 
@@ -261,6 +262,142 @@ __device__ __forceinline__ void pair_of(long long t, int nv, int &x, int &y) {
 
 constexpr int kBitsCells = 64;  // count slots per test
 
+// ---- register-blocked marginal tests (a PC run's level 0, all pairs of a pair-index range)
+// One wave per task = a block of BX x-variables x BY y-variables of one state-count class each
+// (tasks built on the host, CiPairTasks in capi.hip): per 4-word step every mask row of the block's
+// variables is loaded once and feeds every pair of the block, so L2 / fabric traffic per pair drops
+// from (dx-1 + dy-1) rows to (BX (dx-1) + BY (dy-1)) / (BX BY) rows.  A pair is the block's
+// (x, y) with x < y and its index in [t0, t1) (each pair of the range exactly once); the counts
+// and the derived last row / column are exactly count_pair's (Counts2D, src/CellTable.cpp:430-455).
+template <int DX, int DY>
+struct PairBlock {
+    static constexpr int MX = DX - 1, MY = DY - 1;
+    static constexpr int BX = MX <= 1 ? 4 : (MX == 2 ? 3 : 2), BY = MY <= 1 ? 4 : (MY == 2 ? 3 : 2);
+    static constexpr int NCC = MX * MY > 0 ? MX * MY : 1;
+};
+constexpr int kPairTaskInts = 12;  // dx, dy, nx, ny, xs[4], ys[4]
+
+template <int DX, int DY>
+__device__ __forceinline__ void pair_block(const uint32_t *__restrict__ bits, const int32_t *__restrict__ row0,
+                                           const int32_t *__restrict__ rowcnt, long long W,
+                                           const int32_t *__restrict__ task, int nvars, long long t0, long long t1,
+                                           int32_t *__restrict__ counts, int32_t *__restrict__ pairtab, int lane) {
+    using PB = PairBlock<DX, DY>;
+    constexpr int MX = PB::MX, MY = PB::MY, BX = PB::BX, BY = PB::BY, NCC = PB::NCC;
+    const int nx = task[2], ny = task[3];
+    int xs[BX], ys[BY];
+#pragma unroll
+    for (int a = 0; a < BX; ++a) xs[a] = task[4 + (a < nx ? a : 0)];  // padding repeats the first
+#pragma unroll
+    for (int b = 0; b < BY; ++b) ys[b] = task[8 + (b < ny ? b : 0)];
+    uint32_t cnt[BX][BY][NCC];
+#pragma unroll
+    for (int a = 0; a < BX; ++a)
+#pragma unroll
+        for (int b = 0; b < BY; ++b)
+#pragma unroll
+            for (int c = 0; c < NCC; ++c) cnt[a][b][c] = 0u;
+    if (MX > 0 && MY > 0) {
+        typedef __attribute__((ext_vector_type(4))) unsigned u4;
+        const uint32_t *px[BX], *py[BY];
+#pragma unroll
+        for (int a = 0; a < BX; ++a) px[a] = bits + (size_t)row0[xs[a]] * W;
+#pragma unroll
+        for (int b = 0; b < BY; ++b) py[b] = bits + (size_t)row0[ys[b]] * W;
+        for (long long w4 = lane; 4 * w4 < W; w4 += 64) {
+            u4 xv[BX][MX > 0 ? MX : 1], yv[BY][MY > 0 ? MY : 1];
+#pragma unroll
+            for (int a = 0; a < BX; ++a)
+#pragma unroll
+                for (int r = 0; r < MX; ++r) xv[a][r] = *reinterpret_cast<const u4 *>(px[a] + r * W + 4 * w4);
+#pragma unroll
+            for (int b = 0; b < BY; ++b)
+#pragma unroll
+                for (int r = 0; r < MY; ++r) yv[b][r] = *reinterpret_cast<const u4 *>(py[b] + r * W + 4 * w4);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int a = 0; a < BX; ++a)
+#pragma unroll
+                    for (int r = 0; r < MX; ++r)
+#pragma unroll
+                        for (int b = 0; b < BY; ++b)
+#pragma unroll
+                            for (int q = 0; q < MY; ++q) cnt[a][b][r * MY + q] += __builtin_popcount(xv[a][r][k] & yv[b][q][k]);
+        }
+#pragma unroll
+        for (int a = 0; a < BX; ++a)
+#pragma unroll
+            for (int b = 0; b < BY; ++b)
+#pragma unroll
+                for (int c = 0; c < NCC; ++c) {
+                    uint32_t v = cnt[a][b][c];
+#pragma unroll
+                    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+                    cnt[a][b][c] = v;
+                }
+    }
+#pragma unroll
+    for (int a = 0; a < BX; ++a)
+#pragma unroll
+        for (int b = 0; b < BY; ++b) {
+            const int x = xs[a], y = ys[b];
+            const int u = x < y ? x : y, v = x < y ? y : x;
+            const long long t = (long long)u * nvars - (long long)u * (u + 1) / 2 + (v - u - 1);
+            if (!(a < nx && b < ny && x < y && t >= t0 && t < t1)) continue;  // wave-uniform
+            const int32_t *cx = rowcnt + row0[x], *cy = rowcnt + row0[y];
+            int32_t full[DX * DY];
+#pragma unroll
+            for (int i = 0; i < MX; ++i) {
+                int32_t r = cx[i];
+#pragma unroll
+                for (int j = 0; j < MY; ++j) full[i * DY + j] = (int32_t)cnt[a][b][i * MY + j], r -= full[i * DY + j];
+                full[i * DY + MY] = r;
+            }
+#pragma unroll
+            for (int j = 0; j < DY; ++j) {
+                int32_t r = cy[j];
+#pragma unroll
+                for (int i = 0; i < MX; ++i) r -= full[i * DY + j];
+                full[MX * DY + j] = r;
+            }
+            if (lane < DX * DY) {
+                int32_t val = 0;
+#pragma unroll
+                for (int c = 0; c < DX * DY; ++c) val = lane == c ? full[c] : val;
+                // x < y here: the table is N[value of x][value of y] (Counts2D of the pair (u, v))
+                int32_t *out = counts + (t - t0) * kBitsCells;
+                out[lane] = val;
+                if (pairtab) pairtab[16 * t + lane] = val;
+            }
+        }
+}
+
+__global__ __launch_bounds__(256) void ci_bits_pairs_tiled(const uint32_t *__restrict__ bits,
+                                                           const int32_t *__restrict__ row0,
+                                                           const int32_t *__restrict__ rowcnt, long long W,
+                                                           const int32_t *__restrict__ tasks, long long ntasks,
+                                                           int nvars, long long t0, long long t1,
+                                                           int32_t *__restrict__ counts, int32_t *__restrict__ pairtab) {
+    const int lane = threadIdx.x & 63;
+    for (long long k = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); k < ntasks; k += (long long)gridDim.x * 4) {
+        const int32_t *task = tasks + k * kPairTaskInts;
+        switch (task[0] * 8 + task[1]) {
+#define FBN_PB(A, B)                                                                                       \
+    case A * 8 + B:                                                                                        \
+        pair_block<A, B>(bits, row0, rowcnt, W, task, nvars, t0, t1, counts, pairtab, lane);               \
+        break;
+            FBN_PB(1, 1) FBN_PB(1, 2) FBN_PB(1, 3) FBN_PB(1, 4)
+            FBN_PB(2, 1) FBN_PB(2, 2) FBN_PB(2, 3) FBN_PB(2, 4)
+            FBN_PB(3, 1) FBN_PB(3, 2) FBN_PB(3, 3) FBN_PB(3, 4)
+            FBN_PB(4, 1) FBN_PB(4, 2) FBN_PB(4, 3) FBN_PB(4, 4)
+#undef FBN_PB
+        default: break;
+        }
+    }
+}
+
+
 // phase 1: counts[t][64] of every test, one wave per test; D = 0 (x, y) or 1 (x, y, z)
 template <int D>
 __global__ __launch_bounds__(256) void ci_bits_count(const uint32_t *__restrict__ bits, const int32_t *__restrict__ dims,
@@ -479,18 +616,33 @@ extern "C" hipError_t fbn_ci_bits_build(const uint8_t *cols, const int32_t *dims
     return hipGetLastError();
 }
 
+// block size per state-count class (the host builds tasks with these)
+extern "C" int fbn_ci_pair_block(int d) { return d - 1 <= 1 ? 4 : (d - 1 == 2 ? 3 : 2); }
+
+extern "C" hipError_t fbn_ci_bits_pairs_tiled(const uint32_t *bits, const int32_t *row0, const int32_t *rowcnt,
+                                              long long W, const int32_t *tasks, long long ntasks, int nvars,
+                                              long long t0, long long t1, int32_t *counts, int32_t *pairtab,
+                                              int num_cu, hipStream_t s) {
+    const long long g = (ntasks + 3) / 4, cap = (long long)num_cu * 8;
+    if (ntasks > 0)
+        hipLaunchKernelGGL(ci_bits_pairs_tiled, dim3((unsigned)(g < cap ? g : cap)), dim3(256), 0, s, bits, row0,
+                           rowcnt, W, tasks, ntasks, nvars, t0, t1, counts, pairtab);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *dims, const int32_t *row0,
                                          const int32_t *items, long long W, long long n, int d, double alpha,
                                          double *g2, int32_t *df, double *p, uint8_t *indep, int32_t *counts,
                                          int32_t *counts0, unsigned long long *stats, const int32_t *rowcnt,
                                          int32_t *pairtab, int pmode, int nvars, int num_cu, long long t0,
-                                         hipStream_t s) {
+                                         int counted, hipStream_t s) {
     const long long g1 = (n + 3) / 4, cap = (long long)num_cu * 8;
     const long long g2g = (n + 255) / 256;
     const dim3 b1((unsigned)(g1 < cap ? g1 : cap)), b2((unsigned)(g2g < cap ? g2g : cap));
     if (d == 0) {
-        hipLaunchKernelGGL(ci_bits_count<0>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts, rowcnt,
-                           pmode == 1 ? pairtab : nullptr, nvars, t0);
+        if (!counted)  // counted = 1: the counts are already in place (ci_bits_pairs_tiled)
+            hipLaunchKernelGGL(ci_bits_count<0>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts, rowcnt,
+                               pmode == 1 ? pairtab : nullptr, nvars, t0);
         hipLaunchKernelGGL(ci_bits_g2<0>, b2, dim3(256), 0, s, counts, dims, items, n, alpha, g2, df, p, indep,
                            counts0, stats, nvars, t0);
     } else if (d == 1) {
