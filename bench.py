@@ -214,16 +214,49 @@ def bench_pc(steps, warmup):
             "unit": "CI-tests/s", "tests": pc.num_ci_test, "tests_per_level": pc.tests_per_level.tolist(),
             "launched_per_level": pc.launched_per_level.tolist(), "ms_per_run": ms,
             "kernel_ms_per_run": 1e3 * pc.kernel_s, "edges": len(pc.edges),
-            "roofline": {"bound": "hbm", "achieved": pc.device_bytes / pc.kernel_s / 1e9, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": pc.device_bytes / pc.kernel_s / 1e9 / HBM_PEAK_GBS,
-                         "algorithmic_bytes": pc.device_bytes,
-                         "note": "N*(d+2) uint8 column bytes per launched test (SURVEY 8(d)) over the CI kernels' "
-                                 "time; the 185 KB column store is cache resident and each level is a few-"
-                                 "microsecond-per-test latency chain (5 dependent launches), so this is far "
-                                 "from any bandwidth bound (DESIGN.md 5.3)"}}
+            "roofline": {"bound": "latency", "kernel_ms_per_run": 1e3 * pc.kernel_s, "wall_ms_per_run": ms,
+                         "column_bytes_read_per_run": pc.device_bytes,
+                         "note": "five dependent levels of a few microseconds of kernels each on a 185 KB column "
+                                 "store that stays in cache: a launch/latency chain, not bound by HBM or VALU "
+                                 "(DESIGN.md 5.3)"}}
 
 
 N_VARS_C5 = 1000
+
+
+INT_VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9  # MI355X: a wave64 32-bit VALU instruction issues in 2 cycles
+
+
+def pc_roofline(kernel_s, device_bytes, byte_column_bytes):
+    """Config 5's CI kernels against the bounds they can hit: 32-bit VALU issue (popcount / AND
+    for the bit-sliced kernels, the binning for the histogram kernel) and L2<->fabric traffic, per
+    PC run; VALU instructions and fabric bytes per run from the committed PMC profile
+    (profiles/pc5_kernels.json: rocprofv3 --pmc SQ_INSTS_VALU / FETCH_SIZE / WRITE_SIZE, calibrated),
+    the kernel time measured live (HIP events around every CI batch of a run)."""
+    path = os.path.join(REPO, "profiles", "pc5_kernels.json")
+    out = {"kernel_ms_per_run": 1e3 * kernel_s, "column_bytes_read_per_run": device_bytes,
+           "byte_column_model_bytes": byte_column_bytes}
+    if not os.path.exists(path):
+        return {"bound": None, **out}
+    with open(path) as f:
+        prof = json.load(f)
+    ks = {k: v for k, v in prof["kernels"].items()
+          if k not in ("ci_cols_check", "ci_bits_build", "ci_bits_rowcount")}  # once per dataset
+    ops = sum(v["valu_lane_ops_per_run"] for v in ks.values())
+    fab = sum(v["fabric_bytes_per_run"] for v in ks.values())
+    valu = ops / kernel_s / INT_VALU_PEAK_LANE_OPS
+    fabric = fab / kernel_s / (HBM_PEAK_GBS * 1e9)
+    top = max(ks, key=lambda k: ks[k]["time_ms_per_run"])
+    if valu >= fabric:
+        r = {"bound": "valu", "achieved": ops / kernel_s / 1e12, "peak": INT_VALU_PEAK_LANE_OPS / 1e12,
+             "unit": "Tlane-op/s", "frac": valu}
+    else:
+        r = {"bound": "hbm", "achieved": fab / kernel_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": fabric}
+    return {**r, "traffic": fab, "valu_frac": valu, "fabric_frac": fabric, **out,
+            "dominant_kernel": {top: ks[top]}, "source": "profiles/pc5_kernels.json",
+            "note": "all CI kernels of one run: PMC VALU lane-ops and calibrated L2<->fabric bytes per run over the "
+                    "live kernel time; neither bound is reached (bit-sliced kernels: 2-3 waves per SIMD, "
+                    "per-wave reductions; DESIGN.md 5.3)"}
 
 
 def synth_c5(nvars=N_VARS_C5, nsamples=100_000):
@@ -262,15 +295,7 @@ def bench_pc_synth(steps, depth=6, cpu_vars=160, with_baseline=True):
            "value": tests / (ms * 1e-3), "unit": "CI-tests/s", "tests": tests,
            "tests_per_level": pc.tests_per_level.tolist(), "launched_per_level": launched, "ms_per_run": ms,
            "kernel_ms_per_run": 1e3 * kern_s, "edges": len(pc.edges),
-           "roofline": {"bound": "hbm", "achieved": alg / kern_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": alg / kern_s / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": alg,
-                        "byte_column_model_bytes": sum(n_d * N * (d + 2) for d, n_d in enumerate(launched)),
-                        "note": "algorithmic = column data each launched test must read once, in the format "
-                                "the kernel reads: levels 0-1 bit-sliced mask rows ((dx-1+dy-1[+dz-1]) * N/8 B: "
-                                "the last value of each variable is derived from counts, ci_bits.hip), "
-                                "levels >= 2 uint8 columns (N*(d+2) B, SURVEY 8(d)); the "
-                                "37.5 MB mask store is Infinity-cache resident, so HBM is not the binding "
-                                "limit at this size (byte_column_model_bytes: SURVEY's model for comparison)"}}
+           "roofline": pc_roofline(kern_s, alg, sum(n_d * N * (d + 2) for d, n_d in enumerate(launched)))}
     # the same workload through the native multi-GPU session at world size 1 (bench.py --gpus N
     # runs it on N ranks): the per-level partition / record / apply overhead of the N > 1 path
     from fastbn_amd import pc_dist
