@@ -12,6 +12,7 @@
 
 #include "fbn_internal.h"
 #include "pc_internal.h"
+#include "ci_chisq.h"
 
 extern "C" hipError_t fbn_jt_launch(const JtOp *ops, int nops, const int32_t *aux, const double *initv,
                                     const uint64_t *dig, const int8_t *evid, int V, long long ncases, int SD,
@@ -33,7 +34,7 @@ extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *di
                                          double *g2, int32_t *df, double *p, uint8_t *indep, int32_t *counts,
                                          int32_t *counts0, unsigned long long *stats, const int32_t *rowcnt,
                                          int32_t *pairtab, int pmode, int nvars, int num_cu, long long t0,
-                                         int counted, hipStream_t s);
+                                         int counted, const double *band, int nband, hipStream_t s);
 extern "C" hipError_t fbn_ci_bits_rowcount(const uint32_t *bits, long long rows, long long W, int32_t *rowcnt,
                                            hipStream_t s);
 extern "C" int fbn_ci_pair_block(int d);
@@ -181,6 +182,11 @@ struct fbn_ci_ctx {
     int64_t ptask_t0 = -1, ptask_t1 = -1, ptask_n = 0;
     int pair_mode = 0;
     bool pairs_recorded = false;
+    // decision band of the bit-sliced G^2 kernel for alpha = band_alpha (ci_chisq.h fbn_chisq_band):
+    // [lo, hi] per df 1..kBandDf, then delta; host copy kept alive for the async upload
+    DevBuf band;
+    std::vector<double> band_host;
+    double band_alpha = -1.0;
     bool bits_ready = false;
     int64_t bits_W = 0;
     CiSlot slot[2];
@@ -191,6 +197,28 @@ struct fbn_ci_ctx {
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
+
+// df <= 36 covers every bit-sliced test (<= 4 states, <= 1 conditioning variable: 4 * 3 * 3)
+constexpr int kBandDf = 36;
+
+// the band for `alpha` (delta = alpha / 4), computed on the host once per ctx and alpha; nullptr
+// (p evaluated for every test) when alpha is outside (0, 1) or FBN_CI_NO_BAND is set
+static int CiBand(fbn_ci_ctx *c, double alpha, hipStream_t s, const double **out) {
+    *out = nullptr;
+    if (!(alpha > 0.0 && alpha < 1.0) || getenv("FBN_CI_NO_BAND")) return FBN_OK;
+    if (c->band_alpha != alpha) {
+        const double delta = alpha / 4;
+        c->band_host.assign(2 * kBandDf + 1, 0.0);
+        for (int df = 1; df <= kBandDf; ++df)
+            fbn_chisq_band(alpha, delta, df, &c->band_host[2 * df - 2], &c->band_host[2 * df - 1]);
+        c->band_host[2 * kBandDf] = delta;
+        if (int rc = c->band.ensure(c->band_host.size() * 8)) return rc;
+        FBN_HIP(hipMemcpyAsync(c->band.p, c->band_host.data(), c->band_host.size() * 8, hipMemcpyHostToDevice, s));
+        c->band_alpha = alpha;
+    }
+    *out = c->band.as<double>();
+    return FBN_OK;
+}
 
 static int PinnedEnsure(void *&ptr, size_t &have, size_t want) {
     if (want <= have) return FBN_OK;
@@ -1047,6 +1075,8 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         // is derived, not read (ci_bits.hip)
         const int64_t skipped = d == 0 ? 2 : (pmode == 2 ? 3 : 0);
         S.last_bytes = (dim_rows - skipped * n) * c->bits_W * 4;
+        const double *band = nullptr;  // decisions only: p evaluated inside the band
+        if (!want_g2p && (rc = CiBand(c, alpha, s, &band))) return rc;
         if (c->timing) FBN_HIP(hipEventRecord(S.ev0, s));
         // all pairs of a range: register-blocked count kernel (ci_bits_pairs_tiled), then phase 2
         const bool tiled = all_pairs && d == 0 && !getenv("FBN_CI_NO_TILED");
@@ -1066,7 +1096,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
                                           zc_indep ? zc_indep : S.indep.as<uint8_t>(),
                                           S.bcounts.as<int32_t>(), counts_dev, c->stats.as<unsigned long long>(),
                                           c->browcnt.as<int32_t>(), c->pairtab.as<int32_t>(), pmode, c->nvars,
-                                          c->num_cu, (long long)pair0, tiled ? 1 : 0, s);
+                                          c->num_cu, (long long)pair0, tiled ? 1 : 0, band, kBandDf, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci bits kernel launch: %s", hipGetErrorString(e));
         if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
         return FBN_OK;

@@ -448,15 +448,30 @@ __device__ __forceinline__ const int32_t *pair_table(const int32_t *pairtab, int
     const int i = u < v ? u : v, j = u < v ? v : u;
     return pairtab + 16 * ((long long)i * nvars - (long long)i * (i + 1) / 2 + (j - i - 1));
 }
-__global__ __launch_bounds__(256) void ci_bits_count_derived(const uint32_t *__restrict__ bits,
+// XCD-contiguous work split: workgroups are dispatched round-robin over the 8 XCDs (block b on XCD
+// b % 8), each with its own L2.  Cutting the n units into 8 contiguous ranges, range j worked by
+// XCD j's blocks in order, keeps consecutive units -- an edge's candidate conditioning variables,
+// which share the x and y mask rows -- in one L2 at about the same time.  xcd = 0: plain grid stride.
+struct XcdSplit {
+    long long first, end, stride;
+};
+__device__ __forceinline__ XcdSplit xcd_split(long long n, int wave, int per_block, int xcd) {
+    const long long G = gridDim.x, b = blockIdx.x;
+    if (!xcd || G < 8) return {b * per_block + wave, n, G * per_block};
+    const long long j = b % 8, nb = (G - j + 7) / 8, i = b / 8;
+    return {n * j / 8 + i * per_block + wave, n * (j + 1) / 8, nb * per_block};
+}
+
+__device__ __forceinline__ void count_derived_items(const uint32_t *__restrict__ bits,
                                                              const int32_t *__restrict__ dims,
                                                              const int32_t *__restrict__ row0,
                                                              const int32_t *__restrict__ items, long long W, long long n,
                                                              int32_t *__restrict__ counts,
-                                                             const int32_t *__restrict__ pairtab, int nvars) {
+                                                             const int32_t *__restrict__ pairtab, int nvars,
+                                                             int xcd) {
     const int lane = threadIdx.x & 63;
-    const long long wave = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    for (long long t = wave; t < n; t += (long long)gridDim.x * 4) {
+    const XcdSplit sp = xcd_split(n, threadIdx.x >> 6, 4, xcd);
+    for (long long t = sp.first; t < sp.end; t += sp.stride) {
         const int x = items[3 * t], y = items[3 * t + 1], z = items[3 * t + 2];
         const int dx = dims[x], dy = dims[y], dz = dims[z];
         const uint32_t *bx = bits + (size_t)row0[x] * W, *by = bits + (size_t)row0[y] * W,
@@ -482,81 +497,341 @@ __global__ __launch_bounds__(256) void ci_bits_count_derived(const uint32_t *__r
     }
 }
 
-// phase 2: one lane per test -- per z: marginals, adjusted df; G^2 as one running sum in the
-// reference's z -> x -> y order (ComputeGSquareXY / XYZ, src/IndependenceTest.cpp:65-155,
-// 295-364; the same arithmetic as ci_g2_kernel), p = 1 - P(df/2, G^2/2) (ci_chisq.h)
+// the kernel's register count is the largest instantiation's (DX = DY = DZ = 4); FBN_CI_L1WAVES
+// asks the compiler for more waves per SIMD instead (fewer registers, more L2 round trips in flight)
+#define FBN_DERIVED_KERNEL(NAME, ATTR)                                                                          \
+    __global__ __launch_bounds__(256) ATTR void NAME(const uint32_t *__restrict__ bits,                        \
+                                                     const int32_t *__restrict__ dims,                         \
+                                                     const int32_t *__restrict__ row0,                         \
+                                                     const int32_t *__restrict__ items, long long W, long long n, \
+                                                     int32_t *__restrict__ counts,                             \
+                                                     const int32_t *__restrict__ pairtab, int nvars, int xcd) {  \
+        count_derived_items(bits, dims, row0, items, W, n, counts, pairtab, nvars, xcd);                       \
+    }
+FBN_DERIVED_KERNEL(ci_bits_count_derived, )
+FBN_DERIVED_KERNEL(ci_bits_count_derived_w4, __attribute__((amdgpu_waves_per_eu(4))))
+FBN_DERIVED_KERNEL(ci_bits_count_derived_w5, __attribute__((amdgpu_waves_per_eu(5))))
+FBN_DERIVED_KERNEL(ci_bits_count_derived_w6, __attribute__((amdgpu_waves_per_eu(6))))
+#undef FBN_DERIVED_KERNEL
+
+// level >= 1 of a PC run, grouped: consecutive items that share (x, y) -- an edge's candidate
+// conditioning variables, which the driver emits contiguously -- are counted together: per 4-word
+// step the x and y mask rows are loaded once and x_a & y_b formed once for the whole group, each
+// item adds only its z rows.  Per item the counts and the derived last values are exactly
+// count_test_derived's (z's state count is a runtime value here, <= 4).  Quads of items that do not
+// share (x, y) fall back to count_test_derived item by item.
+template <int DX, int DY>
+__device__ __forceinline__ void count_group_derived(const uint32_t *__restrict__ bits, const int32_t *__restrict__ dims,
+                                                    const int32_t *__restrict__ row0, const int32_t *__restrict__ items,
+                                                    long long t0, int m, long long W, int lane,
+                                                    int32_t *__restrict__ counts, const int32_t *__restrict__ pairtab,
+                                                    int nvars, int32_t *__restrict__ sc) {
+    constexpr int MX = DX - 1, MY = DY - 1, NXY = MX * MY > 0 ? MX * MY : 1;
+    constexpr int G = MX * MY >= 6 ? 2 : 4;  // items per register group
+    typedef __attribute__((ext_vector_type(4))) unsigned u4;
+    const int x = items[3 * t0], y = items[3 * t0 + 1];
+    const uint32_t *bx = bits + (size_t)row0[x] * W, *by = bits + (size_t)row0[y] * W;
+    const int32_t *Txy = pair_table(pairtab, nvars, x, y);
+    const bool txy = x > y;
+    for (int g0 = 0; g0 < m; g0 += G) {
+        const int gm = m - g0 < G ? m - g0 : G;
+        int zv[G], dz[G];
+        const uint32_t *bz[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            zv[g] = items[3 * (t0 + g0 + (g < gm ? g : 0)) + 2];
+            dz[g] = g < gm ? dims[zv[g]] : 1;  // a padding item counts nothing
+            bz[g] = bits + (size_t)row0[zv[g]] * W;
+        }
+        uint32_t cnt[G][3][NXY];
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+#pragma unroll
+                for (int k = 0; k < NXY; ++k) cnt[g][c][k] = 0u;
+        if (MX > 0 && MY > 0) {
+            for (long long w4 = lane; 4 * w4 < W; w4 += 64) {
+                u4 xv[MX > 0 ? MX : 1], yv[MY > 0 ? MY : 1];
+#pragma unroll
+                for (int a = 0; a < MX; ++a) xv[a] = *reinterpret_cast<const u4 *>(bx + a * W + 4 * w4);
+#pragma unroll
+                for (int b = 0; b < MY; ++b) yv[b] = *reinterpret_cast<const u4 *>(by + b * W + 4 * w4);
+                u4 zr[G][3];
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c)
+                        zr[g][c] = c < dz[g] - 1 ? *reinterpret_cast<const u4 *>(bz[g] + c * W + 4 * w4)
+                                                 : u4{0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int a = 0; a < MX; ++a)
+#pragma unroll
+                        for (int b = 0; b < MY; ++b) {
+                            const uint32_t xy = xv[a][k] & yv[b][k];
+#pragma unroll
+                            for (int g = 0; g < G; ++g)
+#pragma unroll
+                                for (int c = 0; c < 3; ++c)
+                                    cnt[g][c][a * MY + b] += __builtin_popcount(xy & zr[g][c][k]);  // absent rows are 0
+                        }
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int c = 0; c < 3; ++c)
+#pragma unroll
+                    for (int k = 0; k < NXY; ++k) {
+                        uint32_t v = cnt[g][c][k];
+#pragma unroll
+                        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+                        cnt[g][c][k] = v;
+                    }
+        }
+        // complete each item's table from the pair tables (count_test_derived's derivation, integer
+        // and so order-free): the reduced counts go through this wave's LDS slot, then lane = cell
+        if (lane == 0)
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int c = 0; c < 3; ++c)
+#pragma unroll
+                    for (int k = 0; k < NXY; ++k) sc[(g * 3 + c) * NXY + k] = (int32_t)cnt[g][c][k];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int a = (lane / DY) % DX, b = lane % DY, c = lane / (DX * DY);
+        for (int g = 0; g < gm; ++g) {
+            const int z = zv[g], DZ = dz[g], MZ = DZ - 1;
+            if (lane >= DZ * DX * DY) continue;
+            const int32_t *Txz = pair_table(pairtab, nvars, x, z), *Tyz = pair_table(pairtab, nvars, y, z);
+            const bool txz = x > z, tyz = y > z;
+            auto S = [&](int cc, int aa, int bb) { return sc[(g * 3 + cc) * NXY + aa * MY + bb]; };
+            auto nxz = [&](int aa, int cc) { return txz ? Txz[cc * DX + aa] : Txz[aa * DZ + cc]; };
+            auto nyz = [&](int bb, int cc) { return tyz ? Tyz[cc * DY + bb] : Tyz[bb * DZ + cc]; };
+            auto fxz = [&](int cc, int aa) {  // N[cc][aa][DY-1]
+                int32_t r = nxz(aa, cc);
+#pragma unroll
+                for (int bb = 0; bb < MY; ++bb) r -= S(cc, aa, bb);
+                return r;
+            };
+            auto f = [&](int cc, int bb) {  // N[cc][a][bb], cc < MZ
+                if (a < MX) return bb < MY ? S(cc, a, bb) : fxz(cc, a);
+                int32_t r = nyz(bb, cc);
+#pragma unroll
+                for (int aa = 0; aa < MX; ++aa) r -= bb < MY ? S(cc, aa, bb) : fxz(cc, aa);
+                return r;
+            };
+            int32_t v;
+            if (c < MZ) {
+                v = f(c, b);
+            } else {
+                v = txy ? Txy[b * DX + a] : Txy[a * DY + b];
+                for (int cc = 0; cc < MZ; ++cc) v -= f(cc, b);
+            }
+            counts[(t0 + g0 + g) * kBitsCells + lane] = v;
+        }
+        __builtin_amdgcn_wave_barrier();  // the slot is rewritten by the next group
+    }
+}
+
+__global__ __launch_bounds__(256) void ci_bits_count_derived_grp(const uint32_t *__restrict__ bits,
+                                                                 const int32_t *__restrict__ dims,
+                                                                 const int32_t *__restrict__ row0,
+                                                                 const int32_t *__restrict__ items, long long W,
+                                                                 long long n, int32_t *__restrict__ counts,
+                                                                 const int32_t *__restrict__ pairtab, int nvars,
+                                                                 int xcd) {
+    __shared__ int32_t slots[4][2 * 3 * 9];  // per wave: a group's reduced counts
+    const int lane = threadIdx.x & 63;
+    int32_t *sc = slots[threadIdx.x >> 6];
+    const XcdSplit sp = xcd_split((n + 3) / 4, threadIdx.x >> 6, 4, xcd);
+    for (long long q = sp.first; q < sp.end; q += sp.stride) {
+        const long long t0 = 4 * q;
+        const int m = n - t0 < 4 ? (int)(n - t0) : 4;
+        const int x = items[3 * t0], y = items[3 * t0 + 1];
+        bool same = true;
+        for (int g = 1; g < m; ++g) same = same && items[3 * (t0 + g)] == x && items[3 * (t0 + g) + 1] == y;
+        if (same) {
+            switch (dims[x] * 8 + dims[y]) {
+#define FBN_GRP(A, B)                                                                                        \
+    case A * 8 + B:                                                                                          \
+        count_group_derived<A, B>(bits, dims, row0, items, t0, m, W, lane, counts, pairtab, nvars, sc);      \
+        break;
+                FBN_GRP(1, 1) FBN_GRP(1, 2) FBN_GRP(1, 3) FBN_GRP(1, 4)
+                FBN_GRP(2, 1) FBN_GRP(2, 2) FBN_GRP(2, 3) FBN_GRP(2, 4)
+                FBN_GRP(3, 1) FBN_GRP(3, 2) FBN_GRP(3, 3) FBN_GRP(3, 4)
+                FBN_GRP(4, 1) FBN_GRP(4, 2) FBN_GRP(4, 3) FBN_GRP(4, 4)
+#undef FBN_GRP
+            default: break;
+            }
+            continue;
+        }
+        for (int g = 0; g < m; ++g) {  // mixed quad: item by item
+            const long long t = t0 + g;
+            const int xi = items[3 * t], yi = items[3 * t + 1], zi = items[3 * t + 2];
+            const int dx = dims[xi], dy = dims[yi], dz = dims[zi];
+            const uint32_t *bx = bits + (size_t)row0[xi] * W, *by = bits + (size_t)row0[yi] * W,
+                           *bz = bits + (size_t)row0[zi] * W;
+            const int32_t *Txy = pair_table(pairtab, nvars, xi, yi), *Txz = pair_table(pairtab, nvars, xi, zi),
+                          *Tyz = pair_table(pairtab, nvars, yi, zi);
+            int32_t *out = counts + t * kBitsCells;
+            switch (dz * 64 + dx * 8 + dy) {
+#define FBN_TRIPLE(C, A, B)                                                                                  \
+    case C * 64 + A * 8 + B:                                                                                 \
+        count_test_derived<A, B, C>(bx, by, bz, W, lane, out, Txy, xi > yi, Txz, xi > zi, Tyz, yi > zi);     \
+        break;
+#define FBN_ROW(C)                                                                                           \
+    FBN_TRIPLE(C, 1, 1) FBN_TRIPLE(C, 1, 2) FBN_TRIPLE(C, 1, 3) FBN_TRIPLE(C, 1, 4)                          \
+    FBN_TRIPLE(C, 2, 1) FBN_TRIPLE(C, 2, 2) FBN_TRIPLE(C, 2, 3) FBN_TRIPLE(C, 2, 4)                          \
+    FBN_TRIPLE(C, 3, 1) FBN_TRIPLE(C, 3, 2) FBN_TRIPLE(C, 3, 3) FBN_TRIPLE(C, 3, 4)                          \
+    FBN_TRIPLE(C, 4, 1) FBN_TRIPLE(C, 4, 2) FBN_TRIPLE(C, 4, 3) FBN_TRIPLE(C, 4, 4)
+                FBN_ROW(1) FBN_ROW(2) FBN_ROW(3) FBN_ROW(4)
+#undef FBN_ROW
+#undef FBN_TRIPLE
+            default: break;
+            }
+        }
+    }
+}
+
+// one test's table N[z][x][y] (dimz <= 4 values of z, DX x DY cells each, the 64-slot record of
+// the count kernels) -> G^2 as one running sum in the reference's z -> x -> y order
+// (ComputeGSquareXY / XYZ, src/IndependenceTest.cpp:65-155, 295-364; the same arithmetic as
+// ci_g2_kernel) and the adjusted df.  The table is loaded with independent 16-byte loads up front
+// and every index is compile-time, so the <= 64 logs are independent instructions the compiler
+// interleaves (a lane's tests are otherwise a chain of dependent loads and long-latency fp64).
+template <int DX, int DY>
+__device__ __forceinline__ void g2_of_table(const int32_t *__restrict__ hz, int dimz, double &g2o, int &dfo) {
+    constexpr int DXY = DX * DY, NQ = DXY;  // 4 * DXY cells at most = DXY int4s
+    typedef __attribute__((ext_vector_type(4))) int i4;
+    i4 q[NQ];
+#pragma unroll
+    for (int v = 0; v < NQ; ++v)
+        q[v] = 4 * v < dimz * DXY ? reinterpret_cast<const i4 *>(hz)[v] : i4{0, 0, 0, 0};
+    auto cell = [&](int c) { return q[c / 4][c % 4]; };
+    double g2 = 0.0;
+    int df = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (k >= dimz) break;
+        int ni[DX], nj[DY];
+        long total = 0;
+        int alx = 0, aly = 0;
+#pragma unroll
+        for (int i = 0; i < DX; ++i) {
+            int s = 0;
+#pragma unroll
+            for (int j = 0; j < DY; ++j) s += cell(k * DXY + i * DY + j);
+            ni[i] = s;
+            alx += s > 0;
+            total += s;
+        }
+#pragma unroll
+        for (int j = 0; j < DY; ++j) {
+            int s = 0;
+#pragma unroll
+            for (int i = 0; i < DX; ++i) s += cell(k * DXY + i * DY + j);
+            nj[j] = s;
+            aly += s > 0;
+        }
+        alx = alx >= 1 ? alx : 1;
+        aly = aly >= 1 ? aly : 1;
+        df += (alx - 1) * (aly - 1);
+        if (total != 0) {
+#pragma unroll
+            for (int i = 0; i < DX; ++i) {
+                const long sum_row = ni[i];
+#pragma unroll
+                for (int j = 0; j < DY; ++j) {
+                    const long sum_col = nj[j];
+                    const long observed = cell(k * DXY + i * DY + j);
+                    // a skipped cell adds nothing (the reference's `continue`s)
+                    if (sum_row == 0 || sum_col == 0 || observed == 0) continue;
+                    const double expected = (double)sum_col * (double)sum_row / (double)total;
+                    g2 += 2.0 * observed * log(observed / expected);
+                }
+            }
+        }
+    }
+    g2o = g2, dfo = df;
+}
+
+// phase 2: one lane per test (g2_of_table per state-count class), p = 1 - P(df/2, G^2/2)
+// (ci_chisq.h).  With no p output and a decision band (band != nullptr: [lo, hi] per df 1..nband,
+// then delta), p is only evaluated for G^2 inside the band (fbn_chisq_band).  The margin log is
+// reduced per wave (one atomic per wave, not per test).
 template <int D>
 __global__ __launch_bounds__(256) void ci_bits_g2(const int32_t *__restrict__ counts, const int32_t *__restrict__ dims,
                                                   const int32_t *__restrict__ items, long long n, double alpha,
                                                   double *__restrict__ g2o, int32_t *__restrict__ dfo,
                                                   double *__restrict__ po, uint8_t *__restrict__ indep,
                                                   int32_t *__restrict__ counts0, unsigned long long *__restrict__ stats,
-                                                  int nvars, long long t0) {
-    for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t < n; t += (long long)gridDim.x * 256) {
-        int px, py;
-        if (D == 0 && !items) pair_of(t0 + t, nvars, px, py);
-        else px = items[(2 + D) * t], py = items[(2 + D) * t + 1];
-        const int dx = dims[px], dy = dims[py];
-        const int dimz = D == 1 ? dims[items[3 * t + 2]] : 1;
-        const int dxy = dx * dy;
-        const int32_t *hz = counts + t * kBitsCells;
-        // one running sum over z -> x -> y, exactly the reference's loop (no per-z partials)
-        double g2 = 0.0;
-        int df = 0;
-        for (int k = 0; k < dimz; ++k) {
-            const int32_t *h = hz + k * dxy;
-            int ni[4], nj[4];
-            long total = 0;
-            int alx = 0, aly = 0;
-            for (int i = 0; i < dx; ++i) {
-                int s = 0;
-                for (int j = 0; j < dy; ++j) s += h[i * dy + j];
-                ni[i] = s;
-                alx += s > 0;
-                total += s;
+                                                  int nvars, long long t0, const double *__restrict__ band,
+                                                  int nband) {
+    const long long stride = (long long)gridDim.x * 256;
+    // wave-uniform trip count (the margin reduction below is a whole-wave operation)
+    for (long long wb = (long long)blockIdx.x * 256 + (threadIdx.x & ~63); wb < n; wb += stride) {
+        const long long t = wb + (threadIdx.x & 63);
+        unsigned long long mbits = ~0ull;  // this lane's |p - alpha| (as ordered bits), none = max
+        bool near = false;
+        if (t < n) {
+            int px, py;
+            if (D == 0 && !items) pair_of(t0 + t, nvars, px, py);
+            else px = items[(2 + D) * t], py = items[(2 + D) * t + 1];
+            const int dx = dims[px], dy = dims[py];
+            const int dimz = D == 1 ? dims[items[3 * t + 2]] : 1;
+            const int32_t *hz = counts + t * kBitsCells;
+            double g2 = 0.0;
+            int df = 0;
+            switch (dx * 8 + dy) {
+#define FBN_G2(A, B)                                                                                         \
+    case A * 8 + B:                                                                                          \
+        g2_of_table<A, B>(hz, dimz, g2, df);                                                                 \
+        break;
+                FBN_G2(1, 1) FBN_G2(1, 2) FBN_G2(1, 3) FBN_G2(1, 4)
+                FBN_G2(2, 1) FBN_G2(2, 2) FBN_G2(2, 3) FBN_G2(2, 4)
+                FBN_G2(3, 1) FBN_G2(3, 2) FBN_G2(3, 3) FBN_G2(3, 4)
+                FBN_G2(4, 1) FBN_G2(4, 2) FBN_G2(4, 3) FBN_G2(4, 4)
+#undef FBN_G2
+            default: break;
             }
-            for (int j = 0; j < dy; ++j) {
-                int s = 0;
-                for (int i = 0; i < dx; ++i) s += h[i * dy + j];
-                nj[j] = s;
-                aly += s > 0;
+            double p = 1.0, m;
+            bool ind;
+            if (df == 0) {  // src/IndependenceTest.cpp:149-151, 349-351
+                ind = true;
+                m = fabs(p - alpha);
+            } else if (!po && band && df <= nband && g2 < band[2 * df - 2]) {
+                ind = true, m = band[2 * nband];  // p > alpha + delta
+            } else if (!po && band && df <= nband && g2 > band[2 * df - 1]) {
+                ind = false, m = band[2 * nband];  // p < alpha - delta
+            } else {
+                p = fbn_chisq_pvalue(g2, df);
+                ind = p > alpha;
+                m = fabs(p - alpha);
             }
-            alx = alx >= 1 ? alx : 1;
-            aly = aly >= 1 ? aly : 1;
-            df += (alx - 1) * (aly - 1);
-            if (total != 0) {
-                for (int i = 0; i < dx; ++i) {
-                    const long sum_row = ni[i];
-                    if (sum_row == 0) continue;
-                    for (int j = 0; j < dy; ++j) {
-                        const long sum_col = nj[j];
-                        const long observed = h[i * dy + j];
-                        if (sum_col == 0 || observed == 0) continue;
-                        const double expected = (double)sum_col * (double)sum_row / (double)total;
-                        g2 += 2.0 * observed * log(observed / expected);
-                    }
-                }
-            }
+            if (g2o) g2o[t] = g2;
+            dfo[t] = df;
+            if (po) po[t] = p;
+            indep[t] = ind;
+            if (counts0 && t == 0)
+                for (int c = 0; c < dimz * dx * dy; ++c) counts0[c] = hz[c];
+            mbits = (unsigned long long)__double_as_longlong(m);
+            near = m < 1e-9;
         }
-        double p;
-        bool ind;
-        if (df == 0) {  // src/IndependenceTest.cpp:149-151, 349-351
-            p = 1.0;
-            ind = true;
-        } else {
-            p = fbn_chisq_pvalue(g2, df);
-            ind = p > alpha;
-        }
-        if (g2o) g2o[t] = g2;
-        dfo[t] = df;
-        if (po) po[t] = p;
-        indep[t] = ind;
-        if (counts0 && t == 0)
-            for (int c = 0; c < dimz * dxy; ++c) counts0[c] = hz[c];
         if (stats) {
-            const double m = fabs(p - alpha);
-            atomicMin(stats, (unsigned long long)__double_as_longlong(m));
-            if (m < 1e-9) atomicAdd(stats + 1, 1ull);
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+                const unsigned long long v = __shfl_xor(mbits, o);
+                mbits = v < mbits ? v : mbits;
+            }
+            const unsigned long long nn = __popcll(__ballot(near));
+            if ((threadIdx.x & 63) == 0) {
+                if (mbits != ~0ull) atomicMin(stats, mbits);
+                if (nn) atomicAdd(stats + 1, nn);
+            }
         }
     }
 }
@@ -635,7 +910,7 @@ extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *di
                                          double *g2, int32_t *df, double *p, uint8_t *indep, int32_t *counts,
                                          int32_t *counts0, unsigned long long *stats, const int32_t *rowcnt,
                                          int32_t *pairtab, int pmode, int nvars, int num_cu, long long t0,
-                                         int counted, hipStream_t s) {
+                                         int counted, const double *band, int nband, hipStream_t s) {
     const long long g1 = (n + 3) / 4, cap = (long long)num_cu * 8;
     const long long g2g = (n + 255) / 256;
     const dim3 b1((unsigned)(g1 < cap ? g1 : cap)), b2((unsigned)(g2g < cap ? g2g : cap));
@@ -644,16 +919,29 @@ extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *di
             hipLaunchKernelGGL(ci_bits_count<0>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts, rowcnt,
                                pmode == 1 ? pairtab : nullptr, nvars, t0);
         hipLaunchKernelGGL(ci_bits_g2<0>, b2, dim3(256), 0, s, counts, dims, items, n, alpha, g2, df, p, indep,
-                           counts0, stats, nvars, t0);
+                           counts0, stats, nvars, t0, band, nband);
     } else if (d == 1) {
-        if (pmode == 2)
-            hipLaunchKernelGGL(ci_bits_count_derived, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts,
-                               (const int32_t *)pairtab, nvars);
+        // FBN_CI_L1MODE: 0 = item per wave, plain grid stride; 1 = item per wave, XCD-contiguous;
+        // 2 = quad of items per wave (x/y rows shared in registers), XCD-contiguous
+        static const int l1mode = getenv("FBN_CI_L1MODE") ? atoi(getenv("FBN_CI_L1MODE")) : 1;
+        if (pmode == 2 && l1mode == 2) {
+            const long long gq = (n + 15) / 16;
+            hipLaunchKernelGGL(ci_bits_count_derived_grp, dim3((unsigned)(gq < cap ? gq : cap)), dim3(256), 0, s, bits,
+                               dims, row0, items, W, n, counts, (const int32_t *)pairtab, nvars, 1);
+        } else if (pmode == 2) {
+            static const int l1waves = getenv("FBN_CI_L1WAVES") ? atoi(getenv("FBN_CI_L1WAVES")) : 0;
+            auto *k = l1waves == 4   ? ci_bits_count_derived_w4
+                      : l1waves == 5 ? ci_bits_count_derived_w5
+                      : l1waves == 6 ? ci_bits_count_derived_w6
+                                     : ci_bits_count_derived;
+            hipLaunchKernelGGL(k, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts, (const int32_t *)pairtab,
+                               nvars, l1mode == 1 ? 1 : 0);
+        }
         else
             hipLaunchKernelGGL(ci_bits_count<1>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts, rowcnt,
                                nullptr, nvars, 0ll);
         hipLaunchKernelGGL(ci_bits_g2<1>, b2, dim3(256), 0, s, counts, dims, items, n, alpha, g2, df, p, indep,
-                           counts0, stats, nvars, 0ll);
+                           counts0, stats, nvars, 0ll, band, nband);
     } else {
         return hipErrorInvalidValue;
     }

@@ -11,7 +11,7 @@
 
 #include <hip/hip_runtime.h>
 
-__device__ inline double fbn_gamma_p(double a, double x) {
+__host__ __device__ inline double fbn_gamma_p(double a, double x) {
     if (x <= 0.0) return 0.0;
     const double lg = lgamma(a);
     if (x < a + 1.0) {
@@ -42,6 +42,28 @@ __device__ inline double fbn_gamma_p(double a, double x) {
 }
 
 // p = 1 - pchisq(g2, df) (df > 0)
-__device__ inline double fbn_chisq_pvalue(double g2, int df) { return 1.0 - fbn_gamma_p(0.5 * df, 0.5 * g2); }
+__host__ __device__ inline double fbn_chisq_pvalue(double g2, int df) { return 1.0 - fbn_gamma_p(0.5 * df, 0.5 * g2); }
+
+// Decision band (skeleton-search batches, which need only the decision p > alpha and the margin
+// log, not p itself): per df, lo < hi with p(lo) > alpha + delta and p(hi) < alpha - delta, found by
+// bisection on this same function.  p is monotone in G^2 and the CDF's rounding error is ~1e-15, far
+// below delta, so G^2 < lo decides "independent" and G^2 > hi "dependent" exactly as evaluating p
+// would; only tests inside [lo, hi] evaluate p.  Skipped tests are >= delta from alpha.
+inline void fbn_chisq_band(double alpha, double delta, int df, double *lo, double *hi) {
+    auto bracket = [&](double target, bool want_lo) {
+        double a = 0.0, b = df + 10.0 * sqrt(2.0 * df) + 10.0;
+        while (fbn_chisq_pvalue(b, df) >= target) a = b, b *= 2.0;  // p(a) >= target > p(b)
+        for (int i = 0; i < 40; ++i) {
+            const double m = 0.5 * (a + b);
+            (fbn_chisq_pvalue(m, df) >= target ? a : b) = m;
+        }
+        return want_lo ? a : b;
+    };
+    double l = bracket(alpha + delta, true);
+    while (l > 0.0 && !(fbn_chisq_pvalue(l, df) > alpha + delta)) l *= 0.999;  // strict
+    double h = bracket(alpha - delta, false);
+    while (!(fbn_chisq_pvalue(h, df) < alpha - delta)) h *= 1.001;
+    *lo = l, *hi = h;
+}
 
 #endif

@@ -80,6 +80,8 @@ class JTGen {
     int nobs = 0;
     // op boundary (+ diagnostic cycle stamp of op category k when FBN_JT_PROFILE is set)
     bool profile = false;
+    int min_waves = 1;
+    bool iv_lds = true;
     std::string B(int k) const {
         return profile ? "        FBN_OP_BOUNDARY(); FBN_STAMP(" + std::to_string(k) + ");\n" : "        FBN_OP_BOUNDARY();\n";
     }
@@ -291,6 +293,10 @@ int JTGen::Run(std::string &src, int64_t *wave_entries, std::vector<double> &ini
     const int nc = (int)plan.cliques.size(), ns = (int)plan.seps.size(), V = plan.num_nodes;
     if (const char *e = getenv("FBN_JT_REG_ENTRIES")) kRegEntries = std::max<int64_t>(1, atoll(e));  // tuning
     profile = getenv("FBN_JT_PROFILE") && atoi(getenv("FBN_JT_PROFILE")) != 0;  // diagnostic build
+    // occupancy: waves per SIMD the register allocation must allow (1: up to 512 registers)
+    min_waves = getenv("FBN_JT_MIN_WAVES") ? std::max(1, atoi(getenv("FBN_JT_MIN_WAVES"))) : min_waves;
+    // initial potentials: LDS copy per wave (1) or scalar loads from the constant buffer (0)
+    iv_lds = getenv("FBN_JT_IV_LDS") ? atoi(getenv("FBN_JT_IV_LDS")) != 0 : iv_lds;
     lds_rows = 0;
     for (const auto &t : plan.cliques) lds_rows = std::max<int64_t>(lds_rows, t.size() - kRegEntries);
     // initial potentials: one constant buffer, read with wave-uniform (scalar) loads
@@ -331,6 +337,7 @@ int JTGen::Run(std::string &src, int64_t *wave_entries, std::vector<double> &ini
     o << "// generated by libfastbn (jt_codegen.cpp): " << nc << " cliques, " << ns << " separators\n";
     o << "#define FBN_V " << V << "\n#define FBN_SD " << SD << "\n#define FBN_WE " << *wave_entries << "LL\n";
     o << "#define FBN_IV_BASE " << lds_rows * 64 << "\n#define FBN_NIV " << initv.size() << "\n";
+    o << "#define FBN_IV_LDS " << (iv_lds ? 1 : 0) << "\n#define FBN_MIN_WAVES " << min_waves << "\n";
     o << R"FBN(typedef signed char i8;
 __device__ __forceinline__ double dv(double x, double den, double y) {  // x / den (Markstein, see jt_kernels.hip)
     const double q = x * y;
@@ -346,8 +353,13 @@ typedef __attribute__((address_space(4))) const double cdouble;
 typedef __attribute__((address_space(3))) double ldouble;
 extern __shared__ double fbn_lds[];
 #define L(row) (ltail[(row) * 64])
-// initial potentials, copied into LDS once per wave (wave-uniform address: broadcast reads)
+// initial potentials: copied into LDS once per wave (wave-uniform address: broadcast reads), or
+// read with scalar loads from the constant buffer
+#if FBN_IV_LDS
 #define IV(k) (ivl[k])
+#else
+#define IV(k) (ivc[k])
+#endif
 // unconditional (LDS broadcast) load + select: no branch per table entry
 __device__ __forceinline__ double sel(bool c, double v) { return c ? v : 0.0; }
 #define FBN_STAMP(k) do { unsigned long long t_; __asm__ volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_) :: "memory"); pacc[k] += t_ - tprev; tprev = t_; } while (0)
@@ -356,7 +368,7 @@ __device__ __forceinline__ unsigned den_bad(double d) { return (d >= 0x1p-600 &&
 #define CS (blkl * 64 + lane)
 #define ACT (CS < ncases)
 #define OUT(k) (marg[CS * FBN_SD + (k)])
-extern "C" __global__ void __launch_bounds__(64, 1)
+extern "C" __global__ void __launch_bounds__(64, FBN_MIN_WAVES)
 fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restrict__ labels,
            double *__restrict__ ws, int *__restrict__ flags, const double *ivp, long long ncases,
            unsigned long long *__restrict__ prof) {
@@ -364,9 +376,14 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
     // LDS bases are laundered at every op boundary (so addresses fold into ds_* offsets instead of
     // being hoisted as loop-invariant constants)
     ldouble *ltail = (ldouble *)fbn_lds + lane;
+#if FBN_IV_LDS
     ldouble *ivl = (ldouble *)fbn_lds + FBN_IV_BASE;
     for (int k = lane; k < FBN_NIV; k += 64) IV(k) = ivp[k];
     __syncthreads();
+#else
+    const cdouble *ivc = (const cdouble *)ivp;
+    ldouble *ivl = (ldouble *)fbn_lds;  // unused (laundered at op boundaries)
+#endif
     unsigned long long pacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tprev = __builtin_amdgcn_s_memtime();
     gdouble *Wb = (gdouble *)ws + (unsigned long long)blockIdx.x * FBN_WE * 64;
     unsigned lo = (unsigned)lane * 8;
@@ -553,7 +570,8 @@ int GenerateJTKernel(const JTPlanHost &plan, std::string &src, int64_t *wave_ent
                      int64_t *lds_bytes) {
     JTGen g(plan);
     int rc = g.Run(src, wave_entries, initv);
-    if (lds_bytes) *lds_bytes = (g.lds_rows * 64 + (int64_t)initv.size()) * 8;
+    const bool iv_lds = !getenv("FBN_JT_IV_LDS") || atoi(getenv("FBN_JT_IV_LDS")) != 0;
+    if (lds_bytes) *lds_bytes = (g.lds_rows * 64 + (iv_lds ? (int64_t)initv.size() : 0)) * 8;
     return rc;
 }
 

@@ -126,17 +126,21 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
         // the (x, y) pairs of the edge range are the items, in place (pair<int, int> = two ints)
         static_assert(sizeof(std::pair<int, int>) == 2 * sizeof(int32_t), "pair layout");
         const int32_t *pairs = reinterpret_cast<const int32_t *>(edges.data() + e_begin);
-        indep.resize(E);
-        // statistics of the pairs without the validation pass (they come from the skeleton)
+        // statistics of the pairs without the validation pass (they come from the skeleton); for
+        // the whole complete graph in closed form: every variable is in nv - 1 pairs
         const int32_t *dims = CiCtxDims(ctx);
-        CiBatchStats st0{0, 0};
-        for (size_t e = e_begin; e < e_end; ++e) {
-            const int a = dims[edges[e].first], b = dims[edges[e].second];
-            st0.dim_rows += a + b, st0.maxdim = std::max(st0.maxdim, std::max(a, b));
-        }
         int nv = 0;
         int64_t ns = 0;
         CiCtxShape(ctx, &nv, &ns);
+        CiBatchStats st0{0, 0};
+        if (e_begin == 0 && (int64_t)E == (int64_t)nv * (nv - 1) / 2 && edges.size() == E) {
+            for (int v = 0; v < nv; ++v) st0.dim_rows += (int64_t)(nv - 1) * dims[v], st0.maxdim = std::max(st0.maxdim, (int)dims[v]);
+        } else {
+            for (size_t e = e_begin; e < e_end; ++e) {
+                const int a = dims[edges[e].first], b = dims[edges[e].second];
+                st0.dim_rows += a + b, st0.maxdim = std::max(st0.maxdim, std::max(a, b));
+            }
+        }
         // the complete graph (a PC run's level 0): edge index = pair index, the kernels decode the
         // pairs of the range themselves
         const bool all_pairs = (int64_t)edges.size() == (int64_t)nv * (nv - 1) / 2 &&
@@ -144,9 +148,10 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
         int rc = all_pairs ? CiBatchLaunchAllPairs(ctx, alpha, &st0, (int64_t)e_begin, (int64_t)E)
                            : CiBatchLaunch(ctx, 0, pairs, (int64_t)E, 0, alpha, false, &st0);
         if (rc) return rc;
-        rc = CiBatchWait(ctx, 0, indep.data(), nullptr, res);
+        // the device's 0/1 decisions land in the removal flags directly
+        static_assert(sizeof(char) == sizeof(uint8_t), "flag layout");
+        rc = CiBatchWait(ctx, 0, reinterpret_cast<uint8_t *>(out.removed.data()), nullptr, res);
         if (rc) return rc;
-        for (size_t e = 0; e < E; ++e) out.removed[e] = indep[e] ? 1 : 0;
         out.counted = out.launched = (int64_t)E;
         return FBN_OK;
     }
@@ -362,11 +367,10 @@ void ApplyRemovals(const std::vector<char> &rm, std::vector<std::pair<int, int>>
     // removals after a level, in vec_edges order (src/PCStable.cpp:310-326); the adjacency lists
     // are rebuilt from the kept edges in O(E) (edges stay in (i < j) lexicographic order, so every
     // list comes out sorted) instead of erasing element by element (the reference's O(E^2) hot spot)
-    std::vector<std::pair<int, int>> keep;
-    keep.reserve(edges.size());
+    size_t w = 0;  // compacted in place (no second edge array)
     for (size_t e = 0; e < edges.size(); ++e)
-        if (!rm[e]) keep.push_back(edges[e]);
-    edges.swap(keep);
+        if (!rm[e]) edges[w++] = edges[e];
+    edges.resize(w);
     for (auto &a : adj) a.clear();
     for (auto &e : edges) adj[e.first].push_back(e.second), adj[e.second].push_back(e.first);
 }

@@ -24,6 +24,7 @@
 #include <set>
 #include <sstream>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "fbn_internal.h"
@@ -103,6 +104,7 @@ struct Graph {
         return !cyc;
     }
     bool DeleteDirected(int p, int c) {
+        if (!parents[c].count(p)) return false;  // not present: skip the linear search
         const int pos = Find(Directed(p, c));
         if (pos < 0) return false;
         parents[c].erase(p);
@@ -110,11 +112,21 @@ struct Graph {
         edges.erase(edges.begin() + pos);
         return true;
     }
-    void AddUndirected(int a, int b) { edges.push_back(Undirected(a, b)); }
+    // undirected edges present, by (min, max) key with multiplicity: an absent edge is rejected
+    // without the linear search over `edges`
+    std::unordered_map<uint64_t, int> und;
+    static uint64_t Key(int a, int b) { return (uint64_t)(uint32_t)std::min(a, b) << 32 | (uint32_t)std::max(a, b); }
+    void AddUndirected(int a, int b) {
+        edges.push_back(Undirected(a, b));
+        ++und[Key(a, b)];
+    }
     bool DeleteUndirected(int a, int b) {
+        auto it = und.find(Key(a, b));
+        if (it == und.end()) return false;
         const int pos = Find(Undirected(a, b));
         if (pos < 0) return false;
         edges.erase(edges.begin() + pos);
+        if (--it->second == 0) und.erase(it);
         return true;
     }
     bool IsDirectedFromTo(int a, int b) const { return parents[b].count(a) != 0; }
@@ -135,8 +147,9 @@ struct Orienter {
     Orienter(int n, const std::vector<std::pair<int, int>> &skeleton,
              const SepsetMap &ss)
         : g(n), adj(n), sepset(ss) {
+        g.edges.reserve(skeleton.size() + 16);
         for (auto &e : skeleton) {
-            g.edges.push_back(Undirected(e.first, e.second));
+            g.AddUndirected(e.first, e.second);
             adj[e.first].insert(e.second);
             adj[e.second].insert(e.first);
         }

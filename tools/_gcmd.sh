@@ -4,12 +4,12 @@ export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_pc.py tests/test_gpu_pc_dist.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t_pc.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/t_pc.log; exit 1; }
 tail -1 gpurun_out/t_pc.log
 timeout -k 10 120 python tools/pc5_timing.py 4 2>&1 | grep -E "run " | tail -2
+FBN_CI_NO_BAND=1 timeout -k 10 120 python tools/pc5_timing.py 4 2>&1 | grep -E "run " | tail -1
 timeout -k 10 120 python tools/pc_alarm_timing.py 2>&1 | tail -1
-FBN_CI_G2_LANE=1 timeout -k 10 120 python tools/pc_alarm_timing.py 2>&1 | tail -1
-mkdir -p gpurun_out/l1prof
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/l1prof -o run --output-format csv -- python tools/pc5_timing.py 3 > /dev/null 2>&1
+mkdir -p gpurun_out/bprof
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/bprof -o run --output-format csv -- python tools/pc5_timing.py 3 > /dev/null 2>&1 || exit 1
 python3 -c "
 import csv
-for r in csv.DictReader(open('gpurun_out/l1prof/run_kernel_stats.csv')):
+for r in list(csv.DictReader(open('gpurun_out/bprof/run_kernel_stats.csv')))[:8]:
     print(r['Name'][:60], r['Calls'], round(float(r['AverageNs'])/1e3,1), 'us', round(float(r['TotalDurationNs'])/1e6/3,3), 'ms/run')
 "
