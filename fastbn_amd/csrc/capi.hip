@@ -38,6 +38,16 @@ extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *di
 extern "C" hipError_t fbn_ci_bits_rowcount(const uint32_t *bits, long long rows, long long W, int32_t *rowcnt,
                                            hipStream_t s);
 extern "C" int fbn_ci_pair_block(int d);
+extern "C" int fbn_ci_gram_task_ints(void);
+extern "C" hipError_t fbn_ci_gram(const uint32_t *bits, long long W, const int32_t *rl, const int32_t *tasks,
+                                  long long ntasks, int masked, int32_t *out, int num_cu, hipStream_t s);
+extern "C" hipError_t fbn_ci_gram_pairs(const int32_t *G, long long ld, const int32_t *lead0, const int32_t *dims,
+                                        const int32_t *row0, const int32_t *rowcnt, long long t0, long long n,
+                                        int nvars, int32_t *counts, int32_t *pairtab, int num_cu, hipStream_t s);
+extern "C" hipError_t fbn_ci_gram_triples(const int32_t *G, const long long *goff, const int32_t *gR,
+                                          const int32_t *adj, const int32_t *adj_off, const int32_t *loff,
+                                          const int32_t *dims, const int32_t *items, long long n, int32_t *counts,
+                                          const int32_t *pairtab, int nvars, int num_cu, hipStream_t s);
 extern "C" hipError_t fbn_ci_bits_pairs_tiled(const uint32_t *bits, const int32_t *row0, const int32_t *rowcnt,
                                               long long W, const int32_t *tasks, long long ntasks, int nvars,
                                               long long t0, long long t1, int32_t *counts, int32_t *pairtab,
@@ -182,6 +192,19 @@ struct fbn_ci_ctx {
     int64_t ptask_t0 = -1, ptask_t1 = -1, ptask_n = 0;
     int pair_mode = 0;
     bool pairs_recorded = false;
+    // row Grams (ci_bits.hip ci_bits_gram): leading rows = values 0..d-2 of every variable;
+    // lead0[v] = v's first leading row, leadrows[r] = the bits row of leading row r
+    std::vector<int32_t> row0_host, lead0_host, leadrows_host;
+    DevBuf lead0, leadrows;
+    bool lead_ready = false;
+    // level 0: the Gram of all leading rows (ld = leading-row count) and its tile tasks for the
+    // pair range [g0_t0, g0_t1)
+    DevBuf gram0, g0tasks;
+    int64_t g0_t0 = -1, g0_t1 = -1, g0_ntasks = 0;
+    // level 1: per-variable masked Grams over the neighbours' leading rows (CiTriplePrepare), used
+    // by the next d = 1 batches while triples_ready
+    DevBuf g1, g1tasks, g1rl, g1goff, g1R, g1adj, g1adjoff, g1loff;
+    bool triples_ready = false;
     // decision band of the bit-sliced G^2 kernel for alpha = band_alpha (ci_chisq.h fbn_chisq_band):
     // [lo, hi] per df 1..kBandDf, then delta; host copy kept alive for the async upload
     DevBuf band;
@@ -998,6 +1021,71 @@ static int CiPairTasks(fbn_ci_ctx *c, int64_t t0, int64_t t1, hipStream_t s) {
     return FBN_OK;
 }
 
+// the leading rows of the bit-sliced store (once per ctx, after the bits build)
+static int CiLeadEnsure(fbn_ci_ctx *c, hipStream_t s) {
+    if (c->lead_ready) return FBN_OK;
+    const int nv = c->nvars;
+    c->lead0_host.assign(nv, 0);
+    c->leadrows_host.clear();
+    for (int v = 0; v < nv; ++v) {
+        c->lead0_host[v] = (int32_t)c->leadrows_host.size();
+        for (int a = 0; a + 1 < c->dims[v]; ++a) c->leadrows_host.push_back(c->row0_host[v] + a);
+    }
+    int rc;
+    if ((rc = c->lead0.ensure((size_t)nv * 4))) return rc;
+    if ((rc = c->leadrows.ensure(std::max<size_t>(c->leadrows_host.size(), 1) * 4))) return rc;
+    FBN_HIP(hipMemcpyAsync(c->lead0.p, c->lead0_host.data(), (size_t)nv * 4, hipMemcpyHostToDevice, s));
+    if (!c->leadrows_host.empty())
+        FBN_HIP(hipMemcpyAsync(c->leadrows.p, c->leadrows_host.data(), c->leadrows_host.size() * 4,
+                               hipMemcpyHostToDevice, s));
+    c->lead_ready = true;
+    return FBN_OK;
+}
+
+// level 0 through the Gram when its ld x ld int32 matrix fits this budget (else the tiled kernel)
+constexpr int64_t kGram0MaxBytes = (int64_t)1 << 30;
+static bool CiGram0Eligible(const fbn_ci_ctx *c) {
+    int64_t R = 0;
+    for (int v = 0; v < c->nvars; ++v) R += c->dims[v] - 1;
+    return R > 0 && R * R * 4 <= kGram0MaxBytes && !getenv("FBN_CI_NO_GRAM");
+}
+
+// 8 x 8 tiles (i-block <= j-block) of the leading-row Gram holding a pair (x < y) of [t0, t1): row
+// i of x's leading rows, column j of y's (x < y puts every needed entry in an upper tile).  Cached
+// per range.
+static int CiGram0Tasks(fbn_ci_ctx *c, int64_t t0, int64_t t1, hipStream_t s) {
+    if (c->g0_t0 == t0 && c->g0_t1 == t1) return FBN_OK;
+    const int nv = c->nvars;
+    const int64_t R = (int64_t)c->leadrows_host.size(), nb = (R + 7) / 8;
+    std::vector<int32_t> var_of(R);
+    for (int v = 0; v < nv; ++v)
+        for (int a = 0; a + 1 < c->dims[v]; ++a) var_of[c->lead0_host[v] + a] = v;
+    auto idx = [&](int64_t u, int64_t v) { return u * nv - u * (u + 1) / 2 + (v - u - 1); };
+    const int TI = fbn_ci_gram_task_ints();
+    std::vector<int32_t> tasks;
+    for (int64_t bi = 0; bi < nb; ++bi) {
+        const int64_t r0 = 8 * bi, r1 = std::min(R, r0 + 8);
+        const int vi0 = var_of[r0], vi1 = var_of[r1 - 1];
+        for (int64_t bj = bi; bj < nb; ++bj) {
+            const int64_t c0 = 8 * bj, c1 = std::min(R, c0 + 8);
+            const int vj0 = var_of[c0], vj1 = var_of[c1 - 1];
+            if (vi0 >= vj1) continue;  // no x < y in the tile
+            const int64_t tmin = idx(vi0, std::max(vj0, vi0 + 1)), tmax = idx(std::min(vi1, vj1 - 1), vj1);
+            if (tmax < t0 || tmin >= t1) continue;
+            const int64_t off = r0 * R + c0;
+            const int32_t t[8] = {-1, (int32_t)r0, (int32_t)(r1 - r0), (int32_t)c0, (int32_t)(c1 - c0),
+                                  (int32_t)(uint32_t)(off & 0xffffffff), (int32_t)(off >> 32), (int32_t)R};
+            tasks.insert(tasks.end(), t, t + TI);
+        }
+    }
+    int rc;
+    if ((rc = c->g0tasks.ensure(std::max<size_t>(tasks.size(), 1) * 4))) return rc;
+    if (!tasks.empty()) FBN_HIP(hipMemcpyAsync(c->g0tasks.p, tasks.data(), tasks.size() * 4, hipMemcpyHostToDevice, s));
+    FBN_HIP(hipStreamSynchronize(s));  // the host vector goes out of scope
+    c->g0_t0 = t0, c->g0_t1 = t1, c->g0_ntasks = (int64_t)tasks.size() / TI;
+    return FBN_OK;
+}
+
 // items: host copy (validated here).  zc_items / zc_indep / zc_df: optional device-visible
 // (pinned, mapped) host buffers the kernels read the items from and write the decisions to
 // directly -- no staging copies for the small batches of a latency-bound driver round.
@@ -1038,6 +1126,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
             std::vector<int32_t> row0(c->nvars);
             int64_t rows = 0;
             for (int v = 0; v < c->nvars; ++v) row0[v] = (int32_t)rows, rows += std::min(c->dims[v], 8);
+            c->row0_host = row0;
             if ((rc = c->bits.ensure((size_t)std::max<int64_t>(rows * W, 1) * 4))) return rc;
             if ((rc = c->brow.ensure((size_t)c->nvars * 4))) return rc;
             FBN_HIP(hipMemcpyAsync(c->brow.p, row0.data(), (size_t)c->nvars * 4, hipMemcpyHostToDevice, s));
@@ -1079,9 +1168,32 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         if (!want_g2p && (rc = CiBand(c, alpha, s, &band))) return rc;
         if (c->timing) FBN_HIP(hipEventRecord(S.ev0, s));
         // all pairs of a range: register-blocked count kernel (ci_bits_pairs_tiled), then phase 2
-        const bool tiled = all_pairs && d == 0 && !getenv("FBN_CI_NO_TILED");
+        const bool gram0 = all_pairs && d == 0 && CiGram0Eligible(c);
+        const bool tiled = all_pairs && d == 0 && !gram0 && !getenv("FBN_CI_NO_TILED");
         if (tiled && (rc = CiPairTasks(c, pair0, pair0 + n, s))) return rc;
         hipError_t e = hipSuccess;
+        if (gram0) {  // Gram of the leading rows, then every pair's table from it
+            if ((rc = CiLeadEnsure(c, s)) || (rc = CiGram0Tasks(c, pair0, pair0 + n, s))) return rc;
+            const int64_t R = (int64_t)c->leadrows_host.size();
+            if ((rc = c->gram0.ensure((size_t)(R * R * 4)))) return rc;
+            e = fbn_ci_gram(c->bits.as<uint32_t>(), c->bits_W, c->leadrows.as<int32_t>(), c->g0tasks.as<int32_t>(),
+                            c->g0_ntasks, 0, c->gram0.as<int32_t>(), c->num_cu, s);
+            if (e == hipSuccess)
+                e = fbn_ci_gram_pairs(c->gram0.as<int32_t>(), R, c->lead0.as<int32_t>(), c->ddims.as<int32_t>(),
+                                      c->brow.as<int32_t>(), c->browcnt.as<int32_t>(), pair0, n, c->nvars,
+                                      S.bcounts.as<int32_t>(), pmode == 1 ? c->pairtab.as<int32_t>() : nullptr,
+                                      c->num_cu, s);
+            if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci gram level 0: %s", hipGetErrorString(e));
+        }
+        // level 1 with the per-variable Grams prepared (CiTriplePrepare): tables gathered from them
+        const bool gram1 = d == 1 && pmode == 2 && c->triples_ready && pre;  // driver batches only
+        if (gram1) {
+            e = fbn_ci_gram_triples(c->g1.as<int32_t>(), c->g1goff.as<long long>(), c->g1R.as<int32_t>(),
+                                    c->g1adj.as<int32_t>(), c->g1adjoff.as<int32_t>(), c->g1loff.as<int32_t>(),
+                                    c->ddims.as<int32_t>(), ditems, n, S.bcounts.as<int32_t>(),
+                                    c->pairtab.as<int32_t>(), c->nvars, c->num_cu, s);
+            if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci gram level 1: %s", hipGetErrorString(e));
+        }
         if (tiled) {
             e = fbn_ci_bits_pairs_tiled(c->bits.as<uint32_t>(), c->brow.as<int32_t>(), c->browcnt.as<int32_t>(),
                                         c->bits_W, c->ptasks.as<int32_t>(), c->ptask_n, c->nvars, pair0, pair0 + n,
@@ -1096,7 +1208,8 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
                                           zc_indep ? zc_indep : S.indep.as<uint8_t>(),
                                           S.bcounts.as<int32_t>(), counts_dev, c->stats.as<unsigned long long>(),
                                           c->browcnt.as<int32_t>(), c->pairtab.as<int32_t>(), pmode, c->nvars,
-                                          c->num_cu, (long long)pair0, tiled ? 1 : 0, band, kBandDf, s);
+                                          c->num_cu, (long long)pair0, (tiled || gram0 || gram1) ? 1 : 0, band,
+                                          kBandDf, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci bits kernel launch: %s", hipGetErrorString(e));
         if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
         return FBN_OK;
@@ -1393,6 +1506,7 @@ constexpr size_t kZeroCopyBytes = 256 << 10;
 const int32_t *CiCtxDims(const fbn_ci_ctx *c) { return c->dims.data(); }
 void CiSetPairMode(fbn_ci_ctx *c, int mode) {
     c->pair_mode = mode;
+    c->triples_ready = false;
     if (mode != 2) c->pairs_recorded = false;
 }
 int CiBatchLaunch(fbn_ci_ctx *c, int k, const int32_t *items, int64_t n, int d, double alpha, bool want_df,
@@ -1472,6 +1586,82 @@ int CiMarginRead(fbn_ci_ctx *c, double *min_margin, int64_t *near_alpha) {
 void CiSetPairsRecorded(fbn_ci_ctx *c) {
     c->pair_mode = 2;
     c->pairs_recorded = true;
+}
+// per-variable masked Grams of a PC run's level 1: for every endpoint u of the edges [e_begin,
+// e_end), G_u[a] = popcount(u_a & r_i & r_j) over u's neighbours' leading rows (upper 8 x 8 tiles),
+// enqueued on the ctx stream ahead of the level's batches; their tests then gather the leading
+// cells instead of counting (ci_bits_gram_triples).  Only with recorded pair tables (the rest of
+// each table is derived from them) and the bit-sliced store; skipped when the Grams exceed the
+// budget.
+constexpr int64_t kGram1MaxBytes = (int64_t)1 << 30;
+int CiTriplePrepare(fbn_ci_ctx *c, const std::vector<std::vector<int>> &adj,
+                    const std::vector<std::pair<int, int>> &edges, size_t e_begin, size_t e_end, bool *ready) {
+    *ready = c->triples_ready = false;
+    if (c->pair_mode != 2 || !c->pairs_recorded || !c->bits_ready || getenv("FBN_CI_NO_GRAM")) return FBN_OK;
+    const int nv = c->nvars;
+    for (int v = 0; v < nv; ++v)
+        if (c->dims[v] > 4) return FBN_OK;
+    FBN_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    int rc;
+    if ((rc = CiLeadEnsure(c, s))) return rc;
+    std::vector<char> need(nv, 0);
+    for (size_t e = e_begin; e < e_end; ++e) need[edges[e].first] = need[edges[e].second] = 1;
+    std::vector<int32_t> adjf, adj_off(nv + 1, 0), loff, R(nv, 0), rl;
+    std::vector<long long> goff(nv, 0);
+    long long gtot = 0;
+    for (int u = 0; u < nv; ++u) {
+        adj_off[u] = (int32_t)adjf.size();
+        int r = 0;
+        for (int v : adj[u]) adjf.push_back(v), loff.push_back(r), r += c->dims[v] - 1;
+        R[u] = r;
+        goff[u] = gtot;
+        if (need[u] && adj[u].size() >= 2) gtot += (long long)(c->dims[u] - 1) * r * r;
+    }
+    adj_off[nv] = (int32_t)adjf.size();
+    if (gtot * 4 > kGram1MaxBytes) return FBN_OK;
+    const int TI = fbn_ci_gram_task_ints();
+    std::vector<int32_t> tasks;
+    for (int u = 0; u < nv; ++u) {
+        if (!need[u] || adj[u].size() < 2 || c->dims[u] < 2 || R[u] == 0) continue;
+        const int64_t base = (int64_t)rl.size(), Ru = R[u], nb = (Ru + 7) / 8;
+        for (int v : adj[u])
+            for (int a = 0; a + 1 < c->dims[v]; ++a) rl.push_back(c->row0_host[v] + a);
+        for (int a = 0; a + 1 < c->dims[u]; ++a)
+            for (int64_t bi = 0; bi < nb; ++bi)
+                for (int64_t bj = bi; bj < nb; ++bj) {
+                    const int64_t off = goff[u] + (a * Ru + 8 * bi) * Ru + 8 * bj;
+                    const int32_t t[8] = {c->row0_host[u] + a, (int32_t)(base + 8 * bi),
+                                          (int32_t)std::min<int64_t>(8, Ru - 8 * bi), (int32_t)(base + 8 * bj),
+                                          (int32_t)std::min<int64_t>(8, Ru - 8 * bj),
+                                          (int32_t)(uint32_t)(off & 0xffffffff), (int32_t)(off >> 32), (int32_t)Ru};
+                    tasks.insert(tasks.end(), t, t + TI);
+                }
+    }
+    if ((rc = c->g1.ensure(std::max<size_t>((size_t)gtot, 1) * 4))) return rc;
+    if ((rc = c->g1tasks.ensure(std::max<size_t>(tasks.size(), 1) * 4))) return rc;
+    if ((rc = c->g1rl.ensure(std::max<size_t>(rl.size(), 1) * 4))) return rc;
+    if ((rc = c->g1goff.ensure((size_t)nv * 8))) return rc;
+    if ((rc = c->g1R.ensure((size_t)nv * 4))) return rc;
+    if ((rc = c->g1adj.ensure(std::max<size_t>(adjf.size(), 1) * 4))) return rc;
+    if ((rc = c->g1adjoff.ensure((size_t)(nv + 1) * 4))) return rc;
+    if ((rc = c->g1loff.ensure(std::max<size_t>(loff.size(), 1) * 4))) return rc;
+    auto up = [&](DevBuf &b, const void *h, size_t bytes) -> int {
+        if (bytes) FBN_HIP(hipMemcpyAsync(b.p, h, bytes, hipMemcpyHostToDevice, s));
+        return FBN_OK;
+    };
+    if ((rc = up(c->g1tasks, tasks.data(), tasks.size() * 4)) || (rc = up(c->g1rl, rl.data(), rl.size() * 4)) ||
+        (rc = up(c->g1goff, goff.data(), (size_t)nv * 8)) || (rc = up(c->g1R, R.data(), (size_t)nv * 4)) ||
+        (rc = up(c->g1adj, adjf.data(), adjf.size() * 4)) ||
+        (rc = up(c->g1adjoff, adj_off.data(), (size_t)(nv + 1) * 4)) ||
+        (rc = up(c->g1loff, loff.data(), loff.size() * 4)))
+        return rc;
+    hipError_t e = fbn_ci_gram(c->bits.as<uint32_t>(), c->bits_W, c->g1rl.as<int32_t>(), c->g1tasks.as<int32_t>(),
+                               (long long)(tasks.size() / TI), 1, c->g1.as<int32_t>(), c->num_cu, s);
+    if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci gram level 1: %s", hipGetErrorString(e));
+    FBN_HIP(hipStreamSynchronize(s));  // the host vectors go out of scope
+    *ready = c->triples_ready = true;
+    return FBN_OK;
 }
 int CiBatchWait(fbn_ci_ctx *c, int k, uint8_t *indep, int32_t *df, PCResultHost &res) {
     CiSlot &S = c->slot[k];

@@ -697,6 +697,222 @@ __global__ __launch_bounds__(256) void ci_bits_count_derived_grp(const uint32_t 
     }
 }
 
+// ---- row Gram matrices (levels 0 and 1 of a PC run on the bit-sliced store)
+// A PC run's level 0 needs popcount(r_i & r_j) for every pair of leading mask rows (values 0..d-2
+// of every variable; the last value is derived), and level 1 needs popcount(x_a & r_i & r_j) for
+// the rows of every pair of x's neighbours: both are Gram matrices of mask rows over the sample
+// bits.  One wave per task = an 8 x 8 tile of (i, j) row pairs (optionally every row ANDed with a
+// mask row x_a): per 4-word step 16 (17) 16-byte loads feed 256 popcounts, counters in registers,
+// then a butterfly reduction that leaves counter l's wave total in lane l (63 shuffles instead of
+// 64 x 6).  Tasks are built on the host (capi.hip CiGram*): one block of one wave per task so the
+// task fields and row pointers are wave-uniform (scalar registers).
+constexpr int kGramTaskInts = 8;  // mask row (-1: none), i0, ni, j0, nj, out offset (lo, hi), ld
+
+template <bool MASKED>
+__global__ __launch_bounds__(64) void ci_bits_gram(const uint32_t *__restrict__ bits, long long W,
+                                                   const int32_t *__restrict__ rl, const int32_t *__restrict__ tasks,
+                                                   long long ntasks, int32_t *__restrict__ out) {
+    typedef __attribute__((ext_vector_type(4))) unsigned u4;
+    const int lane = threadIdx.x;
+    for (long long k = blockIdx.x; k < ntasks; k += gridDim.x) {
+        const int32_t *t = tasks + k * kGramTaskInts;
+        const int mrow = t[0], i0 = t[1], ni = t[2], j0 = t[3], nj = t[4], ld = t[7];
+        const long long off = (long long)(uint32_t)t[5] | ((long long)t[6] << 32);
+        const uint32_t *pi[8], *pj[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) pi[r] = bits + (size_t)rl[i0 + (r < ni ? r : 0)] * W;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) pj[r] = bits + (size_t)rl[j0 + (r < nj ? r : 0)] * W;
+        const uint32_t *pm = bits + (size_t)(MASKED ? mrow : 0) * W;
+        uint32_t v[64];
+#pragma unroll
+        for (int c = 0; c < 64; ++c) v[c] = 0u;
+        for (long long w4 = lane; 4 * w4 < W; w4 += 64) {
+            u4 xi[8], yj[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) xi[r] = *reinterpret_cast<const u4 *>(pi[r] + 4 * w4);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) yj[r] = *reinterpret_cast<const u4 *>(pj[r] + 4 * w4);
+            if (MASKED) {
+                const u4 m = *reinterpret_cast<const u4 *>(pm + 4 * w4);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) xi[r] &= m;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int a = 0; a < 8; ++a)
+#pragma unroll
+                    for (int b = 0; b < 8; ++b) v[a * 8 + b] += __builtin_popcount(xi[a][q] & yj[b][q]);
+        }
+        // butterfly: at distance o each lane keeps the half of its counters selected by lane bit o
+        // and adds its partner's copy of that half; lane l ends with counter l's total
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const bool hi = (lane & o) != 0;
+#pragma unroll
+            for (int c = 0; c < o; ++c) {
+                const uint32_t send = hi ? v[c] : v[c + o], keep = hi ? v[c + o] : v[c];
+                v[c] = keep + (uint32_t)__shfl_xor((int)send, o);
+            }
+        }
+        const int a = lane >> 3, b = lane & 7;
+        if (a < ni && b < nj) out[off + (long long)a * ld + b] = (int32_t)v[0];
+    }
+}
+
+// level 0 from the Gram G of all leading rows (ld x ld, lead0[v] = v's first leading row): the
+// (x < y) pair table of test t (pair t0 + t of the complete graph), last row / column derived from
+// the per-row sample counts exactly as pair_block / count_pair; the 64-slot record and, when
+// recording, the pair table
+template <int DX, int DY>
+__device__ __forceinline__ void gram_pair(const int32_t *__restrict__ G, long long ld, int x, int y,
+                                          const int32_t *__restrict__ lead0, const int32_t *__restrict__ cx,
+                                          const int32_t *__restrict__ cy, int32_t *__restrict__ out,
+                                          int32_t *__restrict__ ptab) {
+    constexpr int MX = DX - 1, MY = DY - 1;
+    int32_t full[DX * DY];
+    const int32_t *g = G + (long long)lead0[x] * ld + lead0[y];
+#pragma unroll
+    for (int i = 0; i < MX; ++i) {
+        int32_t r = cx[i];
+#pragma unroll
+        for (int j = 0; j < MY; ++j) full[i * DY + j] = g[i * ld + j], r -= full[i * DY + j];
+        full[i * DY + MY] = r;
+    }
+#pragma unroll
+    for (int j = 0; j < DY; ++j) {
+        int32_t r = cy[j];
+#pragma unroll
+        for (int i = 0; i < MX; ++i) r -= full[i * DY + j];
+        full[MX * DY + j] = r;
+    }
+#pragma unroll
+    for (int c = 0; c < DX * DY; ++c) out[c] = full[c];
+    if (ptab)
+#pragma unroll
+        for (int c = 0; c < DX * DY; ++c) ptab[c] = full[c];
+}
+
+__global__ __launch_bounds__(256) void ci_bits_gram_pairs(const int32_t *__restrict__ G, long long ld,
+                                                          const int32_t *__restrict__ lead0,
+                                                          const int32_t *__restrict__ dims,
+                                                          const int32_t *__restrict__ row0,
+                                                          const int32_t *__restrict__ rowcnt, long long t0, long long n,
+                                                          int nvars, int32_t *__restrict__ counts,
+                                                          int32_t *__restrict__ pairtab) {
+    for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t < n; t += (long long)gridDim.x * 256) {
+        int x, y;
+        pair_of(t0 + t, nvars, x, y);
+        int32_t *out = counts + t * kBitsCells, *ptab = pairtab ? pairtab + 16 * (t0 + t) : nullptr;
+        const int32_t *cx = rowcnt + row0[x], *cy = rowcnt + row0[y];
+        switch (dims[x] * 8 + dims[y]) {
+#define FBN_GP(A, B)                                                                                         \
+    case A * 8 + B:                                                                                          \
+        gram_pair<A, B>(G, ld, x, y, lead0, cx, cy, out, ptab);                                              \
+        break;
+            FBN_GP(1, 1) FBN_GP(1, 2) FBN_GP(1, 3) FBN_GP(1, 4)
+            FBN_GP(2, 1) FBN_GP(2, 2) FBN_GP(2, 3) FBN_GP(2, 4)
+            FBN_GP(3, 1) FBN_GP(3, 2) FBN_GP(3, 3) FBN_GP(3, 4)
+            FBN_GP(4, 1) FBN_GP(4, 2) FBN_GP(4, 3) FBN_GP(4, 4)
+#undef FBN_GP
+        default: break;
+        }
+    }
+}
+
+// position of v in the sorted list a[0..n) (present by construction)
+__device__ __forceinline__ int find_sorted(const int32_t *__restrict__ a, int n, int v) {
+    int lo = 0, hi = n;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (a[mid] <= v) lo = mid;
+        else hi = mid;
+    }
+    return lo < n && a[lo] == v ? lo : -1;
+}
+
+// level 1 from the per-variable masked Grams: item (x, y, z) reads its (dx-1)(dy-1)(dz-1) leading
+// cells popcount(x_a & y_b & z_c) from G_u, u = x if z is x's neighbour, else y (then x and z are
+// y's neighbours); G_u[a] is R_u x R_u over u's neighbours' leading rows (upper tiles only: the
+// entry is read as (row of the earlier neighbour, row of the later one)).  The rest of the table
+// is derived from the pair tables exactly as count_test_derived; every value is an integer.
+__global__ __launch_bounds__(256) void ci_bits_gram_triples(
+    const int32_t *__restrict__ G, const long long *__restrict__ goff, const int32_t *__restrict__ gR,
+    const int32_t *__restrict__ adj, const int32_t *__restrict__ adj_off, const int32_t *__restrict__ loff,
+    const int32_t *__restrict__ dims, const int32_t *__restrict__ items, long long n, int32_t *__restrict__ counts,
+    const int32_t *__restrict__ pairtab, int nvars) {
+    for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t < n; t += (long long)gridDim.x * 256) {
+        const int x = items[3 * t], y = items[3 * t + 1], z = items[3 * t + 2];
+        const int DX = dims[x], DY = dims[y], DZ = dims[z], MX = DX - 1, MY = DY - 1, MZ = DZ - 1;
+        int pzx = find_sorted(adj + adj_off[x], adj_off[x + 1] - adj_off[x], z);
+        const bool ux = pzx >= 0;
+        const int u = ux ? x : y, o = ux ? y : x;
+        const int32_t *au = adj + adj_off[u];
+        const int nu = adj_off[u + 1] - adj_off[u];
+        const int po = find_sorted(au, nu, o), pz = ux ? pzx : find_sorted(au, nu, z);
+        if (po < 0 || pz < 0) continue;  // not a level-1 item of this skeleton (never generated)
+        const int32_t *lu = loff + adj_off[u];
+        const int Ru = gR[u], ro = lu[po], rz = lu[pz];
+        const bool oz = po < pz;
+        const int32_t *Gu = G + goff[u];
+        // leading cells cnt[c][a][b] (a: value of x, b: value of y, c: value of z)
+        int32_t cnt[3][3][3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    int32_t v = 0;
+                    if (c < MZ && a < MX && b < MY) {
+                        const int ua = ux ? a : b, ob = ux ? b : a;  // u's value, the other's value
+                        const long long ri = ro + ob, rj = rz + c;
+                        v = Gu[((long long)ua * Ru + (oz ? ri : rj)) * Ru + (oz ? rj : ri)];
+                    }
+                    cnt[c][a][b] = v;
+                }
+        const int32_t *Txy = pair_table(pairtab, nvars, x, y), *Txz = pair_table(pairtab, nvars, x, z),
+                      *Tyz = pair_table(pairtab, nvars, y, z);
+        const bool txy = x > y, txz = x > z, tyz = y > z;
+        auto nxy = [&](int a, int b) { return txy ? Txy[b * DX + a] : Txy[a * DY + b]; };
+        auto nxz = [&](int a, int c) { return txz ? Txz[c * DX + a] : Txz[a * DZ + c]; };
+        auto nyz = [&](int b, int c) { return tyz ? Tyz[c * DY + b] : Tyz[b * DZ + c]; };
+        // N[c][a][b] for c < MZ: leading cells, then the last y value, then the last x value
+        auto fz = [&](int c, int a, int b) {
+            auto row_last = [&](int aa) {  // N[c][aa][MY], aa < MX
+                int32_t r = nxz(aa, c);
+#pragma unroll
+                for (int bb = 0; bb < 3; ++bb)
+                    if (bb < MY) r -= cnt[c][aa][bb];
+                return r;
+            };
+            if (a < MX) return b < MY ? cnt[c][a][b] : row_last(a);
+            int32_t r = nyz(b, c);
+#pragma unroll
+            for (int aa = 0; aa < 3; ++aa)
+                if (aa < MX) r -= b < MY ? cnt[c][aa][b] : row_last(aa);
+            return r;
+        };
+        int32_t *out = counts + t * kBitsCells;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                if (a >= DX || b >= DY) continue;
+                int32_t last = nxy(a, b);
+#pragma unroll
+                for (int c = 0; c < 3; ++c)
+                    if (c < MZ) {
+                        const int32_t v = fz(c, a, b);
+                        out[(c * DX + a) * DY + b] = v;
+                        last -= v;
+                    }
+                out[(MZ * DX + a) * DY + b] = last;
+            }
+    }
+}
+
 // one test's table N[z][x][y] (dimz <= 4 values of z, DX x DY cells each, the 64-slot record of
 // the count kernels) -> G^2 as one running sum in the reference's z -> x -> y order
 // (ComputeGSquareXY / XYZ, src/IndependenceTest.cpp:65-155, 295-364; the same arithmetic as
@@ -905,6 +1121,39 @@ extern "C" hipError_t fbn_ci_bits_pairs_tiled(const uint32_t *bits, const int32_
     return hipGetLastError();
 }
 
+extern "C" int fbn_ci_gram_task_ints(void) { return kGramTaskInts; }
+
+extern "C" hipError_t fbn_ci_gram(const uint32_t *bits, long long W, const int32_t *rl, const int32_t *tasks,
+                                  long long ntasks, int masked, int32_t *out, int num_cu, hipStream_t s) {
+    const long long cap = (long long)num_cu * 32;
+    const dim3 g((unsigned)(ntasks < cap ? ntasks : cap));
+    if (ntasks <= 0) return hipSuccess;
+    if (masked) hipLaunchKernelGGL(ci_bits_gram<true>, g, dim3(64), 0, s, bits, W, rl, tasks, ntasks, out);
+    else hipLaunchKernelGGL(ci_bits_gram<false>, g, dim3(64), 0, s, bits, W, rl, tasks, ntasks, out);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t fbn_ci_gram_pairs(const int32_t *G, long long ld, const int32_t *lead0, const int32_t *dims,
+                                        const int32_t *row0, const int32_t *rowcnt, long long t0, long long n,
+                                        int nvars, int32_t *counts, int32_t *pairtab, int num_cu, hipStream_t s) {
+    const long long g = (n + 255) / 256, cap = (long long)num_cu * 8;
+    if (n > 0)
+        hipLaunchKernelGGL(ci_bits_gram_pairs, dim3((unsigned)(g < cap ? g : cap)), dim3(256), 0, s, G, ld, lead0,
+                           dims, row0, rowcnt, t0, n, nvars, counts, pairtab);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t fbn_ci_gram_triples(const int32_t *G, const long long *goff, const int32_t *gR,
+                                          const int32_t *adj, const int32_t *adj_off, const int32_t *loff,
+                                          const int32_t *dims, const int32_t *items, long long n, int32_t *counts,
+                                          const int32_t *pairtab, int nvars, int num_cu, hipStream_t s) {
+    const long long g = (n + 255) / 256, cap = (long long)num_cu * 8;
+    if (n > 0)
+        hipLaunchKernelGGL(ci_bits_gram_triples, dim3((unsigned)(g < cap ? g : cap)), dim3(256), 0, s, G, goff, gR,
+                           adj, adj_off, loff, dims, items, n, counts, pairtab, nvars);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *dims, const int32_t *row0,
                                          const int32_t *items, long long W, long long n, int d, double alpha,
                                          double *g2, int32_t *df, double *p, uint8_t *indep, int32_t *counts,
@@ -924,7 +1173,9 @@ extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *di
         // FBN_CI_L1MODE: 0 = item per wave, plain grid stride; 1 = item per wave, XCD-contiguous;
         // 2 = quad of items per wave (x/y rows shared in registers), XCD-contiguous
         static const int l1mode = getenv("FBN_CI_L1MODE") ? atoi(getenv("FBN_CI_L1MODE")) : 1;
-        if (pmode == 2 && l1mode == 2) {
+        if (counted) {
+            // the counts are already in place (ci_bits_gram_triples)
+        } else if (pmode == 2 && l1mode == 2) {
             const long long gq = (n + 15) / 16;
             hipLaunchKernelGGL(ci_bits_count_derived_grp, dim3((unsigned)(gq < cap ? gq : cap)), dim3(256), 0, s, bits,
                                dims, row0, items, W, n, counts, (const int32_t *)pairtab, nvars, 1);

@@ -156,6 +156,11 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
         return FBN_OK;
     }
     if (d > kMaxD) return SetError(FBN_ERR_LIMIT, "conditioning set size %d (supported 0..%d)", d, kMaxD);
+    // level 1 on the bit-sliced store: per-variable Grams make every candidate set's table a gather,
+    // so a test costs about its G^2 pass and more speculation per round pays (FBN_PC_FULLSPEC1)
+    bool gram = false;
+    if (d == 1 && !getenv("FBN_CI_NO_GRAM"))
+        if (int rc = CiTriplePrepare(ctx, adj, edges, e_begin, e_end, &gram)) return rc;
     std::vector<EdgeState> st(E);
     for (size_t e = 0; e < E; ++e) {
         st[e].x = edges[e_begin + e].first;
@@ -174,7 +179,7 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
     // small levels: every candidate set of every edge in one round (one host round trip per level;
     // the extra speculative tests cost less than the round trips they save)
     {
-        const int64_t cap = FullSpeculation();
+        const int64_t cap = gram ? EnvOr("FBN_PC_FULLSPEC1", 16384) : FullSpeculation();
         int64_t all = 0;
         for (auto &s : st) {
             if (s.resolved) continue;

@@ -169,6 +169,10 @@ void CiSetPairsRecorded(fbn_ci_ctx *c);
 // must test all pairs i < j: a PC run's level 0), 2 = one-conditioning-variable batches derive the
 // last value of x, y and z from them, 0 = off (also drops what was recorded)
 void CiSetPairMode(fbn_ci_ctx *c, int mode);
+// level 1 of a PC run: per-variable masked Grams for the endpoints of edges [e_begin, e_end)
+// (capi.hip); a no-op when not eligible
+int CiTriplePrepare(fbn_ci_ctx *c, const std::vector<std::vector<int>> &adj,
+                    const std::vector<std::pair<int, int>> &edges, size_t e_begin, size_t e_end, bool *ready);
 int CiBatchWait(fbn_ci_ctx *c, int k, uint8_t *indep, int32_t *df, PCResultHost &res);
 int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResultHost &res);
 // one level for an edge range (the unit a multi-GPU driver partitions), see pc_driver.cpp

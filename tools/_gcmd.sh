@@ -3,13 +3,17 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_pc.py tests/test_gpu_pc_dist.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t_pc.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/t_pc.log; exit 1; }
 tail -1 gpurun_out/t_pc.log
-timeout -k 10 120 python tools/pc5_timing.py 4 2>&1 | grep -E "run " | tail -2
-FBN_CI_NO_BAND=1 timeout -k 10 120 python tools/pc5_timing.py 4 2>&1 | grep -E "run " | tail -1
+timeout -k 10 120 python tools/pc5_cands.py 2>&1 | tail -1
+echo "default"; timeout -k 10 120 python tools/pc5_timing.py 4 2>&1 | grep -E "run " | tail -1
+echo "no gram"; FBN_CI_NO_GRAM=1 timeout -k 10 120 python tools/pc5_timing.py 4 2>&1 | grep -E "run " | tail -1
+echo "fullspec1"; FBN_PC_FULLSPEC1=4000000 timeout -k 10 120 python tools/pc5_timing.py 4 2>&1 | grep -E "run " | tail -1
+echo "round0 64k"; FBN_PC_ROUND0=65536 timeout -k 10 120 python tools/pc5_timing.py 4 2>&1 | grep -E "run " | tail -1
+FBN_PC_TIMING=1 timeout -k 10 120 python tools/pc5_timing.py 2 2>&1 | grep -E "^pc" | tail -7
 timeout -k 10 120 python tools/pc_alarm_timing.py 2>&1 | tail -1
 mkdir -p gpurun_out/bprof
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/bprof -o run --output-format csv -- python tools/pc5_timing.py 3 > /dev/null 2>&1 || exit 1
 python3 -c "
 import csv
-for r in list(csv.DictReader(open('gpurun_out/bprof/run_kernel_stats.csv')))[:8]:
+for r in list(csv.DictReader(open('gpurun_out/bprof/run_kernel_stats.csv')))[:10]:
     print(r['Name'][:60], r['Calls'], round(float(r['AverageNs'])/1e3,1), 'us', round(float(r['TotalDurationNs'])/1e6/3,3), 'ms/run')
 "
