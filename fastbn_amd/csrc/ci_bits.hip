@@ -913,72 +913,13 @@ __global__ __launch_bounds__(256) void ci_bits_gram_triples(
     }
 }
 
-// one test's table N[z][x][y] (dimz <= 4 values of z, DX x DY cells each, the 64-slot record of
-// the count kernels) -> G^2 as one running sum in the reference's z -> x -> y order
-// (ComputeGSquareXY / XYZ, src/IndependenceTest.cpp:65-155, 295-364; the same arithmetic as
-// ci_g2_kernel) and the adjusted df.  The table is loaded with independent 16-byte loads up front
-// and every index is compile-time, so the <= 64 logs are independent instructions the compiler
-// interleaves (a lane's tests are otherwise a chain of dependent loads and long-latency fp64).
-template <int DX, int DY>
-__device__ __forceinline__ void g2_of_table(const int32_t *__restrict__ hz, int dimz, double &g2o, int &dfo) {
-    constexpr int DXY = DX * DY, NQ = DXY;  // 4 * DXY cells at most = DXY int4s
-    typedef __attribute__((ext_vector_type(4))) int i4;
-    i4 q[NQ];
-#pragma unroll
-    for (int v = 0; v < NQ; ++v)
-        q[v] = 4 * v < dimz * DXY ? reinterpret_cast<const i4 *>(hz)[v] : i4{0, 0, 0, 0};
-    auto cell = [&](int c) { return q[c / 4][c % 4]; };
-    double g2 = 0.0;
-    int df = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        if (k >= dimz) break;
-        int ni[DX], nj[DY];
-        long total = 0;
-        int alx = 0, aly = 0;
-#pragma unroll
-        for (int i = 0; i < DX; ++i) {
-            int s = 0;
-#pragma unroll
-            for (int j = 0; j < DY; ++j) s += cell(k * DXY + i * DY + j);
-            ni[i] = s;
-            alx += s > 0;
-            total += s;
-        }
-#pragma unroll
-        for (int j = 0; j < DY; ++j) {
-            int s = 0;
-#pragma unroll
-            for (int i = 0; i < DX; ++i) s += cell(k * DXY + i * DY + j);
-            nj[j] = s;
-            aly += s > 0;
-        }
-        alx = alx >= 1 ? alx : 1;
-        aly = aly >= 1 ? aly : 1;
-        df += (alx - 1) * (aly - 1);
-        if (total != 0) {
-#pragma unroll
-            for (int i = 0; i < DX; ++i) {
-                const long sum_row = ni[i];
-#pragma unroll
-                for (int j = 0; j < DY; ++j) {
-                    const long sum_col = nj[j];
-                    const long observed = cell(k * DXY + i * DY + j);
-                    // a skipped cell adds nothing (the reference's `continue`s)
-                    if (sum_row == 0 || sum_col == 0 || observed == 0) continue;
-                    const double expected = (double)sum_col * (double)sum_row / (double)total;
-                    g2 += 2.0 * observed * log(observed / expected);
-                }
-            }
-        }
-    }
-    g2o = g2, dfo = df;
-}
-
-// phase 2: one lane per test (g2_of_table per state-count class), p = 1 - P(df/2, G^2/2)
-// (ci_chisq.h).  With no p output and a decision band (band != nullptr: [lo, hi] per df 1..nband,
-// then delta), p is only evaluated for G^2 inside the band (fbn_chisq_band).  The margin log is
-// reduced per wave (one atomic per wave, not per test).
+// phase 2: one lane per test -- per z: marginals, adjusted df; G^2 as one running sum in the
+// reference's z -> x -> y order (ComputeGSquareXY / XYZ, src/IndependenceTest.cpp:65-155,
+// 295-364; the same arithmetic as ci_g2_kernel), p = 1 - P(df/2, G^2/2) (ci_chisq.h).  With no p
+// output and a decision band (band != nullptr: [lo, hi] per df 1..nband, then delta), p is only
+// evaluated for G^2 inside the band (fbn_chisq_band).  The margin log is reduced per wave (one
+// atomic per wave, not per test).  (Measured and not kept: 16 lanes per test with the terms in
+// LDS, 10x slower at level 0; per-class instantiations with the table in registers, 1.7x slower.)
 template <int D>
 __global__ __launch_bounds__(256) void ci_bits_g2(const int32_t *__restrict__ counts, const int32_t *__restrict__ dims,
                                                   const int32_t *__restrict__ items, long long n, double alpha,
@@ -999,20 +940,45 @@ __global__ __launch_bounds__(256) void ci_bits_g2(const int32_t *__restrict__ co
             else px = items[(2 + D) * t], py = items[(2 + D) * t + 1];
             const int dx = dims[px], dy = dims[py];
             const int dimz = D == 1 ? dims[items[3 * t + 2]] : 1;
+            const int dxy = dx * dy;
             const int32_t *hz = counts + t * kBitsCells;
+            // one running sum over z -> x -> y, exactly the reference's loop (no per-z partials)
             double g2 = 0.0;
             int df = 0;
-            switch (dx * 8 + dy) {
-#define FBN_G2(A, B)                                                                                         \
-    case A * 8 + B:                                                                                          \
-        g2_of_table<A, B>(hz, dimz, g2, df);                                                                 \
-        break;
-                FBN_G2(1, 1) FBN_G2(1, 2) FBN_G2(1, 3) FBN_G2(1, 4)
-                FBN_G2(2, 1) FBN_G2(2, 2) FBN_G2(2, 3) FBN_G2(2, 4)
-                FBN_G2(3, 1) FBN_G2(3, 2) FBN_G2(3, 3) FBN_G2(3, 4)
-                FBN_G2(4, 1) FBN_G2(4, 2) FBN_G2(4, 3) FBN_G2(4, 4)
-#undef FBN_G2
-            default: break;
+            for (int k = 0; k < dimz; ++k) {
+                const int32_t *h = hz + k * dxy;
+                int ni[4], nj[4];
+                long total = 0;
+                int alx = 0, aly = 0;
+                for (int i = 0; i < dx; ++i) {
+                    int s = 0;
+                    for (int j = 0; j < dy; ++j) s += h[i * dy + j];
+                    ni[i] = s;
+                    alx += s > 0;
+                    total += s;
+                }
+                for (int j = 0; j < dy; ++j) {
+                    int s = 0;
+                    for (int i = 0; i < dx; ++i) s += h[i * dy + j];
+                    nj[j] = s;
+                    aly += s > 0;
+                }
+                alx = alx >= 1 ? alx : 1;
+                aly = aly >= 1 ? aly : 1;
+                df += (alx - 1) * (aly - 1);
+                if (total != 0) {
+                    for (int i = 0; i < dx; ++i) {
+                        const long sum_row = ni[i];
+                        if (sum_row == 0) continue;
+                        for (int j = 0; j < dy; ++j) {
+                            const long sum_col = nj[j];
+                            const long observed = h[i * dy + j];
+                            if (sum_col == 0 || observed == 0) continue;
+                            const double expected = (double)sum_col * (double)sum_row / (double)total;
+                            g2 += 2.0 * observed * log(observed / expected);
+                        }
+                    }
+                }
             }
             double p = 1.0, m;
             bool ind;
@@ -1033,7 +999,7 @@ __global__ __launch_bounds__(256) void ci_bits_g2(const int32_t *__restrict__ co
             if (po) po[t] = p;
             indep[t] = ind;
             if (counts0 && t == 0)
-                for (int c = 0; c < dimz * dx * dy; ++c) counts0[c] = hz[c];
+                for (int c = 0; c < dimz * dxy; ++c) counts0[c] = hz[c];
             mbits = (unsigned long long)__double_as_longlong(m);
             near = m < 1e-9;
         }

@@ -156,10 +156,12 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
         return FBN_OK;
     }
     if (d > kMaxD) return SetError(FBN_ERR_LIMIT, "conditioning set size %d (supported 0..%d)", d, kMaxD);
-    // level 1 on the bit-sliced store: per-variable Grams make every candidate set's table a gather,
-    // so a test costs about its G^2 pass and more speculation per round pays (FBN_PC_FULLSPEC1)
+    // level 1 on the bit-sliced store, FBN_CI_GRAM1 = 1: per-variable Grams make every candidate
+    // set's table a gather (a test then costs about its G^2 pass; FBN_PC_FULLSPEC1 = speculation
+    // cap).  Off by default: config 5's Grams cover all 3.46M candidate sets (45.9 G popcount words,
+    // 4.6 ms) where the rounds launch 0.39M sets (1.9 ms of derived counting).
     bool gram = false;
-    if (d == 1 && !getenv("FBN_CI_NO_GRAM"))
+    if (d == 1 && getenv("FBN_CI_GRAM1") && !getenv("FBN_CI_NO_GRAM"))
         if (int rc = CiTriplePrepare(ctx, adj, edges, e_begin, e_end, &gram)) return rc;
     std::vector<EdgeState> st(E);
     for (size_t e = 0; e < E; ++e) {

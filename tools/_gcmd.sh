@@ -3,11 +3,11 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_pc.py tests/test_gpu_pc_dist.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t_pc.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/t_pc.log; exit 1; }
 tail -1 gpurun_out/t_pc.log
-timeout -k 10 120 python tools/pc5_cands.py 2>&1 | tail -1
+FBN_CI_GRAM1=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_pc.py -x -q --timeout 200 --timeout-method thread -k "config5 or alarm" > gpurun_out/t_pc2.log 2>&1 || { echo "gram1 tests failed"; tail -40 gpurun_out/t_pc2.log; exit 1; }
+tail -1 gpurun_out/t_pc2.log
 echo "default"; timeout -k 10 120 python tools/pc5_timing.py 4 2>&1 | grep -E "run " | tail -1
-echo "no gram"; FBN_CI_NO_GRAM=1 timeout -k 10 120 python tools/pc5_timing.py 4 2>&1 | grep -E "run " | tail -1
-echo "fullspec1"; FBN_PC_FULLSPEC1=4000000 timeout -k 10 120 python tools/pc5_timing.py 4 2>&1 | grep -E "run " | tail -1
-echo "round0 64k"; FBN_PC_ROUND0=65536 timeout -k 10 120 python tools/pc5_timing.py 4 2>&1 | grep -E "run " | tail -1
+for r in 131072 262144 1048576; do echo "round0 $r"; FBN_PC_ROUND0=$r timeout -k 10 120 python tools/pc5_timing.py 4 2>&1 | grep -E "run " | tail -1; done
+echo "growth 8"; FBN_PC_GROWTH=8 timeout -k 10 120 python tools/pc5_timing.py 4 2>&1 | grep -E "run " | tail -1
 FBN_PC_TIMING=1 timeout -k 10 120 python tools/pc5_timing.py 2 2>&1 | grep -E "^pc" | tail -7
 timeout -k 10 120 python tools/pc_alarm_timing.py 2>&1 | tail -1
 mkdir -p gpurun_out/bprof
