@@ -39,6 +39,17 @@ extern "C" hipError_t fbn_ci_bits_rowcount(const uint32_t *bits, long long rows,
                                            hipStream_t s);
 extern "C" int fbn_ci_pair_block(int d);
 extern "C" int fbn_ci_gram_task_ints(void);
+extern "C" size_t fbn_ci_l1_edge_bytes(void);
+extern "C" hipError_t fbn_ci_l1_setup(const int32_t *pairs, int E, const int32_t *adj, const int32_t *adj_off,
+                                      void *ed, int32_t *pos, uint8_t *st, int32_t *sep, long long *counted,
+                                      hipStream_t s);
+extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims, const int32_t *row0, long long W,
+                                      const int32_t *adj, const int32_t *pairtab, int nvars, void *edv, int32_t *pos,
+                                      uint8_t *st, int32_t *sep, long long *counted, int32_t *len, int32_t *off,
+                                      int E, int chunk, long long cap, long long *total, long long *launched,
+                                      int32_t *items, int32_t *counts, int32_t *df, uint8_t *indep, double alpha,
+                                      unsigned long long *stats, const double *band, int nband, unsigned *open_cnt,
+                                      unsigned long long *rows_read, int num_cu, hipStream_t s);
 extern "C" hipError_t fbn_ci_gram(const uint32_t *bits, long long W, const int32_t *rl, const int32_t *tasks,
                                   long long ntasks, int masked, int32_t *out, int num_cu, hipStream_t s);
 extern "C" hipError_t fbn_ci_gram_pairs(const int32_t *G, long long ld, const int32_t *lead0, const int32_t *dims,
@@ -205,6 +216,12 @@ struct fbn_ci_ctx {
     // by the next d = 1 batches while triples_ready
     DevBuf g1, g1tasks, g1rl, g1goff, g1R, g1adj, g1adjoff, g1loff;
     bool triples_ready = false;
+    // device-resident level-1 search (CiLevel1Device): edge state, round buffers, per-round open
+    // counts (pinned mirror), round events
+    DevBuf l1pairs, l1adj, l1adjoff, l1ed, l1pos, l1st, l1sep, l1cnt, l1len, l1off, l1scal, l1open;
+    DevBuf l1items, l1counts, l1df, l1indep;
+    unsigned *h_open = nullptr;
+    hipEvent_t l1ev[2] = {nullptr, nullptr};
     // decision band of the bit-sliced G^2 kernel for alpha = band_alpha (ci_chisq.h fbn_chisq_band):
     // [lo, hi] per df 1..kBandDf, then delta; host copy kept alive for the async upload
     DevBuf band;
@@ -217,9 +234,17 @@ struct fbn_ci_ctx {
     float last_ms = 0.f;
     bool timing = true;  // HIP events around every CI kernel (fbn_ci_set_kernel_timing)
     ~fbn_ci_ctx() {
+        if (h_open) (void)hipHostFree(h_open);
+        for (auto &e : l1ev)
+            if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
+
+static int64_t EnvOr0(const char *name, int64_t dflt) {
+    const char *v = getenv(name);
+    return v ? atoll(v) : dflt;
+}
 
 // df <= 36 covers every bit-sliced test (<= 4 states, <= 1 conditioning variable: 4 * 3 * 3)
 constexpr int kBandDf = 36;
@@ -1587,6 +1612,115 @@ void CiSetPairsRecorded(fbn_ci_ctx *c) {
     c->pair_mode = 2;
     c->pairs_recorded = true;
 }
+// A PC run's level 1 (group size 1) entirely on the device: ci_bits.hip's ci_l1_* kernels keep every
+// edge's search state in device memory, generate each round's tests from the adjacency, count them
+// from the bit-sliced store + pair tables, decide and resolve each edge's prefix in order; the host
+// enqueues rounds (next chunk x4, FBN_PC_ROUND0 / FBN_PC_GROWTH as the host driver) and reads one
+// open-edge count per round, one round behind, to stop.  Results equal the host driver's: the same
+// tests in the same per-edge order and the same first-independent rule.  *done = false when not
+// eligible (the host driver runs the level).
+constexpr int kL1MaxRounds = 256;
+int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<int>> &adj,
+                   const std::vector<std::pair<int, int>> &edges, size_t e_begin, size_t e_end, LevelOut &out,
+                   PCResultHost &res, bool *done) {
+    *done = false;
+    if (c->pair_mode != 2 || !c->pairs_recorded || !c->bits_ready || getenv("FBN_PC_HOST_L1")) return FBN_OK;
+    const int nv = c->nvars;
+    for (int v = 0; v < nv; ++v)
+        if (c->dims[v] > 4) return FBN_OK;
+    const int E = (int)(e_end - e_begin);
+    out.removed.assign(E, 0);
+    out.d = 1;
+    out.sep.assign(E, -1);
+    out.counted = out.launched = 0;
+    *done = true;
+    if (E == 0) return FBN_OK;
+    FBN_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    int rc;
+    std::vector<int32_t> adjf, adj_off(nv + 1, 0);
+    for (int u = 0; u < nv; ++u) {
+        adj_off[u] = (int32_t)adjf.size();
+        adjf.insert(adjf.end(), adj[u].begin(), adj[u].end());
+    }
+    adj_off[nv] = (int32_t)adjf.size();
+    int64_t cands = 0;  // every candidate set of the range: the most one round could hold
+    for (size_t e = e_begin; e < e_end; ++e) cands += adj[edges[e].first].size() + adj[edges[e].second].size() - 2;
+    const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(cands, EnvOr0("FBN_PC_L1CAP", 1 << 19)));
+    if ((rc = c->l1pairs.ensure((size_t)E * 8)) || (rc = c->l1adj.ensure(std::max<size_t>(adjf.size(), 1) * 4)) ||
+        (rc = c->l1adjoff.ensure((size_t)(nv + 1) * 4)) || (rc = c->l1ed.ensure((size_t)E * fbn_ci_l1_edge_bytes())) ||
+        (rc = c->l1pos.ensure((size_t)E * 4)) || (rc = c->l1st.ensure((size_t)E)) ||
+        (rc = c->l1sep.ensure((size_t)E * 4)) || (rc = c->l1cnt.ensure((size_t)E * 8)) ||
+        (rc = c->l1len.ensure((size_t)E * 4)) || (rc = c->l1off.ensure((size_t)E * 4)) ||
+        (rc = c->l1scal.ensure(32)) || (rc = c->l1open.ensure(kL1MaxRounds * 4)) ||
+        (rc = c->l1items.ensure((size_t)cap * 12)) || (rc = c->l1counts.ensure((size_t)cap * 256)) ||
+        (rc = c->l1df.ensure((size_t)cap * 4)) || (rc = c->l1indep.ensure((size_t)cap)))
+        return rc;
+    if (!c->h_open) {
+        hipError_t e = hipHostMalloc((void **)&c->h_open, kL1MaxRounds * 4, hipHostMallocDefault);
+        if (e != hipSuccess) return SetError(FBN_ERR_NOMEM, "hipHostMalloc: %s", hipGetErrorString(e));
+        for (auto &ev : c->l1ev) FBN_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
+    const double *band = nullptr;
+    if ((rc = CiBand(c, alpha, s, &band))) return rc;
+    static_assert(sizeof(std::pair<int, int>) == 8, "pair layout");
+    FBN_HIP(hipMemcpyAsync(c->l1pairs.p, edges.data() + e_begin, (size_t)E * 8, hipMemcpyHostToDevice, s));
+    if (!adjf.empty()) FBN_HIP(hipMemcpyAsync(c->l1adj.p, adjf.data(), adjf.size() * 4, hipMemcpyHostToDevice, s));
+    FBN_HIP(hipMemcpyAsync(c->l1adjoff.p, adj_off.data(), (size_t)(nv + 1) * 4, hipMemcpyHostToDevice, s));
+    FBN_HIP(hipMemsetAsync(c->l1scal.p, 0, 32, s));
+    FBN_HIP(hipMemsetAsync(c->l1open.p, 0, kL1MaxRounds * 4, s));
+    CiSlot &S = c->slot[0];
+    if (c->timing) FBN_HIP(hipEventRecord(S.ev0, s));
+    hipError_t e = fbn_ci_l1_setup(c->l1pairs.as<int32_t>(), E, c->l1adj.as<int32_t>(), c->l1adjoff.as<int32_t>(),
+                                   c->l1ed.p, c->l1pos.as<int32_t>(), c->l1st.as<uint8_t>(), c->l1sep.as<int32_t>(),
+                                   c->l1cnt.as<long long>(), s);
+    if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci level-1 setup: %s", hipGetErrorString(e));
+    long long *scal = c->l1scal.as<long long>();  // total, launched, rows read
+    int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(32, EnvOr0("FBN_PC_ROUND0", 8192) / E));
+    const int64_t growth = std::max<int64_t>(2, EnvOr0("FBN_PC_GROWTH", 4));
+    for (int r = 0;; ++r) {
+        if (r >= kL1MaxRounds) return SetError(FBN_ERR_LIMIT, "level 1: more than %d device rounds", kL1MaxRounds);
+        e = fbn_ci_l1_round(c->bits.as<uint32_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(), c->bits_W,
+                            c->l1adj.as<int32_t>(), c->pairtab.as<int32_t>(), nv, c->l1ed.p, c->l1pos.as<int32_t>(),
+                            c->l1st.as<uint8_t>(), c->l1sep.as<int32_t>(), c->l1cnt.as<long long>(),
+                            c->l1len.as<int32_t>(), c->l1off.as<int32_t>(), E, (int)chunk, cap, scal, scal + 1,
+                            c->l1items.as<int32_t>(), c->l1counts.as<int32_t>(), c->l1df.as<int32_t>(),
+                            c->l1indep.as<uint8_t>(), alpha, c->stats.as<unsigned long long>(), band, kBandDf,
+                            c->l1open.as<unsigned>() + r, reinterpret_cast<unsigned long long *>(scal + 2), c->num_cu,
+                            s);
+        if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci level-1 round: %s", hipGetErrorString(e));
+        FBN_HIP(hipMemcpyAsync(c->h_open + r, c->l1open.as<unsigned>() + r, 4, hipMemcpyDeviceToHost, s));
+        FBN_HIP(hipEventRecord(c->l1ev[r & 1], s));
+        if (r >= 1) {  // round r - 1's open count, while round r runs
+            FBN_HIP(hipEventSynchronize(c->l1ev[(r - 1) & 1]));
+            if (c->h_open[r - 1] == 0) break;  // round r found nothing to do
+        }
+        chunk = std::min<int64_t>(chunk * growth, 1 << 16);
+    }
+    if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
+    std::vector<uint8_t> st(E);
+    std::vector<long long> cnt(E);
+    long long sc[3];
+    FBN_HIP(hipMemcpyAsync(st.data(), c->l1st.p, (size_t)E, hipMemcpyDeviceToHost, s));
+    FBN_HIP(hipMemcpyAsync(out.sep.data(), c->l1sep.p, (size_t)E * 4, hipMemcpyDeviceToHost, s));
+    FBN_HIP(hipMemcpyAsync(cnt.data(), c->l1cnt.p, (size_t)E * 8, hipMemcpyDeviceToHost, s));
+    FBN_HIP(hipMemcpyAsync(sc, scal, 24, hipMemcpyDeviceToHost, s));
+    FBN_HIP(hipStreamSynchronize(s));
+    for (int i = 0; i < E; ++i) {
+        out.removed[i] = st[i] == 1;
+        if (st[i] != 1) out.sep[i] = -1;
+        out.counted += cnt[i];
+    }
+    out.launched = sc[1];
+    if (c->timing) {
+        float ms = 0.f;
+        FBN_HIP(hipEventElapsedTime(&ms, S.ev0, S.ev1));
+        res.kernel_s += ms * 1e-3;
+    }
+    res.device_bytes += sc[2] * c->bits_W * 4;
+    return FBN_OK;
+}
+
 // per-variable masked Grams of a PC run's level 1: for every endpoint u of the edges [e_begin,
 // e_end), G_u[a] = popcount(u_a & r_i & r_j) over u's neighbours' leading rows (upper 8 x 8 tiles),
 // enqueued on the ctx stream ahead of the level's batches; their tests then gather the leading

@@ -497,205 +497,17 @@ __device__ __forceinline__ void count_derived_items(const uint32_t *__restrict__
     }
 }
 
-// the kernel's register count is the largest instantiation's (DX = DY = DZ = 4); FBN_CI_L1WAVES
-// asks the compiler for more waves per SIMD instead (fewer registers, more L2 round trips in flight)
-#define FBN_DERIVED_KERNEL(NAME, ATTR)                                                                          \
-    __global__ __launch_bounds__(256) ATTR void NAME(const uint32_t *__restrict__ bits,                        \
-                                                     const int32_t *__restrict__ dims,                         \
-                                                     const int32_t *__restrict__ row0,                         \
-                                                     const int32_t *__restrict__ items, long long W, long long n, \
-                                                     int32_t *__restrict__ counts,                             \
-                                                     const int32_t *__restrict__ pairtab, int nvars, int xcd) {  \
-        count_derived_items(bits, dims, row0, items, W, n, counts, pairtab, nvars, xcd);                       \
-    }
-FBN_DERIVED_KERNEL(ci_bits_count_derived, )
-FBN_DERIVED_KERNEL(ci_bits_count_derived_w4, __attribute__((amdgpu_waves_per_eu(4))))
-FBN_DERIVED_KERNEL(ci_bits_count_derived_w5, __attribute__((amdgpu_waves_per_eu(5))))
-FBN_DERIVED_KERNEL(ci_bits_count_derived_w6, __attribute__((amdgpu_waves_per_eu(6))))
-#undef FBN_DERIVED_KERNEL
-
-// level >= 1 of a PC run, grouped: consecutive items that share (x, y) -- an edge's candidate
-// conditioning variables, which the driver emits contiguously -- are counted together: per 4-word
-// step the x and y mask rows are loaded once and x_a & y_b formed once for the whole group, each
-// item adds only its z rows.  Per item the counts and the derived last values are exactly
-// count_test_derived's (z's state count is a runtime value here, <= 4).  Quads of items that do not
-// share (x, y) fall back to count_test_derived item by item.
-template <int DX, int DY>
-__device__ __forceinline__ void count_group_derived(const uint32_t *__restrict__ bits, const int32_t *__restrict__ dims,
-                                                    const int32_t *__restrict__ row0, const int32_t *__restrict__ items,
-                                                    long long t0, int m, long long W, int lane,
-                                                    int32_t *__restrict__ counts, const int32_t *__restrict__ pairtab,
-                                                    int nvars, int32_t *__restrict__ sc) {
-    constexpr int MX = DX - 1, MY = DY - 1, NXY = MX * MY > 0 ? MX * MY : 1;
-    constexpr int G = MX * MY >= 6 ? 2 : 4;  // items per register group
-    typedef __attribute__((ext_vector_type(4))) unsigned u4;
-    const int x = items[3 * t0], y = items[3 * t0 + 1];
-    const uint32_t *bx = bits + (size_t)row0[x] * W, *by = bits + (size_t)row0[y] * W;
-    const int32_t *Txy = pair_table(pairtab, nvars, x, y);
-    const bool txy = x > y;
-    for (int g0 = 0; g0 < m; g0 += G) {
-        const int gm = m - g0 < G ? m - g0 : G;
-        int zv[G], dz[G];
-        const uint32_t *bz[G];
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            zv[g] = items[3 * (t0 + g0 + (g < gm ? g : 0)) + 2];
-            dz[g] = g < gm ? dims[zv[g]] : 1;  // a padding item counts nothing
-            bz[g] = bits + (size_t)row0[zv[g]] * W;
-        }
-        uint32_t cnt[G][3][NXY];
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int c = 0; c < 3; ++c)
-#pragma unroll
-                for (int k = 0; k < NXY; ++k) cnt[g][c][k] = 0u;
-        if (MX > 0 && MY > 0) {
-            for (long long w4 = lane; 4 * w4 < W; w4 += 64) {
-                u4 xv[MX > 0 ? MX : 1], yv[MY > 0 ? MY : 1];
-#pragma unroll
-                for (int a = 0; a < MX; ++a) xv[a] = *reinterpret_cast<const u4 *>(bx + a * W + 4 * w4);
-#pragma unroll
-                for (int b = 0; b < MY; ++b) yv[b] = *reinterpret_cast<const u4 *>(by + b * W + 4 * w4);
-                u4 zr[G][3];
-#pragma unroll
-                for (int g = 0; g < G; ++g)
-#pragma unroll
-                    for (int c = 0; c < 3; ++c)
-                        zr[g][c] = c < dz[g] - 1 ? *reinterpret_cast<const u4 *>(bz[g] + c * W + 4 * w4)
-                                                 : u4{0u, 0u, 0u, 0u};
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-#pragma unroll
-                    for (int a = 0; a < MX; ++a)
-#pragma unroll
-                        for (int b = 0; b < MY; ++b) {
-                            const uint32_t xy = xv[a][k] & yv[b][k];
-#pragma unroll
-                            for (int g = 0; g < G; ++g)
-#pragma unroll
-                                for (int c = 0; c < 3; ++c)
-                                    cnt[g][c][a * MY + b] += __builtin_popcount(xy & zr[g][c][k]);  // absent rows are 0
-                        }
-            }
-#pragma unroll
-            for (int g = 0; g < G; ++g)
-#pragma unroll
-                for (int c = 0; c < 3; ++c)
-#pragma unroll
-                    for (int k = 0; k < NXY; ++k) {
-                        uint32_t v = cnt[g][c][k];
-#pragma unroll
-                        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-                        cnt[g][c][k] = v;
-                    }
-        }
-        // complete each item's table from the pair tables (count_test_derived's derivation, integer
-        // and so order-free): the reduced counts go through this wave's LDS slot, then lane = cell
-        if (lane == 0)
-#pragma unroll
-            for (int g = 0; g < G; ++g)
-#pragma unroll
-                for (int c = 0; c < 3; ++c)
-#pragma unroll
-                    for (int k = 0; k < NXY; ++k) sc[(g * 3 + c) * NXY + k] = (int32_t)cnt[g][c][k];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int a = (lane / DY) % DX, b = lane % DY, c = lane / (DX * DY);
-        for (int g = 0; g < gm; ++g) {
-            const int z = zv[g], DZ = dz[g], MZ = DZ - 1;
-            if (lane >= DZ * DX * DY) continue;
-            const int32_t *Txz = pair_table(pairtab, nvars, x, z), *Tyz = pair_table(pairtab, nvars, y, z);
-            const bool txz = x > z, tyz = y > z;
-            auto S = [&](int cc, int aa, int bb) { return sc[(g * 3 + cc) * NXY + aa * MY + bb]; };
-            auto nxz = [&](int aa, int cc) { return txz ? Txz[cc * DX + aa] : Txz[aa * DZ + cc]; };
-            auto nyz = [&](int bb, int cc) { return tyz ? Tyz[cc * DY + bb] : Tyz[bb * DZ + cc]; };
-            auto fxz = [&](int cc, int aa) {  // N[cc][aa][DY-1]
-                int32_t r = nxz(aa, cc);
-#pragma unroll
-                for (int bb = 0; bb < MY; ++bb) r -= S(cc, aa, bb);
-                return r;
-            };
-            auto f = [&](int cc, int bb) {  // N[cc][a][bb], cc < MZ
-                if (a < MX) return bb < MY ? S(cc, a, bb) : fxz(cc, a);
-                int32_t r = nyz(bb, cc);
-#pragma unroll
-                for (int aa = 0; aa < MX; ++aa) r -= bb < MY ? S(cc, aa, bb) : fxz(cc, aa);
-                return r;
-            };
-            int32_t v;
-            if (c < MZ) {
-                v = f(c, b);
-            } else {
-                v = txy ? Txy[b * DX + a] : Txy[a * DY + b];
-                for (int cc = 0; cc < MZ; ++cc) v -= f(cc, b);
-            }
-            counts[(t0 + g0 + g) * kBitsCells + lane] = v;
-        }
-        __builtin_amdgcn_wave_barrier();  // the slot is rewritten by the next group
-    }
+// n_dev != nullptr: the test count is read on the device (batches generated on the device)
+__global__ __launch_bounds__(256) void ci_bits_count_derived(const uint32_t *__restrict__ bits,
+                                                             const int32_t *__restrict__ dims,
+                                                             const int32_t *__restrict__ row0,
+                                                             const int32_t *__restrict__ items, long long W, long long n,
+                                                             int32_t *__restrict__ counts,
+                                                             const int32_t *__restrict__ pairtab, int nvars, int xcd,
+                                                             const long long *__restrict__ n_dev) {
+    count_derived_items(bits, dims, row0, items, W, n_dev ? *n_dev : n, counts, pairtab, nvars, xcd);
 }
 
-__global__ __launch_bounds__(256) void ci_bits_count_derived_grp(const uint32_t *__restrict__ bits,
-                                                                 const int32_t *__restrict__ dims,
-                                                                 const int32_t *__restrict__ row0,
-                                                                 const int32_t *__restrict__ items, long long W,
-                                                                 long long n, int32_t *__restrict__ counts,
-                                                                 const int32_t *__restrict__ pairtab, int nvars,
-                                                                 int xcd) {
-    __shared__ int32_t slots[4][2 * 3 * 9];  // per wave: a group's reduced counts
-    const int lane = threadIdx.x & 63;
-    int32_t *sc = slots[threadIdx.x >> 6];
-    const XcdSplit sp = xcd_split((n + 3) / 4, threadIdx.x >> 6, 4, xcd);
-    for (long long q = sp.first; q < sp.end; q += sp.stride) {
-        const long long t0 = 4 * q;
-        const int m = n - t0 < 4 ? (int)(n - t0) : 4;
-        const int x = items[3 * t0], y = items[3 * t0 + 1];
-        bool same = true;
-        for (int g = 1; g < m; ++g) same = same && items[3 * (t0 + g)] == x && items[3 * (t0 + g) + 1] == y;
-        if (same) {
-            switch (dims[x] * 8 + dims[y]) {
-#define FBN_GRP(A, B)                                                                                        \
-    case A * 8 + B:                                                                                          \
-        count_group_derived<A, B>(bits, dims, row0, items, t0, m, W, lane, counts, pairtab, nvars, sc);      \
-        break;
-                FBN_GRP(1, 1) FBN_GRP(1, 2) FBN_GRP(1, 3) FBN_GRP(1, 4)
-                FBN_GRP(2, 1) FBN_GRP(2, 2) FBN_GRP(2, 3) FBN_GRP(2, 4)
-                FBN_GRP(3, 1) FBN_GRP(3, 2) FBN_GRP(3, 3) FBN_GRP(3, 4)
-                FBN_GRP(4, 1) FBN_GRP(4, 2) FBN_GRP(4, 3) FBN_GRP(4, 4)
-#undef FBN_GRP
-            default: break;
-            }
-            continue;
-        }
-        for (int g = 0; g < m; ++g) {  // mixed quad: item by item
-            const long long t = t0 + g;
-            const int xi = items[3 * t], yi = items[3 * t + 1], zi = items[3 * t + 2];
-            const int dx = dims[xi], dy = dims[yi], dz = dims[zi];
-            const uint32_t *bx = bits + (size_t)row0[xi] * W, *by = bits + (size_t)row0[yi] * W,
-                           *bz = bits + (size_t)row0[zi] * W;
-            const int32_t *Txy = pair_table(pairtab, nvars, xi, yi), *Txz = pair_table(pairtab, nvars, xi, zi),
-                          *Tyz = pair_table(pairtab, nvars, yi, zi);
-            int32_t *out = counts + t * kBitsCells;
-            switch (dz * 64 + dx * 8 + dy) {
-#define FBN_TRIPLE(C, A, B)                                                                                  \
-    case C * 64 + A * 8 + B:                                                                                 \
-        count_test_derived<A, B, C>(bx, by, bz, W, lane, out, Txy, xi > yi, Txz, xi > zi, Tyz, yi > zi);     \
-        break;
-#define FBN_ROW(C)                                                                                           \
-    FBN_TRIPLE(C, 1, 1) FBN_TRIPLE(C, 1, 2) FBN_TRIPLE(C, 1, 3) FBN_TRIPLE(C, 1, 4)                          \
-    FBN_TRIPLE(C, 2, 1) FBN_TRIPLE(C, 2, 2) FBN_TRIPLE(C, 2, 3) FBN_TRIPLE(C, 2, 4)                          \
-    FBN_TRIPLE(C, 3, 1) FBN_TRIPLE(C, 3, 2) FBN_TRIPLE(C, 3, 3) FBN_TRIPLE(C, 3, 4)                          \
-    FBN_TRIPLE(C, 4, 1) FBN_TRIPLE(C, 4, 2) FBN_TRIPLE(C, 4, 3) FBN_TRIPLE(C, 4, 4)
-                FBN_ROW(1) FBN_ROW(2) FBN_ROW(3) FBN_ROW(4)
-#undef FBN_ROW
-#undef FBN_TRIPLE
-            default: break;
-            }
-        }
-    }
-}
 
 // ---- row Gram matrices (levels 0 and 1 of a PC run on the bit-sliced store)
 // A PC run's level 0 needs popcount(r_i & r_j) for every pair of leading mask rows (values 0..d-2
@@ -927,7 +739,8 @@ __global__ __launch_bounds__(256) void ci_bits_g2(const int32_t *__restrict__ co
                                                   double *__restrict__ po, uint8_t *__restrict__ indep,
                                                   int32_t *__restrict__ counts0, unsigned long long *__restrict__ stats,
                                                   int nvars, long long t0, const double *__restrict__ band,
-                                                  int nband) {
+                                                  int nband, const long long *__restrict__ n_dev) {
+    if (n_dev) n = *n_dev;
     const long long stride = (long long)gridDim.x * 256;
     // wave-uniform trip count (the margin reduction below is a whole-wave operation)
     for (long long wb = (long long)blockIdx.x * 256 + (threadIdx.x & ~63); wb < n; wb += stride) {
@@ -1018,6 +831,147 @@ __global__ __launch_bounds__(256) void ci_bits_g2(const int32_t *__restrict__ co
     }
 }
 
+// ---- device-resident level-1 search (a PC run's level 1, group size 1)
+// Edge e = (x < y) of the level's range; its candidate k walks the combined list adj(x)\{y} then
+// adj(y)\{x} in sorted order (CheckEdge's two sides, src/PCStable.cpp:402-470 with d = 1); pos =
+// next candidate, st = 0 open / 1 removed (sep = z of its first independent test) / 2 kept
+// (exhausted).  Every round takes the next `chunk` candidates of each open edge, counts and tests
+// them (ci_bits_count_derived + ci_bits_g2<1> with the test count read on the device) and resolves
+// each edge's prefix in order: counted = tests up to and including the first independent one.  The
+// host only enqueues rounds; nothing per test crosses PCIe.
+struct L1Edge {
+    int32_t x, y, m0, L, skx, sky, ax, ay;  // ax / ay: adjacency offsets, skx / sky: position of y / x
+};
+
+__global__ __launch_bounds__(256) void ci_l1_setup(const int32_t *__restrict__ pairs, int E,
+                                                   const int32_t *__restrict__ adj,
+                                                   const int32_t *__restrict__ adj_off, L1Edge *__restrict__ ed,
+                                                   int32_t *__restrict__ pos, uint8_t *__restrict__ st,
+                                                   int32_t *__restrict__ sep, long long *__restrict__ counted) {
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < E; e += gridDim.x * 256) {
+        const int x = pairs[2 * e], y = pairs[2 * e + 1];
+        const int ax = adj_off[x], nx = adj_off[x + 1] - ax, ay = adj_off[y], ny = adj_off[y + 1] - ay;
+        int skx = find_sorted(adj + ax, nx, y), sky = find_sorted(adj + ay, ny, x);
+        const int m0 = skx >= 0 ? nx - 1 : nx, m1 = sky >= 0 ? ny - 1 : ny;
+        skx = skx >= 0 ? skx : nx + 1, sky = sky >= 0 ? sky : ny + 1;
+        ed[e] = L1Edge{x, y, m0, m0 + m1, skx, sky, ax, ay};
+        pos[e] = 0;
+        st[e] = m0 + m1 == 0 ? 2 : 0;  // no candidate on either side: kept
+        sep[e] = -1;
+        counted[e] = 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void ci_l1_len(const L1Edge *__restrict__ ed, const int32_t *__restrict__ pos,
+                                                 const uint8_t *__restrict__ st, int E, int chunk,
+                                                 int32_t *__restrict__ len) {
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < E; e += gridDim.x * 256) {
+        const int left = ed[e].L - pos[e];
+        len[e] = st[e] == 0 ? (left < chunk ? left : chunk) : 0;
+    }
+}
+
+// one workgroup: exclusive scan of len -> off, lengths clipped so the round holds at most cap tests
+// (the clipped edges continue next round), *total = the round's tests, *launched += *total
+__global__ __launch_bounds__(1024) void ci_l1_scan(int32_t *__restrict__ len, int E, long long cap,
+                                                   int32_t *__restrict__ off, long long *__restrict__ total,
+                                                   long long *__restrict__ launched) {
+    __shared__ long long part[1024];
+    const int tid = threadIdx.x, per = (E + 1023) / 1024;
+    const int b = tid * per < E ? tid * per : E, e_ = (tid + 1) * per < E ? (tid + 1) * per : E;
+    long long sum = 0;
+    for (int e = b; e < e_; ++e) sum += len[e];
+    part[tid] = sum;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan of the partial sums
+        const long long v = tid >= o ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    long long run = part[tid] - sum;
+    for (int e = b; e < e_; ++e) {
+        const long long l = len[e];
+        const long long keep = run >= cap ? 0 : (run + l > cap ? cap - run : l);
+        off[e] = (int32_t)(run < cap ? run : cap);
+        len[e] = (int32_t)keep;
+        run += l;
+    }
+    if (tid == 1023) {
+        const long long t = part[1023] < cap ? part[1023] : cap;
+        *total = t;
+        *launched += t;
+    }
+}
+
+// one thread per generated test: its edge by binary search over off (edges with len 0 share an
+// offset with the next one; the last edge whose off <= t owns t)
+__global__ __launch_bounds__(256) void ci_l1_gen(const L1Edge *__restrict__ ed, const int32_t *__restrict__ pos,
+                                                 const int32_t *__restrict__ off, int E,
+                                                 const long long *__restrict__ total,
+                                                 const int32_t *__restrict__ adj, int32_t *__restrict__ items,
+                                                 const int32_t *__restrict__ dims,
+                                                 unsigned long long *__restrict__ rows_read) {
+    const long long n = *total;
+    // wave-uniform trip count (the row tally below is reduced per wave)
+    for (long long wb = (long long)blockIdx.x * 256 + (threadIdx.x & ~63); wb < n; wb += (long long)gridDim.x * 256) {
+        const long long t = wb + (threadIdx.x & 63);
+        unsigned rows = 0;
+        if (t < n) {
+        int lo = 0, hi = E;  // last e with off[e] <= t
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (off[mid] <= t) lo = mid;
+            else hi = mid;
+        }
+        const L1Edge g = ed[lo];
+        const int k = pos[lo] + (int)(t - off[lo]);
+        int z;
+        if (k < g.m0) z = adj[g.ax + k + (k >= g.skx)];
+        else z = adj[g.ay + (k - g.m0) + ((k - g.m0) >= g.sky)];
+        items[3 * t] = g.x, items[3 * t + 1] = g.y, items[3 * t + 2] = z;
+        rows = dims[g.x] + dims[g.y] + dims[z] - 3;  // mask rows the derived count reads
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) rows += __shfl_xor(rows, o);
+        if ((threadIdx.x & 63) == 0 && rows) atomicAdd(rows_read, (unsigned long long)rows);
+    }
+}
+
+__global__ __launch_bounds__(256) void ci_l1_resolve(const L1Edge *__restrict__ ed, int32_t *__restrict__ pos,
+                                                     const int32_t *__restrict__ len,
+                                                     const int32_t *__restrict__ off, uint8_t *__restrict__ st,
+                                                     int32_t *__restrict__ sep, long long *__restrict__ counted,
+                                                     const uint8_t *__restrict__ indep,
+                                                     const int32_t *__restrict__ items, int E,
+                                                     unsigned *__restrict__ open_cnt) {
+    for (int e0 = blockIdx.x * 256 + (threadIdx.x & ~63); e0 < E; e0 += gridDim.x * 256) {
+        const int e = e0 + (threadIdx.x & 63);
+        bool open = false;
+        if (e < E && st[e] == 0) {
+            const int n = len[e], o = off[e];
+            int found = -1;
+            for (int i = 0; i < n; ++i)
+                if (indep[o + i]) {
+                    found = i;
+                    break;
+                }
+            if (found >= 0) {
+                st[e] = 1;
+                sep[e] = items[3 * (o + found) + 2];
+                counted[e] += found + 1;
+            } else {
+                counted[e] += n;
+                pos[e] += n;
+                if (pos[e] >= ed[e].L) st[e] = 2;
+                else open = true;
+            }
+        }
+        const unsigned nopen = (unsigned)__popcll(__ballot(open));  // one atomic per wave
+        if ((threadIdx.x & 63) == 0 && nopen) atomicAdd(open_cnt, nopen);
+    }
+}
+
 }  // namespace
 
 // bad[0] = 1 and bad[1] = v + 1 (some such v) if any code of variable v is >= dims[v]
@@ -1087,6 +1041,47 @@ extern "C" hipError_t fbn_ci_bits_pairs_tiled(const uint32_t *bits, const int32_
     return hipGetLastError();
 }
 
+extern "C" size_t fbn_ci_l1_edge_bytes(void) { return sizeof(L1Edge); }
+
+extern "C" hipError_t fbn_ci_l1_setup(const int32_t *pairs, int E, const int32_t *adj, const int32_t *adj_off,
+                                      void *ed, int32_t *pos, uint8_t *st, int32_t *sep, long long *counted,
+                                      hipStream_t s) {
+    if (E > 0)
+        hipLaunchKernelGGL(ci_l1_setup, dim3((E + 255) / 256), dim3(256), 0, s, pairs, E, adj, adj_off,
+                           (L1Edge *)ed, pos, st, sep, counted);
+    return hipGetLastError();
+}
+
+// one round: lengths, scan, generation, counting, G^2 / decisions, resolution; `total` = the
+// round's test count (device), `open_cnt` += edges still open after it
+extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims, const int32_t *row0, long long W,
+                                      const int32_t *adj, const int32_t *pairtab, int nvars, void *edv, int32_t *pos,
+                                      uint8_t *st, int32_t *sep, long long *counted, int32_t *len, int32_t *off,
+                                      int E, int chunk, long long cap, long long *total, long long *launched,
+                                      int32_t *items, int32_t *counts, int32_t *df, uint8_t *indep, double alpha,
+                                      unsigned long long *stats, const double *band, int nband, unsigned *open_cnt,
+                                      unsigned long long *rows_read, int num_cu, hipStream_t s) {
+    const L1Edge *ed = (const L1Edge *)edv;
+    const long long ge = ((long long)E + 255) / 256, gcap = (long long)num_cu * 8;
+    const dim3 gE((unsigned)(ge < gcap ? ge : gcap));
+    const long long gt = (cap + 255) / 256;
+    const dim3 gT((unsigned)(gt < gcap ? gt : gcap));
+    const long long gw = (cap + 3) / 4;
+    const dim3 gW((unsigned)(gw < gcap ? gw : gcap));
+    hipLaunchKernelGGL(ci_l1_len, gE, dim3(256), 0, s, ed, pos, st, E, chunk, len);
+    hipLaunchKernelGGL(ci_l1_scan, dim3(1), dim3(1024), 0, s, len, E, cap, off, total, launched);
+    hipLaunchKernelGGL(ci_l1_gen, gT, dim3(256), 0, s, ed, pos, off, E, (const long long *)total, adj, items, dims,
+                       rows_read);
+    hipLaunchKernelGGL(ci_bits_count_derived, gW, dim3(256), 0, s, bits, dims, row0, (const int32_t *)items, W, cap,
+                       counts, pairtab, nvars, 1, (const long long *)total);
+    hipLaunchKernelGGL(ci_bits_g2<1>, gT, dim3(256), 0, s, (const int32_t *)counts, dims, (const int32_t *)items, cap,
+                       alpha, (double *)nullptr, df, (double *)nullptr, indep, (int32_t *)nullptr, stats, nvars, 0ll,
+                       band, nband, (const long long *)total);
+    hipLaunchKernelGGL(ci_l1_resolve, gE, dim3(256), 0, s, ed, pos, (const int32_t *)len, (const int32_t *)off, st,
+                       sep, counted, (const uint8_t *)indep, (const int32_t *)items, E, open_cnt);
+    return hipGetLastError();
+}
+
 extern "C" int fbn_ci_gram_task_ints(void) { return kGramTaskInts; }
 
 extern "C" hipError_t fbn_ci_gram(const uint32_t *bits, long long W, const int32_t *rl, const int32_t *tasks,
@@ -1134,31 +1129,21 @@ extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *di
             hipLaunchKernelGGL(ci_bits_count<0>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts, rowcnt,
                                pmode == 1 ? pairtab : nullptr, nvars, t0);
         hipLaunchKernelGGL(ci_bits_g2<0>, b2, dim3(256), 0, s, counts, dims, items, n, alpha, g2, df, p, indep,
-                           counts0, stats, nvars, t0, band, nband);
+                           counts0, stats, nvars, t0, band, nband, (const long long *)nullptr);
     } else if (d == 1) {
-        // FBN_CI_L1MODE: 0 = item per wave, plain grid stride; 1 = item per wave, XCD-contiguous;
-        // 2 = quad of items per wave (x/y rows shared in registers), XCD-contiguous
+        // FBN_CI_L1MODE = 0: plain grid stride instead of the XCD-contiguous split
         static const int l1mode = getenv("FBN_CI_L1MODE") ? atoi(getenv("FBN_CI_L1MODE")) : 1;
         if (counted) {
             // the counts are already in place (ci_bits_gram_triples)
-        } else if (pmode == 2 && l1mode == 2) {
-            const long long gq = (n + 15) / 16;
-            hipLaunchKernelGGL(ci_bits_count_derived_grp, dim3((unsigned)(gq < cap ? gq : cap)), dim3(256), 0, s, bits,
-                               dims, row0, items, W, n, counts, (const int32_t *)pairtab, nvars, 1);
         } else if (pmode == 2) {
-            static const int l1waves = getenv("FBN_CI_L1WAVES") ? atoi(getenv("FBN_CI_L1WAVES")) : 0;
-            auto *k = l1waves == 4   ? ci_bits_count_derived_w4
-                      : l1waves == 5 ? ci_bits_count_derived_w5
-                      : l1waves == 6 ? ci_bits_count_derived_w6
-                                     : ci_bits_count_derived;
-            hipLaunchKernelGGL(k, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts, (const int32_t *)pairtab,
-                               nvars, l1mode == 1 ? 1 : 0);
+            hipLaunchKernelGGL(ci_bits_count_derived, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts,
+                               (const int32_t *)pairtab, nvars, l1mode == 1 ? 1 : 0, (const long long *)nullptr);
         }
         else
             hipLaunchKernelGGL(ci_bits_count<1>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts, rowcnt,
                                nullptr, nvars, 0ll);
         hipLaunchKernelGGL(ci_bits_g2<1>, b2, dim3(256), 0, s, counts, dims, items, n, alpha, g2, df, p, indep,
-                           counts0, stats, nvars, 0ll, band, nband);
+                           counts0, stats, nvars, 0ll, band, nband, (const long long *)nullptr);
     } else {
         return hipErrorInvalidValue;
     }

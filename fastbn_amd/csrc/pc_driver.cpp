@@ -156,6 +156,11 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
         return FBN_OK;
     }
     if (d > kMaxD) return SetError(FBN_ERR_LIMIT, "conditioning set size %d (supported 0..%d)", d, kMaxD);
+    if (d == 1 && group_size == 1) {  // the whole level on the device when eligible
+        bool done = false;
+        if (int rc = CiLevel1Device(ctx, alpha, adj, edges, e_begin, e_end, out, res, &done)) return rc;
+        if (done) return FBN_OK;
+    }
     // level 1 on the bit-sliced store, FBN_CI_GRAM1 = 1: per-variable Grams make every candidate
     // set's table a gather (a test then costs about its G^2 pass; FBN_PC_FULLSPEC1 = speculation
     // cap).  Off by default: config 5's Grams cover all 3.46M candidate sets (45.9 G popcount words,
