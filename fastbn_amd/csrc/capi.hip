@@ -1,5 +1,6 @@
 // capi.hip -- the extern "C" boundary (include/fastbn.h): handles, device memory, uploads, launches.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 #include <chrono>
 
 #include <algorithm>
@@ -49,7 +50,9 @@ extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims,
                                       int E, int chunk, long long cap, long long *total, long long *launched,
                                       int32_t *items, int32_t *counts, int32_t *df, uint8_t *indep, double alpha,
                                       unsigned long long *stats, const double *band, int nband, unsigned *open_cnt,
-                                      unsigned long long *rows_read, int num_cu, hipStream_t s);
+                                      unsigned long long *rows_read, void *scan_tmp, size_t scan_tmp_bytes,
+                                      int num_cu, hipStream_t s);
+extern "C" size_t fbn_ci_l1_scan_bytes(int E);
 extern "C" hipError_t fbn_ci_gram(const uint32_t *bits, long long W, const int32_t *rl, const int32_t *tasks,
                                   long long ntasks, int masked, int32_t *out, int num_cu, hipStream_t s);
 extern "C" hipError_t fbn_ci_gram_pairs(const int32_t *G, long long ld, const int32_t *lead0, const int32_t *dims,
@@ -219,7 +222,9 @@ struct fbn_ci_ctx {
     // device-resident level-1 search (CiLevel1Device): edge state, round buffers, per-round open
     // counts (pinned mirror), round events
     DevBuf l1pairs, l1adj, l1adjoff, l1ed, l1pos, l1st, l1sep, l1cnt, l1len, l1off, l1scal, l1open;
-    DevBuf l1items, l1counts, l1df, l1indep;
+    DevBuf l1items, l1counts, l1df, l1indep, l1tmp;
+    DevBuf keptidx, kepttmp;  // level-0 kept pair indices (CiAllPairsKept)
+    int *h_kept = nullptr;
     unsigned *h_open = nullptr;
     hipEvent_t l1ev[2] = {nullptr, nullptr};
     // decision band of the bit-sliced G^2 kernel for alpha = band_alpha (ci_chisq.h fbn_chisq_band):
@@ -235,6 +240,7 @@ struct fbn_ci_ctx {
     bool timing = true;  // HIP events around every CI kernel (fbn_ci_set_kernel_timing)
     ~fbn_ci_ctx() {
         if (h_open) (void)hipHostFree(h_open);
+        if (h_kept) (void)hipHostFree(h_kept);
         for (auto &e : l1ev)
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
@@ -1629,6 +1635,11 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
     for (int v = 0; v < nv; ++v)
         if (c->dims[v] > 4) return FBN_OK;
     const int E = (int)(e_end - e_begin);
+    int64_t cands = 0;  // every candidate set of the range: the most one round could hold
+    for (size_t e = e_begin; e < e_end; ++e) cands += adj[edges[e].first].size() + adj[edges[e].second].size() - 2;
+    // a level the host driver takes in one round (full speculation, ALARM-size) stays there: one
+    // launch instead of a round's seven
+    if (cands <= EnvOr0("FBN_PC_FULLSPEC", 16384)) return FBN_OK;
     out.removed.assign(E, 0);
     out.d = 1;
     out.sep.assign(E, -1);
@@ -1644,8 +1655,6 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
         adjf.insert(adjf.end(), adj[u].begin(), adj[u].end());
     }
     adj_off[nv] = (int32_t)adjf.size();
-    int64_t cands = 0;  // every candidate set of the range: the most one round could hold
-    for (size_t e = e_begin; e < e_end; ++e) cands += adj[edges[e].first].size() + adj[edges[e].second].size() - 2;
     const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(cands, EnvOr0("FBN_PC_L1CAP", 1 << 19)));
     if ((rc = c->l1pairs.ensure((size_t)E * 8)) || (rc = c->l1adj.ensure(std::max<size_t>(adjf.size(), 1) * 4)) ||
         (rc = c->l1adjoff.ensure((size_t)(nv + 1) * 4)) || (rc = c->l1ed.ensure((size_t)E * fbn_ci_l1_edge_bytes())) ||
@@ -1656,6 +1665,8 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
         (rc = c->l1items.ensure((size_t)cap * 12)) || (rc = c->l1counts.ensure((size_t)cap * 256)) ||
         (rc = c->l1df.ensure((size_t)cap * 4)) || (rc = c->l1indep.ensure((size_t)cap)))
         return rc;
+    const size_t scan_bytes = std::max<size_t>(fbn_ci_l1_scan_bytes(E), 16);
+    if ((rc = c->l1tmp.ensure(scan_bytes))) return rc;
     if (!c->h_open) {
         hipError_t e = hipHostMalloc((void **)&c->h_open, kL1MaxRounds * 4, hipHostMallocDefault);
         if (e != hipSuccess) return SetError(FBN_ERR_NOMEM, "hipHostMalloc: %s", hipGetErrorString(e));
@@ -1686,8 +1697,8 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
                             c->l1len.as<int32_t>(), c->l1off.as<int32_t>(), E, (int)chunk, cap, scal, scal + 1,
                             c->l1items.as<int32_t>(), c->l1counts.as<int32_t>(), c->l1df.as<int32_t>(),
                             c->l1indep.as<uint8_t>(), alpha, c->stats.as<unsigned long long>(), band, kBandDf,
-                            c->l1open.as<unsigned>() + r, reinterpret_cast<unsigned long long *>(scal + 2), c->num_cu,
-                            s);
+                            c->l1open.as<unsigned>() + r, reinterpret_cast<unsigned long long *>(scal + 2),
+                            c->l1tmp.p, scan_bytes, c->num_cu, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci level-1 round: %s", hipGetErrorString(e));
         FBN_HIP(hipMemcpyAsync(c->h_open + r, c->l1open.as<unsigned>() + r, 4, hipMemcpyDeviceToHost, s));
         FBN_HIP(hipEventRecord(c->l1ev[r & 1], s));
@@ -1795,6 +1806,45 @@ int CiTriplePrepare(fbn_ci_ctx *c, const std::vector<std::vector<int>> &adj,
     if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci gram level 1: %s", hipGetErrorString(e));
     FBN_HIP(hipStreamSynchronize(s));  // the host vectors go out of scope
     *ready = c->triples_ready = true;
+    return FBN_OK;
+}
+struct FlagIsZero {
+    __host__ __device__ bool operator()(uint8_t f) const { return f == 0; }
+};
+// the pairs (i < j) of the complete graph level 0 kept (decision 0), in pair order: compacted on the
+// device from the last all-pairs batch (slot 0), only the kept indices cross PCIe
+int CiAllPairsKept(fbn_ci_ctx *c, int64_t P, std::vector<std::pair<int, int>> &kept) {
+    kept.clear();
+    if (P <= 0) return FBN_OK;
+    if (P > INT32_MAX) return SetError(FBN_ERR_LIMIT, "too many pairs for the kept-pair compaction");
+    FBN_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    CiSlot &S = c->slot[0];
+    hipcub::CountingInputIterator<int32_t> in(0);
+    hipcub::TransformInputIterator<bool, FlagIsZero, const uint8_t *> flags(S.indep.as<uint8_t>(), FlagIsZero());
+    size_t tmp = 0;
+    FBN_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmp, in, flags, (int32_t *)nullptr, (int *)nullptr, (int)P, s));
+    int rc;
+    if ((rc = c->kepttmp.ensure(std::max<size_t>(tmp, 16) + 16)) || (rc = c->keptidx.ensure((size_t)P * 4))) return rc;
+    if (!c->h_kept) {
+        hipError_t e = hipHostMalloc((void **)&c->h_kept, 16, hipHostMallocDefault);
+        if (e != hipSuccess) return SetError(FBN_ERR_NOMEM, "hipHostMalloc: %s", hipGetErrorString(e));
+    }
+    int *d_num = reinterpret_cast<int *>(c->kepttmp.as<char>() + std::max<size_t>(tmp, 16));
+    FBN_HIP(hipcub::DeviceSelect::Flagged(c->kepttmp.p, tmp, in, flags, c->keptidx.as<int32_t>(), d_num, (int)P, s));
+    FBN_HIP(hipMemcpyAsync(c->h_kept, d_num, 4, hipMemcpyDeviceToHost, s));
+    FBN_HIP(hipStreamSynchronize(s));
+    const int nk = c->h_kept[0];
+    std::vector<int32_t> idx((size_t)nk);
+    if (nk) FBN_HIP(hipMemcpy(idx.data(), c->keptidx.p, (size_t)nk * 4, hipMemcpyDeviceToHost));
+    kept.resize((size_t)nk);
+    const int n = c->nvars;
+    int i = 0;
+    int64_t row0 = 0, row1 = n - 1;  // pair indices of row i: [row0, row1)
+    for (int t = 0; t < nk; ++t) {
+        while (idx[t] >= row1) ++i, row0 = row1, row1 += n - 1 - i;
+        kept[t] = {i, i + 1 + (int)(idx[t] - row0)};
+    }
     return FBN_OK;
 }
 int CiBatchWait(fbn_ci_ctx *c, int k, uint8_t *indep, int32_t *df, PCResultHost &res) {

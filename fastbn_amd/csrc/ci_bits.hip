@@ -21,6 +21,8 @@
 
 #include "ci_chisq.h"
 
+#include <hipcub/hipcub.hpp>
+
 namespace {
 
 // bits[(row0[v] + a) * W + w]: samples 32w .. 32w+31 of variable v equal to a
@@ -871,36 +873,22 @@ __global__ __launch_bounds__(256) void ci_l1_len(const L1Edge *__restrict__ ed, 
     }
 }
 
-// one workgroup: exclusive scan of len -> off, lengths clipped so the round holds at most cap tests
-// (the clipped edges continue next round), *total = the round's tests, *launched += *total
-__global__ __launch_bounds__(1024) void ci_l1_scan(int32_t *__restrict__ len, int E, long long cap,
-                                                   int32_t *__restrict__ off, long long *__restrict__ total,
-                                                   long long *__restrict__ launched) {
-    __shared__ long long part[1024];
-    const int tid = threadIdx.x, per = (E + 1023) / 1024;
-    const int b = tid * per < E ? tid * per : E, e_ = (tid + 1) * per < E ? (tid + 1) * per : E;
-    long long sum = 0;
-    for (int e = b; e < e_; ++e) sum += len[e];
-    part[tid] = sum;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan of the partial sums
-        const long long v = tid >= o ? part[tid - o] : 0;
-        __syncthreads();
-        part[tid] += v;
-        __syncthreads();
-    }
-    long long run = part[tid] - sum;
-    for (int e = b; e < e_; ++e) {
-        const long long l = len[e];
-        const long long keep = run >= cap ? 0 : (run + l > cap ? cap - run : l);
-        off[e] = (int32_t)(run < cap ? run : cap);
-        len[e] = (int32_t)keep;
-        run += l;
-    }
-    if (tid == 1023) {
-        const long long t = part[1023] < cap ? part[1023] : cap;
-        *total = t;
-        *launched += t;
+// after the exclusive scan of len (off, hipcub): lengths clipped so the round holds at most cap
+// tests (the clipped edges continue next round); *total = the round's tests, *launched += *total
+__global__ __launch_bounds__(256) void ci_l1_clip(int32_t *__restrict__ len, int32_t *__restrict__ off, int E,
+                                                  long long cap, long long *__restrict__ total,
+                                                  long long *__restrict__ launched) {
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < E; e += gridDim.x * 256) {
+        const long long run = off[e], l = len[e];
+        if (e == E - 1) {
+            const long long t = run + l < cap ? run + l : cap;
+            *total = t;
+            *launched += t;
+        }
+        if (run + l > cap) {
+            len[e] = (int32_t)(run >= cap ? 0 : cap - run);
+            off[e] = (int32_t)(run < cap ? run : cap);
+        }
     }
 }
 
@@ -1043,6 +1031,13 @@ extern "C" hipError_t fbn_ci_bits_pairs_tiled(const uint32_t *bits, const int32_
 
 extern "C" size_t fbn_ci_l1_edge_bytes(void) { return sizeof(L1Edge); }
 
+// temporary storage of the round's length scan for E edges
+extern "C" size_t fbn_ci_l1_scan_bytes(int E) {
+    size_t b = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const int32_t *)nullptr, (int32_t *)nullptr, E);
+    return b;
+}
+
 extern "C" hipError_t fbn_ci_l1_setup(const int32_t *pairs, int E, const int32_t *adj, const int32_t *adj_off,
                                       void *ed, int32_t *pos, uint8_t *st, int32_t *sep, long long *counted,
                                       hipStream_t s) {
@@ -1060,7 +1055,8 @@ extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims,
                                       int E, int chunk, long long cap, long long *total, long long *launched,
                                       int32_t *items, int32_t *counts, int32_t *df, uint8_t *indep, double alpha,
                                       unsigned long long *stats, const double *band, int nband, unsigned *open_cnt,
-                                      unsigned long long *rows_read, int num_cu, hipStream_t s) {
+                                      unsigned long long *rows_read, void *scan_tmp, size_t scan_tmp_bytes,
+                                      int num_cu, hipStream_t s) {
     const L1Edge *ed = (const L1Edge *)edv;
     const long long ge = ((long long)E + 255) / 256, gcap = (long long)num_cu * 8;
     const dim3 gE((unsigned)(ge < gcap ? ge : gcap));
@@ -1069,7 +1065,10 @@ extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims,
     const long long gw = (cap + 3) / 4;
     const dim3 gW((unsigned)(gw < gcap ? gw : gcap));
     hipLaunchKernelGGL(ci_l1_len, gE, dim3(256), 0, s, ed, pos, st, E, chunk, len);
-    hipLaunchKernelGGL(ci_l1_scan, dim3(1), dim3(1024), 0, s, len, E, cap, off, total, launched);
+    size_t tmp_bytes = scan_tmp_bytes;
+    hipError_t e = hipcub::DeviceScan::ExclusiveSum(scan_tmp, tmp_bytes, len, off, E, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(ci_l1_clip, gE, dim3(256), 0, s, len, off, E, cap, total, launched);
     hipLaunchKernelGGL(ci_l1_gen, gT, dim3(256), 0, s, ed, pos, off, E, (const long long *)total, adj, items, dims,
                        rows_read);
     hipLaunchKernelGGL(ci_bits_count_derived, gW, dim3(256), 0, s, bits, dims, row0, (const int32_t *)items, W, cap,

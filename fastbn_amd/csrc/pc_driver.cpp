@@ -401,16 +401,9 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
     int64_t nsamples = 0;
     CiCtxShape(ctx, &nvars, &nsamples);
     const int n = nvars;
+    const int64_t P = (int64_t)n * (n - 1) / 2;
     std::vector<std::pair<int, int>> edges;
-    edges.reserve((size_t)n * (n - 1) / 2);
-    for (int i = 0; i < n; ++i)
-        for (int j = i + 1; j < n; ++j) edges.push_back({i, j});
     std::vector<std::vector<int>> adj(n);
-    for (int i = 0; i < n; ++i) {
-        adj[i].reserve(n - 1);
-        for (int j = 0; j < n; ++j)
-            if (i != j) adj[i].push_back(j);
-    }
     const bool timing = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic: host phase times per level
     // level 0 tests every pair: its tables are recorded for the level-1 kernel (derived counting)
     // and dropped when this run ends, however it ends
@@ -420,7 +413,50 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
     } pair_guard{ctx};
     const bool pairs = !getenv("FBN_CI_NO_PAIRS");
     CiSetPairMode(ctx, pairs ? 1 : 0);
-    for (int d = 0; d == 0 || d < depth; ++d) {
+    // level 0 over the implicit complete graph (the kernels decode pair indices): no edge list or
+    // adjacency of the complete graph is built; the kept pairs become the skeleton directly
+    const int32_t *dims = CiCtxDims(ctx);
+    CiBatchStats st_all{0, 0};
+    for (int v = 0; v < n; ++v) st_all.dim_rows += (int64_t)(n - 1) * dims[v], st_all.maxdim = std::max(st_all.maxdim, (int)dims[v]);
+    int d0 = 0;
+    if (n >= 2 && CiAllPairsEligible(ctx, st_all) && !getenv("FBN_CI_NO_IMPLICIT")) {
+        auto ta = std::chrono::steady_clock::now();
+        const double k0 = res.kernel_s;
+        std::vector<char> removed((size_t)P);
+        static_assert(sizeof(char) == sizeof(uint8_t), "flag layout");
+        int rc = CiBatchLaunchAllPairs(ctx, alpha, &st_all, 0, P);
+        if (!rc) rc = CiBatchWait(ctx, 0, reinterpret_cast<uint8_t *>(removed.data()), nullptr, res);
+        if (rc) return rc;
+        auto tb = std::chrono::steady_clock::now();
+        res.sepset.set_level0(n, removed.data());
+        res.tests_per_level.push_back(P);
+        res.launched_per_level.push_back(P);
+        if (P > (1 << 16)) {
+            if ((rc = CiAllPairsKept(ctx, P, edges))) return rc;  // kept pairs, compacted on the device
+        } else {  // small graphs: a host pass over the flags costs less than the extra round trip
+            int64_t k = 0;
+            for (int i = 0; i < n; ++i)
+                for (int j = i + 1; j < n; ++j, ++k)
+                    if (!removed[k]) edges.push_back({i, j});
+        }
+        for (auto &e : edges) adj[e.first].push_back(e.second), adj[e.second].push_back(e.first);
+        if (pairs) CiSetPairMode(ctx, 2);
+        if (timing)
+            fprintf(stderr, "pc level 0 (implicit): run %.2f ms (kernels %.2f), skeleton %.2f ms\n",
+                    std::chrono::duration<double, std::milli>(tb - ta).count(), (res.kernel_s - k0) * 1e3,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb).count());
+        d0 = 1;
+    } else {
+        edges.reserve((size_t)P);
+        for (int i = 0; i < n; ++i)
+            for (int j = i + 1; j < n; ++j) edges.push_back({i, j});
+        for (int i = 0; i < n; ++i) {
+            adj[i].reserve(n - 1);
+            for (int j = 0; j < n; ++j)
+                if (i != j) adj[i].push_back(j);
+        }
+    }
+    for (int d = d0; d < std::max(depth, 1); ++d) {
         LevelOut out;
         auto ta = std::chrono::steady_clock::now();
         const double k0 = res.kernel_s;

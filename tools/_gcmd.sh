@@ -3,17 +3,14 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_pc.py tests/test_gpu_pc_dist.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t_pc.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/t_pc.log; exit 1; }
 tail -1 gpurun_out/t_pc.log
-echo "default"; timeout -k 10 120 python tools/pc5_timing.py 4 2>&1 | grep -E "run " | tail -1
+echo "default"; timeout -k 10 120 python tools/pc5_timing.py 5 2>&1 | grep -E "run " | tail -1
 echo "host l1"; FBN_PC_HOST_L1=1 timeout -k 10 120 python tools/pc5_timing.py 4 2>&1 | grep -E "run " | tail -1
-for r in 32768 131072; do echo "round0 $r"; FBN_PC_ROUND0=$r timeout -k 10 120 python tools/pc5_timing.py 4 2>&1 | grep -E "run " | tail -1; done
-echo "growth 8"; FBN_PC_GROWTH=8 timeout -k 10 120 python tools/pc5_timing.py 4 2>&1 | grep -E "run " | tail -1
-FBN_PC_TIMING=1 timeout -k 10 120 python tools/pc5_timing.py 2 2>&1 | grep -E "^pc" | tail -7
+FBN_PC_TIMING=1 timeout -k 10 120 python tools/pc5_timing.py 2 2>&1 | grep -E "^pc|^orient" | tail -8
 timeout -k 10 120 python tools/pc_alarm_timing.py 2>&1 | tail -1
-timeout -k 10 200 python tools/pc5_dump_skeleton.py 2>&1 | tail -1
 mkdir -p gpurun_out/bprof
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/bprof -o run --output-format csv -- python tools/pc5_timing.py 3 > /dev/null 2>&1 || exit 1
 python3 -c "
 import csv
-for r in list(csv.DictReader(open('gpurun_out/bprof/run_kernel_stats.csv')))[:14]:
+for r in list(csv.DictReader(open('gpurun_out/bprof/run_kernel_stats.csv')))[:16]:
     print(r['Name'][:60], r['Calls'], round(float(r['AverageNs'])/1e3,1), 'us', round(float(r['TotalDurationNs'])/1e6/3,3), 'ms/run')
 "
