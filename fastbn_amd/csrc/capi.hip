@@ -1094,10 +1094,15 @@ static int CiGram0Tasks(fbn_ci_ctx *c, int64_t t0, int64_t t1, hipStream_t s) {
     auto idx = [&](int64_t u, int64_t v) { return u * nv - u * (u + 1) / 2 + (v - u - 1); };
     const int TI = fbn_ci_gram_task_ints();
     std::vector<int32_t> tasks;
-    for (int64_t bi = 0; bi < nb; ++bi) {
+    // tiles in 16 x 16-tile super-blocks (128 + 128 rows = 3.2 MB at 100k samples: one XCD's L2),
+    // consecutive in the task list, which the kernel splits XCD-contiguously
+    constexpr int64_t SB = 16;
+    for (int64_t si = 0; si < nb; si += SB)
+    for (int64_t sj = si; sj < nb; sj += SB)
+    for (int64_t bi = si; bi < std::min(nb, si + SB); ++bi) {
         const int64_t r0 = 8 * bi, r1 = std::min(R, r0 + 8);
         const int vi0 = var_of[r0], vi1 = var_of[r1 - 1];
-        for (int64_t bj = bi; bj < nb; ++bj) {
+        for (int64_t bj = std::max(bi, sj); bj < std::min(nb, sj + SB); ++bj) {
             const int64_t c0 = 8 * bj, c1 = std::min(R, c0 + 8);
             const int vj0 = var_of[c0], vj1 = var_of[c1 - 1];
             if (vi0 >= vj1) continue;  // no x < y in the tile

@@ -525,10 +525,12 @@ constexpr int kGramTaskInts = 8;  // mask row (-1: none), i0, ni, j0, nj, out of
 template <bool MASKED>
 __global__ __launch_bounds__(64) void ci_bits_gram(const uint32_t *__restrict__ bits, long long W,
                                                    const int32_t *__restrict__ rl, const int32_t *__restrict__ tasks,
-                                                   long long ntasks, int32_t *__restrict__ out) {
+                                                   long long ntasks, int32_t *__restrict__ out, int xcd) {
     typedef __attribute__((ext_vector_type(4))) unsigned u4;
     const int lane = threadIdx.x;
-    for (long long k = blockIdx.x; k < ntasks; k += gridDim.x) {
+    // consecutive tiles (the same i-block of rows) on one XCD: the rows stay in that XCD's L2
+    const XcdSplit sp = xcd_split(ntasks, 0, 1, xcd);
+    for (long long k = sp.first; k < sp.end; k += sp.stride) {
         const int32_t *t = tasks + k * kGramTaskInts;
         const int mrow = t[0], i0 = t[1], ni = t[2], j0 = t[3], nj = t[4], ld = t[7];
         const long long off = (long long)(uint32_t)t[5] | ((long long)t[6] << 32);
@@ -1088,8 +1090,9 @@ extern "C" hipError_t fbn_ci_gram(const uint32_t *bits, long long W, const int32
     const long long cap = (long long)num_cu * 32;
     const dim3 g((unsigned)(ntasks < cap ? ntasks : cap));
     if (ntasks <= 0) return hipSuccess;
-    if (masked) hipLaunchKernelGGL(ci_bits_gram<true>, g, dim3(64), 0, s, bits, W, rl, tasks, ntasks, out);
-    else hipLaunchKernelGGL(ci_bits_gram<false>, g, dim3(64), 0, s, bits, W, rl, tasks, ntasks, out);
+    static const int xcd = getenv("FBN_CI_GRAM_XCD") ? atoi(getenv("FBN_CI_GRAM_XCD")) : 1;
+    if (masked) hipLaunchKernelGGL(ci_bits_gram<true>, g, dim3(64), 0, s, bits, W, rl, tasks, ntasks, out, xcd);
+    else hipLaunchKernelGGL(ci_bits_gram<false>, g, dim3(64), 0, s, bits, W, rl, tasks, ntasks, out, xcd);
     return hipGetLastError();
 }
 
