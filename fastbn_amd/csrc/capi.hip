@@ -1,6 +1,8 @@
 // capi.hip -- the extern "C" boundary (include/fastbn.h): handles, device memory, uploads, launches.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rocblas/rocblas.h>
+#include <dlfcn.h>
 #include <chrono>
 
 #include <algorithm>
@@ -40,6 +42,8 @@ extern "C" hipError_t fbn_ci_bits_rowcount(const uint32_t *bits, long long rows,
                                            hipStream_t s);
 extern "C" int fbn_ci_pair_block(int d);
 extern "C" int fbn_ci_gram_task_ints(void);
+extern "C" hipError_t fbn_ci_onehot_build(const uint8_t *cols, const int32_t *dims, const int32_t *lead0, long long N,
+                                          long long Npad, int nvars, int8_t *out, hipStream_t s);
 extern "C" size_t fbn_ci_l1_edge_bytes(void);
 extern "C" hipError_t fbn_ci_l1_setup(const int32_t *pairs, int E, const int32_t *adj, const int32_t *adj_off,
                                       void *ed, int32_t *pos, uint8_t *st, int32_t *sep, long long *counted,
@@ -224,6 +228,11 @@ struct fbn_ci_ctx {
     DevBuf l1pairs, l1adj, l1adjoff, l1ed, l1pos, l1st, l1sep, l1cnt, l1len, l1off, l1scal, l1open;
     DevBuf l1items, l1counts, l1df, l1indep, l1tmp;
     DevBuf keptidx, kepttmp;  // level-0 kept pair indices (CiAllPairsKept)
+    // level-0 Gram as an int8 library GEMM: one byte per (leading row, sample), rocBLAS handle
+    DevBuf onehot;
+    int64_t onehot_Npad = 0;
+    bool onehot_ready = false, blas_failed = false;
+    void *blas = nullptr;
     int *h_kept = nullptr;
     unsigned *h_open = nullptr;
     hipEvent_t l1ev[2] = {nullptr, nullptr};
@@ -238,7 +247,8 @@ struct fbn_ci_ctx {
     hipStream_t stream = nullptr;  // the PC driver's rounds (pinned staging, one sync per round)
     float last_ms = 0.f;
     bool timing = true;  // HIP events around every CI kernel (fbn_ci_set_kernel_timing)
-    ~fbn_ci_ctx() {
+    ~fbn_ci_ctx();
+    void destroy_() {
         if (h_open) (void)hipHostFree(h_open);
         if (h_kept) (void)hipHostFree(h_kept);
         for (auto &e : l1ev)
@@ -272,6 +282,39 @@ static int CiBand(fbn_ci_ctx *c, double alpha, hipStream_t s, const double **out
     }
     *out = c->band.as<double>();
     return FBN_OK;
+}
+
+// rocBLAS, resolved at first use (dlopen): the level-0 Gram is a plain int8 GEMM (O O^T of the
+// one-hot leading rows); without the library the popcount Gram kernel computes it
+struct BlasLib {
+    bool ok = false;
+    rocblas_status (*create)(rocblas_handle *) = nullptr;
+    rocblas_status (*destroy)(rocblas_handle) = nullptr;
+    rocblas_status (*set_stream)(rocblas_handle, hipStream_t) = nullptr;
+    rocblas_status (*gemm_ex)(rocblas_handle, rocblas_operation, rocblas_operation, rocblas_int, rocblas_int,
+                              rocblas_int, const void *, const void *, rocblas_datatype, rocblas_int, const void *,
+                              rocblas_datatype, rocblas_int, const void *, const void *, rocblas_datatype, rocblas_int,
+                              void *, rocblas_datatype, rocblas_int, rocblas_datatype, rocblas_gemm_algo, int32_t,
+                              uint32_t) = nullptr;
+};
+static BlasLib &Blas() {
+    static BlasLib b = [] {
+        BlasLib r;
+        void *h = dlopen("librocblas.so.5", RTLD_NOW);
+        if (!h) h = dlopen("/opt/rocm/lib/librocblas.so.5", RTLD_NOW);
+        if (!h) return r;
+        r.create = (decltype(r.create))dlsym(h, "rocblas_create_handle");
+        r.destroy = (decltype(r.destroy))dlsym(h, "rocblas_destroy_handle");
+        r.set_stream = (decltype(r.set_stream))dlsym(h, "rocblas_set_stream");
+        r.gemm_ex = (decltype(r.gemm_ex))dlsym(h, "rocblas_gemm_ex");
+        r.ok = r.create && r.destroy && r.set_stream && r.gemm_ex;
+        return r;
+    }();
+    return b;
+}
+fbn_ci_ctx::~fbn_ci_ctx() {
+    if (blas) (void)Blas().destroy((rocblas_handle)blas);
+    destroy_();
 }
 
 static int PinnedEnsure(void *&ptr, size_t &have, size_t want) {
@@ -1122,6 +1165,72 @@ static int CiGram0Tasks(fbn_ci_ctx *c, int64_t t0, int64_t t1, hipStream_t s) {
     return FBN_OK;
 }
 
+// The level-0 Gram as an int8 GEMM on the matrix cores (rocBLAS gemm_ex, int32 accumulation: the
+// counts are exact): O = one byte per (leading row, sample), built once per ctx; for the pairs
+// [t0, t0 + n) only the columns of their x-variables' leading rows are computed (C[:, r0:r1] = O^T
+// O[:, r0:r1], column-major, ld = R).  *done = false: not used (no library, over the byte budget,
+// FBN_CI_GRAM_NO_BLAS, or a failed call) -- the popcount Gram kernel runs instead.
+constexpr int64_t kOnehotMaxBytes = (int64_t)4 << 30;
+static int CiGram0Blas(fbn_ci_ctx *c, int64_t t0, int64_t n, hipStream_t s, bool *done) {
+    *done = false;
+    const int64_t R = (int64_t)c->leadrows_host.size(), Npad = (c->N + 63) & ~(int64_t)63;
+    // small Grams (ALARM: 60 rows x 5k samples) stay on the popcount kernel: a library call and the
+    // one-hot store cost more than they save there
+    if (c->blas_failed || getenv("FBN_CI_GRAM_NO_BLAS") || R * Npad > kOnehotMaxBytes || Npad > INT32_MAX ||
+        (double)R * R * Npad < 1e10 || !Blas().ok)
+        return FBN_OK;
+    int rc;
+    if (!c->onehot_ready) {
+        if ((rc = c->onehot.ensure((size_t)(R * Npad)))) return rc;
+        hipError_t e = fbn_ci_onehot_build(c->cols.as<uint8_t>(), c->ddims.as<int32_t>(), c->lead0.as<int32_t>(), c->N,
+                                           Npad, c->nvars, c->onehot.as<int8_t>(), s);
+        if (e != hipSuccess) return SetError(FBN_ERR_HIP, "one-hot build: %s", hipGetErrorString(e));
+        c->onehot_Npad = Npad;
+        c->onehot_ready = true;
+    }
+    if (!c->blas) {
+        rocblas_handle h = nullptr;
+        if (Blas().create(&h) != rocblas_status_success) {
+            c->blas_failed = true;
+            return FBN_OK;
+        }
+        c->blas = h;
+    }
+    rocblas_handle h = (rocblas_handle)c->blas;
+    if (Blas().set_stream(h, s) != rocblas_status_success) return FBN_OK;
+    // x-variables of the range: pair rows u0 .. u1
+    const int nv = c->nvars;
+    auto row_of = [&](int64_t t) {
+        int64_t lo = 0, hi = nv - 2;
+        while (lo < hi) {
+            const int64_t m = (lo + hi + 1) / 2;
+            if (m * nv - m * (m + 1) / 2 <= t) lo = m;
+            else hi = m - 1;
+        }
+        return (int)lo;
+    };
+    const int u0 = row_of(t0), u1 = row_of(t0 + n - 1);
+    const int64_t r0 = c->lead0_host[u0], r1 = u1 + 1 < nv ? c->lead0_host[u1 + 1] : R;
+    if (r1 <= r0) {
+        *done = true;
+        return FBN_OK;
+    }
+    const int32_t one = 1, zero = 0;
+    const int8_t *O = c->onehot.as<int8_t>();
+    rocblas_status st = Blas().gemm_ex(h, rocblas_operation_transpose, rocblas_operation_none, (rocblas_int)R,
+                                       (rocblas_int)(r1 - r0), (rocblas_int)Npad, &one, O, rocblas_datatype_i8_r,
+                                       (rocblas_int)Npad, O + r0 * Npad, rocblas_datatype_i8_r, (rocblas_int)Npad,
+                                       &zero, c->gram0.as<int32_t>() + r0 * R, rocblas_datatype_i32_r, (rocblas_int)R,
+                                       c->gram0.as<int32_t>() + r0 * R, rocblas_datatype_i32_r, (rocblas_int)R,
+                                       rocblas_datatype_i32_r, rocblas_gemm_algo_standard, 0, 0);
+    if (st != rocblas_status_success) {
+        c->blas_failed = true;
+        return FBN_OK;
+    }
+    *done = true;
+    return FBN_OK;
+}
+
 // items: host copy (validated here).  zc_items / zc_indep / zc_df: optional device-visible
 // (pinned, mapped) host buffers the kernels read the items from and write the decisions to
 // directly -- no staging copies for the small batches of a latency-bound driver round.
@@ -1209,11 +1318,16 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         if (tiled && (rc = CiPairTasks(c, pair0, pair0 + n, s))) return rc;
         hipError_t e = hipSuccess;
         if (gram0) {  // Gram of the leading rows, then every pair's table from it
-            if ((rc = CiLeadEnsure(c, s)) || (rc = CiGram0Tasks(c, pair0, pair0 + n, s))) return rc;
+            if ((rc = CiLeadEnsure(c, s))) return rc;
             const int64_t R = (int64_t)c->leadrows_host.size();
             if ((rc = c->gram0.ensure((size_t)(R * R * 4)))) return rc;
-            e = fbn_ci_gram(c->bits.as<uint32_t>(), c->bits_W, c->leadrows.as<int32_t>(), c->g0tasks.as<int32_t>(),
-                            c->g0_ntasks, 0, c->gram0.as<int32_t>(), c->num_cu, s);
+            bool done = false;
+            if ((rc = CiGram0Blas(c, pair0, n, s, &done))) return rc;
+            if (!done) {
+                if ((rc = CiGram0Tasks(c, pair0, pair0 + n, s))) return rc;
+                e = fbn_ci_gram(c->bits.as<uint32_t>(), c->bits_W, c->leadrows.as<int32_t>(),
+                                c->g0tasks.as<int32_t>(), c->g0_ntasks, 0, c->gram0.as<int32_t>(), c->num_cu, s);
+            }
             if (e == hipSuccess)
                 e = fbn_ci_gram_pairs(c->gram0.as<int32_t>(), R, c->lead0.as<int32_t>(), c->ddims.as<int32_t>(),
                                       c->brow.as<int32_t>(), c->browcnt.as<int32_t>(), pair0, n, c->nvars,

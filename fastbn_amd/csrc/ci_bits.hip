@@ -1083,6 +1083,40 @@ extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims,
     return hipGetLastError();
 }
 
+// one byte per (leading row, sample): out[r][s] = [cols[v][s] == a] for leading row r = lead0[v] + a
+// (a < dims[v] - 1), samples N..Npad-1 zero -- the int8 operand of the level-0 Gram as a library
+// GEMM (capi.hip); 4 samples per thread
+__global__ __launch_bounds__(256) void ci_onehot_build(const uint8_t *__restrict__ cols, const int32_t *__restrict__ dims,
+                                                       const int32_t *__restrict__ lead0, long long N, long long Npad,
+                                                       int nvars, int8_t *__restrict__ out) {
+    const long long n4 = Npad / 4;
+    for (int v = blockIdx.y; v < nvars; v += gridDim.y) {
+        const int m = dims[v] - 1;
+        if (m <= 0) continue;
+        const uint8_t *c = cols + (size_t)v * N;
+        int8_t *o = out + (size_t)lead0[v] * Npad;
+        for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < n4; q += (long long)gridDim.x * 256) {
+            uint8_t b[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) b[k] = 4 * q + k < N ? c[4 * q + k] : 0xFF;
+            for (int a = 0; a < m; ++a) {
+                uint32_t w = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) w |= (uint32_t)(b[k] == a) << (8 * k);
+                reinterpret_cast<uint32_t *>(o + (size_t)a * Npad)[q] = w;
+            }
+        }
+    }
+}
+
+extern "C" hipError_t fbn_ci_onehot_build(const uint8_t *cols, const int32_t *dims, const int32_t *lead0, long long N,
+                                          long long Npad, int nvars, int8_t *out, hipStream_t s) {
+    const long long g = (Npad / 4 + 255) / 256;
+    hipLaunchKernelGGL(ci_onehot_build, dim3((unsigned)(g < 64 ? g : 64), (unsigned)(nvars < 1024 ? nvars : 1024)),
+                       dim3(256), 0, s, cols, dims, lead0, N, Npad, nvars, out);
+    return hipGetLastError();
+}
+
 extern "C" int fbn_ci_gram_task_ints(void) { return kGramTaskInts; }
 
 extern "C" hipError_t fbn_ci_gram(const uint32_t *bits, long long W, const int32_t *rl, const int32_t *tasks,

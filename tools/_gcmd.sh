@@ -3,15 +3,12 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_pc.py tests/test_gpu_pc_dist.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t_pc.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/t_pc.log; exit 1; }
 tail -1 gpurun_out/t_pc.log
-echo "default"; timeout -k 10 120 python tools/pc5_timing.py 5 2>&1 | grep -E "run " | tail -1
-echo "no runs"; FBN_CI_NO_RUNS=1 timeout -k 10 120 python tools/pc5_timing.py 5 2>&1 | grep -E "run " | tail -1
-timeout -k 10 60 ./tools/micro/valu_rate
-for x in 0 1; do
-mkdir -p gpurun_out/gx$x
-FBN_CI_NO_RUNS=$x timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/gx$x -o run --output-format csv -- python tools/pc5_timing.py 3 > /dev/null 2>&1 || exit 1
+echo "default"; timeout -k 10 120 python tools/pc5_timing.py 5 2>&1 | grep -E "run " | tail -5
+echo "no blas"; FBN_CI_GRAM_NO_BLAS=1 timeout -k 10 120 python tools/pc5_timing.py 5 2>&1 | grep -E "run " | tail -1
+mkdir -p gpurun_out/bl
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/bl -o run --output-format csv -- python tools/pc5_timing.py 3 > /dev/null 2>&1 || exit 1
 python3 -c "
 import csv
-for r in list(csv.DictReader(open('gpurun_out/gx$x/run_kernel_stats.csv')))[:4]:
-    print('$x', r['Name'][:60], r['Calls'], round(float(r['AverageNs'])/1e3,1), 'us', round(float(r['TotalDurationNs'])/1e6/3,3), 'ms/run')
+for r in list(csv.DictReader(open('gpurun_out/bl/run_kernel_stats.csv')))[:8]:
+    print(r['Name'][:70], r['Calls'], round(float(r['AverageNs'])/1e3,1), 'us', round(float(r['TotalDurationNs'])/1e6/3,3), 'ms/run')
 "
-done
