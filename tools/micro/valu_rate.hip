@@ -1,6 +1,10 @@
 // valu_rate.hip -- diagnostic: int32 VALU issue rate on gfx950 for the bit-sliced CI kernels' inner
-// ops: v_bcnt_u32_b32 (popcount + accumulate), v_and_b32 and the pair (and + bcnt), 16 independent
-// chains per lane, 8 waves per SIMD (8192 blocks of 256 threads); prints lane-ops/s per kind.
+// ops, 16 independent chains per lane, 8 waves per SIMD (8192 blocks of 256 threads):
+//   kind 0: xor + v_bcnt_u32_b32 (popcount + accumulate)   2 instructions per chain step
+//   kind 1: (a & b) ^ k -- the compiler emits ONE v_bitop3_b32   1 instruction per step
+//   kind 2: and + bcnt (the CI kernels' inner pair)            2 instructions per step
+// Measured (round 2): kind 1 70 T instr-lanes/s (0.89 of the 78.6 T issue peak: 2 cycles per wave64
+// instruction), kind 0 / 2: 29 / 34 ms vs 9.6 ms -- v_bcnt_u32_b32 issues at half rate (4 cycles).
 //   hipcc --offload-arch=gfx950 -O3 tools/micro/valu_rate.hip -o tools/micro/valu_rate
 #include <hip/hip_runtime.h>
 
@@ -44,9 +48,8 @@ int main() {
             (void)hipEventSynchronize(e1);
             float ms = 0;
             (void)hipEventElapsedTime(&ms, e0, e1);
-            // two VALU ops per chain step in every kind (the xor / and feeding the bcnt or the xor)
-            const double lane_ops = 2.0 * 16 * iters * (double)blocks * 256;
-            if (rep) printf("%s %.3f ms  %.1f T lane-ops/s (2 ops per chain step)\n", names[kind], ms, lane_ops / (ms * 1e-3) / 1e12);
+            const double steps = 16.0 * iters * (double)blocks * 256;  // chain steps (lanes)
+            if (rep) printf("%s %.3f ms  %.1f T chain-steps/s\n", names[kind], ms, steps / (ms * 1e-3) / 1e12);
         }
     }
     return 0;
