@@ -24,7 +24,8 @@ extern "C" hipError_t fbn_jt_launch(const JtOp *ops, int nops, const int32_t *au
 extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, const int32_t *items, long long N,
                                     long long n, int d, double alpha, double *g2, int32_t *df, double *p,
                                     uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
-                                    int32_t *gscratch, unsigned long long *stats, hipStream_t stream);
+                                    int32_t *gscratch, unsigned long long *stats, const uint32_t *bits,
+                                    const int32_t *row0, long long W, hipStream_t stream);
 extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy);
 extern "C" hipError_t fbn_jt_evidence_check(const int8_t *ev, long long n, int V, const int32_t *dom,
                                             unsigned long long *first, hipStream_t s);
@@ -1366,12 +1367,14 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
     }
     if (all_pairs) return SetError(FBN_ERR_ARG, "implicit pair batches need the bit-sliced path");
     size_t lds = 0;
+    int64_t mask_rows = 0;  // bit-sliced counting: dimz * (dx + dy + d) mask rows per test
     for (int64_t i = 0; i < n; ++i) {
         const int32_t *it = items + i * w;
         int64_t dimz = 1;
         for (int j = 0; j < d; ++j) dimz *= c->dims[it[2 + j]];
         if (dimz > (1 << 24)) return SetError(FBN_ERR_LIMIT, "test %lld: conditioning table too large", (long long)i);
         lds = std::max(lds, fbn_ci_lds_bytes((int)dimz, c->dims[it[0]], c->dims[it[1]]));
+        mask_rows += dimz * (c->dims[it[0]] + c->dims[it[1]] + d);
     }
     // tables beyond the LDS budget: the same layout in a per-workgroup global scratch region
     const bool global_tables = lds > 160 * 1024;
@@ -1393,14 +1396,20 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         if ((rc = S.scratch.ensure((size_t)grid * stride))) return rc;
         gscratch = S.scratch.as<int32_t>();
     }
-    S.last_bytes = n * c->N * (2 + d);  // uint8 columns x, y, z_1..z_d streamed once
+    // FBN_CI_BITSN = 1: d >= 2 tests with every state count <= 4 count from the bit-sliced store
+    // (ci_kernels.hip) when it is built.  Opt-in: every z-configuration re-reads the x / y value rows,
+    // so config 5 level 2 moves more bytes than the byte columns (0.79 vs 0.76 ms) and levels 3-5
+    // are several times slower (up to 4^5 configurations per test)
+    const bool bitsn = d >= 2 && c->bits_ready && maxdim <= 4 && getenv("FBN_CI_BITSN");
+    S.last_bytes = bitsn ? mask_rows * c->bits_W * 4  // the mask rows each z-configuration reads
+                         : n * c->N * (2 + d);  // uint8 columns x, y, z_1..z_d streamed once
     if (c->timing) FBN_HIP(hipEventRecord(S.ev0, s));
     hipError_t e = fbn_ci_launch(c->cols.as<uint8_t>(), c->ddims.as<int32_t>(),
                                  zc_items ? zc_items : S.items.as<int32_t>(), c->N, n, d, alpha,
                                  want_g2p ? c->g2.as<double>() : nullptr, zc_df ? zc_df : S.df.as<int32_t>(),
                                  want_g2p ? c->p.as<double>() : nullptr, zc_indep ? zc_indep : S.indep.as<uint8_t>(),
-                                 counts_dev, lds, grid,
-                                 gscratch, c->stats.as<unsigned long long>(), s);
+                                 counts_dev, lds, grid, gscratch, c->stats.as<unsigned long long>(),
+                                 bitsn ? c->bits.as<uint32_t>() : nullptr, c->brow.as<int32_t>(), c->bits_W, s);
     if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci kernel launch: %s", hipGetErrorString(e));
     if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
     return FBN_OK;

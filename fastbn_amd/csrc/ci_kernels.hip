@@ -42,6 +42,11 @@ struct CiArgs {
     // decision-margin log: [0] = min over tests of |p - alpha| as IEEE bits
     // (non-negative doubles order like their bit patterns), [1] = #tests with |p - alpha| < 1e-9
     unsigned long long *stats;
+    // non-null: count from the bit-sliced store instead (every variable of every test has <= 4
+    // states; all value rows of variable v start at row0[v], W words per row)
+    const uint32_t *bits;
+    const int32_t *row0;
+    long long W;
 };
 
 template <int D>
@@ -81,11 +86,64 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
         double *term = reinterpret_cast<double *>(smem + term_off);
 
         for (int c = tid; c < cells; c += 256) hist[c] = 0;
-        if (nsub > 1)
+        if (nsub > 1 && !A.bits)
             for (int c = tid; c < nsub * cells; c += 256) sub[c] = 0;
         __syncthreads();
+        if (A.bits) {
+            // bit-sliced counting: wave w takes the z-configurations k = w, w + 4, ... (k = sum of
+            // value * cum, last conditioning variable fastest); per 4-word step m = AND of the z
+            // rows of k, then popcount(x_a & m & y_b) for every cell -- every value row is read, no
+            // derivation; one wave total per (k, cell), written once (no atomics)
+            typedef __attribute__((ext_vector_type(4))) unsigned u4;
+            const long long W = A.W;
+            const uint32_t *px = A.bits + (size_t)A.row0[x] * W, *py = A.bits + (size_t)A.row0[y] * W;
+            for (int k = tid >> 6; k < dimz; k += 4) {
+                const uint32_t *pz[D > 0 ? D : 1];
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+                    const int v = (k / cum[j]) % A.dims[zv[j]];
+                    pz[j] = A.bits + (size_t)(A.row0[zv[j]] + v) * W;
+                }
+                uint32_t cnt[16];
+#pragma unroll
+                for (int c = 0; c < 16; ++c) cnt[c] = 0u;
+                for (long long w4 = lane; 4 * w4 < W; w4 += 64) {
+                    u4 m = {~0u, ~0u, ~0u, ~0u};
+#pragma unroll
+                    for (int j = 0; j < D; ++j) m &= *reinterpret_cast<const u4 *>(pz[j] + 4 * w4);
+                    u4 xv[4], yv[4];
+#pragma unroll
+                    for (int a = 0; a < 4; ++a)
+                        xv[a] = a < dx ? *reinterpret_cast<const u4 *>(px + a * W + 4 * w4) & m : u4{0u, 0u, 0u, 0u};
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        yv[b] = b < dy ? *reinterpret_cast<const u4 *>(py + b * W + 4 * w4) : u4{0u, 0u, 0u, 0u};
+#pragma unroll
+                    for (int a = 0; a < 4; ++a) {
+                        if (a >= dx) continue;
+#pragma unroll
+                        for (int b = 0; b < 4; ++b) {
+                            if (b >= dy) continue;
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) cnt[a * 4 + b] += __builtin_popcount(xv[a][q] & yv[b][q]);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        if (a >= dx || b >= dy) continue;
+                        uint32_t v = cnt[a * 4 + b];
+#pragma unroll
+                        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+                        if (lane == 0) hist[k * dxy + a * dy + b] = (int32_t)v;
+                    }
+            }
+        }
         int32_t *myhist = nsub > 1 ? sub + (tid >> 6) * cells : hist;
 
+        if (!A.bits) {
         const uint8_t *cx = A.cols + (size_t)x * A.N;
         const uint8_t *cy = A.cols + (size_t)y * A.N;
         const uint8_t *cz[D > 0 ? D : 1];
@@ -144,8 +202,9 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
                 if (lane == 0 && v) atomicAdd(&hist[c], v);
             }
         }
+        }  // byte columns
         __syncthreads();
-        if (nsub > 1) {
+        if (nsub > 1 && !A.bits) {
             for (int c = tid; c < cells; c += 256) {
                 int v = 0;
                 for (int w = 0; w < nsub; ++w) v += sub[w * cells + c];
@@ -252,9 +311,10 @@ extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy) {
 extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, const int32_t *items, long long N,
                                     long long n, int d, double alpha, double *g2, int32_t *df, double *p,
                                     uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
-                                    int32_t *gscratch, unsigned long long *stats, hipStream_t stream) {
+                                    int32_t *gscratch, unsigned long long *stats, const uint32_t *bits,
+                                    const int32_t *row0, long long W, hipStream_t stream) {
     CiArgs a{cols, dims, items, N, n, alpha, g2, df, p, indep, counts, gscratch, (long long)(lds_bytes / 4 + 1) & ~1ll,
-             stats};
+             stats, bits, row0, W};
     if (gscratch) lds_bytes = 0;
     switch (d) {
 #define FBN_CI_CASE(DD)                                                                              \

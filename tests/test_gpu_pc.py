@@ -235,6 +235,48 @@ def test_bit_sliced_marginal_tests_match_histogram_kernel(ns):
             assert abs(g2[k] - r["g2"]) <= G2_TOL * max(1.0, abs(r["g2"]))
 
 
+@pytest.mark.parametrize("ns", [33, 5000, 100003])
+def test_bit_sliced_conditional_tables_match_byte_columns(ns):
+    """FBN_CI_BITSN: d >= 2 tests whose variables all have <= 4 states count from the bit-sliced
+    store (z-configurations x cells of popcount(x_a & y_b & AND of z rows)).  Tables, df, G^2 and p
+    must equal the byte-column histogram kernel's and the oracle's, for ragged sample counts,
+    1..4-state variables and d = 2, 3."""
+    rng = np.random.default_rng(ns + 7)
+    nv = 9
+    dims = np.array([2, 3, 4, 1, 4, 3, 2, 4, 3], np.int32)
+    cols = np.stack([rng.integers(0, d, ns) for d in dims]).astype(np.uint8)
+    cols[4] = (cols[2] + cols[1]) % 4
+    ci = F.IndependenceTest(F.Dataset(columns=cols, dims=dims), 0.05, device=0)
+    od = O.OracleDataset(columns=cols, dims=dims)
+    os.environ["FBN_CI_FORCE_BITS"] = "1"
+    try:
+        ci.run(np.array([[0, 1]], np.int32), 0)  # builds the bit-sliced store
+    finally:
+        del os.environ["FBN_CI_FORCE_BITS"]
+    items2 = np.array([[x, y, a, b] for x in range(nv) for y in range(x + 1, nv) for a in range(nv) for b in
+                       range(a + 1, nv) if len({x, y, a, b}) == 4][::7], np.int32)
+    items3 = np.array([[0, 4, 1, 2, 7], [2, 5, 0, 4, 8], [1, 7, 3, 6, 5], [4, 8, 2, 0, 1]], np.int32)
+    for d, items in ((2, items2), (3, items3)):
+        os.environ["FBN_CI_BITSN"] = "1"
+        try:
+            g2, df, p, ind = ci.run(items, d)
+            cnt = ci.counts(int(items[0][0]), int(items[0][1]), [int(v) for v in items[0][2:]])
+        finally:
+            del os.environ["FBN_CI_BITSN"]
+        g2h, dfh, ph, indh = ci.run(items, d)
+        cnth = ci.counts(int(items[0][0]), int(items[0][1]), [int(v) for v in items[0][2:]])
+        np.testing.assert_array_equal(cnt, cnth)
+        np.testing.assert_array_equal(df, dfh)
+        np.testing.assert_array_equal(g2, g2h)
+        np.testing.assert_array_equal(p, ph)
+        np.testing.assert_array_equal(ind, indh)
+        for k in range(0, len(items), max(1, len(items) // 20)):
+            it = [int(v) for v in items[k]]
+            r = od.ci_test(it[0], it[1], it[2:])
+            assert df[k] == r["df"] and ind[k] == r["is_independent"]
+            assert abs(g2[k] - r["g2"]) <= G2_TOL * max(1.0, abs(r["g2"]))
+
+
 def test_g2_bit_exact_every_alarm5000_test(ci, alarm_paths):
     """Every CI test the reference's PC-stable run executes on ALARM-5000 (5206 tests, levels 0-4,
     from the restatement's log): G^2 bit-identical (the reference's single running sum over
