@@ -25,7 +25,8 @@ extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, co
                                     long long n, int d, double alpha, double *g2, int32_t *df, double *p,
                                     uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
                                     int32_t *gscratch, unsigned long long *stats, const uint32_t *bits,
-                                    const int32_t *row0, long long W, hipStream_t stream);
+                                    const int32_t *row0, long long W, const double *band, int nband,
+                                    hipStream_t stream);
 extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy);
 extern "C" hipError_t fbn_jt_evidence_check(const int8_t *ev, long long n, int V, const int32_t *dom,
                                             unsigned long long *first, hipStream_t s);
@@ -242,6 +243,7 @@ struct fbn_ci_ctx {
     DevBuf band;
     std::vector<double> band_host;
     double band_alpha = -1.0;
+    int band_n = 0;
     bool bits_ready = false;
     int64_t bits_W = 0;
     CiSlot slot[2];
@@ -265,23 +267,31 @@ static int64_t EnvOr0(const char *name, int64_t dflt) {
 
 // df <= 36 covers every bit-sliced test (<= 4 states, <= 1 conditioning variable: 4 * 3 * 3)
 constexpr int kBandDf = 36;
+constexpr int kBandDfMax = 256;  // larger df (few tests, deep levels): p evaluated
 
-// the band for `alpha` (delta = alpha / 4), computed on the host once per ctx and alpha; nullptr
-// (p evaluated for every test) when alpha is outside (0, 1) or FBN_CI_NO_BAND is set
-static int CiBand(fbn_ci_ctx *c, double alpha, hipStream_t s, const double **out) {
+// the band for `alpha` (delta = alpha / 4) over df 1..max(want_df, kBandDf) (at most kBandDfMax),
+// computed on the host per ctx and alpha and extended on demand; *out = nullptr (p evaluated for
+// every test) when alpha is outside (0, 1) or FBN_CI_NO_BAND is set
+static int CiBand(fbn_ci_ctx *c, double alpha, hipStream_t s, const double **out, int *nband, int want_df = 0) {
     *out = nullptr;
+    *nband = 0;
     if (!(alpha > 0.0 && alpha < 1.0) || getenv("FBN_CI_NO_BAND")) return FBN_OK;
-    if (c->band_alpha != alpha) {
+    const int want = std::min(kBandDfMax, std::max(kBandDf, want_df));
+    if (c->band_alpha != alpha || c->band_n < want) {
         const double delta = alpha / 4;
-        c->band_host.assign(2 * kBandDf + 1, 0.0);
-        for (int df = 1; df <= kBandDf; ++df)
+        const int have = c->band_alpha == alpha ? c->band_n : 0;
+        FBN_HIP(hipStreamSynchronize(s));  // the previous upload of the host table has completed
+        c->band_host.resize(2 * (size_t)want + 1);
+        for (int df = have + 1; df <= want; ++df)
             fbn_chisq_band(alpha, delta, df, &c->band_host[2 * df - 2], &c->band_host[2 * df - 1]);
-        c->band_host[2 * kBandDf] = delta;
+        c->band_host[2 * (size_t)want] = delta;
         if (int rc = c->band.ensure(c->band_host.size() * 8)) return rc;
         FBN_HIP(hipMemcpyAsync(c->band.p, c->band_host.data(), c->band_host.size() * 8, hipMemcpyHostToDevice, s));
         c->band_alpha = alpha;
+        c->band_n = want;
     }
     *out = c->band.as<double>();
+    *nband = c->band_n;
     return FBN_OK;
 }
 
@@ -1311,7 +1321,8 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         const int64_t skipped = d == 0 ? 2 : (pmode == 2 ? 3 : 0);
         S.last_bytes = (dim_rows - skipped * n) * c->bits_W * 4;
         const double *band = nullptr;  // decisions only: p evaluated inside the band
-        if (!want_g2p && (rc = CiBand(c, alpha, s, &band))) return rc;
+        int nband = 0;
+        if (!want_g2p && (rc = CiBand(c, alpha, s, &band, &nband))) return rc;
         if (c->timing) FBN_HIP(hipEventRecord(S.ev0, s));
         // all pairs of a range: register-blocked count kernel (ci_bits_pairs_tiled), then phase 2
         const bool gram0 = all_pairs && d == 0 && CiGram0Eligible(c);
@@ -1360,7 +1371,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
                                           S.bcounts.as<int32_t>(), counts_dev, c->stats.as<unsigned long long>(),
                                           c->browcnt.as<int32_t>(), c->pairtab.as<int32_t>(), pmode, c->nvars,
                                           c->num_cu, (long long)pair0, (tiled || gram0 || gram1) ? 1 : 0, band,
-                                          kBandDf, s);
+                                          nband, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci bits kernel launch: %s", hipGetErrorString(e));
         if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
         return FBN_OK;
@@ -1401,6 +1412,14 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
     // so config 5 level 2 moves more bytes than the byte columns (0.79 vs 0.76 ms) and levels 3-5
     // are several times slower (up to 4^5 configurations per test)
     const bool bitsn = d >= 2 && c->bits_ready && maxdim <= 4 && getenv("FBN_CI_BITSN");
+    // decisions only: the decision band up to this batch's largest df ((maxdim-1)^2 maxdim^d)
+    const double *hband = nullptr;
+    int hnband = 0;
+    if (!want_g2p) {
+        double dfmax = (double)(maxdim - 1) * (maxdim - 1);
+        for (int j = 0; j < d; ++j) dfmax *= maxdim;
+        if ((rc = CiBand(c, alpha, s, &hband, &hnband, (int)std::min<double>(dfmax, kBandDfMax)))) return rc;
+    }
     S.last_bytes = bitsn ? mask_rows * c->bits_W * 4  // the mask rows each z-configuration reads
                          : n * c->N * (2 + d);  // uint8 columns x, y, z_1..z_d streamed once
     if (c->timing) FBN_HIP(hipEventRecord(S.ev0, s));
@@ -1409,7 +1428,8 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
                                  want_g2p ? c->g2.as<double>() : nullptr, zc_df ? zc_df : S.df.as<int32_t>(),
                                  want_g2p ? c->p.as<double>() : nullptr, zc_indep ? zc_indep : S.indep.as<uint8_t>(),
                                  counts_dev, lds, grid, gscratch, c->stats.as<unsigned long long>(),
-                                 bitsn ? c->bits.as<uint32_t>() : nullptr, c->brow.as<int32_t>(), c->bits_W, s);
+                                 bitsn ? c->bits.as<uint32_t>() : nullptr, c->brow.as<int32_t>(), c->bits_W, hband,
+                                 hnband, s);
     if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci kernel launch: %s", hipGetErrorString(e));
     if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
     return FBN_OK;
@@ -1801,7 +1821,8 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
         for (auto &ev : c->l1ev) FBN_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     }
     const double *band = nullptr;
-    if ((rc = CiBand(c, alpha, s, &band))) return rc;
+    int nband = 0;
+    if ((rc = CiBand(c, alpha, s, &band, &nband))) return rc;
     static_assert(sizeof(std::pair<int, int>) == 8, "pair layout");
     FBN_HIP(hipMemcpyAsync(c->l1pairs.p, edges.data() + e_begin, (size_t)E * 8, hipMemcpyHostToDevice, s));
     if (!adjf.empty()) FBN_HIP(hipMemcpyAsync(c->l1adj.p, adjf.data(), adjf.size() * 4, hipMemcpyHostToDevice, s));
@@ -1824,7 +1845,7 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
                             c->l1st.as<uint8_t>(), c->l1sep.as<int32_t>(), c->l1cnt.as<long long>(),
                             c->l1len.as<int32_t>(), c->l1off.as<int32_t>(), E, (int)chunk, cap, scal, scal + 1,
                             c->l1items.as<int32_t>(), c->l1counts.as<int32_t>(), c->l1df.as<int32_t>(),
-                            c->l1indep.as<uint8_t>(), alpha, c->stats.as<unsigned long long>(), band, kBandDf,
+                            c->l1indep.as<uint8_t>(), alpha, c->stats.as<unsigned long long>(), band, nband,
                             c->l1open.as<unsigned>() + r, reinterpret_cast<unsigned long long *>(scal + 2),
                             c->l1tmp.p, scan_bytes, c->num_cu, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci level-1 round: %s", hipGetErrorString(e));

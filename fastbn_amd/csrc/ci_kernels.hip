@@ -47,9 +47,14 @@ struct CiArgs {
     const uint32_t *bits;
     const int32_t *row0;
     long long W;
+    // decisions only (p == nullptr): [lo, hi] per df 1..nband then delta (ci_chisq.h fbn_chisq_band)
+    const double *band;
+    int nband;
 };
 
-template <int D>
+// BITS: count from the bit-sliced store (A.bits); a separate instantiation, so the byte-column
+// kernel keeps its register budget (74 VGPRs vs 178 with the bit-sliced counters compiled in)
+template <int D, bool BITS>
 __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
     extern __shared__ __align__(16) int32_t lds_base[];
     int32_t *smem = A.gscratch ? A.gscratch + (size_t)blockIdx.x * A.gstride : lds_base;
@@ -86,32 +91,38 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
         double *term = reinterpret_cast<double *>(smem + term_off);
 
         for (int c = tid; c < cells; c += 256) hist[c] = 0;
-        if (nsub > 1 && !A.bits)
+        if (nsub > 1 && !BITS)
             for (int c = tid; c < nsub * cells; c += 256) sub[c] = 0;
         __syncthreads();
-        if (A.bits) {
-            // bit-sliced counting: wave w takes the z-configurations k = w, w + 4, ... (k = sum of
-            // value * cum, last conditioning variable fastest); per 4-word step m = AND of the z
-            // rows of k, then popcount(x_a & m & y_b) for every cell -- every value row is read, no
-            // derivation; one wave total per (k, cell), written once (no atomics)
+        if (BITS) {
+            // bit-sliced counting: wave w takes the prefixes p = w, w + 4, ... of the z-configuration
+            // (values of z_1 .. z_{d-1}; the last conditioning variable is the fastest digit, so
+            // configuration k = p * dl + c for its value c).  Per 4-word step: m = AND of the prefix's
+            // z rows, then for each value c of the last z (<= 4), every x value row ANDed with
+            // m & z_last[c] and popcounted against every y value row -- the x, y and last-z rows are
+            // loaded once per step for all dl configurations; one wave total per (k, cell)
             typedef __attribute__((ext_vector_type(4))) unsigned u4;
             const long long W = A.W;
             const uint32_t *px = A.bits + (size_t)A.row0[x] * W, *py = A.bits + (size_t)A.row0[y] * W;
-            for (int k = tid >> 6; k < dimz; k += 4) {
-                const uint32_t *pz[D > 0 ? D : 1];
+            const int dl = A.dims[zv[D > 0 ? D - 1 : 0]];
+            const uint32_t *pl = A.bits + (size_t)A.row0[zv[D > 0 ? D - 1 : 0]] * W;
+            for (int pfx = tid >> 6; pfx < dimz / dl; pfx += 4) {
+                const uint32_t *pz[D > 1 ? D - 1 : 1];
 #pragma unroll
-                for (int j = 0; j < D; ++j) {
-                    const int v = (k / cum[j]) % A.dims[zv[j]];
+                for (int j = 0; j + 1 < D; ++j) {
+                    const int v = (pfx * dl / cum[j]) % A.dims[zv[j]];
                     pz[j] = A.bits + (size_t)(A.row0[zv[j]] + v) * W;
                 }
-                uint32_t cnt[16];
+                uint32_t cnt[4][16];
 #pragma unroll
-                for (int c = 0; c < 16; ++c) cnt[c] = 0u;
+                for (int c = 0; c < 4; ++c)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) cnt[c][e] = 0u;
                 for (long long w4 = lane; 4 * w4 < W; w4 += 64) {
                     u4 m = {~0u, ~0u, ~0u, ~0u};
 #pragma unroll
-                    for (int j = 0; j < D; ++j) m &= *reinterpret_cast<const u4 *>(pz[j] + 4 * w4);
-                    u4 xv[4], yv[4];
+                    for (int j = 0; j + 1 < D; ++j) m &= *reinterpret_cast<const u4 *>(pz[j] + 4 * w4);
+                    u4 xv[4], yv[4], zl[4];
 #pragma unroll
                     for (int a = 0; a < 4; ++a)
                         xv[a] = a < dx ? *reinterpret_cast<const u4 *>(px + a * W + 4 * w4) & m : u4{0u, 0u, 0u, 0u};
@@ -119,31 +130,40 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
                     for (int b = 0; b < 4; ++b)
                         yv[b] = b < dy ? *reinterpret_cast<const u4 *>(py + b * W + 4 * w4) : u4{0u, 0u, 0u, 0u};
 #pragma unroll
-                    for (int a = 0; a < 4; ++a) {
-                        if (a >= dx) continue;
+                    for (int c = 0; c < 4; ++c)
+                        zl[c] = c < dl ? *reinterpret_cast<const u4 *>(pl + c * W + 4 * w4) : u4{0u, 0u, 0u, 0u};
 #pragma unroll
-                        for (int b = 0; b < 4; ++b) {
-                            if (b >= dy) continue;
+                    for (int c = 0; c < 4; ++c) {
+                        if (c >= dl) continue;
 #pragma unroll
-                            for (int q = 0; q < 4; ++q) cnt[a * 4 + b] += __builtin_popcount(xv[a][q] & yv[b][q]);
+                        for (int a = 0; a < 4; ++a) {
+                            if (a >= dx) continue;
+                            const u4 xm = xv[a] & zl[c];
+#pragma unroll
+                            for (int b = 0; b < 4; ++b) {
+                                if (b >= dy) continue;
+#pragma unroll
+                                for (int q = 0; q < 4; ++q) cnt[c][a * 4 + b] += __builtin_popcount(xm[q] & yv[b][q]);
+                            }
                         }
                     }
                 }
 #pragma unroll
-                for (int a = 0; a < 4; ++a)
+                for (int c = 0; c < 4; ++c)
 #pragma unroll
-                    for (int b = 0; b < 4; ++b) {
-                        if (a >= dx || b >= dy) continue;
-                        uint32_t v = cnt[a * 4 + b];
+                    for (int a = 0; a < 4; ++a)
 #pragma unroll
-                        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-                        if (lane == 0) hist[k * dxy + a * dy + b] = (int32_t)v;
-                    }
+                        for (int b = 0; b < 4; ++b) {
+                            if (c >= dl || a >= dx || b >= dy) continue;
+                            uint32_t v = cnt[c][a * 4 + b];
+#pragma unroll
+                            for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+                            if (lane == 0) hist[(pfx * dl + c) * dxy + a * dy + b] = (int32_t)v;
+                        }
             }
         }
+        if (!BITS) {
         int32_t *myhist = nsub > 1 ? sub + (tid >> 6) * cells : hist;
-
-        if (!A.bits) {
         const uint8_t *cx = A.cols + (size_t)x * A.N;
         const uint8_t *cy = A.cols + (size_t)y * A.N;
         const uint8_t *cz[D > 0 ? D : 1];
@@ -204,7 +224,7 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
         }
         }  // byte columns
         __syncthreads();
-        if (nsub > 1 && !A.bits) {
+        if (nsub > 1 && !BITS) {
             for (int c = tid; c < cells; c += 256) {
                 int v = 0;
                 for (int w = 0; w < nsub; ++w) v += sub[w * cells + c];
@@ -278,6 +298,12 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
             if (df == 0) {  // src/IndependenceTest.cpp:140-142, 349-351
                 p = 1.0;
                 ind = true;
+            } else if (!A.p && A.band && df <= A.nband && g2 < A.band[2 * df - 2]) {
+                p = A.alpha + A.band[2 * A.nband];  // p > alpha + delta: logged as margin delta
+                ind = true;
+            } else if (!A.p && A.band && df <= A.nband && g2 > A.band[2 * df - 1]) {
+                p = A.alpha - A.band[2 * A.nband];
+                ind = false;
             } else {
                 p = fbn_chisq_pvalue(g2, df);
                 ind = p > A.alpha;
@@ -312,14 +338,18 @@ extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, co
                                     long long n, int d, double alpha, double *g2, int32_t *df, double *p,
                                     uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
                                     int32_t *gscratch, unsigned long long *stats, const uint32_t *bits,
-                                    const int32_t *row0, long long W, hipStream_t stream) {
+                                    const int32_t *row0, long long W, const double *band, int nband,
+                                    hipStream_t stream) {
     CiArgs a{cols, dims, items, N, n, alpha, g2, df, p, indep, counts, gscratch, (long long)(lds_bytes / 4 + 1) & ~1ll,
-             stats, bits, row0, W};
+             stats, bits, row0, W, band, nband};
     if (gscratch) lds_bytes = 0;
     switch (d) {
 #define FBN_CI_CASE(DD)                                                                              \
     case DD:                                                                                         \
-        hipLaunchKernelGGL(ci_g2_kernel<DD>, dim3(grid), dim3(256), lds_bytes, stream, a);           \
+        if (bits && DD >= 2)                                                                         \
+            hipLaunchKernelGGL((ci_g2_kernel<DD, true>), dim3(grid), dim3(256), lds_bytes, stream, a);  \
+        else                                                                                         \
+            hipLaunchKernelGGL((ci_g2_kernel<DD, false>), dim3(grid), dim3(256), lds_bytes, stream, a); \
         break;
         FBN_CI_CASE(0)
         FBN_CI_CASE(1)
