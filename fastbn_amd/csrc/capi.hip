@@ -1837,7 +1837,9 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
     if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci level-1 setup: %s", hipGetErrorString(e));
     long long *scal = c->l1scal.as<long long>();  // total, launched, rows read
     int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(32, EnvOr0("FBN_PC_ROUND0", 8192) / E));
-    const int64_t growth = std::max<int64_t>(2, EnvOr0("FBN_PC_GROWTH", 4));
+    // chunk x2 per round: rounds here cost a few launches, speculation costs counted tests (config 5:
+    // x4 launches 430k tests for 294k counted, x2 345k)
+    const int64_t growth = std::max<int64_t>(2, EnvOr0("FBN_PC_GROWTH", 2));
     for (int r = 0;; ++r) {
         if (r >= kL1MaxRounds) return SetError(FBN_ERR_LIMIT, "level 1: more than %d device rounds", kL1MaxRounds);
         e = fbn_ci_l1_round(c->bits.as<uint32_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(), c->bits_W,

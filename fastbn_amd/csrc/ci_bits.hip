@@ -168,11 +168,13 @@ __device__ __forceinline__ void count_pair(const uint32_t *__restrict__ bx, cons
 // exactly -- N[c][a][DY-1] = N_xz[a][c] - sum_b, N[c][DX-1][b] = N_yz[b][c] - sum_a,
 // N[DZ-1][a][b] = N_xy[a][b] - sum_c; only DX-1, DY-1, DZ-1 mask rows are read
 template <int DX, int DY, int DZ>
-__device__ __forceinline__ void count_test_derived(const uint32_t *__restrict__ bx, const uint32_t *__restrict__ by,
-                                                   const uint32_t *__restrict__ bz, long long W, int lane,
-                                                   int32_t *__restrict__ out, const int32_t *__restrict__ Txy, bool txy,
-                                                   const int32_t *__restrict__ Txz, bool txz,
-                                                   const int32_t *__restrict__ Tyz, bool tyz) {
+__device__ __forceinline__ void count_test_derived_full(const uint32_t *__restrict__ bx,
+                                                        const uint32_t *__restrict__ by,
+                                                        const uint32_t *__restrict__ bz, long long W, int lane,
+                                                        const int32_t *__restrict__ Txy, bool txy,
+                                                        const int32_t *__restrict__ Txz, bool txz,
+                                                        const int32_t *__restrict__ Tyz, bool tyz,
+                                                        int32_t (&full)[DZ * DX * DY]) {
     constexpr int MX = DX - 1, MY = DY - 1, MZ = DZ - 1, M = MX * MY * MZ, NC = M > 0 ? M : 1;
     uint32_t cnt[NC];
 #pragma unroll
@@ -209,7 +211,6 @@ __device__ __forceinline__ void count_test_derived(const uint32_t *__restrict__ 
     auto nxy = [&](int a, int b) { return txy ? Txy[b * DX + a] : Txy[a * DY + b]; };
     auto nxz = [&](int a, int c) { return txz ? Txz[c * DX + a] : Txz[a * DZ + c]; };
     auto nyz = [&](int b, int c) { return tyz ? Tyz[c * DY + b] : Tyz[b * DZ + c]; };
-    int32_t full[DZ * DX * DY];
 #pragma unroll
     for (int c = 0; c < MZ; ++c) {
 #pragma unroll
@@ -240,6 +241,16 @@ __device__ __forceinline__ void count_test_derived(const uint32_t *__restrict__ 
             for (int c = 0; c < MZ; ++c) r -= full[(c * DX + a) * DY + b];
             full[(MZ * DX + a) * DY + b] = r;
         }
+}
+
+template <int DX, int DY, int DZ>
+__device__ __forceinline__ void count_test_derived(const uint32_t *__restrict__ bx, const uint32_t *__restrict__ by,
+                                                   const uint32_t *__restrict__ bz, long long W, int lane,
+                                                   int32_t *__restrict__ out, const int32_t *__restrict__ Txy, bool txy,
+                                                   const int32_t *__restrict__ Txz, bool txz,
+                                                   const int32_t *__restrict__ Tyz, bool tyz) {
+    int32_t full[DZ * DX * DY];
+    count_test_derived_full<DX, DY, DZ>(bx, by, bz, W, lane, Txy, txy, Txz, txz, Tyz, tyz, full);
     if (lane < DZ * DX * DY) {
         int32_t v = 0;
 #pragma unroll
