@@ -1962,10 +1962,10 @@ int CiTriplePrepare(fbn_ci_ctx *c, const std::vector<std::vector<int>> &adj,
 struct FlagIsZero {
     __host__ __device__ bool operator()(uint8_t f) const { return f == 0; }
 };
-// the pairs (i < j) of the complete graph level 0 kept (decision 0), in pair order: compacted on the
-// device from the last all-pairs batch (slot 0), only the kept indices cross PCIe
-int CiAllPairsKept(fbn_ci_ctx *c, int64_t P, std::vector<std::pair<int, int>> &kept) {
-    kept.clear();
+// the pairs (i < j) of the complete graph kept (decision 0) by the last all-pairs batch (slot 0:
+// pairs [t0, t0 + P)), appended to `kept` in pair order: compacted on the device, only the kept
+// indices cross PCIe
+int CiAllPairsKept(fbn_ci_ctx *c, int64_t t0, int64_t P, std::vector<std::pair<int, int>> &kept) {
     if (P <= 0) return FBN_OK;
     if (P > INT32_MAX) return SetError(FBN_ERR_LIMIT, "too many pairs for the kept-pair compaction");
     FBN_HIP(hipSetDevice(c->device));
@@ -1988,13 +1988,15 @@ int CiAllPairsKept(fbn_ci_ctx *c, int64_t P, std::vector<std::pair<int, int>> &k
     const int nk = c->h_kept[0];
     std::vector<int32_t> idx((size_t)nk);
     if (nk) FBN_HIP(hipMemcpy(idx.data(), c->keptidx.p, (size_t)nk * 4, hipMemcpyDeviceToHost));
-    kept.resize((size_t)nk);
+    const size_t base = kept.size();
+    kept.resize(base + (size_t)nk);
     const int n = c->nvars;
     int i = 0;
     int64_t row0 = 0, row1 = n - 1;  // pair indices of row i: [row0, row1)
     for (int t = 0; t < nk; ++t) {
-        while (idx[t] >= row1) ++i, row0 = row1, row1 += n - 1 - i;
-        kept[t] = {i, i + 1 + (int)(idx[t] - row0)};
+        const int64_t q = t0 + idx[t];
+        while (q >= row1) ++i, row0 = row1, row1 += n - 1 - i;
+        kept[base + t] = {i, i + 1 + (int)(q - row0)};
     }
     return FBN_OK;
 }

@@ -424,16 +424,22 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
         const double k0 = res.kernel_s;
         std::vector<char> removed((size_t)P);
         static_assert(sizeof(char) == sizeof(uint8_t), "flag layout");
-        int rc = CiBatchLaunchAllPairs(ctx, alpha, &st_all, 0, P);
-        if (!rc) rc = CiBatchWait(ctx, 0, reinterpret_cast<uint8_t *>(removed.data()), nullptr, res);
+        // batches of at most FBN_PC_L0CHUNK pairs (per-test count records: 256 B each; a
+        // 10k-variable graph has 5e7 pairs), kept pairs compacted per batch
+        const int64_t chunk = std::max<int64_t>(1, EnvOr("FBN_PC_L0CHUNK", (int64_t)1 << 22));
+        int rc = FBN_OK;
+        for (int64_t t0 = 0; t0 < P && !rc; t0 += chunk) {
+            const int64_t m = std::min(chunk, P - t0);
+            rc = CiBatchLaunchAllPairs(ctx, alpha, &st_all, t0, m);
+            if (!rc) rc = CiBatchWait(ctx, 0, reinterpret_cast<uint8_t *>(removed.data() + t0), nullptr, res);
+            if (!rc && P > (1 << 16)) rc = CiAllPairsKept(ctx, t0, m, edges);  // compacted on the device
+        }
         if (rc) return rc;
         auto tb = std::chrono::steady_clock::now();
         res.sepset.set_level0(n, removed.data());
         res.tests_per_level.push_back(P);
         res.launched_per_level.push_back(P);
-        if (P > (1 << 16)) {
-            if ((rc = CiAllPairsKept(ctx, P, edges))) return rc;  // kept pairs, compacted on the device
-        } else {  // small graphs: a host pass over the flags costs less than the extra round trip
+        if (P <= (1 << 16)) {  // small graphs: a host pass over the flags costs less than the round trip
             int64_t k = 0;
             for (int i = 0; i < n; ++i)
                 for (int j = i + 1; j < n; ++j, ++k)

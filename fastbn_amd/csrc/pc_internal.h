@@ -182,8 +182,9 @@ struct LevelOut {
     std::vector<int> sep;  // [edge][d]: the sorted sepset of each removed edge of the range
     int64_t counted = 0, launched = 0;
 };
-// the kept pairs of the last complete-graph level-0 batch, compacted on the device (capi.hip)
-int CiAllPairsKept(fbn_ci_ctx *c, int64_t P, std::vector<std::pair<int, int>> &kept);
+// the kept pairs of the last complete-graph level-0 batch (pairs [t0, t0 + P)), appended in pair
+// order, compacted on the device (capi.hip)
+int CiAllPairsKept(fbn_ci_ctx *c, int64_t t0, int64_t P, std::vector<std::pair<int, int>> &kept);
 // a PC run's level 1 (group size 1) on the device (capi.hip); *done = false: not eligible
 int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<int>> &adj,
                    const std::vector<std::pair<int, int>> &edges, size_t e_begin, size_t e_end, LevelOut &out,

@@ -277,6 +277,24 @@ def test_bit_sliced_conditional_tables_match_byte_columns(ns):
             assert abs(g2[k] - r["g2"]) <= G2_TOL * max(1.0, abs(r["g2"]))
 
 
+def test_level0_batches_and_device_compaction_match_single_batch():
+    """Level 0 of the complete graph in bounded batches (FBN_PC_L0CHUNK) with the kept pairs
+    compacted on the device per batch: the same skeleton, sepsets and counts as one batch, on a
+    400-variable x 20k synthetic dataset (79,800 pairs: the device-compaction path)."""
+    from fastbn_amd import synth
+    cols, dims = synth.config5_dataset(400, 20000)
+    ci = F.IndependenceTest(F.Dataset(columns=cols, dims=dims))
+    a = F.PCStable(0.05, 3).StructLearnCompData(ci)
+    os.environ["FBN_PC_L0CHUNK"] = "9999"
+    try:
+        b = F.PCStable(0.05, 3).StructLearnCompData(ci)
+    finally:
+        del os.environ["FBN_PC_L0CHUNK"]
+    assert a.edges == b.edges and a.sepset == b.sepset
+    assert a.tests_per_level.tolist() == b.tests_per_level.tolist()
+    assert a.oriented == b.oriented
+
+
 def test_g2_bit_exact_every_alarm5000_test(ci, alarm_paths):
     """Every CI test the reference's PC-stable run executes on ALARM-5000 (5206 tests, levels 0-4,
     from the restatement's log): G^2 bit-identical (the reference's single running sum over
