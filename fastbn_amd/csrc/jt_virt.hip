@@ -268,6 +268,47 @@ __device__ __forceinline__ void vbins(const Store &S, const Clq &C, const Dens &
     }
 }
 
+// The marginals of up to kFuseVars variables of one clique in ONE in-order sweep over the final table
+// (stored scratch rows when MAT, else recomputed entries): entry e adds into bin (variable i, value
+// (e / cum_i) % dim_i) of an LDS accumulator [bin][64 lanes].  Every bin receives its entries in
+// increasing e -- the order of the per-variable SeqMarg pass it replaces -- starting from 0.0, so
+// each bin sum is bit-identical; one pass instead of one per variable.
+constexpr int kFuseVars = 4, kFuseBins = 16;
+template <int L, bool P32, int SP, bool MAT>
+__device__ __forceinline__ void vmarg_fused(const Store &S, const Clq &C, const Dens &D, int scr, const Den &Df,
+                                            int T, int nf, const int (&cum)[kFuseVars],
+                                            const int (&dim)[kFuseVars], const int (&base)[kFuseVars],
+                                            double *__restrict__ acc, int lane) {
+    constexpr int U = MAT ? 16 : Unroll<L>::U;
+    int lo[kFuseVars], dd[kFuseVars];
+#pragma unroll
+    for (int i = 0; i < kFuseVars; ++i) lo[i] = 0, dd[i] = 0;
+    for (int n0 = 0; n0 < T; n0 += U) {
+        const int cnt = T - n0 < U ? T - n0 : U;
+        double val[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = u < cnt ? n0 + u : 0;
+            if (MAT) val[u] = mdiv(S.template ldp<(SP >> 8)>(scr + e * 512), Df);
+            else val[u] = entry<L, true, P32>(S, C, D, e);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (u >= cnt) continue;
+#pragma unroll
+            for (int i = 0; i < kFuseVars; ++i) {
+                if (i >= nf) continue;
+                double *a = acc + (base[i] + dd[i]) * 64 + lane;
+                *a += val[u];
+                if (++lo[i] == cum[i]) {
+                    lo[i] = 0;
+                    if (++dd[i] == dim[i]) dd[i] = 0;
+                }
+            }
+        }
+    }
+}
+
 // dispatch on the (wave-uniform) chain length and digit packing
 #define FBN_VDISPATCH(Lv, P32v, CALL)                                  \
     do {                                                               \
@@ -310,6 +351,7 @@ void jt_virt_kernel(
     long long ncases, long long store_rows, long long scratch_row, long long scratch_rows, int nc, int V, int SD,
     int dbg) {
     __shared__ int sbad[JT_V_WAVES];
+    __shared__ double macc[JT_V_WAVES][kFuseBins * 64];  // fused marginal bins, per wave
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     Store S;  // the block's store (messages, denominators, one scratch table per wave)
@@ -489,24 +531,64 @@ void jt_virt_kernel(
                         if (j0 + u < Ts) S.st_row(dis + j0 + u, (o[u] == 0.0) ? 0.0 : a[u] / o[u]);
                 }
             }
-            // marginals of the variables whose chosen clique (for this case) is this one
-            for (int mi = 0; mi < ((dbg & 4) ? 0 : q.nmarg); ++mi) {
+            // marginals of the variables whose chosen clique (for this case) is this one: up to
+            // kFuseVars of them (kFuseBins values in total) in one fused sweep, the rest one pass each
+            const bool mat = q.mat && !(dbg & 64) && !((dbg & 512) && q.k < 2);
+            const bool fuse = !(dbg & 1024);
+            int fv[kFuseVars], fcum[kFuseVars], fdim[kFuseVars], fbase[kFuseVars];
+#pragma unroll
+            for (int i = 0; i < kFuseVars; ++i) fv[i] = 0, fcum[i] = 1, fdim[i] = 1, fbase[i] = 0;
+            int nf = 0, nb = 0;
+            auto finish = [&](int mi, auto bin_of) {  // outputs of marginal record mi from its bins
                 const int32_t *__restrict__ rec = aux + q.marg_off + 4 * mi;
-                const int off = rec[0], dim = rec[1], var = rec[2], cum = rec[3];
+                const int off = rec[0], dim = rec[1], var = rec[2];
                 const int sb = IROW(nc + var);
                 const bool mine = ((sb & 0xFFFFFF) == q.id) && ev[var] < 0;
-                if (__ballot(mine) == 0ull) continue;
                 const int best = sb >> 24;
                 double *__restrict__ o = out + off;
                 const bool wr = mine && act;
-                const int bw = dim * cum;
                 double tot = 0.0;
-                // bins = values of the variable, each in entry order; tot = sum of the bins in order
+                for (int d = 0; d < dim; ++d) {  // bins in value order; tot = their sum in order
+                    const double acc = bin_of(d);
+                    if (wr) o[d] = acc;
+                    tot += acc;
+                }
+                if (wr) {
+                    if (var == 0) {  // label: ArgMax, strict '>' from 0 (src/Inference.cpp:92-102)
+                        int lab = 0;
+                        double mx = 0.0;
+                        for (int d = 0; d < dim; ++d) {
+                            const double p = (best == 1) ? o[d] : o[d] / tot;
+                            if (p > mx) mx = p, lab = d;
+                        }
+                        labels[cs] = lab;
+                    }
+                    for (int d = 0; d < dim; ++d) o[d] = o[d] / tot;
+                }
+            };
+            for (int mi = 0; mi < ((dbg & 4) ? 0 : q.nmarg); ++mi) {
+                const int32_t *__restrict__ rec = aux + q.marg_off + 4 * mi;
+                const int dim = rec[1], var = rec[2], cum = rec[3];
+                const int sb = IROW(nc + var);
+                const bool mine = ((sb & 0xFFFFFF) == q.id) && ev[var] < 0;
+                if (__ballot(mine) == 0ull) continue;
+                if (fuse && nf < kFuseVars && nb + dim <= kFuseBins) {  // into the fused sweep
+#pragma unroll
+                    for (int i = 0; i < kFuseVars; ++i)
+                        if (i == nf) fv[i] = mi, fcum[i] = cum, fdim[i] = dim, fbase[i] = nb;
+                    ++nf, nb += dim;
+                    continue;
+                }
+                const int bw = dim * cum;
+                double *__restrict__ o = out + (aux + q.marg_off + 4 * mi)[0];
+                const bool wr = mine && act;
+                const int best = sb >> 24;
+                double tot = 0.0;
                 auto fl = [&](int d, double acc) {
                     if (wr) o[d] = acc;
                     tot += acc;
                 };
-                if (q.mat && !(dbg & 64) && !((dbg & 512) && q.k < 2)) {
+                if (mat) {
                     vbins_scr<SP>(S, scr, pick(D, Lf), q.T, SeqMarg{0, 0, 0, 0, cum, bw, q.T / bw}, q.T / dim, fl);
                 } else {
 #define FBN_MARGCALL(Lc, P) vbins<Lc, P>(S, C, D, SeqMarg{0, 0, 0, 0, cum, bw, q.T / bw}, q.T / dim, fl)
@@ -525,6 +607,21 @@ void jt_virt_kernel(
                     }
                     for (int d = 0; d < dim; ++d) o[d] = o[d] / tot;
                 }
+            }
+            if (nf > 0) {
+                double *acc = macc[wv];
+                for (int b = 0; b < nb; ++b) acc[b * 64 + lane] = 0.0;
+                const Den Df = pick(D, Lf);
+                if (mat) {
+                    vmarg_fused<0, true, SP, true>(S, C, D, scr, Df, q.T, nf, fcum, fdim, fbase, acc, lane);
+                } else {
+#define FBN_FUSECALL(Lc, P) vmarg_fused<Lc, P, SP, false>(S, C, D, scr, Df, q.T, nf, fcum, fdim, fbase, acc, lane)
+                    FBN_VDISPATCH(Lf, p32, FBN_FUSECALL);
+#undef FBN_FUSECALL
+                }
+#pragma unroll
+                for (int i = 0; i < kFuseVars; ++i)
+                    if (i < nf) finish(fv[i], [&](int d) { return acc[(fbase[i] + d) * 64 + lane]; });
             }
         };
 
