@@ -255,8 +255,9 @@ def pc_roofline(kernel_s, device_bytes, byte_column_bytes):
     return {**r, "traffic": fab, "valu_frac": valu, "fabric_frac": fabric, **out,
             "dominant_kernel": {top: ks[top]}, "source": "profiles/pc5_kernels.json",
             "note": "all CI kernels of one run: PMC VALU lane-ops and calibrated L2<->fabric bytes per run over the "
-                    "live kernel time; neither bound is reached (bit-sliced kernels: 2-3 waves per SIMD, "
-                    "per-wave reductions; DESIGN.md 5.3)"}
+                    "live kernel time; neither bound is reached: the popcount kernels are bound by v_bcnt issue "
+                    "(half rate on gfx950, tools/micro/valu_rate.hip) and latency, the level-0 Gram is an int8 GEMM "
+                    "on the matrix cores (DESIGN.md 5.3)"}
 
 
 def synth_c5(nvars=N_VARS_C5, nsamples=100_000):
@@ -276,10 +277,11 @@ def bench_pc_synth(steps, depth=6, cpu_vars=160, with_baseline=True):
     N = cols.shape[1]
     ci = F.IndependenceTest(F.Dataset(columns=cols, dims=dims))
     pc = F.PCStable(0.05, depth)
-    pc.StructLearnCompData(ci)  # warm-up (bit-sliced columns built here, once per dataset)
+    pc.StructLearnCompData(ci)  # warm-up: per-dataset stores (bit-sliced / one-hot) and library init
+    pc.StructLearnCompData(ci)  # the kernel time / bytes of a steady-state run
     t, ks = [], []
     h = ctypes.c_void_p()
-    ci.set_kernel_timing(False)  # kernel time / bytes come from the warm-up run above
+    ci.set_kernel_timing(False)  # kernel time / bytes come from the second warm-up run above
     for _ in range(steps):
         t0 = time.perf_counter()
         F.lib.fbn_pc_stable(ci._h, 0.05, depth, 1, ctypes.byref(h))

@@ -44,6 +44,7 @@ extern "C" hipError_t fbn_ci_bits_rowcount(const uint32_t *bits, long long rows,
                                            hipStream_t s);
 extern "C" int fbn_ci_pair_block(int d);
 extern "C" int fbn_ci_gram_task_ints(void);
+extern "C" hipError_t fbn_ci_sum_planes(const int32_t *planes, int np, long long n, int32_t *out, hipStream_t s);
 extern "C" hipError_t fbn_ci_onehot_build(const uint8_t *cols, const int32_t *dims, const int32_t *lead0, long long N,
                                           long long Npad, int nvars, int8_t *out, hipStream_t s);
 extern "C" size_t fbn_ci_l1_edge_bytes(void);
@@ -231,7 +232,7 @@ struct fbn_ci_ctx {
     DevBuf l1items, l1counts, l1df, l1indep, l1tmp;
     DevBuf keptidx, kepttmp;  // level-0 kept pair indices (CiAllPairsKept)
     // level-0 Gram as an int8 library GEMM: one byte per (leading row, sample), rocBLAS handle
-    DevBuf onehot;
+    DevBuf onehot, gram0split;
     int64_t onehot_Npad = 0;
     bool onehot_ready = false, blas_failed = false;
     void *blas = nullptr;
@@ -307,6 +308,12 @@ struct BlasLib {
                               rocblas_datatype, rocblas_int, const void *, const void *, rocblas_datatype, rocblas_int,
                               void *, rocblas_datatype, rocblas_int, rocblas_datatype, rocblas_gemm_algo, int32_t,
                               uint32_t) = nullptr;
+    rocblas_status (*gemm_sb_ex)(rocblas_handle, rocblas_operation, rocblas_operation, rocblas_int, rocblas_int,
+                                 rocblas_int, const void *, const void *, rocblas_datatype, rocblas_int, rocblas_stride,
+                                 const void *, rocblas_datatype, rocblas_int, rocblas_stride, const void *,
+                                 const void *, rocblas_datatype, rocblas_int, rocblas_stride, void *,
+                                 rocblas_datatype, rocblas_int, rocblas_stride, rocblas_int, rocblas_datatype,
+                                 rocblas_gemm_algo, int32_t, uint32_t) = nullptr;
 };
 static BlasLib &Blas() {
     static BlasLib b = [] {
@@ -318,6 +325,7 @@ static BlasLib &Blas() {
         r.destroy = (decltype(r.destroy))dlsym(h, "rocblas_destroy_handle");
         r.set_stream = (decltype(r.set_stream))dlsym(h, "rocblas_set_stream");
         r.gemm_ex = (decltype(r.gemm_ex))dlsym(h, "rocblas_gemm_ex");
+        r.gemm_sb_ex = (decltype(r.gemm_sb_ex))dlsym(h, "rocblas_gemm_strided_batched_ex");
         r.ok = r.create && r.destroy && r.set_stream && r.gemm_ex;
         return r;
     }();
@@ -1184,7 +1192,7 @@ static int CiGram0Tasks(fbn_ci_ctx *c, int64_t t0, int64_t t1, hipStream_t s) {
 constexpr int64_t kOnehotMaxBytes = (int64_t)4 << 30;
 static int CiGram0Blas(fbn_ci_ctx *c, int64_t t0, int64_t n, hipStream_t s, bool *done) {
     *done = false;
-    const int64_t R = (int64_t)c->leadrows_host.size(), Npad = (c->N + 63) & ~(int64_t)63;
+    const int64_t R = (int64_t)c->leadrows_host.size(), Npad = (c->N + 511) & ~(int64_t)511;
     // small Grams (ALARM: 60 rows x 5k samples) stay on the popcount kernel: a library call and the
     // one-hot store cost more than they save there
     if (c->blas_failed || getenv("FBN_CI_GRAM_NO_BLAS") || R * Npad > kOnehotMaxBytes || Npad > INT32_MAX ||
@@ -1228,6 +1236,28 @@ static int CiGram0Blas(fbn_ci_ctx *c, int64_t t0, int64_t n, hipStream_t s, bool
     }
     const int32_t one = 1, zero = 0;
     const int8_t *O = c->onehot.as<int8_t>();
+    // split-K: the 2000 x 2000 output is only 256 tiles of rocBLAS's 128 x 128 for 256 CUs; KS
+    // batches over K slices (strided views of the same operand) into separate int32 planes, then one
+    // summing pass (integers: exact in any order)
+    const int KS = (int)std::max<int64_t>(1, EnvOr0("FBN_CI_GRAM_SPLITK", 4));
+    if (KS > 1 && Blas().gemm_sb_ex && Npad % (64 * KS) == 0) {
+        const int64_t Kc = Npad / KS, m = r1 - r0;
+        int rc2;
+        if ((rc2 = c->gram0split.ensure((size_t)(KS * R * m * 4)))) return rc2;
+        rocblas_status st = Blas().gemm_sb_ex(
+            h, rocblas_operation_transpose, rocblas_operation_none, (rocblas_int)R, (rocblas_int)m, (rocblas_int)Kc,
+            &one, O, rocblas_datatype_i8_r, (rocblas_int)Npad, (rocblas_stride)Kc, O + r0 * Npad,
+            rocblas_datatype_i8_r, (rocblas_int)Npad, (rocblas_stride)Kc, &zero, c->gram0split.as<int32_t>(),
+            rocblas_datatype_i32_r, (rocblas_int)R, (rocblas_stride)(R * m), c->gram0split.as<int32_t>(),
+            rocblas_datatype_i32_r, (rocblas_int)R, (rocblas_stride)(R * m), KS, rocblas_datatype_i32_r,
+            rocblas_gemm_algo_standard, 0, 0);
+        if (st == rocblas_status_success) {
+            hipError_t e = fbn_ci_sum_planes(c->gram0split.as<int32_t>(), KS, R * m, c->gram0.as<int32_t>() + r0 * R, s);
+            if (e != hipSuccess) return SetError(FBN_ERR_HIP, "gram plane sum: %s", hipGetErrorString(e));
+            *done = true;
+            return FBN_OK;
+        }
+    }
     rocblas_status st = Blas().gemm_ex(h, rocblas_operation_transpose, rocblas_operation_none, (rocblas_int)R,
                                        (rocblas_int)(r1 - r0), (rocblas_int)Npad, &one, O, rocblas_datatype_i8_r,
                                        (rocblas_int)Npad, O + r0 * Npad, rocblas_datatype_i8_r, (rocblas_int)Npad,

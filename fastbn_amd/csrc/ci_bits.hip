@@ -1128,6 +1128,43 @@ extern "C" hipError_t fbn_ci_onehot_build(const uint8_t *cols, const int32_t *di
     return hipGetLastError();
 }
 
+// out[i] = sum over np planes of planes[p * n + i] (split-K partial Grams; integers)
+__global__ __launch_bounds__(256) void ci_sum_planes(const int4 *__restrict__ planes, int np, long long n4,
+                                                     int4 *__restrict__ out) {
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+        int4 a = planes[i];
+        for (int p = 1; p < np; ++p) {
+            const int4 b = planes[p * n4 + i];
+            a.x += b.x, a.y += b.y, a.z += b.z, a.w += b.w;
+        }
+        out[i] = a;
+    }
+}
+__global__ __launch_bounds__(256) void ci_sum_planes_tail(const int32_t *__restrict__ planes, int np, long long n,
+                                                          long long from, int32_t *__restrict__ out) {
+    const long long i = from + (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    int32_t a = 0;
+    for (int p = 0; p < np; ++p) a += planes[p * n + i];
+    out[i] = a;
+}
+
+extern "C" hipError_t fbn_ci_sum_planes(const int32_t *planes, int np, long long n, int32_t *out, hipStream_t s) {
+    // the int4 path needs every plane 16-byte aligned: n % 4 == 0 (and 16-byte aligned bases)
+    const bool vec = n % 4 == 0 && ((uintptr_t)planes % 16) == 0 && ((uintptr_t)out % 16) == 0;
+    const long long n4 = vec ? n / 4 : 0;
+    if (n4) {
+        const long long g = (n4 + 255) / 256;
+        hipLaunchKernelGGL(ci_sum_planes, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s,
+                           (const int4 *)planes, np, n4, (int4 *)out);
+    }
+    const long long rest = n - 4 * n4;
+    if (rest > 0)
+        hipLaunchKernelGGL(ci_sum_planes_tail, dim3((unsigned)((rest + 255) / 256)), dim3(256), 0, s, planes, np, n,
+                           4 * n4, out);
+    return hipGetLastError();
+}
+
 extern "C" int fbn_ci_gram_task_ints(void) { return kGramTaskInts; }
 
 extern "C" hipError_t fbn_ci_gram(const uint32_t *bits, long long W, const int32_t *rl, const int32_t *tasks,
