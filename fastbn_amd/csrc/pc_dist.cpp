@@ -34,6 +34,9 @@ struct fbn_pc_dist {
     int depth = 1000, group_size = 1;
     int d = 0;
     bool done = false;
+    // level 0 works on the implicit complete graph (pair index = edge index): edges / adj are built
+    // from the kept pairs after it (or materialized on demand: Complete())
+    bool implicit0 = true;
     std::vector<std::pair<int, int>> edges;
     std::vector<std::vector<int>> adj;
     fbn::PCResultHost res;
@@ -69,8 +72,29 @@ int64_t Get64(const int32_t *p) {
     return v;
 }
 
+// the complete graph's edge list and adjacency (GenerateUndirectedCompleteGraph order,
+// src/Network.cpp:346-358), only when a level-0 path needs them explicitly
+void Complete(fbn_pc_dist *s) {
+    if (!s->implicit0) return;
+    const int n = s->nvars;
+    s->edges.clear();
+    s->edges.reserve((size_t)n * (n - 1) / 2);
+    for (int i = 0; i < n; ++i)
+        for (int j = i + 1; j < n; ++j) s->edges.push_back({i, j});
+    s->adj.assign(n, {});
+    for (int i = 0; i < n; ++i) {
+        s->adj[i].reserve(n - 1);
+        for (int j = 0; j < n; ++j)
+            if (i != j) s->adj[i].push_back(j);
+    }
+    s->implicit0 = false;
+}
+int64_t NumEdges(const fbn_pc_dist *s) {
+    return s->d == 0 && s->implicit0 ? (int64_t)s->nvars * (s->nvars - 1) / 2 : (int64_t)s->edges.size();
+}
+
 int Partition(fbn_pc_dist *s, int world) {
-    const int64_t E = (int64_t)s->edges.size();
+    const int64_t E = NumEdges(s);
     s->cuts.assign(world + 1, E);
     s->cuts[0] = 0;
     if (s->d == 0) {
@@ -92,7 +116,8 @@ int Partition(fbn_pc_dist *s, int world) {
     }
     int64_t maxe = 0;
     for (int r = 0; r < world; ++r) maxe = std::max(maxe, s->cuts[r + 1] - s->cuts[r]);
-    s->rec_len = kHdr + maxe * (1 + s->d);
+    // level 0: one removal bit per pair (32 per int); level d: removal flag + sepset per edge
+    s->rec_len = kHdr + (s->d == 0 ? (maxe + 31) / 32 : maxe * (1 + s->d));
     return FBN_OK;
 }
 
@@ -107,10 +132,18 @@ int Pack(fbn_pc_dist *s, const uint8_t *removed, const int32_t *sep, int64_t cou
     Put64(rec + 4, launched);
     Put64(rec + 6, (int64_t)std::llround(kernel_s * 1e9));  // ns
     int32_t *p = rec + kHdr;
-    for (int64_t e = 0; e < n; ++e) {
-        const bool rm = removed[e] != 0;
-        *p++ = rm ? 1 : 0;
-        for (int j = 0; j < d; ++j) *p++ = rm && sep ? sep[e * d + j] : -1;
+    if (d == 0) {
+        for (int64_t w = 0; w < (n + 31) / 32; ++w) {
+            uint32_t bits = 0;
+            for (int k = 0; k < 32 && 32 * w + k < n; ++k) bits |= (uint32_t)(removed[32 * w + k] != 0) << k;
+            p[w] = (int32_t)bits;
+        }
+    } else {
+        for (int64_t e = 0; e < n; ++e) {
+            const bool rm = removed[e] != 0;
+            *p++ = rm ? 1 : 0;
+            for (int j = 0; j < d; ++j) *p++ = rm && sep ? sep[e * d + j] : -1;
+        }
     }
     s->ran = true;
     return FBN_OK;
@@ -130,16 +163,7 @@ int fbn_pc_dist_create(int nvars, double alpha, int depth, int group_size, fbn_p
     s->depth = depth;
     s->group_size = group_size;
     s->pairs = !getenv("FBN_CI_NO_PAIRS");
-    const int n = nvars;
-    s->edges.reserve((size_t)n * (n - 1) / 2);
-    for (int i = 0; i < n; ++i)  // GenerateUndirectedCompleteGraph order (src/Network.cpp:346-358)
-        for (int j = i + 1; j < n; ++j) s->edges.push_back({i, j});
-    s->adj.assign(n, {});
-    for (int i = 0; i < n; ++i) {
-        s->adj[i].reserve(n - 1);
-        for (int j = 0; j < n; ++j)
-            if (i != j) s->adj[i].push_back(j);
-    }
+    s->adj.assign(nvars, {});
     *out = s.release();
     return FBN_OK;
 }
@@ -165,13 +189,19 @@ int fbn_pc_dist_level(fbn_pc_dist *s, int world, int rank, int *d, int64_t *e_be
 
 int fbn_pc_dist_num_edges(const fbn_pc_dist *s, int64_t *n) {
     if (!s || !n) return SetError(FBN_ERR_ARG, "null pointer");
-    *n = (int64_t)s->edges.size();
+    *n = NumEdges(s);
     return FBN_OK;
 }
 
 int fbn_pc_dist_edges(const fbn_pc_dist *s, int32_t *pairs, int64_t cap) {
     if (!s || (!pairs && cap > 0)) return SetError(FBN_ERR_ARG, "null pointer");
-    const int64_t n = std::min<int64_t>(cap, (int64_t)s->edges.size());
+    const int64_t n = std::min<int64_t>(cap, NumEdges(s));
+    if (s->d == 0 && s->implicit0) {  // the complete graph, decoded
+        int64_t k = 0;
+        for (int i = 0; i < s->nvars && k < n; ++i)
+            for (int j = i + 1; j < s->nvars && k < n; ++j, ++k) pairs[2 * k] = i, pairs[2 * k + 1] = j;
+        return FBN_OK;
+    }
     for (int64_t i = 0; i < n; ++i) pairs[2 * i] = s->edges[i].first, pairs[2 * i + 1] = s->edges[i].second;
     return FBN_OK;
 }
@@ -193,6 +223,27 @@ int fbn_pc_dist_run(fbn_pc_dist *s, fbn_ci_ctx *c, int32_t *record) {
     fbn::LevelOut out;
     fbn::PCResultHost scratch;
     const size_t b = (size_t)s->cuts[s->rank], e = (size_t)s->cuts[s->rank + 1];
+    if (s->d == 0 && s->implicit0) {
+        // the range of the implicit complete graph: all-pairs batches straight into the flags
+        const int32_t *dims = fbn::CiCtxDims(c);
+        fbn::CiBatchStats st{0, 0};
+        for (int v = 0; v < nv; ++v) st.dim_rows += (int64_t)(nv - 1) * dims[v], st.maxdim = std::max(st.maxdim, (int)dims[v]);
+        if (fbn::CiAllPairsEligible(c, st) && !getenv("FBN_CI_NO_IMPLICIT")) {
+            std::vector<uint8_t> rm(e - b);
+            const int64_t chunk = getenv("FBN_PC_L0CHUNK") ? std::max(1ll, atoll(getenv("FBN_PC_L0CHUNK"))) : (1ll << 22);
+            for (int64_t t0 = (int64_t)b; t0 < (int64_t)e; t0 += chunk) {
+                const int64_t m = std::min<int64_t>(chunk, (int64_t)e - t0);
+                if ((rc = fbn::CiBatchLaunchAllPairs(c, s->alpha, &st, t0, m))) return rc;
+                if ((rc = fbn::CiBatchWait(c, 0, rm.data() + (t0 - (int64_t)b), nullptr, scratch))) return rc;
+            }
+            s->res.kernel_s += scratch.kernel_s;
+            s->res.device_bytes += scratch.device_bytes;
+            rc = Pack(s, rm.data(), nullptr, (int64_t)(e - b), (int64_t)(e - b), scratch.kernel_s, record);
+            s->wall_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            return rc;
+        }
+        Complete(s);
+    }
     rc = fbn::RunLevel(c, s->alpha, s->d, s->group_size, s->adj, s->edges, b, e, out, scratch);
     if (rc) return rc;
     s->res.kernel_s += scratch.kernel_s;
@@ -244,10 +295,11 @@ int fbn_pc_dist_apply(fbn_pc_dist *s, const int32_t *records, int *more) {
     if (s->done || s->world == 0) return SetError(FBN_ERR_ARG, "no level in progress (fbn_pc_dist_level)");
     auto t0 = std::chrono::steady_clock::now();
     const int d = s->d, world = s->world;
-    const size_t E = s->edges.size();
+    const size_t E = (size_t)NumEdges(s);
     std::vector<char> rm(E, 0);
     std::vector<int> sep(d > 0 ? E * (size_t)d : 0, -1);
     int64_t counted = 0, launched = 0;
+    std::vector<int64_t> kept;  // level 0: kept pair indices, ascending
     for (int r = 0; r < world; ++r) {
         const int32_t *rec = records + (size_t)r * s->rec_len;
         const int64_t b = s->cuts[r], n = s->cuts[r + 1] - b;
@@ -257,9 +309,22 @@ int fbn_pc_dist_apply(fbn_pc_dist *s, const int32_t *records, int *more) {
         counted += Get64(rec + 2);
         launched += Get64(rec + 4);
         const int32_t *p = rec + kHdr;
+        if (d == 0) {  // removal bits -> flags; kept pair indices collected from the zero bits
+            for (int64_t w = 0; w < (n + 31) / 32; ++w) {
+                const uint32_t bits = (uint32_t)p[w];
+                const int cnt = (int)std::min<int64_t>(32, n - 32 * w);
+                for (int k = 0; k < cnt; ++k) rm[b + 32 * w + k] = (char)((bits >> k) & 1u);
+                uint32_t m = ~bits & (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u));
+                while (m) {
+                    kept.push_back(b + 32 * w + __builtin_ctz(m));
+                    m &= m - 1;
+                }
+            }
+            continue;
+        }
         for (int64_t e = 0; e < n; ++e) {
             rm[b + e] = p[0] != 0;
-            if (d > 0 && p[0])
+            if (p[0])
                 for (int j = 0; j < d; ++j) sep[(b + e) * d + j] = p[1 + j];
             p += 1 + d;
         }
@@ -268,7 +333,21 @@ int fbn_pc_dist_apply(fbn_pc_dist *s, const int32_t *records, int *more) {
     else s->res.sepset.append_level(s->edges.data(), rm.data(), sep.data(), E, d);
     s->res.tests_per_level.push_back(counted);
     s->res.launched_per_level.push_back(launched);
-    fbn::ApplyRemovals(rm, s->edges, s->adj);
+    if (d == 0) {  // the kept pairs of the complete graph, in pair order, become the skeleton
+        const int n = s->nvars;
+        s->edges.resize(kept.size());
+        int i = 0;
+        int64_t row0 = 0, row1 = n - 1;  // pair indices of row i: [row0, row1)
+        for (size_t t = 0; t < kept.size(); ++t) {
+            while (kept[t] >= row1) ++i, row0 = row1, row1 += n - 1 - i;
+            s->edges[t] = {i, i + 1 + (int)(kept[t] - row0)};
+        }
+        s->adj.assign(n, {});
+        for (auto &ed : s->edges) s->adj[ed.first].push_back(ed.second), s->adj[ed.second].push_back(ed.first);
+        s->implicit0 = false;
+    } else {
+        fbn::ApplyRemovals(rm, s->edges, s->adj);
+    }
     if (d == 0 && s->ctx) {
         // level 1 derives from pair tables only if every pair's table is in the ctx
         if (world == 1 && s->pairs) fbn::CiSetPairMode(s->ctx, 2);

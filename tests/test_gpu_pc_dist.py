@@ -104,3 +104,36 @@ def test_config5_full_size_through_session_world1():
     single = F.PCStable(0.05, 6).StructLearnCompData(ci)
     assert launched == single.launched_per_level.tolist()  # same rounds: derived level 1 kept
     assert res.oriented == single.oriented
+
+
+def _worker_c5(rank, world, port, out):
+    import json
+    import torch.distributed as dist
+    from conftest import pc_digest
+    from fastbn_amd import pc_dist, synth
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cols, dims = synth.config5_dataset()  # every rank regenerates the seeded dataset
+    ci = F.IndependenceTest(F.Dataset(columns=cols, dims=dims))
+    res, tests, launched = pc_dist.pc_stable_distributed(ci, 1000, 0.05, 6)
+    if rank == 0:
+        with open(out, "w") as f:
+            json.dump({"tests": tests, **pc_digest(res.edges, res.sepset), "oriented": len(res.oriented)}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_config5_two_ranks_vs_fixture(tmp_path):
+    """BASELINE config 5 at full size on two ranks (the N > 1 path: level-0 pair ranges through the
+    Gram GEMM column slices, pair tables all-gathered, device-resident level-1 search per edge range,
+    one record all-gather per level; gloo carries the exchange, both ranks share the test GPU): the
+    fixture's tests per level, edge list and sepsets."""
+    import json
+    import torch.multiprocessing as mp
+    ref = json.load(open(os.path.join(GOLD, "pc_c5.json")))
+    out = str(tmp_path / "c5.json")
+    mp.start_processes(_worker_c5, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    got = json.load(open(out))
+    assert got["tests"] == ref["tests_per_level"]
+    assert {k: got[k] for k in ("edges_sha256", "sepsets_sha256")} == {k: ref[k] for k in ("edges_sha256", "sepsets_sha256")}
