@@ -1,6 +1,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_pc_dist.py -x -q --timeout 300 --timeout-method thread > gpurun_out/t_pcd.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/t_pcd.log; exit 1; }
-tail -1 gpurun_out/t_pcd.log
-timeout -k 10 200 python tools/pc_dist_timing.py 2>&1 | grep -E "median|^pc level|session"
+bash tools/profile_r02.sh gpurun_out/r02b || exit 1
+python3 tools/pmc_r02.py gpurun_out/r02b > gpurun_out/r02b/pmc_r02b.json || exit 1
+python3 tools/pc5_kernels_json.py gpurun_out/r02b/pmc_r02b.json gpurun_out/r02b/pc5_kernels.json
+tail -c 300 gpurun_out/r02b/stats_bench.json
