@@ -66,6 +66,22 @@ def test_pc_stable_alarm5000(alarm_ds, alarm_paths, gs):
         assert pc.GetSHD(alarm_paths["bif"]) == 5
 
 
+@pytest.mark.parametrize("alpha,device_l1", [(0.001, False), (0.2, False), (0.2, True), (0.0, True)])
+def test_pc_stable_alarm5000_other_alphas(alarm_ds, alarm_paths, alpha, device_l1, monkeypatch):
+    """Decisions at other significance levels (depth 3): the decision band (ci_chisq.h
+    fbn_chisq_band) is built per alpha (none at alpha 0: p evaluated for every test); device_l1
+    forces the device-resident level-1 search.  Counts, skeleton and sepsets equal the
+    restatement's."""
+    od = O.OracleDataset(csv=alarm_paths["csv"])
+    ref = od.pc_stable(alpha, 3, 1)
+    if device_l1:
+        monkeypatch.setenv("FBN_PC_FULLSPEC", "0")
+    pc = F.PCStable(alpha, 3).StructLearnCompData(alarm_ds)
+    assert pc.tests_per_level.tolist() == ref["tests_per_level"]
+    assert pc.edges == ref["edges"]
+    assert pc.sepset == ref["sepset"]
+
+
 @pytest.mark.parametrize("gs,staged", [(1, False), (3, False), (1, True)])
 def test_pc_stable_alarm5000_pipelined_rounds(alarm_ds, alarm_paths, gs, staged, monkeypatch):
     """The driver's multi-round path (no full speculation) with the level's edges in two halves

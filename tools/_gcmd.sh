@@ -1,7 +1,4 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-bash tools/profile_r02.sh gpurun_out/r02b || exit 1
-python3 tools/pmc_r02.py gpurun_out/r02b > gpurun_out/r02b/pmc_r02b.json || exit 1
-python3 tools/pc5_kernels_json.py gpurun_out/r02b/pmc_r02b.json gpurun_out/r02b/pc5_kernels.json
-tail -c 300 gpurun_out/r02b/stats_bench.json
+timeout -k 10 300 python -u -m pytest tests/test_gpu_pc.py -x -v --timeout 120 --timeout-method thread -k "alpha" 2>&1 | tee gpurun_out/t_pc.log | grep -E "PASS|FAIL|ERROR|passed|failed"
