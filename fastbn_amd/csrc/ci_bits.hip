@@ -798,13 +798,22 @@ __global__ __launch_bounds__(256) void ci_bits_g2(const int32_t *__restrict__ co
                     for (int i = 0; i < dx; ++i) {
                         const long sum_row = ni[i];
                         if (sum_row == 0) continue;
-                        for (int j = 0; j < dy; ++j) {
-                            const long sum_col = nj[j];
-                            const long observed = h[i * dy + j];
-                            if (sum_col == 0 || observed == 0) continue;
-                            const double expected = (double)sum_col * (double)sum_row / (double)total;
-                            g2 += 2.0 * observed * log(observed / expected);
+                        // the row's terms are independent: evaluate all four side by side (one latency
+                        // chain instead of dy), then add the present ones in the reference's order
+                        double tm[4];
+                        bool on[4];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const long sum_col = j < dy ? nj[j] : 0;
+                            const long observed = j < dy ? h[i * dy + j] : 0;
+                            on[j] = sum_col != 0 && observed != 0;
+                            const long o1 = on[j] ? observed : 1, c1 = on[j] ? sum_col : 1;
+                            const double expected = (double)c1 * (double)sum_row / (double)total;
+                            tm[j] = 2.0 * o1 * log(o1 / expected);
                         }
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (on[j]) g2 += tm[j];
                     }
                 }
             }

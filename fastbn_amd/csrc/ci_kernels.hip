@@ -260,21 +260,71 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
             nk[k] = total;
         }
         __syncthreads();
+        // decision-only batches (no G^2 / p returned, band present): the terms summed as a block tree
+        // first.  Tree and in-order sums of the same terms differ by at most (cells + 64) u sum|t|, so
+        // a tree sum that clears the band [lo, hi] by that much decides exactly as the reference's
+        // ordered sum would; only the rest (near the band, or df past it) add in order below.
+        auto term_of = [&](int c) {
+            const int k = c / dxy, i = (c / dy) % dx, j = c % dy;
+            const long total = nk[k], sum_row = ni[k * dx + i], sum_col = nj[k * dy + j], observed = hist[c];
+            double t = 0.0;
+            if (total != 0 && sum_row != 0 && sum_col != 0 && observed != 0) {
+                const double expected = (double)sum_col * (double)sum_row / (double)total;
+                t = 2.0 * observed * log(observed / expected);
+            }
+            return t;
+        };
+        __shared__ double sred[8];
+        __shared__ int sdf[4], sdec;
+        if (!A.p && !A.g2 && A.band) {
+            double ps = 0.0, pa = 0.0;
+            int pdf = 0;
+            for (int c = tid; c < cells; c += 256) {
+                const double t = term_of(c);
+                ps += t;
+                pa += fabs(t);
+            }
+            for (int k = tid; k < dimz; k += 256) pdf += dfp[k];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+                ps += __shfl_xor(ps, o);
+                pa += __shfl_xor(pa, o);
+                pdf += __shfl_xor(pdf, o);
+            }
+            if (lane == 0) sred[2 * (tid >> 6)] = ps, sred[2 * (tid >> 6) + 1] = pa, sdf[tid >> 6] = pdf;
+            __syncthreads();
+            if (tid == 0) {
+                const double gs = (sred[0] + sred[2]) + (sred[4] + sred[6]);
+                const double ga = (sred[1] + sred[3]) + (sred[5] + sred[7]);
+                const int df = sdf[0] + sdf[1] + sdf[2] + sdf[3];
+                const double err = (cells + 64) * 2.3e-16 * ga;
+                int dec = -1;  // 0 dependent, 1 independent, -1 in-order sum
+                if (df == 0) dec = 1;  // src/IndependenceTest.cpp:140-142
+                else if (df <= A.nband && gs + err < A.band[2 * df - 2]) dec = 1;
+                else if (df <= A.nband && gs - err > A.band[2 * df - 1]) dec = 0;
+                if (dec >= 0) {
+                    const double p = df == 0 ? 1.0 : dec ? A.alpha + A.band[2 * A.nband] : A.alpha - A.band[2 * A.nband];
+                    if (A.df) A.df[it] = df;
+                    if (A.indep) A.indep[it] = dec;
+                    if (A.stats) {
+                        const double m = fabs(p - A.alpha);
+                        atomicMin(A.stats, (unsigned long long)__double_as_longlong(m));
+                        if (m < 1e-9) atomicAdd(A.stats + 1, 1ull);
+                    }
+                }
+                sdec = dec;
+            }
+            __syncthreads();
+            const bool done = sdec >= 0;
+            __syncthreads();  // sdec / sred reused by the next test
+            if (done) continue;
+        }
         // G^2: the terms of a chunk of cells in parallel (cell c = (k * dx + i) * dy + j, the
         // reference's loop order), then one lane adds them in order (src/IndependenceTest.cpp:112-137)
         double g2 = 0.0;
         for (int c0 = 0; c0 < cells; c0 += tc) {
             const int c1 = c0 + tc < cells ? c0 + tc : cells;
-            for (int c = c0 + tid; c < c1; c += 256) {
-                const int k = c / dxy, i = (c / dy) % dx, j = c % dy;
-                const long total = nk[k], sum_row = ni[k * dx + i], sum_col = nj[k * dy + j], observed = hist[c];
-                double t = 0.0;
-                if (total != 0 && sum_row != 0 && sum_col != 0 && observed != 0) {
-                    const double expected = (double)sum_col * (double)sum_row / (double)total;
-                    t = 2.0 * observed * log(observed / expected);
-                }
-                term[c - c0] = t;
-            }
+            for (int c = c0 + tid; c < c1; c += 256) term[c - c0] = term_of(c);
             __syncthreads();
             if (tid == 0) {  // loads batched ahead of the dependent adds (LDS latency off the chain)
                 const int m = c1 - c0;
