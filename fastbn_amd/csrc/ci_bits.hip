@@ -770,51 +770,60 @@ __global__ __launch_bounds__(256) void ci_bits_g2(const int32_t *__restrict__ co
             const int dimz = D == 1 ? dims[items[3 * t + 2]] : 1;
             const int dxy = dx * dy;
             const int32_t *hz = counts + t * kBitsCells;
+            // the record unpacked into a fixed KZ x 4 x 4 register table (absent cells 0): every load
+            // is independent (one memory latency per test, not one per loop step) and every index
+            // below is static.  Absent rows / columns / z values have zero counts, so they add
+            // nothing to df (max(0, 1) - 1 = 0) or G^2 (their terms are skipped) -- the sums are the
+            // reference's over the real table, in its order.
+            constexpr int KZ = D == 1 ? 4 : 1;
+            int h[KZ][4][4];
+#pragma unroll
+            for (int k = 0; k < KZ; ++k)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const bool in = k < dimz && i < dx && j < dy;
+                        const int v = hz[in ? k * dxy + i * dy + j : 0];
+                        h[k][i][j] = in ? v : 0;
+                    }
             // one running sum over z -> x -> y, exactly the reference's loop (no per-z partials)
             double g2 = 0.0;
             int df = 0;
-            for (int k = 0; k < dimz; ++k) {
-                const int32_t *h = hz + k * dxy;
-                int ni[4], nj[4];
+#pragma unroll
+            for (int k = 0; k < KZ; ++k) {
+                int ni[4], nj[4], alx = 0, aly = 0;
                 long total = 0;
-                int alx = 0, aly = 0;
-                for (int i = 0; i < dx; ++i) {
-                    int s = 0;
-                    for (int j = 0; j < dy; ++j) s += h[i * dy + j];
-                    ni[i] = s;
-                    alx += s > 0;
-                    total += s;
-                }
-                for (int j = 0; j < dy; ++j) {
-                    int s = 0;
-                    for (int i = 0; i < dx; ++i) s += h[i * dy + j];
-                    nj[j] = s;
-                    aly += s > 0;
-                }
-                alx = alx >= 1 ? alx : 1;
-                aly = aly >= 1 ? aly : 1;
-                df += (alx - 1) * (aly - 1);
-                if (total != 0) {
-                    for (int i = 0; i < dx; ++i) {
-                        const long sum_row = ni[i];
-                        if (sum_row == 0) continue;
-                        // the row's terms are independent: evaluate all four side by side (one latency
-                        // chain instead of dy), then add the present ones in the reference's order
-                        double tm[4];
-                        bool on[4];
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const long sum_col = j < dy ? nj[j] : 0;
-                            const long observed = j < dy ? h[i * dy + j] : 0;
-                            on[j] = sum_col != 0 && observed != 0;
-                            const long o1 = on[j] ? observed : 1, c1 = on[j] ? sum_col : 1;
-                            const double expected = (double)c1 * (double)sum_row / (double)total;
-                            tm[j] = 2.0 * o1 * log(o1 / expected);
-                        }
+                for (int i = 0; i < 4; ++i) {
+                    ni[i] = (h[k][i][0] + h[k][i][1]) + (h[k][i][2] + h[k][i][3]);
+                    alx += ni[i] > 0;
+                    total += ni[i];
+                }
 #pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            if (on[j]) g2 += tm[j];
+                for (int j = 0; j < 4; ++j) {
+                    nj[j] = (h[k][0][j] + h[k][1][j]) + (h[k][2][j] + h[k][3][j]);
+                    aly += nj[j] > 0;
+                }
+                df += ((alx >= 1 ? alx : 1) - 1) * ((aly >= 1 ? aly : 1) - 1);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const long sum_row = ni[i];
+                    if (total == 0 || sum_row == 0) continue;
+                    // the row's four terms side by side (independent latency chains), then the present
+                    // ones added in order
+                    double tm[4];
+                    bool on[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        on[j] = nj[j] != 0 && h[k][i][j] != 0;
+                        const long o1 = on[j] ? h[k][i][j] : 1, c1 = on[j] ? nj[j] : 1;
+                        const double expected = (double)c1 * (double)sum_row / (double)total;
+                        tm[j] = 2.0 * o1 * log(o1 / expected);
                     }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (on[j]) g2 += tm[j];
                 }
             }
             double p = 1.0, m;
