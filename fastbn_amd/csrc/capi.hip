@@ -270,7 +270,7 @@ static int64_t EnvOr0(const char *name, int64_t dflt) {
 constexpr int kBandDf = 36;
 constexpr int kBandDfMax = 256;  // larger df (few tests, deep levels): p evaluated
 
-// the band for `alpha` (delta = alpha / 4) over df 1..max(want_df, kBandDf) (at most kBandDfMax),
+// the band for `alpha` (delta = alpha / 1024: few tests fall inside, so few evaluate p) over df 1..max(want_df, kBandDf) (at most kBandDfMax),
 // computed on the host per ctx and alpha and extended on demand; *out = nullptr (p evaluated for
 // every test) when alpha is outside (0, 1) or FBN_CI_NO_BAND is set
 static int CiBand(fbn_ci_ctx *c, double alpha, hipStream_t s, const double **out, int *nband, int want_df = 0) {
@@ -279,7 +279,7 @@ static int CiBand(fbn_ci_ctx *c, double alpha, hipStream_t s, const double **out
     if (!(alpha > 0.0 && alpha < 1.0) || getenv("FBN_CI_NO_BAND")) return FBN_OK;
     const int want = std::min(kBandDfMax, std::max(kBandDf, want_df));
     if (c->band_alpha != alpha || c->band_n < want) {
-        const double delta = alpha / 4;
+        const double delta = alpha / 1024;
         const int have = c->band_alpha == alpha ? c->band_n : 0;
         FBN_HIP(hipStreamSynchronize(s));  // the previous upload of the host table has completed
         c->band_host.resize(2 * (size_t)want + 1);
