@@ -276,3 +276,23 @@ def test_libsvm_writer_and_streaming_loader(alarm_paths, tmp_path, monkeypatch):
     oe, ol = O.load_libsvm(alarm_paths["test"], 37)
     np.testing.assert_array_equal(e4, oe)
     np.testing.assert_array_equal(l4, ol)
+
+
+def test_host_threads_under_tsan(alarm_paths, tmp_path):
+    """SURVEY §5 race detection: the threaded host code (forward sampling, evidence generation, the
+    chunked CSV / LIBSVM writers and the block-parallel parsers) built with ThreadSanitizer from its
+    sources (g++ -fsanitize=thread, no HIP) and round-tripped on ALARM; any report fails the run."""
+    import shutil
+    import subprocess
+    if not shutil.which("g++"):
+        pytest.skip("g++ not available")
+    csrc = os.path.join(REPO, "fastbn_amd", "csrc")
+    exe = str(tmp_path / "host_tsan")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-I" + os.path.join(REPO, "include"),
+                    os.path.join(csrc, "io.cpp"), os.path.join(csrc, "synth.cpp"),
+                    os.path.join(REPO, "tests", "tsan", "host_tsan.cpp"), "-o", exe], check=True)
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66")
+    r = subprocess.run([exe, alarm_paths["xml"], str(tmp_path)], capture_output=True, text=True, env=env,
+                       timeout=600)
+    assert r.returncode == 0 and "ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
+    assert "host_tsan ok" in r.stdout
