@@ -740,7 +740,7 @@ __global__ __launch_bounds__(256) void ci_bits_gram_triples(
     }
 }
 
-// phase 2: one lane per test -- per z: marginals, adjusted df; G^2 as one running sum in the
+// phase 2, large launches (ci_bits_g2): one lane per test -- per z: marginals, adjusted df; G^2 as one running sum in the
 // reference's z -> x -> y order (ComputeGSquareXY / XYZ, src/IndependenceTest.cpp:65-155,
 // 295-364; the same arithmetic as ci_g2_kernel), p = 1 - P(df/2, G^2/2) (ci_chisq.h).  With no p
 // output and a decision band (band != nullptr: [lo, hi] per df 1..nband, then delta), p is only
@@ -857,6 +857,165 @@ __global__ __launch_bounds__(256) void ci_bits_g2(const int32_t *__restrict__ co
             }
             const unsigned long long nn = __popcll(__ballot(near));
             if ((threadIdx.x & 63) == 0) {
+                if (mbits != ~0ull) atomicMin(stats, mbits);
+                if (nn) atomicAdd(stats + 1, nn);
+            }
+        }
+    }
+}
+
+// phase 2, small launches (ci_bits_g2q): four lanes per test -- marginals, adjusted df; G^2 as one running sum in the reference's
+// z -> x -> y order (ComputeGSquareXY / XYZ, src/IndependenceTest.cpp:65-155, 295-364; the same
+// arithmetic as ci_g2_kernel), p = 1 - P(df/2, G^2/2) (ci_chisq.h).  Lane q of a test's group owns z
+// value q (D = 1: a 4 x 4 slice) or x value q (D = 0: a row of 4): it unpacks its part of the 256-B
+// count record into a zero-padded register table (independent loads, static indices; absent rows,
+// columns and z values add nothing to df or G^2), evaluates its terms -- the costly part, a division
+// chain and a log each -- in parallel with the other three lanes, and then the four lanes add
+// their terms into the one running sum in turn.  With no p output and a decision band (band !=
+// nullptr: [lo, hi] per df 1..nband, then delta), p is only evaluated for G^2 inside the band
+// (fbn_chisq_band).  The margin log is reduced per wave (one atomic per wave, not per test).
+constexpr int kG2Lanes = 4;
+constexpr int kG2TestsPerBlock = 256 / kG2Lanes;
+constexpr long long kG2QuadMax = 16384;  // launches of at most this many tests use ci_bits_g2q
+template <int D>
+__global__ __launch_bounds__(256) void ci_bits_g2q(const int32_t *__restrict__ counts, const int32_t *__restrict__ dims,
+                                                  const int32_t *__restrict__ items, long long n, double alpha,
+                                                  double *__restrict__ g2o, int32_t *__restrict__ dfo,
+                                                  double *__restrict__ po, uint8_t *__restrict__ indep,
+                                                  int32_t *__restrict__ counts0, unsigned long long *__restrict__ stats,
+                                                  int nvars, long long t0, const double *__restrict__ band,
+                                                  int nband, const long long *__restrict__ n_dev) {
+    if (n_dev) n = *n_dev;
+    const int lane = threadIdx.x & 63, q = lane & (kG2Lanes - 1), g0 = lane & ~(kG2Lanes - 1);
+    const long long stride = (long long)gridDim.x * kG2TestsPerBlock;
+    // wave-uniform trip count (the shuffles and the margin reduction are whole-wave operations)
+    for (long long wb = (long long)blockIdx.x * kG2TestsPerBlock + (threadIdx.x >> 6) * (64 / kG2Lanes); wb < n;
+         wb += stride) {
+        const long long t = wb + lane / kG2Lanes;
+        const bool live = t < n;
+        int px = 0, py = 0, pz = 0;
+        if (live) {
+            if (D == 0 && !items) pair_of(t0 + t, nvars, px, py);
+            else px = items[(2 + D) * t], py = items[(2 + D) * t + 1];
+            if (D == 1) pz = items[3 * t + 2];
+        }
+        const int dx = live ? dims[px] : 1, dy = live ? dims[py] : 1;
+        const int dimz = D == 1 && live ? dims[pz] : 1;
+        const int dxy = dx * dy;
+        const int32_t *hz = counts + (live ? t : 0) * kBitsCells;
+        constexpr int NR = D == 1 ? 4 : 1;  // rows this lane owns
+        int h[NR][4];
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int k = D == 1 ? q : 0, i = D == 1 ? r : q;
+                const bool in = live && k < dimz && i < dx && j < dy;
+                const int v = hz[in ? k * dxy + i * dy + j : 0];
+                h[r][j] = in ? v : 0;
+            }
+        // this lane's slice (D = 1) or the test's only slice (D = 0): marginals, total, df
+        int ni[NR], nj[4], df;
+        long total = 0;
+        {
+            int alx = 0, aly = 0;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                ni[r] = (h[r][0] + h[r][1]) + (h[r][2] + h[r][3]);
+                alx += ni[r] > 0;
+                total += ni[r];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                int c = 0;
+#pragma unroll
+                for (int r = 0; r < NR; ++r) c += h[r][j];
+                nj[j] = c;
+            }
+            if (D == 0) {  // the slice's rows are spread over the group
+#pragma unroll
+                for (int o = 1; o < kG2Lanes; o <<= 1) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) nj[j] += __shfl_xor(nj[j], o);
+                    alx += __shfl_xor(alx, o);
+                    total += __shfl_xor(total, o);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) aly += nj[j] > 0;
+            df = ((alx >= 1 ? alx : 1) - 1) * ((aly >= 1 ? aly : 1) - 1);
+            if (D == 1)
+#pragma unroll
+                for (int o = 1; o < kG2Lanes; o <<= 1) df += __shfl_xor(df, o);
+        }
+        // this lane's terms, side by side (independent latency chains)
+        double tm[NR][4];
+        bool on[NR][4];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const long sum_row = ni[r];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                on[r][j] = total != 0 && sum_row != 0 && nj[j] != 0 && h[r][j] != 0;
+                tm[r][j] = 0.0;
+            }
+            if (total != 0 && sum_row != 0) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const long o1 = on[r][j] ? h[r][j] : 1, c1 = on[r][j] ? nj[j] : 1;
+                    const double expected = (double)c1 * (double)sum_row / (double)total;
+                    tm[r][j] = 2.0 * o1 * log(o1 / expected);
+                }
+            }
+        }
+        // the running sum, lane 0's cells first: z (D = 1) or x (D = 0) is the group's outer digit
+        double g2 = 0.0;
+#pragma unroll
+        for (int s = 0; s < kG2Lanes; ++s) {
+            if (q == s)
+#pragma unroll
+                for (int r = 0; r < NR; ++r)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (on[r][j]) g2 += tm[r][j];
+            g2 = __shfl(g2, g0 + s);
+        }
+        unsigned long long mbits = ~0ull;  // this test's |p - alpha| (as ordered bits), none = max
+        bool near = false;
+        if (live) {
+            double p = 1.0, m;
+            bool ind;
+            if (df == 0) {  // src/IndependenceTest.cpp:149-151, 349-351
+                ind = true;
+                m = fabs(p - alpha);
+            } else if (!po && band && df <= nband && g2 < band[2 * df - 2]) {
+                ind = true, m = band[2 * nband];  // p > alpha + delta
+            } else if (!po && band && df <= nband && g2 > band[2 * df - 1]) {
+                ind = false, m = band[2 * nband];  // p < alpha - delta
+            } else {
+                p = fbn_chisq_pvalue(g2, df);
+                ind = p > alpha;
+                m = fabs(p - alpha);
+            }
+            if (q == 0) {
+                if (g2o) g2o[t] = g2;
+                dfo[t] = df;
+                if (po) po[t] = p;
+                indep[t] = ind;
+                if (counts0 && t == 0)
+                    for (int c = 0; c < dimz * dxy; ++c) counts0[c] = hz[c];
+                mbits = (unsigned long long)__double_as_longlong(m);
+                near = m < 1e-9;
+            }
+        }
+        if (stats) {
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+                const unsigned long long v = __shfl_xor(mbits, o);
+                mbits = v < mbits ? v : mbits;
+            }
+            const unsigned long long nn = __popcll(__ballot(near));
+            if (lane == 0) {
                 if (mbits != ~0ull) atomicMin(stats, mbits);
                 if (nn) atomicAdd(stats + 1, nn);
             }
@@ -1224,14 +1383,17 @@ extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *di
                                          int32_t *pairtab, int pmode, int nvars, int num_cu, long long t0,
                                          int counted, const double *band, int nband, hipStream_t s) {
     const long long g1 = (n + 3) / 4, cap = (long long)num_cu * 8;
-    const long long g2g = (n + 255) / 256;
+    // launches too small to fill the chip with a lane per test (ALARM's 8.7k level-1 tests: 137
+    // waves on 1024 SIMDs) take four lanes per test, which cuts each test's latency chain ~4x
+    const bool quad = n <= kG2QuadMax;
+    const long long g2g = quad ? (n + kG2TestsPerBlock - 1) / kG2TestsPerBlock : (n + 255) / 256;
     const dim3 b1((unsigned)(g1 < cap ? g1 : cap)), b2((unsigned)(g2g < cap ? g2g : cap));
     if (d == 0) {
         if (!counted)  // counted = 1: the counts are already in place (ci_bits_pairs_tiled)
             hipLaunchKernelGGL(ci_bits_count<0>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts, rowcnt,
                                pmode == 1 ? pairtab : nullptr, nvars, t0);
-        hipLaunchKernelGGL(ci_bits_g2<0>, b2, dim3(256), 0, s, counts, dims, items, n, alpha, g2, df, p, indep,
-                           counts0, stats, nvars, t0, band, nband, (const long long *)nullptr);
+        hipLaunchKernelGGL((quad ? ci_bits_g2q<0> : ci_bits_g2<0>), b2, dim3(256), 0, s, counts, dims, items, n,
+                           alpha, g2, df, p, indep, counts0, stats, nvars, t0, band, nband, (const long long *)nullptr);
     } else if (d == 1) {
         // FBN_CI_L1MODE = 0: plain grid stride instead of the XCD-contiguous split
         static const int l1mode = getenv("FBN_CI_L1MODE") ? atoi(getenv("FBN_CI_L1MODE")) : 1;
@@ -1244,8 +1406,8 @@ extern "C" hipError_t fbn_ci_bits_launch(const uint32_t *bits, const int32_t *di
         else
             hipLaunchKernelGGL(ci_bits_count<1>, b1, dim3(256), 0, s, bits, dims, row0, items, W, n, counts, rowcnt,
                                nullptr, nvars, 0ll);
-        hipLaunchKernelGGL(ci_bits_g2<1>, b2, dim3(256), 0, s, counts, dims, items, n, alpha, g2, df, p, indep,
-                           counts0, stats, nvars, 0ll, band, nband, (const long long *)nullptr);
+        hipLaunchKernelGGL((quad ? ci_bits_g2q<1> : ci_bits_g2<1>), b2, dim3(256), 0, s, counts, dims, items, n,
+                           alpha, g2, df, p, indep, counts0, stats, nvars, 0ll, band, nband, (const long long *)nullptr);
     } else {
         return hipErrorInvalidValue;
     }
