@@ -238,6 +238,7 @@ struct fbn_ci_ctx {
     void *blas = nullptr;
     int *h_kept = nullptr;
     unsigned *h_open = nullptr;
+    unsigned long long *h_margin = nullptr;  // pinned: reset value, read-back (CiResetMargin)
     hipEvent_t l1ev[2] = {nullptr, nullptr};
     // decision band of the bit-sliced G^2 kernel for alpha = band_alpha (ci_chisq.h fbn_chisq_band):
     // [lo, hi] per df 1..kBandDf, then delta; host copy kept alive for the async upload
@@ -254,6 +255,7 @@ struct fbn_ci_ctx {
     ~fbn_ci_ctx();
     void destroy_() {
         if (h_open) (void)hipHostFree(h_open);
+        if (h_margin) (void)hipHostFree(h_margin);
         if (h_kept) (void)hipHostFree(h_kept);
         for (auto &e : l1ev)
             if (e) (void)hipEventDestroy(e);
@@ -348,21 +350,34 @@ static int PinnedEnsure(void *&ptr, size_t &have, size_t want) {
     return FBN_OK;
 }
 
-static int CiResetMargin(fbn_ci_ctx *c) {
-    const unsigned long long init[2] = {0x7FF0000000000000ull /* +inf */, 0};
-    FBN_HIP(hipDeviceSynchronize());
-    FBN_HIP(hipMemcpy(c->stats.p, init, 16, hipMemcpyHostToDevice));
+// The margin log lives on the device (atomics of every batch kernel); reset and read are
+// stream-ordered copies through a pinned 32-byte buffer ([0..1] the reset value, constant; [2..3]
+// the read-back).  Work the caller queued on its own streams (fbn_ci_run_device) is drained first.
+static int CiMarginPinned(fbn_ci_ctx *c) {
+    if (c->h_margin) return FBN_OK;
+    hipError_t e = hipHostMalloc((void **)&c->h_margin, 32, hipHostMallocDefault);
+    if (e != hipSuccess) return SetError(FBN_ERR_NOMEM, "hipHostMalloc: %s", hipGetErrorString(e));
+    c->h_margin[0] = 0x7FF0000000000000ull;  // +inf
+    c->h_margin[1] = 0;
     return FBN_OK;
 }
 
-static int CiReadMargin(fbn_ci_ctx *c, double *min_margin, int64_t *near_alpha) {
-    unsigned long long h[2];
+static int CiResetMargin(fbn_ci_ctx *c) {
+    if (int rc = CiMarginPinned(c)) return rc;
     FBN_HIP(hipDeviceSynchronize());
-    FBN_HIP(hipMemcpy(h, c->stats.p, 16, hipMemcpyDeviceToHost));
+    FBN_HIP(hipMemcpyAsync(c->stats.p, c->h_margin, 16, hipMemcpyHostToDevice, c->stream));
+    return FBN_OK;
+}
+
+static int CiReadMargin(fbn_ci_ctx *c, double *min_margin, int64_t *near_alpha, bool own_stream_only = false) {
+    if (int rc = CiMarginPinned(c)) return rc;
+    if (!own_stream_only) FBN_HIP(hipDeviceSynchronize());
+    FBN_HIP(hipMemcpyAsync(c->h_margin + 2, c->stats.p, 16, hipMemcpyDeviceToHost, c->stream));
+    FBN_HIP(hipStreamSynchronize(c->stream));
     double m;
-    memcpy(&m, &h[0], 8);
+    memcpy(&m, &c->h_margin[2], 8);
     if (min_margin) *min_margin = m;
-    if (near_alpha) *near_alpha = (int64_t)h[1];
+    if (near_alpha) *near_alpha = (int64_t)c->h_margin[3];
     return FBN_OK;
 }
 
@@ -1542,7 +1557,8 @@ int fbn_pc_stable(fbn_ci_ctx *c, double alpha, int depth, int group_size, fbn_pc
     auto t1 = std::chrono::steady_clock::now();
     if ((rc = fbn::RunPCStable(c, alpha, depth, group_size, r->r))) return rc;
     auto t2 = std::chrono::steady_clock::now();
-    if ((rc = CiReadMargin(c, &r->r.min_margin, &r->r.near_alpha))) return rc;
+    // the run's work is all on the ctx stream
+    if ((rc = CiReadMargin(c, &r->r.min_margin, &r->r.near_alpha, true))) return rc;
     auto t3 = std::chrono::steady_clock::now();
     if ((rc = fbn::OrientPC(c->nvars, r->r))) return rc;  // StructLearnByPCStable steps 2-3
     if (timing) {

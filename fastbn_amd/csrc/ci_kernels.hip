@@ -184,23 +184,32 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
             }
         };
         const long long N4 = (A.N % 4 == 0) ? A.N / 4 : 0;
-        for (long long k4 = tid; k4 < ((N4 + 255) / 256) * 256; k4 += 256) {
-            const bool v4 = k4 < N4;
-            uint32_t wx = 0, wy = 0, wz[D > 0 ? D : 1];
-            if (v4) {
-                wx = reinterpret_cast<const uint32_t *>(cx)[k4];
-                wy = reinterpret_cast<const uint32_t *>(cy)[k4];
+        // kU words per column in flight per thread: one memory latency per kU steps, not per step
+        constexpr int kU = 4;
+        for (long long kb = tid; kb < N4; kb += 256 * kU) {
+            uint32_t wx[kU], wy[kU], wz[kU][D > 0 ? D : 1];
+            bool v4[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const long long k4 = kb + u * 256;
+                v4[u] = k4 < N4;
+                const long long kk = v4[u] ? k4 : 0;
+                wx[u] = reinterpret_cast<const uint32_t *>(cx)[kk];
+                wy[u] = reinterpret_cast<const uint32_t *>(cy)[kk];
+#pragma unroll
+                for (int j = 0; j < D; ++j) wz[u][j] = reinterpret_cast<const uint32_t *>(cz[j])[kk];
             }
 #pragma unroll
-            for (int j = 0; j < D; ++j) wz[j] = v4 ? reinterpret_cast<const uint32_t *>(cz[j])[k4] : 0u;
+            for (int u = 0; u < kU; ++u)
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                int zi = 0;
+                for (int s = 0; s < 4; ++s) {
+                    int zi = 0;
 #pragma unroll
-                for (int j = 0; j < D; ++j) zi += (int)((wz[j] >> (8 * s)) & 0xFF) * cum[j];
-                const int cell = (zi * dx + (int)((wx >> (8 * s)) & 0xFF)) * dy + (int)((wy >> (8 * s)) & 0xFF);
-                bin(cell, v4);
-            }
+                    for (int j = 0; j < D; ++j) zi += (int)((wz[u][j] >> (8 * s)) & 0xFF) * cum[j];
+                    const int cell =
+                        (zi * dx + (int)((wx[u] >> (8 * s)) & 0xFF)) * dy + (int)((wy[u] >> (8 * s)) & 0xFF);
+                    bin(v4[u] ? cell : 0, v4[u]);
+                }
         }
         for (long long k = 4 * N4 + tid; k < ((A.N - 4 * N4 + 255) / 256) * 256 + 4 * N4; k += 256) {
             const bool v = k < A.N;

@@ -5,6 +5,7 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_pc.py tests/test_gpu_pc_dis
 tail -1 gpurun_out/t_pc.log
 echo "default"; timeout -k 10 120 python tools/pc5_timing.py 5 2>&1 | grep -E "run " | tail -1
 timeout -k 10 120 python tools/pc_alarm_timing.py 2>&1 | tail -1
+FBN_CI_BITSN=1 timeout -k 10 120 python tools/pc_alarm_timing.py 2>&1 | tail -1
 mkdir -p gpurun_out/gl
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/gl -o run --output-format csv -- python tools/pc5_timing.py 3 > /dev/null 2>&1 || exit 1
 python3 -c "
