@@ -268,6 +268,18 @@ static int64_t EnvOr0(const char *name, int64_t dflt) {
     return v ? atoll(v) : dflt;
 }
 
+// Wait for a PC round's event by polling it from this thread (a PC level is a chain of short
+// rounds: polling avoids the blocking wait's wake-up latency on every round trip).
+// FBN_CI_SPIN = 0 restores hipEventSynchronize.
+static hipError_t EventWaitSpin(hipEvent_t ev) {
+    static const bool spin = EnvOr0("FBN_CI_SPIN", 1) != 0;
+    if (!spin) return hipEventSynchronize(ev);
+    hipError_t e;
+    while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
+    }
+    return e;
+}
+
 // df <= 36 covers every bit-sliced test (<= 4 states, <= 1 conditioning variable: 4 * 3 * 3)
 constexpr int kBandDf = 36;
 constexpr int kBandDfMax = 256;  // larger df (few tests, deep levels): p evaluated
@@ -1900,7 +1912,7 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
         FBN_HIP(hipMemcpyAsync(c->h_open + r, c->l1open.as<unsigned>() + r, 4, hipMemcpyDeviceToHost, s));
         FBN_HIP(hipEventRecord(c->l1ev[r & 1], s));
         if (r >= 1) {  // round r - 1's open count, while round r runs
-            FBN_HIP(hipEventSynchronize(c->l1ev[(r - 1) & 1]));
+            FBN_HIP(EventWaitSpin(c->l1ev[(r - 1) & 1]));
             if (c->h_open[r - 1] == 0) break;  // round r found nothing to do
         }
         chunk = std::min<int64_t>(chunk * growth, 1 << 16);
@@ -2052,7 +2064,7 @@ int CiBatchWait(fbn_ci_ctx *c, int k, uint8_t *indep, int32_t *df, PCResultHost 
     if (n == 0) return FBN_OK;
     static const bool timing = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic
     auto t1 = std::chrono::steady_clock::now();
-    FBN_HIP(hipEventSynchronize(S.done));
+    FBN_HIP(EventWaitSpin(S.done));
     auto t2 = std::chrono::steady_clock::now();
     const uint8_t *h_ind = static_cast<const uint8_t *>(S.h_res);
     memcpy(indep, h_ind, (size_t)n);

@@ -229,46 +229,56 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
         hf.items.clear();
         hf.pend.clear();
         hf.stats = CiBatchStats{0, 0};
-        if (d == 1 && group_size == 1 && !full) {
+        if (d == 1 && group_size == 1 && !getenv("FBN_PC_GEN_GENERAL")) {
             // one conditioning variable, no groups: an edge's next chunk is a contiguous slice of
-            // its candidate list -- sized first, then written without per-test bookkeeping (the
-            // same tests and state transitions as the general loop below)
-            size_t total = 0;
+            // its candidate list (with full speculation: both sides whole) -- written into arrays
+            // sized up front, without per-test bookkeeping (the same tests and state transitions
+            // as the general loop below)
+            size_t cap = 0;
             for (size_t e = hf.e0; e < hf.e1; ++e) {
                 const EdgeState &s = st[e];
-                if (!s.resolved && s.has_next) total += (size_t)std::min<int64_t>(hf.chunk, s.m - s.ch[0]);
+                if (!s.resolved && s.has_next)
+                    cap += full ? adj[s.x].size() + adj[s.y].size()
+                                : (size_t)std::min<int64_t>(hf.chunk, s.m - s.ch[0]);
             }
-            hf.items.resize(3 * total);
-            hf.pend.resize(total);
+            hf.items.resize(3 * cap);
+            hf.pend.resize(cap);
             int32_t *it = hf.items.data();
             Pending *pp = hf.pend.data();
             int64_t rows = 0;
             int mx = 0;
             for (size_t e = hf.e0; e < hf.e1; ++e) {
                 EdgeState &s = st[e];
-                if (s.resolved || !s.has_next) continue;
-                const int cnt = (int)std::min<int64_t>(hf.chunk, s.m - s.ch[0]);
+                if (s.resolved) continue;
                 const int dx = dims[s.x], dy = dims[s.y];
-                mx = std::max(mx, std::max(dx, dy));
-                for (int i = 0; i < cnt; ++i) {
-                    const int z = s.A(s.ch[0] + i);
-                    it[0] = s.x, it[1] = s.y, it[2] = z, it += 3;
-                    rows += dx + dy + dims[z], mx = std::max(mx, dims[z]);
-                    *pp++ = Pending{(int)e, s.side, s.pos_in_side + i + 1};
-                }
-                if (s.ch[0] + cnt == s.m) {  // side exhausted: the next side starts fresh
-                    if (s.side == 0) {
-                        s.side = 1;
-                        StartSide(s, adj, d);
-                    } else {
-                        s.side = 2;
-                        s.has_next = false;
+                while (s.has_next) {
+                    const int cnt = (int)std::min<int64_t>(hf.chunk, s.m - s.ch[0]);
+                    mx = std::max(mx, std::max(dx, dy));
+                    for (int i = 0; i < cnt; ++i) {
+                        const int z = s.A(s.ch[0] + i);
+                        it[0] = s.x, it[1] = s.y, it[2] = z, it += 3;
+                        rows += dx + dy + dims[z], mx = std::max(mx, dims[z]);
+                        *pp++ = Pending{(int)e, s.side, s.pos_in_side + i + 1};
                     }
-                } else {
-                    s.ch[0] += cnt;
-                    s.pos_in_side += cnt;
+                    if (s.ch[0] + cnt == s.m) {  // side exhausted: the next side starts fresh
+                        if (s.side == 0) {
+                            s.side = 1;
+                            StartSide(s, adj, d);
+                            if (full) continue;  // one round takes every candidate set
+                        } else {
+                            s.side = 2;
+                            s.has_next = false;
+                        }
+                    } else {
+                        s.ch[0] += cnt;
+                        s.pos_in_side += cnt;
+                    }
+                    break;
                 }
             }
+            const size_t total = (size_t)(pp - hf.pend.data());
+            hf.items.resize(3 * total);
+            hf.pend.resize(total);
             hf.stats = CiBatchStats{mx, rows};
             hf.chunk = std::min<int64_t>(hf.chunk * growth, 1 << 16);
             return;

@@ -38,6 +38,29 @@ namespace {
 
 enum { ARROW = 0, TAIL = 1 };
 
+// a node's parents / children / skeleton neighbours: a sorted vector (iteration in ascending node
+// index, as the reference's node-pointer sets; degrees are small, so a vector beats std::set's
+// per-element allocations)
+struct IntSet {
+    std::vector<int> v;
+    bool insert(int x) {
+        auto it = std::lower_bound(v.begin(), v.end(), x);
+        if (it != v.end() && *it == x) return false;
+        v.insert(it, x);
+        return true;
+    }
+    bool erase(int x) {
+        auto it = std::lower_bound(v.begin(), v.end(), x);
+        if (it == v.end() || *it != x) return false;
+        v.erase(it);
+        return true;
+    }
+    size_t count(int x) const { return std::binary_search(v.begin(), v.end(), x) ? 1 : 0; }
+    size_t size() const { return v.size(); }
+    std::vector<int>::const_iterator begin() const { return v.begin(); }
+    std::vector<int>::const_iterator end() const { return v.end(); }
+};
+
 struct GEdge {
     int n1, n2, ep1, ep2;
     bool operator==(const GEdge &o) const { return n1 == o.n1 && n2 == o.n2 && ep1 == o.ep1 && ep2 == o.ep2; }
@@ -51,7 +74,7 @@ GEdge Directed(int p, int c) { return GEdge{p, c, TAIL, ARROW}; }
 struct Graph {
     int n = 0;
     std::vector<GEdge> edges;
-    std::vector<std::set<int>> parents, children;
+    std::vector<IntSet> parents, children;
     explicit Graph(int nn) : n(nn), parents(nn), children(nn) {}
 
     int Find(const GEdge &e) const {
@@ -177,7 +200,7 @@ struct Graph {
 
 struct Orienter {
     Graph g;
-    std::vector<std::set<int>> adj;  // skeleton adjacencies (fixed during orientation)
+    std::vector<IntSet> adj;  // skeleton adjacencies (fixed during orientation)
     const SepsetMap &sepset;
 
     Orienter(int n, const std::vector<std::pair<int, int>> &skeleton,
@@ -241,7 +264,7 @@ struct Orienter {
     bool Rule1(int b, int c) {
         // node-pointer order == index order; Direct(b, c) edits parents[c] / children[b] only, so
         // b's parent set is stable while it is walked
-        const std::set<int> &par = g.parents[b];
+        const IntSet &par = g.parents[b];
         for (int a : par) {
             if (IsAdjacentTo(c, a)) continue;
             if (Direct(b, c)) return true;
@@ -421,7 +444,7 @@ int ComputeSHD(int n, const std::vector<std::pair<int, int>> &arcs, const std::v
         }
         if (done) continue;
         bool found = false;
-        const std::set<int> py_set = t.parents[y];
+        const IntSet py_set = t.parents[y];
         for (int z : py_set) {
             if (z == x || t.parents[x].count(z)) continue;
             // as in the reference (src/Network.cpp:828-845): x->y is labelled and the *front* of the
