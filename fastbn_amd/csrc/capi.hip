@@ -238,6 +238,8 @@ struct fbn_ci_ctx {
     void *blas = nullptr;
     int *h_kept = nullptr;
     unsigned *h_open = nullptr;
+    void *h_xfer = nullptr;  // pinned staging of level-0 kept pairs / level-1 results (read-back)
+    size_t h_xfer_bytes = 0;
     unsigned long long *h_margin = nullptr;  // pinned: reset value, read-back (CiResetMargin)
     hipEvent_t l1ev[2] = {nullptr, nullptr};
     // decision band of the bit-sliced G^2 kernel for alpha = band_alpha (ci_chisq.h fbn_chisq_band):
@@ -257,6 +259,7 @@ struct fbn_ci_ctx {
         if (h_open) (void)hipHostFree(h_open);
         if (h_margin) (void)hipHostFree(h_margin);
         if (h_kept) (void)hipHostFree(h_kept);
+        if (h_xfer) (void)hipHostFree(h_xfer);
         for (auto &e : l1ev)
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
@@ -268,11 +271,10 @@ static int64_t EnvOr0(const char *name, int64_t dflt) {
     return v ? atoll(v) : dflt;
 }
 
-// Wait for a PC round's event by polling it from this thread (a PC level is a chain of short
-// rounds: polling avoids the blocking wait's wake-up latency on every round trip).
-// FBN_CI_SPIN = 0 restores hipEventSynchronize.
+// Wait for a PC round's event: hipEventSynchronize, or with FBN_CI_SPIN = 1 by polling it from
+// this thread (measured on ALARM-5000 / config 5: no faster than HIP's own wait, so off)
 static hipError_t EventWaitSpin(hipEvent_t ev) {
-    static const bool spin = EnvOr0("FBN_CI_SPIN", 1) != 0;
+    static const bool spin = EnvOr0("FBN_CI_SPIN", 0) != 0;
     if (!spin) return hipEventSynchronize(ev);
     hipError_t e;
     while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
@@ -1852,6 +1854,8 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
     out.counted = out.launched = 0;
     *done = true;
     if (E == 0) return FBN_OK;
+    static const bool ptiming = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic
+    auto tq0 = std::chrono::steady_clock::now();
     FBN_HIP(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     int rc;
@@ -1887,6 +1891,9 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
     FBN_HIP(hipMemcpyAsync(c->l1adjoff.p, adj_off.data(), (size_t)(nv + 1) * 4, hipMemcpyHostToDevice, s));
     FBN_HIP(hipMemsetAsync(c->l1scal.p, 0, 32, s));
     FBN_HIP(hipMemsetAsync(c->l1open.p, 0, kL1MaxRounds * 4, s));
+    if (ptiming)
+        fprintf(stderr, "  level 1 device setup (host): %.3f ms\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
     CiSlot &S = c->slot[0];
     if (c->timing) FBN_HIP(hipEventRecord(S.ev0, s));
     hipError_t e = fbn_ci_l1_setup(c->l1pairs.as<int32_t>(), E, c->l1adj.as<int32_t>(), c->l1adjoff.as<int32_t>(),
@@ -1918,14 +1925,20 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
         chunk = std::min<int64_t>(chunk * growth, 1 << 16);
     }
     if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
-    std::vector<uint8_t> st(E);
-    std::vector<long long> cnt(E);
-    long long sc[3];
-    FBN_HIP(hipMemcpyAsync(st.data(), c->l1st.p, (size_t)E, hipMemcpyDeviceToHost, s));
-    FBN_HIP(hipMemcpyAsync(out.sep.data(), c->l1sep.p, (size_t)E * 4, hipMemcpyDeviceToHost, s));
-    FBN_HIP(hipMemcpyAsync(cnt.data(), c->l1cnt.p, (size_t)E * 8, hipMemcpyDeviceToHost, s));
-    FBN_HIP(hipMemcpyAsync(sc, scal, 24, hipMemcpyDeviceToHost, s));
+    // read-back through one pinned staging buffer (DMA, no pageable staging copies):
+    // [counters 8E | scalars 24 | sepsets 4E | status E] (each part aligned to its type)
+    if ((rc = PinnedEnsure(c->h_xfer, c->h_xfer_bytes, (size_t)E * 13 + 32))) return rc;
+    char *hx = static_cast<char *>(c->h_xfer);
+    const long long *cnt = reinterpret_cast<const long long *>(hx);
+    const long long *sc = reinterpret_cast<const long long *>(hx + (size_t)E * 8);
+    const int32_t *hsep = reinterpret_cast<const int32_t *>(hx + (size_t)E * 8 + 24);
+    const uint8_t *st = reinterpret_cast<const uint8_t *>(hx + (size_t)E * 12 + 24);
+    FBN_HIP(hipMemcpyAsync(hx, c->l1cnt.p, (size_t)E * 8, hipMemcpyDeviceToHost, s));
+    FBN_HIP(hipMemcpyAsync(hx + (size_t)E * 8, scal, 24, hipMemcpyDeviceToHost, s));
+    FBN_HIP(hipMemcpyAsync(hx + (size_t)E * 8 + 24, c->l1sep.p, (size_t)E * 4, hipMemcpyDeviceToHost, s));
+    FBN_HIP(hipMemcpyAsync(hx + (size_t)E * 12 + 24, c->l1st.p, (size_t)E, hipMemcpyDeviceToHost, s));
     FBN_HIP(hipStreamSynchronize(s));
+    std::memcpy(out.sep.data(), hsep, (size_t)E * 4);
     for (int i = 0; i < E; ++i) {
         out.removed[i] = st[i] == 1;
         if (st[i] != 1) out.sep[i] = -1;
@@ -2044,8 +2057,12 @@ int CiAllPairsKept(fbn_ci_ctx *c, int64_t t0, int64_t P, std::vector<std::pair<i
     FBN_HIP(hipMemcpyAsync(c->h_kept, d_num, 4, hipMemcpyDeviceToHost, s));
     FBN_HIP(hipStreamSynchronize(s));
     const int nk = c->h_kept[0];
-    std::vector<int32_t> idx((size_t)nk);
-    if (nk) FBN_HIP(hipMemcpy(idx.data(), c->keptidx.p, (size_t)nk * 4, hipMemcpyDeviceToHost));
+    if ((rc = PinnedEnsure(c->h_xfer, c->h_xfer_bytes, (size_t)std::max(nk, 1) * 4))) return rc;
+    const int32_t *idx = static_cast<const int32_t *>(c->h_xfer);
+    if (nk) {
+        FBN_HIP(hipMemcpyAsync(c->h_xfer, c->keptidx.p, (size_t)nk * 4, hipMemcpyDeviceToHost, s));
+        FBN_HIP(hipStreamSynchronize(s));
+    }
     const size_t base = kept.size();
     kept.resize(base + (size_t)nk);
     const int n = c->nvars;

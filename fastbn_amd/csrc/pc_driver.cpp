@@ -283,6 +283,10 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
             hf.chunk = std::min<int64_t>(hf.chunk * growth, 1 << 16);
             return;
         }
+        if (full) {  // one round takes all `chunk` candidate sets of the level
+            hf.items.reserve((size_t)chunk * (2 + d));
+            hf.pend.reserve((size_t)chunk);
+        }
         for (size_t e = hf.e0; e < hf.e1; ++e) {
             EdgeState &s = st[e];
             if (s.resolved) continue;
@@ -438,15 +442,21 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
         // 10k-variable graph has 5e7 pairs), kept pairs compacted per batch
         const int64_t chunk = std::max<int64_t>(1, EnvOr("FBN_PC_L0CHUNK", (int64_t)1 << 22));
         int rc = FBN_OK;
+        double t_wait = 0, t_kept = 0;
         for (int64_t t0 = 0; t0 < P && !rc; t0 += chunk) {
             const int64_t m = std::min(chunk, P - t0);
+            auto q0 = std::chrono::steady_clock::now();
             rc = CiBatchLaunchAllPairs(ctx, alpha, &st_all, t0, m);
             if (!rc) rc = CiBatchWait(ctx, 0, reinterpret_cast<uint8_t *>(removed.data() + t0), nullptr, res);
+            auto q1 = std::chrono::steady_clock::now();
             if (!rc && P > (1 << 16)) rc = CiAllPairsKept(ctx, t0, m, edges);  // compacted on the device
+            auto q2 = std::chrono::steady_clock::now();
+            t_wait += std::chrono::duration<double, std::milli>(q1 - q0).count();
+            t_kept += std::chrono::duration<double, std::milli>(q2 - q1).count();
         }
         if (rc) return rc;
         auto tb = std::chrono::steady_clock::now();
-        res.sepset.set_level0(n, removed.data());
+        if (timing) fprintf(stderr, "pc level 0: launch + wait %.3f ms, kept pairs %.3f ms\n", t_wait, t_kept);
         res.tests_per_level.push_back(P);
         res.launched_per_level.push_back(P);
         if (P <= (1 << 16)) {  // small graphs: a host pass over the flags costs less than the round trip
@@ -454,6 +464,12 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
             for (int i = 0; i < n; ++i)
                 for (int j = i + 1; j < n; ++j, ++k)
                     if (!removed[k]) edges.push_back({i, j});
+        }
+        res.sepset.set_level0(n, std::move(removed));
+        {  // adjacency lists sized first (one allocation per variable)
+            std::vector<int> deg(n, 0);
+            for (auto &e : edges) ++deg[e.first], ++deg[e.second];
+            for (int v = 0; v < n; ++v) adj[v].reserve(deg[v]);
         }
         for (auto &e : edges) adj[e.first].push_back(e.second), adj[e.second].push_back(e.first);
         if (pairs) CiSetPairMode(ctx, 2);

@@ -55,9 +55,24 @@ class SepsetMap {
         n0_ = n;
         l0_.assign(removed, removed + (size_t)n * (n - 1) / 2);
     }
+    void set_level0(int n, std::vector<char> &&removed) {  // takes the flags over (no copy)
+        n0_ = n;
+        l0_ = std::move(removed);
+        l0_.resize((size_t)n * (n - 1) / 2);
+    }
     // lookups need no sort: the entries are a few ascending runs (one per level), searched from the
     // last run back (a key set twice keeps its last value)
     bool find(std::pair<int, int> key, View *v) const {
+        // a pair removed at level 0 is never tested again, so its flag is its only entry: checked
+        // first (most absent skeleton pairs of a PC run were removed at level 0)
+        {
+            const int i = key.first, j = key.second;
+            if (!l0_.empty() && 0 <= i && i < j && j < n0_ &&
+                l0_[(size_t)i * n0_ - (size_t)i * (i + 1) / 2 + (size_t)(j - i - 1)]) {
+                *v = View{pool_.data(), 0};
+                return true;
+            }
+        }
         size_t end = e_.size();
         for (size_t r = runs_.size() + 1; r-- > 0;) {
             const size_t begin = r ? runs_[r - 1] : 0;
@@ -68,12 +83,6 @@ class SepsetMap {
                 return true;
             }
             end = begin;
-        }
-        const int i = key.first, j = key.second;
-        if (!l0_.empty() && 0 <= i && i < j && j < n0_ &&
-            l0_[(size_t)i * n0_ - (size_t)i * (i + 1) / 2 + (size_t)(j - i - 1)]) {
-            *v = View{pool_.data(), 0};
-            return true;
         }
         return false;
     }
