@@ -25,6 +25,14 @@ namespace {
 // G^2 terms buffered per chunk of cells (LDS doubles) before the in-order sum
 constexpr int kTermChunk = 1024;
 
+// sub-histogram copies per wave for a table of `cells` > 16 cells (0: one shared table, beyond
+// 64 KB of LDS for the 4 waves' copies): 4 for small tables (config-5 level 2, <= 256 cells:
+// 0.589 -> 0.519 ms), 2 up to 512 cells, else 1 -- on larger tables the extra copies' zeroing and
+// merging cost more than the atomic conflicts they remove (level 3: 0.100 -> 0.138 ms with 4)
+__device__ __host__ inline int sub_lanes(int cells) {
+    return cells <= 16 ? 0 : cells <= 256 ? 4 : cells <= 512 ? 2 : cells <= 4096 ? 1 : 0;
+}
+
 struct CiArgs {
     const uint8_t *cols;  // [nvars][N]
     const int32_t *dims;
@@ -50,11 +58,17 @@ struct CiArgs {
     // decisions only (p == nullptr): [lo, hi] per df 1..nband then delta (ci_chisq.h fbn_chisq_band)
     const double *band;
     int nband;
+    // PK instantiation: the columns packed 2 bits per sample (every state count <= 4), 16 samples
+    // per word, PW words per variable (fbn_ci_pack2_build)
+    const uint32_t *pk;
+    long long PW;
 };
 
 // BITS: count from the bit-sliced store (A.bits); a separate instantiation, so the byte-column
-// kernel keeps its register budget (74 VGPRs vs 178 with the bit-sliced counters compiled in)
-template <int D, bool BITS>
+// kernel keeps its register budget (74 VGPRs vs 178 with the bit-sliced counters compiled in).
+// PK: count from the 2-bit packed columns (A.pk): a quarter of the byte columns' bytes, the same
+// per-sample binning (one field extract per variable and sample, as the byte extract)
+template <int D, bool BITS, bool PK = false>
 __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
     extern __shared__ __align__(16) int32_t lds_base[];
     int32_t *smem = A.gscratch ? A.gscratch + (size_t)blockIdx.x * A.gstride : lds_base;
@@ -75,15 +89,20 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
         const int dxy = dx * dy;
         const int cells = dimz * dxy;
         // small tables (<= 16 cells): per-lane packed 16-bit counters in registers, no LDS traffic
-        // in the sample loop; larger tables: per-wave LDS sub-histograms (no cross-wave contention)
+        // in the sample loop; larger tables: LDS sub-histograms, kLanes per wave (lane l of wave w
+        // adds into copy w * kl + l % kl): no cross-wave contention, and kl-fold fewer same-address
+        // atomics within a wave on skewed tables (a popular cell's lanes serialize in one copy);
+        // copies at an odd stride, so one cell's copies fall in different banks
         const bool packed = cells <= 16 && A.N <= (1ll << 24);
-        const int nsub = (cells > 16 && cells * 16 <= 64 * 1024) ? 4 : 1;  // = fbn_ci_lds_bytes
-        // LDS layout (ints): hist[cells] | sub[nsub][cells] | ni | nj | nk | dfp | (even) term[tc] f64
+        const int kl = sub_lanes(cells);
+        const int nsub = kl ? 4 * kl : 1;  // = fbn_ci_lds_bytes
+        const int sstr = cells | 1;
+        // LDS layout (ints): hist[cells] | sub[nsub][sstr] | ni | nj | nk | dfp | (even) term[tc] f64
         // (tc = min(cells, kTermChunk): the G^2 terms of one chunk of cells)
         const int tc = cells < kTermChunk ? cells : kTermChunk;
         int32_t *hist = smem;
         int32_t *sub = hist + ((cells + 3) & ~3);
-        int32_t *ni = sub + (nsub > 1 ? nsub * cells : 0);
+        int32_t *ni = sub + (nsub > 1 ? nsub * sstr : 0);
         int32_t *nj = ni + dimz * dx;
         int32_t *nk = nj + dimz * dy;
         int32_t *dfp = nk + dimz;
@@ -92,7 +111,7 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
 
         for (int c = tid; c < cells; c += 256) hist[c] = 0;
         if (nsub > 1 && !BITS)
-            for (int c = tid; c < nsub * cells; c += 256) sub[c] = 0;
+            for (int c = tid; c < nsub * sstr; c += 256) sub[c] = 0;
         __syncthreads();
         if (BITS) {
             // bit-sliced counting: wave w takes the prefixes p = w, w + 4, ... of the z-configuration
@@ -163,13 +182,7 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
             }
         }
         if (!BITS) {
-        int32_t *myhist = nsub > 1 ? sub + (tid >> 6) * cells : hist;
-        const uint8_t *cx = A.cols + (size_t)x * A.N;
-        const uint8_t *cy = A.cols + (size_t)y * A.N;
-        const uint8_t *cz[D > 0 ? D : 1];
-#pragma unroll
-        for (int j = 0; j < D; ++j) cz[j] = A.cols + (size_t)zv[j] * A.N;
-
+        int32_t *myhist = nsub > 1 ? sub + ((tid >> 6) * kl + (lane & (kl - 1))) * sstr : hist;
         unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;  // cell c: a[c >> 2] bits [16 (c & 3), +16)
         auto bin = [&](int cell, bool valid) {
             if (packed) {
@@ -183,6 +196,53 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
                 atomicAdd(&myhist[cell], 1);
             }
         };
+        if (PK) {
+            // full words (16 samples each) unchecked, kU in flight per thread; the tail word's
+            // samples beyond N (zero padding) excluded
+            const uint32_t *px = A.pk + (size_t)x * A.PW, *py = A.pk + (size_t)y * A.PW;
+            const uint32_t *pz[D > 0 ? D : 1];
+#pragma unroll
+            for (int j = 0; j < D; ++j) pz[j] = A.pk + (size_t)zv[j] * A.PW;
+            const long long full = A.N / 16;
+            auto bin16 = [&](uint32_t wx, uint32_t wy, const uint32_t *wz, int lim) {
+#pragma unroll
+                for (int s = 0; s < 16; ++s) {
+                    int zi = 0;
+#pragma unroll
+                    for (int j = 0; j < D; ++j) zi += (int)((wz[j] >> (2 * s)) & 3u) * cum[j];
+                    const int cell = (zi * dx + (int)((wx >> (2 * s)) & 3u)) * dy + (int)((wy >> (2 * s)) & 3u);
+                    bin(s < lim ? cell : 0, s < lim);
+                }
+            };
+            constexpr int kU = 2;
+            for (long long kb = tid; kb < full; kb += 256 * kU) {
+                uint32_t wx[kU], wy[kU], wz[kU][D > 0 ? D : 1];
+                bool v[kU];
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    const long long k = kb + u * 256;
+                    v[u] = k < full;
+                    const long long kk = v[u] ? k : 0;
+                    wx[u] = px[kk], wy[u] = py[kk];
+#pragma unroll
+                    for (int j = 0; j < D; ++j) wz[u][j] = pz[j][kk];
+                }
+#pragma unroll
+                for (int u = 0; u < kU; ++u) bin16(wx[u], wy[u], wz[u], v[u] ? 16 : 0);
+            }
+            if (A.N % 16 && tid == 0) {
+                uint32_t wz[D > 0 ? D : 1];
+#pragma unroll
+                for (int j = 0; j < D; ++j) wz[j] = pz[j][full];
+                bin16(px[full], py[full], wz, (int)(A.N % 16));
+            }
+        } else {
+        const uint8_t *cx = A.cols + (size_t)x * A.N;
+        const uint8_t *cy = A.cols + (size_t)y * A.N;
+        const uint8_t *cz[D > 0 ? D : 1];
+#pragma unroll
+        for (int j = 0; j < D; ++j) cz[j] = A.cols + (size_t)zv[j] * A.N;
+
         const long long N4 = (A.N % 4 == 0) ? A.N / 4 : 0;
         // kU words per column in flight per thread: one memory latency per kU steps, not per step
         constexpr int kU = 4;
@@ -222,6 +282,7 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
             }
             bin(cell, v);
         }
+        }  // byte / 2-bit columns
         if (packed) {  // wave reduction of the packed counters, one LDS add per cell per wave
             for (int c = 0; c < cells; ++c) {
                 const unsigned long long w = (c >> 2) == 0 ? a0 : (c >> 2) == 1 ? a1 : (c >> 2) == 2 ? a2 : a3;
@@ -231,12 +292,12 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
                 if (lane == 0 && v) atomicAdd(&hist[c], v);
             }
         }
-        }  // byte columns
+        }  // !BITS
         __syncthreads();
         if (nsub > 1 && !BITS) {
             for (int c = tid; c < cells; c += 256) {
                 int v = 0;
-                for (int w = 0; w < nsub; ++w) v += sub[w * cells + c];
+                for (int w = 0; w < nsub; ++w) v += sub[w * sstr + c];
                 hist[c] = v;
             }
             __syncthreads();
@@ -387,8 +448,9 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
 extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy) {
     // must match the kernel's layout
     const size_t cells = (size_t)dimz * dx * dy;
-    const size_t nsub = (cells > 16 && cells * 16 <= 64 * 1024) ? 4 : 0;
-    size_t ints = ((cells + 3) & ~(size_t)3) + nsub * cells + (size_t)dimz * (dx + dy + 2);
+    const size_t kl = cells > (1u << 30) ? 0 : sub_lanes((int)cells);
+    const size_t nsub = 4 * kl;
+    size_t ints = ((cells + 3) & ~(size_t)3) + nsub * (cells | 1) + (size_t)dimz * (dx + dy + 2);
     ints = (ints + 1) & ~(size_t)1;
     return ints * 4 + std::min<size_t>(cells, kTermChunk) * 8;
 }
@@ -398,15 +460,17 @@ extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, co
                                     uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
                                     int32_t *gscratch, unsigned long long *stats, const uint32_t *bits,
                                     const int32_t *row0, long long W, const double *band, int nband,
-                                    hipStream_t stream) {
+                                    const uint32_t *pk, long long PW, hipStream_t stream) {
     CiArgs a{cols, dims, items, N, n, alpha, g2, df, p, indep, counts, gscratch, (long long)(lds_bytes / 4 + 1) & ~1ll,
-             stats, bits, row0, W, band, nband};
+             stats, bits, row0, W, band, nband, pk, PW};
     if (gscratch) lds_bytes = 0;
     switch (d) {
 #define FBN_CI_CASE(DD)                                                                              \
     case DD:                                                                                         \
         if (bits && DD >= 2)                                                                         \
             hipLaunchKernelGGL((ci_g2_kernel<DD, true>), dim3(grid), dim3(256), lds_bytes, stream, a);  \
+        else if (pk)                                                                                 \
+            hipLaunchKernelGGL((ci_g2_kernel<DD, false, true>), dim3(grid), dim3(256), lds_bytes, stream, a); \
         else                                                                                         \
             hipLaunchKernelGGL((ci_g2_kernel<DD, false>), dim3(grid), dim3(256), lds_bytes, stream, a); \
         break;
@@ -423,5 +487,29 @@ extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, co
     default:
         return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+// the 2-bit packed column store: word w of variable v holds samples 16w .. 16w + 15 (sample 16w + s
+// in bits 2s, 2s + 1); samples past N are zero (the kernel excludes them)
+__global__ __launch_bounds__(256) void ci_pack2_build(const uint8_t *__restrict__ cols, long long N, long long PW,
+                                                      long long total, uint32_t *__restrict__ pk) {
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+        const long long v = i / PW, w = i % PW;
+        const uint8_t *c = cols + v * N + 16 * w;
+        const long long left = N - 16 * w;
+        uint32_t r = 0;
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+            if (s < left) r |= (uint32_t)(c[s] & 3u) << (2 * s);
+        pk[i] = r;
+    }
+}
+
+extern "C" hipError_t fbn_ci_pack2_build(const uint8_t *cols, int nvars, long long N, long long PW, uint32_t *pk,
+                                         hipStream_t stream) {
+    const long long total = (long long)nvars * PW;
+    const int grid = (int)std::min<long long>((total + 255) / 256, 65536);
+    if (total > 0) hipLaunchKernelGGL(ci_pack2_build, dim3(grid), dim3(256), 0, stream, cols, N, PW, total, pk);
     return hipGetLastError();
 }

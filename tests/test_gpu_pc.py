@@ -82,6 +82,27 @@ def test_pc_stable_alarm5000_other_alphas(alarm_ds, alarm_paths, alpha, device_l
     assert pc.sepset == ref["sepset"]
 
 
+@pytest.mark.parametrize("fullspec", [True, False])
+def test_level1_generators_agree(alarm_ds, alarm_paths, fullspec, monkeypatch):
+    """Level-1 candidate generation: the single-pass writer (both sides of every edge in one round
+    under full speculation, one slice per round otherwise) and the general per-test loop
+    (FBN_PC_GEN_GENERAL) launch the same tests and give the restatement's result."""
+    od = O.OracleDataset(csv=alarm_paths["csv"])
+    ref = od.pc_stable(0.05, 1000, 1)
+    monkeypatch.setenv("FBN_PC_HOST_L1", "1")  # level 1 through the host rounds
+    if not fullspec:
+        monkeypatch.setenv("FBN_PC_FULLSPEC", "0")
+    runs = []
+    for general in (False, True):
+        if general:
+            monkeypatch.setenv("FBN_PC_GEN_GENERAL", "1")
+        pc = F.PCStable(0.05, 1000).StructLearnCompData(alarm_ds)
+        assert pc.tests_per_level.tolist() == ref["tests_per_level"]
+        assert pc.edges == ref["edges"] and pc.sepset == ref["sepset"]
+        runs.append(pc.launched_per_level.tolist())
+    assert runs[0] == runs[1]
+
+
 @pytest.mark.parametrize("gs,staged", [(1, False), (3, False), (1, True)])
 def test_pc_stable_alarm5000_pipelined_rounds(alarm_ds, alarm_paths, gs, staged, monkeypatch):
     """The driver's multi-round path (no full speculation) with the level's edges in two halves
@@ -287,6 +308,50 @@ def test_bit_sliced_conditional_tables_match_byte_columns(ns):
         np.testing.assert_array_equal(p, ph)
         np.testing.assert_array_equal(ind, indh)
         for k in range(0, len(items), max(1, len(items) // 20)):
+            it = [int(v) for v in items[k]]
+            r = od.ci_test(it[0], it[1], it[2:])
+            assert df[k] == r["df"] and ind[k] == r["is_independent"]
+            assert abs(g2[k] - r["g2"]) <= G2_TOL * max(1.0, abs(r["g2"]))
+
+
+@pytest.mark.parametrize("ns", [33, 5000, 100003])
+def test_packed_columns_match_byte_columns(ns, monkeypatch):
+    """Histogram-kernel batches whose variables all have <= 4 states read the columns packed 2 bits
+    per sample (16 per word, the tail word's padding excluded): tables, df, G^2, p and decisions
+    equal the byte-column kernel's (FBN_CI_NO_PACK2) and the oracle's, for ragged sample counts and
+    d = 0..4; a batch with a 5-state variable keeps the byte columns."""
+    rng = np.random.default_rng(ns + 11)
+    dims = np.array([2, 3, 4, 1, 4, 3, 2, 4, 3, 5], np.int32)
+    nv = len(dims)
+    cols = np.stack([rng.integers(0, d, ns) for d in dims]).astype(np.uint8)
+    cols[4] = (cols[2] + cols[1]) % 4
+    ci = F.IndependenceTest(F.Dataset(columns=cols, dims=dims), 0.05, device=0)
+    od = O.OracleDataset(columns=cols, dims=dims)
+    monkeypatch.setenv("FBN_CI_PACK2", "1")  # the packed columns at every sample count
+    batches = {
+        0: np.array([[x, y] for x in range(9) for y in range(x + 1, 9)], np.int32),
+        1: np.array([[0, 4, 2], [1, 2, 4], [5, 8, 7], [3, 6, 0]], np.int32),
+        2: np.array([[x, y, a, b] for x in range(9) for y in range(x + 1, 9) for a in range(9) for b in
+                     range(a + 1, 9) if len({x, y, a, b}) == 4][::11], np.int32),
+        3: np.array([[0, 4, 1, 2, 7], [2, 5, 0, 4, 8], [1, 7, 3, 6, 5]], np.int32),
+        4: np.array([[0, 4, 1, 2, 7, 8], [2, 5, 0, 4, 8, 6]], np.int32),
+        5: np.array([[0, 9, 1, 2, 7, 8, 4]], np.int32),  # 5-state variable: byte columns
+    }
+    for d, items in batches.items():
+        g2, df, p, ind = ci.run(items, d)
+        cnt = ci.counts(int(items[0][0]), int(items[0][1]), [int(v) for v in items[0][2:]])
+        os.environ["FBN_CI_NO_PACK2"] = "1"
+        try:
+            g2b, dfb, pb, indb = ci.run(items, d)
+            cntb = ci.counts(int(items[0][0]), int(items[0][1]), [int(v) for v in items[0][2:]])
+        finally:
+            del os.environ["FBN_CI_NO_PACK2"]
+        np.testing.assert_array_equal(cnt, cntb)
+        np.testing.assert_array_equal(df, dfb)
+        np.testing.assert_array_equal(g2, g2b)
+        np.testing.assert_array_equal(p, pb)
+        np.testing.assert_array_equal(ind, indb)
+        for k in range(0, len(items), max(1, len(items) // 10)):
             it = [int(v) for v in items[k]]
             r = od.ci_test(it[0], it[1], it[2:])
             assert df[k] == r["df"] and ind[k] == r["is_independent"]
