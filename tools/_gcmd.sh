@@ -1,7 +1,11 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-o=gpurun_out/r02c_prof; mkdir -p $o
-timeout -k 10 400 python -u bench.py > $o/bench.json 2> $o/bench.err || { echo bench failed; tail -20 $o/bench.err; exit 1; }
-echo bench ok
-bash tools/profile_r02.sh $o || { echo profile failed; exit 1; }
+cp fastbn_amd/libfastbn.so /tmp/libfastbn_w3.so
+for w in w3 w4 w5; do
+  cp /tmp/libfastbn_$w.so fastbn_amd/libfastbn.so 2>/dev/null || cp fastbn_amd/libfastbn_$w.so fastbn_amd/libfastbn.so
+  echo $w; timeout -k 10 200 python tools/pc5_timing.py 6 2>&1 | grep "run " | tail -2 | sed 's/tests \[.*launched/launched/' || exit 1
+  mkdir -p gpurun_out/r02l_$w
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r02l_$w -o run --output-format csv -- python tools/pc5_timing.py 3 > /dev/null 2>&1 || exit 1
+done
+cp /tmp/libfastbn_w3.so fastbn_amd/libfastbn.so
