@@ -70,17 +70,158 @@ struct GEdge {
 GEdge Undirected(int a, int b) { return GEdge{std::min(a, b), std::max(a, b), TAIL, TAIL}; }
 GEdge Directed(int p, int c) { return GEdge{p, c, TAIL, ARROW}; }
 
+// The reference's vec_edges (a std::vector of edges: push_back, erase of the first equal element
+// found by a linear search, positional sweeps) with the same order semantics in O(1) / O(log E)
+// per operation: edges live in append-only slots, an erased slot becomes a tombstone, a Fenwick
+// tree over the live flags maps a position to its slot, and an open-addressing table maps every
+// edge to the chain of its live slots in ascending order (its head = the linear search's hit).
+class EdgeSeq {
+  public:
+    int size() const { return nlive_; }
+    int slots() const { return (int)e_.size(); }
+    bool live(int s) const { return live_[s] != 0; }
+    const GEdge &at_slot(int s) const { return e_[s]; }
+    int64_t erasures() const { return nerased_; }
+    void reserve(size_t n) {
+        e_.reserve(n), live_.reserve(n), next_.reserve(n);
+        Rehash(4 * n);
+    }
+    void push(const GEdge &g) {
+        const int s = (int)e_.size();
+        e_.push_back(g), live_.push_back(1), next_.push_back(-1);
+        if ((int)e_.size() > cap_) Rebuild();
+        else FenAdd(s, 1);
+        ++nlive_;
+        Ent &h = Insert(Key(g));
+        if (h.head < 0) h.head = h.tail = s;
+        else next_[h.tail] = s, h.tail = s;
+    }
+    int find(const GEdge &g) const {  // slot of the first live equal edge, -1 if none
+        const Ent *h = Lookup(Key(g));
+        return h ? h->head : -1;
+    }
+    bool erase_first(const GEdge &g) {
+        const uint64_t k = Key(g);
+        Ent *h = const_cast<Ent *>(Lookup(k));
+        if (!h) return false;
+        const int s = h->head;
+        h->head = next_[s];
+        if (h->head < 0) Remove(k);
+        live_[s] = 0;
+        FenAdd(s, -1);
+        --nlive_, ++nerased_;
+        return true;
+    }
+    int slot_at(int pos) const {  // the slot at position pos (0-based among live slots)
+        int idx = 0, rem = pos + 1;
+        for (int step = cap_; step > 0; step >>= 1)
+            if (idx + step <= cap_ && fen_[idx + step] < rem) idx += step, rem -= fen_[idx];
+        return idx;
+    }
+    int next_live(int s) const {  // first live slot after s (slots() if none)
+        do ++s;
+        while (s < (int)e_.size() && !live_[s]);
+        return s;
+    }
+    // overwrite the edge of a slot alone in its chain (the SHD's reversible arcs of a DAG)
+    void replace_single(int s, const GEdge &g) {
+        Remove(Key(e_[s]));
+        e_[s] = g;
+        Ent &h = Insert(Key(g));
+        if (h.head < 0) h.head = h.tail = s;
+        else next_[h.tail] = s, h.tail = s;
+    }
+
+  private:
+    struct Ent {
+        int head = -1, tail = -1;
+    };
+    static uint64_t Key(const GEdge &g) {
+        return (uint64_t)(uint32_t)g.n1 << 34 ^ (uint64_t)(uint32_t)g.n2 << 2 ^ (uint64_t)(g.ep1 << 1 | g.ep2);
+    }
+    static size_t Hash(uint64_t k) {
+        k ^= k >> 33, k *= 0xff51afd7ed558ccdull, k ^= k >> 33;
+        return (size_t)k;
+    }
+    // open addressing, linear probing; state 0 empty, 1 full, 2 deleted
+    std::vector<uint64_t> keys_;
+    std::vector<Ent> vals_;
+    std::vector<uint8_t> state_;
+    size_t used_ = 0;  // full + deleted
+    const Ent *Lookup(uint64_t k) const {
+        if (keys_.empty()) return nullptr;
+        const size_t m = keys_.size() - 1;
+        for (size_t i = Hash(k) & m;; i = (i + 1) & m) {
+            if (state_[i] == 0) return nullptr;
+            if (state_[i] == 1 && keys_[i] == k) return &vals_[i];
+        }
+    }
+    Ent &Insert(uint64_t k) {
+        if (keys_.empty() || 2 * (used_ + 1) > keys_.size()) Rehash(4 * (used_ + 1));
+        const size_t m = keys_.size() - 1;
+        size_t tomb = SIZE_MAX;
+        for (size_t i = Hash(k) & m;; i = (i + 1) & m) {
+            if (state_[i] == 1 && keys_[i] == k) return vals_[i];
+            if (state_[i] == 2 && tomb == SIZE_MAX) tomb = i;
+            if (state_[i] == 0) {
+                const size_t j = tomb != SIZE_MAX ? tomb : i;
+                if (state_[j] == 0) ++used_;
+                state_[j] = 1, keys_[j] = k, vals_[j] = Ent();
+                return vals_[j];
+            }
+        }
+    }
+    void Remove(uint64_t k) {
+        const size_t m = keys_.size() - 1;
+        for (size_t i = Hash(k) & m;; i = (i + 1) & m) {
+            if (state_[i] == 0) return;
+            if (state_[i] == 1 && keys_[i] == k) {
+                state_[i] = 2;
+                return;
+            }
+        }
+    }
+    void Rehash(size_t want) {
+        size_t cap = 64;
+        while (cap < want) cap <<= 1;
+        std::vector<uint64_t> k0(cap, 0);
+        std::vector<Ent> v0(cap);
+        std::vector<uint8_t> s0(cap, 0);
+        k0.swap(keys_), v0.swap(vals_), s0.swap(state_);
+        used_ = 0;
+        for (size_t i = 0; i < s0.size(); ++i)
+            if (s0[i] == 1) Insert(k0[i]) = v0[i];
+    }
+    // Fenwick tree over live_ (1-based, cap_ a power of two)
+    std::vector<GEdge> e_;
+    std::vector<uint8_t> live_;
+    std::vector<int> next_, fen_;
+    int cap_ = 0, nlive_ = 0;
+    int64_t nerased_ = 0;
+    void FenAdd(int s, int v) {
+        for (int i = s + 1; i <= cap_; i += i & -i) fen_[i] += v;
+    }
+    void Rebuild() {
+        int cap = std::max(cap_, 64);
+        while (cap < (int)e_.size()) cap <<= 1;
+        cap_ = cap;
+        fen_.assign(cap_ + 1, 0);
+        for (size_t s = 0; s < live_.size(); ++s) fen_[s + 1] = live_[s];
+        for (int i = 1; i <= cap_; ++i) {
+            const int j = i + (i & -i);
+            if (j <= cap_) fen_[j] += fen_[i];
+        }
+    }
+};
+
 // the reference's Network state used by orientation: edge list + parent/child sets
 struct Graph {
     int n = 0;
-    std::vector<GEdge> edges;
+    EdgeSeq edges;  // vec_edges
     std::vector<IntSet> parents, children;
     explicit Graph(int nn) : n(nn), parents(nn), children(nn) {}
 
-    int Find(const GEdge &e) const {
-        auto it = std::find(edges.begin(), edges.end(), e);
-        return it == edges.end() ? -1 : (int)(it - edges.begin());
-    }
+    int Find(const GEdge &e) const { return edges.find(e); }  // slot of the first equal edge, -1 if none
     bool ContainCircle() const {
         std::vector<int> indeg(n, 0);
         for (int i = 0; i < n; ++i)
@@ -158,36 +299,19 @@ struct Graph {
         const bool cyc = ClosesCycle(p, c);
         parents[c].insert(p);
         children[p].insert(c);
-        edges.push_back(Directed(p, c));
+        edges.push(Directed(p, c));
         if (cyc) DeleteDirected(p, c);
         return !cyc;
     }
     bool DeleteDirected(int p, int c) {
-        if (!parents[c].count(p)) return false;  // not present: skip the linear search
-        const int pos = Find(Directed(p, c));
-        if (pos < 0) return false;
+        if (!parents[c].count(p)) return false;
+        if (!edges.erase_first(Directed(p, c))) return false;
         parents[c].erase(p);
         children[p].erase(c);
-        edges.erase(edges.begin() + pos);
         return true;
     }
-    // undirected edges present, by (min, max) key with multiplicity: an absent edge is rejected
-    // without the linear search over `edges`
-    std::unordered_map<uint64_t, int> und;
-    static uint64_t Key(int a, int b) { return (uint64_t)(uint32_t)std::min(a, b) << 32 | (uint32_t)std::max(a, b); }
-    void AddUndirected(int a, int b) {
-        edges.push_back(Undirected(a, b));
-        ++und[Key(a, b)];
-    }
-    bool DeleteUndirected(int a, int b) {
-        auto it = und.find(Key(a, b));
-        if (it == und.end()) return false;
-        const int pos = Find(Undirected(a, b));
-        if (pos < 0) return false;
-        edges.erase(edges.begin() + pos);
-        if (--it->second == 0) und.erase(it);
-        return true;
-    }
+    void AddUndirected(int a, int b) { edges.push(Undirected(a, b)); }
+    bool DeleteUndirected(int a, int b) { return edges.erase_first(Undirected(a, b)); }
     bool IsDirectedFromTo(int a, int b) const { return parents[b].count(a) != 0; }
     // first matching edge for the SHD: undirected, a->b, b->a
     int GetEdge(int a, int b) const {
@@ -206,7 +330,7 @@ struct Orienter {
     Orienter(int n, const std::vector<std::pair<int, int>> &skeleton,
              const SepsetMap &ss)
         : g(n), adj(n), sepset(ss) {
-        g.edges.reserve(skeleton.size() + 16);
+        g.edges.reserve(2 * skeleton.size() + 16);
         for (auto &e : skeleton) {
             g.AddUndirected(e.first, e.second);
             adj[e.first].insert(e.second);
@@ -291,16 +415,20 @@ struct Orienter {
         bool oriented = true;
         while (oriented) {
             oriented = false;
-            for (size_t i = 0; i < g.edges.size();) {
-                const int x = g.edges[i].n1, y = g.edges[i].n2;
+            // position i of vec_edges = live slot s; a step that erased nothing moves to the next
+            // live slot, otherwise the slot of the step's next position is looked up
+            int s = g.edges.size() ? g.edges.slot_at(0) : 0;
+            for (int i = 0; i < g.edges.size();) {
+                const int x = g.edges.at_slot(s).n1, y = g.edges.at_slot(s).n2;
+                const int64_t er = g.edges.erasures();
+                bool stay = false;
                 if (IsUndirectedFromTo(x, y)) {
                     if (Rule1(x, y) || Rule1(y, x) || Rule2(x, y) || Rule2(y, x) || Rule3(x, y) || Rule3(y, x))
-                        oriented = true;  // edge at i erased: i now holds the next one
-                    else
-                        ++i;
-                } else {
-                    ++i;
+                        oriented = stay = true;  // edge at i erased: i now holds the next one
                 }
+                if (!stay) ++i;
+                if (!stay && g.edges.erasures() == er) s = g.edges.next_live(s);
+                else if (i < g.edges.size()) s = g.edges.slot_at(i);
             }
         }
     }
@@ -328,7 +456,9 @@ int OrientPC(int nvars, PCResultHost &r) {
                 ms(t2, t3));
     }
     r.oriented.clear();
-    for (auto &e : o.g.edges) {
+    for (int sl = 0; sl < o.g.edges.slots(); ++sl) {
+        if (!o.g.edges.live(sl)) continue;
+        const GEdge &e = o.g.edges.at_slot(sl);
         if (!e.directed()) r.oriented.push_back({e.n1, e.n2, 0});
         else if (e.ep1 == TAIL) r.oriented.push_back({e.n1, e.n2, 1});
         else r.oriented.push_back({e.n2, e.n1, 1});
@@ -384,7 +514,7 @@ int ComputeSHD(int n, const std::vector<std::pair<int, int>> &arcs, const std::v
     for (auto &a : arcs) {
         t.parents[a.second].insert(a.first);
         t.children[a.first].insert(a.second);
-        t.edges.push_back(Directed(a.first, a.second));
+        t.edges.push(Directed(a.first, a.second));
     }
     if (t.ContainCircle()) return SetError(FBN_ERR_ARG, "true graph is not a DAG");
     // topological order: Kahn, queue, children scanned by ascending index (TopoSortOfDAGZeroInDegreeFirst)
@@ -410,10 +540,10 @@ int ComputeSHD(int n, const std::vector<std::pair<int, int>> &arcs, const std::v
             const int x = topo[k];
             if (!t.parents[y].count(x)) continue;
             const int pos = t.Find(Directed(x, y));
-            if (!ordered[pos]) ordered[pos] = true, order.push_back(t.edges[pos]);
+            if (!ordered[pos]) ordered[pos] = true, order.push_back(t.edges.at_slot(pos));
         }
     }
-    if (order.size() != t.edges.size()) return SetError(FBN_ERR_ARG, "true graph has duplicate arcs");
+    if (order.size() != (size_t)t.edges.size()) return SetError(FBN_ERR_ARG, "true graph has duplicate arcs");
     // FindCompelled (Chickering 1995)
     enum { UNKNOWN = 0, COMPELLED = 1, REVERSIBLE = 2 };
     std::vector<int> label(t.edges.size(), UNKNOWN);
@@ -467,16 +597,16 @@ int ComputeSHD(int n, const std::vector<std::pair<int, int>> &arcs, const std::v
             }
         }
     }
-    for (size_t i = 0; i < t.edges.size(); ++i)
-        if (label[i] == REVERSIBLE) t.edges[i] = Undirected(t.edges[i].n1, t.edges[i].n2);
+    for (int i = 0; i < t.edges.slots(); ++i)  // (no erasures in t: slot = position)
+        if (label[i] == REVERSIBLE) t.edges.replace_single(i, Undirected(t.edges.at_slot(i).n1, t.edges.at_slot(i).n2));
     Graph l(n);
-    for (auto &e : learned) l.edges.push_back(e[2] ? Directed(e[0], e[1]) : Undirected(e[0], e[1]));
+    for (auto &e : learned) l.edges.push(e[2] ? Directed(e[0], e[1]) : Undirected(e[0], e[1]));
     int err = 0;
     for (int a = 0; a < n; ++a)
         for (int b = a + 1; b < n; ++b) {
             const int p1 = t.GetEdge(a, b), p2 = l.GetEdge(a, b);
             if (p1 < 0 && p2 < 0) continue;
-            if (p1 >= 0 && p2 >= 0 && t.edges[p1] == l.edges[p2]) continue;
+            if (p1 >= 0 && p2 >= 0 && t.edges.at_slot(p1) == l.edges.at_slot(p2)) continue;
             ++err;
         }
     *shd = err;

@@ -146,6 +146,27 @@ def test_orientation_random_skeletons():
         assert res.oriented == orient.orient(n, edges, sep), trial
 
 
+def test_orientation_larger_sparse_skeletons():
+    """Sparse skeletons of 150-300 nodes (degree ~2-6, many v-structures, long Meek-rule sweeps):
+    the indexed vec_edges (tombstoned slots, hashed first occurrence, positional sweeps) gives the
+    restatement's edge list, order included."""
+    import random
+    import orient
+    rng = random.Random(11)
+    for trial in range(4):
+        n = rng.randint(150, 300)
+        edges = sorted({(min(a, b), max(a, b)) for a in range(n) for b in rng.sample(range(n), 2) if a != b})
+        present = set(edges)
+        sep = {}
+        for a in range(n):
+            for b in range(a + 1, min(n, a + 12)):  # sepsets of nearby absent pairs; others empty
+                if (a, b) not in present:
+                    others = [v for v in range(n) if v not in (a, b)]
+                    sep[(a, b)] = tuple(sorted(rng.sample(others, rng.randint(0, 2))))
+        res = F.orient_skeleton(n, edges, sep)
+        assert res.oriented == orient.orient(n, edges, sep), trial
+
+
 def _tree_from_dump(path):
     """parent clique of every clique from a plan dump ('c id ... | up s | down ...', 's id ... | up P | down C')."""
     sep_parent, clique_up = {}, {}
