@@ -8,6 +8,7 @@
 // result only on its parent's message, so the values are the reference's level-order values.
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 
 #include "fbn_internal.h"
 
@@ -185,7 +186,12 @@ int CompileJTProgramV(const JTPlanHost &plan, JTProgramV &prog) {
         q.k = k;
         q.root = root ? 1 : 0;
         q.id = c;
-        q.mat = (!root && k > 0) ? 1 : 0;
+        // the Distribute table goes to the per-wave scratch for SEPDIS / MARG when the clique has
+        // >= 2 children; with one child its two passes recompute the entries from the messages
+        // (3 reads of L2-friendly message rows per entry instead of a scratch write + 2 reads that
+        // reach HBM): 369 -> 364 ms per 125k Munin-like cases (FBN_JT_VDEBUG bit 512 measured it)
+        static const int mat_min = getenv("FBN_JT_VMATK") ? atoi(getenv("FBN_JT_VMATK")) : 2;  // (tuning knob)
+        q.mat = (!root && k >= mat_min) ? 1 : 0;
         q.iv_off = (int32_t)prog.initv.size();
         prog.initv.insert(prog.initv.end(), t.pot.begin(), t.pot.end());
         // digits of every entry for the evidence test: packed into one 32-bit word with the
