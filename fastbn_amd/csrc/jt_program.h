@@ -83,6 +83,8 @@ struct JtVClique {
     int32_t mat;                    // Distribute: the final table is written to the per-wave scratch
                                     // rows once (fused into its normalization pass) and the separator
                                     // and marginal passes read it instead of recomputing the chain
+    int32_t cmat;                   // Collect: the last normalization pass writes the table to the
+                                    // scratch rows for SEPCOL (else SEPCOL recomputes the chain)
 };
 #define JT_V_MAX_CHILDREN 6
 #define JT_V_WAVES 2  // waves sharing one 64-case block (disjoint subtrees in parallel)

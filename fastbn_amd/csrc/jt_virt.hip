@@ -414,7 +414,7 @@ void jt_virt_kernel(
 #pragma unroll
             for (int j = 0; j < JT_V_MAX_CHILDREN + 2; ++j) D[j] = Den{1.0, 1.0};
             // the last normalization pass of a clique with children also stores the table for SEPCOL
-            const bool cmat = !q.root && q.k > (dbg & 128 ? 0 : 1) && !(dbg & 32);
+            const bool cmat = q.cmat && !(dbg & 32);
             for (int L = 0; L <= q.k; ++L) {
                 double s = 0.0;
                 if (cmat && L == q.k) {

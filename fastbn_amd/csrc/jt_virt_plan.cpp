@@ -192,6 +192,8 @@ int CompileJTProgramV(const JTPlanHost &plan, JTProgramV &prog) {
         // reach HBM): 369 -> 364 ms per 125k Munin-like cases (FBN_JT_VDEBUG bit 512 measured it)
         static const int mat_min = getenv("FBN_JT_VMATK") ? atoi(getenv("FBN_JT_VMATK")) : 2;  // (tuning knob)
         q.mat = (!root && k >= mat_min) ? 1 : 0;
+        static const int cmat_min = getenv("FBN_JT_VCMATK") ? atoi(getenv("FBN_JT_VCMATK")) : 2;  // (tuning knob)
+        q.cmat = (!root && k >= cmat_min) ? 1 : 0;
         q.iv_off = (int32_t)prog.initv.size();
         prog.initv.insert(prog.initv.end(), t.pot.begin(), t.pot.end());
         // digits of every entry for the evidence test: packed into one 32-bit word with the

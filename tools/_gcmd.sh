@@ -1,4 +1,6 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-for k in 1 2 3 4; do echo "matk=$k $(FBN_JT_VMATK=$k timeout -k 10 120 python tools/munin_once.py 125000 4 0 2>&1 | tail -1)" || exit 1; done
+o=gpurun_out/r02p; mkdir -p $o
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $o/t.log 2>&1 || { tail -30 $o/t.log; exit 1; }
+tail -1 $o/t.log
