@@ -4,3 +4,6 @@ export TMPDIR=/tmp
 o=gpurun_out/r02p; mkdir -p $o
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $o/t.log 2>&1 || { tail -30 $o/t.log; exit 1; }
 tail -1 $o/t.log
+for v in "FBN_CI_L1SCAN=1" "FBN_X=0" "FBN_CI_L1SCAN=1" "FBN_X=0"; do
+  echo $v; env $v timeout -k 10 200 python tools/pc5_timing.py 8 2>&1 | grep "run " | tail -1 | sed 's/tests \[.*launched/launched/' || exit 1
+done
