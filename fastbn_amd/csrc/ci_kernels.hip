@@ -15,6 +15,7 @@
 // which leaves a running sum unchanged).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -24,6 +25,7 @@ namespace {
 
 // G^2 terms buffered per chunk of cells (LDS doubles) before the in-order sum
 constexpr int kTermChunk = 1024;
+constexpr long long kWideTests = 512;  // batches up to this size: 1024-thread workgroups
 
 // sub-histogram copies per wave for a table of `cells` > 16 cells (0: one shared table, beyond
 // 64 KB of LDS for the 4 waves' copies): 4 for small tables (config-5 level 2, <= 256 cells:
@@ -68,8 +70,9 @@ struct CiArgs {
 // kernel keeps its register budget (74 VGPRs vs 178 with the bit-sliced counters compiled in).
 // PK: count from the 2-bit packed columns (A.pk): a quarter of the byte columns' bytes, the same
 // per-sample binning (one field extract per variable and sample, as the byte extract)
-template <int D, bool BITS, bool PK = false>
-__global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
+template <int D, bool BITS, bool PK = false, int BS = 256>
+__global__ __launch_bounds__(BS) void ci_g2_kernel(CiArgs A) {
+    constexpr int NW = BS / 64;  // waves per workgroup (sub-histogram copies exist for 4 of them)
     extern __shared__ __align__(16) int32_t lds_base[];
     int32_t *smem = A.gscratch ? A.gscratch + (size_t)blockIdx.x * A.gstride : lds_base;
     const int tid = threadIdx.x;
@@ -109,9 +112,9 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
         const int term_off = (int)((dfp + dimz) - smem + 1) & ~1;
         double *term = reinterpret_cast<double *>(smem + term_off);
 
-        for (int c = tid; c < cells; c += 256) hist[c] = 0;
+        for (int c = tid; c < cells; c += BS) hist[c] = 0;
         if (nsub > 1 && !BITS)
-            for (int c = tid; c < nsub * sstr; c += 256) sub[c] = 0;
+            for (int c = tid; c < nsub * sstr; c += BS) sub[c] = 0;
         __syncthreads();
         if (BITS) {
             // bit-sliced counting: wave w takes the prefixes p = w, w + 4, ... of the z-configuration
@@ -125,7 +128,7 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
             const uint32_t *px = A.bits + (size_t)A.row0[x] * W, *py = A.bits + (size_t)A.row0[y] * W;
             const int dl = A.dims[zv[D > 0 ? D - 1 : 0]];
             const uint32_t *pl = A.bits + (size_t)A.row0[zv[D > 0 ? D - 1 : 0]] * W;
-            for (int pfx = tid >> 6; pfx < dimz / dl; pfx += 4) {
+            for (int pfx = tid >> 6; pfx < dimz / dl; pfx += NW) {
                 const uint32_t *pz[D > 1 ? D - 1 : 1];
 #pragma unroll
                 for (int j = 0; j + 1 < D; ++j) {
@@ -182,7 +185,7 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
             }
         }
         if (!BITS) {
-        int32_t *myhist = nsub > 1 ? sub + ((tid >> 6) * kl + (lane & (kl - 1))) * sstr : hist;
+        int32_t *myhist = nsub > 1 ? sub + (((tid >> 6) & 3) * kl + (lane & (kl - 1))) * sstr : hist;
         unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;  // cell c: a[c >> 2] bits [16 (c & 3), +16)
         auto bin = [&](int cell, bool valid) {
             if (packed) {
@@ -215,12 +218,12 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
                 }
             };
             constexpr int kU = 2;
-            for (long long kb = tid; kb < full; kb += 256 * kU) {
+            for (long long kb = tid; kb < full; kb += BS * kU) {
                 uint32_t wx[kU], wy[kU], wz[kU][D > 0 ? D : 1];
                 bool v[kU];
 #pragma unroll
                 for (int u = 0; u < kU; ++u) {
-                    const long long k = kb + u * 256;
+                    const long long k = kb + u * BS;
                     v[u] = k < full;
                     const long long kk = v[u] ? k : 0;
                     wx[u] = px[kk], wy[u] = py[kk];
@@ -246,12 +249,12 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
         const long long N4 = (A.N % 4 == 0) ? A.N / 4 : 0;
         // kU words per column in flight per thread: one memory latency per kU steps, not per step
         constexpr int kU = 4;
-        for (long long kb = tid; kb < N4; kb += 256 * kU) {
+        for (long long kb = tid; kb < N4; kb += BS * kU) {
             uint32_t wx[kU], wy[kU], wz[kU][D > 0 ? D : 1];
             bool v4[kU];
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
-                const long long k4 = kb + u * 256;
+                const long long k4 = kb + u * BS;
                 v4[u] = k4 < N4;
                 const long long kk = v4[u] ? k4 : 0;
                 wx[u] = reinterpret_cast<const uint32_t *>(cx)[kk];
@@ -271,7 +274,7 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
                     bin(v4[u] ? cell : 0, v4[u]);
                 }
         }
-        for (long long k = 4 * N4 + tid; k < ((A.N - 4 * N4 + 255) / 256) * 256 + 4 * N4; k += 256) {
+        for (long long k = 4 * N4 + tid; k < ((A.N - 4 * N4 + BS - 1) / BS) * BS + 4 * N4; k += BS) {
             const bool v = k < A.N;
             int cell = 0;
             if (v) {
@@ -295,7 +298,7 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
         }  // !BITS
         __syncthreads();
         if (nsub > 1 && !BITS) {
-            for (int c = tid; c < cells; c += 256) {
+            for (int c = tid; c < cells; c += BS) {
                 int v = 0;
                 for (int w = 0; w < nsub; ++w) v += sub[w * sstr + c];
                 hist[c] = v;
@@ -303,16 +306,16 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
             __syncthreads();
         }
         if (A.counts && it == 0)
-            for (int c = tid; c < cells; c += 256) A.counts[c] = hist[c];
+            for (int c = tid; c < cells; c += BS) A.counts[c] = hist[c];
 
         // marginals N_{x+z}, N_{+yz}, N_{++z} (src/CellTable.cpp:242-250)
-        for (int r = tid; r < dimz * dx; r += 256) {
+        for (int r = tid; r < dimz * dx; r += BS) {
             const int k = r / dx, i = r % dx;
             int s = 0;
             for (int j = 0; j < dy; ++j) s += hist[k * dxy + i * dy + j];
             ni[r] = s;
         }
-        for (int r = tid; r < dimz * dy; r += 256) {
+        for (int r = tid; r < dimz * dy; r += BS) {
             const int k = r / dy, j = r % dy;
             int s = 0;
             for (int i = 0; i < dx; ++i) s += hist[k * dxy + i * dy + j];
@@ -320,7 +323,7 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
         }
         __syncthreads();
         // N_{++z} and the adjusted df per z (src/IndependenceTest.cpp:96-112)
-        for (int k = tid; k < dimz; k += 256) {
+        for (int k = tid; k < dimz; k += BS) {
             int alx = 0, aly = 0, total = 0;
             for (int i = 0; i < dx; ++i) alx += ni[k * dx + i] > 0, total += ni[k * dx + i];
             for (int j = 0; j < dy; ++j) aly += nj[k * dy + j] > 0;
@@ -344,17 +347,17 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
             }
             return t;
         };
-        __shared__ double sred[8];
-        __shared__ int sdf[4], sdec;
+        __shared__ double sred[2 * NW];
+        __shared__ int sdf[NW], sdec;
         if (!A.p && !A.g2 && A.band) {
             double ps = 0.0, pa = 0.0;
             int pdf = 0;
-            for (int c = tid; c < cells; c += 256) {
+            for (int c = tid; c < cells; c += BS) {
                 const double t = term_of(c);
                 ps += t;
                 pa += fabs(t);
             }
-            for (int k = tid; k < dimz; k += 256) pdf += dfp[k];
+            for (int k = tid; k < dimz; k += BS) pdf += dfp[k];
 #pragma unroll
             for (int o = 32; o >= 1; o >>= 1) {
                 ps += __shfl_xor(ps, o);
@@ -364,9 +367,11 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
             if (lane == 0) sred[2 * (tid >> 6)] = ps, sred[2 * (tid >> 6) + 1] = pa, sdf[tid >> 6] = pdf;
             __syncthreads();
             if (tid == 0) {
-                const double gs = (sred[0] + sred[2]) + (sred[4] + sred[6]);
-                const double ga = (sred[1] + sred[3]) + (sred[5] + sred[7]);
-                const int df = sdf[0] + sdf[1] + sdf[2] + sdf[3];
+                double gs = (sred[0] + sred[2]) + (sred[4] + sred[6]);
+                double ga = (sred[1] + sred[3]) + (sred[5] + sred[7]);
+                int df = sdf[0] + sdf[1] + sdf[2] + sdf[3];
+#pragma unroll
+                for (int w = 4; w < NW; ++w) gs += sred[2 * w], ga += sred[2 * w + 1], df += sdf[w];
                 const double err = (cells + 64) * 2.3e-16 * ga;
                 int dec = -1;  // 0 dependent, 1 independent, -1 in-order sum
                 if (df == 0) dec = 1;  // src/IndependenceTest.cpp:140-142
@@ -394,7 +399,7 @@ __global__ __launch_bounds__(256) void ci_g2_kernel(CiArgs A) {
         double g2 = 0.0;
         for (int c0 = 0; c0 < cells; c0 += tc) {
             const int c1 = c0 + tc < cells ? c0 + tc : cells;
-            for (int c = c0 + tid; c < c1; c += 256) term[c - c0] = term_of(c);
+            for (int c = c0 + tid; c < c1; c += BS) term[c - c0] = term_of(c);
             __syncthreads();
             if (tid == 0) {  // loads batched ahead of the dependent adds (LDS latency off the chain)
                 const int m = c1 - c0;
@@ -464,11 +469,20 @@ extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, co
     CiArgs a{cols, dims, items, N, n, alpha, g2, df, p, indep, counts, gscratch, (long long)(lds_bytes / 4 + 1) & ~1ll,
              stats, bits, row0, W, band, nband, pk, PW};
     if (gscratch) lds_bytes = 0;
+    // batches of at most kWideTests tests (deep PC levels: a few hundred tests or fewer, one
+    // workgroup per test on part of the chip): 16 waves per test instead of 4, so each test's
+    // sample loop and epilogue have 4x the waves to hide latency (FBN_CI_NO_WIDE: always 4)
+    static const bool no_wide = getenv("FBN_CI_NO_WIDE") != nullptr;
+    const bool wide = n <= kWideTests && !no_wide;
     switch (d) {
 #define FBN_CI_CASE(DD)                                                                              \
     case DD:                                                                                         \
         if (bits && DD >= 2)                                                                         \
             hipLaunchKernelGGL((ci_g2_kernel<DD, true>), dim3(grid), dim3(256), lds_bytes, stream, a);  \
+        else if (wide && pk)                                                                         \
+            hipLaunchKernelGGL((ci_g2_kernel<DD, false, true, 1024>), dim3(grid), dim3(1024), lds_bytes, stream, a); \
+        else if (wide)                                                                               \
+            hipLaunchKernelGGL((ci_g2_kernel<DD, false, false, 1024>), dim3(grid), dim3(1024), lds_bytes, stream, a); \
         else if (pk)                                                                                 \
             hipLaunchKernelGGL((ci_g2_kernel<DD, false, true>), dim3(grid), dim3(256), lds_bytes, stream, a); \
         else                                                                                         \
