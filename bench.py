@@ -703,7 +703,7 @@ def main():
                                  "note": "fbn_jt_run from host buffers: evidence H2D, kernel, labels + "
                                          f"{info['sum_dom']} marginals per case D2H"}
         if not args.no_pc:
-            out["pc_stable"] = bench_pc(max(5, args.steps // 2), args.warmup)
+            out["pc_stable"] = bench_pc(max(50, args.steps), args.warmup)  # 0.3 ms per call: 50 calls for a stable median
         if not args.no_munin:
             out["munin_like"] = bench_munin(3, 1, with_baseline=not args.no_baseline)
         if not args.no_pc:
