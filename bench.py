@@ -49,11 +49,25 @@ def host_info():
                 break
     except OSError:
         pass
-    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    affinity = len(cpus)
+    # physical cores among the CPUs this process may use: distinct (package, core) pairs (SMT
+    # siblings counted once); the driver's OMP_NUM_THREADS (the box's CPU share) does not cap it
+    phys = set()
+    for c in cpus:
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            phys.add((open(base + "physical_package_id").read().strip(), open(base + "core_id").read().strip()))
+        except OSError:
+            phys.add(("?", str(c)))
+    cores = max(1, len(phys))
     omp = os.environ.get("OMP_NUM_THREADS")
-    cores = min(affinity, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else affinity
-    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": affinity,
-            "omp_num_threads_env": omp, "cores": cores, "sweep": sorted({1, max(1, cores // 2), cores})}
+    share = int(omp) if omp and omp.isdigit() and 0 < int(omp) < cores else None
+    sweep = {1, max(1, cores // 2), cores} | ({share} if share else set())
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": affinity, "physical_cores": cores,
+            "omp_num_threads_env": omp, "cores": cores, "sweep": sorted(sweep),
+            "note": "sweep = {1, cores/2, cores} over the physical cores of the CPUs usable here, plus the "
+                    "driver's OMP_NUM_THREADS share; each reference run gets OMP_NUM_THREADS = t"}
 
 
 def _ref_env(threads):
@@ -94,7 +108,8 @@ def cpu_baseline_jt(budget_cases=40_000):
             _libsvm(path, ev)
             # the reference slows down with threads on ALARM (fork/join per tree level): fewer cases
             best, sweep = _jt_sweep(os.path.join(ALARM, "alarm.xml"), os.path.join(ALARM, "testing_alarm_1k_p20"),
-                                    path, lambda t: budget_cases if t == 1 else budget_cases // 4, hi)
+                                    path, lambda t: budget_cases if t == 1 else budget_cases // (4 if t <= 16 else 16),
+                                    hi)
         return {"value": best["value"], "unit": "cases/s", "cores": best["threads"], "kind": "reference",
                 "cpu": hi, "sweep": sweep,
                 "sample": f"{best['cases']} ALARM cases (7 evidence vars, seed 20250131) through the reference's "

@@ -16,6 +16,7 @@
 #include "fbn_internal.h"
 #include "pc_internal.h"
 #include "ci_chisq.h"
+#include "pc_small.h"
 
 extern "C" hipError_t fbn_jt_launch(const JtOp *ops, int nops, const int32_t *aux, const double *initv,
                                     const uint64_t *dig, const int8_t *evid, int V, long long ncases, int SD,
@@ -247,6 +248,11 @@ struct fbn_ci_ctx {
     size_t h_xfer_bytes = 0;
     unsigned long long *h_margin = nullptr;  // pinned: reset value, read-back (CiResetMargin)
     hipEvent_t l1ev[2] = {nullptr, nullptr};
+    // device-resident skeleton search of small graphs (pc_small.hip): scratch (barrier counters +
+    // first-independent words, zeroed per run; statistics slots; level-0 pair tables) and the
+    // pinned result record the kernel writes
+    DevBuf small_scr;
+    fbn::PcSmallOut *h_small = nullptr;
     // decision band of the bit-sliced G^2 kernel for alpha = band_alpha (ci_chisq.h fbn_chisq_band):
     // [lo, hi] per df 1..kBandDf, then delta; host copy kept alive for the async upload
     DevBuf band;
@@ -265,6 +271,7 @@ struct fbn_ci_ctx {
         if (h_margin) (void)hipHostFree(h_margin);
         if (h_kept) (void)hipHostFree(h_kept);
         if (h_xfer) (void)hipHostFree(h_xfer);
+        if (h_small) (void)hipHostFree(h_small);
         for (auto &e : l1ev)
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
@@ -1309,6 +1316,43 @@ static int CiGram0Blas(fbn_ci_ctx *c, int64_t t0, int64_t n, hipStream_t s, bool
 // items: host copy (validated here).  zc_items / zc_indep / zc_df: optional device-visible
 // (pinned, mapped) host buffers the kernels read the items from and write the decisions to
 // directly -- no staging copies for the small batches of a latency-bound driver round.
+// the bit-sliced store (one mask row per value, W words per row padded to a multiple of 4 for
+// 16-byte loads) and the per-row sample counts, built once per ctx on stream s
+static int CiBitsEnsure(fbn_ci_ctx *c, hipStream_t s) {
+    if (c->bits_ready) return FBN_OK;
+    int rc;
+    const int64_t W = ((c->N + 31) / 32 + 3) & ~(int64_t)3;
+    std::vector<int32_t> row0(c->nvars);
+    int64_t rows = 0;
+    for (int v = 0; v < c->nvars; ++v) row0[v] = (int32_t)rows, rows += std::min(c->dims[v], 8);
+    c->row0_host = row0;
+    if ((rc = c->bits.ensure((size_t)std::max<int64_t>(rows * W, 1) * 4))) return rc;
+    if ((rc = c->brow.ensure((size_t)c->nvars * 4))) return rc;
+    FBN_HIP(hipMemcpyAsync(c->brow.p, c->row0_host.data(), (size_t)c->nvars * 4, hipMemcpyHostToDevice, s));
+    hipError_t e = fbn_ci_bits_build(c->cols.as<uint8_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(), c->N, W,
+                                     c->nvars, c->bits.as<uint32_t>(), s);
+    if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci bits build: %s", hipGetErrorString(e));
+    if ((rc = c->browcnt.ensure((size_t)std::max<int64_t>(rows, 1) * 4))) return rc;
+    e = fbn_ci_bits_rowcount(c->bits.as<uint32_t>(), rows, W, c->browcnt.as<int32_t>(), s);
+    if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci bits row counts: %s", hipGetErrorString(e));
+    c->bits_W = W;
+    c->bits_ready = true;
+    return FBN_OK;
+}
+
+// the 2-bit packed columns (every state count <= 4): PW words per variable, built once per ctx
+static int CiPack2Ensure(fbn_ci_ctx *c, hipStream_t s) {
+    if (c->pack2_ready) return FBN_OK;
+    int rc;
+    const int64_t PW = (c->N + 15) / 16;
+    if ((rc = c->pack2.ensure((size_t)std::max<int64_t>(PW * c->nvars, 1) * 4))) return rc;
+    hipError_t e = fbn_ci_pack2_build(c->cols.as<uint8_t>(), c->nvars, c->N, PW, c->pack2.as<uint32_t>(), s);
+    if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci pack2 build: %s", hipGetErrorString(e));
+    c->pack2_W = PW;
+    c->pack2_ready = true;
+    return FBN_OK;
+}
+
 static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alpha, bool want_g2p,
                           int32_t *counts_dev, hipStream_t s, int k = 0, const int32_t *zc_items = nullptr,
                           uint8_t *zc_indep = nullptr, int32_t *zc_df = nullptr, const fbn::CiBatchStats *pre = nullptr,
@@ -1340,25 +1384,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
     const bool bits_path = d <= 1 && maxdim <= 4 && !getenv("FBN_CI_NO_BITS") &&
                            (c->N >= kBitsMinSamples || getenv("FBN_CI_FORCE_BITS"));
     if (bits_path) {
-        if (!c->bits_ready) {
-            // words per mask row, padded to a multiple of 4 (zero words) for 16-byte row loads
-            const int64_t W = ((c->N + 31) / 32 + 3) & ~(int64_t)3;
-            std::vector<int32_t> row0(c->nvars);
-            int64_t rows = 0;
-            for (int v = 0; v < c->nvars; ++v) row0[v] = (int32_t)rows, rows += std::min(c->dims[v], 8);
-            c->row0_host = row0;
-            if ((rc = c->bits.ensure((size_t)std::max<int64_t>(rows * W, 1) * 4))) return rc;
-            if ((rc = c->brow.ensure((size_t)c->nvars * 4))) return rc;
-            FBN_HIP(hipMemcpyAsync(c->brow.p, row0.data(), (size_t)c->nvars * 4, hipMemcpyHostToDevice, s));
-            hipError_t e = fbn_ci_bits_build(c->cols.as<uint8_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(), c->N,
-                                             W, c->nvars, c->bits.as<uint32_t>(), s);
-            if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci bits build: %s", hipGetErrorString(e));
-            if ((rc = c->browcnt.ensure((size_t)std::max<int64_t>(rows, 1) * 4))) return rc;
-            e = fbn_ci_bits_rowcount(c->bits.as<uint32_t>(), rows, W, c->browcnt.as<int32_t>(), s);
-            if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci bits row counts: %s", hipGetErrorString(e));
-            c->bits_W = W;
-            c->bits_ready = true;
-        }
+        if ((rc = CiBitsEnsure(c, s))) return rc;
         if (!all_pairs && (rc = S.items.ensure((size_t)n * w * 4))) return rc;
         if ((rc = S.indep.ensure((size_t)n))) return rc;
         if ((rc = S.df.ensure((size_t)n * 4))) return rc;
@@ -1491,14 +1517,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
     // FBN_CI_PACK2 = 1 forces it at any size, FBN_CI_NO_PACK2 = 1 disables it.
     const bool pk = !bitsn && maxdim <= 4 && !getenv("FBN_CI_NO_PACK2") &&
                     (c->N >= 65536 || getenv("FBN_CI_PACK2"));
-    if (pk && !c->pack2_ready) {
-        const int64_t PW = (c->N + 15) / 16;
-        if ((rc = c->pack2.ensure((size_t)std::max<int64_t>(PW * c->nvars, 1) * 4))) return rc;
-        hipError_t e = fbn_ci_pack2_build(c->cols.as<uint8_t>(), c->nvars, c->N, PW, c->pack2.as<uint32_t>(), s);
-        if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci pack2 build: %s", hipGetErrorString(e));
-        c->pack2_W = PW;
-        c->pack2_ready = true;
-    }
+    if (pk && (rc = CiPack2Ensure(c, s))) return rc;
     S.last_bytes = bitsn ? mask_rows * c->bits_W * 4  // the mask rows each z-configuration reads
                    : pk  ? n * c->pack2_W * 4 * (2 + d)  // the 2-bit columns x, y, z_1..z_d
                          : n * c->N * (2 + d);  // uint8 columns x, y, z_1..z_d streamed once
@@ -1587,13 +1606,14 @@ int fbn_pc_stable(fbn_ci_ctx *c, double alpha, int depth, int group_size, fbn_pc
     FBN_HIP(hipSetDevice(c->device));
     static const bool timing = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic
     auto t0 = std::chrono::steady_clock::now();
-    int rc = CiResetMargin(c);
-    if (rc) return rc;
+    int rc;
+    // the device-resident search (small graphs) sets the ctx's margin log itself
+    if (!fbn::CiPCSmallEligible(c, group_size) && (rc = CiResetMargin(c))) return rc;
     auto t1 = std::chrono::steady_clock::now();
     if ((rc = fbn::RunPCStable(c, alpha, depth, group_size, r->r))) return rc;
     auto t2 = std::chrono::steady_clock::now();
     // the run's work is all on the ctx stream
-    if ((rc = CiReadMargin(c, &r->r.min_margin, &r->r.near_alpha, true))) return rc;
+    if (!r->r.margin_done && (rc = CiReadMargin(c, &r->r.min_margin, &r->r.near_alpha, true))) return rc;
     auto t3 = std::chrono::steady_clock::now();
     if ((rc = fbn::OrientPC(c->nvars, r->r))) return rc;  // StructLearnByPCStable steps 2-3
     if (timing) {
@@ -1843,6 +1863,7 @@ int CiMarginRead(fbn_ci_ctx *c, double *min_margin, int64_t *near_alpha) {
     FBN_HIP(hipSetDevice(c->device));
     return CiReadMargin(c, min_margin, near_alpha);
 }
+bool CiPairsRecorded(const fbn_ci_ctx *c) { return c->pairs_recorded; }
 void CiSetPairsRecorded(fbn_ci_ctx *c) {
     c->pair_mode = 2;
     c->pairs_recorded = true;
@@ -1854,7 +1875,10 @@ void CiSetPairsRecorded(fbn_ci_ctx *c) {
 // open-edge count per round, one round behind, to stop.  Results equal the host driver's: the same
 // tests in the same per-edge order and the same first-independent rule.  *done = false when not
 // eligible (the host driver runs the level).
-constexpr int kL1MaxRounds = 256;
+// Rounds are unbounded: the per-round open count lives in a two-entry ring (round r writes entry
+// r & 1, the host reads round r - 1's entry while round r runs).  The per-edge chunk is clamped so
+// a round's exclusive scan of the lengths (int32 offsets, hipcub) cannot overflow: E * chunk < 2^31.
+constexpr int kL1Ring = 2;
 int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<int>> &adj,
                    const std::vector<std::pair<int, int>> &edges, size_t e_begin, size_t e_end, LevelOut &out,
                    PCResultHost &res, bool *done) {
@@ -1892,14 +1916,14 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
         (rc = c->l1pos.ensure((size_t)E * 4)) || (rc = c->l1st.ensure((size_t)E)) ||
         (rc = c->l1sep.ensure((size_t)E * 4)) || (rc = c->l1cnt.ensure((size_t)E * 8)) ||
         (rc = c->l1len.ensure((size_t)E * 4)) || (rc = c->l1off.ensure((size_t)E * 4)) ||
-        (rc = c->l1scal.ensure(32)) || (rc = c->l1open.ensure(kL1MaxRounds * 4)) ||
+        (rc = c->l1scal.ensure(32)) || (rc = c->l1open.ensure(kL1Ring * 4)) ||
         (rc = c->l1items.ensure((size_t)cap * 12)) || (rc = c->l1counts.ensure((size_t)cap * 256)) ||
         (rc = c->l1df.ensure((size_t)cap * 4)) || (rc = c->l1indep.ensure((size_t)cap)))
         return rc;
     const size_t scan_bytes = std::max<size_t>(fbn_ci_l1_scan_bytes(E), 16);
     if ((rc = c->l1tmp.ensure(scan_bytes))) return rc;
     if (!c->h_open) {
-        hipError_t e = hipHostMalloc((void **)&c->h_open, kL1MaxRounds * 4, hipHostMallocDefault);
+        hipError_t e = hipHostMalloc((void **)&c->h_open, kL1Ring * 4, hipHostMallocDefault);
         if (e != hipSuccess) return SetError(FBN_ERR_NOMEM, "hipHostMalloc: %s", hipGetErrorString(e));
         for (auto &ev : c->l1ev) FBN_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     }
@@ -1911,7 +1935,7 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
     if (!adjf.empty()) FBN_HIP(hipMemcpyAsync(c->l1adj.p, adjf.data(), adjf.size() * 4, hipMemcpyHostToDevice, s));
     FBN_HIP(hipMemcpyAsync(c->l1adjoff.p, adj_off.data(), (size_t)(nv + 1) * 4, hipMemcpyHostToDevice, s));
     FBN_HIP(hipMemsetAsync(c->l1scal.p, 0, 32, s));
-    FBN_HIP(hipMemsetAsync(c->l1open.p, 0, kL1MaxRounds * 4, s));
+
     if (ptiming)
         fprintf(stderr, "  level 1 device setup (host): %.3f ms\n",
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
@@ -1926,24 +1950,27 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
     // chunk x2 per round: rounds here cost a few launches, speculation costs counted tests (config 5:
     // x4 launches 430k tests for 294k counted, x2 345k)
     const int64_t growth = std::max<int64_t>(2, EnvOr0("FBN_PC_GROWTH", 2));
+    const int64_t max_chunk = std::max<int64_t>(1, std::min<int64_t>(1 << 16, (int64_t)INT32_MAX / E));
+    chunk = std::min(chunk, max_chunk);
     for (int r = 0;; ++r) {
-        if (r >= kL1MaxRounds) return SetError(FBN_ERR_LIMIT, "level 1: more than %d device rounds", kL1MaxRounds);
+        unsigned *open_r = c->l1open.as<unsigned>() + (r & 1);
+        FBN_HIP(hipMemsetAsync(open_r, 0, 4, s));
         e = fbn_ci_l1_round(c->bits.as<uint32_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(), c->bits_W,
                             c->l1adj.as<int32_t>(), c->pairtab.as<int32_t>(), nv, c->l1ed.p, c->l1pos.as<int32_t>(),
                             c->l1st.as<uint8_t>(), c->l1sep.as<int32_t>(), c->l1cnt.as<long long>(),
                             c->l1len.as<int32_t>(), c->l1off.as<int32_t>(), E, (int)chunk, cap, scal, scal + 1,
                             c->l1items.as<int32_t>(), c->l1counts.as<int32_t>(), c->l1df.as<int32_t>(),
                             c->l1indep.as<uint8_t>(), alpha, c->stats.as<unsigned long long>(), band, nband,
-                            c->l1open.as<unsigned>() + r, reinterpret_cast<unsigned long long *>(scal + 2),
+                            open_r, reinterpret_cast<unsigned long long *>(scal + 2),
                             c->l1tmp.p, scan_bytes, c->num_cu, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci level-1 round: %s", hipGetErrorString(e));
-        FBN_HIP(hipMemcpyAsync(c->h_open + r, c->l1open.as<unsigned>() + r, 4, hipMemcpyDeviceToHost, s));
+        FBN_HIP(hipMemcpyAsync(c->h_open + (r & 1), open_r, 4, hipMemcpyDeviceToHost, s));
         FBN_HIP(hipEventRecord(c->l1ev[r & 1], s));
         if (r >= 1) {  // round r - 1's open count, while round r runs
             FBN_HIP(EventWaitSpin(c->l1ev[(r - 1) & 1]));
-            if (c->h_open[r - 1] == 0) break;  // round r found nothing to do
+            if (c->h_open[(r - 1) & 1] == 0) break;  // round r found nothing to do
         }
-        chunk = std::min<int64_t>(chunk * growth, 1 << 16);
+        chunk = std::min<int64_t>(chunk * growth, max_chunk);
     }
     if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
     // read-back through one pinned staging buffer (DMA, no pageable staging copies):
@@ -2122,5 +2149,134 @@ int CiRunBatch(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alp
     int rc = CiBatchLaunch(c, 0, items, n, d, alpha, df != nullptr);
     if (rc) return rc;
     return CiBatchWait(c, 0, indep, df, res);
+}
+
+bool CiPCSmallEligible(const fbn_ci_ctx *c, int group_size) {
+    if (group_size != 1 || c->nvars < 2 || c->nvars > kSmallMaxVars || c->N < 1 || c->N > (1ll << 30) ||
+        getenv("FBN_PC_NO_SMALL"))
+        return false;
+    for (int v = 0; v < c->nvars; ++v)
+        if (c->dims[v] < 1 || c->dims[v] > 4) return false;
+    return true;
+}
+
+int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::vector<std::pair<int, int>> &edges,
+              std::vector<std::vector<int>> &adj, int *levels, bool *handoff) {
+    *levels = 0;
+    *handoff = false;
+    FBN_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    int rc;
+    if ((rc = CiBitsEnsure(c, s)) || (rc = CiPack2Ensure(c, s))) return rc;
+    const double *band = nullptr;
+    int nband = 0;
+    if ((rc = CiBand(c, alpha, s, &band, &nband, kBandDfMax))) return rc;
+    int per_cu = 0;
+    FBN_HIP(fbn_pc_small_occupancy(&per_cu));
+    if (per_cu < 1) return SetError(FBN_ERR_HIP, "pc small kernel: no workgroup fits a CU");
+    const int grid = c->num_cu;  // one workgroup per CU: every workgroup resident (grid barrier)
+    // scratch: [zeroed: barrier words | first-independent words] [statistics slots] [pair tables]
+    const size_t acc_off = (kSmallZeroBytes + 255) & ~(size_t)255;
+    const size_t pt_off = acc_off + (size_t)grid * 64;
+    const size_t bytes = pt_off + (size_t)kSmallMaxEdges * 16 * 4;
+    if ((rc = c->small_scr.ensure(bytes))) return rc;
+    if (!c->h_small) {
+        hipError_t e = hipHostMalloc((void **)&c->h_small, sizeof(PcSmallOut), hipHostMallocDefault);
+        if (e != hipSuccess) return SetError(FBN_ERR_NOMEM, "hipHostMalloc: %s", hipGetErrorString(e));
+    }
+    PcSmallOut *out = c->h_small;
+    out->status = -1;
+    char *scr = c->small_scr.as<char>();
+    PcSmallArgs a{};
+    a.bits = c->bits.as<uint32_t>();
+    a.row0 = c->brow.as<int32_t>();
+    a.rowcnt = c->browcnt.as<int32_t>();
+    a.W = c->bits_W;
+    a.pk = c->pack2.as<uint32_t>();
+    a.PW = c->pack2_W;
+    a.dims = c->ddims.as<int32_t>();
+    a.nvars = c->nvars;
+    a.N = c->N;
+    a.alpha = alpha;
+    a.band = band;
+    a.nband = nband;
+    a.depth = depth;
+    a.bar = reinterpret_cast<unsigned *>(scr);
+    a.first = reinterpret_cast<unsigned *>(scr + (size_t)kSmallBarWords * 4);
+    a.acc = reinterpret_cast<unsigned long long *>(scr + acc_off);
+    a.pairtab = reinterpret_cast<int32_t *>(scr + pt_off);
+    a.ctx_stats = c->stats.as<unsigned long long>();
+    a.out = out;
+    CiSlot &S = c->slot[0];
+    FBN_HIP(hipMemsetAsync(scr, 0, kSmallZeroBytes, s));
+    if (c->timing) FBN_HIP(hipEventRecord(S.ev0, s));
+    FBN_HIP(fbn_pc_small_launch(&a, grid, s));
+    if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
+    FBN_HIP(hipStreamSynchronize(s));
+    if (out->status != 0)
+        return SetError(FBN_ERR_HIP, "pc small kernel: %s (status %d)",
+                        out->status == 1 ? "grid barrier timed out" : "no result", out->status);
+    if (c->timing) {
+        float ms = 0.f;
+        FBN_HIP(hipEventElapsedTime(&ms, S.ev0, S.ev1));
+        res.kernel_s += ms * 1e-3;
+    }
+    // the levels the device completed -> counts, sepsets, skeleton (edges in vec_edges order =
+    // lexicographic pairs of each snapshot)
+    const int n = c->nvars;
+    const int L = out->levels;
+    std::vector<uint64_t> prev(n);
+    for (int v = 0; v < n; ++v) prev[v] = (n >= 64 ? ~0ull : ((1ull << n) - 1ull)) & ~(1ull << v);
+    std::vector<std::pair<int, int>> ledges;
+    std::vector<char> rm;
+    std::vector<int> sep;
+    for (int d = 0; d < L; ++d) {
+        ledges.clear();
+        rm.clear();
+        for (int x = 0; x < n; ++x)
+            for (int y = x + 1; y < n; ++y)
+                if ((prev[x] >> y) & 1ull) {
+                    ledges.push_back({x, y});
+                    rm.push_back(((out->adj[d][x] >> y) & 1ull) ? 0 : 1);
+                }
+        if (d == 0) {
+            res.sepset.set_level0(n, rm.data());  // level 0 = the complete graph
+        } else {
+            sep.assign(ledges.size() * (size_t)d, -1);
+            const int32_t *pool = out->pool + out->sep_off[d];
+            size_t r = 0;
+            for (size_t e = 0; e < ledges.size(); ++e)
+                if (rm[e]) {
+                    for (int j = 0; j < d; ++j) sep[e * d + j] = pool[r * d + j];
+                    ++r;
+                }
+            if ((int64_t)r * d != (int64_t)(out->sep_off[d + 1] - out->sep_off[d]))
+                return SetError(FBN_ERR_HIP, "pc small kernel: level %d sepset count mismatch", d);
+            res.sepset.append_level(ledges.data(), rm.data(), sep.data(), ledges.size(), d);
+        }
+        res.tests_per_level.push_back(out->counted[d]);
+        res.launched_per_level.push_back(out->launched[d]);
+        // bytes of the 2-bit packed columns / bit-sliced rows the tests touched: (d + 2) columns of
+        // N / 4 bytes per launched test (roofline accounting)
+        res.device_bytes += out->launched[d] * (int64_t)(d + 2) * ((c->N + 3) / 4);
+        for (int v = 0; v < n; ++v) prev[v] = out->adj[d][v];
+    }
+    edges.clear();
+    for (int x = 0; x < n; ++x)
+        for (int y = x + 1; y < n; ++y)
+            if ((prev[x] >> y) & 1ull) edges.push_back({x, y});
+    adj.assign(n, {});
+    for (auto &e : edges) adj[e.first].push_back(e.second), adj[e.second].push_back(e.first);
+    for (auto &l : adj) std::sort(l.begin(), l.end());
+    *levels = L;
+    *handoff = out->handoff != 0;
+    if (!*handoff) {
+        double m;
+        memcpy(&m, &out->margin_bits, 8);
+        res.min_margin = m;
+        res.near_alpha = (int64_t)out->near;
+        res.margin_done = true;
+    }
+    return FBN_OK;
 }
 }  // namespace fbn

@@ -47,8 +47,12 @@ struct fbn_pc_dist {
     bool ran = false;           // this rank's range of the current level was run / packed
     bool pairs = true;          // level 0 records pair tables (derived level-1 counting)
     bool pairs_imported = false;
-    fbn_ci_ctx *ctx = nullptr;  // last context run on (pair mode / margin bookkeeping)
+    fbn_ci_ctx *ctx = nullptr;  // last context run on (pair mode / margin bookkeeping); released by
+                                // the last fbn_pc_dist_apply, which snapshots its margin log
     double wall_s = 0.0;
+    bool margin_taken = false;
+    double min_margin = 0.0;
+    int64_t near_alpha = 0;
 };
 
 namespace {
@@ -266,6 +270,13 @@ int fbn_pc_dist_pack(fbn_pc_dist *s, const uint8_t *removed, const int32_t *seps
 int fbn_pc_dist_pairs_chunk(const fbn_pc_dist *s, int64_t *pairs_per_rank) {
     if (!s || !pairs_per_rank) return SetError(FBN_ERR_ARG, "null pointer");
     if (s->world == 0) return SetError(FBN_ERR_ARG, "no level in progress (fbn_pc_dist_level)");
+    // 0 = nothing to exchange: this rank's level 0 recorded no pair tables (the bit-sliced path was
+    // not eligible -- > 4 states, < 4096 samples, FBN_CI_NO_BITS -- or FBN_CI_NO_PAIRS); that depends
+    // only on the dataset and the environment, so every rank of a run agrees
+    if (!s->pairs || s->d != 0 || !s->ran || !s->ctx || !fbn::CiPairsRecorded(s->ctx)) {
+        *pairs_per_rank = 0;
+        return FBN_OK;
+    }
     const int64_t P = (int64_t)s->nvars * (s->nvars - 1) / 2;
     *pairs_per_rank = (P + s->world - 1) / s->world;
     return FBN_OK;
@@ -273,8 +284,8 @@ int fbn_pc_dist_pairs_chunk(const fbn_pc_dist *s, int64_t *pairs_per_rank) {
 
 int fbn_pc_dist_pairs_export(fbn_pc_dist *s, void *buf, int buf_on_device) {
     if (!s || !buf) return SetError(FBN_ERR_ARG, "null pointer");
-    if (s->d != 0 || !s->ran || !s->ctx || !s->pairs)
-        return SetError(FBN_ERR_ARG, "pair tables exist after this rank's level-0 run only");
+    if (s->d != 0 || !s->ran || !s->ctx || !s->pairs || !fbn::CiPairsRecorded(s->ctx))
+        return SetError(FBN_ERR_ARG, "pair tables exist after this rank's level-0 run only (fbn_pc_dist_pairs_chunk = 0)");
     const int64_t b = s->cuts[s->rank], n = s->cuts[s->rank + 1] - b;
     return fbn::CiPairTablesCopy(s->ctx, b, n, buf, buf_on_device != 0, false);
 }
@@ -356,6 +367,16 @@ int fbn_pc_dist_apply(fbn_pc_dist *s, const int32_t *records, int *more) {
     const bool cont = d + 1 < s->depth && (d == 0 || fbn::ContinueAfter(s->adj, d));
     if (cont) ++s->d;
     else s->done = true;
+    if (!cont && s->ctx) {
+        // the search is over: this rank's margin log is read and the pair tables dropped now, while
+        // the ctx is certainly alive (the caller's level loop), so fbn_pc_dist_result never touches a
+        // ctx the caller may already have destroyed
+        int rc = fbn::CiMarginRead(s->ctx, &s->min_margin, &s->near_alpha);
+        if (rc) return rc;
+        fbn::CiSetPairMode(s->ctx, 0);
+        s->margin_taken = true;
+        s->ctx = nullptr;
+    }
     s->world = 0;
     s->ran = false;
     if (more) *more = cont ? 1 : 0;
@@ -371,11 +392,7 @@ int fbn_pc_dist_result(fbn_pc_dist *s, fbn_pc_result **out) {
     r->r = s->res;
     r->r.edges = s->edges;
     r->r.total_s = s->wall_s;
-    if (s->ctx) {
-        int rc = fbn::CiMarginRead(s->ctx, &r->r.min_margin, &r->r.near_alpha);  // this rank's tests
-        if (rc) return rc;
-        fbn::CiSetPairMode(s->ctx, 0);  // drop the pair tables
-    }
+    if (s->margin_taken) r->r.min_margin = s->min_margin, r->r.near_alpha = s->near_alpha;  // this rank's tests
     int rc = fbn::OrientPC(s->nvars, r->r);
     if (rc) return rc;
     *out = r.release();

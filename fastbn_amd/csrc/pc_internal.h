@@ -145,6 +145,7 @@ struct PCResultHost {
     // SURVEY §8(c) decision-margin log over every test evaluated (speculative ones included)
     double min_margin = 0.0;
     int64_t near_alpha = 0;
+    bool margin_done = false;  // min_margin / near_alpha already hold the run's log (device-resident run)
 };
 
 void CiCtxShape(const fbn_ci_ctx *c, int *nvars, int64_t *nsamples);
@@ -174,6 +175,8 @@ int CiBatchLaunchAllPairs(fbn_ci_ctx *c, double alpha, const CiBatchStats *pre, 
 int CiPairTablesCopy(fbn_ci_ctx *c, int64_t p0, int64_t np, void *buf, bool buf_on_device, bool to_ctx);
 // every pair's table is now in the ctx (imported from all ranks): level-1 batches derive from them
 void CiSetPairsRecorded(fbn_ci_ctx *c);
+// whether the ctx holds pair tables of the current run (recorded by its level 0, or imported)
+bool CiPairsRecorded(const fbn_ci_ctx *c);
 // pair tables of the bit-sliced path: 1 = the next marginal batch records every pair's table (it
 // must test all pairs i < j: a PC run's level 0), 2 = one-conditioning-variable batches derive the
 // last value of x, y and z from them, 0 = off (also drops what was recorded)
@@ -184,6 +187,14 @@ int CiTriplePrepare(fbn_ci_ctx *c, const std::vector<std::vector<int>> &adj,
                     const std::vector<std::pair<int, int>> &edges, size_t e_begin, size_t e_end, bool *ready);
 int CiBatchWait(fbn_ci_ctx *c, int k, uint8_t *indep, int32_t *df, PCResultHost &res);
 int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResultHost &res);
+// The skeleton search of a small graph (<= 64 variables, every state count <= 4, group size 1) in
+// ONE device launch (pc_small.hip).  Levels [0, *levels) land in res (tests and launched per level,
+// sepsets) and edges / adj hold the skeleton after them; *handoff: a level the kernel does not take
+// (d > 4 or > 2^22 candidate sets) follows, and the host driver continues at level *levels.  When
+// the search ended on the device res.min_margin / near_alpha hold its decision-margin log.
+bool CiPCSmallEligible(const fbn_ci_ctx *c, int group_size);
+int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::vector<std::pair<int, int>> &edges,
+              std::vector<std::vector<int>> &adj, int *levels, bool *handoff);
 // one level for an edge range (the unit a multi-GPU driver partitions), see pc_driver.cpp
 struct LevelOut {
     std::vector<char> removed;

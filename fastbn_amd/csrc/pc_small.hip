@@ -1,0 +1,733 @@
+// pc_small.hip -- the whole PC-stable skeleton search of a small graph in ONE launch (gfx950).
+//
+// Why: on ALARM-5000 (37 variables, 5000 samples; BASELINE config 3) a level is a few microseconds
+// of CI tests, and the host-driven level loop spent more time in round trips (event wait, host
+// bookkeeping, next launch) than in kernels.  Here the level loop itself runs on the device:
+//
+//   for d = 0, 1, ...:                                    (src/PCStable.cpp:49-200, SearchAtDepth
+//     every workgroup rebuilds the level's edge list from the adjacency snapshot in LDS   :209-328)
+//       (vec_edges order = lexicographic (x < y) pairs of the skeleton, src/Network.cpp:346-358);
+//     every candidate set of every edge is a test t (edge-major, then side, then ChoiceGenerator
+//       order: the d-subsets of adj(x)\{y} in lexicographic order, then those of adj(y)\{x},
+//       CheckEdge src/PCStable.cpp:339-470, ChoiceGenerator src/ChoiceGenerator.cpp:14-85);
+//     tests are counted and decided (d <= 1: one wave per test on the bit-sliced store, level 1
+//       deriving the last value of x, y and z from the level-0 pair tables; d >= 2: one workgroup
+//       per test, LDS histogram of the 2-bit packed columns -- Counts2D/Counts3D,
+//       src/CellTable.cpp:23-91,226-291,430-455; G^2 / df / p as ComputeGSquareXY/XYZ,
+//       src/IndependenceTest.cpp:65-155,295-364);
+//     an independent test does atomicMax(first[d][edge], ~its index within the edge): the edge's
+//       first independent set in the reference's sequential order is the minimum (speculative
+//       tests beyond it are evaluated but not counted: counted = first + 1, else every set);
+//     ONE grid barrier; every workgroup applies the removals to its own LDS adjacency (removals
+//       after the level, src/PCStable.cpp:310-326) and evaluates FreeDegree (:557-563);
+//       workgroup 0 writes the level's counts, adjacency and sepsets into the pinned result.
+//
+// Sizes: <= 64 variables (adjacency = one u64 each), every state count <= 4, levels <= 4 and
+// <= 2^22 candidate sets per level; a level outside those hands the search to the host driver
+// (pc_driver.cpp) at that level.  Synchronisation follows MI355X_MICROARCH.md's barrier-xcd form:
+// per-group arrival counters (group = blockIdx % 8), the last arriver of a group adds to the top
+// counter, every workgroup polls relaxed with s_sleep, one release before and one acquire after,
+// every spin bounded (a timed-out launch reports status 1 and exits).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ci_chisq.h"
+#include "pc_small.h"
+
+using namespace fbn;
+
+namespace {
+
+constexpr int BS = 512;             // threads per workgroup, one workgroup per CU
+constexpr int NWAVE = BS / 64;
+constexpr int kHistCells = 4096;    // 4^(kSmallMaxD + 2)
+constexpr int kMaxZ = 256;          // 4^kSmallMaxD conditioning configurations
+constexpr int kTermChunk = 1024;
+constexpr int kGroups = 8;          // barrier groups (blockIdx % 8: the XCD when dispatch is round-robin)
+constexpr long long kSpinTicks = 200000000ll;  // wall_clock64 ticks (100 MHz): 2 s per barrier
+
+typedef __attribute__((ext_vector_type(4))) unsigned u4;
+
+struct Lds {
+    uint64_t adj[kSmallMaxVars];
+    int32_t rowoff[kSmallMaxVars + 1];     // edges of rows before x
+    int32_t eoff[kSmallMaxEdges + 1];      // first test of each edge
+    uint8_t ex[kSmallMaxEdges], ey[kSmallMaxEdges], rm[kSmallMaxEdges];
+    int32_t binom[kSmallMaxVars + 1][kSmallMaxD + 1];
+    int32_t wscan[NWAVE];
+    long long wsum[NWAVE];
+    int32_t E;
+    long long T;
+    int flag;
+    // one workgroup-wide test (d >= 2)
+    int32_t hist[kHistCells];
+    int32_t ni[kMaxZ * 4], nj[kMaxZ * 4], nk[kMaxZ], dfp[kMaxZ];
+    double term[kTermChunk];
+    double red[2 * NWAVE];
+    int redi[NWAVE];
+    int32_t wtab[NWAVE][64];  // one test per wave (d <= 1): the wave's table
+    int dec;
+    double g2;
+};
+
+__device__ __forceinline__ int popc64(uint64_t v) { return __popcll(v); }
+
+// the k-th (0-based) set bit of m
+__device__ __forceinline__ int select_bit(uint64_t m, int k) {
+    for (int j = 0; j < k; ++j) m &= m - 1;
+    return __ffsll((unsigned long long)m) - 1;
+}
+
+__device__ __forceinline__ int binom_l(const Lds &L, int m, int k) {
+    return (m < 0 || k < 0 || m < k) ? 0 : L.binom[m][k];
+}
+
+// test k of edge (x, y) at level d >= 1 -> its conditioning set z[0..d-1] (ascending): sets of
+// adj(x)\{y} first, then of adj(y)\{x}; lexicographic unranking = ChoiceGenerator::Next order
+__device__ __forceinline__ void unrank(const Lds &L, int x, int y, int d, int k, int *z) {
+    const uint64_t ax = L.adj[x] & ~(1ull << y), ay = L.adj[y] & ~(1ull << x);
+    const int m0 = popc64(ax);
+    const int c0 = binom_l(L, m0, d);
+    uint64_t base = ax;
+    int m = m0;
+    if (k >= c0) base = ay, m = popc64(ay), k -= c0;
+    int p = 0;
+    for (int i = 0; i < d; ++i) {
+        while (true) {
+            const int cnt = binom_l(L, m - p - 1, d - i - 1);
+            if (k < cnt) break;
+            k -= cnt;
+            ++p;
+        }
+        const int v = select_bit(base, p);
+        z[i] = v < 0 ? 0 : v;  // (never: k < C(m, d) by construction; no out-of-range variable either way)
+        ++p;
+    }
+}
+
+__device__ __forceinline__ int pair_index(int n, int x, int y) {  // x < y
+    return x * n - x * (x + 1) / 2 + (y - x - 1);
+}
+
+// ---- grid barrier (barrier-xcd form), phase = 1, 2, ...
+struct Barrier {
+    unsigned *grp;   // kGroups arrival counters, each on its own 64-B line (stride 16)
+    unsigned *top;   // groups done
+    int nblocks;
+};
+
+__device__ bool grid_barrier(const Barrier &B, unsigned phase, Lds &L) {
+    // every wave's stores are complete before the workgroup's release
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int g = blockIdx.x % kGroups;
+        const int ngroups = B.nblocks < kGroups ? B.nblocks : kGroups;
+        const unsigned gsize = (unsigned)((B.nblocks - g + kGroups - 1) / kGroups);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old = __hip_atomic_fetch_add(B.grp + 16 * g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == phase * gsize - 1)  // last of its group in this phase: the group arrives
+            __hip_atomic_fetch_add(B.top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned target = phase * (unsigned)ngroups;
+        const long long t0 = wall_clock64();
+        int ok = 1;
+        while (__hip_atomic_load(B.top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(2);
+            if (wall_clock64() - t0 > kSpinTicks) {
+                ok = 0;
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        L.flag = ok;
+    }
+    __syncthreads();
+    return L.flag != 0;
+}
+
+// ---- block-wide helpers
+__device__ __forceinline__ long long block_sum_ll(long long v, Lds &L) {
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) L.wsum[threadIdx.x >> 6] = v;
+    __syncthreads();
+    long long s = 0;
+#pragma unroll
+    for (int w = 0; w < NWAVE; ++w) s += L.wsum[w];
+    return s;
+}
+
+__device__ __forceinline__ unsigned long long block_min_u64(unsigned long long v, Lds &L) {
+    for (int o = 32; o >= 1; o >>= 1) {
+        const unsigned long long u = __shfl_xor(v, o);
+        v = u < v ? u : v;
+    }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) L.wsum[threadIdx.x >> 6] = (long long)v;
+    __syncthreads();
+    unsigned long long m = ~0ull;
+#pragma unroll
+    for (int w = 0; w < NWAVE; ++w) m = (unsigned long long)L.wsum[w] < m ? (unsigned long long)L.wsum[w] : m;
+    return m;
+}
+
+// exclusive scan of v over the workgroup (thread order); returns the thread's offset, *total
+__device__ __forceinline__ int block_excl_scan(int v, Lds &L, int *total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    __syncthreads();
+    if (lane == 63) L.wscan[w] = x;
+    __syncthreads();
+    int before = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NWAVE; ++i) {
+        before += i < w ? L.wscan[i] : 0;
+        tot += L.wscan[i];
+    }
+    *total = tot;
+    return before + x - v;
+}
+
+// ---- G^2 decision, shared by the wave and workgroup paths.  The reference (src/IndependenceTest.cpp
+// :94-155, 295-364) forms G^2 as one running sum over cells z -> x -> y and p = 1 - pchisq(G^2, df),
+// independent iff p > alpha (df == 0: independent, p = 1).  `gs` / `ga` = tree sum of the terms and
+// of their magnitudes: with the decision band [lo, hi] (ci_chisq.h) a tree sum clearing it by the
+// tree-vs-in-order error bound decides exactly; otherwise *need_inorder and the caller sums in order.
+struct Decision {
+    int ind;        // -1: undecided (in-order sum needed)
+    double margin;  // |p - alpha| as logged
+};
+
+__device__ __forceinline__ Decision decide_tree(double gs, double ga, int df, int cells, const PcSmallArgs &A) {
+    if (df == 0) return Decision{1, fabs(1.0 - A.alpha)};
+    if (A.band && df <= A.nband) {
+        const double err = (cells + 64) * 2.3e-16 * ga;
+        if (gs + err < A.band[2 * df - 2]) return Decision{1, A.band[2 * A.nband]};
+        if (gs - err > A.band[2 * df - 1]) return Decision{0, A.band[2 * A.nband]};
+    }
+    return Decision{-1, 0.0};
+}
+
+__device__ __noinline__ Decision decide_exact(double g2, int df, const PcSmallArgs &A) {
+    if (df == 0) return Decision{1, fabs(1.0 - A.alpha)};
+    if (A.band && df <= A.nband && g2 < A.band[2 * df - 2]) return Decision{1, A.band[2 * A.nband]};
+    if (A.band && df <= A.nband && g2 > A.band[2 * df - 1]) return Decision{0, A.band[2 * A.nband]};
+    const double p = fbn_chisq_pvalue(g2, df);
+    return Decision{p > A.alpha ? 1 : 0, fabs(p - A.alpha)};
+}
+
+__device__ __forceinline__ double g2_term(long observed, long sum_row, long sum_col, long total) {
+    if (total == 0 || sum_row == 0 || sum_col == 0 || observed == 0) return 0.0;
+    const double expected = (double)sum_col * (double)sum_row / (double)total;
+    return 2.0 * observed * log(observed / expected);
+}
+
+// ---- one test per wave on the bit-sliced store (d = 0: marginal; d = 1: one conditioning
+// variable).  Leading-value popcounts only: the last value of every variable follows from the
+// per-row sample counts (d = 0) or from the level-0 pair tables (d = 1), integers, exact.  The
+// table is completed in the wave's LDS slot, cell l = (c * dx + a) * dy + b (Counts3D layout,
+// src/CellTable.cpp:277-281), in dependency order: leading cells, then the last y value of every
+// leading (z, x) row, then the last x value of every leading z slice, then the last z slice.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int D>
+__device__ __noinline__ Decision wave_test(const PcSmallArgs &A, int x, int y, int z, int lane, bool record_pair,
+                              int32_t *tab) {
+    const int n = A.nvars;
+    const int dx = A.dims[x], dy = A.dims[y], dz = D == 1 ? A.dims[z] : 1;
+    const int mx = dx - 1, my = dy - 1, mz = D == 1 ? dz - 1 : 1;
+    const long long W = A.W;
+    const uint32_t *bx = A.bits + (size_t)A.row0[x] * W, *by = A.bits + (size_t)A.row0[y] * W;
+    const uint32_t *bz = D == 1 ? A.bits + (size_t)A.row0[z] * W : bx;
+    constexpr int MZ = D == 1 ? 3 : 1;
+    uint32_t cnt[MZ][3][3];
+#pragma unroll
+    for (int c = 0; c < MZ; ++c)
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int b = 0; b < 3; ++b) cnt[c][a][b] = 0u;
+    for (long long w4 = lane; 4 * w4 < W; w4 += 64) {
+        u4 xv[3], yv[3], zv[MZ];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) xv[a] = a < mx ? *reinterpret_cast<const u4 *>(bx + a * W + 4 * w4) : u4{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int b = 0; b < 3; ++b) yv[b] = b < my ? *reinterpret_cast<const u4 *>(by + b * W + 4 * w4) : u4{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int c = 0; c < MZ; ++c) {
+            if (D == 1) zv[c] = c < mz ? *reinterpret_cast<const u4 *>(bz + c * W + 4 * w4) : u4{0u, 0u, 0u, 0u};
+            else zv[c] = u4{~0u, ~0u, ~0u, ~0u};
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    const uint32_t xy = xv[a][k] & yv[b][k];
+#pragma unroll
+                    for (int c = 0; c < MZ; ++c) cnt[c][a][b] += __builtin_popcount(xy & zv[c][k]);
+                }
+    }
+    // leading cells: wave totals straight into the table
+#pragma unroll
+    for (int c = 0; c < MZ; ++c)
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int b = 0; b < 3; ++b) {
+                if (c >= mz || a >= mx || b >= my) continue;  // wave-uniform
+                uint32_t v = cnt[c][a][b];
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+                if (lane == 0) tab[(c * dx + a) * dy + b] = (int32_t)v;
+            }
+    // margins of the full table, all exact integers
+    //   d = 0: N_x[a] = rowcnt(x, a), N_y[b] = rowcnt(y, b)
+    //   d = 1: N_xz(a, c), N_yz(b, c), N_xy(a, b) from the pair tables (u < v stored [u value][v value])
+    const int32_t *Txy = A.pairtab + 16 * (size_t)pair_index(n, x < y ? x : y, x < y ? y : x);
+    const int32_t *Txz = D == 1 ? A.pairtab + 16 * (size_t)pair_index(n, x < z ? x : z, x < z ? z : x) : Txy;
+    const int32_t *Tyz = D == 1 ? A.pairtab + 16 * (size_t)pair_index(n, y < z ? y : z, y < z ? z : y) : Txy;
+    auto nxz = [&](int a, int c) -> int {
+        if (D == 0) return A.rowcnt[A.row0[x] + a];
+        return x < z ? Txz[a * dz + c] : Txz[c * dx + a];
+    };
+    auto nyz = [&](int b, int c) -> int {
+        if (D == 0) return A.rowcnt[A.row0[y] + b];
+        return y < z ? Tyz[b * dz + c] : Tyz[c * dy + b];
+    };
+    const int dxy = dx * dy, cells = dz * dxy;
+    const int c = lane / dxy, a = (lane / dy) % dx, b = lane % dy;
+    const bool live = lane < cells;
+    wave_lds_sync();
+    // last y value of the leading (z, x) rows: N_xz(a, c) - sum of the row
+    if (live && c < mz && a < mx && b == my) {
+        int s = nxz(a, c);
+        for (int j = 0; j < my; ++j) s -= tab[(c * dx + a) * dy + j];
+        tab[lane] = s;
+    }
+    wave_lds_sync();
+    // last x value of the leading z slices: N_yz(b, c) - sum of the column
+    if (live && c < mz && a == mx) {
+        int s = nyz(b, c);
+        for (int i = 0; i < mx; ++i) s -= tab[(c * dx + i) * dy + b];
+        tab[lane] = s;
+    }
+    wave_lds_sync();
+    // last z slice (d = 1): N_xy(a, b) - the other slices
+    if (D == 1 && live && c == mz) {
+        int s = Txy[a * dy + b];  // x < y
+        for (int k = 0; k < mz; ++k) s -= tab[(k * dx + a) * dy + b];
+        tab[lane] = s;
+    }
+    wave_lds_sync();
+    const int ob = live ? tab[lane] : 0;
+    if (D == 0 && record_pair && live) A.pairtab[16 * (size_t)pair_index(n, x, y) + lane] = ob;
+    // marginals: N_{x+z} = N_xz, N_{+yz} = N_yz, N_{++z} = sum_a N_xz; adjusted df per z
+    // (src/IndependenceTest.cpp:96-112, 309-322)
+    double t = 0.0;
+    if (live) {
+        long tot = 0;
+        if (D == 0) tot = A.N;
+        else
+            for (int i = 0; i < dx; ++i) tot += nxz(i, c);
+        t = g2_term(ob, nxz(a, c), nyz(b, c), tot);
+    }
+    int df = 0;
+    for (int k = 0; k < dz; ++k) {
+        int alx = 0, aly = 0;
+        for (int i = 0; i < dx; ++i) alx += nxz(i, k) > 0;
+        for (int j = 0; j < dy; ++j) aly += nyz(j, k) > 0;
+        df += ((alx >= 1 ? alx : 1) - 1) * ((aly >= 1 ? aly : 1) - 1);
+    }
+    double gs = t, ga = fabs(t);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        gs += __shfl_xor(gs, o);
+        ga += __shfl_xor(ga, o);
+    }
+    Decision r = decide_tree(gs, ga, df, cells, A);
+    if (r.ind < 0) {  // in the band: the reference's in-order running sum, then p
+        double g2 = 0.0;
+        for (int l = 0; l < cells; ++l) g2 += __shfl(t, l);
+        r = decide_exact(g2, df, A);
+    }
+    wave_lds_sync();  // the slot is reused by the wave's next test
+    return r;
+}
+
+// ---- one test per workgroup (d >= 2): LDS histogram of the 2-bit packed columns.  z index with
+// the LAST conditioning variable fastest (src/CellTable.cpp:39-51, 277-281).
+template <int D>
+__device__ __noinline__ Decision block_test(const PcSmallArgs &A, int x, int y, const int *z, Lds &L) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int dx = A.dims[x], dy = A.dims[y];
+    int cum[D], dimz = 1;
+#pragma unroll
+    for (int j = D - 1; j >= 0; --j) cum[j] = dimz, dimz *= A.dims[z[j]];
+    const int dxy = dx * dy, cells = dimz * dxy;
+    // sub-histogram copies: each wave adds into copy (wave mod copies), fewer same-cell conflicts
+    int copies = 1;
+    while (copies < NWAVE && 2 * copies * cells <= kHistCells) copies *= 2;
+    int32_t *hist = L.hist;
+    for (int i = tid; i < copies * cells; i += BS) hist[i] = 0;
+    __syncthreads();
+    int32_t *my = hist + (wv & (copies - 1)) * cells;
+    const long long PW = A.PW, N = A.N;
+    const uint32_t *px = A.pk + (size_t)x * PW, *py = A.pk + (size_t)y * PW;
+    const uint32_t *pz[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) pz[j] = A.pk + (size_t)z[j] * PW;
+    for (long long w = tid; w < PW; w += BS) {
+        const uint32_t wx = px[w], wy = py[w];
+        uint32_t wz[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) wz[j] = pz[j][w];
+        const long long left = N - 16 * w;
+        const int lim = left < 16 ? (int)left : 16;
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            if (s >= lim) break;
+            int zi = 0;
+#pragma unroll
+            for (int j = 0; j < D; ++j) zi += (int)((wz[j] >> (2 * s)) & 3u) * cum[j];
+            const int cl = (zi * dx + (int)((wx >> (2 * s)) & 3u)) * dy + (int)((wy >> (2 * s)) & 3u);
+            atomicAdd(&my[cl], 1);
+        }
+    }
+    __syncthreads();
+    if (copies > 1) {
+        for (int i = tid; i < cells; i += BS) {
+            int v = 0;
+            for (int k = 0; k < copies; ++k) v += hist[k * cells + i];
+            hist[i] = v;
+        }
+        __syncthreads();
+    }
+    // marginals N_{x+z}, N_{+yz}, N_{++z}, adjusted df per z (src/CellTable.cpp:242-250,
+    // src/IndependenceTest.cpp:96-112)
+    for (int r = tid; r < dimz * dx; r += BS) {
+        const int k = r / dx, i = r % dx;
+        int s = 0;
+        for (int j = 0; j < dy; ++j) s += hist[k * dxy + i * dy + j];
+        L.ni[r] = s;
+    }
+    for (int r = tid; r < dimz * dy; r += BS) {
+        const int k = r / dy, j = r % dy;
+        int s = 0;
+        for (int i = 0; i < dx; ++i) s += hist[k * dxy + i * dy + j];
+        L.nj[r] = s;
+    }
+    __syncthreads();
+    for (int k = tid; k < dimz; k += BS) {
+        int alx = 0, aly = 0, tot = 0;
+        for (int i = 0; i < dx; ++i) alx += L.ni[k * dx + i] > 0, tot += L.ni[k * dx + i];
+        for (int j = 0; j < dy; ++j) aly += L.nj[k * dy + j] > 0;
+        L.dfp[k] = ((alx >= 1 ? alx : 1) - 1) * ((aly >= 1 ? aly : 1) - 1);
+        L.nk[k] = tot;
+    }
+    __syncthreads();
+    auto term_of = [&](int c) {
+        const int k = c / dxy, i = (c / dy) % dx, j = c % dy;
+        return g2_term(hist[c], L.ni[k * dx + i], L.nj[k * dy + j], L.nk[k]);
+    };
+    double ps = 0.0, pa = 0.0;
+    int pdf = 0;
+    for (int c = tid; c < cells; c += BS) {
+        const double t = term_of(c);
+        ps += t;
+        pa += fabs(t);
+    }
+    for (int k = tid; k < dimz; k += BS) pdf += L.dfp[k];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        ps += __shfl_xor(ps, o);
+        pa += __shfl_xor(pa, o);
+        pdf += __shfl_xor(pdf, o);
+    }
+    if (lane == 0) L.red[2 * wv] = ps, L.red[2 * wv + 1] = pa, L.redi[wv] = pdf;
+    __syncthreads();
+    double gs = 0.0, ga = 0.0;
+    int df = 0;
+#pragma unroll
+    for (int w = 0; w < NWAVE; ++w) gs += L.red[2 * w], ga += L.red[2 * w + 1], df += L.redi[w];
+    Decision r = decide_tree(gs, ga, df, cells, A);
+    if (r.ind < 0) {  // in-order running sum over z -> x -> y, chunk by chunk (terms in LDS)
+        double g2 = 0.0;
+        for (int c0 = 0; c0 < cells; c0 += kTermChunk) {
+            const int c1 = c0 + kTermChunk < cells ? c0 + kTermChunk : cells;
+            __syncthreads();
+            for (int c = c0 + tid; c < c1; c += BS) L.term[c - c0] = term_of(c);
+            __syncthreads();
+            if (tid == 0)
+                for (int c = 0; c < c1 - c0; ++c) g2 += L.term[c];
+        }
+        if (tid == 0) L.g2 = g2;
+        __syncthreads();
+        r = decide_exact(L.g2, df, A);
+    }
+    __syncthreads();  // LDS reused by the next test
+    return r;
+}
+
+// workgroup 0, at the end of the device's part of the search: the run's decision-margin log (over
+// every workgroup's slot) into the result and into the ctx's log, the level count, hand-off flag
+__device__ void finalize(const PcSmallArgs &A, Lds &L, int nb, int levels, int handoff) {
+    const int tid = threadIdx.x;
+    unsigned long long mm = ~0ull;
+    long long nn = 0;
+    for (int b = tid; b < nb; b += BS) {
+        const unsigned long long v = A.acc[8 * (size_t)b];
+        mm = v < mm ? v : mm;
+        nn += (long long)A.acc[8 * (size_t)b + 1];
+    }
+    mm = block_min_u64(mm, L);
+    nn = block_sum_ll(nn, L);
+    if (tid == 0) {
+        A.out->margin_bits = mm;
+        A.out->near = (unsigned long long)nn;
+        A.ctx_stats[0] = mm;
+        A.ctx_stats[1] = (unsigned long long)nn;
+        A.out->levels = levels;
+        A.out->handoff = handoff;
+        A.out->status = 0;
+    }
+}
+
+__global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) {
+    __shared__ Lds L;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int n = A.nvars;
+    const int nb = gridDim.x;
+    const int bid = blockIdx.x;
+    for (int i = tid; i < (kSmallMaxVars + 1) * (kSmallMaxD + 1); i += BS) {
+        const int m = i / (kSmallMaxD + 1), k = i % (kSmallMaxD + 1);
+        long long r = 1;
+        for (int j = 1; j <= k; ++j) r = r * (m - k + j) / j;
+        L.binom[m][k] = m < k ? 0 : (int)r;
+    }
+    for (int v = tid; v < kSmallMaxVars; v += BS) {
+        const uint64_t all = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
+        L.adj[v] = v < n ? (all & ~(1ull << v)) : 0ull;
+    }
+    __syncthreads();
+    // this workgroup's statistics slot: [0] min margin bits, [1] near, [2 + d] tests evaluated
+    unsigned long long wmin = ~0ull, wnear = 0ull;
+    unsigned long long *slot = A.acc + 8 * (size_t)bid;
+    unsigned phase = 0;
+    int32_t sep_cursor = 0;
+    for (int d = 0;; ++d) {
+        // ---- the level's edges (lexicographic pairs of the snapshot) and their test offsets
+        if (tid <= kSmallMaxVars) {
+            int c = 0;
+            if (tid > 0 && tid - 1 < n) {
+                const int x = tid - 1;
+                c = x + 1 < 64 ? popc64(L.adj[x] >> (x + 1)) : 0;
+            }
+            L.rowoff[tid] = c;  // counts, prefix-summed below
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int s = 0;
+            for (int i = 0; i <= kSmallMaxVars; ++i) s += L.rowoff[i], L.rowoff[i] = s;
+            L.E = s;  // rowoff[x] = edges of rows < x
+        }
+        __syncthreads();
+        const int E = L.E;
+        if (tid < n) {
+            const int x = tid;
+            uint64_t m = x + 1 < 64 ? (L.adj[x] >> (x + 1)) << (x + 1) : 0ull;
+            int e = L.rowoff[x];
+            while (m) {
+                const int y = __ffsll((unsigned long long)m) - 1;
+                m &= m - 1;
+                L.ex[e] = (uint8_t)x, L.ey[e] = (uint8_t)y;
+                ++e;
+            }
+        }
+        __syncthreads();
+        // tests per edge (level 0: one marginal test; level d: C(|adj(x)|-1, d) + C(|adj(y)|-1, d))
+        // -> exclusive offsets, in chunks of BS edges
+        long long tot64 = 0;
+        {
+            int carry = 0;
+            for (int e0 = 0; e0 < E; e0 += BS) {
+                const int e = e0 + tid;
+                int ne = 0;
+                if (e < E) {
+                    const int x = L.ex[e], y = L.ey[e];
+                    ne = d == 0 ? 1 : binom_l(L, popc64(L.adj[x]) - 1, d) + binom_l(L, popc64(L.adj[y]) - 1, d);
+                    tot64 += ne;
+                }
+                int total = 0;
+                const int off = block_excl_scan(ne, L, &total);
+                if (e < E) L.eoff[e] = carry + off;
+                carry += total;
+                __syncthreads();
+            }
+            if (tid == 0) L.eoff[E] = carry;
+        }
+        tot64 = block_sum_ll(tot64, L);
+        __syncthreads();
+        const bool fits = d <= kSmallMaxD && tot64 <= kSmallMaxTests;
+        if (!fits) {
+            // hand the search to the host driver at this level (its snapshot = adj after d - 1)
+            if (bid == 0) finalize(A, L, nb, d, 1);
+            return;
+        }
+        const int T = (int)tot64;
+        // ---- the tests
+        unsigned long long launched = 0;
+        if (d <= 1) {
+            const int gw = bid * NWAVE + wv, nw = nb * NWAVE;
+            for (int t = gw; t < T; t += nw) {
+                int lo = 0, hi = E;  // last edge whose first test <= t
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (L.eoff[mid] <= t) lo = mid;
+                    else hi = mid;
+                }
+                const int e = lo, k = t - L.eoff[e];
+                const int x = L.ex[e], y = L.ey[e];
+                Decision r;
+                if (d == 0) {
+                    r = wave_test<0>(A, x, y, 0, lane, true, L.wtab[wv]);
+                } else {
+                    int zz[1];
+                    unrank(L, x, y, 1, k, zz);
+                    r = wave_test<1>(A, x, y, zz[0], lane, false, L.wtab[wv]);
+                }
+                ++launched;
+                const unsigned long long mb = (unsigned long long)__double_as_longlong(r.margin);
+                wmin = mb < wmin ? mb : wmin;
+                wnear += r.margin < 1e-9;
+                if (r.ind == 1 && lane == 0)  // first[] holds ~min k (0 = none): max of the complements
+                    __hip_atomic_fetch_max(A.first + (size_t)d * kSmallMaxEdges + e, ~(unsigned)k, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else {
+            for (int t = bid; t < T; t += nb) {
+                int lo = 0, hi = E;
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (L.eoff[mid] <= t) lo = mid;
+                    else hi = mid;
+                }
+                const int e = lo, k = t - L.eoff[e];
+                const int x = L.ex[e], y = L.ey[e];
+                int zz[kSmallMaxD];
+                unrank(L, x, y, d, k, zz);
+                Decision r;
+                if (d == 2) r = block_test<2>(A, x, y, zz, L);
+                else if (d == 3) r = block_test<3>(A, x, y, zz, L);
+                else r = block_test<4>(A, x, y, zz, L);
+                if (tid == 0) {
+                    ++launched;
+                    const unsigned long long mb = (unsigned long long)__double_as_longlong(r.margin);
+                    wmin = mb < wmin ? mb : wmin;
+                    wnear += r.margin < 1e-9;
+                    if (r.ind == 1)
+                        __hip_atomic_fetch_max(A.first + (size_t)d * kSmallMaxEdges + e, ~(unsigned)k,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+        // this workgroup's statistics into its slot (plain stores, published by the barrier)
+        {
+            const unsigned long long mm = block_min_u64(lane == 0 ? wmin : ~0ull, L);
+            const long long nn = block_sum_ll(lane == 0 ? (long long)wnear : 0ll, L);
+            const long long ll = block_sum_ll(lane == 0 ? (long long)launched : 0ll, L);
+            if (tid == 0) {
+                slot[0] = mm;
+                slot[1] = (unsigned long long)nn;
+                slot[2 + d] = (unsigned long long)ll;
+            }
+        }
+        if (!grid_barrier(B, ++phase, L)) {
+            if (tid == 0) A.out->status = 1;
+            return;
+        }
+        // ---- apply: removed = some independent set found; counted = first + 1, else all sets
+        long long counted = 0;
+        for (int e = tid; e < E; e += BS) {
+            const unsigned f = ~__hip_atomic_load(A.first + (size_t)d * kSmallMaxEdges + e, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+            const bool rmv = f != ~0u;
+            L.rm[e] = rmv;
+            counted += rmv ? (long long)f + 1 : (long long)(L.eoff[e + 1] - L.eoff[e]);
+        }
+        counted = block_sum_ll(counted, L);
+        __syncthreads();
+        if (bid == 0) {
+            // sepsets of the removed edges in edge order (unranked against the level's snapshot)
+            int carry = 0;
+            for (int e0 = 0; e0 < E; e0 += BS) {
+                const int e = e0 + tid;
+                const int r = e < E ? L.rm[e] : 0;
+                int total = 0;
+                const int off = block_excl_scan(r, L, &total);
+                if (r && d > 0) {
+                    const unsigned f = ~__hip_atomic_load(A.first + (size_t)d * kSmallMaxEdges + e, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                    int zz[kSmallMaxD];
+                    unrank(L, L.ex[e], L.ey[e], d, (int)f, zz);
+                    for (int j = 0; j < d; ++j) A.out->pool[sep_cursor + (carry + off) * d + j] = zz[j];
+                }
+                carry += total;
+                __syncthreads();
+            }
+            if (tid == 0) {
+                A.out->sep_off[d] = sep_cursor;
+                A.out->sep_off[d + 1] = sep_cursor + carry * d;
+                A.out->counted[d] = counted;
+                long long la = 0;
+                for (int b = 0; b < nb; ++b) la += (long long)A.acc[8 * (size_t)b + 2 + d];
+                A.out->launched[d] = la;
+            }
+            sep_cursor += carry * d;
+        }
+        __syncthreads();
+        for (int e = tid; e < E; e += BS)
+            if (L.rm[e]) {
+                const int x = L.ex[e], y = L.ey[e];
+                atomicAnd((unsigned long long *)&L.adj[x], ~(1ull << y));
+                atomicAnd((unsigned long long *)&L.adj[y], ~(1ull << x));
+            }
+        __syncthreads();
+        int maxdeg = 0;
+        for (int v = 0; v < n; ++v) maxdeg = maxdeg > popc64(L.adj[v]) ? maxdeg : popc64(L.adj[v]);
+        if (bid == 0 && tid < kSmallMaxVars) A.out->adj[d][tid] = L.adj[tid];
+        const bool cont = d + 1 < A.depth && (d == 0 || maxdeg - 1 > d);  // FreeDegree (src/PCStable.cpp:557-563)
+        if (!cont) {
+            if (bid == 0) finalize(A, L, nb, d + 1, 0);
+            return;
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+extern "C" int fbn_pc_small_block_threads(void) { return BS; }
+
+extern "C" hipError_t fbn_pc_small_occupancy(int *blocks_per_cu) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, pc_small_kernel, BS, 0);
+}
+
+// a->bar: (kGroups * 16 + 16) unsigned words, zeroed by the caller before every launch
+extern "C" hipError_t fbn_pc_small_launch(const PcSmallArgs *a, int grid, hipStream_t s) {
+    Barrier b{a->bar, a->bar + 16 * kGroups, grid};
+    hipLaunchKernelGGL(pc_small_kernel, dim3(grid), dim3(BS), 0, s, *a, b);
+    return hipGetLastError();
+}

@@ -92,12 +92,20 @@ def _world_rank():
     return 1, 0
 
 
+def _force_exchange():
+    """FBN_PC_DIST_FORCE_EXCHANGE=1: run every collective of the level loop even at world size 1
+    (records and pair tables through the process group, device buffers with nccl), so a one-GPU box
+    executes the RCCL data paths an 8-GPU run takes.  Testing / rehearsal switch."""
+    import os
+    return os.environ.get("FBN_PC_DIST_FORCE_EXCHANGE", "0") not in ("", "0")
+
+
 def _all_gather_fixed(arr, device):
     """Every rank's equal-length int32 array, stacked in rank order -> numpy [world][len]."""
     import torch
     import torch.distributed as dist
     world, _ = _world_rank()
-    if world == 1:
+    if world == 1 and not (_force_exchange() and dist.is_available() and dist.is_initialized()):
         return arr[None, :]
     t = torch.from_numpy(arr)
     if device is not None:
@@ -116,6 +124,13 @@ def _exchange_pair_tables(sess, ci, device):
     import torch.distributed as dist
     world, _ = _world_rank()
     chunk = sess.pairs_chunk()
+    # 0: no pair tables were recorded (dataset not bit-slice eligible, or FBN_CI_NO_PAIRS).  That
+    # depends on the dataset only, but the ranks agree on it explicitly before any collective that
+    # assumes a chunk size: min over ranks, 0 -> every rank skips, level 1 counts without them
+    if world > 1 or _force_exchange():
+        chunk = int(_all_gather_fixed(np.array([chunk], np.int32), device).min())
+    if chunk == 0:
+        return
     on_dev = device is not None
     dev = torch.device(device) if on_dev else torch.device("cpu")
     inp = torch.zeros(chunk * 16, dtype=torch.int32, device=dev)
@@ -145,7 +160,7 @@ def pc_skeleton_distributed(engine, nvars, alpha=0.05, depth=1000, group_size=1,
             break
         d, b, e, L = lv
         rec = engine(sess, d, b, e, L)
-        if d == 0 and world > 1 and ci is not None:
+        if d == 0 and (world > 1 or _force_exchange()) and ci is not None:
             _exchange_pair_tables(sess, ci, device)
         if not sess.apply(_all_gather_fixed(rec, device)):
             break

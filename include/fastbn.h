@@ -265,7 +265,10 @@ int fbn_pc_dist_pack(fbn_pc_dist *s, const uint8_t *removed, const int32_t *seps
 /* Level 0 pair tables (16 int32 per pair) for the derived level-1 counting: after this rank's
  * level-0 run, export writes its chunk (pairs_chunk pairs, the tail zero-padded by the caller) to
  * buf; the caller all-gathers the chunks in rank order (pair index = offset / 16) and imports the
- * gathered buffer into its context.  buf in device (buf_on_device = 1) or host memory. */
+ * gathered buffer into its context.  buf in device (buf_on_device = 1) or host memory.
+ * pairs_chunk = 0: this rank's level 0 recorded no pair tables (the bit-sliced path was not eligible
+ * for the dataset, or FBN_CI_NO_PAIRS); the exchange is then skipped on every rank (eligibility
+ * depends on the dataset only) and level 1 counts without them. */
 int fbn_pc_dist_pairs_chunk(const fbn_pc_dist *s, int64_t *pairs_per_rank);
 int fbn_pc_dist_pairs_export(fbn_pc_dist *s, void *buf, int buf_on_device);
 int fbn_pc_dist_pairs_import(fbn_pc_dist *s, fbn_ci_ctx *c, const void *buf, int buf_on_device);
@@ -273,7 +276,10 @@ int fbn_pc_dist_pairs_import(fbn_pc_dist *s, fbn_ci_ctx *c, const void *buf, int
  * another level follows (depth and FreeDegree, src/PCStable.cpp:159-178). */
 int fbn_pc_dist_apply(fbn_pc_dist *s, const int32_t *records, int *more);
 /* After the last level: skeleton, sepsets, per-level counts (all ranks), this rank's kernel time /
- * decision margin, orientation (as fbn_pc_stable). */
+ * decision margin, orientation (as fbn_pc_stable).  Lifetime: the fbn_ci_ctx passed to
+ * fbn_pc_dist_run / _pairs_import must stay alive until the last fbn_pc_dist_apply (the one that
+ * reports no further level), which snapshots its margin log and drops its pair tables; result never
+ * touches it, so the ctx may be destroyed before this call. */
 int fbn_pc_dist_result(fbn_pc_dist *s, fbn_pc_result **out);
 int fbn_pc_dist_destroy(fbn_pc_dist *s);
 /* Roofline accounting: bytes of column data the CI kernels had to read for every launched test,

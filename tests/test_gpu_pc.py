@@ -50,10 +50,14 @@ def test_g2_df_p_vs_oracle(ci, alarm_paths):
             assert ind[k] == r["is_independent"]
 
 
-@pytest.mark.parametrize("gs", [1, 4])
-def test_pc_stable_alarm5000(alarm_ds, alarm_paths, gs):
+@pytest.mark.parametrize("gs,host", [(1, False), (1, True), (4, False)])
+def test_pc_stable_alarm5000(alarm_ds, alarm_paths, gs, host, monkeypatch):
+    """gs 1: the device-resident search (pc_small.hip, the default for <= 64 variables) and the
+    host-driven level loop (FBN_PC_NO_SMALL); gs 4: grouped tests (host-driven)."""
     od = O.OracleDataset(csv=alarm_paths["csv"])
     ref = od.pc_stable(0.05, 1000, gs)
+    if host:
+        monkeypatch.setenv("FBN_PC_NO_SMALL", "1")
     pc = F.PCStable(0.05, 1000).StructLearnCompData(alarm_ds, group_size=gs)
     assert pc.tests_per_level.tolist() == ref["tests_per_level"]
     assert pc.edges == ref["edges"]
@@ -74,6 +78,7 @@ def test_pc_stable_alarm5000_other_alphas(alarm_ds, alarm_paths, alpha, device_l
     restatement's."""
     od = O.OracleDataset(csv=alarm_paths["csv"])
     ref = od.pc_stable(alpha, 3, 1)
+    monkeypatch.setenv("FBN_PC_NO_SMALL", "1")  # the host-driven level loop (pc_small: test_gpu_pc_small.py)
     if device_l1:
         monkeypatch.setenv("FBN_PC_FULLSPEC", "0")
     pc = F.PCStable(alpha, 3).StructLearnCompData(alarm_ds)
@@ -89,6 +94,7 @@ def test_level1_generators_agree(alarm_ds, alarm_paths, fullspec, monkeypatch):
     (FBN_PC_GEN_GENERAL) launch the same tests and give the restatement's result."""
     od = O.OracleDataset(csv=alarm_paths["csv"])
     ref = od.pc_stable(0.05, 1000, 1)
+    monkeypatch.setenv("FBN_PC_NO_SMALL", "1")  # the host-driven level loop
     monkeypatch.setenv("FBN_PC_HOST_L1", "1")  # level 1 through the host rounds
     if not fullspec:
         monkeypatch.setenv("FBN_PC_FULLSPEC", "0")
@@ -111,6 +117,7 @@ def test_pc_stable_alarm5000_pipelined_rounds(alarm_ds, alarm_paths, gs, staged,
     every round through the per-slot device buffers and DMA copies instead of zero-copy."""
     od = O.OracleDataset(csv=alarm_paths["csv"])
     ref = od.pc_stable(0.05, 1000, gs)
+    monkeypatch.setenv("FBN_PC_NO_SMALL", "1")  # the host-driven level loop
     monkeypatch.setenv("FBN_PC_FULLSPEC", "0")
     monkeypatch.setenv("FBN_PC_PIPELINE_EDGES", "1")
     if staged:
@@ -129,6 +136,7 @@ def test_pc_stable_alarm5000_bit_sliced_pair_tables(alarm_ds, alarm_paths, pairs
     (ci_bits_count_derived) -- identical counts, skeleton and sepsets to the restatement."""
     od = O.OracleDataset(csv=alarm_paths["csv"])
     ref = od.pc_stable(0.05, 1000, 1)
+    monkeypatch.setenv("FBN_PC_NO_SMALL", "1")  # the host-driven level loop
     monkeypatch.setenv("FBN_CI_FORCE_BITS", "1")
     if not pairs:
         monkeypatch.setenv("FBN_CI_NO_PAIRS", "1")
@@ -376,11 +384,12 @@ def test_level0_batches_and_device_compaction_match_single_batch():
     assert a.oriented == b.oriented
 
 
-def test_g2_bit_exact_every_alarm5000_test(ci, alarm_paths):
+def test_g2_within_1e12_every_alarm5000_test(ci, alarm_paths):
     """Every CI test the reference's PC-stable run executes on ALARM-5000 (5206 tests, levels 0-4,
-    from the restatement's log): G^2 bit-identical (the reference's single running sum over
-    z -> x -> y, src/IndependenceTest.cpp:94-138), df and decisions identical, p within 1e-12
-    (pchisq parity unpinned)."""
+    from the restatement's log): G^2 within 1e-12 of max(1, |G^2|) -- the reference's single running
+    sum over z -> x -> y (src/IndependenceTest.cpp:94-138) of the same terms; only the last bit of a
+    term's log can differ (device log vs glibc's; north star: 1e-6) -- df and decisions
+    identical, p within 1e-12 (pchisq parity unpinned)."""
     od = O.OracleDataset(csv=alarm_paths["csv"])
     ref = od.pc_stable(0.05, 1000, 1, keep_log=True)
     by_d = {}

@@ -137,3 +137,71 @@ def test_config5_two_ranks_vs_fixture(tmp_path):
     got = json.load(open(out))
     assert got["tests"] == ref["tests_per_level"]
     assert {k: got[k] for k in ("edges_sha256", "sepsets_sha256")} == {k: ref[k] for k in ("edges_sha256", "sepsets_sha256")}
+
+
+@pytest.mark.parametrize("knob", ["FBN_CI_NO_PAIRS", "FBN_CI_NO_BITS"])
+def test_two_ranks_without_pair_tables(tmp_path, monkeypatch, knob):
+    """when level 0 records no pair tables (no bit-sliced path for the dataset, or pair
+    tables switched off) fbn_pc_dist_pairs_chunk reports 0 and every rank skips the exchange; level
+    1 then counts without them.  Two ranks (gloo, sharing the test GPU) = the single-GPU driver."""
+    import torch.multiprocessing as mp
+    monkeypatch.setenv(knob, "1")  # inherited by the spawned ranks
+    out = str(tmp_path / "r.npy")
+    mp.start_processes(_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    edges, sep, tests, oriented, shd = np.load(out, allow_pickle=True)  # written by this test's worker
+    pc = F.PCStable(0.05, 1000).StructLearnCompData(F.Dataset(CSV))
+    assert [tuple(e) for e in edges] == pc.edges
+    assert dict(sep) == pc.sepset
+    assert list(tests) == pc.tests_per_level.tolist()
+    assert [tuple(o) for o in oriented] == pc.oriented and shd == 5
+
+
+def _worker_nccl(rank, world, port, out):
+    """One rank of an RCCL ("nccl") process group on the box's GPU: configs 3 and 5 through the
+    device-memory broadcast of the column store and the distributed session with every collective
+    forced through the group (device all-gathers of the records and of the pair tables)."""
+    import json
+    import torch
+    import torch.distributed as dist
+    from conftest import pc_digest
+    from fastbn_amd import pc_dist, synth
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["FBN_PC_DIST_FORCE_EXCHANGE"] = "1"
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    got = {}
+    ds = F.Dataset(CSV)
+    ci = pc_dist.independence_test_broadcast(ds.columns, [int(v) for v in ds.dims], [ds.num_vars, ds.num_instance])
+    res, tests, _ = pc_dist.pc_stable_distributed(ci, 37, device="cuda:0")
+    got["alarm"] = {"tests": tests, **pc_digest(res.edges, res.sepset), "shd": res.GetSHD(BIF)}
+    cols, dims = synth.config5_dataset()
+    ci5 = pc_dist.independence_test_broadcast(cols, [int(v) for v in dims], list(cols.shape))
+    res5, tests5, _ = pc_dist.pc_stable_distributed(ci5, 1000, 0.05, 6, device="cuda:0")
+    got["c5"] = {"tests": tests5, **pc_digest(res5.edges, res5.sepset)}
+    if rank == 0:
+        with open(out, "w") as f:
+            json.dump(got, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_nccl_world1_forced_exchange_configs_3_and_5(tmp_path):
+    """the RCCL data paths of the multi-GPU PC loop executed on one GPU -- an
+    "nccl" process group of world size 1, the column store broadcast into device memory
+    (independence_test_broadcast), the records and the level-0 pair tables all-gathered through
+    RCCL on the device (FBN_PC_DIST_FORCE_EXCHANGE: fbn_pc_dist_pairs_export / _import with
+    buf_on_device = 1).  ALARM-5000 = the single-GPU driver, config 5 = tests/golden/pc_c5.json."""
+    import json
+    import torch.multiprocessing as mp
+    from conftest import pc_digest
+    out = str(tmp_path / "nccl.json")
+    mp.start_processes(_worker_nccl, args=(1, _free_port(), out), nprocs=1, join=True, start_method="spawn")
+    got = json.load(open(out))
+    pc = F.PCStable(0.05, 1000).StructLearnCompData(F.Dataset(CSV))
+    assert got["alarm"]["tests"] == pc.tests_per_level.tolist() and got["alarm"]["shd"] == 5
+    assert {k: got["alarm"][k] for k in ("edges_sha256", "sepsets_sha256")} == pc_digest(pc.edges, pc.sepset)
+    ref = json.load(open(os.path.join(GOLD, "pc_c5.json")))
+    assert got["c5"]["tests"] == ref["tests_per_level"]
+    assert {k: got["c5"][k] for k in ("edges_sha256", "sepsets_sha256")} == \
+        {k: ref[k] for k in ("edges_sha256", "sepsets_sha256")}

@@ -1,0 +1,114 @@
+"""The device-resident PC-stable skeleton search for small graphs (fastbn_amd/csrc/pc_small.hip: one
+launch runs every level, one grid barrier per level) against the restatement (oracle/pc_oracle.cpp)
+and against the host-driven level loop (FBN_PC_NO_SMALL): tests per level, skeleton (vec_edges
+order), sepsets, orientation; launched = every candidate set of every edge (full speculation)."""
+import os
+
+import numpy as np
+import pytest
+from conftest import GOLD
+
+import fastbn_amd as F
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+CSV = os.path.join(GOLD, "alarm", "alarm_s5000.txt")
+
+
+def _host(ds, alpha, depth, monkeypatch):
+    monkeypatch.setenv("FBN_PC_NO_SMALL", "1")
+    try:
+        return F.PCStable(alpha, depth).StructLearnCompData(ds)
+    finally:
+        monkeypatch.delenv("FBN_PC_NO_SMALL")
+
+
+def _check(ds, od, alpha, depth, monkeypatch, host=True):
+    ref = od.pc_stable(alpha, depth, 1)
+    pc = F.PCStable(alpha, depth).StructLearnCompData(ds)
+    assert pc.tests_per_level.tolist() == ref["tests_per_level"]
+    assert pc.edges == ref["edges"]
+    assert pc.sepset == ref["sepset"]
+    if host:
+        h = _host(ds, alpha, depth, monkeypatch)
+        assert pc.tests_per_level.tolist() == h.tests_per_level.tolist()
+        assert pc.edges == h.edges and pc.sepset == h.sepset and pc.oriented == h.oriented
+    return pc
+
+
+@pytest.fixture(scope="module")
+def alarm():
+    return F.Dataset(CSV), O.OracleDataset(csv=CSV)
+
+
+def test_alarm5000_default_is_device_resident(alarm, monkeypatch):
+    ds, od = alarm
+    pc = _check(ds, od, 0.05, 1000, monkeypatch)
+    assert pc.tests_per_level.tolist() == [666, 3579, 828, 118, 15] and len(pc.edges) == 44
+    # every candidate set of every edge is evaluated once: the host driver's one-round schedule
+    assert pc.launched_per_level.tolist() == [666, 8732, 1212, 128, 15]
+    assert pc.GetSHD(os.path.join(GOLD, "alarm", "alarm.bif")) == 5
+    assert pc.near_alpha == 0 and pc.min_margin > 1e-9
+
+
+@pytest.mark.parametrize("alpha", [0.0, 0.001, 0.01, 0.2, 0.5, 1.0])
+def test_alarm5000_alphas(alarm, alpha, monkeypatch):
+    ds, od = alarm
+    _check(ds, od, alpha, 1000, monkeypatch)
+
+
+@pytest.mark.parametrize("depth", [1, 2, 3, 4])
+def test_alarm5000_depths(alarm, depth, monkeypatch):
+    ds, od = alarm
+    pc = _check(ds, od, 0.05, depth, monkeypatch)
+    assert len(pc.tests_per_level) == depth
+
+
+@pytest.mark.parametrize("ns,nv", [(1, 6), (33, 12), (4999, 40), (20011, 64)])
+def test_synthetic_ragged_sizes(tmp_path, ns, nv, monkeypatch):
+    """Ragged sample counts (bit-sliced tail words, 2-bit packed tail), up to the 64-variable cap."""
+    from fastbn_amd import synth
+    p = str(tmp_path / "s.xml")
+    synth.random_network(nv, seed=ns, window=6, dom=(2, 4), path=p)
+    cols = synth.forward_sample(synth.read_xmlbif(p), ns, seed=ns + 1)
+    dims = np.maximum(cols.max(axis=1).astype(np.int32) + 1, 1)
+    assert dims.max() <= 4  # eligible for the device-resident search
+    ds = F.Dataset(columns=cols, dims=dims)
+    _check(ds, O.OracleDataset(columns=cols, dims=dims), 0.05, 1000, monkeypatch)
+
+
+def test_dense_graph_hands_off_to_host_at_level_5(monkeypatch):
+    """Twelve noisy copies of one latent variable: nothing is independent, so the search reaches
+    level 5, which the device kernel hands to the host driver (levels 0-4 on the device)."""
+    rng = np.random.default_rng(7)
+    base = rng.integers(0, 4, 3000)
+    cols = np.stack([(base + (rng.random(3000) < 0.2) * rng.integers(0, 4, 3000)) % 4 for _ in range(12)])
+    cols = cols.astype(np.uint8)
+    dims = np.full(12, 4, np.int32)
+    ds = F.Dataset(columns=cols, dims=dims)
+    pc = _check(ds, O.OracleDataset(columns=cols, dims=dims), 0.05, 8, monkeypatch)
+    assert len(pc.tests_per_level) >= 6
+
+
+def test_constant_and_two_state_columns(monkeypatch):
+    """1-state (constant) columns (df 0: independent) next to 2..4-state ones."""
+    rng = np.random.default_rng(3)
+    dims = np.array([1, 2, 3, 4, 2, 1, 4, 3], np.int32)
+    cols = np.stack([rng.integers(0, d, 6000) for d in dims]).astype(np.uint8)
+    cols[2] = (cols[1] + cols[3]) % 3
+    cols[6] = (cols[3] + cols[4]) % 4
+    ds = F.Dataset(columns=cols, dims=dims)
+    _check(ds, O.OracleDataset(columns=cols, dims=dims), 0.05, 1000, monkeypatch)
+
+
+def test_repeated_runs_and_context_margin_log(alarm):
+    """Back-to-back runs on one context reuse its scratch (re-zeroed per launch): identical results;
+    the ctx-level margin log afterwards holds the run's log."""
+    ds, _ = alarm
+    ci = F.IndependenceTest(ds)
+    runs = [F.PCStable(0.05, 1000).StructLearnCompData(ci) for _ in range(3)]
+    for r in runs[1:]:
+        assert r.edges == runs[0].edges and r.sepset == runs[0].sepset
+        assert r.tests_per_level.tolist() == runs[0].tests_per_level.tolist()
+    m, near = ci.decision_margin()
+    assert m == runs[-1].min_margin and near == runs[-1].near_alpha
