@@ -56,6 +56,7 @@ _SIGS = {
     "fbn_ci_counts": [_vp, C.c_int, C.c_int, _vp, C.c_int, _vp, _i64, _vp],
     "fbn_ci_last_kernel_ms": [_vp, _vp],
     "fbn_ci_decision_margin": [_vp, _vp, _vp, C.c_int],
+    "fbn_ci_debug_counts": [_vp, _vp, _i64, C.c_int, _vp, _i64],
     "fbn_pc_decision_margin": [_vp, _vp, _vp],
     "fbn_ci_ctx_destroy": [_vp],
     "fbn_pc_stable": [_vp, _dbl, C.c_int, C.c_int, _pp],
@@ -386,6 +387,7 @@ class IndependenceTest:
 
     def __init__(self, dataset, alpha=0.05, device=0):
         self.alpha = alpha
+        self.dims = np.ascontiguousarray(dataset.dims, np.int32)
         h = C.c_void_p()
         lib.fbn_ci_dataset_upload(_p(dataset.columns), dataset.num_vars, dataset.num_instance,
                                   _p(dataset.dims), device, C.byref(h))
@@ -398,6 +400,7 @@ class IndependenceTest:
         self = cls.__new__(cls)
         self.alpha = alpha
         dims = np.ascontiguousarray(dims, np.int32)
+        self.dims = dims
         h = C.c_void_p()
         lib.fbn_ci_dataset_from_device(C.c_void_p(d_cols_ptr), int(nvars), int(nsamples), _p(dims), device,
                                        C.byref(h))
@@ -435,6 +438,18 @@ class IndependenceTest:
     def IndependenceResult(self, x, y, z=()):
         g2, df, p, ind = self.run(np.array([[x, y, *z]], np.int32), len(z))
         return {"g2": g2[0], "df": int(df[0]), "p_value": p[0], "is_independent": bool(ind[0])}
+
+    def production_counts(self, items, d, cap=None):
+        """Counts of the tests `items` [n][2+d] through the kernels a PC run uses at level d
+        (fbn_ci_debug_counts: level-0 Gram + pair tables, derived level-1 counting, histogram
+        kernel) -> int32 [n][cap] (Counts3D order; cells beyond a test's table are 0)."""
+        items = np.ascontiguousarray(items, np.int32).reshape(-1, 2 + d)
+        if cap is None:
+            dims = np.asarray(self.dims)
+            cap = int(np.max(np.prod(dims[items], axis=1))) if len(items) else 1
+        out = np.zeros((len(items), cap), np.int32)
+        lib.fbn_ci_debug_counts(self._h, _p(items), len(items), d, _p(out), cap)
+        return out
 
     def counts(self, x, y, z=()):
         zz = np.array(z, np.int32)

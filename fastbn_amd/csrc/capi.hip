@@ -27,7 +27,7 @@ extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, co
                                     uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
                                     int32_t *gscratch, unsigned long long *stats, const uint32_t *bits,
                                     const int32_t *row0, long long W, const double *band, int nband,
-                                    const uint32_t *pk, long long PW, hipStream_t stream);
+                                    const uint32_t *pk, long long PW, long long cstride, hipStream_t stream);
 extern "C" hipError_t fbn_ci_pack2_build(const uint8_t *cols, int nvars, long long N, long long PW, uint32_t *pk,
                                          hipStream_t stream);
 extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy);
@@ -253,6 +253,8 @@ struct fbn_ci_ctx {
     // pinned result record the kernel writes
     DevBuf small_scr;
     fbn::PcSmallOut *h_small = nullptr;
+    // fbn_ci_debug_counts: the histogram kernel writes every test's table (stride in ints), 0 off
+    int64_t counts_stride = 0;
     // decision band of the bit-sliced G^2 kernel for alpha = band_alpha (ci_chisq.h fbn_chisq_band):
     // [lo, hi] per df 1..kBandDf, then delta; host copy kept alive for the async upload
     DevBuf band;
@@ -1528,7 +1530,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
                                  want_g2p ? c->p.as<double>() : nullptr, zc_indep ? zc_indep : S.indep.as<uint8_t>(),
                                  counts_dev, lds, grid, gscratch, c->stats.as<unsigned long long>(),
                                  bitsn ? c->bits.as<uint32_t>() : nullptr, c->brow.as<int32_t>(), c->bits_W, hband,
-                                 hnband, pk ? c->pack2.as<uint32_t>() : nullptr, c->pack2_W, s);
+                                 hnband, pk ? c->pack2.as<uint32_t>() : nullptr, c->pack2_W, c->counts_stride, s);
     if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci kernel launch: %s", hipGetErrorString(e));
     if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
     return FBN_OK;
@@ -1568,6 +1570,73 @@ int fbn_ci_counts(fbn_ci_ctx *c, int x, int y, const int32_t *z, int d, int32_t 
     if (rc) return rc;
     if (counts) FBN_HIP(hipMemcpy(counts, c->counts.p, (size_t)std::min(nc, cap) * 4, hipMemcpyDeviceToHost));
     FBN_HIP(hipDeviceSynchronize());
+    return FBN_OK;
+}
+
+// Counts of n tests through the kernels a PC run uses at level d (parity pinning of the production
+// paths): d = 0 the complete-graph level-0 batch (the Gram of the leading mask rows, then every
+// pair's table, recorded for level 1), d = 1 the derived counting from those recorded pair tables
+// (the level-0 batch runs first if none are recorded), d >= 2 the histogram kernel over one batch.
+// counts [n][cap]: test t's table in Counts3D order, cells beyond it untouched.
+int fbn_ci_debug_counts(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, int32_t *counts, int64_t cap) {
+    if (!c || (!items && n > 0) || n < 0 || d < 0 || d > 8 || (!counts && n > 0) || cap < 1)
+        return SetError(FBN_ERR_ARG, "bad argument");
+    if (n == 0) return FBN_OK;
+    const int w = 2 + d;
+    for (int64_t i = 0; i < n * w; ++i)
+        if ((unsigned)items[i] >= (unsigned)c->nvars) return SetError(FBN_ERR_ARG, "variable out of range");
+    FBN_HIP(hipSetDevice(c->device));
+    int rc;
+    const int nv = c->nvars;
+    fbn::PCResultHost scratch;
+    auto level0 = [&]() -> int {  // the PC run's level 0, pair tables recorded
+        fbn::CiBatchStats st{0, 0};
+        for (int v = 0; v < nv; ++v) st.dim_rows += (int64_t)(nv - 1) * c->dims[v], st.maxdim = std::max(st.maxdim, (int)c->dims[v]);
+        if (!fbn::CiAllPairsEligible(c, st))
+            return SetError(FBN_ERR_ARG, "dataset not eligible for the bit-sliced level-0 path");
+        const int64_t P = (int64_t)nv * (nv - 1) / 2;
+        fbn::CiSetPairMode(c, 1);
+        int r = fbn::CiBatchLaunchAllPairs(c, 0.05, &st, 0, P);
+        std::vector<uint8_t> flags((size_t)P);
+        if (!r) r = fbn::CiBatchWait(c, 0, flags.data(), nullptr, scratch);
+        if (!r) fbn::CiSetPairMode(c, 2);
+        return r;
+    };
+    std::vector<int32_t> rec((size_t)n * 64);
+    if (d == 0) {
+        if ((rc = level0())) return rc;
+        FBN_HIP(hipStreamSynchronize(c->stream));
+        for (int64_t t = 0; t < n; ++t) {
+            const int x = items[2 * t], y = items[2 * t + 1];
+            if (x >= y) return SetError(FBN_ERR_ARG, "level-0 tests are pairs x < y");
+            const int64_t pi = (int64_t)x * nv - (int64_t)x * (x + 1) / 2 + (y - x - 1);
+            FBN_HIP(hipMemcpy(rec.data() + t * 64, c->slot[0].bcounts.as<int32_t>() + pi * 64, 64 * 4,
+                              hipMemcpyDeviceToHost));
+        }
+    } else if (d == 1) {
+        if (!c->pairs_recorded && (rc = level0())) return rc;
+        fbn::CiSetPairMode(c, 2);
+        std::vector<uint8_t> ind((size_t)n);
+        if ((rc = fbn::CiBatchLaunch(c, 0, items, n, 1, 0.05, false)) || (rc = fbn::CiBatchWait(c, 0, ind.data(), nullptr, scratch)))
+            return rc;
+        FBN_HIP(hipMemcpy(rec.data(), c->slot[0].bcounts.p, (size_t)n * 64 * 4, hipMemcpyDeviceToHost));
+    }
+    if (d <= 1) {
+        for (int64_t t = 0; t < n; ++t) {
+            int64_t cells = (int64_t)c->dims[items[w * t]] * c->dims[items[w * t + 1]];
+            if (d == 1) cells *= c->dims[items[w * t + 2]];
+            std::copy(rec.begin() + t * 64, rec.begin() + t * 64 + std::min<int64_t>(cells, cap), counts + t * cap);
+        }
+        return FBN_OK;
+    }
+    if ((rc = c->counts.ensure((size_t)n * cap * 4))) return rc;
+    FBN_HIP(hipMemsetAsync(c->counts.p, 0, (size_t)n * cap * 4, c->stream));  // cells beyond a table: 0
+    c->counts_stride = cap;
+    rc = CiLaunchDevice(c, items, n, d, 0.05, false, c->counts.as<int32_t>(), c->stream);
+    c->counts_stride = 0;
+    if (rc) return rc;
+    FBN_HIP(hipStreamSynchronize(c->stream));
+    FBN_HIP(hipMemcpy(counts, c->counts.p, (size_t)n * cap * 4, hipMemcpyDeviceToHost));
     return FBN_OK;
 }
 
@@ -2207,12 +2276,33 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
     a.pairtab = reinterpret_cast<int32_t *>(scr + pt_off);
     a.ctx_stats = c->stats.as<unsigned long long>();
     a.out = out;
+    static const bool trace = getenv("FBN_PC_SMALL_TRACE") != nullptr;  // diagnostic
+    unsigned long long *h_trace = nullptr;
+    if (trace) {
+        FBN_HIP(hipHostMalloc((void **)&h_trace, (64 + 5 * 1024) * 8, hipHostMallocDefault));
+        memset(h_trace, 0, (64 + 5 * 1024) * 8);
+        a.trace = h_trace;
+    }
     CiSlot &S = c->slot[0];
     FBN_HIP(hipMemsetAsync(scr, 0, kSmallZeroBytes, s));
     if (c->timing) FBN_HIP(hipEventRecord(S.ev0, s));
     FBN_HIP(fbn_pc_small_launch(&a, grid, s));
     if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
     FBN_HIP(hipStreamSynchronize(s));
+    if (h_trace) {
+        const unsigned long long t0 = h_trace[63];
+        for (int d = 0; d < out->levels; ++d) {
+            unsigned long long mx = 0, mn = ~0ull;
+            for (int b = 0; b < grid; ++b) {
+                const unsigned long long v = h_trace[64 + d * 1024 + b];
+                if (v) mx = std::max(mx, v), mn = std::min(mn, v);
+            }
+            fprintf(stderr, "pc small level %d: tests start %.2f us, first / last workgroup done %.2f / %.2f us, "
+                    "barrier passed %.2f us, applied %.2f us\n", d, (h_trace[8 * d] - t0) * 0.01, (mn - t0) * 0.01,
+                    (mx - t0) * 0.01, (h_trace[8 * d + 2] - t0) * 0.01, (h_trace[8 * d + 3] - t0) * 0.01);
+        }
+        (void)hipHostFree(h_trace);
+    }
     if (out->status != 0)
         return SetError(FBN_ERR_HIP, "pc small kernel: %s (status %d)",
                         out->status == 1 ? "grid barrier timed out" : "no result", out->status);

@@ -64,6 +64,9 @@ struct CiArgs {
     // per word, PW words per variable (fbn_ci_pack2_build)
     const uint32_t *pk;
     long long PW;
+    // counts != nullptr: cstride == 0 -> the table of test 0 only; cstride > 0 -> every test's table
+    // at counts + test * cstride (fbn_ci_debug_counts)
+    long long cstride;
 };
 
 // BITS: count from the bit-sliced store (A.bits); a separate instantiation, so the byte-column
@@ -305,8 +308,8 @@ __global__ __launch_bounds__(BS) void ci_g2_kernel(CiArgs A) {
             }
             __syncthreads();
         }
-        if (A.counts && it == 0)
-            for (int c = tid; c < cells; c += BS) A.counts[c] = hist[c];
+        if (A.counts && (A.cstride > 0 || it == 0))
+            for (int c = tid; c < cells; c += BS) A.counts[it * A.cstride + c] = hist[c];
 
         // marginals N_{x+z}, N_{+yz}, N_{++z} (src/CellTable.cpp:242-250)
         for (int r = tid; r < dimz * dx; r += BS) {
@@ -465,9 +468,9 @@ extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, co
                                     uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
                                     int32_t *gscratch, unsigned long long *stats, const uint32_t *bits,
                                     const int32_t *row0, long long W, const double *band, int nband,
-                                    const uint32_t *pk, long long PW, hipStream_t stream) {
+                                    const uint32_t *pk, long long PW, long long cstride, hipStream_t stream) {
     CiArgs a{cols, dims, items, N, n, alpha, g2, df, p, indep, counts, gscratch, (long long)(lds_bytes / 4 + 1) & ~1ll,
-             stats, bits, row0, W, band, nband, pk, PW};
+             stats, bits, row0, W, band, nband, pk, PW, cstride};
     if (gscratch) lds_bytes = 0;
     // batches of at most kWideTests tests (deep PC levels: a few hundred tests or fewer, one
     // workgroup per test on part of the chip): 16 waves per test instead of 4, so each test's

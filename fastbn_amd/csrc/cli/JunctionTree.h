@@ -19,7 +19,8 @@ struct TestSet {  // what Dataset::LoadLIBSVMDataKnownNetwork + Inference ctor e
 
 class JunctionTree {
 public:
-    JunctionTree(fbn_network *net, TestSet *tester, int device = 0);
+    // gpus > 1: the cases are sharded over devices device .. device + gpus - 1 (RCCL, MultiGpu.h)
+    JunctionTree(fbn_network *net, TestSet *tester, int device = 0, int gpus = 1);
     ~JunctionTree();
     // LoadGroundTruthProbabilityTable + PredictUseJTInfer over all cases + Accuracy
     // (src/JunctionTree.cpp:57-129, 1508-1534).  num_threads is accepted for CLI compatibility.
@@ -34,6 +35,9 @@ private:
     TestSet *tester_;
     fbn_jt_plan *plan_ = nullptr;
     fbn_jt_plan_info info_{};
+    int device_ = 0, gpus_ = 1;
+    // PredictUseJTInfer over all cases on gpus_ devices -> predictions / marginals; "" or an error
+    std::string RunSharded(float *kernel_ms);
 };
 
 #endif

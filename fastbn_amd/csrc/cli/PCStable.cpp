@@ -7,6 +7,126 @@
 #include <cstdlib>
 #include <iostream>
 
+#include "MultiGpu.h"
+
+namespace {
+
+struct DevMem {  // one device allocation on the calling thread's device
+    void *p = nullptr;
+    std::string alloc(size_t bytes) { return HipErr(hipMalloc(&p, bytes ? bytes : 1), "hipMalloc"); }
+    ~DevMem() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+std::string FbnErr(int rc, const char *what) {
+    if (rc == 0) return std::string();
+    return std::string(what) + ": " + fbn_last_error();
+}
+
+// The skeleton search on g.size() GPUs (INTEGRATION.md "Multi-GPU"): rank 0's column
+// store reaches every device by ONE ncclBroadcast; each rank runs its edge range of every level
+// through the native session; per level ONE ncclAllGather of the fixed-size records (level 0 also
+// of the pair tables, device to device, after the ranks agree on their size with an ncclAllReduce).
+// Every rank ends with the same skeleton; rank 0's result is returned.
+std::string PcDistributed(const std::vector<uint8_t> &cols, const std::vector<int32_t> &dims, int nvars,
+                          int64_t nsamples, double alpha, int depth, int group_size, GpuGroup &g,
+                          fbn_pc_result **out) {
+    const int world = g.size();
+    std::vector<fbn_pc_result *> res(world, nullptr);
+    std::string err = g.Run([&](int r) -> std::string {
+        hipStream_t s = g.stream(r);
+        ncclComm_t comm = g.comm(r);
+        std::string e;
+        const size_t bytes = (size_t)nvars * nsamples;
+        fbn_ci_ctx *ctx = nullptr;
+        {
+            DevMem d_cols;
+            if ((e = d_cols.alloc(bytes)).size()) return e;
+            if (r == 0 && (e = HipErr(hipMemcpyAsync(d_cols.p, cols.data(), bytes, hipMemcpyHostToDevice, s),
+                                      "hipMemcpyAsync")).size())
+                return e;
+            if ((e = NcclErr(ncclBroadcast(d_cols.p, d_cols.p, bytes, ncclUint8, 0, comm, s), "ncclBroadcast")).size())
+                return e;
+            if ((e = HipErr(hipStreamSynchronize(s), "broadcast")).size()) return e;
+            if ((e = FbnErr(fbn_ci_dataset_from_device(static_cast<const uint8_t *>(d_cols.p), nvars, nsamples,
+                                                       dims.data(), g.device(r), &ctx),
+                            "fbn_ci_dataset_from_device")).size())
+                return e;
+        }
+        fbn_pc_dist *sess = nullptr;
+        if ((e = FbnErr(fbn_pc_dist_create(nvars, alpha, depth, group_size, &sess), "fbn_pc_dist_create")).size()) {
+            fbn_ci_ctx_destroy(ctx);
+            return e;
+        }
+        auto body = [&]() -> std::string {
+            std::string e2;
+            for (;;) {
+                int d = 0;
+                int64_t b = 0, en = 0, L = 0;
+                if ((e2 = FbnErr(fbn_pc_dist_level(sess, world, r, &d, &b, &en, &L), "fbn_pc_dist_level")).size())
+                    return e2;
+                if (d < 0) break;
+                std::vector<int32_t> rec((size_t)L), all((size_t)L * world);
+                if ((e2 = FbnErr(fbn_pc_dist_run(sess, ctx, rec.data()), "fbn_pc_dist_run")).size()) return e2;
+                if (d == 0) {  // level-0 pair tables to every rank (derived level-1 counting)
+                    int64_t chunk = 0;
+                    if ((e2 = FbnErr(fbn_pc_dist_pairs_chunk(sess, &chunk), "fbn_pc_dist_pairs_chunk")).size())
+                        return e2;
+                    DevMem d_c;
+                    if ((e2 = d_c.alloc(8)).size()) return e2;
+                    (void)hipMemcpyAsync(d_c.p, &chunk, 8, hipMemcpyHostToDevice, s);
+                    if ((e2 = NcclErr(ncclAllReduce(d_c.p, d_c.p, 1, ncclInt64, ncclMin, comm, s), "ncclAllReduce")).size())
+                        return e2;
+                    (void)hipMemcpyAsync(&chunk, d_c.p, 8, hipMemcpyDeviceToHost, s);
+                    if ((e2 = HipErr(hipStreamSynchronize(s), "pair chunk")).size()) return e2;
+                    if (chunk > 0) {
+                        DevMem mine, gathered;
+                        if ((e2 = mine.alloc((size_t)chunk * 64)).size() ||
+                            (e2 = gathered.alloc((size_t)chunk * 64 * world)).size())
+                            return e2;
+                        (void)hipMemsetAsync(mine.p, 0, (size_t)chunk * 64, s);
+                        if ((e2 = HipErr(hipStreamSynchronize(s), "memset")).size()) return e2;
+                        if ((e2 = FbnErr(fbn_pc_dist_pairs_export(sess, mine.p, 1), "fbn_pc_dist_pairs_export")).size())
+                            return e2;
+                        if ((e2 = NcclErr(ncclAllGather(mine.p, gathered.p, (size_t)chunk * 16, ncclInt32, comm, s),
+                                          "ncclAllGather")).size())
+                            return e2;
+                        if ((e2 = HipErr(hipStreamSynchronize(s), "pair tables")).size()) return e2;
+                        if ((e2 = FbnErr(fbn_pc_dist_pairs_import(sess, ctx, gathered.p, 1), "fbn_pc_dist_pairs_import")).size())
+                            return e2;
+                    }
+                }
+                DevMem d_rec, d_all;
+                if ((e2 = d_rec.alloc((size_t)L * 4)).size() || (e2 = d_all.alloc((size_t)L * 4 * world)).size()) return e2;
+                (void)hipMemcpyAsync(d_rec.p, rec.data(), (size_t)L * 4, hipMemcpyHostToDevice, s);
+                if ((e2 = NcclErr(ncclAllGather(d_rec.p, d_all.p, (size_t)L, ncclInt32, comm, s), "ncclAllGather")).size())
+                    return e2;
+                (void)hipMemcpyAsync(all.data(), d_all.p, (size_t)L * 4 * world, hipMemcpyDeviceToHost, s);
+                if ((e2 = HipErr(hipStreamSynchronize(s), "records")).size()) return e2;
+                int more = 0;
+                if ((e2 = FbnErr(fbn_pc_dist_apply(sess, all.data(), &more), "fbn_pc_dist_apply")).size()) return e2;
+                if (!more) break;
+            }
+            return FbnErr(fbn_pc_dist_result(sess, &res[r]), "fbn_pc_dist_result");
+        };
+        e = body();
+        fbn_pc_dist_destroy(sess);
+        fbn_ci_ctx_destroy(ctx);
+        return e;
+    });
+    for (int r = 1; r < world; ++r)
+        if (res[r]) fbn_pc_result_destroy(res[r]);
+    if (!err.empty()) {
+        if (res[0]) fbn_pc_result_destroy(res[0]);
+        return err;
+    }
+    *out = res[0];
+    return std::string();
+}
+
+}  // namespace
+
 void PCStable::StructLearnCompData(fbn_dataset *dts, int group_size, int /*num_threads*/, bool print_struct,
                                    bool /*verbose*/) {
     std::cout << "==================================================" << '\n'
@@ -22,8 +142,16 @@ void PCStable::StructLearnCompData(fbn_dataset *dts, int group_size, int /*num_t
     fbn_dataset_columns(dts, cols.data());
     fbn_ci_ctx *ctx = nullptr;
     fbn_pc_result *res = nullptr;
-    if (fbn_ci_dataset_upload(cols.data(), nvars, nsamples, dims.data(), device_, &ctx) ||
-        fbn_pc_stable(ctx, alpha, depth, group_size, &res)) {
+    if (gpus_ > 1 || ForceExchange()) {  // RCCL over the node's GPUs (MultiGpu.h)
+        GpuGroup g(gpus_, device_);
+        std::string e = g.ok() ? PcDistributed(cols, dims, nvars, nsamples, alpha, depth, group_size, g, &res) : g.error();
+        if (!e.empty()) {
+            fprintf(stderr, "Error in StructLearnCompData: %s\n", e.c_str());
+            exit(1);
+        }
+        std::cout << "PC-stable skeleton on " << g.size() << " GPU(s) (RCCL)" << std::endl;
+    } else if (fbn_ci_dataset_upload(cols.data(), nvars, nsamples, dims.data(), device_, &ctx) ||
+               fbn_pc_stable(ctx, alpha, depth, group_size, &res)) {
         fprintf(stderr, "Error in StructLearnCompData: %s\n", fbn_last_error());
         exit(1);
     }
@@ -82,7 +210,7 @@ void PCStable::StructLearnCompData(fbn_dataset *dts, int group_size, int /*num_t
         }
     }
     fbn_pc_result_destroy(res);
-    fbn_ci_ctx_destroy(ctx);
+    if (ctx) fbn_ci_ctx_destroy(ctx);
 }
 
 int PCStable::GetSHD(const std::string &bif_path) const {

@@ -16,7 +16,9 @@
 
 class PCStable {
 public:
-    PCStable(double alpha, int depth = 1000, int device = 0) : alpha(alpha), depth(depth), device_(device) {}
+    // gpus > 1: the skeleton search runs on devices device .. device + gpus - 1 (RCCL, MultiGpu.h)
+    PCStable(double alpha, int depth = 1000, int device = 0, int gpus = 1)
+        : alpha(alpha), depth(depth), device_(device), gpus_(gpus) {}
     void StructLearnCompData(fbn_dataset *dts, int group_size, int num_threads, bool print_struct, bool verbose);
 
     double alpha;
@@ -34,6 +36,7 @@ public:
 
 private:
     int device_;
+    int gpus_;
     int nvars_ = 0;
 };
 

@@ -1,6 +1,7 @@
 // main.cpp -- drop-in for `./BayesianNetwork -a 0|2 ...` (src/main.cpp:17-201, src/Parameter.cpp:6-107):
 // same flags, defaults and "../dataset/" path prefix; -a 0 (PC-stable) and -a 2 (junction tree)
-// run on the GPU.  Extra flags: --device N, --depth D (PC-stable max depth, reference default 1000).
+// run on the GPU.  Extra flags: --device N, --gpus G (devices N .. N + G - 1, RCCL: MultiGpu.h),
+// --depth D (PC-stable max depth, reference default 1000).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -12,7 +13,7 @@
 #include "fastbn.h"
 
 int main(int argc, char **argv) {
-    int algorithm = 2, num_threads = 1, group_size = 1, device = 0, depth = 1000;
+    int algorithm = 2, num_threads = 1, group_size = 1, device = 0, depth = 1000, gpus = 1;
     std::string net_file = "alarm/alarm.xml", ref_net_file = "alarm/alarm.bif",
                 train_set_file = "alarm/alarm_s5000.txt", test_set_file = "alarm/testing_alarm_1k_p20",
                 pt_file = "alarm/alarm_1k_pt", prefix = "../dataset/";
@@ -20,12 +21,13 @@ int main(int argc, char **argv) {
     for (i = 1; i < argc && argv[i][0] == '-'; i++) {
         std::string a = argv[i];
         if (a == "--device" && i + 1 < argc) { device = atoi(argv[++i]); continue; }
+        if (a == "--gpus" && i + 1 < argc) { gpus = atoi(argv[++i]); continue; }
         if (a == "--depth" && i + 1 < argc) { depth = atoi(argv[++i]); continue; }
         if (a == "--prefix" && i + 1 < argc) { prefix = argv[++i]; continue; }
         switch (argv[i][1]) {
         case 'h':
             std::cout << "Usage: ./BayesianNetwork [-a 0|2] [-t threads] [-g group] [-f0 net] [-f1 refnet] "
-                         "[-f2 train] [-f3 test] [-f4 pt] [--device N] [--depth D] [--prefix DIR]" << std::endl;
+                         "[-f2 train] [-f3 test] [-f4 pt] [--device N] [--gpus G] [--depth D] [--prefix DIR]" << std::endl;
             return 0;
         case 'a': algorithm = atoi(argv[++i]); break;
         case 't': num_threads = atoi(argv[++i]); break;
@@ -63,7 +65,7 @@ int main(int argc, char **argv) {
             fprintf(stderr, "Error: %s\n", fbn_last_error());
             return 1;
         }
-        PCStable pc(0.05, depth, device);
+        PCStable pc(0.05, depth, device, gpus);
         pc.StructLearnCompData(ds, group_size, num_threads, false, false);
         fbn_dataset_destroy(ds);
         std::cout << "SHD = " << pc.GetSHD(ref_net_file) << std::endl;
@@ -88,7 +90,7 @@ int main(int argc, char **argv) {
         }
         double accuracy;
         {
-            JunctionTree jt(net, &tester, device);
+            JunctionTree jt(net, &tester, device, gpus);
             accuracy = jt.EvaluateAccuracy(pt_file, num_threads);
         }
         std::cout << "accuracy = " << accuracy << std::endl;

@@ -61,6 +61,10 @@ struct PcSmallArgs {
     int32_t *pairtab;        // [kSmallMaxEdges][16] level-0 tables (derived level-1 counting)
     unsigned long long *ctx_stats;  // the ctx's margin log, set to this run's at the end
     PcSmallOut *out;         // pinned host memory
+    // diagnostic (FBN_PC_SMALL_TRACE): wall_clock64 stamps -- [8d + 0] level d's tests start,
+    // [8d + 2] its barrier passed, [8d + 3] applied (workgroup 0), [63] kernel start,
+    // [64 + 1024 d + b] workgroup b done with level d's tests
+    unsigned long long *trace;
 };
 
 }  // namespace fbn

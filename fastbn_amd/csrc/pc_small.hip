@@ -66,6 +66,7 @@ struct Lds {
     double red[2 * NWAVE];
     int redi[NWAVE];
     int32_t wtab[NWAVE][64];  // one test per wave (d <= 1): the wave's table
+    int32_t waux[NWAVE][64];  // ... and its margins (sample counts / pair tables)
     int dec;
     double g2;
 };
@@ -243,9 +244,25 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 template <int D>
 __device__ __noinline__ Decision wave_test(const PcSmallArgs &A, int x, int y, int z, int lane, bool record_pair,
-                              int32_t *tab) {
+                                           int32_t *tab, int32_t *aux) {
     const int n = A.nvars;
     const int dx = A.dims[x], dy = A.dims[y], dz = D == 1 ? A.dims[z] : 1;
+    // the margins, staged into the wave's LDS slot by one load per lane (issued ahead of the
+    // popcount loop): d = 0 the per-value sample counts of x and y, d = 1 the pair tables
+    // N_xy, N_xz, N_yz (16 ints each, u < v stored [u value][v value])
+    {
+        const int32_t *src = nullptr;
+        int k = 0;
+        if (D == 0) {
+            if (lane < dx) src = A.rowcnt + A.row0[x], k = lane;
+            else if (lane >= 4 && lane < 4 + dy) src = A.rowcnt + A.row0[y], k = lane - 4;
+        } else if (lane < 48) {
+            const int u = lane < 32 ? x : y, v = lane < 16 ? y : z;
+            src = A.pairtab + 16 * (size_t)pair_index(n, u < v ? u : v, u < v ? v : u);
+            k = lane & 15;
+        }
+        if (src) aux[lane] = src[k];
+    }
     const int mx = dx - 1, my = dy - 1, mz = D == 1 ? dz - 1 : 1;
     const long long W = A.W;
     const uint32_t *bx = A.bits + (size_t)A.row0[x] * W, *by = A.bits + (size_t)A.row0[y] * W;
@@ -296,15 +313,13 @@ __device__ __noinline__ Decision wave_test(const PcSmallArgs &A, int x, int y, i
     // margins of the full table, all exact integers
     //   d = 0: N_x[a] = rowcnt(x, a), N_y[b] = rowcnt(y, b)
     //   d = 1: N_xz(a, c), N_yz(b, c), N_xy(a, b) from the pair tables (u < v stored [u value][v value])
-    const int32_t *Txy = A.pairtab + 16 * (size_t)pair_index(n, x < y ? x : y, x < y ? y : x);
-    const int32_t *Txz = D == 1 ? A.pairtab + 16 * (size_t)pair_index(n, x < z ? x : z, x < z ? z : x) : Txy;
-    const int32_t *Tyz = D == 1 ? A.pairtab + 16 * (size_t)pair_index(n, y < z ? y : z, y < z ? z : y) : Txy;
+    const int32_t *Txy = aux, *Txz = aux + 16, *Tyz = aux + 32;
     auto nxz = [&](int a, int c) -> int {
-        if (D == 0) return A.rowcnt[A.row0[x] + a];
+        if (D == 0) return aux[a];
         return x < z ? Txz[a * dz + c] : Txz[c * dx + a];
     };
     auto nyz = [&](int b, int c) -> int {
-        if (D == 0) return A.rowcnt[A.row0[y] + b];
+        if (D == 0) return aux[4 + b];
         return y < z ? Tyz[b * dz + c] : Tyz[c * dy + b];
     };
     const int dxy = dx * dy, cells = dz * dxy;
@@ -327,7 +342,7 @@ __device__ __noinline__ Decision wave_test(const PcSmallArgs &A, int x, int y, i
     wave_lds_sync();
     // last z slice (d = 1): N_xy(a, b) - the other slices
     if (D == 1 && live && c == mz) {
-        int s = Txy[a * dy + b];  // x < y
+        int s = Txy[a * dy + b];  // x < y: N_xy stored [x value][y value]
         for (int k = 0; k < mz; ++k) s -= tab[(k * dx + a) * dy + b];
         tab[lane] = s;
     }
@@ -511,6 +526,7 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
     const int n = A.nvars;
     const int nb = gridDim.x;
     const int bid = blockIdx.x;
+    if (A.trace && bid == 0 && tid == 0) A.trace[63] = (unsigned long long)wall_clock64();
     for (int i = tid; i < (kSmallMaxVars + 1) * (kSmallMaxD + 1); i += BS) {
         const int m = i / (kSmallMaxD + 1), k = i % (kSmallMaxD + 1);
         long long r = 1;
@@ -587,6 +603,7 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
             return;
         }
         const int T = (int)tot64;
+        if (A.trace && bid == 0 && tid == 0) A.trace[8 * d + 0] = (unsigned long long)wall_clock64();
         // ---- the tests
         unsigned long long launched = 0;
         if (d <= 1) {
@@ -602,11 +619,11 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
                 const int x = L.ex[e], y = L.ey[e];
                 Decision r;
                 if (d == 0) {
-                    r = wave_test<0>(A, x, y, 0, lane, true, L.wtab[wv]);
+                    r = wave_test<0>(A, x, y, 0, lane, true, L.wtab[wv], L.waux[wv]);
                 } else {
                     int zz[1];
                     unrank(L, x, y, 1, k, zz);
-                    r = wave_test<1>(A, x, y, zz[0], lane, false, L.wtab[wv]);
+                    r = wave_test<1>(A, x, y, zz[0], lane, false, L.wtab[wv], L.waux[wv]);
                 }
                 ++launched;
                 const unsigned long long mb = (unsigned long long)__double_as_longlong(r.margin);
@@ -654,10 +671,12 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
                 slot[2 + d] = (unsigned long long)ll;
             }
         }
+        if (A.trace && tid == 0) A.trace[64 + (size_t)d * 1024 + bid] = (unsigned long long)wall_clock64();
         if (!grid_barrier(B, ++phase, L)) {
             if (tid == 0) A.out->status = 1;
             return;
         }
+        if (A.trace && bid == 0 && tid == 0) A.trace[8 * d + 2] = (unsigned long long)wall_clock64();
         // ---- apply: removed = some independent set found; counted = first + 1, else all sets
         long long counted = 0;
         for (int e = tid; e < E; e += BS) {
@@ -705,6 +724,7 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
                 atomicAnd((unsigned long long *)&L.adj[y], ~(1ull << x));
             }
         __syncthreads();
+        if (A.trace && bid == 0 && tid == 0) A.trace[8 * d + 3] = (unsigned long long)wall_clock64();
         int maxdeg = 0;
         for (int v = 0; v < n; ++v) maxdeg = maxdeg > popc64(L.adj[v]) ? maxdeg : popc64(L.adj[v]);
         if (bid == 0 && tid < kSmallMaxVars) A.out->adj[d][tid] = L.adj[tid];

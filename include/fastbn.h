@@ -194,6 +194,12 @@ int fbn_ci_last_kernel_ms(const fbn_ci_ctx *c, float *ms);
  * 268,355) is not pinned by any reference fixture, so every test records min |p - alpha| and counts
  * tests with |p - alpha| < 1e-9 (a decision a different-but-accurate CDF could flip).  Covers every
  * test run on `c` since the last reset (creation resets; `reset` != 0 resets after reading). */
+/* Parity pinning of the production paths: counts of n tests (items [n][2+d], level-0 pairs x < y)
+ * through the kernels a PC run uses at level d -- d = 0 the complete-graph level-0 batch (Gram of
+ * the leading bit-sliced rows, every pair's table recorded), d = 1 the derived counting from those
+ * recorded pair tables, d >= 2 the histogram kernel (2-bit packed columns at >= 64k samples) over
+ * one batch.  counts [n][cap], Counts3D cell order (src/CellTable.cpp:277-281). */
+int fbn_ci_debug_counts(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, int32_t *counts, int64_t cap);
 int fbn_ci_decision_margin(fbn_ci_ctx *c, double *min_margin, int64_t *near_alpha, int reset);
 int fbn_ci_ctx_destroy(fbn_ci_ctx *c);
 

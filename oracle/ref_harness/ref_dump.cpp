@@ -232,10 +232,41 @@ static unsigned long long Fnv1a(const int *col, int n) {
     return h;
 }
 
+// "cols:<file>" (int32 nvars, int64 nsamples, int32 dims[nvars], uint8 codes [nvars][nsamples]) into
+// the reference's Dataset (dataset_columns int32 [var][sample], as LoadCSVData leaves them), or a CSV
+// through the reference's own LoadCSVData; nullptr on a read error
+static Dataset *LoadColsOrCsv(const std::string &src) {
+    auto *dts = new Dataset();
+    if (src.rfind("cols:", 0) != 0) {
+        dts->LoadCSVData(src, true, true, 0);
+        return dts;
+    }
+    FILE *f = fopen(src.c_str() + 5, "rb");
+    if (!f) return nullptr;
+    int32_t V;
+    int64_t N;
+    if (fread(&V, 4, 1, f) != 1 || fread(&N, 8, 1, f) != 1) return nullptr;
+    dts->num_vars = V;
+    dts->num_instance = (int)N;
+    dts->num_of_possible_values_of_disc_vars.resize(V);
+    if (fread(dts->num_of_possible_values_of_disc_vars.data(), 4, V, f) != (size_t)V) return nullptr;
+    dts->dataset_columns = new int *[V];
+    std::vector<uint8_t> buf(N);
+    for (int v = 0; v < V; ++v) {
+        if (fread(buf.data(), 1, N, f) != (size_t)N) return nullptr;
+        dts->dataset_columns[v] = new int[N];
+        for (int64_t k = 0; k < N; ++k) dts->dataset_columns[v][k] = buf[k];
+    }
+    fclose(f);
+    return dts;
+}
+
+// ci <csv | cols:file> <tests file> <out>: the reference's Counts2D / Counts3D::FillTable
+// (src/CellTable.cpp) for every listed test (x y z...), plus the FNV-1a hash of every column it saw
 static int RunCI(int argc, char **argv) {
     if (argc < 5) return 2;
-    auto *dts = new Dataset();
-    dts->LoadCSVData(argv[2], true, true, 0);
+    Dataset *dts = LoadColsOrCsv(argv[2]);
+    if (!dts) return 3;
     std::ifstream tin(argv[3]);
     FILE *f = fopen(argv[4], "w");
     fprintf(f, "vars %d samples %d\n", dts->num_vars, dts->num_instance);
@@ -642,30 +673,9 @@ bool SearchAtDepth(Run &R, int d, int threads) {  // :209-328
 static int RunPCBench(int argc, char **argv) {
     if (argc < 7) return 2;
     std::streambuf *old = std::cout.rdbuf(nullptr);
-    auto *dts = new Dataset();
-    std::string src = argv[2];
-    if (src.rfind("cols:", 0) == 0) {
-        FILE *f = fopen(src.c_str() + 5, "rb");
-        if (!f) return 3;
-        int32_t V;
-        int64_t N;
-        if (fread(&V, 4, 1, f) != 1 || fread(&N, 8, 1, f) != 1) return 3;
-        dts->num_vars = V;
-        dts->num_instance = (int)N;
-        dts->num_of_possible_values_of_disc_vars.resize(V);
-        if (fread(dts->num_of_possible_values_of_disc_vars.data(), 4, V, f) != (size_t)V) return 3;
-        dts->dataset_columns = new int *[V];
-        std::vector<uint8_t> buf(N);
-        for (int v = 0; v < V; ++v) {
-            if (fread(buf.data(), 1, N, f) != (size_t)N) return 3;
-            dts->dataset_columns[v] = new int[N];
-            for (int64_t k = 0; k < N; ++k) dts->dataset_columns[v][k] = buf[k];
-        }
-        fclose(f);
-    } else {
-        dts->LoadCSVData(src, true, true, 0);
-    }
+    Dataset *dts = LoadColsOrCsv(argv[2]);
     std::cout.rdbuf(old);
+    if (!dts) return 3;
     pcb::Run R;
     R.dts = dts;
     R.alpha = atof(argv[3]);

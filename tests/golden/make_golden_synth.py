@@ -8,6 +8,7 @@ TEST INFRASTRUCTURE -- runs in the build container.
                 *reference's own* outputs on them (oracle/_ref/ref_dump jt: the unmodified
                 reference JunctionTree compiled in place): per-case label + 17-digit marginals
                 (ref.marg.gz) and the reference's junction-tree plan (ref.plan.gz).
+  pc_c5.ci.gz   config 5: the reference's own Counts2D / Counts3D tables (pc_c5_ci below)
   pc_c5.json    config 5: PC-stable (depth 6, alpha 0.05) on the seeded 1000-variable x 100k-sample
                 dataset, run by the CPU restatement (oracle/pc_oracle.cpp; the reference's
                 PCStable/IndependenceTest cannot be compiled here: stats/gcem absent): tests per
@@ -85,9 +86,61 @@ def pc_c5():
     print("pc_c5:", {k: v for k, v in rec.items() if k != "dims"})
 
 
+# per level of the config-5 run: how many of the tests the reference's sequential search runs are
+# pinned (seeded sample of the restatement's log; deep levels have few tests and large tables)
+C5CI_PER_LEVEL = {0: 256, 1: 256, 2: 192, 3: 128, 4: 96, 5: 30}
+
+
+def pc_c5_ci():
+    """pc_c5.ci.gz: the UNMODIFIED reference's Counts2D / Counts3D::FillTable (src/CellTable.cpp,
+    compiled in place into oracle/_ref/ref_dump) on a seeded sample of the CI tests a config-5 run
+    performs at every level 0-5 -- the tests come from the restatement's log of the full run
+    (oracle/pc_oracle.cpp, the order the reference's sequential search would run them), the counts
+    and the per-column FNV-1a hashes from the reference's own code reading the same column store."""
+    import random
+
+    import numpy as np
+    import oracle as O
+    from fastbn_amd import synth
+    ref_dump = os.path.join(REPO, "oracle", "_ref", "ref_dump")
+    if not os.path.exists(ref_dump):
+        subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref"], check=True)
+    cols, dims = synth.config5_dataset()
+    t0 = time.time()
+    r = O.OracleDataset(columns=cols, dims=dims).pc_stable(0.05, 6, 1, keep_log=True)
+    print("restatement run: %.1f s, %d logged tests" % (time.time() - t0, len(r["log"])))
+    by_level = {}
+    for t in r["log"]:
+        by_level.setdefault(t[0], []).append(t)
+    rng = random.Random(20251017)
+    sample = []
+    for d in sorted(by_level):
+        tests = by_level[d]
+        k = min(C5CI_PER_LEVEL.get(d, 32), len(tests))
+        sample += [tests[i] for i in sorted(rng.sample(range(len(tests)), k))]
+    with tempfile.TemporaryDirectory() as td:
+        cpath = os.path.join(td, "c5.cols")
+        with open(cpath, "wb") as f:
+            import struct
+            f.write(struct.pack("<iq", cols.shape[0], cols.shape[1]))
+            f.write(np.asarray(dims, np.int32).tobytes())
+            f.write(np.ascontiguousarray(cols, np.uint8).tobytes())
+        tfile = os.path.join(td, "tests")
+        with open(tfile, "w") as f:
+            for t in sample:
+                f.write(" ".join(map(str, [t[1], t[2]] + list(t[3]))) + "\n")
+        out = os.path.join(td, "c5.ci")
+        subprocess.run([ref_dump, "ci", "cols:" + cpath, tfile, out], check=True, stdout=subprocess.DEVNULL)
+        gz_write(os.path.join(HERE, "pc_c5.ci.gz"), open(out, "rb").read())
+    print("pc_c5.ci.gz: %d tests, per level %s" % (len(sample), {d: min(C5CI_PER_LEVEL.get(d, 32), len(v))
+                                                             for d, v in sorted(by_level.items())}))
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["munin", "c5"]
+    which = sys.argv[1:] or ["munin", "c5", "c5ci"]
     if "munin" in which:
         munin_like()
     if "c5" in which:
         pc_c5()
+    if "c5ci" in which:
+        pc_c5_ci()

@@ -51,10 +51,13 @@ def test_alarm5000_default_is_device_resident(alarm, monkeypatch):
     assert pc.near_alpha == 0 and pc.min_margin > 1e-9
 
 
-@pytest.mark.parametrize("alpha", [0.0, 0.001, 0.01, 0.2, 0.5, 1.0])
-def test_alarm5000_alphas(alarm, alpha, monkeypatch):
+@pytest.mark.parametrize("alpha,depth", [(0.0, 1000), (0.001, 1000), (0.01, 1000), (0.2, 1000), (0.5, 1000),
+                                         (1.0, 3)])
+def test_alarm5000_alphas(alarm, alpha, depth, monkeypatch):
+    """alpha 1: nothing but df-0 tests is independent, the graph stays (nearly) complete -- depth 3
+    keeps the restatement's CPU run short."""
     ds, od = alarm
-    _check(ds, od, alpha, 1000, monkeypatch)
+    _check(ds, od, alpha, depth, monkeypatch)
 
 
 @pytest.mark.parametrize("depth", [1, 2, 3, 4])
@@ -78,15 +81,16 @@ def test_synthetic_ragged_sizes(tmp_path, ns, nv, monkeypatch):
 
 
 def test_dense_graph_hands_off_to_host_at_level_5(monkeypatch):
-    """Twelve noisy copies of one latent variable: nothing is independent, so the search reaches
-    level 5, which the device kernel hands to the host driver (levels 0-4 on the device)."""
+    """Twelve noisy binary copies of one latent variable, 20k samples: the edges stay dependent
+    given any conditioning set, so the search reaches level 5, which the device kernel hands to the
+    host driver (levels 0-4 on the device)."""
     rng = np.random.default_rng(7)
-    base = rng.integers(0, 4, 3000)
-    cols = np.stack([(base + (rng.random(3000) < 0.2) * rng.integers(0, 4, 3000)) % 4 for _ in range(12)])
-    cols = cols.astype(np.uint8)
-    dims = np.full(12, 4, np.int32)
+    n = 20000
+    base = rng.integers(0, 2, n)
+    cols = np.stack([base ^ (rng.random(n) < 0.1) for _ in range(12)]).astype(np.uint8)
+    dims = np.full(12, 2, np.int32)
     ds = F.Dataset(columns=cols, dims=dims)
-    pc = _check(ds, O.OracleDataset(columns=cols, dims=dims), 0.05, 8, monkeypatch)
+    pc = _check(ds, O.OracleDataset(columns=cols, dims=dims), 0.05, 7, monkeypatch)
     assert len(pc.tests_per_level) >= 6
 
 
