@@ -2247,7 +2247,8 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
     // scratch: [zeroed: barrier words | first-independent words] [statistics slots] [pair tables]
     const size_t acc_off = (kSmallZeroBytes + 255) & ~(size_t)255;
     const size_t pt_off = acc_off + (size_t)grid * 64;
-    const size_t bytes = pt_off + (size_t)kSmallMaxEdges * 16 * 4;
+    const size_t dout_off = (pt_off + (size_t)kSmallMaxEdges * 16 * 4 + 255) & ~(size_t)255;
+    const size_t bytes = dout_off + sizeof(PcSmallOut);
     if ((rc = c->small_scr.ensure(bytes))) return rc;
     if (!c->h_small) {
         hipError_t e = hipHostMalloc((void **)&c->h_small, sizeof(PcSmallOut), hipHostMallocDefault);
@@ -2275,13 +2276,18 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
     a.acc = reinterpret_cast<unsigned long long *>(scr + acc_off);
     a.pairtab = reinterpret_cast<int32_t *>(scr + pt_off);
     a.ctx_stats = c->stats.as<unsigned long long>();
+    a.dout = reinterpret_cast<PcSmallOut *>(scr + dout_off);
     a.out = out;
     static const bool trace = getenv("FBN_PC_SMALL_TRACE") != nullptr;  // diagnostic
+    std::vector<unsigned long long> trace_host;
     unsigned long long *h_trace = nullptr;
+    DevBuf trace_dev;
     if (trace) {
-        FBN_HIP(hipHostMalloc((void **)&h_trace, (64 + 5 * 1024) * 8, hipHostMallocDefault));
-        memset(h_trace, 0, (64 + 5 * 1024) * 8);
-        a.trace = h_trace;
+        const size_t tb = (64 + 10 * 1024) * 8;
+        if ((rc = trace_dev.ensure(tb))) return rc;
+        FBN_HIP(hipMemsetAsync(trace_dev.p, 0, tb, s));
+        a.trace = trace_dev.as<unsigned long long>();
+        trace_host.assign(tb / 8, 0);
     }
     CiSlot &S = c->slot[0];
     FBN_HIP(hipMemsetAsync(scr, 0, kSmallZeroBytes, s));
@@ -2289,19 +2295,29 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
     FBN_HIP(fbn_pc_small_launch(&a, grid, s));
     if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
     FBN_HIP(hipStreamSynchronize(s));
+    if (trace) {
+        FBN_HIP(hipMemcpy(trace_host.data(), trace_dev.p, trace_host.size() * 8, hipMemcpyDeviceToHost));
+        h_trace = trace_host.data();
+    }
     if (h_trace) {
         const unsigned long long t0 = h_trace[63];
         for (int d = 0; d < out->levels; ++d) {
-            unsigned long long mx = 0, mn = ~0ull;
+            unsigned long long mx = 0, mn = ~0ull, smx = 0, smn = ~0ull;
+            double dur = 0, dmax = 0;
             for (int b = 0; b < grid; ++b) {
-                const unsigned long long v = h_trace[64 + d * 1024 + b];
+                const unsigned long long v = h_trace[64 + d * 1024 + b], u = h_trace[64 + 5 * 1024 + d * 1024 + b];
                 if (v) mx = std::max(mx, v), mn = std::min(mn, v);
+                if (u) smx = std::max(smx, u), smn = std::min(smn, u);
+                if (u && v) dur += (v - u) * 0.01, dmax = std::max(dmax, (v - u) * 0.01);
             }
-            fprintf(stderr, "pc small level %d: tests start %.2f us, first / last workgroup done %.2f / %.2f us, "
-                    "barrier passed %.2f us, applied %.2f us\n", d, (h_trace[8 * d] - t0) * 0.01, (mn - t0) * 0.01,
-                    (mx - t0) * 0.01, (h_trace[8 * d + 2] - t0) * 0.01, (h_trace[8 * d + 3] - t0) * 0.01);
+            fprintf(stderr, "pc small level %d: workgroups start %.2f..%.2f us, done %.2f..%.2f us (test phase mean "
+                    "%.2f max %.2f us), barrier passed %.2f us, applied %.2f us\n", d, (smn - t0) * 0.01,
+                    (smx - t0) * 0.01, (mn - t0) * 0.01, (mx - t0) * 0.01, dur / grid, dmax,
+                    (h_trace[8 * d + 2] - t0) * 0.01, (h_trace[8 * d + 3] - t0) * 0.01);
+            const double nt = (double)std::max<unsigned long long>(1, h_trace[8 * d + 7]);
+            fprintf(stderr, "    one-wave tests: %.0f, cycles per test: count %.0f, complete/margins %.0f, G2/decision %.0f\n",
+                    nt, h_trace[8 * d + 4] / nt, h_trace[8 * d + 5] / nt, h_trace[8 * d + 6] / nt);
         }
-        (void)hipHostFree(h_trace);
     }
     if (out->status != 0)
         return SetError(FBN_ERR_HIP, "pc small kernel: %s (status %d)",

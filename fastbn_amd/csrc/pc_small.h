@@ -60,7 +60,8 @@ struct PcSmallArgs {
     unsigned long long *acc; // [0] margin bits (min), [1] near, [2 + d] launched at level d
     int32_t *pairtab;        // [kSmallMaxEdges][16] level-0 tables (derived level-1 counting)
     unsigned long long *ctx_stats;  // the ctx's margin log, set to this run's at the end
-    PcSmallOut *out;         // pinned host memory
+    PcSmallOut *dout;        // the record, built in device memory during the run
+    PcSmallOut *out;         // pinned host memory: the record's used part, copied at the end
     // diagnostic (FBN_PC_SMALL_TRACE): wall_clock64 stamps -- [8d + 0] level d's tests start,
     // [8d + 2] its barrier passed, [8d + 3] applied (workgroup 0), [63] kernel start,
     // [64 + 1024 d + b] workgroup b done with level d's tests

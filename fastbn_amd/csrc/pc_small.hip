@@ -11,8 +11,8 @@
 //       order: the d-subsets of adj(x)\{y} in lexicographic order, then those of adj(y)\{x},
 //       CheckEdge src/PCStable.cpp:339-470, ChoiceGenerator src/ChoiceGenerator.cpp:14-85);
 //     tests are counted and decided (d <= 1: one wave per test on the bit-sliced store, level 1
-//       deriving the last value of x, y and z from the level-0 pair tables; d >= 2: one workgroup
-//       per test, LDS histogram of the 2-bit packed columns -- Counts2D/Counts3D,
+//       deriving the last value of x, y and z from the level-0 pair tables; d = 2, 3: one wave per
+//       test, d = 4: one workgroup per test, LDS histograms of the 2-bit packed columns -- Counts2D/Counts3D,
 //       src/CellTable.cpp:23-91,226-291,430-455; G^2 / df / p as ComputeGSquareXY/XYZ,
 //       src/IndependenceTest.cpp:65-155,295-364);
 //     an independent test does atomicMax(first[d][edge], ~its index within the edge): the edge's
@@ -29,6 +29,7 @@
 // counter, every workgroup polls relaxed with s_sleep, one release before and one acquire after,
 // every spin bounded (a timed-out launch reports status 1 and exits).
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "ci_chisq.h"
@@ -48,7 +49,13 @@ constexpr long long kSpinTicks = 200000000ll;  // wall_clock64 ticks (100 MHz): 
 
 typedef __attribute__((ext_vector_type(4))) unsigned u4;
 
+constexpr int kWaveHist = 2048;    // per-wave region of the one-wave histogram tests (d = 2, 3)
+
 struct Lds {
+    // per-run constants staged once: state counts, first mask row and per-row sample counts of
+    // every variable, the decision band
+    int32_t dims[kSmallMaxVars], row0[kSmallMaxVars], rowcnt[4 * kSmallMaxVars];
+    double band[2 * 256 + 1];
     uint64_t adj[kSmallMaxVars];
     int32_t rowoff[kSmallMaxVars + 1];     // edges of rows before x
     int32_t eoff[kSmallMaxEdges + 1];      // first test of each edge
@@ -65,6 +72,9 @@ struct Lds {
     double term[kTermChunk];
     double red[2 * NWAVE];
     int redi[NWAVE];
+    int32_t whist[NWAVE][kWaveHist];  // one test per wave (d = 2, 3): table + margins
+    unsigned bfirst[kSmallMaxEdges];   // this workgroup's first independent candidate per edge
+    unsigned long long ph[NWAVE][4];   // diagnostic (trace): cycles per test phase, per wave
     int32_t wtab[NWAVE][64];  // one test per wave (d <= 1): the wave's table
     int32_t waux[NWAVE][64];  // ... and its margins (sample counts / pair tables)
     int dec;
@@ -72,6 +82,48 @@ struct Lds {
 };
 
 __device__ __forceinline__ int popc64(uint64_t v) { return __popcll(v); }
+
+// ---- wave-wide reductions on DPP (VALU lane moves, no LDS round trip): an inclusive scan inside
+// each 16-lane row (row_shr 1, 2, 4, 8 with zeros shifted in), then row_bcast:15 / :31 carry the
+// row totals up, lane 63 holds the wave total; readlane broadcasts it (a wave-uniform value)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ int dpp_i32(int x) {
+    return __builtin_amdgcn_update_dpp(0, x, CTRL, ROWS, 0xf, CTRL < 0x140);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_f64(double x) {
+    const long long b = __double_as_longlong(x);
+    const int lo = dpp_i32<CTRL, ROWS>((int)(unsigned)b), hi = dpp_i32<CTRL, ROWS>((int)(b >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ int wsum_i32(int x) {
+    x += dpp_i32<0x111, 0xf>(x);
+    x += dpp_i32<0x112, 0xf>(x);
+    x += dpp_i32<0x114, 0xf>(x);
+    x += dpp_i32<0x118, 0xf>(x);
+    x += dpp_i32<0x142, 0xa>(x);
+    x += dpp_i32<0x143, 0xc>(x);
+    return __builtin_amdgcn_readlane(x, 63);
+}
+__device__ __forceinline__ double wsum_f64(double x) {
+    x += dpp_f64<0x111, 0xf>(x);
+    x += dpp_f64<0x112, 0xf>(x);
+    x += dpp_f64<0x114, 0xf>(x);
+    x += dpp_f64<0x118, 0xf>(x);
+    x += dpp_f64<0x142, 0xa>(x);
+    x += dpp_f64<0x143, 0xc>(x);
+    const long long b = __double_as_longlong(x);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, 63),
+                   hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), 63);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ long long wsum_i64(long long x) {
+    // 64-bit sums of small per-lane values: the two halves summed separately, carries folded
+    const unsigned long long u = (unsigned long long)x;
+    const long long lo = (long long)(unsigned)wsum_i32((int)(u & 0xFFFFu)) +
+                         ((long long)wsum_i32((int)((u >> 16) & 0xFFFFu)) << 16);
+    return lo + ((long long)wsum_i32((int)(u >> 32)) << 32);
+}
 
 // the k-th (0-based) set bit of m
 __device__ __forceinline__ int select_bit(uint64_t m, int k) {
@@ -150,7 +202,7 @@ __device__ bool grid_barrier(const Barrier &B, unsigned phase, Lds &L) {
 
 // ---- block-wide helpers
 __device__ __forceinline__ long long block_sum_ll(long long v, Lds &L) {
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    v = wsum_i64(v);
     __syncthreads();
     if ((threadIdx.x & 63) == 0) L.wsum[threadIdx.x >> 6] = v;
     __syncthreads();
@@ -206,20 +258,21 @@ struct Decision {
     double margin;  // |p - alpha| as logged
 };
 
-__device__ __forceinline__ Decision decide_tree(double gs, double ga, int df, int cells, const PcSmallArgs &A) {
+__device__ __forceinline__ Decision decide_tree(double gs, double ga, int df, int cells, const PcSmallArgs &A,
+                                                const double *band) {
     if (df == 0) return Decision{1, fabs(1.0 - A.alpha)};
     if (A.band && df <= A.nband) {
         const double err = (cells + 64) * 2.3e-16 * ga;
-        if (gs + err < A.band[2 * df - 2]) return Decision{1, A.band[2 * A.nband]};
-        if (gs - err > A.band[2 * df - 1]) return Decision{0, A.band[2 * A.nband]};
+        if (gs + err < band[2 * df - 2]) return Decision{1, band[2 * A.nband]};
+        if (gs - err > band[2 * df - 1]) return Decision{0, band[2 * A.nband]};
     }
     return Decision{-1, 0.0};
 }
 
-__device__ __noinline__ Decision decide_exact(double g2, int df, const PcSmallArgs &A) {
+__device__ __noinline__ Decision decide_exact(double g2, int df, const PcSmallArgs &A, const double *band) {
     if (df == 0) return Decision{1, fabs(1.0 - A.alpha)};
-    if (A.band && df <= A.nband && g2 < A.band[2 * df - 2]) return Decision{1, A.band[2 * A.nband]};
-    if (A.band && df <= A.nband && g2 > A.band[2 * df - 1]) return Decision{0, A.band[2 * A.nband]};
+    if (A.band && df <= A.nband && g2 < band[2 * df - 2]) return Decision{1, band[2 * A.nband]};
+    if (A.band && df <= A.nband && g2 > band[2 * df - 1]) return Decision{0, band[2 * A.nband]};
     const double p = fbn_chisq_pvalue(g2, df);
     return Decision{p > A.alpha ? 1 : 0, fabs(p - A.alpha)};
 }
@@ -236,17 +289,21 @@ __device__ __forceinline__ double g2_term(long observed, long sum_row, long sum_
 // table is completed in the wave's LDS slot, cell l = (c * dx + a) * dy + b (Counts3D layout,
 // src/CellTable.cpp:277-281), in dependency order: leading cells, then the last y value of every
 // leading (z, x) row, then the last x value of every leading z slice, then the last z slice.
+// LDS written by some lanes of a wave, then read by others: the wave's LDS operations complete in
+// order, so waiting for its own LDS counter suffices (no vector-memory wait: a pending global atomic
+// or store must not stall the table passes); the clobber keeps the compiler from moving LDS
+// accesses across it
 __device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 template <int D>
-__device__ __noinline__ Decision wave_test(const PcSmallArgs &A, int x, int y, int z, int lane, bool record_pair,
-                                           int32_t *tab, int32_t *aux) {
+__device__ __forceinline__ Decision wave_test(const PcSmallArgs &A, const Lds &L, int x, int y, int z, int lane,
+                                           bool record_pair, int32_t *tab, int32_t *aux, unsigned long long *ph) {
+    const unsigned long long c0 = A.trace ? clock64() : 0;
     const int n = A.nvars;
-    const int dx = A.dims[x], dy = A.dims[y], dz = D == 1 ? A.dims[z] : 1;
+    const int dx = L.dims[x], dy = L.dims[y], dz = D == 1 ? L.dims[z] : 1;
     // the margins, staged into the wave's LDS slot by one load per lane (issued ahead of the
     // popcount loop): d = 0 the per-value sample counts of x and y, d = 1 the pair tables
     // N_xy, N_xz, N_yz (16 ints each, u < v stored [u value][v value])
@@ -254,8 +311,8 @@ __device__ __noinline__ Decision wave_test(const PcSmallArgs &A, int x, int y, i
         const int32_t *src = nullptr;
         int k = 0;
         if (D == 0) {
-            if (lane < dx) src = A.rowcnt + A.row0[x], k = lane;
-            else if (lane >= 4 && lane < 4 + dy) src = A.rowcnt + A.row0[y], k = lane - 4;
+            if (lane < dx) aux[lane] = L.rowcnt[L.row0[x] + lane];
+            else if (lane >= 4 && lane < 4 + dy) aux[lane] = L.rowcnt[L.row0[y] + lane - 4];
         } else if (lane < 48) {
             const int u = lane < 32 ? x : y, v = lane < 16 ? y : z;
             src = A.pairtab + 16 * (size_t)pair_index(n, u < v ? u : v, u < v ? v : u);
@@ -265,8 +322,8 @@ __device__ __noinline__ Decision wave_test(const PcSmallArgs &A, int x, int y, i
     }
     const int mx = dx - 1, my = dy - 1, mz = D == 1 ? dz - 1 : 1;
     const long long W = A.W;
-    const uint32_t *bx = A.bits + (size_t)A.row0[x] * W, *by = A.bits + (size_t)A.row0[y] * W;
-    const uint32_t *bz = D == 1 ? A.bits + (size_t)A.row0[z] * W : bx;
+    const uint32_t *bx = A.bits + (size_t)L.row0[x] * W, *by = A.bits + (size_t)L.row0[y] * W;
+    const uint32_t *bz = D == 1 ? A.bits + (size_t)L.row0[z] * W : bx;
     constexpr int MZ = D == 1 ? 3 : 1;
     uint32_t cnt[MZ][3][3];
 #pragma unroll
@@ -297,19 +354,26 @@ __device__ __noinline__ Decision wave_test(const PcSmallArgs &A, int x, int y, i
                     for (int c = 0; c < MZ; ++c) cnt[c][a][b] += __builtin_popcount(xy & zv[c][k]);
                 }
     }
-    // leading cells: wave totals straight into the table
+    // leading cells: wave totals straight into the table.  Transposing butterfly over the 32
+    // (padded) counters: at distance o every lane keeps one half of its counters and adds its
+    // partner's copy of that half (32 shuffles in 6 independent stages, instead of 6 dependent
+    // shuffles per counter); lane l ends with the total of counter l >> 1 = (c * 3 + a) * 3 + b
+    {
+        // every counter reduced on DPP (independent chains, interleaved), totals wave-uniform; lane
+        // i writes counter i = (c * 3 + a) * 3 + b
+        int mine = 0;
 #pragma unroll
-    for (int c = 0; c < MZ; ++c)
+        for (int c = 0; c < MZ; ++c)
 #pragma unroll
-        for (int a = 0; a < 3; ++a)
+            for (int a = 0; a < 3; ++a)
 #pragma unroll
-            for (int b = 0; b < 3; ++b) {
-                if (c >= mz || a >= mx || b >= my) continue;  // wave-uniform
-                uint32_t v = cnt[c][a][b];
-#pragma unroll
-                for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-                if (lane == 0) tab[(c * dx + a) * dy + b] = (int32_t)v;
-            }
+                for (int b = 0; b < 3; ++b) {
+                    const int tot = wsum_i32((int)cnt[c][a][b]);
+                    mine = lane == (c * 3 + a) * 3 + b ? tot : mine;
+                }
+        const int i = lane, c = i / 9, a = (i / 3) % 3, b = i % 3;
+        if (i < 9 * MZ && c < mz && a < mx && b < my) tab[(c * dx + a) * dy + b] = mine;
+    }
     // margins of the full table, all exact integers
     //   d = 0: N_x[a] = rowcnt(x, a), N_y[b] = rowcnt(y, b)
     //   d = 1: N_xz(a, c), N_yz(b, c), N_xy(a, b) from the pair tables (u < v stored [u value][v value])
@@ -326,6 +390,7 @@ __device__ __noinline__ Decision wave_test(const PcSmallArgs &A, int x, int y, i
     const int c = lane / dxy, a = (lane / dy) % dx, b = lane % dy;
     const bool live = lane < cells;
     wave_lds_sync();
+    const unsigned long long c1 = A.trace ? clock64() : 0;
     // last y value of the leading (z, x) rows: N_xz(a, c) - sum of the row
     if (live && c < mz && a < mx && b == my) {
         int s = nxz(a, c);
@@ -349,36 +414,165 @@ __device__ __noinline__ Decision wave_test(const PcSmallArgs &A, int x, int y, i
     wave_lds_sync();
     const int ob = live ? tab[lane] : 0;
     if (D == 0 && record_pair && live) A.pairtab[16 * (size_t)pair_index(n, x, y) + lane] = ob;
+    const unsigned long long c2 = A.trace ? clock64() : 0;
     // marginals: N_{x+z} = N_xz, N_{+yz} = N_yz, N_{++z} = sum_a N_xz; adjusted df per z
     // (src/IndependenceTest.cpp:96-112, 309-322)
+    // nonzero margins as wave ballots: lane l < dz * dx holds N_xz(l % dx, l / dx), lane l < dz * dy
+    // N_yz(l % dy, l / dy); alx(c) / aly(c) = set bits in slice c's lane range
+    const int mxz = lane < dz * dx ? nxz(lane % dx, lane / dx) : 0;
+    const int myz = lane < dz * dy ? nyz(lane % dy, lane / dy) : 0;
+    const unsigned long long nzx = __ballot(mxz > 0), nzy = __ballot(myz > 0);
+    int df = 0;
+    for (int k = 0; k < dz; ++k) {  // wave-uniform
+        const int alx = __popcll((nzx >> (k * dx)) & ((1ull << dx) - 1)),
+                  aly = __popcll((nzy >> (k * dy)) & ((1ull << dy) - 1));
+        df += ((alx >= 1 ? alx : 1) - 1) * ((aly >= 1 ? aly : 1) - 1);
+    }
     double t = 0.0;
     if (live) {
         long tot = 0;
-        if (D == 0) tot = A.N;
-        else
-            for (int i = 0; i < dx; ++i) tot += nxz(i, c);
+        if (D == 0) {
+            tot = A.N;
+        } else {
+            int q[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) q[i] = i < dx ? nxz(i, c) : 0;  // independent loads
+            tot = (long)q[0] + q[1] + q[2] + q[3];
+        }
         t = g2_term(ob, nxz(a, c), nyz(b, c), tot);
     }
-    int df = 0;
-    for (int k = 0; k < dz; ++k) {
-        int alx = 0, aly = 0;
-        for (int i = 0; i < dx; ++i) alx += nxz(i, k) > 0;
-        for (int j = 0; j < dy; ++j) aly += nyz(j, k) > 0;
-        df += ((alx >= 1 ? alx : 1) - 1) * ((aly >= 1 ? aly : 1) - 1);
-    }
-    double gs = t, ga = fabs(t);
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        gs += __shfl_xor(gs, o);
-        ga += __shfl_xor(ga, o);
-    }
-    Decision r = decide_tree(gs, ga, df, cells, A);
+    const double gs = wsum_f64(t), ga = wsum_f64(fabs(t));
+    Decision r = decide_tree(gs, ga, df, cells, A, L.band);
     if (r.ind < 0) {  // in the band: the reference's in-order running sum, then p
         double g2 = 0.0;
         for (int l = 0; l < cells; ++l) g2 += __shfl(t, l);
-        r = decide_exact(g2, df, A);
+        r = decide_exact(g2, df, A, L.band);
     }
     wave_lds_sync();  // the slot is reused by the wave's next test
+    if (A.trace && lane == 0) {
+        const unsigned long long c3 = clock64();
+        ph[0] += c1 - c0, ph[1] += c2 - c1, ph[2] += c3 - c2, ph[3] += 1;
+    }
+    return r;
+}
+
+// ---- one test per wave on the 2-bit packed columns (d = 2, 3: tables of <= 4^5 = 1024 cells): the
+// wave's histogram, margins and adjusted df in its LDS region (wh: hist[1024] ni[256] nj[256]
+// nk[64] dfp[64]); z index with the LAST conditioning variable fastest (src/CellTable.cpp:39-51,
+// 277-281); G^2 as block_test, the in-order fallback 64 terms at a time
+template <int D>
+__device__ __noinline__ Decision wave_hist_test(const PcSmallArgs &A, const Lds &L, int x, int y, const int *z,
+                                                int lane, int32_t *wh, unsigned long long *ph) {
+    const unsigned long long c0 = A.trace ? clock64() : 0;
+    const int dx = L.dims[x], dy = L.dims[y];
+    int cum[D], dimz = 1;
+#pragma unroll
+    for (int j = D - 1; j >= 0; --j) cum[j] = dimz, dimz *= L.dims[z[j]];
+    const int dxy = dx * dy, cells = dimz * dxy;
+    int32_t *hist = wh, *ni = wh + 1024, *nj = ni + 256, *nk = nj + 256, *dfp = nk + 64;
+    // up to 4 sub-histogram copies (lane l adds into copy l mod copies, copies at an odd stride: a
+    // popular cell's same-address LDS atomics serialize copies-fold less), merged after the sweep
+    int copies = 1;
+    while (copies < 4 && 2 * copies * (cells | 1) <= 1024) copies *= 2;
+    const int cstr = copies > 1 ? (cells | 1) : cells;
+    for (int c = lane; c < copies * cstr; c += 64) hist[c] = 0;
+    int32_t *myh = hist + (lane & (copies - 1)) * cstr;
+    wave_lds_sync();
+    const long long PW = A.PW, N = A.N;
+    const uint32_t *px = A.pk + (size_t)x * PW, *py = A.pk + (size_t)y * PW;
+    const uint32_t *pz[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) pz[j] = A.pk + (size_t)z[j] * PW;
+    // kU words of every column in flight per lane: one memory latency per kU words, not per word
+    constexpr int kU = 4;
+    for (long long w0 = lane; w0 < PW; w0 += 64 * kU) {
+        uint32_t wx[kU], wy[kU], wz[kU][D];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const long long w = w0 + 64 * u < PW ? w0 + 64 * u : w0;
+            wx[u] = px[w], wy[u] = py[w];
+#pragma unroll
+            for (int j = 0; j < D; ++j) wz[u][j] = pz[j][w];
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const long long w = w0 + 64 * u;
+            const long long left = w < PW ? N - 16 * w : 0;
+            const int lim = left < 16 ? (int)left : 16;
+#pragma unroll
+            for (int s = 0; s < 16; ++s) {
+                if (s >= lim) break;
+                int zi = 0;
+#pragma unroll
+                for (int j = 0; j < D; ++j) zi += (int)((wz[u][j] >> (2 * s)) & 3u) * cum[j];
+                atomicAdd(&myh[(zi * dx + (int)((wx[u] >> (2 * s)) & 3u)) * dy + (int)((wy[u] >> (2 * s)) & 3u)], 1);
+            }
+        }
+    }
+    wave_lds_sync();
+    if (copies > 1) {
+        for (int c = lane; c < cells; c += 64) {
+            int v = 0;
+            for (int k = 0; k < copies; ++k) v += hist[k * cstr + c];
+            hist[c] = v;  // copy 0 in place: cell c of copy 0 is read only by this lane
+        }
+        wave_lds_sync();
+    }
+    const unsigned long long c1 = A.trace ? clock64() : 0;
+    // marginals N_{x+z}, N_{+yz} (src/CellTable.cpp:242-250)
+    for (int r = lane; r < dimz * dx; r += 64) {
+        const int k = r / dx, i = r % dx;
+        int sm = 0;
+        for (int j = 0; j < dy; ++j) sm += hist[k * dxy + i * dy + j];
+        ni[r] = sm;
+    }
+    for (int r = lane; r < dimz * dy; r += 64) {
+        const int k = r / dy, j = r % dy;
+        int sm = 0;
+        for (int i = 0; i < dx; ++i) sm += hist[k * dxy + i * dy + j];
+        nj[r] = sm;
+    }
+    wave_lds_sync();
+    // N_{++z}, adjusted df per z (src/IndependenceTest.cpp:96-112)
+    for (int k = lane; k < dimz; k += 64) {
+        int alx = 0, aly = 0, tot = 0;
+        for (int i = 0; i < dx; ++i) alx += ni[k * dx + i] > 0, tot += ni[k * dx + i];
+        for (int j = 0; j < dy; ++j) aly += nj[k * dy + j] > 0;
+        dfp[k] = ((alx >= 1 ? alx : 1) - 1) * ((aly >= 1 ? aly : 1) - 1);
+        nk[k] = tot;
+    }
+    wave_lds_sync();
+    const unsigned long long c2 = A.trace ? clock64() : 0;
+    auto term_of = [&](int c) {
+        const int k = c / dxy, i = (c / dy) % dx, j = c % dy;
+        return g2_term(hist[c], ni[k * dx + i], nj[k * dy + j], nk[k]);
+    };
+    double ps = 0.0, pa = 0.0;
+    int df = 0;
+    for (int c = lane; c < cells; c += 64) {
+        const double t = term_of(c);
+        ps += t;
+        pa += fabs(t);
+    }
+    for (int k = lane; k < dimz; k += 64) df += dfp[k];
+    ps = wsum_f64(ps);
+    pa = wsum_f64(pa);
+    df = wsum_i32(df);
+    Decision r = decide_tree(ps, pa, df, cells, A, L.band);
+    if (r.ind < 0) {  // in-order running sum over z -> x -> y, 64 terms at a time
+        double g2 = 0.0;
+        for (int c0 = 0; c0 < cells; c0 += 64) {
+            const double t = c0 + lane < cells ? term_of(c0 + lane) : 0.0;
+            const int m = cells - c0 < 64 ? cells - c0 : 64;
+            for (int l = 0; l < m; ++l) g2 += __shfl(t, l);
+        }
+        r = decide_exact(g2, df, A, L.band);
+    }
+    wave_lds_sync();  // the region is reused by the wave's next test
+    if (A.trace && lane == 0) {
+        const unsigned long long c3 = clock64();
+        ph[0] += c1 - c0, ph[1] += c2 - c1, ph[2] += c3 - c2, ph[3] += 1;
+    }
     return r;
 }
 
@@ -387,10 +581,10 @@ __device__ __noinline__ Decision wave_test(const PcSmallArgs &A, int x, int y, i
 template <int D>
 __device__ __noinline__ Decision block_test(const PcSmallArgs &A, int x, int y, const int *z, Lds &L) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int dx = A.dims[x], dy = A.dims[y];
+    const int dx = L.dims[x], dy = L.dims[y];
     int cum[D], dimz = 1;
 #pragma unroll
-    for (int j = D - 1; j >= 0; --j) cum[j] = dimz, dimz *= A.dims[z[j]];
+    for (int j = D - 1; j >= 0; --j) cum[j] = dimz, dimz *= L.dims[z[j]];
     const int dxy = dx * dy, cells = dimz * dxy;
     // sub-histogram copies: each wave adds into copy (wave mod copies), fewer same-cell conflicts
     int copies = 1;
@@ -465,19 +659,16 @@ __device__ __noinline__ Decision block_test(const PcSmallArgs &A, int x, int y, 
         pa += fabs(t);
     }
     for (int k = tid; k < dimz; k += BS) pdf += L.dfp[k];
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        ps += __shfl_xor(ps, o);
-        pa += __shfl_xor(pa, o);
-        pdf += __shfl_xor(pdf, o);
-    }
+    ps = wsum_f64(ps);
+    pa = wsum_f64(pa);
+    pdf = wsum_i32(pdf);
     if (lane == 0) L.red[2 * wv] = ps, L.red[2 * wv + 1] = pa, L.redi[wv] = pdf;
     __syncthreads();
     double gs = 0.0, ga = 0.0;
     int df = 0;
 #pragma unroll
     for (int w = 0; w < NWAVE; ++w) gs += L.red[2 * w], ga += L.red[2 * w + 1], df += L.redi[w];
-    Decision r = decide_tree(gs, ga, df, cells, A);
+    Decision r = decide_tree(gs, ga, df, cells, A, L.band);
     if (r.ind < 0) {  // in-order running sum over z -> x -> y, chunk by chunk (terms in LDS)
         double g2 = 0.0;
         for (int c0 = 0; c0 < cells; c0 += kTermChunk) {
@@ -490,7 +681,7 @@ __device__ __noinline__ Decision block_test(const PcSmallArgs &A, int x, int y, 
         }
         if (tid == 0) L.g2 = g2;
         __syncthreads();
-        r = decide_exact(L.g2, df, A);
+        r = decide_exact(L.g2, df, A, L.band);
     }
     __syncthreads();  // LDS reused by the next test
     return r;
@@ -509,15 +700,26 @@ __device__ void finalize(const PcSmallArgs &A, Lds &L, int nb, int levels, int h
     }
     mm = block_min_u64(mm, L);
     nn = block_sum_ll(nn, L);
+    PcSmallOut *o = A.dout;
     if (tid == 0) {
-        A.out->margin_bits = mm;
-        A.out->near = (unsigned long long)nn;
+        o->margin_bits = mm;
+        o->near = (unsigned long long)nn;
         A.ctx_stats[0] = mm;
         A.ctx_stats[1] = (unsigned long long)nn;
-        A.out->levels = levels;
-        A.out->handoff = handoff;
-        A.out->status = 0;
+        o->levels = levels;
+        o->handoff = handoff;
+        o->status = 0;
+        o->pad = 0;
+        for (int d = levels; d <= kSmallMaxD; ++d) o->sep_off[d + 1] = o->sep_off[d > 0 ? d : 0];
     }
+    __syncthreads();
+    // the record, built in device memory during the run, goes to the pinned host copy in one
+    // parallel pass: everything before the sepset pool, then the pool's used part
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(o);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(A.out);
+    const int head = (int)(offsetof(PcSmallOut, pool) / 4);
+    const int used = head + (levels > 0 ? o->sep_off[levels] : 0);
+    for (int i = tid; i < used; i += BS) dst[i] = src[i];
 }
 
 __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) {
@@ -536,7 +738,15 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
     for (int v = tid; v < kSmallMaxVars; v += BS) {
         const uint64_t all = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
         L.adj[v] = v < n ? (all & ~(1ull << v)) : 0ull;
+        L.dims[v] = v < n ? A.dims[v] : 1;
+        L.row0[v] = v < n ? A.row0[v] : 0;
     }
+    for (int r = tid; r < 4 * kSmallMaxVars; r += BS) L.rowcnt[r] = 0;
+    if (A.band)
+        for (int i = tid; i <= 2 * A.nband; i += BS) L.band[i] = A.band[i];
+    __syncthreads();
+    for (int v = tid; v < n; v += BS)
+        for (int a = 0; a < L.dims[v]; ++a) L.rowcnt[L.row0[v] + a] = A.rowcnt[L.row0[v] + a];
     __syncthreads();
     // this workgroup's statistics slot: [0] min margin bits, [1] near, [2 + d] tests evaluated
     unsigned long long wmin = ~0ull, wnear = 0ull;
@@ -545,19 +755,16 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
     int32_t sep_cursor = 0;
     for (int d = 0;; ++d) {
         // ---- the level's edges (lexicographic pairs of the snapshot) and their test offsets
-        if (tid <= kSmallMaxVars) {
-            int c = 0;
-            if (tid > 0 && tid - 1 < n) {
-                const int x = tid - 1;
-                c = x + 1 < 64 ? popc64(L.adj[x] >> (x + 1)) : 0;
+        if (tid < 64) {  // rowoff[x] = edges (x' < y) of rows x' < x: one wave's inclusive scan
+            int c = tid < n && tid + 1 < 64 ? popc64(L.adj[tid] >> (tid + 1)) : 0;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(c, o);
+                if (tid >= o) c += y;
             }
-            L.rowoff[tid] = c;  // counts, prefix-summed below
-        }
-        __syncthreads();
-        if (tid == 0) {
-            int s = 0;
-            for (int i = 0; i <= kSmallMaxVars; ++i) s += L.rowoff[i], L.rowoff[i] = s;
-            L.E = s;  // rowoff[x] = edges of rows < x
+            L.rowoff[tid + 1] = c;
+            if (tid == 0) L.rowoff[0] = 0;
+            if (tid == 63) L.E = c;
         }
         __syncthreads();
         const int E = L.E;
@@ -603,10 +810,14 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
             return;
         }
         const int T = (int)tot64;
+        for (int e = tid; e < E; e += BS) L.bfirst[e] = ~0u;
+        if (tid < NWAVE * 4) (&L.ph[0][0])[tid] = 0ull;
+        __syncthreads();
         if (A.trace && bid == 0 && tid == 0) A.trace[8 * d + 0] = (unsigned long long)wall_clock64();
+        if (A.trace && tid == 0) A.trace[64 + 5 * 1024 + (size_t)d * 1024 + bid] = (unsigned long long)wall_clock64();
         // ---- the tests
         unsigned long long launched = 0;
-        if (d <= 1) {
+        if (d <= 2) {
             const int gw = bid * NWAVE + wv, nw = nb * NWAVE;
             for (int t = gw; t < T; t += nw) {
                 int lo = 0, hi = E;  // last edge whose first test <= t
@@ -619,19 +830,19 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
                 const int x = L.ex[e], y = L.ey[e];
                 Decision r;
                 if (d == 0) {
-                    r = wave_test<0>(A, x, y, 0, lane, true, L.wtab[wv], L.waux[wv]);
+                    r = wave_test<0>(A, L, x, y, 0, lane, true, L.wtab[wv], L.waux[wv], L.ph[wv]);
                 } else {
-                    int zz[1];
-                    unrank(L, x, y, 1, k, zz);
-                    r = wave_test<1>(A, x, y, zz[0], lane, false, L.wtab[wv], L.waux[wv]);
+                    int zz[3];
+                    unrank(L, x, y, d, k, zz);
+                    if (d == 1) r = wave_test<1>(A, L, x, y, zz[0], lane, false, L.wtab[wv], L.waux[wv], L.ph[wv]);
+                    else if (d == 2) r = wave_hist_test<2>(A, L, x, y, zz, lane, L.whist[wv], L.ph[wv]);
+                    else r = wave_hist_test<3>(A, L, x, y, zz, lane, L.whist[wv], L.ph[wv]);
                 }
                 ++launched;
                 const unsigned long long mb = (unsigned long long)__double_as_longlong(r.margin);
                 wmin = mb < wmin ? mb : wmin;
                 wnear += r.margin < 1e-9;
-                if (r.ind == 1 && lane == 0)  // first[] holds ~min k (0 = none): max of the complements
-                    __hip_atomic_fetch_max(A.first + (size_t)d * kSmallMaxEdges + e, ~(unsigned)k, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
+                if (r.ind == 1 && lane == 0) atomicMin(&L.bfirst[e], (unsigned)k);  // LDS, flushed below
             }
         } else {
             for (int t = bid; t < T; t += nb) {
@@ -646,20 +857,23 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
                 int zz[kSmallMaxD];
                 unrank(L, x, y, d, k, zz);
                 Decision r;
-                if (d == 2) r = block_test<2>(A, x, y, zz, L);
-                else if (d == 3) r = block_test<3>(A, x, y, zz, L);
-                else r = block_test<4>(A, x, y, zz, L);
+                r = d == 3 ? block_test<3>(A, x, y, zz, L) : block_test<4>(A, x, y, zz, L);
                 if (tid == 0) {
                     ++launched;
                     const unsigned long long mb = (unsigned long long)__double_as_longlong(r.margin);
                     wmin = mb < wmin ? mb : wmin;
                     wnear += r.margin < 1e-9;
-                    if (r.ind == 1)
-                        __hip_atomic_fetch_max(A.first + (size_t)d * kSmallMaxEdges + e, ~(unsigned)k,
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (r.ind == 1) atomicMin(&L.bfirst[e], (unsigned)k);
                 }
             }
         }
+        // this workgroup's first independent candidates -> the global per-edge words (first[] holds
+        // ~min k, 0 = none: an atomic max of the complements), all in flight together
+        __syncthreads();
+        for (int e = tid; e < E; e += BS)
+            if (L.bfirst[e] != ~0u)
+                __hip_atomic_fetch_max(A.first + (size_t)d * kSmallMaxEdges + e, ~L.bfirst[e], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
         // this workgroup's statistics into its slot (plain stores, published by the barrier)
         {
             const unsigned long long mm = block_min_u64(lane == 0 ? wmin : ~0ull, L);
@@ -672,6 +886,11 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
             }
         }
         if (A.trace && tid == 0) A.trace[64 + (size_t)d * 1024 + bid] = (unsigned long long)wall_clock64();
+        if (A.trace && tid < 4) {  // phase cycles summed over the workgroup's waves -> trace[8d + 4 + k]
+            unsigned long long sum = 0;
+            for (int w = 0; w < NWAVE; ++w) sum += L.ph[w][tid];
+            atomicAdd(A.trace + 8 * d + 4 + tid, sum);
+        }
         if (!grid_barrier(B, ++phase, L)) {
             if (tid == 0) A.out->status = 1;
             return;
@@ -701,18 +920,19 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
                                                           __HIP_MEMORY_SCOPE_AGENT);
                     int zz[kSmallMaxD];
                     unrank(L, L.ex[e], L.ey[e], d, (int)f, zz);
-                    for (int j = 0; j < d; ++j) A.out->pool[sep_cursor + (carry + off) * d + j] = zz[j];
+                    for (int j = 0; j < d; ++j) A.dout->pool[sep_cursor + (carry + off) * d + j] = zz[j];
                 }
                 carry += total;
                 __syncthreads();
             }
+            long long la = 0;
+            for (int b = tid; b < nb; b += BS) la += (long long)A.acc[8 * (size_t)b + 2 + d];
+            la = block_sum_ll(la, L);
             if (tid == 0) {
-                A.out->sep_off[d] = sep_cursor;
-                A.out->sep_off[d + 1] = sep_cursor + carry * d;
-                A.out->counted[d] = counted;
-                long long la = 0;
-                for (int b = 0; b < nb; ++b) la += (long long)A.acc[8 * (size_t)b + 2 + d];
-                A.out->launched[d] = la;
+                A.dout->sep_off[d] = sep_cursor;
+                A.dout->sep_off[d + 1] = sep_cursor + carry * d;
+                A.dout->counted[d] = counted;
+                A.dout->launched[d] = la;
             }
             sep_cursor += carry * d;
         }
@@ -727,7 +947,7 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
         if (A.trace && bid == 0 && tid == 0) A.trace[8 * d + 3] = (unsigned long long)wall_clock64();
         int maxdeg = 0;
         for (int v = 0; v < n; ++v) maxdeg = maxdeg > popc64(L.adj[v]) ? maxdeg : popc64(L.adj[v]);
-        if (bid == 0 && tid < kSmallMaxVars) A.out->adj[d][tid] = L.adj[tid];
+        if (bid == 0 && tid < kSmallMaxVars) A.dout->adj[d][tid] = L.adj[tid];
         const bool cont = d + 1 < A.depth && (d == 0 || maxdeg - 1 > d);  // FreeDegree (src/PCStable.cpp:557-563)
         if (!cont) {
             if (bid == 0) finalize(A, L, nb, d + 1, 0);
