@@ -47,6 +47,12 @@ extern "C" hipError_t fbn_ci_bits_rowcount(const uint32_t *bits, long long rows,
                                            hipStream_t s);
 extern "C" int fbn_ci_pair_block(int d);
 extern "C" int fbn_ci_gram_task_ints(void);
+extern "C" hipError_t fbn_ci_onehot4_build(const uint8_t *cols, const int32_t *dims, const int32_t *lead0, long long N,
+                                           long long Kb, int nvars, uint8_t *O4, hipStream_t s);
+extern "C" hipError_t fbn_ci_gram4(const uint8_t *O4, long long Kb, const int2 *tasks, int nt, int S, int KS,
+                                   uint16_t *slab, int R, long long ld, int32_t *gram, hipStream_t s);
+extern "C" int fbn_ci_gram4_tile(void);
+extern "C" int fbn_ci_gram4_stage(void);
 extern "C" hipError_t fbn_ci_sum_planes(const int32_t *planes, int np, long long n, int32_t *out, hipStream_t s);
 extern "C" hipError_t fbn_ci_onehot_build(const uint8_t *cols, const int32_t *dims, const int32_t *lead0, long long N,
                                           long long Npad, int nvars, int8_t *out, hipStream_t s);
@@ -237,7 +243,13 @@ struct fbn_ci_ctx {
     DevBuf l1pairs, l1adj, l1adjoff, l1ed, l1pos, l1st, l1sep, l1cnt, l1len, l1off, l1scal, l1open;
     DevBuf l1items, l1counts, l1df, l1indep, l1tmp;
     DevBuf keptidx, kepttmp;  // level-0 kept pair indices (CiAllPairsKept)
-    // level-0 Gram as an int8 library GEMM: one byte per (leading row, sample), rocBLAS handle
+    // level-0 Gram on the matrix cores (ci_gram_mfma.hip): FP4 one-hot store (Rp x Kb bytes, built
+    // once), the tile list of row range [g4_r0, g4_r1), split-K slabs
+    DevBuf onehot4, g4tasks, g4slab;
+    int64_t g4_r0 = -1, g4_r1 = -1, g4_Kb = 0;
+    int g4_nt = 0;
+    bool onehot4_ready = false;
+    // level-0 Gram as an int8 library GEMM (FBN_CI_GRAM_ROCBLAS=1 only: the measured alternative)
     DevBuf onehot, gram0split;
     int64_t onehot_Npad = 0;
     bool onehot_ready = false, blas_failed = false;
@@ -1227,6 +1239,74 @@ static int CiGram0Tasks(fbn_ci_ctx *c, int64_t t0, int64_t t1, hipStream_t s) {
     return FBN_OK;
 }
 
+// x-variable row range [r0, r1) of the leading rows that the pairs [t0, t0 + n) read as rows of G
+static void CiPairRowRange(const fbn_ci_ctx *c, int64_t t0, int64_t n, int64_t *r0, int64_t *r1) {
+    const int nv = c->nvars;
+    auto row_of = [&](int64_t t) {
+        int64_t lo = 0, hi = nv - 2;
+        while (lo < hi) {
+            const int64_t m = (lo + hi + 1) / 2;
+            if (m * nv - m * (m + 1) / 2 <= t) lo = m;
+            else hi = m - 1;
+        }
+        return (int)lo;
+    };
+    const int u0 = row_of(t0), u1 = row_of(t0 + n - 1);
+    *r0 = c->lead0_host[u0];
+    *r1 = u1 + 1 < nv ? c->lead0_host[u1 + 1] : (int64_t)c->leadrows_host.size();
+}
+
+// The level-0 Gram on the matrix cores, hand-written (ci_gram_mfma.hip): FP4 one-hot store built
+// once per ctx, the 256 x 256 tiles (I, J >= I) covering rows [r0, r1) x all columns, split-K so the
+// launch fills the CUs, uint16 partial slabs summed into gram0 (entries i < j).  *done = false: not
+// used (small Gram -- ALARM's 60 rows x 5k samples stay on the popcount kernel --, over the byte
+// budget, or FBN_CI_GRAM_NO_MFMA).
+constexpr int64_t kOnehot4MaxBytes = (int64_t)4 << 30;
+static int CiGram0Mfma(fbn_ci_ctx *c, int64_t t0, int64_t n, hipStream_t s, bool *done) {
+    *done = false;
+    const int64_t R = (int64_t)c->leadrows_host.size(), T = fbn_ci_gram4_tile(), KT = fbn_ci_gram4_stage();
+    const int64_t Rp = (R + T - 1) / T * T, KS = (c->N + KT - 1) / KT, Kb = KS * KT / 2;
+    if (getenv("FBN_CI_GRAM_NO_MFMA") || (double)R * R * c->N < 1e10 || Rp * Kb > kOnehot4MaxBytes || KS > INT32_MAX)
+        return FBN_OK;
+    int rc;
+    if (!c->onehot4_ready) {
+        if ((rc = c->onehot4.ensure((size_t)(Rp * Kb)))) return rc;
+        FBN_HIP(hipMemsetAsync(c->onehot4.p, 0, (size_t)(Rp * Kb), s));  // pad rows R..Rp-1
+        hipError_t e = fbn_ci_onehot4_build(c->cols.as<uint8_t>(), c->ddims.as<int32_t>(), c->lead0.as<int32_t>(), c->N,
+                                            Kb, c->nvars, c->onehot4.as<uint8_t>(), s);
+        if (e != hipSuccess) return SetError(FBN_ERR_HIP, "fp4 one-hot build: %s", hipGetErrorString(e));
+        c->g4_Kb = Kb;
+        c->onehot4_ready = true;
+    }
+    int64_t r0, r1;
+    CiPairRowRange(c, t0, n, &r0, &r1);
+    if (r1 <= r0) {
+        *done = true;
+        return FBN_OK;
+    }
+    if (c->g4_r0 != r0 || c->g4_r1 != r1) {
+        std::vector<int32_t> tasks;
+        const int64_t nb = Rp / T;
+        for (int64_t I = r0 / T; I <= (r1 - 1) / T; ++I)
+            for (int64_t J = I; J < nb; ++J) tasks.push_back((int32_t)I), tasks.push_back((int32_t)J);
+        if ((rc = c->g4tasks.ensure(tasks.size() * 4))) return rc;
+        FBN_HIP(hipMemcpyAsync(c->g4tasks.p, tasks.data(), tasks.size() * 4, hipMemcpyHostToDevice, s));
+        FBN_HIP(hipStreamSynchronize(s));  // the host vector goes out of scope
+        c->g4_nt = (int)(tasks.size() / 2), c->g4_r0 = r0, c->g4_r1 = r1;
+    }
+    // split-K: about one block per CU; uint16 partials need every slice <= 65535 samples
+    const int nt = c->g4_nt;
+    int64_t S = std::max<int64_t>(1, EnvOr0("FBN_CI_GRAM4_SPLITS", c->num_cu / nt));
+    S = std::max<int64_t>(S, (KS + 510) / 511);  // slices of <= 511 stages x 128 samples
+    S = std::min<int64_t>(S, KS);
+    if ((rc = c->g4slab.ensure((size_t)(nt * S * T * T * 2)))) return rc;
+    hipError_t e = fbn_ci_gram4(c->onehot4.as<uint8_t>(), Kb, c->g4tasks.as<int2>(), nt, (int)S, (int)KS,
+                                c->g4slab.as<uint16_t>(), (int)R, R, c->gram0.as<int32_t>(), s);
+    if (e != hipSuccess) return SetError(FBN_ERR_HIP, "mfma gram: %s", hipGetErrorString(e));
+    *done = true;
+    return FBN_OK;
+}
+
 // The level-0 Gram as an int8 GEMM on the matrix cores (rocBLAS gemm_ex, int32 accumulation: the
 // counts are exact): O = one byte per (leading row, sample), built once per ctx; for the pairs
 // [t0, t0 + n) only the columns of their x-variables' leading rows are computed (C[:, r0:r1] = O^T
@@ -1238,7 +1318,7 @@ static int CiGram0Blas(fbn_ci_ctx *c, int64_t t0, int64_t n, hipStream_t s, bool
     const int64_t R = (int64_t)c->leadrows_host.size(), Npad = (c->N + 511) & ~(int64_t)511;
     // small Grams (ALARM: 60 rows x 5k samples) stay on the popcount kernel: a library call and the
     // one-hot store cost more than they save there
-    if (c->blas_failed || getenv("FBN_CI_GRAM_NO_BLAS") || R * Npad > kOnehotMaxBytes || Npad > INT32_MAX ||
+    if (c->blas_failed || !getenv("FBN_CI_GRAM_ROCBLAS") || getenv("FBN_CI_GRAM_NO_BLAS") || R * Npad > kOnehotMaxBytes || Npad > INT32_MAX ||
         (double)R * R * Npad < 1e10 || !Blas().ok)
         return FBN_OK;
     int rc;
@@ -1426,7 +1506,8 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
             const int64_t R = (int64_t)c->leadrows_host.size();
             if ((rc = c->gram0.ensure((size_t)(R * R * 4)))) return rc;
             bool done = false;
-            if ((rc = CiGram0Blas(c, pair0, n, s, &done))) return rc;
+            if (!getenv("FBN_CI_GRAM_NO_BLAS") && (rc = CiGram0Mfma(c, pair0, n, s, &done))) return rc;
+            if (!done && (rc = CiGram0Blas(c, pair0, n, s, &done))) return rc;
             if (!done) {
                 if ((rc = CiGram0Tasks(c, pair0, pair0 + n, s))) return rc;
                 e = fbn_ci_gram(c->bits.as<uint32_t>(), c->bits_W, c->leadrows.as<int32_t>(),
