@@ -48,8 +48,8 @@ extern "C" hipError_t fbn_ci_bits_rowcount(const uint32_t *bits, long long rows,
 extern "C" int fbn_ci_pair_block(int d);
 extern "C" int fbn_ci_gram_task_ints(void);
 extern "C" hipError_t fbn_ci_onehot4_build(const uint8_t *cols, const int32_t *dims, const int32_t *lead0, long long N,
-                                           long long Kb, int nvars, uint8_t *O4, hipStream_t s);
-extern "C" hipError_t fbn_ci_gram4(const uint8_t *O4, long long Kb, const int2 *tasks, int nt, int S, int KS,
+                                           long long KS, long long Rp, int nvars, uint8_t *O4, hipStream_t s);
+extern "C" hipError_t fbn_ci_gram4(const uint8_t *O4, long long Rp, const int2 *tasks, int nt, int S, int KS,
                                    uint16_t *slab, int R, long long ld, int32_t *gram, hipStream_t s);
 extern "C" int fbn_ci_gram4_tile(void);
 extern "C" int fbn_ci_gram4_stage(void);
@@ -244,9 +244,9 @@ struct fbn_ci_ctx {
     DevBuf l1items, l1counts, l1df, l1indep, l1tmp;
     DevBuf keptidx, kepttmp;  // level-0 kept pair indices (CiAllPairsKept)
     // level-0 Gram on the matrix cores (ci_gram_mfma.hip): FP4 one-hot store (Rp x Kb bytes, built
-    // once), the tile list of row range [g4_r0, g4_r1), split-K slabs
+    // once, stage-major), the tile list of row range [g4_r0, g4_r1), split-K slabs
     DevBuf onehot4, g4tasks, g4slab;
-    int64_t g4_r0 = -1, g4_r1 = -1, g4_Kb = 0;
+    int64_t g4_r0 = -1, g4_r1 = -1;
     int g4_nt = 0;
     bool onehot4_ready = false;
     // level-0 Gram as an int8 library GEMM (FBN_CI_GRAM_ROCBLAS=1 only: the measured alternative)
@@ -1273,9 +1273,8 @@ static int CiGram0Mfma(fbn_ci_ctx *c, int64_t t0, int64_t n, hipStream_t s, bool
         if ((rc = c->onehot4.ensure((size_t)(Rp * Kb)))) return rc;
         FBN_HIP(hipMemsetAsync(c->onehot4.p, 0, (size_t)(Rp * Kb), s));  // pad rows R..Rp-1
         hipError_t e = fbn_ci_onehot4_build(c->cols.as<uint8_t>(), c->ddims.as<int32_t>(), c->lead0.as<int32_t>(), c->N,
-                                            Kb, c->nvars, c->onehot4.as<uint8_t>(), s);
+                                            KS, Rp, c->nvars, c->onehot4.as<uint8_t>(), s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "fp4 one-hot build: %s", hipGetErrorString(e));
-        c->g4_Kb = Kb;
         c->onehot4_ready = true;
     }
     int64_t r0, r1;
@@ -1300,7 +1299,7 @@ static int CiGram0Mfma(fbn_ci_ctx *c, int64_t t0, int64_t n, hipStream_t s, bool
     S = std::max<int64_t>(S, (KS + 510) / 511);  // slices of <= 511 stages x 128 samples
     S = std::min<int64_t>(S, KS);
     if ((rc = c->g4slab.ensure((size_t)(nt * S * T * T * 2)))) return rc;
-    hipError_t e = fbn_ci_gram4(c->onehot4.as<uint8_t>(), Kb, c->g4tasks.as<int2>(), nt, (int)S, (int)KS,
+    hipError_t e = fbn_ci_gram4(c->onehot4.as<uint8_t>(), Rp, c->g4tasks.as<int2>(), nt, (int)S, (int)KS,
                                 c->g4slab.as<uint16_t>(), (int)R, R, c->gram0.as<int32_t>(), s);
     if (e != hipSuccess) return SetError(FBN_ERR_HIP, "mfma gram: %s", hipGetErrorString(e));
     *done = true;
