@@ -283,8 +283,8 @@ def pc_roofline(kernel_s, device_bytes, byte_column_bytes):
             "dominant_kernel": {top: ks[top]}, "source": "profiles/pc5_kernels.json",
             "note": "all CI kernels of one run: PMC VALU lane-ops and calibrated L2<->fabric bytes per run over the "
                     "live kernel time; neither bound is reached: the popcount kernels are bound by v_bcnt issue "
-                    "(half rate on gfx950, tools/micro/valu_rate.hip) and latency, the level-0 Gram is an int8 GEMM "
-                    "on the matrix cores (DESIGN.md 5.3)"}
+                    "(half rate on gfx950, tools/micro/valu_rate.hip) and latency, the level-0 Gram is a hand-written "
+                    "FP4 MFMA kernel on the matrix cores (ci_gram_mfma.hip, DESIGN.md 5.3)"}
 
 
 def synth_c5(nvars=N_VARS_C5, nsamples=100_000):
