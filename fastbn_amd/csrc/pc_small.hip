@@ -63,6 +63,7 @@ struct Lds {
     int32_t binom[kSmallMaxVars + 1][kSmallMaxD + 1];
     int32_t wscan[NWAVE];
     long long wsum[NWAVE];
+    unsigned long long wst[NWAVE][3];  // per-wave statistics of a level: min margin bits, near, launched
     int32_t E;
     long long T;
     int flag;
@@ -246,6 +247,25 @@ __device__ __forceinline__ int block_excl_scan(int v, Lds &L, int *total) {
     }
     *total = tot;
     return before + x - v;
+}
+
+// g + t(lane 0) + t(lane 1) + ... + t(lane 63), one add at a time in lane order (the reference's
+// running sum), skipping the terms that are 0.0 (empty cells, unit ratios): x + 0.0 == x for every
+// running sum that can occur (never -0.0: it starts at +0.0 and round-to-nearest gives +0.0 for
+// a + (-a)), so the result is the full in-order sum bit for bit; v_readlane with a uniform lane
+// index, no LDS round trip
+__device__ __forceinline__ double wave_inorder_add(double g, double t) {
+    unsigned long long m = __ballot(t != 0.0);
+    const long long bits = __double_as_longlong(t);
+    const int lo = (int)(bits & 0xffffffffll), hi = (int)(bits >> 32);
+    while (m) {
+        const int l = __ffsll((unsigned long long)m) - 1;
+        m &= m - 1;
+        const unsigned long long b = ((unsigned long long)(unsigned)__builtin_amdgcn_readlane(hi, l) << 32) |
+                                     (unsigned)__builtin_amdgcn_readlane(lo, l);
+        g += __longlong_as_double((long long)b);
+    }
+    return g;
 }
 
 // ---- G^2 decision, shared by the wave and workgroup paths.  The reference (src/IndependenceTest.cpp
@@ -444,9 +464,7 @@ __device__ __forceinline__ Decision wave_test(const PcSmallArgs &A, const Lds &L
     const double gs = wsum_f64(t), ga = wsum_f64(fabs(t));
     Decision r = decide_tree(gs, ga, df, cells, A, L.band);
     if (r.ind < 0) {  // in the band: the reference's in-order running sum, then p
-        double g2 = 0.0;
-        for (int l = 0; l < cells; ++l) g2 += __shfl(t, l);
-        r = decide_exact(g2, df, A, L.band);
+        r = decide_exact(wave_inorder_add(0.0, t), df, A, L.band);  // lane l = cell l (t = 0 beyond)
     }
     wave_lds_sync();  // the slot is reused by the wave's next test
     if (A.trace && lane == 0) {
@@ -501,11 +519,11 @@ __device__ __noinline__ Decision wave_hist_test(const PcSmallArgs &A, const Lds 
             const int lim = left < 16 ? (int)left : 16;
 #pragma unroll
             for (int s = 0; s < 16; ++s) {
-                if (s >= lim) break;
                 int zi = 0;
 #pragma unroll
                 for (int j = 0; j < D; ++j) zi += (int)((wz[u][j] >> (2 * s)) & 3u) * cum[j];
-                atomicAdd(&myh[(zi * dx + (int)((wx[u] >> (2 * s)) & 3u)) * dy + (int)((wy[u] >> (2 * s)) & 3u)], 1);
+                const int cl = (zi * dx + (int)((wx[u] >> (2 * s)) & 3u)) * dy + (int)((wy[u] >> (2 * s)) & 3u);
+                if (s < lim) atomicAdd(&myh[cl], 1);
             }
         }
     }
@@ -563,8 +581,7 @@ __device__ __noinline__ Decision wave_hist_test(const PcSmallArgs &A, const Lds 
         double g2 = 0.0;
         for (int c0 = 0; c0 < cells; c0 += 64) {
             const double t = c0 + lane < cells ? term_of(c0 + lane) : 0.0;
-            const int m = cells - c0 < 64 ? cells - c0 : 64;
-            for (int l = 0; l < m; ++l) g2 += __shfl(t, l);
+            g2 = wave_inorder_add(g2, t);
         }
         r = decide_exact(g2, df, A, L.band);
     }
@@ -581,6 +598,7 @@ __device__ __noinline__ Decision wave_hist_test(const PcSmallArgs &A, const Lds 
 template <int D>
 __device__ __noinline__ Decision block_test(const PcSmallArgs &A, int x, int y, const int *z, Lds &L) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const unsigned long long c0 = A.trace ? clock64() : 0;
     const int dx = L.dims[x], dy = L.dims[y];
     int cum[D], dimz = 1;
 #pragma unroll
@@ -607,12 +625,11 @@ __device__ __noinline__ Decision block_test(const PcSmallArgs &A, int x, int y, 
         const int lim = left < 16 ? (int)left : 16;
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
-            if (s >= lim) break;
             int zi = 0;
 #pragma unroll
             for (int j = 0; j < D; ++j) zi += (int)((wz[j] >> (2 * s)) & 3u) * cum[j];
             const int cl = (zi * dx + (int)((wx >> (2 * s)) & 3u)) * dy + (int)((wy >> (2 * s)) & 3u);
-            atomicAdd(&my[cl], 1);
+            if (s < lim) atomicAdd(&my[cl], 1);
         }
     }
     __syncthreads();
@@ -624,6 +641,7 @@ __device__ __noinline__ Decision block_test(const PcSmallArgs &A, int x, int y, 
         }
         __syncthreads();
     }
+    const unsigned long long c1 = A.trace ? clock64() : 0;
     // marginals N_{x+z}, N_{+yz}, N_{++z}, adjusted df per z (src/CellTable.cpp:242-250,
     // src/IndependenceTest.cpp:96-112)
     for (int r = tid; r < dimz * dx; r += BS) {
@@ -647,6 +665,7 @@ __device__ __noinline__ Decision block_test(const PcSmallArgs &A, int x, int y, 
         L.nk[k] = tot;
     }
     __syncthreads();
+    const unsigned long long c2 = A.trace ? clock64() : 0;
     auto term_of = [&](int c) {
         const int k = c / dxy, i = (c / dy) % dx, j = c % dy;
         return g2_term(hist[c], L.ni[k * dx + i], L.nj[k * dy + j], L.nk[k]);
@@ -676,12 +695,16 @@ __device__ __noinline__ Decision block_test(const PcSmallArgs &A, int x, int y, 
             __syncthreads();
             for (int c = c0 + tid; c < c1; c += BS) L.term[c - c0] = term_of(c);
             __syncthreads();
-            if (tid == 0)
-                for (int c = 0; c < c1 - c0; ++c) g2 += L.term[c];
+            if (wv == 0)  // wave 0: 64 terms per step, zero terms skipped
+                for (int c = 0; c < c1 - c0; c += 64) g2 = wave_inorder_add(g2, c + lane < c1 - c0 ? L.term[c + lane] : 0.0);
         }
         if (tid == 0) L.g2 = g2;
         __syncthreads();
         r = decide_exact(L.g2, df, A, L.band);
+    }
+    if (A.trace && tid == 0) {
+        const unsigned long long c3 = clock64();
+        L.ph[0][0] += c1 - c0, L.ph[0][1] += c2 - c1, L.ph[0][2] += c3 - c2, L.ph[0][3] += 1;
     }
     __syncthreads();  // LDS reused by the next test
     return r;
@@ -781,27 +804,24 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
         }
         __syncthreads();
         // tests per edge (level 0: one marginal test; level d: C(|adj(x)|-1, d) + C(|adj(y)|-1, d))
-        // -> exclusive offsets, in chunks of BS edges
+        // -> exclusive offsets: thread tid owns a contiguous run of edges, one workgroup scan
         long long tot64 = 0;
         {
-            int carry = 0;
-            for (int e0 = 0; e0 < E; e0 += BS) {
-                const int e = e0 + tid;
-                int ne = 0;
-                if (e < E) {
-                    const int x = L.ex[e], y = L.ey[e];
-                    ne = d == 0 ? 1 : binom_l(L, popc64(L.adj[x]) - 1, d) + binom_l(L, popc64(L.adj[y]) - 1, d);
-                    tot64 += ne;
-                }
+            const int seg = (E + BS - 1) / BS, e0 = tid * seg, e1 = e0 + seg < E ? e0 + seg : E;
+            auto ntests = [&](int e) {
+                const int x = L.ex[e], y = L.ey[e];
+                return d == 0 ? 1 : binom_l(L, popc64(L.adj[x]) - 1, d) + binom_l(L, popc64(L.adj[y]) - 1, d);
+            };
+            long long mine = 0;  // (int64: a level's total may exceed 2^31 -> hand-off below)
+            for (int e = e0; e < e1; ++e) mine += ntests(e);
+            tot64 = block_sum_ll(mine, L);
+            if (tot64 <= kSmallMaxTests) {  // (workgroup-uniform) int32 offsets
                 int total = 0;
-                const int off = block_excl_scan(ne, L, &total);
-                if (e < E) L.eoff[e] = carry + off;
-                carry += total;
-                __syncthreads();
+                int run = block_excl_scan((int)mine, L, &total);
+                for (int e = e0; e < e1; ++e) L.eoff[e] = run, run += ntests(e);
+                if (tid == 0) L.eoff[E] = total;
             }
-            if (tid == 0) L.eoff[E] = carry;
         }
-        tot64 = block_sum_ll(tot64, L);
         __syncthreads();
         const bool fits = d <= kSmallMaxD && tot64 <= kSmallMaxTests;
         if (!fits) {
@@ -867,6 +887,8 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
                 }
             }
         }
+        // per-wave statistics (lane 0 holds the wave's; the workgroup path's are thread 0's)
+        if (lane == 0) L.wst[wv][0] = wmin, L.wst[wv][1] = wnear, L.wst[wv][2] = launched;
         // this workgroup's first independent candidates -> the global per-edge words (first[] holds
         // ~min k, 0 = none: an atomic max of the complements), all in flight together
         __syncthreads();
@@ -875,15 +897,16 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
                 __hip_atomic_fetch_max(A.first + (size_t)d * kSmallMaxEdges + e, ~L.bfirst[e], __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
         // this workgroup's statistics into its slot (plain stores, published by the barrier)
-        {
-            const unsigned long long mm = block_min_u64(lane == 0 ? wmin : ~0ull, L);
-            const long long nn = block_sum_ll(lane == 0 ? (long long)wnear : 0ll, L);
-            const long long ll = block_sum_ll(lane == 0 ? (long long)launched : 0ll, L);
-            if (tid == 0) {
-                slot[0] = mm;
-                slot[1] = (unsigned long long)nn;
-                slot[2 + d] = (unsigned long long)ll;
+        if (tid == 0) {
+            unsigned long long mm = ~0ull, nn = 0, ll = 0;
+#pragma unroll
+            for (int w = 0; w < NWAVE; ++w) {
+                mm = L.wst[w][0] < mm ? L.wst[w][0] : mm;
+                nn += L.wst[w][1], ll += L.wst[w][2];
             }
+            slot[0] = mm;
+            slot[1] = nn;
+            slot[2 + d] = ll;
         }
         if (A.trace && tid == 0) A.trace[64 + (size_t)d * 1024 + bid] = (unsigned long long)wall_clock64();
         if (A.trace && tid < 4) {  // phase cycles summed over the workgroup's waves -> trace[8d + 4 + k]
@@ -905,9 +928,9 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
             L.rm[e] = rmv;
             counted += rmv ? (long long)f + 1 : (long long)(L.eoff[e + 1] - L.eoff[e]);
         }
-        counted = block_sum_ll(counted, L);
         __syncthreads();
-        if (bid == 0) {
+        if (bid == 0) {  // the result record (the other workgroups go straight on to the next level)
+            counted = block_sum_ll(counted, L);
             // sepsets of the removed edges in edge order (unranked against the level's snapshot)
             int carry = 0;
             for (int e0 = 0; e0 < E; e0 += BS) {
