@@ -48,6 +48,7 @@ _SIGS = {
     "fbn_jt_kernel_options": [C.c_char_p, C.c_int64],
     "fbn_jt_kernel_build": [_vp],
     "fbn_jt_debug_force_fixup": [_vp, C.c_int],
+    "fbn_jt_set_exact": [_vp, C.c_int],
     "fbn_jt_plan_destroy": [_vp],
     "fbn_ci_dataset_upload": [_vp, C.c_int, _i64, _vp, C.c_int, _pp],
     "fbn_ci_dataset_from_device": [_vp, C.c_int, _i64, _vp, C.c_int, _pp],
@@ -308,6 +309,12 @@ class JunctionTree:
 
     def debug_force_fixup(self, enable):
         lib.fbn_jt_debug_force_fixup(self._h, int(enable))
+
+    def set_exact(self, exact):
+        """Streamed kernel arithmetic order: True = the reference's (bit-identical), False = fast
+        (one-pass Collect denominators, within a few ulp), None = auto (exact for ALARM-class plans,
+        fast for Munin-class ones)."""
+        lib.fbn_jt_set_exact(self._h, -1 if exact is None else int(bool(exact)))
 
     def build_kernel(self):
         """Compile the plan-specialized kernel into the on-disk cache (no GPU needed)."""

@@ -169,6 +169,10 @@ struct fbn_jt_plan {
     int64_t gen_we = 0, gen_lds = 0;
     DevBuf flags, ws_fix, gen_iv;
     bool force_fixup = false;
+    // arithmetic order of the streamed kernel: 1 = the reference's (bit-identical), 0 = fast (one-pass
+    // Collect denominators, results within a few ulp per operation), -1 = auto (exact for plans
+    // the specialized kernel takes -- ALARM class --, fast for the rest -- Munin class)
+    int exact = -1;
     DevBuf ops, aux, initv, dig;
     DevBuf lops, laux, linitv, ldig;
     DevBuf prof;       // diagnostic per-op-type cycle counters
@@ -653,6 +657,9 @@ int fbn_jt_plan_dump(const fbn_jt_plan *p, const char *plan_path, const char *in
     return FBN_OK;
 }
 
+constexpr int kJtVFast = 1 << 12;  // jt_virt.hip kVFast
+static bool JtFast(const fbn_jt_plan *p) { return p->exact == 0 || (p->exact < 0 && !p->gen_eligible); }
+
 int fbn_jt_set_waves_per_cu(fbn_jt_plan *p, int waves) {
     if (!p || waves < 0 || waves > 32) return SetError(FBN_ERR_ARG, "waves per CU must be 0..32");
     p->waves_per_cu = waves;
@@ -730,6 +737,12 @@ int fbn_jt_kernel_cache_path(const fbn_jt_plan *p, char *buf, int64_t cap) {
     int rc = fbn::GenerateJTKernel(p->host, src, &we, iv);
     if (rc) return rc;
     snprintf(buf, (size_t)cap, "%s", fbn::JitCachePath(src).c_str());
+    return FBN_OK;
+}
+
+int fbn_jt_set_exact(fbn_jt_plan *p, int exact) {
+    if (!p || exact < -1 || exact > 1) return SetError(FBN_ERR_ARG, "exact must be -1 (auto), 0 (fast) or 1 (exact)");
+    p->exact = exact;
     return FBN_OK;
 }
 
@@ -930,7 +943,9 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
                                           reinterpret_cast<int32_t *>(p->ws.as<char>() + ws_d), p->flags.as<int>(),
                                           ncases, v.store_rows, v.scratch_row, v.scratch_rows, nc, V, SD, grid,
                                           // diagnostic ablation only (tools/): skip pass types, wrong results
-                                          getenv("FBN_JT_VDEBUG") ? atoi(getenv("FBN_JT_VDEBUG")) : 0, s);
+                                          (getenv("FBN_JT_VDEBUG") ? atoi(getenv("FBN_JT_VDEBUG")) : 0) |
+                                              (JtFast(p) ? kJtVFast : 0),
+                                          s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt kernel launch: %s", hipGetErrorString(e));
         if (p->force_fixup) FBN_HIP(hipMemsetAsync(p->flags.p, 1, (size_t)nblk * 4, s));  // testing only
         // exact recomputation of the blocks whose denominators left the fast-division range

@@ -37,6 +37,7 @@ typedef __attribute__((address_space(1))) int gint;
 struct Den {
     double den, y;
 };
+constexpr int kVFast = 1 << 12;  // launch flag (dbg word): one-pass Collect denominators (vsum_all)
 __device__ __forceinline__ double mdiv(double x, const Den &d) {
     const double q = x * d.y;
     const double r = __builtin_fma(-d.den, q, x);
@@ -210,6 +211,40 @@ __device__ __forceinline__ double vsum(const Store &S, const Clq &C, const Dens 
     return acc;
 }
 
+// fast mode (kVFast): every Collect normalization sum of a clique in ONE pass.  c_L(e) = init(e)
+// M_1(e) ... M_L(e) / (D_0 ... D_{L-1}), so D_L = P_L / (D_0 ... D_{L-1}) with P_L = sum_e init(e)
+// M_1(e) ... M_L(e): one sweep accumulates P_0 .. P_K from prefix products (K message loads per
+// entry instead of 1 + 2 + ... + K over K + 1 sweeps).  Same values up to rounding (a few ulp per
+// operation: well inside north_star's 1e-6 on potentials); not bit-identical to the reference's
+// sequential Normalize, hence opt-in per plan (fbn_jt_set_exact).
+// STORE: the full product init(e) M_1(e) ... M_K(e) also goes to the scratch rows at byte offset scr
+// (SEPCOL then divides by D_0 ... D_K).
+template <int K, bool P32, bool STORE = false, int SP = 0>
+__device__ __forceinline__ void vsum_all(const Store &S, const Clq &C, double (&P)[JT_V_MAX_CHILDREN + 2],
+                                         int scr = 0) {
+    constexpr int U = Unroll<K>::U;
+#pragma unroll
+    for (int j = 0; j < JT_V_MAX_CHILDREN + 2; ++j) P[j] = 0.0;
+    const int T = C.T;
+    for (int n0 = 0; n0 < T; n0 += U) {
+        Pre<K> X[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) pre_load<K, P32>(S, C, n0 + u < T ? n0 + u : n0, X[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (n0 + u >= T) continue;
+            double w = X[u].w0;
+            P[0] += w;
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                w *= X[u].m[j];
+                P[j + 1] += w;
+            }
+            if (STORE) S.template stp<(SP & 255)>(scr + (n0 + u) * 512, w);
+        }
+    }
+}
+
 // binned pass over the stored table (scratch rows at byte offset scr), divided by Df
 template <int SP, class Seq, class Flush>
 __device__ __forceinline__ void vbins_scr(const Store &S, int scr, const Den &Df, int total, Seq seq, int per,
@@ -351,6 +386,7 @@ void jt_virt_kernel(
     long long ncases, long long store_rows, long long scratch_row, long long scratch_rows, int nc, int V, int SD,
     int dbg) {
     __shared__ int sbad[JT_V_WAVES];
+    const bool fast = (dbg & kVFast) != 0;
     __shared__ double macc[JT_V_WAVES][kFuseBins * 64];  // fused marginal bins, per wave
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -414,8 +450,32 @@ void jt_virt_kernel(
 #pragma unroll
             for (int j = 0; j < JT_V_MAX_CHILDREN + 2; ++j) D[j] = Den{1.0, 1.0};
             // the last normalization pass of a clique with children also stores the table for SEPCOL
+            // (exact mode; fast mode recomputes the SEPCOL entries with its one-pass denominators)
             const bool cmat = q.cmat && !(dbg & 32);
-            for (int L = 0; L <= q.k; ++L) {
+            double prod = 1.0;  // fast mode: D_0 ... D_k (the stored products' divisor)
+            if (fast) {
+                double P[JT_V_MAX_CHILDREN + 2];
+                if (cmat) {
+#define FBN_ALLCALL(Lc, Pc) vsum_all<Lc, Pc, true, SP>(S, C, P, scr)
+                    FBN_VDISPATCH(q.k, p32, FBN_ALLCALL);
+#undef FBN_ALLCALL
+                } else {
+#define FBN_ALLCALL(Lc, Pc) vsum_all<Lc, Pc>(S, C, P)
+                    FBN_VDISPATCH(q.k, p32, FBN_ALLCALL);
+#undef FBN_ALLCALL
+                }
+#pragma unroll
+                for (int L = 0; L < JT_V_MAX_CHILDREN + 2; ++L) {
+                    if (L > q.k) continue;
+                    const double s = P[L] / prod;
+                    // a product chain that leaves the normal range: the block goes to the exact pass
+                    bad |= !den_ok(s) || !(P[L] >= 0x1p-960 && P[L] <= 0x1p+960);
+                    S.st_row(q.den_row + L, s);
+                    D[L] = Den{s, 1.0 / s};
+                    prod *= s;
+                }
+            }
+            for (int L = 0; L <= (fast ? -1 : q.k); ++L) {
                 double s = 0.0;
                 if (cmat && L == q.k) {
 #define FBN_SUMCALL(Lc, P) s = vsum<Lc, P, true, SP>(S, C, D, scr)
@@ -438,7 +498,8 @@ void jt_virt_kernel(
                 const int Ts = q.up_Ts, per = q.T / Ts, dst = q.up_col_row;
                 auto fl = [&](int j, double acc) { S.st_row(dst + j, acc); };
                 if (cmat) {
-                    vbins_scr<SP>(S, scr, pick(D, q.k), q.T, SeqCol{0, 0, 0, Ts, per}, per, fl);
+                    const Den Dc = fast ? Den{prod, 1.0 / prod} : pick(D, q.k);
+                    vbins_scr<SP>(S, scr, Dc, q.T, SeqCol{0, 0, 0, Ts, per}, per, fl);
                 } else {
 #define FBN_COLCALL(Lc, P) vbins<Lc, P>(S, C, D, SeqCol{0, 0, 0, Ts, per}, per, fl)
                     FBN_VDISPATCH(q.k, p32, FBN_COLCALL);

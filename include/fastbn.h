@@ -147,6 +147,14 @@ int fbn_jt_set_waves_per_cu(fbn_jt_plan *p, int waves);
  *     from initial potentials + received messages, only messages stored; exact-path fixup as 3.
  *     Selecting 4 fails for plans it cannot take (a clique with more than 6 children, ...). */
 int fbn_jt_set_variant(fbn_jt_plan *p, int variant);
+/* Arithmetic order of the streamed kernel (variant 4): 1 = exact (the reference's sequential
+ * Normalize after every multiply: bit-identical marginals), 0 = fast (all Collect normalization sums
+ * of a clique in one pass from prefix products, D_L = P_L / (D_0 ... D_{L-1}): the same values up to a
+ * few ulp per operation, inside north_star's 1e-6 relative on potentials), -1 = auto (default:
+ * exact for plans the specialized kernel takes -- ALARM class --, fast for the others -- the
+ * Munin class, where the bit-exact order costs most of the achievable rate).  Replaces no
+ * reference interface (the reference has one arithmetic order, src/JunctionTree.cpp:829-941). */
+int fbn_jt_set_exact(fbn_jt_plan *p, int exact);
 /* Diagnostics (LDS variant): enable per-op-type s_memtime accounting for subsequent runs and/or
  * read the totals of the last run (cycles[10], op types JT_L_INIT..JT_L_EVZERO, summed over waves). */
 int fbn_jt_debug_op_cycles(fbn_jt_plan *p, int enable, unsigned long long *cycles);

@@ -128,6 +128,7 @@ def test_synthetic_network(tmp_path):
     net = synth.read_xmlbif(p)
     ev = synth.evidence_cases(net, 300, 40, seed=5)
     jt = F.JunctionTree(F.Network(p), device=0)
+    jt.set_exact(True)  # the streamed kernel in the reference's arithmetic order
     olab, omarg = O.OracleJT(p).infer(ev)
     for variant in (0, 1, 2, 4):
         jt.set_variant(variant)
@@ -166,11 +167,18 @@ def test_streamed_variant_munin_like(tmp_path):
     ev[0, :] = -1  # no evidence at all
     olab, omarg = O.OracleJT(p).infer(ev)
     jt = F.JunctionTree(F.Network(p), device=0)
+    jt.set_exact(True)
     for variant in (4, 1):
         jt.set_variant(variant)
         lab, marg = jt.infer(ev)
         np.testing.assert_array_equal(lab, olab)
         np.testing.assert_array_equal(marg, omarg)
+    # the fast arithmetic order (the Munin-class default): within 1e-12 relative, same labels
+    jt.set_exact(False)
+    jt.set_variant(4)
+    lab, marg = jt.infer(ev)
+    np.testing.assert_array_equal(lab, olab)
+    np.testing.assert_allclose(marg, omarg, rtol=1e-12, atol=1e-300)
 
 
 def test_device_resident_path(jt, ojt):
@@ -245,11 +253,19 @@ def test_munin_like_full_network_vs_reference(munin_fixture):
     jt = F.JunctionTree(F.Network(munin_fixture["xml"]), device=0)
     o = O.OracleJT(munin_fixture["xml"])
     ev, _ = O.load_libsvm(munin_fixture["libsvm"], o.n)
+    rlab, rmarg, _, _ = read_ref_marg(munin_fixture["marg"], o.dims)
+    olab, omarg = o.infer(ev)
+    # default (auto = fast order for this plan): labels equal the reference's, marginals within 1e-9
+    # relative of the reference's own (north_star: 1e-6)
     lab, marg = jt.infer(ev)
     assert jt.refresh_info()["variant"] == 4
-    rlab, rmarg, _, _ = read_ref_marg(munin_fixture["marg"], o.dims)
+    np.testing.assert_array_equal(lab, rlab)
+    np.testing.assert_allclose(marg, rmarg, rtol=1e-9, atol=1e-300)
+    np.testing.assert_allclose(marg, omarg, rtol=1e-12, atol=1e-300)
+    # exact order: bit-identical to the restatement on our tree, 1e-12 of the reference's
+    jt.set_exact(True)
+    lab, marg = jt.infer(ev)
     np.testing.assert_array_equal(lab, rlab)
     np.testing.assert_allclose(marg, rmarg, rtol=MUNIN_REF_RTOL, atol=1e-300)
-    olab, omarg = o.infer(ev)
     np.testing.assert_array_equal(lab, olab)
     np.testing.assert_array_equal(marg, omarg)
