@@ -211,6 +211,45 @@ __device__ __forceinline__ double vsum(const Store &S, const Clq &C, const Dens 
     return acc;
 }
 
+constexpr int kFuseVars = 4, kFuseBins = 16;
+// fast mode: the Distribute normalization pass (vsum) also accumulates the fused marginal bins of
+// up to kFuseVars variables from the entries before their division by D_L (vmarg_fused's bins, each
+// in increasing entry order): the caller divides the bins by D_L afterwards (one rounding apart
+// from the exact order's per-entry division), and the separate marginal sweep is gone.
+template <int L, bool P32, bool STORE, int SP>
+__device__ __forceinline__ double vsum_m(const Store &S, const Clq &C, const Dens &D, int scr, int nf,
+                                         const int (&cum)[kFuseVars], const int (&dim)[kFuseVars],
+                                         const int (&base)[kFuseVars], double *__restrict__ macc, int lane) {
+    constexpr int U = Unroll<L>::U;
+    double acc = 0.0;
+    const int T = C.T;
+    int lo[kFuseVars], dd[kFuseVars];
+#pragma unroll
+    for (int i = 0; i < kFuseVars; ++i) lo[i] = 0, dd[i] = 0;
+    for (int n0 = 0; n0 < T; n0 += U) {
+        Pre<L> X[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) pre_load<L, P32>(S, C, n0 + u < T ? n0 + u : n0, X[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (n0 + u >= T) continue;
+            const double v = pre_eval<L>(X[u], D);
+            acc += v;
+            if (STORE) S.template stp<(SP & 255)>(scr + (n0 + u) * 512, v);
+#pragma unroll
+            for (int i = 0; i < kFuseVars; ++i) {
+                if (i >= nf) continue;
+                macc[(base[i] + dd[i]) * 64 + lane] += v;
+                if (++lo[i] == cum[i]) {
+                    lo[i] = 0;
+                    if (++dd[i] == dim[i]) dd[i] = 0;
+                }
+            }
+        }
+    }
+    return acc;
+}
+
 // fast mode (kVFast): every Collect normalization sum of a clique in ONE pass.  c_L(e) = init(e)
 // M_1(e) ... M_L(e) / (D_0 ... D_{L-1}), so D_L = P_L / (D_0 ... D_{L-1}) with P_L = sum_e init(e)
 // M_1(e) ... M_L(e): one sweep accumulates P_0 .. P_K from prefix products (K message loads per
@@ -308,7 +347,6 @@ __device__ __forceinline__ void vbins(const Store &S, const Clq &C, const Dens &
 // (e / cum_i) % dim_i) of an LDS accumulator [bin][64 lanes].  Every bin receives its entries in
 // increasing e -- the order of the per-variable SeqMarg pass it replaces -- starting from 0.0, so
 // each bin sum is bit-identical; one pass instead of one per variable.
-constexpr int kFuseVars = 4, kFuseBins = 16;
 template <int L, bool P32, int SP, bool MAT>
 __device__ __forceinline__ void vmarg_fused(const Store &S, const Clq &C, const Dens &D, int scr, const Den &Df,
                                             int T, int nf, const int (&cum)[kFuseVars],
@@ -537,10 +575,52 @@ void jt_virt_kernel(
                     D[j] = Den{s, 1.0 / s};
                 }
             }
+            // marginals of the variables whose chosen clique (for this case) is this one: up to
+            // kFuseVars of them (kFuseBins values in total) in one fused sweep, the rest one pass each
+            const bool fuse = !(dbg & 1024);
+            int fv[kFuseVars], fcum[kFuseVars], fdim[kFuseVars], fbase[kFuseVars];
+#pragma unroll
+            for (int i = 0; i < kFuseVars; ++i) fv[i] = 0, fcum[i] = 1, fdim[i] = 1, fbase[i] = 0;
+            int nf = 0, nb = 0;
+            uint32_t fmask = 0;  // marginal records fused
+            auto pick_fused = [&]() {
+                for (int mi = 0; mi < ((dbg & 4) ? 0 : q.nmarg); ++mi) {
+                    const int32_t *__restrict__ rec = aux + q.marg_off + 4 * mi;
+                    const int dim = rec[1], var = rec[2], cum = rec[3];
+                    const int sb = IROW(nc + var);
+                    const bool mine = ((sb & 0xFFFFFF) == q.id) && ev[var] < 0;
+                    if (__ballot(mine) == 0ull) continue;
+                    if (fuse && nf < kFuseVars && nb + dim <= kFuseBins && mi < 32) {
+#pragma unroll
+                        for (int i = 0; i < kFuseVars; ++i)
+                            if (i == nf) fv[i] = mi, fcum[i] = cum, fdim[i] = dim, fbase[i] = nb;
+                        ++nf, nb += dim;
+                        fmask |= 1u << mi;
+                    }
+                }
+            };
+            // fast mode: the marginal bins ride on the Distribute normalization pass (vsum_m)
+            const bool mfused = fast && !q.root && !(dbg & 8);
+            double *macc_w = macc[wv];
+            if (mfused) {
+                pick_fused();
+                for (int b = 0; b < nb; ++b) macc_w[b * 64 + lane] = 0.0;
+            }
             int Lf = q.k;
             if (!q.root && !(dbg & 8)) {
                 double s = 0.0;
-                if (q.mat && !(dbg & 64) && !((dbg & 512) && q.k < 2)) {
+                if (mfused && nf > 0) {
+                    const bool st = q.mat && !(dbg & 64) && !((dbg & 512) && q.k < 2);
+                    if (st) {
+#define FBN_SUMCALL(Lc, P) s = vsum_m<Lc, P, true, SP>(S, C, D, scr, nf, fcum, fdim, fbase, macc_w, lane)
+                        FBN_VDISPATCH(q.k + 1, p32, FBN_SUMCALL);
+#undef FBN_SUMCALL
+                    } else {
+#define FBN_SUMCALL(Lc, P) s = vsum_m<Lc, P, false, SP>(S, C, D, scr, nf, fcum, fdim, fbase, macc_w, lane)
+                        FBN_VDISPATCH(q.k + 1, p32, FBN_SUMCALL);
+#undef FBN_SUMCALL
+                    }
+                } else if (q.mat && !(dbg & 64) && !((dbg & 512) && q.k < 2)) {
 #define FBN_SUMCALL(Lc, P) s = vsum<Lc, P, true, SP>(S, C, D, scr)
                     FBN_VDISPATCH(q.k + 1, p32, FBN_SUMCALL);
 #undef FBN_SUMCALL
@@ -592,14 +672,7 @@ void jt_virt_kernel(
                         if (j0 + u < Ts) S.st_row(dis + j0 + u, (o[u] == 0.0) ? 0.0 : a[u] / o[u]);
                 }
             }
-            // marginals of the variables whose chosen clique (for this case) is this one: up to
-            // kFuseVars of them (kFuseBins values in total) in one fused sweep, the rest one pass each
             const bool mat = q.mat && !(dbg & 64) && !((dbg & 512) && q.k < 2);
-            const bool fuse = !(dbg & 1024);
-            int fv[kFuseVars], fcum[kFuseVars], fdim[kFuseVars], fbase[kFuseVars];
-#pragma unroll
-            for (int i = 0; i < kFuseVars; ++i) fv[i] = 0, fcum[i] = 1, fdim[i] = 1, fbase[i] = 0;
-            int nf = 0, nb = 0;
             auto finish = [&](int mi, auto bin_of) {  // outputs of marginal record mi from its bins
                 const int32_t *__restrict__ rec = aux + q.marg_off + 4 * mi;
                 const int off = rec[0], dim = rec[1], var = rec[2];
@@ -633,7 +706,9 @@ void jt_virt_kernel(
                 const int sb = IROW(nc + var);
                 const bool mine = ((sb & 0xFFFFFF) == q.id) && ev[var] < 0;
                 if (__ballot(mine) == 0ull) continue;
-                if (fuse && nf < kFuseVars && nb + dim <= kFuseBins) {  // into the fused sweep
+                if (mfused ? ((fmask >> mi) & 1u) != 0 : (fuse && nf < kFuseVars && nb + dim <= kFuseBins)) {
+                    if (mfused) continue;  // accumulated by the normalization pass
+                    // into the fused sweep
 #pragma unroll
                     for (int i = 0; i < kFuseVars; ++i)
                         if (i == nf) fv[i] = mi, fcum[i] = cum, fdim[i] = dim, fbase[i] = nb;
@@ -669,7 +744,12 @@ void jt_virt_kernel(
                     for (int d = 0; d < dim; ++d) o[d] = o[d] / tot;
                 }
             }
-            if (nf > 0) {
+            if (nf > 0 && mfused) {  // bins from the normalization pass, divided by its sum D_Lf
+                const Den Df = pick(D, Lf);
+#pragma unroll
+                for (int i = 0; i < kFuseVars; ++i)
+                    if (i < nf) finish(fv[i], [&](int d) { return mdiv(macc_w[(fbase[i] + d) * 64 + lane], Df); });
+            } else if (nf > 0) {
                 double *acc = macc[wv];
                 for (int b = 0; b < nb; ++b) acc[b * 64 + lane] = 0.0;
                 const Den Df = pick(D, Lf);
