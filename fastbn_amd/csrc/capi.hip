@@ -265,9 +265,12 @@ struct fbn_ci_ctx {
     unsigned long long *h_margin = nullptr;  // pinned: reset value, read-back (CiResetMargin)
     hipEvent_t l1ev[2] = {nullptr, nullptr};
     // device-resident skeleton search of small graphs (pc_small.hip): scratch (barrier counters +
-    // first-independent words, zeroed per run; statistics slots; level-0 pair tables) and the
+    // first-independent words, zeroed once; statistics slots; level-0 pair tables) and the
     // pinned result record the kernel writes
     DevBuf small_scr;
+    void *small_zeroed = nullptr;       // scratch whose barrier / first[] words are zeroed (and its size)
+    size_t small_zeroed_bytes = 0;
+    unsigned small_epoch = 0, small_phase = 0;  // launches so far, grid-barrier phases so far
     fbn::PcSmallOut *h_small = nullptr;
     // fbn_ci_debug_counts: the histogram kernel writes every test's table (stride in ints), 0 off
     int64_t counts_stride = 0;
@@ -2345,13 +2348,21 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
     const size_t dout_off = (pt_off + (size_t)kSmallMaxEdges * 16 * 4 + 255) & ~(size_t)255;
     const size_t bytes = dout_off + sizeof(PcSmallOut);
     if ((rc = c->small_scr.ensure(bytes))) return rc;
-    if (!c->h_small) {
-        hipError_t e = hipHostMalloc((void **)&c->h_small, sizeof(PcSmallOut), hipHostMallocDefault);
+    if (!c->h_small) {  // coherent: the host polls its completion word while the kernel runs
+        hipError_t e = hipHostMalloc((void **)&c->h_small, sizeof(PcSmallOut), hipHostMallocCoherent);
         if (e != hipSuccess) return SetError(FBN_ERR_NOMEM, "hipHostMalloc: %s", hipGetErrorString(e));
+        c->h_small->done = 0;
     }
     PcSmallOut *out = c->h_small;
     out->status = -1;
     char *scr = c->small_scr.as<char>();
+    if (c->small_zeroed != c->small_scr.p || c->small_zeroed_bytes != c->small_scr.bytes) {
+        FBN_HIP(hipMemsetAsync(scr, 0, kSmallZeroBytes, s));  // barrier counters and first[] words: once
+        c->small_zeroed = c->small_scr.p;
+        c->small_zeroed_bytes = c->small_scr.bytes;
+        c->small_phase = 0;
+    }
+    if (++c->small_epoch == 0) ++c->small_epoch;  // (wrapped: skip 0 -- the zeroed words' epoch)
     PcSmallArgs a{};
     a.bits = c->bits.as<uint32_t>();
     a.row0 = c->brow.as<int32_t>();
@@ -2367,7 +2378,9 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
     a.nband = nband;
     a.depth = depth;
     a.bar = reinterpret_cast<unsigned *>(scr);
-    a.first = reinterpret_cast<unsigned *>(scr + (size_t)kSmallBarWords * 4);
+    a.first = reinterpret_cast<unsigned long long *>(scr + (size_t)kSmallBarWords * 4);
+    a.epoch = c->small_epoch;
+    a.phase_base = c->small_phase;
     a.acc = reinterpret_cast<unsigned long long *>(scr + acc_off);
     a.pairtab = reinterpret_cast<int32_t *>(scr + pt_off);
     a.ctx_stats = c->stats.as<unsigned long long>();
@@ -2385,11 +2398,23 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
         trace_host.assign(tb / 8, 0);
     }
     CiSlot &S = c->slot[0];
-    FBN_HIP(hipMemsetAsync(scr, 0, kSmallZeroBytes, s));
     if (c->timing) FBN_HIP(hipEventRecord(S.ev0, s));
     FBN_HIP(fbn_pc_small_launch(&a, grid, s));
     if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
-    FBN_HIP(hipStreamSynchronize(s));
+    // wait for the kernel's completion word (written after the record) instead of a stream sync;
+    // a stream sync only for the events / trace, or when the word does not come (fault, hang)
+    {
+        const auto t0 = std::chrono::steady_clock::now();
+        bool got = false;
+        for (unsigned spin = 0;; ++spin) {
+            if (__atomic_load_n(&out->done, __ATOMIC_ACQUIRE) == c->small_epoch) {
+                got = true;
+                break;
+            }
+            if ((spin & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) break;
+        }
+        if (!got || c->timing || trace) FBN_HIP(hipStreamSynchronize(s));
+    }
     if (trace) {
         FBN_HIP(hipMemcpy(trace_host.data(), trace_dev.p, trace_host.size() * 8, hipMemcpyDeviceToHost));
         h_trace = trace_host.data();
@@ -2414,9 +2439,12 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
                     nt, h_trace[8 * d + 4] / nt, h_trace[8 * d + 5] / nt, h_trace[8 * d + 6] / nt);
         }
     }
-    if (out->status != 0)
+    if (out->status != 0) {
+        c->small_zeroed = nullptr;  // barrier counters left mid-phase: zero again next launch
         return SetError(FBN_ERR_HIP, "pc small kernel: %s (status %d)",
                         out->status == 1 ? "grid barrier timed out" : "no result", out->status);
+    }
+    c->small_phase += (unsigned)out->levels;  // one grid barrier per completed level
     if (c->timing) {
         float ms = 0.f;
         FBN_HIP(hipEventElapsedTime(&ms, S.ev0, S.ev1));

@@ -22,7 +22,9 @@ constexpr int kSmallMaxLevels = kSmallMaxD + 1;
 constexpr int64_t kSmallMaxTests = 1 << 22;  // a level with more candidate sets hands off to the host
 
 constexpr int kSmallBarWords = 256;  // 8 group counters 64 B apart + the top counter (1 KB)
-constexpr size_t kSmallZeroBytes = (size_t)kSmallBarWords * 4 + (size_t)kSmallMaxLevels * kSmallMaxEdges * 4;
+// barrier words + epoch-tagged first-independent words: zeroed once when the scratch is allocated
+// (never per launch: the barrier counts phases across launches, first[] values carry the launch epoch)
+constexpr size_t kSmallZeroBytes = (size_t)kSmallBarWords * 4 + (size_t)kSmallMaxLevels * kSmallMaxEdges * 8;
 
 // result record (int32 words; 64-bit values little-endian in two words)
 struct PcSmallOut {
@@ -37,6 +39,10 @@ struct PcSmallOut {
     uint64_t adj[kSmallMaxLevels][kSmallMaxVars];  // adjacency after each completed level
     int32_t sep_off[kSmallMaxLevels + 1];  // removed edges' sepsets of level d: pool[sep_off[d] ..)
     int32_t pool[kSmallMaxEdges * kSmallMaxD];     // level d: d ints per removed edge, edge order
+    // written last (after the record, system-scope release): the launch epoch -- the host polls it
+    // instead of synchronizing the stream; never part of the record copy
+    uint32_t done;
+    uint32_t pad2;
 };
 
 struct PcSmallArgs {
@@ -53,10 +59,12 @@ struct PcSmallArgs {
     const double *band;      // decision band [lo, hi] per df 1..nband, then delta (or nullptr)
     int nband;
     int depth;               // levels 0 .. depth - 1 at most
-    // scratch: bar and first zeroed by the host before every launch (one memset, kSmallZeroBytes
-    // from the start of the scratch allocation)
-    unsigned *bar;           // grid barrier arrivals (kSmallBarWords)
-    unsigned *first;         // [kSmallMaxLevels][kSmallMaxEdges] ~(first independent candidate), 0 none
+    // scratch: bar and first zeroed once at allocation (kSmallZeroBytes from its start)
+    unsigned *bar;           // grid barrier arrivals (kSmallBarWords), counting phases across launches
+    unsigned long long *first;  // [kSmallMaxLevels][kSmallMaxEdges] (epoch << 32) | ~(first independent
+                                // candidate); a word of another epoch = none
+    unsigned epoch;          // this launch's number (1, 2, ...; never 0)
+    unsigned phase_base;     // grid barrier phases completed by the earlier launches on this scratch
     unsigned long long *acc; // [0] margin bits (min), [1] near, [2 + d] launched at level d
     int32_t *pairtab;        // [kSmallMaxEdges][16] level-0 tables (derived level-1 counting)
     unsigned long long *ctx_stats;  // the ctx's margin log, set to this run's at the end

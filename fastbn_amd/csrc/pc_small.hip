@@ -201,6 +201,14 @@ __device__ bool grid_barrier(const Barrier &B, unsigned phase, Lds &L) {
     return L.flag != 0;
 }
 
+// this launch's first independent candidate of edge e at level d (~0u: none): first[] words of
+// earlier launches carry another epoch
+__device__ __forceinline__ unsigned first_of(const PcSmallArgs &A, int d, int e) {
+    const unsigned long long v =
+        __hip_atomic_load(A.first + (size_t)d * kSmallMaxEdges + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (unsigned)(v >> 32) == A.epoch ? ~(unsigned)v : ~0u;
+}
+
 // ---- block-wide helpers
 __device__ __forceinline__ long long block_sum_ll(long long v, Lds &L) {
     v = wsum_i64(v);
@@ -743,6 +751,10 @@ __device__ void finalize(const PcSmallArgs &A, Lds &L, int nb, int levels, int h
     const int head = (int)(offsetof(PcSmallOut, pool) / 4);
     const int used = head + (levels > 0 ? o->sep_off[levels] : 0);
     for (int i = tid; i < used; i += BS) dst[i] = src[i];
+    // every thread's part of the copy reaches the host before the completion word
+    __threadfence_system();
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(&A.out->done, A.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) {
@@ -894,7 +906,8 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
         __syncthreads();
         for (int e = tid; e < E; e += BS)
             if (L.bfirst[e] != ~0u)
-                __hip_atomic_fetch_max(A.first + (size_t)d * kSmallMaxEdges + e, ~L.bfirst[e], __ATOMIC_RELAXED,
+                __hip_atomic_fetch_max(A.first + (size_t)d * kSmallMaxEdges + e,
+                                       ((unsigned long long)A.epoch << 32) | (unsigned)~L.bfirst[e], __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
         // this workgroup's statistics into its slot (plain stores, published by the barrier)
         if (tid == 0) {
@@ -914,16 +927,19 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
             for (int w = 0; w < NWAVE; ++w) sum += L.ph[w][tid];
             atomicAdd(A.trace + 8 * d + 4 + tid, sum);
         }
-        if (!grid_barrier(B, ++phase, L)) {
-            if (tid == 0) A.out->status = 1;
+        if (!grid_barrier(B, A.phase_base + ++phase, L)) {
+            if (tid == 0) {  // the host sees the failure (and stops waiting) without a stream sync
+                A.out->status = 1;
+                __threadfence_system();
+                __hip_atomic_store(&A.out->done, A.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
             return;
         }
         if (A.trace && bid == 0 && tid == 0) A.trace[8 * d + 2] = (unsigned long long)wall_clock64();
         // ---- apply: removed = some independent set found; counted = first + 1, else all sets
         long long counted = 0;
         for (int e = tid; e < E; e += BS) {
-            const unsigned f = ~__hip_atomic_load(A.first + (size_t)d * kSmallMaxEdges + e, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned f = first_of(A, d, e);
             const bool rmv = f != ~0u;
             L.rm[e] = rmv;
             counted += rmv ? (long long)f + 1 : (long long)(L.eoff[e + 1] - L.eoff[e]);
@@ -939,8 +955,7 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
                 int total = 0;
                 const int off = block_excl_scan(r, L, &total);
                 if (r && d > 0) {
-                    const unsigned f = ~__hip_atomic_load(A.first + (size_t)d * kSmallMaxEdges + e, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT);
+                    const unsigned f = first_of(A, d, e);
                     int zz[kSmallMaxD];
                     unrank(L, L.ex[e], L.ey[e], d, (int)f, zz);
                     for (int j = 0; j < d; ++j) A.dout->pool[sep_cursor + (carry + off) * d + j] = zz[j];
