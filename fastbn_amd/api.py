@@ -330,7 +330,8 @@ class JunctionTree:
     def set_variant(self, v):
         """-1 auto, 0 = clique-in-LDS interpreter, 1 = global-workspace interpreter,
         2 = LDS interpreter with IEEE division, 3 = plan-specialized kernel,
-        4 = streamed (virtual-table) kernel for large trees."""
+        4 = streamed (virtual-table) kernel for large trees, 5 = per-case evidence-reduced
+        kernel for large trees (fast arithmetic order)."""
         lib.fbn_jt_set_variant(self._h, v)
 
     def infer(self, evidence, marginals=True):

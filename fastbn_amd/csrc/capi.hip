@@ -82,6 +82,12 @@ extern "C" hipError_t fbn_ci_bits_pairs_tiled(const uint32_t *bits, const int32_
                                               long long W, const int32_t *tasks, long long ntasks, int nvars,
                                               long long t0, long long t1, int32_t *counts, int32_t *pairtab,
                                               int num_cu, hipStream_t s);
+extern "C" hipError_t fbn_jt_case_launch(const JtCClique *cls, const int32_t *vrec, const int32_t *aux,
+                                         const double *initv, const int32_t *post, const int32_t *pre,
+                                         const int32_t *vsel, const int8_t *evid, double *marg, int32_t *labels,
+                                         double *ws, int *flags, long long ncases, long long msg_doubles,
+                                         long long gbin_doubles, int nc, int V, int SD, int lds_bins, int grid,
+                                         int dbg, unsigned long long *prof, hipStream_t stream);
 extern "C" hipError_t fbn_jt_virt_launch(const JtVClique *cls, const int32_t *aux, const double *initv,
                                          const uint64_t *dig, const int32_t *order, const int32_t *sched,
                                          const int32_t *vsel, const int8_t *evid, double *marg, int32_t *labels,
@@ -160,6 +166,9 @@ struct fbn_jt_plan {
     fbn::JTProgramV vprog;    // variant 4: streamed (virtual) tables, large trees
     bool v_ok = false;
     DevBuf vcl, vaux, viv, vdig, vorder, vsched, vsel;
+    fbn::JTProgramC cprog;    // variant 5: per-case, evidence-reduced (fast order), large trees
+    bool c_ok = false;
+    DevBuf ccl, cvrec, caux, civ, cpost, cpre, cvsel;
     int device = 0, num_cu = 0, waves_per_cu = 0, variant = -1, last_variant = -1;
     // plan-specialized kernel (variant 3)
     bool gen_eligible = false;
@@ -548,6 +557,16 @@ static int JtUpload(fbn_jt_plan *p) {
         if ((rc = up(p->vsched, v.sched.data(), v.sched.size() * 4))) return rc;
         if ((rc = up(p->vsel, v.vsel.data(), v.vsel.size() * 4))) return rc;
     }
+    if (p->c_ok) {
+        const auto &c = p->cprog;
+        if ((rc = up(p->ccl, c.cl.data(), c.cl.size() * sizeof(JtCClique)))) return rc;
+        if ((rc = up(p->cvrec, c.vrec.data(), c.vrec.size() * 4))) return rc;
+        if ((rc = up(p->caux, c.aux.data(), c.aux.size() * 4))) return rc;
+        if ((rc = up(p->civ, c.initv.data(), c.initv.size() * 8))) return rc;
+        if ((rc = up(p->cpost, c.post.data(), c.post.size() * 4))) return rc;
+        if ((rc = up(p->cpre, c.pre.data(), c.pre.size() * 4))) return rc;
+        if ((rc = up(p->cvsel, c.vsel.data(), c.vsel.size() * 4))) return rc;
+    }
     return FBN_OK;
 }
 
@@ -565,6 +584,11 @@ int fbn_jt_plan_create(const fbn_network *net, int device, fbn_jt_plan **out) {
     if (rc && rc != FBN_ERR_LIMIT) return rc;
     p->v_ok = rc == FBN_OK;
     if (!p->v_ok) p->vprog = fbn::JTProgramV();
+    rc = fbn::CompileJTProgramC(p->host, p->cprog);
+    if (rc && rc != FBN_ERR_LIMIT) return rc;
+    p->c_ok = rc == FBN_OK;
+    for (int d : p->host.dom) p->c_ok = p->c_ok && d <= 64;
+    if (!p->c_ok) p->cprog = fbn::JTProgramC();
     p->gen_eligible = fbn::JTCodegenEligible(p->host, nullptr);
     p->device = device;
     if (device >= 0) {  // device < 0: host-only plan (info / dump), runs fail with FBN_ERR_NODEV
@@ -670,11 +694,12 @@ int fbn_jt_set_waves_per_cu(fbn_jt_plan *p, int waves) {
 }
 
 int fbn_jt_set_variant(fbn_jt_plan *p, int variant) {
-    if (!p || variant < -1 || variant > 4)
+    if (!p || variant < -1 || variant > 5)
         return SetError(FBN_ERR_ARG, "variant must be -1 (auto), 0 (LDS), 1 (global), 2 (LDS, IEEE division), "
-                                     "3 (specialized) or 4 (streamed)");
+                                     "3 (specialized), 4 (streamed) or 5 (per-case)");
     if (variant == 3 && !p->gen_eligible) return SetError(FBN_ERR_ARG, "plan not eligible for the specialized kernel");
     if (variant == 4 && !p->v_ok) return SetError(FBN_ERR_ARG, "plan not eligible for the streamed kernel");
+    if (variant == 5 && !p->c_ok) return SetError(FBN_ERR_ARG, "plan not eligible for the per-case kernel");
     p->variant = variant;
     return FBN_OK;
 }
@@ -953,6 +978,42 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
         if (p->force_fixup) FBN_HIP(hipMemsetAsync(p->flags.p, 1, (size_t)nblk * 4, s));  // testing only
         // exact recomputation of the blocks whose denominators left the fast-division range
         if (!getenv("FBN_JT_VDEBUG") &&
+            (rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s)))
+            return rc;
+    } else if (variant == 5) {
+        // one wave per case (persistent, striding over the cases); per wave: the case's messages
+        // plus a global bin area for bin sets beyond the LDS budget
+        const auto &c = p->cprog;
+        const int lds_env = getenv("FBN_JT_CLDS") ? atoi(getenv("FBN_JT_CLDS")) : 1024;  // (tuning / testing knob)
+        const int lds_bins = std::max(64, std::min(lds_env, 16384));
+        const int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 8;
+        int grid = (int)std::min<int64_t>(ncases, (int64_t)p->num_cu * wpc);
+        const size_t per_wave = (size_t)(c.msg_doubles + c.max_bins) * 8;
+        const size_t lds = (size_t)lds_bins * 8 + (size_t)((V + 7) & ~7) + (size_t)((c.num_cliques + 7) & ~7) + (size_t)V * 2;
+        if (lds > kLdsBytes) return SetError(FBN_ERR_LIMIT, "per-case kernel: %zu B of LDS per wave", lds);
+        if ((rc = p->ws.ensure((size_t)grid * per_wave))) return rc;
+        if ((rc = p->flags.ensure((size_t)nblk * 4))) return rc;
+        FBN_HIP(hipMemsetAsync(p->flags.p, 0, (size_t)nblk * 4, s));
+        // diagnostics: bits 1/2/4 skip work (wrong results), 8 = per-phase cycle totals
+        // (fbn_jt_debug_op_cycles reads them)
+        const int cdbg = getenv("FBN_JT_CDEBUG") ? atoi(getenv("FBN_JT_CDEBUG")) : 0;
+        if (cdbg & 8) {
+            if ((rc = p->prof.ensure(16 * 8))) return rc;
+            FBN_HIP(hipMemsetAsync(p->prof.p, 0, 16 * 8, s));
+            p->last_grid = 1;
+        }
+        FBN_HIP(hipEventRecord(p->ev0, s));
+        hipError_t e = fbn_jt_case_launch(p->ccl.as<JtCClique>(), p->cvrec.as<int32_t>(), p->caux.as<int32_t>(),
+                                          p->civ.as<double>(), p->cpost.as<int32_t>(), p->cpre.as<int32_t>(),
+                                          p->cvsel.as<int32_t>(), d_evidence, marg, labels, p->ws.as<double>(),
+                                          p->flags.as<int>(), ncases, c.msg_doubles, c.max_bins, nc, V, SD, lds_bins,
+                                          grid,
+                                          // diagnostic ablation only (tools/): skip work, wrong results
+                                          cdbg, cdbg & 8 ? p->prof.as<unsigned long long>() : nullptr, s);
+        if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt kernel launch: %s", hipGetErrorString(e));
+        if (p->force_fixup) FBN_HIP(hipMemsetAsync(p->flags.p, 1, (size_t)nblk * 4, s));  // testing only
+        // exact recomputation of the blocks holding a case whose sums left the checked range
+        if (!(cdbg & 7) &&
             (rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s)))
             return rc;
     } else if (variant == 3) {

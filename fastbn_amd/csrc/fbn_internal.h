@@ -118,6 +118,22 @@ struct JTProgramV {
 // more than 8 * JT_MAX_DIG_WORDS variables, or tables beyond int32 indexing)
 int CompileJTProgramV(const JTPlanHost &plan, JTProgramV &prog);
 
+// per-case variant (jt_case.hip), see jt_program.h
+struct JTProgramC {
+    std::vector<JtCClique> cl;
+    std::vector<int32_t> vrec;   // JT_C_VREC int32 per clique variable
+    std::vector<int32_t> aux;    // child records {Ts, col, dis}, then candidate clique lists
+    std::vector<double> initv;
+    std::vector<int32_t> post, pre;  // Collect (DFS post-order, root excluded) / Distribute (pre-order)
+    std::vector<int32_t> vsel;       // per variable {cand_off, ncand, out_off, dim}
+    int64_t msg_doubles = 0;         // per-wave message slice: Collect messages, then Distribute ones
+    int32_t max_bins = 0;            // largest bin set of any pass (fp64 values)
+    int num_cliques = 0, sum_dom = 0;
+};
+// FBN_ERR_LIMIT when the plan does not fit (> JT_C_MAX_CHILDREN children, > 64 variables in a
+// clique, > 65535 cliques, tables beyond int32 indexing)
+int CompileJTProgramC(const JTPlanHost &plan, JTProgramC &prog);
+
 // plan-specialized kernel source (jt_codegen.cpp): eligibility and generation.  The generated
 // kernel's per-wave workspace holds wave_entries rows of 64 fp64 lanes; initv is its constant input.
 bool JTCodegenEligible(const JTPlanHost &plan, int64_t *entry_ops);

@@ -89,4 +89,28 @@ struct JtVClique {
 #define JT_V_MAX_CHILDREN 6
 #define JT_V_WAVES 2  // waves sharing one 64-case block (disjoint subtrees in parallel)
 
+// ---- per-case variant, jt_case.hip (fast arithmetic order only): one wave = ONE evidence case,
+// lanes over that case's evidence-reduced clique entries (the reference's TableReduction,
+// src/PotentialTable.cpp:309-396, as an index space instead of a copied table: observed digits are
+// fixed, only the consistent entries are visited).  A pass over a clique forms every entry as
+//     init(e) * M_1(s_1(e)) * ... * M_k(s_k(e)) [* M_parent(s_up(e))]
+// (child Collect messages, then the parent's Distribute message) and accumulates the normalization
+// sum and the separator / marginal bins of that product; the per-step normalizations of the
+// reference cancel in the normalized result, so every message equals the reference's up to
+// rounding (one pass per clique and direction, no table is stored).  Messages of one case live in
+// the wave's slice of a global workspace as plain fp64 vectors (one 8-byte slot per separator
+// entry, not a 512-byte 64-case row).
+#define JT_C_MAX_CHILDREN 6
+#define JT_C_VREC 12  // per clique variable: {var, dim, cum, up-separator stride, child separator
+                      // strides [JT_C_MAX_CHILDREN], output offset of the variable, division magic}
+struct JtCClique {
+    int32_t T, nv, k, root;          // entries, variables, children, is the root
+    int32_t iv_off;                  // initial potentials (fp64 index)
+    int32_t var_off;                 // first of nv JT_C_VREC records
+    int32_t up_Ts, up_col, up_dis;   // upstream separator: entries, Collect / Distribute message
+                                     // offsets (fp64 index into the wave's message slice)
+    int32_t child_off;               // aux: k records {Ts, col, dis}
+    int32_t id, dbins;               // clique id; bins of its Distribute pass (sum child Ts + 4 * max dim)
+};
+
 #endif
