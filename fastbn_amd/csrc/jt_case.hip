@@ -131,9 +131,9 @@ __device__ __forceinline__ void make_space(const JtCClique &q, const Cv &v, int 
 
 typedef __attribute__((address_space(3))) double ldouble;
 typedef __attribute__((address_space(1))) double gdouble;
-template <bool GLOB>
-__device__ __forceinline__ void bin_add(double *b, double w) {
-    if (GLOB) __hip_atomic_fetch_add((gdouble *)b, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// bins in LDS, or in the wave's global bin area for bin sets beyond the LDS budget (uniform choice)
+__device__ __forceinline__ void bin_add(bool glob, double *b, double w) {
+    if (glob) __hip_atomic_fetch_add((gdouble *)b, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else __hip_atomic_fetch_add((ldouble *)b, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 constexpr int kU = 2;  // records in flight together (their loads issued before any product)
@@ -154,8 +154,8 @@ constexpr int kProf = 10;  // 0 case set-up, 1 Collect set-up, 2-4 Collect inner
 // gathers the K child Collect messages (+ the parent's Distribute message unless root) and adds into
 // the K child bins (when sepdis) and the m marginal bins; Collect: gathers the K child messages and
 // adds into the upstream separator's bins (unless root).  Returns this lane's partial sum.
-template <int K, bool DIST, bool GLOB>
-__device__ __forceinline__ double clique_pass_impl(const double *__restrict__ iv, const double *msg, double *bins,
+template <int K, bool DIST>
+__device__ __forceinline__ double clique_pass(bool glob, const double *__restrict__ iv, const double *msg, double *bins,
                                               const Cv &v, const Space &sp, int lane, bool root, const int (&ccol)[kMaxC],
                                               int up_dis, bool sepdis, const int (&cb)[kMaxC], int m,
                                               const int (&mpos)[kMaxM], const int (&mb)[kMaxM], int dbg,
@@ -249,15 +249,15 @@ __device__ __forceinline__ double clique_pass_impl(const double *__restrict__ iv
                     if (gp) x *= g[u][K];
                     acc += x;
                     if (dbg & kDbgNoAtomics) continue;
-                    if (bu) bin_add<GLOB>(bins + su[u] + vu, x);
+                    if (bu) bin_add(glob, bins + su[u] + vu, x);
                     if (DIST) {
                         if (sepdis) {
 #pragma unroll
-                            for (int k = 0; k < K; ++k) bin_add<GLOB>(bins + cb[k] + sc[u][k] + vc[k], x);
+                            for (int k = 0; k < K; ++k) bin_add(glob, bins + cb[k] + sc[u][k] + vc[k], x);
                         }
 #pragma unroll
                         for (int t = 0; t < kMaxM; ++t)
-                            if (t < m) bin_add<GLOB>(bins + mb[t] + sm[u][t] + vm[t], x);
+                            if (t < m) bin_add(glob, bins + mb[t] + sm[u][t] + vm[t], x);
                     }
                 }
             }
@@ -265,32 +265,6 @@ __device__ __forceinline__ double clique_pass_impl(const double *__restrict__ iv
         }
     }
     return acc;
-}
-
-// the LDS-bin pass inline; the global-bin one (bin sets beyond the LDS budget: rare, large
-// cliques) out of line, so the kernel's register allocation sees one copy per child count
-template <int K, bool DIST>
-__device__ __noinline__ double clique_pass_glob(const double *__restrict__ iv, const double *msg, double *bins,
-                                                const Cv &v, const Space &sp, int lane, bool root,
-                                                const int (&ccol)[kMaxC], int up_dis, bool sepdis,
-                                                const int (&cb)[kMaxC], int m, const int (&mpos)[kMaxM],
-                                                const int (&mb)[kMaxM], int dbg, unsigned long long (&tp)[kProf],
-                                                unsigned long long &t0) {
-    return clique_pass_impl<K, DIST, true>(iv, msg, bins, v, sp, lane, root, ccol, up_dis, sepdis, cb, m, mpos, mb,
-                                           dbg, tp, t0);
-}
-template <int K, bool DIST, bool GLOB>
-__device__ __forceinline__ double clique_pass(const double *__restrict__ iv, const double *msg, double *bins,
-                                              const Cv &v, const Space &sp, int lane, bool root,
-                                              const int (&ccol)[kMaxC], int up_dis, bool sepdis,
-                                              const int (&cb)[kMaxC], int m, const int (&mpos)[kMaxM],
-                                              const int (&mb)[kMaxM], int dbg, unsigned long long (&tp)[kProf],
-                                              unsigned long long &t0) {
-    if (GLOB)
-        return clique_pass_glob<K, DIST>(iv, msg, bins, v, sp, lane, root, ccol, up_dis, sepdis, cb, m, mpos, mb, dbg,
-                                         tp, t0);
-    return clique_pass_impl<K, DIST, false>(iv, msg, bins, v, sp, lane, root, ccol, up_dis, sepdis, cb, m, mpos, mb,
-                                            dbg, tp, t0);
 }
 
 // bins visible to every lane after the pass: LDS atomics are ordered within the wave; global ones
@@ -372,13 +346,10 @@ __global__ __launch_bounds__(64) void jt_case_kernel(
 
         // ---------------- Collect (children first; the root needs no pass of its own).  The next
         // clique's variable records are loaded while this one runs.
-        Cv vn;
-        if (nc > 1) load_vars(cls[post[0]], vrec, ev_s, lane, vn);
         for (int n = 0; n < nc - 1; ++n) {
             const JtCClique q = cls[post[n]];
-            Cv v = vn;
-            v.x = lane < q.nv ? ev_s[v.var] : -1;
-            if (n + 2 < nc) load_vars(cls[post[n + 1]], vrec, ev_s, lane, vn);
+            Cv v;
+            load_vars(q, vrec, ev_s, lane, v);
             FBN_TP(1);
             const bool glob = q.up_Ts > lds_bins;
             double *B = glob ? gbins : lbins;
@@ -395,8 +366,7 @@ __global__ __launch_bounds__(64) void jt_case_kernel(
             Space sp;
 #define FBN_CCALL(Kc)                                                                                          \
     make_space<Kc>(q, v, lane, sp);                                                                             \
-    a = glob ? clique_pass<Kc, false, true>(initv, msg, B, v, sp, lane, false, ccol, 0, false, cb, 0, mpos, mb, dbg, tp, t0) \
-             : clique_pass<Kc, false, false>(initv, msg, B, v, sp, lane, false, ccol, 0, false, cb, 0, mpos, mb, dbg, tp, t0)
+    a = clique_pass<Kc, false>(glob, initv, msg, B, v, sp, lane, false, ccol, 0, false, cb, 0, mpos, mb, dbg, tp, t0)
             FBN_CDISPATCH(q.k, FBN_CCALL);
 #undef FBN_CCALL
             const double S = wave_sum(a);
@@ -409,13 +379,11 @@ __global__ __launch_bounds__(64) void jt_case_kernel(
         }
 
         // ---------------- Distribute (parents first) and the marginals
-        load_vars(cls[pre[0]], vrec, ev_s, lane, vn);
         for (int n = 0; n < nc; ++n) {
             const int c = pre[n];
             const JtCClique q = cls[c];
-            Cv v = vn;
-            v.x = lane < q.nv ? ev_s[v.var] : -1;
-            if (n + 1 < nc) load_vars(cls[pre[n + 1]], vrec, ev_s, lane, vn);
+            Cv v;
+            load_vars(q, vrec, ev_s, lane, v);
             uint64_t mine = __ballot(lane < q.nv && v.x < 0 && sel_s[v.var] == c);
             if (q.k == 0 && mine == 0) continue;  // a leaf nobody reads a marginal from
             bool first = true;
@@ -455,10 +423,8 @@ __global__ __launch_bounds__(64) void jt_case_kernel(
                 FBN_WAVE_ORDER();
                 double a = 0.0;
 #define FBN_DCALL(Kc)                                                                                               \
-    a = glob ? clique_pass<Kc, true, true>(initv, msg, B, v, sp, lane, q.root != 0, ccol, q.up_dis, sepdis, cb, m, mpos, \
-                                           mb, dbg, tp, t0)                                                                  \
-             : clique_pass<Kc, true, false>(initv, msg, B, v, sp, lane, q.root != 0, ccol, q.up_dis, sepdis, cb, m,      \
-                                            mpos, mb, dbg, tp, t0)
+    a = clique_pass<Kc, true>(glob, initv, msg, B, v, sp, lane, q.root != 0, ccol, q.up_dis, sepdis, cb, m, mpos, mb, \
+                              dbg, tp, t0)
                 FBN_CDISPATCH(q.k, FBN_DCALL);
 #undef FBN_DCALL
                 const double R = wave_sum(a);

@@ -26,7 +26,8 @@
 // <= 2^22 candidate sets per level; a level outside those hands the search to the host driver
 // (pc_driver.cpp) at that level.  Synchronisation follows MI355X_MICROARCH.md's barrier-xcd form:
 // per-group arrival counters (group = blockIdx % 8), the last arriver of a group adds to the top
-// counter, every workgroup polls relaxed with s_sleep, one release before and one acquire after,
+// counter, every workgroup polls relaxed with s_sleep; the data crossing workgroups moves through
+// agent-coherent accesses, so the barrier carries no cache-maintenance fence (see grid_barrier);
 // every spin bounded (a timed-out launch reports status 1 and exits).
 #include <hip/hip_runtime.h>
 #include <stddef.h>
@@ -83,6 +84,13 @@ struct Lds {
 };
 
 __device__ __forceinline__ int popc64(uint64_t v) { return __popcll(v); }
+// agent-coherent (sc1) accesses of data one workgroup hands to another (see grid_barrier)
+__device__ __forceinline__ unsigned long long ld_agent(const unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // ---- wave-wide reductions on DPP (VALU lane moves, no LDS round trip): an inclusive scan inside
 // each 16-lane row (row_shr 1, 2, 4, 8 with zeros shifted in), then row_bcast:15 / :31 carry the
@@ -164,6 +172,12 @@ __device__ __forceinline__ int pair_index(int n, int x, int y) {  // x < y
 }
 
 // ---- grid barrier (barrier-xcd form), phase = 1, 2, ...
+// Everything one workgroup hands to another crosses through agent-coherent accesses (sc1: the
+// first[] atomics, the level-0 pair tables and the statistics slots as relaxed agent-scope atomic
+// stores / loads), so the barrier needs no release / acquire fence: on MI355X those are an L2
+// writeback and an L2 invalidate per arriving workgroup (each XCD has its own L2), ~4 us per level
+// and a cold L2 for the next level's column reads.  What it does need is that every such store has
+// completed (vmcnt(0) in every wave) before the workgroup arrives.
 struct Barrier {
     unsigned *grp;   // kGroups arrival counters, each on its own 64-B line (stride 16)
     unsigned *top;   // groups done
@@ -171,15 +185,12 @@ struct Barrier {
 };
 
 __device__ bool grid_barrier(const Barrier &B, unsigned phase, Lds &L) {
-    // every wave's stores are complete before the workgroup's release
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         const int g = blockIdx.x % kGroups;
         const int ngroups = B.nblocks < kGroups ? B.nblocks : kGroups;
         const unsigned gsize = (unsigned)((B.nblocks - g + kGroups - 1) / kGroups);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned old = __hip_atomic_fetch_add(B.grp + 16 * g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old == phase * gsize - 1)  // last of its group in this phase: the group arrives
             __hip_atomic_fetch_add(B.top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -193,7 +204,6 @@ __device__ bool grid_barrier(const Barrier &B, unsigned phase, Lds &L) {
                 break;
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         L.flag = ok;
     }
@@ -346,7 +356,7 @@ __device__ __forceinline__ Decision wave_test(const PcSmallArgs &A, const Lds &L
             src = A.pairtab + 16 * (size_t)pair_index(n, u < v ? u : v, u < v ? v : u);
             k = lane & 15;
         }
-        if (src) aux[lane] = src[k];
+        if (src) aux[lane] = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     const int mx = dx - 1, my = dy - 1, mz = D == 1 ? dz - 1 : 1;
     const long long W = A.W;
@@ -441,7 +451,9 @@ __device__ __forceinline__ Decision wave_test(const PcSmallArgs &A, const Lds &L
     }
     wave_lds_sync();
     const int ob = live ? tab[lane] : 0;
-    if (D == 0 && record_pair && live) A.pairtab[16 * (size_t)pair_index(n, x, y) + lane] = ob;
+    if (D == 0 && record_pair && live)
+        __hip_atomic_store(A.pairtab + 16 * (size_t)pair_index(n, x, y) + lane, ob, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long c2 = A.trace ? clock64() : 0;
     // marginals: N_{x+z} = N_xz, N_{+yz} = N_yz, N_{++z} = sum_a N_xz; adjusted df per z
     // (src/IndependenceTest.cpp:96-112, 309-322)
@@ -725,9 +737,9 @@ __device__ void finalize(const PcSmallArgs &A, Lds &L, int nb, int levels, int h
     unsigned long long mm = ~0ull;
     long long nn = 0;
     for (int b = tid; b < nb; b += BS) {
-        const unsigned long long v = A.acc[8 * (size_t)b];
+        const unsigned long long v = ld_agent(A.acc + 8 * (size_t)b);
         mm = v < mm ? v : mm;
-        nn += (long long)A.acc[8 * (size_t)b + 1];
+        nn += (long long)ld_agent(A.acc + 8 * (size_t)b + 1);
     }
     mm = block_min_u64(mm, L);
     nn = block_sum_ll(nn, L);
@@ -909,7 +921,7 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
                 __hip_atomic_fetch_max(A.first + (size_t)d * kSmallMaxEdges + e,
                                        ((unsigned long long)A.epoch << 32) | (unsigned)~L.bfirst[e], __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
-        // this workgroup's statistics into its slot (plain stores, published by the barrier)
+        // this workgroup's statistics into its slot (agent-coherent stores, published by the barrier)
         if (tid == 0) {
             unsigned long long mm = ~0ull, nn = 0, ll = 0;
 #pragma unroll
@@ -917,9 +929,9 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
                 mm = L.wst[w][0] < mm ? L.wst[w][0] : mm;
                 nn += L.wst[w][1], ll += L.wst[w][2];
             }
-            slot[0] = mm;
-            slot[1] = nn;
-            slot[2 + d] = ll;
+            st_agent(slot, mm);
+            st_agent(slot + 1, nn);
+            st_agent(slot + 2 + d, ll);
         }
         if (A.trace && tid == 0) A.trace[64 + (size_t)d * 1024 + bid] = (unsigned long long)wall_clock64();
         if (A.trace && tid < 4) {  // phase cycles summed over the workgroup's waves -> trace[8d + 4 + k]
@@ -964,7 +976,7 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
                 __syncthreads();
             }
             long long la = 0;
-            for (int b = tid; b < nb; b += BS) la += (long long)A.acc[8 * (size_t)b + 2 + d];
+            for (int b = tid; b < nb; b += BS) la += (long long)ld_agent(A.acc + 8 * (size_t)b + 2 + d);
             la = block_sum_ll(la, L);
             if (tid == 0) {
                 A.dout->sep_off[d] = sep_cursor;
