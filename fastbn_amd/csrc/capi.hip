@@ -2392,6 +2392,8 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
               std::vector<std::vector<int>> &adj, int *levels, bool *handoff) {
     *levels = 0;
     *handoff = false;
+    static const bool htime = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic: host phases of the call
+    const auto h0 = std::chrono::steady_clock::now();
     FBN_HIP(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     int rc;
@@ -2399,8 +2401,8 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
     const double *band = nullptr;
     int nband = 0;
     if ((rc = CiBand(c, alpha, s, &band, &nband, kBandDfMax))) return rc;
-    int per_cu = 0;
-    FBN_HIP(fbn_pc_small_occupancy(&per_cu));
+    static int per_cu = 0;  // (a property of the kernel: queried once)
+    if (per_cu == 0) FBN_HIP(fbn_pc_small_occupancy(&per_cu));
     if (per_cu < 1) return SetError(FBN_ERR_HIP, "pc small kernel: no workgroup fits a CU");
     const int grid = c->num_cu;  // one workgroup per CU: every workgroup resident (grid barrier)
     // scratch: [zeroed: barrier words | first-independent words] [statistics slots] [pair tables]
@@ -2428,6 +2430,7 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
     a.bits = c->bits.as<uint32_t>();
     a.row0 = c->brow.as<int32_t>();
     a.rowcnt = c->browcnt.as<int32_t>();
+    a.nrows = c->row0_host.back() + std::min(c->dims[c->nvars - 1], 8);
     a.W = c->bits_W;
     a.pk = c->pack2.as<uint32_t>();
     a.PW = c->pack2_W;
@@ -2459,9 +2462,11 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
         trace_host.assign(tb / 8, 0);
     }
     CiSlot &S = c->slot[0];
+    const auto h1 = std::chrono::steady_clock::now();
     if (c->timing) FBN_HIP(hipEventRecord(S.ev0, s));
     FBN_HIP(fbn_pc_small_launch(&a, grid, s));
     if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
+    const auto h2 = std::chrono::steady_clock::now();
     // wait for the kernel's completion word (written after the record) instead of a stream sync;
     // a stream sync only for the events / trace, or when the word does not come (fault, hang)
     {
@@ -2476,6 +2481,7 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
         }
         if (!got || c->timing || trace) FBN_HIP(hipStreamSynchronize(s));
     }
+    const auto h3 = std::chrono::steady_clock::now();
     if (trace) {
         FBN_HIP(hipMemcpy(trace_host.data(), trace_dev.p, trace_host.size() * 8, hipMemcpyDeviceToHost));
         h_trace = trace_host.data();
@@ -2566,6 +2572,14 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
         res.min_margin = m;
         res.near_alpha = (int64_t)out->near;
         res.margin_done = true;
+    }
+    if (htime) {
+        const auto h4 = std::chrono::steady_clock::now();
+        auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+            return std::chrono::duration<double, std::micro>(b - a).count();
+        };
+        fprintf(stderr, "pc small host: set-up %.1f us, launch %.1f us, wait %.1f us, record -> result %.1f us\n",
+                us(h0, h1), us(h1, h2), us(h2, h3), us(h3, h4));
     }
     return FBN_OK;
 }

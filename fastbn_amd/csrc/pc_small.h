@@ -49,6 +49,7 @@ struct PcSmallArgs {
     const uint32_t *bits;    // bit-sliced masks: row (row0[v] + a), W words (multiple of 4)
     const int32_t *row0;
     const int32_t *rowcnt;   // samples per mask row
+    int nrows;               // mask rows (rowcnt entries)
     long long W;
     const uint32_t *pk;      // 2-bit packed columns: PW words per variable, 16 samples per word
     long long PW;

@@ -51,6 +51,12 @@ constexpr long long kSpinTicks = 200000000ll;  // wall_clock64 ticks (100 MHz): 
 typedef __attribute__((ext_vector_type(4))) unsigned u4;
 
 constexpr int kWaveHist = 2048;    // per-wave region of the one-wave histogram tests (d = 2, 3)
+// One-wave levels (1, 2) run in two parts: A = the first kSpecA candidate sets of every edge
+// (about one round of the grid's waves on ALARM-5000), then B = the rest, edge-major.  A part-B test
+// first checks whether its edge already has an independent set at a lower index (published by
+// every independent test as it happens, not at the end of the level) and is skipped if so: it
+// could never be the edge's first.  Counts, removals and sepsets are those of full speculation.
+constexpr int kSpecA = 8;
 
 struct Lds {
     // per-run constants staged once: state counts, first mask row and per-row sample counts of
@@ -59,7 +65,10 @@ struct Lds {
     double band[2 * 256 + 1];
     uint64_t adj[kSmallMaxVars];
     int32_t rowoff[kSmallMaxVars + 1];     // edges of rows before x
-    int32_t eoff[kSmallMaxEdges + 1];      // first test of each edge
+    int32_t eoff[kSmallMaxEdges + 1];      // part A: first test of each edge (its first kSpecA candidates)
+    int32_t eoffB[kSmallMaxEdges + 1];     // part B: first test of each edge's remaining candidates
+    int32_t TA;                            // tests in part A
+    int32_t next;                          // one-wave levels: this workgroup's next test (dynamic)
     uint8_t ex[kSmallMaxEdges], ey[kSmallMaxEdges], rm[kSmallMaxEdges];
     int32_t binom[kSmallMaxVars + 1][kSmallMaxD + 1];
     int32_t wscan[NWAVE];
@@ -744,6 +753,12 @@ __device__ void finalize(const PcSmallArgs &A, Lds &L, int nb, int levels, int h
     mm = block_min_u64(mm, L);
     nn = block_sum_ll(nn, L);
     PcSmallOut *o = A.dout;
+    for (int d = 0; d < levels; ++d) {  // tests evaluated per level, over every workgroup's slot
+        long long la = 0;
+        for (int b = tid; b < nb; b += BS) la += (long long)ld_agent(A.acc + 8 * (size_t)b + 2 + d);
+        la = block_sum_ll(la, L);
+        if (tid == 0) o->launched[d] = la;
+    }
     if (tid == 0) {
         o->margin_bits = mm;
         o->near = (unsigned long long)nn;
@@ -776,11 +791,13 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
     const int nb = gridDim.x;
     const int bid = blockIdx.x;
     if (A.trace && bid == 0 && tid == 0) A.trace[63] = (unsigned long long)wall_clock64();
+    // prologue: every constant staged in ONE round of independent loads (no load depends on
+    // another), binomials in 32-bit arithmetic (C(64, 4) < 2^20)
     for (int i = tid; i < (kSmallMaxVars + 1) * (kSmallMaxD + 1); i += BS) {
         const int m = i / (kSmallMaxD + 1), k = i % (kSmallMaxD + 1);
-        long long r = 1;
+        int r = 1;
         for (int j = 1; j <= k; ++j) r = r * (m - k + j) / j;
-        L.binom[m][k] = m < k ? 0 : (int)r;
+        L.binom[m][k] = m < k ? 0 : r;
     }
     for (int v = tid; v < kSmallMaxVars; v += BS) {
         const uint64_t all = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
@@ -788,12 +805,9 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
         L.dims[v] = v < n ? A.dims[v] : 1;
         L.row0[v] = v < n ? A.row0[v] : 0;
     }
-    for (int r = tid; r < 4 * kSmallMaxVars; r += BS) L.rowcnt[r] = 0;
+    for (int r = tid; r < 4 * kSmallMaxVars; r += BS) L.rowcnt[r] = r < A.nrows ? A.rowcnt[r] : 0;
     if (A.band)
         for (int i = tid; i <= 2 * A.nband; i += BS) L.band[i] = A.band[i];
-    __syncthreads();
-    for (int v = tid; v < n; v += BS)
-        for (int a = 0; a < L.dims[v]; ++a) L.rowcnt[L.row0[v] + a] = A.rowcnt[L.row0[v] + a];
     __syncthreads();
     // this workgroup's statistics slot: [0] min margin bits, [1] near, [2 + d] tests evaluated
     unsigned long long wmin = ~0ull, wnear = 0ull;
@@ -836,14 +850,24 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
                 const int x = L.ex[e], y = L.ey[e];
                 return d == 0 ? 1 : binom_l(L, popc64(L.adj[x]) - 1, d) + binom_l(L, popc64(L.adj[y]) - 1, d);
             };
-            long long mine = 0;  // (int64: a level's total may exceed 2^31 -> hand-off below)
-            for (int e = e0; e < e1; ++e) mine += ntests(e);
+            const int KA = (d == 1 || d == 2) ? kSpecA : 0x40000000;  // part A per edge
+            long long mine = 0, mineA = 0;  // (int64: a level's total may exceed 2^31 -> hand-off below)
+            for (int e = e0; e < e1; ++e) {
+                const int nt = ntests(e);
+                mine += nt;
+                mineA += nt < KA ? nt : KA;
+            }
             tot64 = block_sum_ll(mine, L);
             if (tot64 <= kSmallMaxTests) {  // (workgroup-uniform) int32 offsets
-                int total = 0;
-                int run = block_excl_scan((int)mine, L, &total);
-                for (int e = e0; e < e1; ++e) L.eoff[e] = run, run += ntests(e);
-                if (tid == 0) L.eoff[E] = total;
+                int totalA = 0, totalB = 0;
+                int runA = block_excl_scan((int)mineA, L, &totalA);
+                int runB = block_excl_scan((int)(mine - mineA), L, &totalB);
+                for (int e = e0; e < e1; ++e) {
+                    const int nt = ntests(e), na = nt < KA ? nt : KA;
+                    L.eoff[e] = runA, runA += na;
+                    L.eoffB[e] = runB, runB += nt - na;
+                }
+                if (tid == 0) L.eoff[E] = totalA, L.eoffB[E] = totalB, L.TA = totalA;
             }
         }
         __syncthreads();
@@ -856,21 +880,44 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
         const int T = (int)tot64;
         for (int e = tid; e < E; e += BS) L.bfirst[e] = ~0u;
         if (tid < NWAVE * 4) (&L.ph[0][0])[tid] = 0ull;
+        if (tid == 0) L.next = 0;
         __syncthreads();
         if (A.trace && bid == 0 && tid == 0) A.trace[8 * d + 0] = (unsigned long long)wall_clock64();
         if (A.trace && tid == 0) A.trace[64 + 5 * 1024 + (size_t)d * 1024 + bid] = (unsigned long long)wall_clock64();
         // ---- the tests
         unsigned long long launched = 0;
         if (d <= 2) {
-            const int gw = bid * NWAVE + wv, nw = nb * NWAVE;
-            for (int t = gw; t < T; t += nw) {
-                int lo = 0, hi = E;  // last edge whose first test <= t
+            // workgroup b takes tests t = b' + nb j (b' = nb - 1 - b: workgroup 0, which builds the
+            // result record between levels, the last and lightest share); its waves claim j
+            // dynamically, so part-B skips do not leave some waves with more tests than others
+            const int b0 = nb - 1 - bid;
+            const int TA = L.TA;
+            // test t -> (edge, candidate index): part A, then part B (see kSpecA)
+            auto locate = [&](int t, int &e, int &k) {
+                const bool b = t >= TA;
+                const int32_t *off = b ? L.eoffB : L.eoff;
+                const int tt = b ? t - TA : t;
+                int lo = 0, hi = E;  // last edge whose first test <= tt
                 while (hi - lo > 1) {
                     const int mid = (lo + hi) >> 1;
-                    if (L.eoff[mid] <= t) lo = mid;
+                    if (off[mid] <= tt) lo = mid;
                     else hi = mid;
                 }
-                const int e = lo, k = t - L.eoff[e];
+                e = lo;
+                k = tt - off[lo] + (b ? kSpecA : 0);
+            };
+            while (true) {
+                int j = 0;
+                if (lane == 0) j = atomicAdd(&L.next, 1);
+                const int t = b0 + nb * __shfl(j, 0);
+                if (t >= T) break;
+                int e, k;
+                locate(t, e, k);
+                if (t >= TA) {  // part B: skip a candidate behind an independent one (read just before
+                                // the test: a check loaded a test earlier sees too little of part A)
+                    const unsigned fl = L.bfirst[e], fg = first_of(A, d, e);
+                    if ((fg != ~0u && fg < (unsigned)k) || (fl != ~0u && fl < (unsigned)k)) continue;
+                }
                 const int x = L.ex[e], y = L.ey[e];
                 Decision r;
                 if (d == 0) {
@@ -886,10 +933,16 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
                 const unsigned long long mb = (unsigned long long)__double_as_longlong(r.margin);
                 wmin = mb < wmin ? mb : wmin;
                 wnear += r.margin < 1e-9;
-                if (r.ind == 1 && lane == 0) atomicMin(&L.bfirst[e], (unsigned)k);  // LDS, flushed below
+                if (r.ind == 1 && lane == 0) {
+                    atomicMin(&L.bfirst[e], (unsigned)k);
+                    if (d >= 1)  // published at once for the part-B checks of every workgroup
+                        __hip_atomic_fetch_max(A.first + (size_t)d * kSmallMaxEdges + e,
+                                               ((unsigned long long)A.epoch << 32) | (unsigned)~(unsigned)k,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
         } else {
-            for (int t = bid; t < T; t += nb) {
+            for (int t = nb - 1 - bid; t < T; t += nb) {
                 int lo = 0, hi = E;
                 while (hi - lo > 1) {
                     const int mid = (lo + hi) >> 1;
@@ -954,7 +1007,8 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
             const unsigned f = first_of(A, d, e);
             const bool rmv = f != ~0u;
             L.rm[e] = rmv;
-            counted += rmv ? (long long)f + 1 : (long long)(L.eoff[e + 1] - L.eoff[e]);
+            counted += rmv ? (long long)f + 1
+                           : (long long)(L.eoff[e + 1] - L.eoff[e]) + (long long)(L.eoffB[e + 1] - L.eoffB[e]);
         }
         __syncthreads();
         if (bid == 0) {  // the result record (the other workgroups go straight on to the next level)
@@ -975,14 +1029,10 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) 
                 carry += total;
                 __syncthreads();
             }
-            long long la = 0;
-            for (int b = tid; b < nb; b += BS) la += (long long)ld_agent(A.acc + 8 * (size_t)b + 2 + d);
-            la = block_sum_ll(la, L);
-            if (tid == 0) {
+            if (tid == 0) {  // (launched[d]: summed over the workgroups' slots in finalize)
                 A.dout->sep_off[d] = sep_cursor;
                 A.dout->sep_off[d + 1] = sep_cursor + carry * d;
                 A.dout->counted[d] = counted;
-                A.dout->launched[d] = la;
             }
             sep_cursor += carry * d;
         }

@@ -1,7 +1,9 @@
 """The device-resident PC-stable skeleton search for small graphs (fastbn_amd/csrc/pc_small.hip: one
 launch runs every level, one grid barrier per level) against the restatement (oracle/pc_oracle.cpp)
 and against the host-driven level loop (FBN_PC_NO_SMALL): tests per level, skeleton (vec_edges
-order), sepsets, orientation; launched = every candidate set of every edge (full speculation)."""
+order), sepsets, orientation.  launched: levels 1-2 evaluate every edge's first 8 candidate sets, then
+skip the rest of an edge once an independent set at a lower index is published (timing-dependent,
+between the counted tests and full speculation); levels 0, 3, 4 evaluate every candidate set."""
 import os
 
 import numpy as np
@@ -45,8 +47,10 @@ def test_alarm5000_default_is_device_resident(alarm, monkeypatch):
     ds, od = alarm
     pc = _check(ds, od, 0.05, 1000, monkeypatch)
     assert pc.tests_per_level.tolist() == [666, 3579, 828, 118, 15] and len(pc.edges) == 44
-    # every candidate set of every edge is evaluated once: the host driver's one-round schedule
-    assert pc.launched_per_level.tolist() == [666, 8732, 1212, 128, 15]
+    # levels 0, 3, 4: every candidate set once; 1, 2: full speculation minus the part-B skips
+    la = pc.launched_per_level.tolist()
+    assert la[0] == 666 and la[3:] == [128, 15]
+    assert 3579 <= la[1] <= 8732 and 828 <= la[2] <= 1212
     assert pc.GetSHD(os.path.join(GOLD, "alarm", "alarm.bif")) == 5
     assert pc.near_alpha == 0 and pc.min_margin > 1e-9
 
