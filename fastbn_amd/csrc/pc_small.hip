@@ -546,14 +546,24 @@ __device__ __noinline__ Decision wave_hist_test(const PcSmallArgs &A, const Lds 
             const long long w = w0 + 64 * u;
             const long long left = w < PW ? N - 16 * w : 0;
             const int lim = left < 16 ? (int)left : 16;
+            // consecutive samples of the word in the same cell fold into one atomic (skewed data)
+            int prev = -1, run = 0;
 #pragma unroll
             for (int s = 0; s < 16; ++s) {
                 int zi = 0;
 #pragma unroll
                 for (int j = 0; j < D; ++j) zi += (int)((wz[u][j] >> (2 * s)) & 3u) * cum[j];
                 const int cl = (zi * dx + (int)((wx[u] >> (2 * s)) & 3u)) * dy + (int)((wy[u] >> (2 * s)) & 3u);
-                if (s < lim) atomicAdd(&myh[cl], 1);
+                if (s < lim) {
+                    if (cl == prev) {
+                        ++run;
+                    } else {
+                        if (run) atomicAdd(&myh[prev], run);
+                        prev = cl, run = 1;
+                    }
+                }
             }
+            if (run) atomicAdd(&myh[prev], run);
         }
     }
     wave_lds_sync();
@@ -652,14 +662,23 @@ __device__ __noinline__ Decision block_test(const PcSmallArgs &A, int x, int y, 
         for (int j = 0; j < D; ++j) wz[j] = pz[j][w];
         const long long left = N - 16 * w;
         const int lim = left < 16 ? (int)left : 16;
+        int prev = -1, run = 0;  // consecutive samples in the same cell: one atomic
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
             int zi = 0;
 #pragma unroll
             for (int j = 0; j < D; ++j) zi += (int)((wz[j] >> (2 * s)) & 3u) * cum[j];
             const int cl = (zi * dx + (int)((wx >> (2 * s)) & 3u)) * dy + (int)((wy >> (2 * s)) & 3u);
-            if (s < lim) atomicAdd(&my[cl], 1);
+            if (s < lim) {
+                if (cl == prev) {
+                    ++run;
+                } else {
+                    if (run) atomicAdd(&my[prev], run);
+                    prev = cl, run = 1;
+                }
+            }
         }
+        if (run) atomicAdd(&my[prev], run);
     }
     __syncthreads();
     if (copies > 1) {

@@ -145,7 +145,11 @@ int fbn_jt_set_waves_per_cu(fbn_jt_plan *p, int waves);
  *     by an exact-path fixup of the blocks it flags.  Selecting 3 fails if the plan is not eligible.
  * 4 = streamed ("virtual table") kernel for large trees (jt_virt.hip): tables recomputed per pass
  *     from initial potentials + received messages, only messages stored; exact-path fixup as 3.
- *     Selecting 4 fails for plans it cannot take (a clique with more than 6 children, ...). */
+ *     Selecting 4 fails for plans it cannot take (a clique with more than 6 children, ...).
+ * 5 = per-case kernel (jt_case.hip, opt-in): one wave per evidence case over its evidence-reduced
+ *     clique entries, one pass per clique and direction, fast arithmetic order only (the exact
+ *     setting does not apply); exact-path fixup as 3.  Fails for plans with > 6 children per clique,
+ *     > 64 variables per clique or a domain > 64 states. */
 int fbn_jt_set_variant(fbn_jt_plan *p, int variant);
 /* Arithmetic order of the streamed kernel (variant 4): 1 = exact (the reference's sequential
  * Normalize after every multiply: bit-identical marginals), 0 = fast (all Collect normalization sums
