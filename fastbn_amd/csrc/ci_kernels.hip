@@ -211,26 +211,14 @@ __global__ __launch_bounds__(BS) void ci_g2_kernel(CiArgs A) {
             for (int j = 0; j < D; ++j) pz[j] = A.pk + (size_t)zv[j] * A.PW;
             const long long full = A.N / 16;
             auto bin16 = [&](uint32_t wx, uint32_t wy, const uint32_t *wz, int lim) {
-                // LDS tables: consecutive samples of the word in the same cell fold into one atomic
-                int prev = -1, run = 0;
 #pragma unroll
                 for (int s = 0; s < 16; ++s) {
                     int zi = 0;
 #pragma unroll
                     for (int j = 0; j < D; ++j) zi += (int)((wz[j] >> (2 * s)) & 3u) * cum[j];
                     const int cell = (zi * dx + (int)((wx >> (2 * s)) & 3u)) * dy + (int)((wy >> (2 * s)) & 3u);
-                    if (packed) {
-                        bin(s < lim ? cell : 0, s < lim);
-                    } else if (s < lim) {
-                        if (cell == prev) {
-                            ++run;
-                        } else {
-                            if (run) atomicAdd(&myhist[prev], run);
-                            prev = cell, run = 1;
-                        }
-                    }
+                    bin(s < lim ? cell : 0, s < lim);
                 }
-                if (run) atomicAdd(&myhist[prev], run);
             };
             constexpr int kU = 2;
             for (long long kb = tid; kb < full; kb += BS * kU) {
