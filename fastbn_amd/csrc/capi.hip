@@ -27,7 +27,8 @@ extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, co
                                     uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
                                     int32_t *gscratch, unsigned long long *stats, const uint32_t *bits,
                                     const int32_t *row0, long long W, const double *band, int nband,
-                                    const uint32_t *pk, long long PW, long long cstride, hipStream_t stream);
+                                    const uint32_t *pk, long long PW, long long cstride, int32_t *tab,
+                                    long long tstride, int split, int split_grid, hipStream_t stream);
 extern "C" hipError_t fbn_ci_pack2_build(const uint8_t *cols, int nvars, long long N, long long PW, uint32_t *pk,
                                          hipStream_t stream);
 extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy);
@@ -1682,6 +1683,30 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
     S.last_bytes = bitsn ? mask_rows * c->bits_W * 4  // the mask rows each z-configuration reads
                    : pk  ? n * c->pack2_W * 4 * (2 + d)  // the 2-bit columns x, y, z_1..z_d
                          : n * c->N * (2 + d);  // uint8 columns x, y, z_1..z_d streamed once
+    // small batches on the packed columns (config 5 levels 3-5: 1056 / 260 / 30 tests of 100k
+    // samples): each test's words split over several workgroups so the batch fills the chip, the
+    // partial histograms added into a global table per test, then one workgroup per test decides
+    int split = 1, split_grid = 0;
+    int64_t tstride = 0;
+    int32_t *tab = nullptr;
+    static const int split_env = getenv("FBN_CI_SPLIT") ? atoi(getenv("FBN_CI_SPLIT")) : -1;  // (tuning knob)
+    if (pk && !bitsn && !global_tables) {
+        const int64_t want = 4 * (int64_t)c->num_cu;  // counting workgroups to aim for
+        split = split_env >= 0 ? std::max(1, split_env) : (int)std::min<int64_t>(16, want / std::max<int64_t>(n, 1));
+        if (split > 1) {
+            int64_t cmax = 1;
+            for (int64_t i = 0; i < n; ++i) {
+                const int32_t *it = items + i * w;
+                int64_t cells = (int64_t)c->dims[it[0]] * c->dims[it[1]];
+                for (int j = 0; j < d; ++j) cells *= c->dims[it[2 + j]];
+                cmax = std::max(cmax, cells);
+            }
+            tstride = (cmax + 63) & ~(int64_t)63;
+            if ((rc = S.scratch.ensure((size_t)n * tstride * 4))) return rc;
+            tab = S.scratch.as<int32_t>();
+            split_grid = (int)std::min<int64_t>(n * split, (int64_t)c->num_cu * 8);
+        }
+    }
     if (c->timing) FBN_HIP(hipEventRecord(S.ev0, s));
     hipError_t e = fbn_ci_launch(c->cols.as<uint8_t>(), c->ddims.as<int32_t>(),
                                  zc_items ? zc_items : S.items.as<int32_t>(), c->N, n, d, alpha,
@@ -1689,7 +1714,8 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
                                  want_g2p ? c->p.as<double>() : nullptr, zc_indep ? zc_indep : S.indep.as<uint8_t>(),
                                  counts_dev, lds, grid, gscratch, c->stats.as<unsigned long long>(),
                                  bitsn ? c->bits.as<uint32_t>() : nullptr, c->brow.as<int32_t>(), c->bits_W, hband,
-                                 hnband, pk ? c->pack2.as<uint32_t>() : nullptr, c->pack2_W, c->counts_stride, s);
+                                 hnband, pk ? c->pack2.as<uint32_t>() : nullptr, c->pack2_W, c->counts_stride, tab,
+                                 tstride, split, split_grid, s);
     if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci kernel launch: %s", hipGetErrorString(e));
     if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
     return FBN_OK;

@@ -67,20 +67,33 @@ struct CiArgs {
     // counts != nullptr: cstride == 0 -> the table of test 0 only; cstride > 0 -> every test's table
     // at counts + test * cstride (fbn_ci_debug_counts)
     long long cstride;
+    // split mode (small batches, MODE 1 / 2): test t's table at tab + t * tstride (zeroed), its
+    // packed words divided among `split` workgroups
+    int32_t *tab;
+    long long tstride;
+    int split;
 };
 
 // BITS: count from the bit-sliced store (A.bits); a separate instantiation, so the byte-column
 // kernel keeps its register budget (74 VGPRs vs 178 with the bit-sliced counters compiled in).
 // PK: count from the 2-bit packed columns (A.pk): a quarter of the byte columns' bytes, the same
 // per-sample binning (one field extract per variable and sample, as the byte extract)
-template <int D, bool BITS, bool PK = false, int BS = 256>
+// MODE (2-bit packed columns only): 0 = one workgroup counts and decides a test; 1 = workgroup
+// (t, part) counts part `part` of test t's packed words and adds its histogram into the global table
+// of t; 2 = one workgroup per test reads the table and decides.  Small batches (the deep levels of
+// config 5: 30-1056 tests of 100k samples each, one workgroup per test leaves most CUs idle) run as
+// 1 then 2.  Counts are integers: the same in any order.
+template <int D, bool BITS, bool PK = false, int BS = 256, int MODE = 0>
 __global__ __launch_bounds__(BS) void ci_g2_kernel(CiArgs A) {
     constexpr int NW = BS / 64;  // waves per workgroup (sub-histogram copies exist for 4 of them)
     extern __shared__ __align__(16) int32_t lds_base[];
     int32_t *smem = A.gscratch ? A.gscratch + (size_t)blockIdx.x * A.gstride : lds_base;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    for (long long it = blockIdx.x; it < A.n; it += gridDim.x) {
+    const long long nwork = MODE == 1 ? A.n * A.split : A.n;
+    for (long long iw = blockIdx.x; iw < nwork; iw += gridDim.x) {
+        const long long it = MODE == 1 ? iw / A.split : iw;
+        const int part = MODE == 1 ? (int)(iw % A.split) : 0, nparts = MODE == 1 ? A.split : 1;
         const int32_t *item = A.items + it * (2 + D);
         const int x = item[0], y = item[1];
         const int dx = A.dims[x], dy = A.dims[y];
@@ -115,8 +128,8 @@ __global__ __launch_bounds__(BS) void ci_g2_kernel(CiArgs A) {
         const int term_off = (int)((dfp + dimz) - smem + 1) & ~1;
         double *term = reinterpret_cast<double *>(smem + term_off);
 
-        for (int c = tid; c < cells; c += BS) hist[c] = 0;
-        if (nsub > 1 && !BITS)
+        for (int c = tid; c < cells; c += BS) hist[c] = MODE == 2 ? A.tab[it * A.tstride + c] : 0;
+        if (nsub > 1 && !BITS && MODE != 2)
             for (int c = tid; c < nsub * sstr; c += BS) sub[c] = 0;
         __syncthreads();
         if (BITS) {
@@ -187,7 +200,7 @@ __global__ __launch_bounds__(BS) void ci_g2_kernel(CiArgs A) {
                         }
             }
         }
-        if (!BITS) {
+        if (!BITS && MODE != 2) {
         int32_t *myhist = nsub > 1 ? sub + (((tid >> 6) & 3) * kl + (lane & (kl - 1))) * sstr : hist;
         unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;  // cell c: a[c >> 2] bits [16 (c & 3), +16)
         auto bin = [&](int cell, bool valid) {
@@ -210,6 +223,8 @@ __global__ __launch_bounds__(BS) void ci_g2_kernel(CiArgs A) {
 #pragma unroll
             for (int j = 0; j < D; ++j) pz[j] = A.pk + (size_t)zv[j] * A.PW;
             const long long full = A.N / 16;
+            // this workgroup's words [w0, w1) (all of them unless MODE 1)
+            const long long w0 = full * part / nparts, w1 = full * (part + 1) / nparts;
             auto bin16 = [&](uint32_t wx, uint32_t wy, const uint32_t *wz, int lim) {
 #pragma unroll
                 for (int s = 0; s < 16; ++s) {
@@ -221,13 +236,13 @@ __global__ __launch_bounds__(BS) void ci_g2_kernel(CiArgs A) {
                 }
             };
             constexpr int kU = 2;
-            for (long long kb = tid; kb < full; kb += BS * kU) {
+            for (long long kb = w0 + tid; kb < w1; kb += BS * kU) {
                 uint32_t wx[kU], wy[kU], wz[kU][D > 0 ? D : 1];
                 bool v[kU];
 #pragma unroll
                 for (int u = 0; u < kU; ++u) {
                     const long long k = kb + u * BS;
-                    v[u] = k < full;
+                    v[u] = k < w1;
                     const long long kk = v[u] ? k : 0;
                     wx[u] = px[kk], wy[u] = py[kk];
 #pragma unroll
@@ -236,7 +251,7 @@ __global__ __launch_bounds__(BS) void ci_g2_kernel(CiArgs A) {
 #pragma unroll
                 for (int u = 0; u < kU; ++u) bin16(wx[u], wy[u], wz[u], v[u] ? 16 : 0);
             }
-            if (A.N % 16 && tid == 0) {
+            if (A.N % 16 && tid == 0 && part == nparts - 1) {
                 uint32_t wz[D > 0 ? D : 1];
 #pragma unroll
                 for (int j = 0; j < D; ++j) wz[j] = pz[j][full];
@@ -300,13 +315,19 @@ __global__ __launch_bounds__(BS) void ci_g2_kernel(CiArgs A) {
         }
         }  // !BITS
         __syncthreads();
-        if (nsub > 1 && !BITS) {
+        if (nsub > 1 && !BITS && MODE != 2) {
             for (int c = tid; c < cells; c += BS) {
                 int v = 0;
                 for (int w = 0; w < nsub; ++w) v += sub[w * sstr + c];
                 hist[c] = v;
             }
             __syncthreads();
+        }
+        if (MODE == 1) {  // this part's counts into the test's global table
+            for (int c = tid; c < cells; c += BS)
+                if (hist[c]) atomicAdd(&A.tab[it * A.tstride + c], hist[c]);
+            __syncthreads();  // LDS reused by the next work item
+            continue;
         }
         if (A.counts && (A.cstride > 0 || it == 0))
             for (int c = tid; c < cells; c += BS) A.counts[it * A.cstride + c] = hist[c];
@@ -468,10 +489,35 @@ extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, co
                                     uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
                                     int32_t *gscratch, unsigned long long *stats, const uint32_t *bits,
                                     const int32_t *row0, long long W, const double *band, int nband,
-                                    const uint32_t *pk, long long PW, long long cstride, hipStream_t stream) {
+                                    const uint32_t *pk, long long PW, long long cstride, int32_t *tab,
+                                    long long tstride, int split, int split_grid, hipStream_t stream) {
     CiArgs a{cols, dims, items, N, n, alpha, g2, df, p, indep, counts, gscratch, (long long)(lds_bytes / 4 + 1) & ~1ll,
-             stats, bits, row0, W, band, nband, pk, PW, cstride};
+             stats, bits, row0, W, band, nband, pk, PW, cstride, tab, tstride, split};
     if (gscratch) lds_bytes = 0;
+    if (split > 1 && pk && !bits && !gscratch) {  // small batch: count in parts, then decide
+        hipError_t e = hipMemsetAsync(tab, 0, (size_t)n * tstride * 4, stream);
+        if (e != hipSuccess) return e;
+        switch (d) {
+#define FBN_CI_SPLIT(DD)                                                                                      \
+    case DD:                                                                                                  \
+        hipLaunchKernelGGL((ci_g2_kernel<DD, false, true, 256, 1>), dim3(split_grid), dim3(256), lds_bytes, stream, a); \
+        hipLaunchKernelGGL((ci_g2_kernel<DD, false, true, 1024, 2>), dim3(grid), dim3(1024), lds_bytes, stream, a); \
+        break;
+            FBN_CI_SPLIT(0)
+            FBN_CI_SPLIT(1)
+            FBN_CI_SPLIT(2)
+            FBN_CI_SPLIT(3)
+            FBN_CI_SPLIT(4)
+            FBN_CI_SPLIT(5)
+            FBN_CI_SPLIT(6)
+            FBN_CI_SPLIT(7)
+            FBN_CI_SPLIT(8)
+#undef FBN_CI_SPLIT
+        default:
+            return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     // batches of at most kWideTests tests (deep PC levels: a few hundred tests or fewer, one
     // workgroup per test on part of the chip): 16 waves per test instead of 4, so each test's
     // sample loop and epilogue have 4x the waves to hide latency (FBN_CI_NO_WIDE: always 4)

@@ -209,7 +209,10 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
         std::vector<int32_t> dfv;
         CiBatchStats stats;
     };
-    const int nh = (full || open_edges < EnvOr("FBN_PC_PIPELINE_EDGES", kPipelineEdges)) ? 1 : 2;
+    // (a single-round level of many candidate sets -- config-5 level 2, 8.7k -- also splits in two:
+    // the second half is generated on the host while the first half's batch runs)
+    const int nh = full ? (chunk >= EnvOr("FBN_PC_PIPELINE_FULL", (int64_t)4096) ? 2 : 1)
+                        : (open_edges < EnvOr("FBN_PC_PIPELINE_EDGES", kPipelineEdges) ? 1 : 2);
     Half H[2];
     for (int h = 0; h < nh; ++h) H[h].e0 = E * h / nh, H[h].e1 = E * (h + 1) / nh, H[h].chunk = chunk;
     if (nh == 2) {  // cut where the candidate-set counts of the open edges reach half
@@ -512,16 +515,18 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
         int rc = RunLevel(ctx, alpha, d, group_size, adj, edges, 0, edges.size(), out, res);
         if (rc) return rc;
         auto tb = std::chrono::steady_clock::now();
+        // (recording a level's sepsets on a worker thread while the next level runs measured slower:
+        // config 5 4.3 -> 4.5 ms of driver time, the orientation then reads a map built on another core)
         if (d == 0) res.sepset.set_level0(n, out.removed.data());  // edges = the complete graph
         else res.sepset.append_level(edges.data(), out.removed.data(), out.sep.data(), edges.size(), d);
         res.tests_per_level.push_back(out.counted);
         res.launched_per_level.push_back(out.launched);
-        auto tc = std::chrono::steady_clock::now();
         ApplyRemovals(out.removed, edges, adj);
+        auto tc = std::chrono::steady_clock::now();
         if (d == 0 && pairs) CiSetPairMode(ctx, 2);
         auto td = std::chrono::steady_clock::now();
         if (timing)
-            fprintf(stderr, "pc level %d: run %.2f ms (kernels %.2f), sepsets %.2f ms, removals %.2f ms\n", d,
+            fprintf(stderr, "pc level %d: run %.2f ms (kernels %.2f), sepsets + removals %.2f ms, %.2f ms\n", d,
                     std::chrono::duration<double, std::milli>(tb - ta).count(), (res.kernel_s - k0) * 1e3,
                     std::chrono::duration<double, std::milli>(tc - tb).count(),
                     std::chrono::duration<double, std::milli>(td - tc).count());

@@ -2,13 +2,8 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 o=gpurun_out/r03s2; mkdir -p $o
-timeout -k 10 400 python -u -m pytest tests/test_gpu_pc_small.py tests/test_gpu_pc.py -x -q --timeout 120 --timeout-method thread > $o/pcs_t.log 2>&1 || { tail -40 $o/pcs_t.log; exit 1; }
-tail -2 $o/pcs_t.log
-FBN_PC_SMALL_TRACE=1 timeout -k 10 200 python -u tools/pc_small_timing.py 3 > $o/pcsmall.log 2>&1 || { tail -30 $o/pcsmall.log; exit 1; }
-tail -14 $o/pcsmall.log | grep -v "^orient\|^pc_stable\|^pc device"
-timeout -k 10 200 python -u tools/pc_small_timing.py 200 > $o/pcsmall2.log 2>&1 || { tail -30 $o/pcsmall2.log; exit 1; }
-tail -1 $o/pcsmall2.log
-timeout -k 10 400 python -u -m pytest tests/test_gpu_pc_c5_pinned.py -x -q --timeout 200 --timeout-method thread > $o/c5_t.log 2>&1 || { tail -40 $o/c5_t.log; exit 1; }
-tail -2 $o/c5_t.log
-FBN_PC_TIMING=1 timeout -k 10 300 python -u tools/pc5_timing.py 3 > $o/pc5t.log 2>&1 || { tail -20 $o/pc5t.log; exit 1; }
-grep "^run\|pc level" $o/pc5t.log | tail -8
+for cfg in "A FBN_PC_SYNC_SEPSETS=1 FBN_PC_PIPELINE_FULL=100000000" "B FBN_PC_PIPELINE_FULL=100000000" "C FBN_PC_SYNC_SEPSETS=1" "D X=1" "A2 FBN_PC_SYNC_SEPSETS=1 FBN_PC_PIPELINE_FULL=100000000"; do
+  set -- $cfg; name=$1; shift
+  env "$@" timeout -k 10 300 python -u tools/pc5_timing.py 20 > $o/ab_$name.log 2>&1 || { tail -20 $o/ab_$name.log; exit 1; }
+  echo "$name $*: $(grep '^run' $o/ab_$name.log | tail -10 | awk '{print $4}' | sort -n | head -5 | tr '\n' ' ') | driver $(grep '^run' $o/ab_$name.log | tail -10 | awk '{print $7}' | sort -n | head -3 | tr '\n' ' ')"
+done
