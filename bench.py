@@ -86,6 +86,7 @@ def _jt_sweep(xml, tree_set, ev_path, cases_at, hi):
     """ref_dump jtbench at every thread count of the sweep -> (best, per-thread list)."""
     sweep = []
     for t in hi["sweep"]:
+        log(f"bench: reference JT baseline, {t} threads")
         n = cases_at(t)
         out = subprocess.run([REF_DUMP, "jtbench", xml, tree_set, ev_path, str(n), str(t)], check=True,
                              capture_output=True, text=True, env=_ref_env(t)).stdout.split()
@@ -146,6 +147,7 @@ def _pc_sweep(src, depth, reps, hi):
     medians of the end-to-end step-1 time and of the time inside the CI rounds."""
     sweep = []
     for t in hi["sweep"]:
+        log(f"bench: reference PC baseline ({os.path.basename(src)}), {t} threads")
         runs = []
         for _ in range(reps):
             out = subprocess.run([REF_DUMP, "pcbench", src, "0.05", str(depth), "1", str(t)], check=True,
@@ -727,6 +729,7 @@ def main():
     if rank == 0 and world == 1:
         # PCIe-inclusive rate (host evidence in, host labels + marginals out through fbn_jt_run):
         # reported beside the metric, never as `value`
+        log("bench: PCIe-inclusive JT rate")
         t_host = []
         for _ in range(3):
             t0 = time.perf_counter()
@@ -736,14 +739,19 @@ def main():
                                  "note": "fbn_jt_run from host buffers: evidence H2D, kernel, labels + "
                                          f"{info['sum_dom']} marginals per case D2H"}
         if not args.no_pc:
+            log("bench: PC-stable ALARM-5000")
             out["pc_stable"] = bench_pc(max(50, args.steps), args.warmup)  # 0.3 ms per call: 50 calls for a stable median
         if not args.no_munin:
+            log("bench: Munin-like JT")
             out["munin_like"] = bench_munin(3, 1, with_baseline=not args.no_baseline)
         if not args.no_pc:
+            log("bench: PC-stable config 5")
             out["pc_synthetic"] = bench_pc_synth(5, with_baseline=not args.no_baseline)
         if not args.no_loaders:
+            log("bench: loaders")
             out["loaders"] = bench_loaders()
         if not args.no_baseline:
+            log("bench: reference JT baseline (ALARM)")
             out["cpu_baseline"] = cpu_baseline_jt()
             if "pc_stable" in out:
                 out["pc_stable"]["cpu_baseline"] = cpu_baseline_pc_alarm()
