@@ -60,7 +60,7 @@ extern "C" hipError_t fbn_ci_onehot_build(const uint8_t *cols, const int32_t *di
 extern "C" size_t fbn_ci_l1_edge_bytes(void);
 extern "C" hipError_t fbn_ci_l1_setup(const int32_t *pairs, int E, const int32_t *adj, const int32_t *adj_off,
                                       void *ed, int32_t *pos, uint8_t *st, int32_t *sep, long long *counted,
-                                      hipStream_t s);
+                                      int chunk0, int32_t *len, unsigned *ring, hipStream_t s);
 extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims, const int32_t *row0, long long W,
                                       const int32_t *adj, const int32_t *pairtab, int nvars, void *edv, int32_t *pos,
                                       uint8_t *st, int32_t *sep, long long *counted, int32_t *len, int32_t *off,
@@ -68,7 +68,7 @@ extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims,
                                       int32_t *items, int32_t *counts, int32_t *df, uint8_t *indep, double alpha,
                                       unsigned long long *stats, const double *band, int nband, unsigned *open_cnt,
                                       unsigned long long *rows_read, void *scan_tmp, size_t scan_tmp_bytes,
-                                      int num_cu, hipStream_t s);
+                                      int num_cu, unsigned *open_next, int next_chunk, hipStream_t s);
 extern "C" size_t fbn_ci_l1_scan_bytes(int E);
 extern "C" hipError_t fbn_ci_gram(const uint32_t *bits, long long W, const int32_t *rl, const int32_t *tasks,
                                   long long ntasks, int masked, int32_t *out, int num_cu, hipStream_t s);
@@ -2195,10 +2195,6 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
     CiSlot &S = c->slot[0];
     if (c->timing) FBN_HIP(hipEventRecord(S.ev0, s));
-    hipError_t e = fbn_ci_l1_setup(c->l1pairs.as<int32_t>(), E, c->l1adj.as<int32_t>(), c->l1adjoff.as<int32_t>(),
-                                   c->l1ed.p, c->l1pos.as<int32_t>(), c->l1st.as<uint8_t>(), c->l1sep.as<int32_t>(),
-                                   c->l1cnt.as<long long>(), s);
-    if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci level-1 setup: %s", hipGetErrorString(e));
     long long *scal = c->l1scal.as<long long>();  // total, launched, rows read
     int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(32, EnvOr0("FBN_PC_ROUND0", 8192) / E));
     // chunk x2 per round: rounds here cost a few launches, speculation costs counted tests (config 5:
@@ -2206,9 +2202,16 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
     const int64_t growth = std::max<int64_t>(2, EnvOr0("FBN_PC_GROWTH", 2));
     const int64_t max_chunk = std::max<int64_t>(1, std::min<int64_t>(1 << 16, (int64_t)INT32_MAX / E));
     chunk = std::min(chunk, max_chunk);
+    // the setup writes round 0's lengths and zeroes the open-count ring; each round's resolve writes
+    // the next round's lengths and zeroes the other ring slot (no length kernel or memset per round)
+    hipError_t e = fbn_ci_l1_setup(c->l1pairs.as<int32_t>(), E, c->l1adj.as<int32_t>(), c->l1adjoff.as<int32_t>(),
+                                   c->l1ed.p, c->l1pos.as<int32_t>(), c->l1st.as<uint8_t>(), c->l1sep.as<int32_t>(),
+                                   c->l1cnt.as<long long>(), (int)chunk, c->l1len.as<int32_t>(),
+                                   c->l1open.as<unsigned>(), s);
+    if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci level-1 setup: %s", hipGetErrorString(e));
     for (int r = 0;; ++r) {
         unsigned *open_r = c->l1open.as<unsigned>() + (r & 1);
-        FBN_HIP(hipMemsetAsync(open_r, 0, 4, s));
+        const int64_t next_chunk = std::min<int64_t>(chunk * growth, max_chunk);
         e = fbn_ci_l1_round(c->bits.as<uint32_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(), c->bits_W,
                             c->l1adj.as<int32_t>(), c->pairtab.as<int32_t>(), nv, c->l1ed.p, c->l1pos.as<int32_t>(),
                             c->l1st.as<uint8_t>(), c->l1sep.as<int32_t>(), c->l1cnt.as<long long>(),
@@ -2216,7 +2219,8 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
                             c->l1items.as<int32_t>(), c->l1counts.as<int32_t>(), c->l1df.as<int32_t>(),
                             c->l1indep.as<uint8_t>(), alpha, c->stats.as<unsigned long long>(), band, nband,
                             open_r, reinterpret_cast<unsigned long long *>(scal + 2),
-                            c->l1tmp.p, scan_bytes, c->num_cu, s);
+                            c->l1tmp.p, scan_bytes, c->num_cu, c->l1open.as<unsigned>() + ((r + 1) & 1),
+                            (int)next_chunk, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci level-1 round: %s", hipGetErrorString(e));
         FBN_HIP(hipMemcpyAsync(c->h_open + (r & 1), open_r, 4, hipMemcpyDeviceToHost, s));
         FBN_HIP(hipEventRecord(c->l1ev[r & 1], s));
@@ -2224,7 +2228,7 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
             FBN_HIP(EventWaitSpin(c->l1ev[(r - 1) & 1]));
             if (c->h_open[(r - 1) & 1] == 0) break;  // round r found nothing to do
         }
-        chunk = std::min<int64_t>(chunk * growth, max_chunk);
+        chunk = next_chunk;
     }
     if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
     // read-back through one pinned staging buffer (DMA, no pageable staging copies):

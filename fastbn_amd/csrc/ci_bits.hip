@@ -1035,11 +1035,14 @@ struct L1Edge {
     int32_t x, y, m0, L, skx, sky, ax, ay;  // ax / ay: adjacency offsets, skx / sky: position of y / x
 };
 
+// (also the first round's lengths, chunk0 candidates per edge, and both open-count ring slots zeroed)
 __global__ __launch_bounds__(256) void ci_l1_setup(const int32_t *__restrict__ pairs, int E,
                                                    const int32_t *__restrict__ adj,
                                                    const int32_t *__restrict__ adj_off, L1Edge *__restrict__ ed,
                                                    int32_t *__restrict__ pos, uint8_t *__restrict__ st,
-                                                   int32_t *__restrict__ sep, long long *__restrict__ counted) {
+                                                   int32_t *__restrict__ sep, long long *__restrict__ counted,
+                                                   int chunk0, int32_t *__restrict__ len, unsigned *__restrict__ ring) {
+    if (blockIdx.x == 0 && threadIdx.x < 2) ring[threadIdx.x] = 0u;
     for (int e = blockIdx.x * 256 + threadIdx.x; e < E; e += gridDim.x * 256) {
         const int x = pairs[2 * e], y = pairs[2 * e + 1];
         const int ax = adj_off[x], nx = adj_off[x + 1] - ax, ay = adj_off[y], ny = adj_off[y + 1] - ay;
@@ -1051,6 +1054,7 @@ __global__ __launch_bounds__(256) void ci_l1_setup(const int32_t *__restrict__ p
         st[e] = m0 + m1 == 0 ? 2 : 0;  // no candidate on either side: kept
         sep[e] = -1;
         counted[e] = 0;
+        len[e] = m0 + m1 == 0 ? 0 : (m0 + m1 < chunk0 ? m0 + m1 : chunk0);
     }
 }
 
@@ -1122,7 +1126,10 @@ __global__ __launch_bounds__(256) void ci_l1_resolve(const L1Edge *__restrict__ 
                                                      int32_t *__restrict__ sep, long long *__restrict__ counted,
                                                      const uint8_t *__restrict__ indep,
                                                      const int32_t *__restrict__ items, int E,
-                                                     unsigned *__restrict__ open_cnt) {
+                                                     unsigned *__restrict__ open_cnt, unsigned *__restrict__ open_next,
+                                                     int next_chunk, int32_t *__restrict__ len_next) {
+    // the next round's open-count slot (its previous value went to the host before this round)
+    if (blockIdx.x == 0 && threadIdx.x == 0) *open_next = 0u;
     for (int e0 = blockIdx.x * 256 + (threadIdx.x & ~63); e0 < E; e0 += gridDim.x * 256) {
         const int e = e0 + (threadIdx.x & 63);
         bool open = false;
@@ -1144,6 +1151,11 @@ __global__ __launch_bounds__(256) void ci_l1_resolve(const L1Edge *__restrict__ 
                 if (pos[e] >= ed[e].L) st[e] = 2;
                 else open = true;
             }
+        }
+        // the next round's length of this edge (what ci_l1_len computed as a kernel of its own)
+        if (e < E) {
+            const int left = ed[e].L - pos[e];
+            len_next[e] = open ? (left < next_chunk ? left : next_chunk) : 0;
         }
         const unsigned nopen = (unsigned)__popcll(__ballot(open));  // one atomic per wave
         if ((threadIdx.x & 63) == 0 && nopen) atomicAdd(open_cnt, nopen);
@@ -1230,15 +1242,16 @@ extern "C" size_t fbn_ci_l1_scan_bytes(int E) {
 
 extern "C" hipError_t fbn_ci_l1_setup(const int32_t *pairs, int E, const int32_t *adj, const int32_t *adj_off,
                                       void *ed, int32_t *pos, uint8_t *st, int32_t *sep, long long *counted,
-                                      hipStream_t s) {
+                                      int chunk0, int32_t *len, unsigned *ring, hipStream_t s) {
     if (E > 0)
         hipLaunchKernelGGL(ci_l1_setup, dim3((E + 255) / 256), dim3(256), 0, s, pairs, E, adj, adj_off,
-                           (L1Edge *)ed, pos, st, sep, counted);
+                           (L1Edge *)ed, pos, st, sep, counted, chunk0, len, ring);
     return hipGetLastError();
 }
 
-// one round: lengths, scan, generation, counting, G^2 / decisions, resolution; `total` = the
-// round's test count (device), `open_cnt` += edges still open after it
+// one round: scan of the lengths (from ci_l1_setup or the previous round's resolve), clip,
+// generation, counting, G^2 / decisions, resolution (+ the next round's lengths for next_chunk);
+// `total` = the round's test count (device), `open_cnt` += edges still open after it, *open_next = 0
 extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims, const int32_t *row0, long long W,
                                       const int32_t *adj, const int32_t *pairtab, int nvars, void *edv, int32_t *pos,
                                       uint8_t *st, int32_t *sep, long long *counted, int32_t *len, int32_t *off,
@@ -1246,7 +1259,7 @@ extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims,
                                       int32_t *items, int32_t *counts, int32_t *df, uint8_t *indep, double alpha,
                                       unsigned long long *stats, const double *band, int nband, unsigned *open_cnt,
                                       unsigned long long *rows_read, void *scan_tmp, size_t scan_tmp_bytes,
-                                      int num_cu, hipStream_t s) {
+                                      int num_cu, unsigned *open_next, int next_chunk, hipStream_t s) {
     const L1Edge *ed = (const L1Edge *)edv;
     const long long ge = ((long long)E + 255) / 256, gcap = (long long)num_cu * 8;
     const dim3 gE((unsigned)(ge < gcap ? ge : gcap));
@@ -1254,7 +1267,7 @@ extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims,
     const dim3 gT((unsigned)(gt < gcap ? gt : gcap));
     const long long gw = (cap + 3) / 4;
     const dim3 gW((unsigned)(gw < gcap ? gw : gcap));
-    hipLaunchKernelGGL(ci_l1_len, gE, dim3(256), 0, s, ed, pos, st, E, chunk, len);
+    (void)chunk;  // (this round's lengths came from ci_l1_setup or the previous round's resolve)
     size_t tmp_bytes = scan_tmp_bytes;
     hipError_t e = hipcub::DeviceScan::ExclusiveSum(scan_tmp, tmp_bytes, len, off, E, s);
     if (e != hipSuccess) return e;
@@ -1267,7 +1280,8 @@ extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims,
                        alpha, (double *)nullptr, df, (double *)nullptr, indep, (int32_t *)nullptr, stats, nvars, 0ll,
                        band, nband, (const long long *)total);
     hipLaunchKernelGGL(ci_l1_resolve, gE, dim3(256), 0, s, ed, pos, (const int32_t *)len, (const int32_t *)off, st,
-                       sep, counted, (const uint8_t *)indep, (const int32_t *)items, E, open_cnt);
+                       sep, counted, (const uint8_t *)indep, (const int32_t *)items, E, open_cnt, open_next,
+                       next_chunk, len);
     return hipGetLastError();
 }
 

@@ -2,5 +2,9 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 o=gpurun_out/r03s2; mkdir -p $o
-timeout -k 10 600 python bench.py > $o/bench.json 2> $o/bench.err || { tail -20 $o/bench.err; exit 1; }
-python -c "import json;d=json.load(open('$o/bench.json'));print(d['value'],d['ms_per_step'],d['pc_stable']['ms_per_run'],d['pc_stable']['kernel_ms_per_run'],d['pc_stable']['launched_per_level'],d['pc_synthetic']['ms_per_run'],d['pc_synthetic']['kernel_ms_per_run'],d['munin_like']['kernel_ms'])"
+timeout -k 10 400 python -u -m pytest tests/test_gpu_pc_small.py tests/test_gpu_pc.py -x -q --timeout 120 --timeout-method thread > $o/pcs_t.log 2>&1 || { tail -40 $o/pcs_t.log; exit 1; }
+tail -2 $o/pcs_t.log
+FBN_PC_SMALL_TRACE=1 timeout -k 10 200 python -u tools/pc_small_timing.py 3 > $o/pcsmall.log 2>&1 || { tail -30 $o/pcsmall.log; exit 1; }
+grep "pc small level" $o/pcsmall.log | tail -5
+timeout -k 10 200 python -u tools/pc_small_timing.py 200 > $o/pcsmall2.log 2>&1 || { tail -30 $o/pcsmall2.log; exit 1; }
+tail -1 $o/pcsmall2.log
