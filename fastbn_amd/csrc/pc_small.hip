@@ -803,8 +803,15 @@ __device__ void finalize(const PcSmallArgs &A, Lds &L, int nb, int levels, int h
     if (tid == 0) __hip_atomic_store(&A.out->done, A.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs A, Barrier B) {
+__global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs Ak, Barrier B) {
     __shared__ Lds L;
+    // the arguments staged in LDS: the out-of-line test functions take them by reference, and a
+    // reference to the kernel parameter made the compiler copy the struct into per-thread scratch
+    // (176 B per thread, ~23 MB of writes per launch, a scratch load per field access)
+    __shared__ PcSmallArgs SA;
+    if (threadIdx.x == 0) SA = Ak;
+    __syncthreads();
+    const PcSmallArgs &A = SA;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n = A.nvars;
     const int nb = gridDim.x;
