@@ -113,14 +113,41 @@ struct Clq {
     uint32_t M32, W32;                                  // this lane's evidence pattern (packed digits)
     uint64_t M[JT_MAX_DIG_WORDS], W[JT_MAX_DIG_WORDS];  // (8-bit digits)
 };
-typedef Den Dens[JT_V_MAX_CHILDREN + 2];
-// D[j] for a wave-uniform runtime j without dynamic register indexing (which would go to scratch)
+// The step denominators D_0 .. D_{k+1} of a clique.  Eight named members, not an array, and the
+// runtime-index accessors (pick / put, wave-uniform j) are bit-mask selects / blends over VALUES: as
+// an array -- or with a switch returning a member, which becomes a select of member addresses -- the
+// compiler turned them into a dynamically indexed load and kept the whole set in per-thread scratch
+// (144 B per lane, stored every clique, reloaded on every pick).  Accesses whose index is known after
+// unrolling (operator[] in the entry loops) fold to one member.
+struct Dens {
+    Den a0, a1, a2, a3, a4, a5, a6, a7;
+    __device__ __forceinline__ Den operator[](int j) const;
+};
+static_assert(JT_V_MAX_CHILDREN + 2 == 8, "Dens holds 8 denominators");
+__device__ __forceinline__ unsigned long long dbits(double x) { return __builtin_bit_cast(unsigned long long, x); }
+__device__ __forceinline__ double dfrom(unsigned long long b) { return __builtin_bit_cast(double, b); }
 __device__ __forceinline__ Den pick(const Dens &D, int j) {
-    Den r = D[0];
-#pragma unroll
-    for (int i = 1; i < JT_V_MAX_CHILDREN + 2; ++i)
-        if (i == j) r = D[i];
-    return r;
+    unsigned long long rd = 0ull, ry = 0ull;
+#define FBN_PK(i)                                                             \
+    {                                                                         \
+        const unsigned long long m = 0ull - (unsigned long long)(j == i);    \
+        rd |= dbits(D.a##i.den) & m;                                          \
+        ry |= dbits(D.a##i.y) & m;                                            \
+    }
+    FBN_PK(0) FBN_PK(1) FBN_PK(2) FBN_PK(3) FBN_PK(4) FBN_PK(5) FBN_PK(6) FBN_PK(7)
+#undef FBN_PK
+    return Den{dfrom(rd), dfrom(ry)};
+}
+__device__ __forceinline__ Den Dens::operator[](int j) const { return pick(*this, j); }
+__device__ __forceinline__ void put(Dens &D, int j, const Den &v) {
+#define FBN_PT(i)                                                                         \
+    {                                                                                     \
+        const unsigned long long m = 0ull - (unsigned long long)(j == i);                \
+        D.a##i.den = dfrom((dbits(D.a##i.den) & ~m) | (dbits(v.den) & m));                \
+        D.a##i.y = dfrom((dbits(D.a##i.y) & ~m) | (dbits(v.y) & m));                      \
+    }
+    FBN_PT(0) FBN_PT(1) FBN_PT(2) FBN_PT(3) FBN_PT(4) FBN_PT(5) FBN_PT(6) FBN_PT(7)
+#undef FBN_PT
 }
 
 // entry e of the clique after L message multiplies (divided by D_L when FINAL), 0 if the entry
@@ -486,7 +513,7 @@ void jt_virt_kernel(
             const bool p32 = q.nw == 0;
             Dens D;
 #pragma unroll
-            for (int j = 0; j < JT_V_MAX_CHILDREN + 2; ++j) D[j] = Den{1.0, 1.0};
+            for (int j = 0; j < JT_V_MAX_CHILDREN + 2; ++j) put(D, j, Den{1.0, 1.0});
             // the last normalization pass of a clique with children also stores the table for SEPCOL
             // (exact mode; fast mode recomputes the SEPCOL entries with its one-pass denominators)
             const bool cmat = q.cmat && !(dbg & 32);
@@ -509,7 +536,7 @@ void jt_virt_kernel(
                     // a product chain that leaves the normal range: the block goes to the exact pass
                     bad |= !den_ok(s) || !(P[L] >= 0x1p-960 && P[L] <= 0x1p+960);
                     S.st_row(q.den_row + L, s);
-                    D[L] = Den{s, 1.0 / s};
+                    put(D, L, Den{s, 1.0 / s});
                     prod *= s;
                 }
             }
@@ -528,9 +555,7 @@ void jt_virt_kernel(
                 S.st_row(q.den_row + L, s);
                 // D is indexed by the uniform L: write every slot under a uniform compare so the
                 // array stays in registers
-#pragma unroll
-                for (int j = 0; j < JT_V_MAX_CHILDREN + 2; ++j)
-                    if (j == L) D[j] = Den{s, 1.0 / s};
+                put(D, L, Den{s, 1.0 / s});
             }
             if (!q.root && !(dbg & 1)) {
                 const int Ts = q.up_Ts, per = q.T / Ts, dst = q.up_col_row;
@@ -569,11 +594,12 @@ void jt_virt_kernel(
             Dens D;
 #pragma unroll
             for (int j = 0; j < JT_V_MAX_CHILDREN + 2; ++j) {
-                D[j] = Den{1.0, 1.0};
+                Den v = Den{1.0, 1.0};
                 if (j <= q.k) {
                     const double s = S.row(q.den_row + j);
-                    D[j] = Den{s, 1.0 / s};
+                    v = Den{s, 1.0 / s};
                 }
+                put(D, j, v);
             }
             // marginals of the variables whose chosen clique (for this case) is this one: up to
             // kFuseVars of them (kFuseBins values in total) in one fused sweep, the rest one pass each
@@ -631,9 +657,7 @@ void jt_virt_kernel(
                 }
                 bad |= !den_ok(s);
                 Lf = q.k + 1;
-#pragma unroll
-                for (int j = 0; j < JT_V_MAX_CHILDREN + 2; ++j)
-                    if (j == Lf) D[j] = Den{s, 1.0 / s};
+                put(D, Lf, Den{s, 1.0 / s});
             }
             // messages to the children
             for (int ci = 0; ci < ((dbg & 2) ? 0 : q.k); ++ci) {
