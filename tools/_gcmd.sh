@@ -2,9 +2,9 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 o=gpurun_out/r03s2; mkdir -p $o
-timeout -k 10 600 python -u -m pytest tests/test_gpu_jt.py tests/test_gpu_jt_case.py -x -q --timeout 200 --timeout-method thread > $o/jt_t.log 2>&1 || { tail -40 $o/jt_t.log; exit 1; }
-tail -2 $o/jt_t.log
-timeout -k 10 400 python -u tools/case_probe.py 125000 4 > $o/probe.log 2>&1 || { tail -20 $o/probe.log; exit 1; }
-cat $o/probe.log | grep variant
-timeout -k 10 600 python -u tools/jt_budget_sweep.py "200:96,190:96,180:96,160:96,200:88,200:104" > $o/budget.log 2>&1 || { tail -20 $o/budget.log; exit 1; }
-grep budget $o/budget.log
+timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $o/t.log 2>&1 || { tail -30 $o/t.log; exit 1; }
+tail -1 $o/t.log
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1 || { echo smoke failed; tail -20 $o/smoke.log; exit 1; }
+tail -1 $o/smoke.log
+timeout -k 10 700 python bench.py > $o/bench.json 2> $o/bench.err || { tail -20 $o/bench.err; exit 1; }
+python -c "import json;d=json.load(open('$o/bench.json'));print(d['value'],d['ms_per_step'],d['pc_stable']['ms_per_run'],d['pc_stable']['kernel_ms_per_run'],d['pc_synthetic']['ms_per_run'],d['pc_synthetic']['kernel_ms_per_run'],d['munin_like']['kernel_ms'])"
