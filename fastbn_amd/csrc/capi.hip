@@ -2471,6 +2471,8 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
     a.band = band;
     a.nband = nband;
     a.depth = depth;
+    static const int spec_a = getenv("FBN_PC_SPEC_A") ? std::max(1, atoi(getenv("FBN_PC_SPEC_A"))) : 8;  // (tuning)
+    a.spec_a = spec_a;
     a.bar = reinterpret_cast<unsigned *>(scr);
     a.first = reinterpret_cast<unsigned long long *>(scr + (size_t)kSmallBarWords * 4);
     a.epoch = c->small_epoch;

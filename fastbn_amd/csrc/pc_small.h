@@ -60,6 +60,7 @@ struct PcSmallArgs {
     const double *band;      // decision band [lo, hi] per df 1..nband, then delta (or nullptr)
     int nband;
     int depth;               // levels 0 .. depth - 1 at most
+    int spec_a;              // levels 1-2: candidate sets per edge in part A (default 8, FBN_PC_SPEC_A)
     // scratch: bar and first zeroed once at allocation (kSmallZeroBytes from its start)
     unsigned *bar;           // grid barrier arrivals (kSmallBarWords), counting phases across launches
     unsigned long long *first;  // [kSmallMaxLevels][kSmallMaxEdges] (epoch << 32) | ~(first independent

@@ -51,12 +51,12 @@ constexpr long long kSpinTicks = 200000000ll;  // wall_clock64 ticks (100 MHz): 
 typedef __attribute__((ext_vector_type(4))) unsigned u4;
 
 constexpr int kWaveHist = 2048;    // per-wave region of the one-wave histogram tests (d = 2, 3)
-// One-wave levels (1, 2) run in two parts: A = the first kSpecA candidate sets of every edge
+// One-wave levels (1, 2) run in two parts: A = the first spec_a candidate sets of every edge
 // (about one round of the grid's waves on ALARM-5000), then B = the rest, edge-major.  A part-B test
 // first checks whether its edge already has an independent set at a lower index (published by
 // every independent test as it happens, not at the end of the level) and is skipped if so: it
 // could never be the edge's first.  Counts, removals and sepsets are those of full speculation.
-constexpr int kSpecA = 8;
+// (part-A width: PcSmallArgs::spec_a, 8 candidate sets per edge by default)
 
 struct Lds {
     // per-run constants staged once: state counts, first mask row and per-row sample counts of
@@ -65,7 +65,7 @@ struct Lds {
     double band[2 * 256 + 1];
     uint64_t adj[kSmallMaxVars];
     int32_t rowoff[kSmallMaxVars + 1];     // edges of rows before x
-    int32_t eoff[kSmallMaxEdges + 1];      // part A: first test of each edge (its first kSpecA candidates)
+    int32_t eoff[kSmallMaxEdges + 1];      // part A: first test of each edge (its first spec_a candidates)
     int32_t eoffB[kSmallMaxEdges + 1];     // part B: first test of each edge's remaining candidates
     int32_t TA;                            // tests in part A
     int32_t next;                          // one-wave levels: this workgroup's next test (dynamic)
@@ -876,7 +876,7 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs Ak, Barrier B)
                 const int x = L.ex[e], y = L.ey[e];
                 return d == 0 ? 1 : binom_l(L, popc64(L.adj[x]) - 1, d) + binom_l(L, popc64(L.adj[y]) - 1, d);
             };
-            const int KA = (d == 1 || d == 2) ? kSpecA : 0x40000000;  // part A per edge
+            const int KA = (d == 1 || d == 2) ? A.spec_a : 0x40000000;  // part A per edge
             long long mine = 0, mineA = 0;  // (int64: a level's total may exceed 2^31 -> hand-off below)
             for (int e = e0; e < e1; ++e) {
                 const int nt = ntests(e);
@@ -918,7 +918,7 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs Ak, Barrier B)
             // dynamically, so part-B skips do not leave some waves with more tests than others
             const int b0 = nb - 1 - bid;
             const int TA = L.TA;
-            // test t -> (edge, candidate index): part A, then part B (see kSpecA)
+            // test t -> (edge, candidate index): part A, then part B (see spec_a)
             auto locate = [&](int t, int &e, int &k) {
                 const bool b = t >= TA;
                 const int32_t *off = b ? L.eoffB : L.eoff;
@@ -930,7 +930,7 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs Ak, Barrier B)
                     else hi = mid;
                 }
                 e = lo;
-                k = tt - off[lo] + (b ? kSpecA : 0);
+                k = tt - off[lo] + (b ? A.spec_a : 0);
             };
             while (true) {
                 int j = 0;
