@@ -65,13 +65,9 @@ class SepsetMap {
     bool find(std::pair<int, int> key, View *v) const {
         // a pair removed at level 0 is never tested again, so its flag is its only entry: checked
         // first (most absent skeleton pairs of a PC run were removed at level 0)
-        {
-            const int i = key.first, j = key.second;
-            if (!l0_.empty() && 0 <= i && i < j && j < n0_ &&
-                l0_[(size_t)i * n0_ - (size_t)i * (i + 1) / 2 + (size_t)(j - i - 1)]) {
-                *v = View{pool_.data(), 0};
-                return true;
-            }
+        if (l0_hit(key)) {
+            *v = View{pool_.data(), 0};
+            return true;
         }
         size_t end = e_.size();
         for (size_t r = runs_.size() + 1; r-- > 0;) {
@@ -85,6 +81,45 @@ class SepsetMap {
             end = begin;
         }
         return false;
+    }
+    // n lookups at once, answers as find() (found[i] = 0/1, v[i]): the keys are sorted and resolved
+    // run by run, each search galloping forward from where the previous one ended, so it touches
+    // the entries near the last hit instead of a cold binary search over the whole run
+    // (orientation's v-structure pass: ~1.7k lookups on a 1000-variable run)
+    void find_many(const std::pair<int, int> *keys, size_t n, View *v, char *found) const {
+        std::vector<uint32_t> open(n);
+        for (size_t i = 0; i < n; ++i) open[i] = (uint32_t)i;
+        std::sort(open.begin(), open.end(), [&](uint32_t a, uint32_t b) { return keys[a] < keys[b]; });
+        size_t k = 0;
+        for (uint32_t q : open) {
+            found[q] = l0_hit(keys[q]);
+            if (found[q]) v[q] = View{pool_.data(), 0};
+            else open[k++] = q;
+        }
+        open.resize(k);
+        size_t end = e_.size();
+        for (size_t r = runs_.size() + 1; r-- > 0 && !open.empty();) {  // last run first, as find()
+            const size_t begin = r ? runs_[r - 1] : 0;
+            size_t p = begin;
+            k = 0;
+            for (uint32_t q : open) {
+                // gallop from the previous position, then binary search the last step's interval
+                size_t lo = p, step = 1;
+                while (lo + step < end && e_[lo + step].key < keys[q]) lo += step, step <<= 1;
+                const size_t hi = std::min(end, lo + step + 1);
+                auto it = std::lower_bound(e_.begin() + lo, e_.begin() + hi, keys[q],
+                                           [](const Ent &a, const std::pair<int, int> &key) { return a.key < key; });
+                p = (size_t)(it - e_.begin());
+                if (it != e_.begin() + end && it->key == keys[q]) {
+                    v[q] = View{pool_.data() + it->off, it->len};
+                    found[q] = 1;
+                } else {
+                    open[k++] = q;
+                }
+            }
+            open.resize(k);
+            end = begin;
+        }
     }
     // iteration in ascending key order: n = sorted_size(), then key(i) / value(i) for i < n (folds
     // the level-0 flags into explicit entries first)
@@ -111,6 +146,11 @@ class SepsetMap {
         int64_t off;
         int len;
     };
+    bool l0_hit(std::pair<int, int> key) const {
+        const int i = key.first, j = key.second;
+        return !l0_.empty() && 0 <= i && i < j && j < n0_ &&
+               l0_[(size_t)i * n0_ - (size_t)i * (i + 1) / 2 + (size_t)(j - i - 1)];
+    }
     void sort() const {
         if (sorted_) return;
         // a key set twice keeps its last value (std::map assignment semantics)

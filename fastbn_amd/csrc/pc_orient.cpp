@@ -341,37 +341,48 @@ struct Orienter {
     bool IsUndirectedFromTo(int a, int b) const {
         return IsAdjacentTo(a, b) && !g.IsDirectedFromTo(a, b) && !g.IsDirectedFromTo(b, a);
     }
-    bool InSepset(int a, int c, int b) const {
-        SepsetMap::View z;
-        if (!sepset.find({a, c}, &z)) return false;
-        return std::find(z.begin(), z.end(), b) != z.end();
-    }
-
     void VStructures() {
+        // the skeleton adjacencies and the sepsets stay fixed while edges are oriented, so which
+        // triples a - b - c are unshielded with b outside sepset(a, c) is known up front: collected
+        // in the reference's visiting order, their sepsets looked up in one batch (find_many), then
+        // the edits applied in that order
+        struct Triple {
+            int a, b, c;
+        };
+        std::vector<Triple> tri;
+        std::vector<std::pair<int, int>> keys;
         for (int b = 0; b < g.n; ++b) {
-            if (adj[b].size() < 2) continue;
-            std::vector<int> nb(adj[b].begin(), adj[b].end());
+            const std::vector<int> &nb = adj[b].v;  // ascending, as the reference's neighbour set
             for (size_t i = 0; i < nb.size(); ++i)
                 for (size_t j = i + 1; j < nb.size(); ++j) {  // ChoiceGenerator(k, 2) order
                     const int a = nb[i], c = nb[j];
-                    if (IsAdjacentTo(a, c) || InSepset(a, c, b)) continue;
-                    const bool dd1 = g.DeleteDirected(b, a);
-                    const bool du1 = dd1 ? false : g.DeleteUndirected(a, b);
-                    const bool add1 = dd1 || du1;
-                    const bool dd2 = g.DeleteDirected(b, c);
-                    const bool du2 = dd2 ? false : g.DeleteUndirected(c, b);
-                    const bool add2 = dd2 || du2;
-                    const bool ok1 = add1 ? g.AddDirected(a, b) : false;
-                    const bool ok2 = add2 ? g.AddDirected(c, b) : false;
-                    if (add1 && !ok1) {
-                        if (dd1) g.AddDirected(b, a);
-                        else g.AddUndirected(a, b);
-                    }
-                    if (add2 && !ok2) {
-                        if (dd2) g.AddDirected(b, c);
-                        else g.AddUndirected(c, b);
-                    }
+                    if (IsAdjacentTo(a, c)) continue;
+                    tri.push_back({a, b, c});
+                    keys.push_back({a, c});
                 }
+        }
+        std::vector<SepsetMap::View> z(tri.size());
+        std::vector<char> found(tri.size());
+        sepset.find_many(keys.data(), keys.size(), z.data(), found.data());
+        for (size_t t = 0; t < tri.size(); ++t) {
+            const int a = tri[t].a, b = tri[t].b, c = tri[t].c;
+            if (found[t] && std::find(z[t].begin(), z[t].end(), b) != z[t].end()) continue;
+            const bool dd1 = g.DeleteDirected(b, a);
+            const bool du1 = dd1 ? false : g.DeleteUndirected(a, b);
+            const bool add1 = dd1 || du1;
+            const bool dd2 = g.DeleteDirected(b, c);
+            const bool du2 = dd2 ? false : g.DeleteUndirected(c, b);
+            const bool add2 = dd2 || du2;
+            const bool ok1 = add1 ? g.AddDirected(a, b) : false;
+            const bool ok2 = add2 ? g.AddDirected(c, b) : false;
+            if (add1 && !ok1) {
+                if (dd1) g.AddDirected(b, a);
+                else g.AddUndirected(a, b);
+            }
+            if (add2 && !ok2) {
+                if (dd2) g.AddDirected(b, c);
+                else g.AddUndirected(c, b);
+            }
         }
     }
     bool Direct(int a, int c) {
