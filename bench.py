@@ -347,12 +347,9 @@ def bench_pc_synth(steps, depth=6, cpu_vars=160, with_baseline=True):
     return out
 
 
-def _pc_dist_timed(load, steps, rank, world, device, depth):
-    """PC-stable through the distributed session on N ranks: rank 0 loads the column store
-    (`load()` -> (cols, dims)) and one RCCL broadcast puts it in every rank's HBM; each level's
-    edges are partitioned over the ranks (fbn_pc_dist_*), one all-gather of the records per level
-    (+ the level-0 pair tables).  Timed on the wall clock between barriers, max over ranks, median
-    of `steps` runs -> (PCResult, tests, launched, ms)."""
+def _pc_broadcast_ctx(load, rank, device):
+    """Rank 0 loads the column store (`load()` -> (cols, dims)) and one RCCL broadcast puts it in
+    every rank's HBM -> (IndependenceTest, collective device or None for gloo, nvars)."""
     import torch
     import torch.distributed as dist
     from fastbn_amd import pc_dist
@@ -369,9 +366,22 @@ def _pc_dist_timed(load, steps, rank, world, device, depth):
         t = pc_dist.broadcast_columns(cols, meta[0]).to(dev)
         torch.cuda.synchronize(dev)
         ci = F.IndependenceTest.from_device(t.data_ptr(), meta[0][0], meta[0][1], dims, 0.05, device)
+        ci._cols_keepalive = t
         coll = None
+    return ci, coll, meta[0][0]
+
+
+def _pc_dist_timed(load, steps, rank, world, device, depth):
+    """PC-stable through the distributed session on N ranks: the column store broadcast once
+    (`_pc_broadcast_ctx`); each level's edges are partitioned over the ranks (fbn_pc_dist_*), one
+    all-gather of the records per level (+ the level-0 pair tables).  Timed on the wall clock
+    between barriers, max over ranks, median of `steps` runs -> (PCResult, tests, launched, ms)."""
+    import torch
+    import torch.distributed as dist
+    from fastbn_amd import pc_dist
+    dev = torch.device("cuda", device)
+    ci, coll, nvars = _pc_broadcast_ctx(load, rank, device)
     ci.set_kernel_timing(False)
-    nvars = meta[0][0]
     res, tests, launched = pc_dist.pc_stable_distributed(ci, nvars, 0.05, depth, device=coll)  # warm-up
     t = []
     for _ in range(steps):
@@ -386,23 +396,54 @@ def _pc_dist_timed(load, steps, rank, world, device, depth):
 
 
 def bench_pc_alarm_dist(steps, rank, world, device):
-    """BASELINE config 3 (alarm_s5000, PC-stable levels 0-4) on N GPUs through the distributed
-    session: the same 5206 tests cut over the ranks per level.  Five dependent levels of a few
-    microseconds of kernels each, so the per-level all-gather latency is what N GPUs add; reported
-    as measured, checked against the single-GPU skeleton facts (5206 tests, 44 edges)."""
+    """BASELINE config 3 (alarm_s5000, PC-stable levels 0-4) on N GPUs.  The graph is small enough
+    for the one-launch device-resident search, so the ranks run REPLICAS: every rank
+    runs the whole search on its own broadcast copy of the column store and one broadcast of rank
+    0's result record reaches every rank (each checks it against its own).  Cutting five dependent
+    levels over N GPUs would add an all-gather per level to a 0.14 ms chain; replicas keep the
+    single-GPU time plus one broadcast.  Timed: the search + record + broadcast, wall clock between
+    barriers, max over ranks, median of runs."""
+    import torch
+    import torch.distributed as dist
+    from fastbn_amd import pc_dist
+
     def load():
         import fastbn_amd as F
         ds = F.Dataset(os.path.join(ALARM, "alarm_s5000.txt"))
         return ds.columns, ds.dims
-    res, tests, launched, ms = _pc_dist_timed(load, steps, rank, world, device, 1000)
+    dev = torch.device("cuda", device)
+    ci, coll, nvars = _pc_broadcast_ctx(load, rank, device)
+    ci.set_kernel_timing(False)
+    if not pc_dist.small_eligible(ci):  # (not ALARM: a larger graph takes the partitioned session)
+        del ci
+        res, tests, launched, ms = _pc_dist_timed(load, steps, rank, world, device, 1000)
+        return {"metric": "PC-stable CI-tests/sec (alarm_s5000, levels 0-4)", "value": sum(tests) / (ms * 1e-3),
+                "unit": "CI-tests/s", "n_gpus": world, "tests": int(sum(tests)), "tests_per_level": tests,
+                "launched_per_level": launched, "ms_per_run": ms, "edges": len(res.edges),
+                "parallelism": f"edge ranges per level x{world}, one all-gather per level"}
+    mode = f"replicas x{world} (one-launch device-resident search per rank) + one broadcast of rank 0's record"
+    for _ in range(3):  # warm-up
+        res, rec0 = pc_dist.pc_stable_replicas(ci, 0.05, 1000, device=coll)
+    t = []
+    for _ in range(steps):
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        res, rec0 = pc_dist.pc_stable_replicas(ci, 0.05, 1000, device=coll, check=False)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t.append(shard.max_over_ranks(time.perf_counter() - t0, dev))
+    res, rec0 = pc_dist.pc_stable_replicas(ci, 0.05, 1000, device=coll, check=True)  # every rank == rank 0
+    ms = 1e3 * float(np.median(t))
+    tests = rec0["tests_per_level"]
     return {"metric": "PC-stable CI-tests/sec (alarm_s5000, levels 0-4)", "value": sum(tests) / (ms * 1e-3),
             "unit": "CI-tests/s", "n_gpus": world, "tests": int(sum(tests)), "tests_per_level": tests,
-            "launched_per_level": launched, "ms_per_run": ms, "edges": len(res.edges),
-            "parallelism": f"edge ranges per level x{world}, one all-gather per level",
+            "launched_per_level": res.launched_per_level.tolist(), "ms_per_run": ms, "edges": len(rec0["edges"]),
+            "parallelism": mode, "scaling": "replicas only (a small graph's search does not shard)",
             "timing": "wall clock between barriers, max over ranks, median of runs",
-            "matches_single_gpu": int(sum(tests)) == 5206 and len(res.edges) == 44,
-            "note": "latency-bound (DESIGN.md 5.3): the per-level all-gathers add to a 0.3 ms chain; "
-                    "N GPUs cannot shorten five dependent levels of ~1k tests each"}
+            "matches_single_gpu": int(sum(tests)) == 5206 and len(rec0["edges"]) == 44,
+            "note": "one launch of five dependent levels (0.14 ms on one GPU): N GPUs cannot shorten it, so "
+                    "each rank runs it and rank 0's result record is broadcast (DESIGN.md 6)"}
 
 
 def bench_pc_synth_dist(steps, rank, world, device, depth=6):
@@ -522,14 +563,22 @@ def bench_munin(steps, warmup, cases=125_000, rank=0, world=1, device=0, with_ba
         rel = float(np.max(np.abs(gm - omarg) / np.maximum(np.abs(omarg), 1e-300)))
         ok = bool((d_lab[:16].cpu().numpy() == olab).all() and rel <= 1e-12)
     ms = []
+    all_lab = None
     if world > 1:
         import torch.distributed as dist
+        nccl = dist.get_backend() == "nccl"
+        all_lab = torch.empty(world * cases, dtype=torch.int32, device=dev if nccl else "cpu")
         dist.barrier()
     torch.cuda.synchronize(dev)
     w0 = time.perf_counter()
     for _ in range(steps):
         jt.run_device(d_ev.data_ptr(), cases, d_lab.data_ptr(), d_marg.data_ptr(), stream)
         ms.append(jt.last_kernel_ms())
+        if all_lab is not None:  # the final gather of every rank's labels (north_star), inside the timing
+            if nccl:
+                dist.all_gather_into_tensor(all_lab, d_lab)
+            else:
+                dist.all_gather(list(all_lab.view(world, cases)), d_lab.cpu())
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -601,6 +650,30 @@ def load_traffic(cases):
     return None if b is None else b * cases / t.get("cases_per_launch", CASES_PER_GPU)
 
 
+def summary(out):
+    """Every workload's headline number in a few hundred bytes (the end of the JSON line)."""
+    def r(x, n=4):
+        return None if x is None else float(f"{x:.{n}g}")
+    sm = {"alarm_jt": {"cases_s": r(out["value"]), "kernel_ms": r(out["roofline"]["kernel_ms"]),
+                       "frac": r(out["roofline"]["frac"], 3)}}
+    pc = out.get("pc_stable")
+    if pc:
+        sm["alarm5000_pc"] = {"ms_call": r(pc["ms_per_run"]), "tests_s": r(pc["value"]),
+                              "frac": r(pc.get("roofline", {}).get("frac"), 3),
+                              "parallelism": "replicas" if "replicas" in pc.get("parallelism", "replicas") else "split"}
+    mu = out.get("munin_like")
+    if mu:
+        tr = mu["roofline"].get("traffic")
+        sm["munin_jt"] = {"cases_s": r(mu["value"]), "kernel_ms": r(mu["kernel_ms"]), "frac": r(mu["roofline"]["frac"], 3),
+                          "traffic_MB_case": r(tr / mu["cases_per_gpu"] / 1e6, 3) if tr else None,
+                          "variant": mu.get("kernel_variant")}
+    c5 = out.get("pc_synthetic")
+    if c5:
+        sm["config5_pc"] = {"ms_run": r(c5["ms_per_run"]), "tests_s": r(c5["value"]),
+                            "frac": r(c5.get("roofline", {}).get("frac"), 3)}
+    return sm
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -658,8 +731,25 @@ def main():
     def step():
         jt.run_device(d_ev.data_ptr(), args.cases, d_lab.data_ptr(), d_marg.data_ptr(), stream.cuda_stream)
 
+    # N > 1: the step ends with north_star's "final gather" -- every rank's labels (4 B per case) to
+    # every rank in one all-gather (RCCL on the device; the gloo rehearsal stages through the host).
+    # Marginals stay on the device; there is no golden table for synthetic cases, so
+    # no MSE / HD sum to reduce.
+    all_lab = torch.empty(world * args.cases, dtype=torch.int32, device=dev) if world > 1 else None
+
+    def gather():
+        if world == 1:
+            return
+        if backend == "nccl":
+            dist.all_gather_into_tensor(all_lab, d_lab)
+        else:
+            parts = [torch.empty(args.cases, dtype=torch.int32) for _ in range(world)]
+            dist.all_gather(parts, d_lab.cpu())
+            all_lab.copy_(torch.cat(parts))
+
     for _ in range(args.warmup):
         step()
+        gather()
     torch.cuda.synchronize(dev)
     ev_pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 for _ in range(args.steps)]
@@ -671,6 +761,7 @@ def main():
         ev_pairs[i][0].record(stream)
         step()
         ev_pairs[i][1].record(stream)
+        gather()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -678,6 +769,8 @@ def main():
     elapsed = shard.max_over_ranks(elapsed, dev)  # identity at N = 1
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_pairs]))
 
+    if world > 1:  # the gathered labels hold every rank's shard in rank order
+        assert torch.equal(all_lab[rank * args.cases:(rank + 1) * args.cases], d_lab), "label all-gather"
     # sanity: labels of the last step agree with a CPU recomputation on a few cases (not timed)
     if rank == 0:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -708,7 +801,8 @@ def main():
         "data": "synthetic (ALARM forward samples, seed 20250131+rank)",
         "config": {"workload": "ALARM (37 vars) JT inference, 100k synthetic cases per GPU @ 7 evidence vars "
                                "(BASELINE config 2)", "cases_per_gpu": args.cases,
-                   "evidence_per_case": EVIDENCE_PER_CASE, "parallelism": f"case-sharded x{world}"},
+                   "evidence_per_case": EVIDENCE_PER_CASE,
+                   "parallelism": f"case-sharded x{world}" + (" + labels all-gather per step" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel_ms": kernel_ms, "algorithmic_bytes_per_case": bpc,
@@ -756,6 +850,7 @@ def main():
             if "pc_stable" in out:
                 out["pc_stable"]["cpu_baseline"] = cpu_baseline_pc_alarm()
     if rank == 0:
+        out["summary"] = summary(out)  # last key: survives a tail-truncated record of this line
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -68,6 +68,10 @@ _SIGS = {
     "fbn_pc_edges": [_vp, _vp],
     "fbn_pc_sepsets": [_vp, _vp, _i64, _vp],
     "fbn_pc_timing": [_vp, _vp, _vp],
+    "fbn_pc_path": [_vp, _vp],
+    "fbn_pc_result_record": [_vp, _vp, C.c_int64, _vp],
+    "fbn_pc_small_eligible": [_vp, C.c_int, _vp],
+    "fbn_pc_small_eligible_shape": [C.c_int, C.c_int64, _vp, C.c_int, _vp],
     "fbn_pc_device_bytes": [_vp, _vp],
     "fbn_pc_orient_skeleton": [C.c_int, _vp, C.c_int, _vp, C.c_int64, _vp],
     "fbn_pc_level": [_vp, C.c_double, C.c_int, C.c_int, _vp, C.c_int64, C.c_int64, C.c_int64, _vp, _vp, _vp, _vp],
@@ -506,6 +510,10 @@ class PCResult:
         tot, ker = C.c_double(), C.c_double()
         lib.fbn_pc_timing(handle, C.byref(tot), C.byref(ker))
         self.total_s, self.kernel_s = tot.value, ker.value
+        path = C.c_int()
+        lib.fbn_pc_path(handle, C.byref(path))
+        # 0 host-driven levels, 1 device-resident search, 2 device-resident search fell back to the host
+        self.path = path.value
         nb = C.c_int64()
         lib.fbn_pc_device_bytes(handle, C.byref(nb))
         self.device_bytes = nb.value

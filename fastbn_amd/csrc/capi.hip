@@ -1861,7 +1861,8 @@ int fbn_pc_stable(fbn_ci_ctx *c, double alpha, int depth, int group_size, fbn_pc
     static const bool timing = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic
     auto t0 = std::chrono::steady_clock::now();
     int rc;
-    // the device-resident search (small graphs) sets the ctx's margin log itself
+    // the device-resident search (small graphs) sets the ctx's margin log itself (and resets it when
+    // it falls back to the host levels)
     if (!fbn::CiPCSmallEligible(c, group_size) && (rc = CiResetMargin(c))) return rc;
     auto t1 = std::chrono::steady_clock::now();
     if ((rc = fbn::RunPCStable(c, alpha, depth, group_size, r->r))) return rc;
@@ -1905,6 +1906,7 @@ int fbn_pc_edges(const fbn_pc_result *r, int32_t *pairs) {
     for (size_t i = 0; i < r->r.edges.size(); ++i) pairs[2 * i] = r->r.edges[i].first, pairs[2 * i + 1] = r->r.edges[i].second;
     return FBN_OK;
 }
+static constexpr int32_t kPcRecordMagic = 0x52504246;  // 'FBPR': fbn_pc_result_record layout version 1
 int fbn_pc_sepsets(const fbn_pc_result *r, int32_t *buf, int64_t cap, int64_t *len) {
     if (!r) return SetError(FBN_ERR_ARG, "null pointer");
     int64_t k = 0;
@@ -1922,6 +1924,38 @@ int fbn_pc_sepsets(const fbn_pc_result *r, int32_t *buf, int64_t cap, int64_t *l
         for (int v : z) put(v);
     }
     if (len) *len = k;
+    return FBN_OK;
+}
+int fbn_pc_result_record(const fbn_pc_result *r, int32_t *buf, int64_t cap, int64_t *len) {
+    if (!r) return SetError(FBN_ERR_ARG, "null pointer");
+    int64_t k = 0;
+    auto put = [&](int32_t v) {
+        if (buf && k < cap) buf[k] = v;
+        ++k;
+    };
+    const auto &R = r->r;
+    put(kPcRecordMagic);
+    put((int32_t)R.tests_per_level.size());
+    for (int64_t t : R.tests_per_level) put((int32_t)(uint32_t)(uint64_t)t), put((int32_t)((uint64_t)t >> 32));
+    put((int32_t)R.edges.size());
+    for (auto &e : R.edges) put(e.first), put(e.second);
+    int64_t slen = 0;
+    fbn_pc_sepsets(r, nullptr, 0, &slen);
+    put((int32_t)slen);
+    if (buf && k + slen <= cap) fbn_pc_sepsets(r, buf + k, slen, nullptr);
+    k += slen;
+    if (len) *len = k;
+    if (buf && k > cap) return SetError(FBN_ERR_LIMIT, "record needs %lld ints (cap %lld)", (long long)k, (long long)cap);
+    return FBN_OK;
+}
+int fbn_pc_small_eligible(const fbn_ci_ctx *c, int group_size, int *eligible) {
+    if (!c || !eligible) return SetError(FBN_ERR_ARG, "null pointer");
+    *eligible = fbn::CiPCSmallEligible(c, group_size) ? 1 : 0;
+    return FBN_OK;
+}
+int fbn_pc_small_eligible_shape(int nvars, int64_t nsamples, const int32_t *dims, int group_size, int *eligible) {
+    if (!eligible || (nvars > 0 && !dims)) return SetError(FBN_ERR_ARG, "null pointer");
+    *eligible = fbn::PCSmallShape(nvars, nsamples, dims, group_size) ? 1 : 0;
     return FBN_OK;
 }
 int fbn_pc_level(fbn_ci_ctx *c, double alpha, int d, int group_size, const int32_t *edges, int64_t nedges,
@@ -2014,6 +2048,11 @@ int fbn_pc_shd_bif(const fbn_pc_result *r, const char *bif_path, int *shd) {
 int fbn_pc_device_bytes(const fbn_pc_result *r, int64_t *bytes) {
     if (!r || !bytes) return SetError(FBN_ERR_ARG, "null pointer");
     *bytes = r->r.device_bytes;
+    return FBN_OK;
+}
+int fbn_pc_path(const fbn_pc_result *r, int *path) {
+    if (!r || !path) return SetError(FBN_ERR_ARG, "null pointer");
+    *path = r->r.path;
     return FBN_OK;
 }
 int fbn_pc_timing(const fbn_pc_result *r, double *total_s, double *kernel_s) {
@@ -2409,19 +2448,24 @@ int CiRunBatch(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alp
     return CiBatchWait(c, 0, indep, df, res);
 }
 
-bool CiPCSmallEligible(const fbn_ci_ctx *c, int group_size) {
-    if (group_size != 1 || c->nvars < 2 || c->nvars > kSmallMaxVars || c->N < 1 || c->N > (1ll << 30) ||
-        getenv("FBN_PC_NO_SMALL"))
+// the device-resident search's domain: <= 64 variables of <= 4 states, group size 1.  N cap: one
+// test's samples bound the workgroups' skew at a grid barrier (its spin limit is 2 s)
+bool PCSmallShape(int nvars, int64_t N, const int32_t *dims, int group_size) {
+    if (group_size != 1 || nvars < 2 || nvars > kSmallMaxVars || N < 1 || N > (1ll << 24) || getenv("FBN_PC_NO_SMALL"))
         return false;
-    for (int v = 0; v < c->nvars; ++v)
-        if (c->dims[v] < 1 || c->dims[v] > 4) return false;
+    for (int v = 0; v < nvars; ++v)
+        if (dims[v] < 1 || dims[v] > 4) return false;
     return true;
+}
+bool CiPCSmallEligible(const fbn_ci_ctx *c, int group_size) {
+    return PCSmallShape(c->nvars, c->N, c->dims.data(), group_size);
 }
 
 int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::vector<std::pair<int, int>> &edges,
-              std::vector<std::vector<int>> &adj, int *levels, bool *handoff) {
+              std::vector<std::vector<int>> &adj, int *levels, bool *handoff, bool *fellback) {
     *levels = 0;
     *handoff = false;
+    *fellback = false;
     static const bool htime = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic: host phases of the call
     const auto h0 = std::chrono::steady_clock::now();
     FBN_HIP(hipSetDevice(c->device));
@@ -2431,9 +2475,20 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
     const double *band = nullptr;
     int nband = 0;
     if ((rc = CiBand(c, alpha, s, &band, &nband, kBandDfMax))) return rc;
-    static int per_cu = 0;  // (a property of the kernel: queried once)
-    if (per_cu == 0) FBN_HIP(fbn_pc_small_occupancy(&per_cu));
-    if (per_cu < 1) return SetError(FBN_ERR_HIP, "pc small kernel: no workgroup fits a CU");
+    // the host-driven levels instead (same answer): the barrier words may be mid-phase, so they are
+    // zeroed again before the next launch, and the margin log starts over for the host levels
+    auto fall_back = [&](const char *why) {
+        c->small_zeroed = nullptr;
+        const bool quiet = getenv("FBN_PC_SMALL_FAIL") != nullptr;  // (the test knob expects it)
+        if (!quiet) fprintf(stderr, "fastbn: device-resident PC search %s; host-driven levels instead\n", why);
+        *fellback = true;
+        return CiResetMargin(c);
+    };
+    static const int per_cu = [] {  // (a property of the kernel: queried once, thread-safe)
+        int v = 0;
+        return fbn_pc_small_occupancy(&v) == hipSuccess ? v : 0;
+    }();
+    if (per_cu < 1) return fall_back("has no workgroup that fits a CU");
     const int grid = c->num_cu;  // one workgroup per CU: every workgroup resident (grid barrier)
     // scratch: [zeroed: barrier words | first-independent words] [statistics slots] [pair tables]
     const size_t acc_off = (kSmallZeroBytes + 255) & ~(size_t)255;
@@ -2496,7 +2551,20 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
     CiSlot &S = c->slot[0];
     const auto h1 = std::chrono::steady_clock::now();
     if (c->timing) FBN_HIP(hipEventRecord(S.ev0, s));
-    FBN_HIP(fbn_pc_small_launch(&a, grid, s));
+    // FBN_PC_SMALL_FAIL (test knob): "launch" = treat the launch as refused, "timeout" = a barrier
+    // limit of one tick, so the first level's barrier times out in the kernel itself
+    const char *force = getenv("FBN_PC_SMALL_FAIL");  // (read per call: tests set it)
+    static const bool plain = getenv("FBN_PC_SMALL_PLAIN") != nullptr;  // (diagnostic: non-cooperative launch)
+    const bool force_launch = force && !strcmp(force, "launch");
+    const long long spin = (force && !strcmp(force, "timeout")) ? 1 : 0;
+    {
+        const hipError_t le = force_launch ? hipErrorCooperativeLaunchTooLarge
+                                           : fbn_pc_small_launch(&a, grid, spin, plain ? 0 : 1, s);
+        if (le != hipSuccess) {
+            (void)hipGetLastError();  // (clear the sticky launch error)
+            return fall_back(hipGetErrorString(le));
+        }
+    }
     if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
     const auto h2 = std::chrono::steady_clock::now();
     // wait for the kernel's completion word (written after the record) instead of a stream sync;
@@ -2539,9 +2607,11 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
         }
     }
     if (out->status != 0) {
-        c->small_zeroed = nullptr;  // barrier counters left mid-phase: zero again next launch
-        return SetError(FBN_ERR_HIP, "pc small kernel: %s (status %d)",
-                        out->status == 1 ? "grid barrier timed out" : "no result", out->status);
+        // a grid barrier timed out (or no record): wait for the kernel's last workgroups, so none
+        // writes into the next launch's record, then run the host levels
+        FBN_HIP(hipStreamSynchronize(s));
+        if (out->status != 1) return SetError(FBN_ERR_HIP, "pc small kernel: no result (status %d)", out->status);
+        return fall_back("timed out at a grid barrier");
     }
     c->small_phase += (unsigned)out->levels;  // one grid barrier per completed level
     if (c->timing) {

@@ -24,6 +24,68 @@ std::string FbnErr(int rc, const char *what) {
     return std::string(what) + ": " + fbn_last_error();
 }
 
+// Rank 0's column store to rank r's device by ONE ncclBroadcast, adopted as rank r's CI context.
+std::string BroadcastCtx(const std::vector<uint8_t> &cols, const std::vector<int32_t> &dims, int nvars,
+                         int64_t nsamples, GpuGroup &g, int r, fbn_ci_ctx **ctx) {
+    hipStream_t s = g.stream(r);
+    std::string e;
+    const size_t bytes = (size_t)nvars * nsamples;
+    DevMem d_cols;
+    if ((e = d_cols.alloc(bytes)).size()) return e;
+    if (r == 0 && (e = HipErr(hipMemcpyAsync(d_cols.p, cols.data(), bytes, hipMemcpyHostToDevice, s),
+                              "hipMemcpyAsync")).size())
+        return e;
+    if ((e = NcclErr(ncclBroadcast(d_cols.p, d_cols.p, bytes, ncclUint8, 0, g.comm(r), s), "ncclBroadcast")).size())
+        return e;
+    if ((e = HipErr(hipStreamSynchronize(s), "broadcast")).size()) return e;
+    return FbnErr(fbn_ci_dataset_from_device(static_cast<const uint8_t *>(d_cols.p), nvars, nsamples, dims.data(),
+                                             g.device(r), ctx),
+                  "fbn_ci_dataset_from_device");
+}
+
+// Small graphs (fbn_pc_small_eligible: the one-launch device-resident search) on g.size() GPUs:
+// REPLICAS -- every rank runs the whole search on its own copy of the broadcast column store, then
+// ONE ncclBroadcast of rank 0's result record (fbn_pc_result_record, fixed capacity) and every
+// rank checks its own result against it.  Five dependent levels in one 0.14 ms launch do not
+// shard: cutting them over ranks would add an all-gather per level.
+std::string PcReplicas(const std::vector<uint8_t> &cols, const std::vector<int32_t> &dims, int nvars,
+                       int64_t nsamples, double alpha, int depth, GpuGroup &g, fbn_pc_result **out) {
+    const int world = g.size();
+    const int64_t P = (int64_t)nvars * (nvars - 1) / 2;
+    const int64_t cap = 3 + 2 * 8 + 1 + 2 * P + 1 + P * (3 + 8);  // (pc_dist.record_cap)
+    std::vector<fbn_pc_result *> res(world, nullptr);
+    std::string err = g.Run([&](int r) -> std::string {
+        hipStream_t s = g.stream(r);
+        fbn_ci_ctx *ctx = nullptr;
+        std::string e = BroadcastCtx(cols, dims, nvars, nsamples, g, r, &ctx);
+        if (e.empty()) e = FbnErr(fbn_pc_stable(ctx, alpha, depth, 1, &res[r]), "fbn_pc_stable");
+        std::vector<int32_t> mine((size_t)cap, 0), got((size_t)cap, 0);
+        if (e.empty()) e = FbnErr(fbn_pc_result_record(res[r], mine.data(), cap, nullptr), "fbn_pc_result_record");
+        DevMem d_rec;
+        if (e.empty()) e = d_rec.alloc((size_t)cap * 4);
+        if (e.empty()) e = HipErr(hipMemcpyAsync(d_rec.p, mine.data(), (size_t)cap * 4, hipMemcpyHostToDevice, s),
+                                  "hipMemcpyAsync");
+        // (every rank reaches the broadcast, even after an error, so no rank waits forever; a rank
+        // with an error broadcasts / receives zeros and reports its own error)
+        std::string e2 = NcclErr(ncclBroadcast(d_rec.p, d_rec.p, (size_t)cap, ncclInt32, 0, g.comm(r), s), "ncclBroadcast");
+        if (e.empty()) e = e2;
+        if (e.empty()) e = HipErr(hipMemcpyAsync(got.data(), d_rec.p, (size_t)cap * 4, hipMemcpyDeviceToHost, s),
+                                  "hipMemcpyAsync");
+        if (e.empty()) e = HipErr(hipStreamSynchronize(s), "record");
+        if (e.empty() && got != mine) e = "PC replicas disagree with rank 0's result record";
+        if (ctx) fbn_ci_ctx_destroy(ctx);
+        return e;
+    });
+    for (int r = 1; r < world; ++r)
+        if (res[r]) fbn_pc_result_destroy(res[r]);
+    if (!err.empty()) {
+        if (res[0]) fbn_pc_result_destroy(res[0]);
+        return err;
+    }
+    *out = res[0];
+    return std::string();
+}
+
 // The skeleton search on g.size() GPUs (INTEGRATION.md "Multi-GPU"): rank 0's column
 // store reaches every device by ONE ncclBroadcast; each rank runs its edge range of every level
 // through the native session; per level ONE ncclAllGather of the fixed-size records (level 0 also
@@ -38,22 +100,8 @@ std::string PcDistributed(const std::vector<uint8_t> &cols, const std::vector<in
         hipStream_t s = g.stream(r);
         ncclComm_t comm = g.comm(r);
         std::string e;
-        const size_t bytes = (size_t)nvars * nsamples;
         fbn_ci_ctx *ctx = nullptr;
-        {
-            DevMem d_cols;
-            if ((e = d_cols.alloc(bytes)).size()) return e;
-            if (r == 0 && (e = HipErr(hipMemcpyAsync(d_cols.p, cols.data(), bytes, hipMemcpyHostToDevice, s),
-                                      "hipMemcpyAsync")).size())
-                return e;
-            if ((e = NcclErr(ncclBroadcast(d_cols.p, d_cols.p, bytes, ncclUint8, 0, comm, s), "ncclBroadcast")).size())
-                return e;
-            if ((e = HipErr(hipStreamSynchronize(s), "broadcast")).size()) return e;
-            if ((e = FbnErr(fbn_ci_dataset_from_device(static_cast<const uint8_t *>(d_cols.p), nvars, nsamples,
-                                                       dims.data(), g.device(r), &ctx),
-                            "fbn_ci_dataset_from_device")).size())
-                return e;
-        }
+        if ((e = BroadcastCtx(cols, dims, nvars, nsamples, g, r, &ctx)).size()) return e;
         fbn_pc_dist *sess = nullptr;
         if ((e = FbnErr(fbn_pc_dist_create(nvars, alpha, depth, group_size, &sess), "fbn_pc_dist_create")).size()) {
             fbn_ci_ctx_destroy(ctx);
@@ -144,12 +192,19 @@ void PCStable::StructLearnCompData(fbn_dataset *dts, int group_size, int /*num_t
     fbn_pc_result *res = nullptr;
     if (gpus_ > 1 || ForceExchange()) {  // RCCL over the node's GPUs (MultiGpu.h)
         GpuGroup g(gpus_, device_);
-        std::string e = g.ok() ? PcDistributed(cols, dims, nvars, nsamples, alpha, depth, group_size, g, &res) : g.error();
+        // a small graph runs the one-launch device-resident search on every rank (replicas); a
+        // larger one is cut by edges per level (the eligibility is a property of the dataset)
+        int small = 0;
+        fbn_pc_small_eligible_shape(nvars, nsamples, dims.data(), group_size, &small);
+        std::string e = !g.ok() ? g.error()
+                        : small ? PcReplicas(cols, dims, nvars, nsamples, alpha, depth, g, &res)
+                                : PcDistributed(cols, dims, nvars, nsamples, alpha, depth, group_size, g, &res);
         if (!e.empty()) {
             fprintf(stderr, "Error in StructLearnCompData: %s\n", e.c_str());
             exit(1);
         }
-        std::cout << "PC-stable skeleton on " << g.size() << " GPU(s) (RCCL)" << std::endl;
+        std::cout << "PC-stable skeleton on " << g.size() << " GPU(s) (RCCL, "
+                  << (small ? "replicas + result broadcast" : "edges split per level") << ")" << std::endl;
     } else if (fbn_ci_dataset_upload(cols.data(), nvars, nsamples, dims.data(), device_, &ctx) ||
                fbn_pc_stable(ctx, alpha, depth, group_size, &res)) {
         fprintf(stderr, "Error in StructLearnCompData: %s\n", fbn_last_error());

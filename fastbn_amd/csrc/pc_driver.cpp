@@ -436,23 +436,31 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
     CiBatchStats st_all{0, 0};
     for (int v = 0; v < n; ++v) st_all.dim_rows += (int64_t)(n - 1) * dims[v], st_all.maxdim = std::max(st_all.maxdim, (int)dims[v]);
     int d0 = 0;
+    bool small_done = false;  // the device-resident search ran (all levels, or the first ones)
+    int small_levels = 0;
+    bool small_handoff = false;
+    auto ta_small = std::chrono::steady_clock::now();
     if (CiPCSmallEligible(ctx, group_size)) {
-        // small graph: the whole search (or its first levels) in one device launch
-        auto ta = std::chrono::steady_clock::now();
-        int levels = 0;
-        bool handoff = false;
-        if (int rc = CiPCSmall(ctx, alpha, depth, res, edges, adj, &levels, &handoff)) return rc;
+        // small graph: the whole search (or its first levels) in one device launch; refused at launch
+        // or timed out at a grid barrier: the host-driven levels below (same answer)
+        bool fellback = false;
+        if (int rc = CiPCSmall(ctx, alpha, depth, res, edges, adj, &small_levels, &small_handoff, &fellback))
+            return rc;
+        res.path = fellback ? 2 : 1;
+        small_done = !fellback;
+    }
+    if (small_done) {
         if (timing)
-            fprintf(stderr, "pc device-resident levels 0-%d: %.3f ms%s\n", levels - 1,
-                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count(),
-                    handoff ? " (host continues)" : "");
-        if (!handoff) {
+            fprintf(stderr, "pc device-resident levels 0-%d: %.3f ms%s\n", small_levels - 1,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta_small).count(),
+                    small_handoff ? " (host continues)" : "");
+        if (!small_handoff) {
             res.edges = edges;
             res.total_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
             return FBN_OK;
         }
         CiSetPairMode(ctx, 0);  // the ctx recorded no pair tables: the host levels count in full
-        d0 = levels;
+        d0 = small_levels;
     } else if (n >= 2 && CiAllPairsEligible(ctx, st_all) && !getenv("FBN_CI_NO_IMPLICIT")) {
         auto ta = std::chrono::steady_clock::now();
         const double k0 = res.kernel_s;

@@ -186,6 +186,9 @@ struct PCResultHost {
     double min_margin = 0.0;
     int64_t near_alpha = 0;
     bool margin_done = false;  // min_margin / near_alpha already hold the run's log (device-resident run)
+    // skeleton path: 0 host-driven levels, 1 device-resident search (pc_small), 2 device-resident
+    // search refused at launch or timed out at a grid barrier -> host-driven levels (same answer)
+    int path = 0;
 };
 
 void CiCtxShape(const fbn_ci_ctx *c, int *nvars, int64_t *nsamples);
@@ -233,8 +236,11 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
 // (d > 4 or > 2^22 candidate sets) follows, and the host driver continues at level *levels.  When
 // the search ended on the device res.min_margin / near_alpha hold its decision-margin log.
 bool CiPCSmallEligible(const fbn_ci_ctx *c, int group_size);
+bool PCSmallShape(int nvars, int64_t N, const int32_t *dims, int group_size);  // (the same rule, from the shape)
+// *fellback: the launch was refused or a grid barrier timed out; res / edges / adj untouched and the
+// ctx's margin log reset, the caller runs the host-driven levels from level 0
 int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::vector<std::pair<int, int>> &edges,
-              std::vector<std::vector<int>> &adj, int *levels, bool *handoff);
+              std::vector<std::vector<int>> &adj, int *levels, bool *handoff, bool *fellback);
 // one level for an edge range (the unit a multi-GPU driver partitions), see pc_driver.cpp
 struct LevelOut {
     std::vector<char> removed;

@@ -80,7 +80,8 @@ struct PcSmallArgs {
 
 }  // namespace fbn
 
-extern "C" hipError_t fbn_pc_small_launch(const fbn::PcSmallArgs *a, int grid, hipStream_t s);
+extern "C" hipError_t fbn_pc_small_launch(const fbn::PcSmallArgs *a, int grid, long long spin_ticks, int cooperative,
+                                          hipStream_t s);
 extern "C" int fbn_pc_small_block_threads(void);
 extern "C" hipError_t fbn_pc_small_occupancy(int *blocks_per_cu);
 

@@ -11,8 +11,8 @@
 //       order: the d-subsets of adj(x)\{y} in lexicographic order, then those of adj(y)\{x},
 //       CheckEdge src/PCStable.cpp:339-470, ChoiceGenerator src/ChoiceGenerator.cpp:14-85);
 //     tests are counted and decided (d <= 1: one wave per test on the bit-sliced store, level 1
-//       deriving the last value of x, y and z from the level-0 pair tables; d = 2, 3: one wave per
-//       test, d = 4: one workgroup per test, LDS histograms of the 2-bit packed columns -- Counts2D/Counts3D,
+//       deriving the last value of x, y and z from the level-0 pair tables; d = 2: one wave per
+//       test, d = 3, 4: one workgroup per test, LDS histograms of the 2-bit packed columns -- Counts2D/Counts3D,
 //       src/CellTable.cpp:23-91,226-291,430-455; G^2 / df / p as ComputeGSquareXY/XYZ,
 //       src/IndependenceTest.cpp:65-155,295-364);
 //     an independent test does atomicMax(first[d][edge], ~its index within the edge): the edge's
@@ -28,7 +28,9 @@
 // per-group arrival counters (group = blockIdx % 8), the last arriver of a group adds to the top
 // counter, every workgroup polls relaxed with s_sleep; the data crossing workgroups moves through
 // agent-coherent accesses, so the barrier carries no cache-maintenance fence (see grid_barrier);
-// every spin bounded (a timed-out launch reports status 1 and exits).
+// every spin bounded (a timed-out launch reports status 1 and exits; the host then runs the search
+// on its level loop).  The launch is cooperative: a grid that cannot be co-resident fails at launch
+// (and the host falls back) instead of spinning.
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -46,7 +48,7 @@ constexpr int kHistCells = 4096;    // 4^(kSmallMaxD + 2)
 constexpr int kMaxZ = 256;          // 4^kSmallMaxD conditioning configurations
 constexpr int kTermChunk = 1024;
 constexpr int kGroups = 8;          // barrier groups (blockIdx % 8: the XCD when dispatch is round-robin)
-constexpr long long kSpinTicks = 200000000ll;  // wall_clock64 ticks (100 MHz): 2 s per barrier
+constexpr long long kSpinTicks = 200000000ll;  // wall_clock64 ticks (100 MHz): 2 s per barrier (default)
 
 typedef __attribute__((ext_vector_type(4))) unsigned u4;
 
@@ -191,6 +193,7 @@ struct Barrier {
     unsigned *grp;   // kGroups arrival counters, each on its own 64-B line (stride 16)
     unsigned *top;   // groups done
     int nblocks;
+    long long spin;  // wall_clock64 ticks a workgroup waits at one barrier before giving up
 };
 
 __device__ bool grid_barrier(const Barrier &B, unsigned phase, Lds &L) {
@@ -208,7 +211,7 @@ __device__ bool grid_barrier(const Barrier &B, unsigned phase, Lds &L) {
         int ok = 1;
         while (__hip_atomic_load(B.top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
             __builtin_amdgcn_s_sleep(2);
-            if (wall_clock64() - t0 > kSpinTicks) {
+            if (wall_clock64() - t0 > B.spin) {
                 ok = 0;
                 break;
             }
@@ -952,8 +955,7 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs Ak, Barrier B)
                     int zz[3];
                     unrank(L, x, y, d, k, zz);
                     if (d == 1) r = wave_test<1>(A, L, x, y, zz[0], lane, false, L.wtab[wv], L.waux[wv], L.ph[wv]);
-                    else if (d == 2) r = wave_hist_test<2>(A, L, x, y, zz, lane, L.whist[wv], L.ph[wv]);
-                    else r = wave_hist_test<3>(A, L, x, y, zz, lane, L.whist[wv], L.ph[wv]);
+                    else r = wave_hist_test<2>(A, L, x, y, zz, lane, L.whist[wv], L.ph[wv]);  // (d == 2)
                 }
                 ++launched;
                 const unsigned long long mb = (unsigned long long)__double_as_longlong(r.margin);
@@ -1091,9 +1093,18 @@ extern "C" hipError_t fbn_pc_small_occupancy(int *blocks_per_cu) {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, pc_small_kernel, BS, 0);
 }
 
-// a->bar: (kGroups * 16 + 16) unsigned words, zeroed by the caller before every launch
-extern "C" hipError_t fbn_pc_small_launch(const PcSmallArgs *a, int grid, hipStream_t s) {
-    Barrier b{a->bar, a->bar + 16 * kGroups, grid};
+// a->bar: (kGroups * 16 + 16) unsigned words, zeroed once (see kSmallZeroBytes).  spin_ticks <= 0:
+// the default barrier limit.  cooperative: hipLaunchCooperativeKernel, which refuses a grid that
+// cannot be resident at once (hipErrorCooperativeLaunchTooLarge) instead of letting it spin.
+extern "C" hipError_t fbn_pc_small_launch(const PcSmallArgs *a, int grid, long long spin_ticks, int cooperative,
+                                          hipStream_t s) {
+    Barrier b{a->bar, a->bar + 16 * kGroups, grid, spin_ticks > 0 ? spin_ticks : kSpinTicks};
+    if (cooperative) {
+        PcSmallArgs ak = *a;
+        void *params[2] = {&ak, &b};
+        return hipLaunchCooperativeKernel(reinterpret_cast<const void *>(pc_small_kernel), dim3(grid), dim3(BS),
+                                          params, 0, s);
+    }
     hipLaunchKernelGGL(pc_small_kernel, dim3(grid), dim3(BS), 0, s, *a, b);
     return hipGetLastError();
 }

@@ -198,3 +198,84 @@ def independence_test_broadcast(cols, dims, shape, alpha=0.05, device=0, src=0):
     t = broadcast_columns(cols, shape, torch.device("cuda", device), src)
     torch.cuda.synchronize(device)
     return api.IndependenceTest.from_device(t.data_ptr(), shape[0], shape[1], dims, alpha, device)
+
+
+# ---------------------------------------------------------------- small graphs: replicas
+# A graph the device-resident search takes (fbn_pc_small_eligible: <= 64 variables of <= 4 states,
+# group size 1 -- ALARM-5000) is ONE launch of five dependent levels on one GPU (0.14 ms); cutting
+# its levels over N GPUs would add an all-gather per level to that chain and cannot shorten it.
+# So N GPUs run it as replicas ("replicas only"): every rank runs the whole search on
+# its own copy of the broadcast column store, and ONE broadcast of rank 0's result record gives
+# every rank the same answer (each rank can check its own against it).
+RECORD_MAGIC = 0x52504246
+
+
+def record_cap(nvars, max_levels=8, max_d=8):
+    """Upper bound of fbn_pc_result_record's length for a graph of `nvars` variables."""
+    P = nvars * (nvars - 1) // 2
+    return 3 + 2 * max_levels + 1 + 2 * P + 1 + P * (3 + max_d)
+
+
+def small_eligible(ci, group_size=1):
+    e = C.c_int()
+    api.lib.fbn_pc_small_eligible(ci._h, int(group_size), C.byref(e))
+    return bool(e.value)
+
+
+def result_record(handle, cap):
+    """fbn_pc_result_record of a result handle into a zero-padded int32 array of length `cap`."""
+    rec = np.zeros(cap, np.int32)
+    n = C.c_int64()
+    api.lib.fbn_pc_result_record(handle, rec.ctypes.data, int(cap), C.byref(n))
+    return rec
+
+
+def unpack_record(rec):
+    """-> {"tests_per_level", "edges", "sepset"} (the PCResult views) from a record."""
+    r = np.asarray(rec, np.int64)
+    if int(r[0]) != RECORD_MAGIC:
+        raise ValueError("not a PC result record")
+    L = int(r[1])
+    k = 2
+    tests = [int((r[k + 2 * i] & 0xFFFFFFFF) | (r[k + 2 * i + 1] << 32)) for i in range(L)]
+    k += 2 * L
+    ne = int(r[k])
+    edges = [(int(r[k + 1 + 2 * i]), int(r[k + 2 + 2 * i])) for i in range(ne)]
+    k += 1 + 2 * ne
+    slen = int(r[k])
+    k += 1
+    sep, end = {}, k + slen
+    while k < end:
+        x, y, m = int(r[k]), int(r[k + 1]), int(r[k + 2])
+        sep[(x, y)] = tuple(int(v) for v in r[k + 3:k + 3 + m])
+        k += 3 + m
+    return {"tests_per_level": tests, "edges": edges, "sepset": sep}
+
+
+def broadcast_record(rec, device=None, src=0):
+    """Rank `src`'s fixed-length int32 record to every rank in one broadcast (device buffers with
+    nccl) -> numpy array (identity at world size 1 unless FBN_PC_DIST_FORCE_EXCHANGE)."""
+    import torch
+    import torch.distributed as dist
+    world, _ = _world_rank()
+    if world == 1 and not (_force_exchange() and dist.is_available() and dist.is_initialized()):
+        return rec
+    t = torch.from_numpy(np.ascontiguousarray(rec, np.int32))
+    if device is not None:
+        t = t.to(device)
+    dist.broadcast(t, src)
+    return t.cpu().numpy()
+
+
+def pc_stable_replicas(ci, alpha=0.05, depth=1000, device=None, check=True):
+    """Small graphs on N ranks: the whole device-resident search on every rank (fbn_pc_stable on
+    its own IndependenceTest `ci`), one broadcast of rank 0's result record.  -> (PCResult of this
+    rank, unpacked rank-0 record); check: every rank's own record must equal rank 0's."""
+    h = C.c_void_p()
+    api.lib.fbn_pc_stable(ci._h, float(alpha), int(depth), 1, C.byref(h))
+    res = api.PCResult(h)
+    mine = result_record(h, record_cap(len(ci.dims)))
+    got = broadcast_record(mine, device)
+    if check and not np.array_equal(got, mine):
+        raise RuntimeError("PC replicas disagree with rank 0's result record")
+    return res, unpack_record(got)

@@ -258,6 +258,19 @@ int fbn_pc_shd_bif(const fbn_pc_result *r, const char *bif_path, int *shd);
 /* Same for any learned graph given as triples [n][3] (from, to, 1) / (a, b, 0). */
 int fbn_shd_bif(const char *bif_path, int nvars, const int32_t *triples, int n, int *shd);
 int fbn_pc_timing(const fbn_pc_result *r, double *total_s, double *kernel_s);
+/* Which skeleton path ran: 0 host-driven levels, 1 the device-resident search (small graphs, one
+ * cooperative launch), 2 the device-resident search was refused at launch or timed out at a grid
+ * barrier and the host-driven levels ran instead (same answer). */
+int fbn_pc_path(const fbn_pc_result *r, int *path);
+/* The result as one flat int32 record (for moving it between ranks): magic 0x52504246, n_levels,
+ * n_levels (lo, hi) halves of the per-level test counts, n_edges, pairs [n_edges][2], then the
+ * fbn_pc_sepsets ints preceded by their count.  *len = ints needed; FBN_ERR_LIMIT if cap is short. */
+int fbn_pc_result_record(const fbn_pc_result *r, int32_t *buf, int64_t cap, int64_t *len);
+/* 1 if fbn_pc_stable on this context runs the device-resident search (small graphs: <= 64 variables
+ * of <= 4 states, group size 1): multi-GPU drivers run such graphs as replicas, not partitioned. */
+int fbn_pc_small_eligible(const fbn_ci_ctx *c, int group_size, int *eligible);
+/* The same rule from the dataset's shape (no context needed). */
+int fbn_pc_small_eligible_shape(int nvars, int64_t nsamples, const int32_t *dims, int group_size, int *eligible);
 
 /* ------------------------------------------------------------------ multi-GPU PC-stable session
  * One session per rank (one process per GPU); the per-level exchange is the caller's collective

@@ -81,6 +81,57 @@ def read_ci_fixture(path):
     return dims, colhash, tests
 
 
+def gram_dataset(nvars, N, seed):
+    """Seeded ragged-shape datasets of the level-0 Gram tests (test_gpu_gram_mfma.py and the
+    reference fixture tests/golden/gram_ragged.ci.gz, make_golden_synth.py gram): state counts 2-4,
+    mildly dependent columns (tables far from uniform), and a sample of pairs that includes the
+    first / last rows of the 256-row Gram tiles."""
+    rng = np.random.default_rng(seed)
+    dims = rng.integers(2, 5, nvars).astype(np.int32)
+    cols = np.empty((nvars, N), np.uint8)
+    base = rng.integers(0, 4, N)
+    for v in range(nvars):
+        noise = rng.integers(0, dims[v], N)
+        keep = rng.random(N) < 0.3
+        cols[v] = np.where(keep, base % dims[v], noise)
+    rng = np.random.default_rng(seed + 100)
+    x = rng.integers(0, nvars - 1, 1500)
+    y = np.minimum(nvars - 1, x + 1 + rng.integers(0, nvars, 1500))
+    pairs = np.unique(np.stack([x, y], 1), axis=0)
+    pairs = np.concatenate([pairs, [[0, 1], [0, nvars - 1], [nvars - 2, nvars - 1]]]).astype(np.int32)
+    return cols, dims, pairs
+
+
+def fnv1a_columns(cols):
+    """FNV-1a 64 over every column's int values (ref_dump ci's colhash), vectorised across columns."""
+    h = np.full(cols.shape[0], 1469598103934665603, np.uint64)
+    prime = np.uint64(1099511628211)
+    with np.errstate(over="ignore"):
+        for k in range(cols.shape[1]):
+            h ^= cols[:, k].astype(np.uint64)
+            h *= prime
+    return h
+
+
+def read_ci_blocks(path):
+    """Multi-block ci fixture (gram_ragged.ci.gz): {(nvars, N, seed): (dims, colhash, tests)}."""
+    import tempfile
+    with gzip.open(path, "rt") as f:
+        text = f.read()
+    out = {}
+    for blk in text.split("shape ")[1:]:
+        head, body = blk.split("\n", 1)
+        key = tuple(int(v) for v in head.split())
+        with tempfile.NamedTemporaryFile("wb", suffix=".gz") as tf:
+            with gzip.open(tf.name, "wt") as g:
+                g.write(body)
+            out[key] = read_ci_fixture(tf.name)
+    return out
+
+
+GRAM_SHAPES = [(520, 30001, 1), (700, 20480, 2), (260, 100003, 3)]
+
+
 def pc_digest(edges, sepset):
     """Digests of a PC-stable skeleton: the edge list in vec_edges order and the sepsets as
     (x, y, |Z|, Z...) records in ascending key order (int32), sha256 hex."""

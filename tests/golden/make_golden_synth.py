@@ -136,11 +136,52 @@ def pc_c5_ci():
                                                              for d, v in sorted(by_level.items())}))
 
 
+GRAM_PAIRS = 320  # per shape: a seeded sample of the test's pairs plus the tile-edge pairs
+
+
+def gram_ragged():
+    """gram_ragged.ci.gz: the UNMODIFIED reference's Counts2D::FillTable (src/CellTable.cpp:430-455,
+    oracle/_ref/ref_dump ci) on the ragged-shape datasets of test_gpu_gram_mfma.py (conftest
+    gram_dataset: leading-row counts not multiples of the 256-row Gram tile, sample counts not
+    multiples of the 128-sample stage), one block per shape: `shape nvars N seed` then the ci dump."""
+    import random
+    import struct
+
+    import numpy as np
+    from conftest import GRAM_SHAPES, gram_dataset
+    ref_dump = os.path.join(REPO, "oracle", "_ref", "ref_dump")
+    if not os.path.exists(ref_dump):
+        subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref"], check=True)
+    blocks = []
+    for nvars, N, seed in GRAM_SHAPES:
+        cols, dims, pairs = gram_dataset(nvars, N, seed)
+        rng = random.Random(seed)
+        idx = sorted(set(rng.sample(range(len(pairs) - 3), GRAM_PAIRS - 3)) | {len(pairs) - 3, len(pairs) - 2,
+                                                                              len(pairs) - 1})
+        with tempfile.TemporaryDirectory() as td:
+            cpath = os.path.join(td, "g.cols")
+            with open(cpath, "wb") as f:
+                f.write(struct.pack("<iq", nvars, N))
+                f.write(np.asarray(dims, np.int32).tobytes())
+                f.write(np.ascontiguousarray(cols, np.uint8).tobytes())
+            tfile = os.path.join(td, "tests")
+            with open(tfile, "w") as f:
+                for i in idx:
+                    f.write("%d %d\n" % (pairs[i, 0], pairs[i, 1]))
+            out = os.path.join(td, "g.ci")
+            subprocess.run([ref_dump, "ci", "cols:" + cpath, tfile, out], check=True, stdout=subprocess.DEVNULL)
+            blocks.append("shape %d %d %d\n" % (nvars, N, seed) + open(out).read())
+    gz_write(os.path.join(HERE, "gram_ragged.ci.gz"), "".join(blocks))
+    print("gram_ragged.ci.gz: %d shapes x %d pairs" % (len(GRAM_SHAPES), GRAM_PAIRS))
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["munin", "c5", "c5ci"]
+    which = sys.argv[1:] or ["munin", "c5", "c5ci", "gram"]
     if "munin" in which:
         munin_like()
     if "c5" in which:
         pc_c5()
     if "c5ci" in which:
         pc_c5_ci()
+    if "gram" in which:
+        gram_ragged()

@@ -43,13 +43,19 @@ def test_cli_rccl_path_at_one_gpu():
         return out.stdout
 
     pc = run_env(["-a", "0", "-f1", "alarm/alarm.bif", "-f2", "alarm/alarm_s5000.txt"])
-    assert "(RCCL)" in pc and "# of CI-tests is 5206" in pc and "SHD = 5" in pc, pc
+    # ALARM-5000 is a small graph: replicas of the one-launch search + ncclBroadcast of rank 0's record
+    assert "(RCCL, replicas" in pc and "# of CI-tests is 5206" in pc and "SHD = 5" in pc, pc
     plain = run(["-a", "0", "-f1", "alarm/alarm.bif", "-f2", "alarm/alarm_s5000.txt"])
     pick = lambda s: [ln for ln in s.splitlines() if ln.startswith(("Level", "# of CI", "# remaining", "SHD"))]
     assert pick(pc) == pick(plain)
+    # the edge-split session (larger graphs) on the same data: FBN_PC_NO_SMALL makes it ineligible
+    env["FBN_PC_NO_SMALL"] = "1"
+    split = run_env(["-a", "0", "-f1", "alarm/alarm.bif", "-f2", "alarm/alarm_s5000.txt"])
+    del env["FBN_PC_NO_SMALL"]
+    assert "(RCCL, edges split" in split and pick(split) == pick(plain), split
     jt_args = ["-a", "2", "-f0", "alarm/alarm.xml", "-f3", "alarm/testing_alarm_1k_p20", "-f4", "alarm/alarm_1k_pt"]
     jt = run_env(jt_args)
-    assert "(RCCL)" in jt and re.search(r"accuracy = 1\b", jt), jt
+    assert "(RCCL" in jt and re.search(r"accuracy = 1\b", jt), jt
     jplain = run(jt_args)
     pickj = lambda s: [ln for ln in s.splitlines() if ln.startswith(("average", "accuracy"))]
     assert pickj(jt) == pickj(jplain)

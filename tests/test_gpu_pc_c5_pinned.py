@@ -11,23 +11,12 @@ import os
 
 import numpy as np
 import pytest
-from conftest import GOLD, read_ci_fixture
+from conftest import GOLD, fnv1a_columns, read_ci_fixture
 
 import fastbn_amd as F
 import oracle as O
 
 pytestmark = pytest.mark.gpu
-
-
-def _fnv1a_columns(cols):
-    """FNV-1a 64 over every column's int values (conftest.fnv1a), vectorised across columns."""
-    h = np.full(cols.shape[0], 1469598103934665603, np.uint64)
-    prime = np.uint64(1099511628211)
-    with np.errstate(over="ignore"):
-        for k in range(cols.shape[1]):
-            h ^= cols[:, k].astype(np.uint64)
-            h *= prime
-    return h
 
 
 @pytest.fixture(scope="module")
@@ -36,7 +25,7 @@ def c5():
     dims, colhash, tests = read_ci_fixture(os.path.join(GOLD, "pc_c5.ci.gz"))
     cols, gdims = synth.config5_dataset()
     assert gdims.tolist() == dims
-    h = _fnv1a_columns(cols)
+    h = fnv1a_columns(cols)
     assert all(int(h[v]) == colhash[v] for v in range(len(dims)))  # the reference read these columns
     ci = F.IndependenceTest(F.Dataset(columns=cols, dims=gdims))
     return cols, gdims, ci, tests
@@ -83,17 +72,27 @@ def test_df_g2_decisions_vs_restatement(c5, d):
         assert abs(p[k] - r["p_value"]) <= 1e-12
 
 
-def test_config5_full_size_hand_written_gram(monkeypatch):
-    """Config 5 at full size with level 0's Gram on the hand-written popcount kernel
-    (FBN_CI_GRAM_NO_BLAS: no library GEMM): the restatement's tests per level, edges, sepsets."""
+def _config5_full_size(monkeypatch, env):
     import hashlib
     import json
     from conftest import pc_digest
     from fastbn_amd import synth
-    monkeypatch.setenv("FBN_CI_GRAM_NO_BLAS", "1")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     ref = json.load(open(os.path.join(GOLD, "pc_c5.json")))
     cols, dims = synth.config5_dataset()
     assert hashlib.sha256(np.ascontiguousarray(cols).tobytes()).hexdigest() == ref["columns_sha256"]
     pc = F.PCStable(ref["alpha"], ref["depth"]).StructLearnCompData(F.Dataset(columns=cols, dims=dims))
     assert pc.tests_per_level.tolist() == ref["tests_per_level"]
     assert pc_digest(pc.edges, pc.sepset) == {k: ref[k] for k in ("edges_sha256", "sepsets_sha256")}
+
+
+def test_config5_full_size_default_mfma_gram(monkeypatch):
+    """Config 5 at full size on the default path (level 0's Gram on the hand-written FP4 MFMA
+    kernel, no library GEMM): the restatement's tests per level, edges, sepsets."""
+    _config5_full_size(monkeypatch, {})
+
+
+def test_config5_full_size_popcount_gram(monkeypatch):
+    """The same with level 0's Gram on the hand-written popcount kernel (FBN_CI_GRAM_NO_MFMA)."""
+    _config5_full_size(monkeypatch, {"FBN_CI_GRAM_NO_MFMA": "1"})

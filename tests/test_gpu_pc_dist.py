@@ -175,6 +175,10 @@ def _worker_nccl(rank, world, port, out):
     ci = pc_dist.independence_test_broadcast(ds.columns, [int(v) for v in ds.dims], [ds.num_vars, ds.num_instance])
     res, tests, _ = pc_dist.pc_stable_distributed(ci, 37, device="cuda:0")
     got["alarm"] = {"tests": tests, **pc_digest(res.edges, res.sepset), "shd": res.GetSHD(BIF)}
+    # small graphs at N > 1: replicas + one RCCL broadcast of rank 0's result record (forced at world 1)
+    rres, rec0 = pc_dist.pc_stable_replicas(ci, 0.05, 1000, device="cuda:0")
+    got["alarm_replicas"] = {"tests": rec0["tests_per_level"], **pc_digest(rec0["edges"], rec0["sepset"]),
+                             "shd": rres.GetSHD(BIF), "path": rres.path}
     cols, dims = synth.config5_dataset()
     ci5 = pc_dist.independence_test_broadcast(cols, [int(v) for v in dims], list(cols.shape))
     res5, tests5, _ = pc_dist.pc_stable_distributed(ci5, 1000, 0.05, 6, device="cuda:0")
@@ -201,6 +205,9 @@ def test_nccl_world1_forced_exchange_configs_3_and_5(tmp_path):
     pc = F.PCStable(0.05, 1000).StructLearnCompData(F.Dataset(CSV))
     assert got["alarm"]["tests"] == pc.tests_per_level.tolist() and got["alarm"]["shd"] == 5
     assert {k: got["alarm"][k] for k in ("edges_sha256", "sepsets_sha256")} == pc_digest(pc.edges, pc.sepset)
+    rep = got["alarm_replicas"]
+    assert rep["tests"] == pc.tests_per_level.tolist() and rep["shd"] == 5 and rep["path"] == 1
+    assert {k: rep[k] for k in ("edges_sha256", "sepsets_sha256")} == pc_digest(pc.edges, pc.sepset)
     ref = json.load(open(os.path.join(GOLD, "pc_c5.json")))
     assert got["c5"]["tests"] == ref["tests_per_level"]
     assert {k: got["c5"][k] for k in ("edges_sha256", "sepsets_sha256")} == \

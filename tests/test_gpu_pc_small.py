@@ -120,3 +120,25 @@ def test_repeated_runs_and_context_margin_log(alarm):
         assert r.tests_per_level.tolist() == runs[0].tests_per_level.tolist()
     m, near = ci.decision_margin()
     assert m == runs[-1].min_margin and near == runs[-1].near_alpha
+
+
+@pytest.mark.parametrize("mode", ["launch", "timeout"])
+def test_fallback_to_host_levels(alarm, mode, monkeypatch):
+    """A refused cooperative launch, or a grid barrier that times out inside the kernel (a barrier
+    limit of one tick), hands the whole search to the host-driven levels: the same tests per level,
+    skeleton, sepsets, orientation and SHD as the device-resident path, and a fresh margin log."""
+    ds, od = alarm
+    dev = F.PCStable(0.05, 1000).StructLearnCompData(ds)
+    assert dev.path == 1
+    monkeypatch.setenv("FBN_PC_SMALL_FAIL", mode)
+    fb = F.PCStable(0.05, 1000).StructLearnCompData(ds)
+    monkeypatch.delenv("FBN_PC_SMALL_FAIL")
+    assert fb.path == 2
+    assert fb.tests_per_level.tolist() == dev.tests_per_level.tolist() == [666, 3579, 828, 118, 15]
+    assert fb.edges == dev.edges and fb.sepset == dev.sepset and fb.oriented == dev.oriented
+    assert fb.GetSHD(os.path.join(GOLD, "alarm", "alarm.bif")) == 5
+    # the host levels' own log (not the failed launch's): the same tests' margins, so no near decisions
+    assert fb.near_alpha == 0 and 1e-9 < fb.min_margin < 1.0
+    # and the device path works again afterwards (barrier words zeroed again)
+    again = F.PCStable(0.05, 1000).StructLearnCompData(ds)
+    assert again.path == 1 and again.edges == dev.edges and again.sepset == dev.sepset

@@ -222,3 +222,42 @@ def test_two_rank_gloo_column_broadcast(tmp_path):
     ref = np.random.default_rng(7).integers(0, 4, (37, 5000)).astype(np.uint8)
     for r in range(2):
         np.testing.assert_array_equal(np.load(f"{out}.{r}.npy"), ref)
+
+
+# ---------------------------------------------------------------- small graphs: replicas
+def _replica_worker(rank, world, port, csv, out_path):
+    """Every rank computes the whole skeleton itself (the oracle stands in for the one-launch device
+    search), packs it with the native fbn_pc_result_record, and rank 0's record is broadcast."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import oracle as O
+    import fastbn_amd as F
+    from fastbn_amd import pc_dist
+    ref = O.OracleDataset(csv=csv).pc_stable(0.05, 1000, 1)
+    res = F.orient_skeleton(37, ref["edges"], {tuple(k): tuple(v) for k, v in ref["sepset"].items()})
+    mine = pc_dist.result_record(res._h, pc_dist.record_cap(37))
+    got = pc_dist.broadcast_record(mine)
+    out = pc_dist.unpack_record(got)
+    np.save(f"{out_path}.{rank}.npy", np.array([out["edges"], sorted(out["sepset"].items()),
+                                                bool(np.array_equal(got, mine))], dtype=object), allow_pickle=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_pc_replicas_record(tmp_path):
+    """Small graphs at N > 1 (bench.py / CLI): replicas + one broadcast of rank 0's result record;
+    every rank decodes the single-process skeleton and sepsets and agrees with its own record."""
+    mp = pytest.importorskip("torch.multiprocessing")
+    import oracle as O
+    csv = os.path.join(REPO, "tests", "golden", "alarm", "alarm_s5000.txt")
+    out = str(tmp_path / "rep")
+    mp.start_processes(_replica_worker, args=(2, _free_port(), csv, out), nprocs=2, join=True,
+                       start_method="spawn")
+    ref = O.OracleDataset(csv=csv).pc_stable(0.05, 1000, 1)
+    for r in range(2):
+        edges, sep, same = np.load(f"{out}.{r}.npy", allow_pickle=True)  # written by this test's own workers
+        assert [tuple(e) for e in edges] == [tuple(e) for e in ref["edges"]]
+        assert dict(sep) == {k: tuple(v) for k, v in ref["sepset"].items()}
+        assert same
