@@ -69,6 +69,7 @@ _SIGS = {
     "fbn_pc_sepsets": [_vp, _vp, _i64, _vp],
     "fbn_pc_timing": [_vp, _vp, _vp],
     "fbn_pc_path": [_vp, _vp],
+    "fbn_jt_tile_program": [_vp, _vp, _vp, _vp, _vp],
     "fbn_pc_result_record": [_vp, _vp, C.c_int64, _vp],
     "fbn_pc_small_eligible": [_vp, C.c_int, _vp],
     "fbn_pc_small_eligible_shape": [C.c_int, C.c_int64, _vp, C.c_int, _vp],
@@ -160,7 +161,9 @@ class _PlanInfo(C.Structure):
                 ("algorithmic_bytes_per_case", C.c_int64), ("num_ops", C.c_int32),
                 ("max_vars_per_table", C.c_int32), ("specialized_eligible", C.c_int32),
                 ("variant", C.c_int32), ("streamed_eligible", C.c_int32), ("streamed_waves", C.c_int32),
-                ("streamed_split_efficiency", C.c_double)]
+                ("streamed_split_efficiency", C.c_double), ("tiled_eligible", C.c_int32),
+                ("tiled_passes", C.c_int32), ("tiled_entry_visits", C.c_int64), ("tiled_lds_bytes", C.c_int64),
+                ("tiled_table_bytes", C.c_int64)]
 
 
 class Network:
@@ -275,6 +278,18 @@ class JunctionTree:
         info = _PlanInfo()
         lib.fbn_jt_plan_info_get(h, C.byref(info))
         self.info = {k: getattr(info, k) for k, _ in _PlanInfo._fields_}
+
+    def tile_program(self):
+        """The tiled kernel's program (variant 5): (passes [n][26] int32, tab int32, initv fp64,
+        geometry dict) -- for host-side checks of its tables (tests/tile_emulator.py)."""
+        g = np.zeros(8, np.int64)
+        lib.fbn_jt_tile_program(self._h, None, None, None, _p(g))
+        passes = np.zeros((int(g[0]), 26), np.int32)
+        tab = np.zeros(max(int(g[1]), 1), np.int32)
+        iv = np.zeros(max(int(g[2]), 1), np.float64)
+        lib.fbn_jt_tile_program(self._h, _p(passes), _p(tab), _p(iv), _p(g))
+        keys = ["n_passes", "n_tab", "n_init", "scr_row", "red_row", "store_rows", "cases_per_wave", "slots"]
+        return passes, tab, iv, dict(zip(keys, (int(x) for x in g)))
 
     def dump_plan(self, plan_path, init_path):
         lib.fbn_jt_plan_dump(self._h, os.fsencode(plan_path), os.fsencode(init_path))

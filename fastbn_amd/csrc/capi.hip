@@ -83,12 +83,10 @@ extern "C" hipError_t fbn_ci_bits_pairs_tiled(const uint32_t *bits, const int32_
                                               long long W, const int32_t *tasks, long long ntasks, int nvars,
                                               long long t0, long long t1, int32_t *counts, int32_t *pairtab,
                                               int num_cu, hipStream_t s);
-extern "C" hipError_t fbn_jt_case_launch(const JtCClique *cls, const int32_t *vrec, const int32_t *aux,
-                                         const double *initv, const int32_t *post, const int32_t *pre,
-                                         const int32_t *vsel, const int8_t *evid, double *marg, int32_t *labels,
-                                         double *ws, int *flags, long long ncases, long long msg_doubles,
-                                         long long gbin_doubles, int nc, int V, int SD, int lds_bins, int grid,
-                                         int dbg, unsigned long long *prof, hipStream_t stream);
+extern "C" hipError_t fbn_jt_tile_launch(const JtTPass *passes, int npass, const int32_t *tab, const double *iv,
+                                         const int8_t *evid, double *marg, int32_t *labels, double *ws, int *flags,
+                                         long long ncases, long long store_rows, long long scr_row, long long red_row,
+                                         int V, int SD, int lds_bytes, int grid, hipStream_t stream);
 extern "C" hipError_t fbn_jt_virt_launch(const JtVClique *cls, const int32_t *aux, const double *initv,
                                          const uint64_t *dig, const int32_t *order, const int32_t *sched,
                                          const int32_t *vsel, const int8_t *evid, double *marg, int32_t *labels,
@@ -167,9 +165,9 @@ struct fbn_jt_plan {
     fbn::JTProgramV vprog;    // variant 4: streamed (virtual) tables, large trees
     bool v_ok = false;
     DevBuf vcl, vaux, viv, vdig, vorder, vsched, vsel;
-    fbn::JTProgramC cprog;    // variant 5: per-case, evidence-reduced (fast order), large trees
-    bool c_ok = false;
-    DevBuf ccl, cvrec, caux, civ, cpost, cpre, cvsel;
+    fbn::JTProgramT tprog;    // variant 5: tiled, JT_T_C cases x JT_T_L entry slots per wave (fast order)
+    bool t_ok = false;
+    DevBuf tpass, ttab, tiv;
     int device = 0, num_cu = 0, waves_per_cu = 0, variant = -1, last_variant = -1;
     // plan-specialized kernel (variant 3)
     bool gen_eligible = false;
@@ -558,15 +556,11 @@ static int JtUpload(fbn_jt_plan *p) {
         if ((rc = up(p->vsched, v.sched.data(), v.sched.size() * 4))) return rc;
         if ((rc = up(p->vsel, v.vsel.data(), v.vsel.size() * 4))) return rc;
     }
-    if (p->c_ok) {
-        const auto &c = p->cprog;
-        if ((rc = up(p->ccl, c.cl.data(), c.cl.size() * sizeof(JtCClique)))) return rc;
-        if ((rc = up(p->cvrec, c.vrec.data(), c.vrec.size() * 4))) return rc;
-        if ((rc = up(p->caux, c.aux.data(), c.aux.size() * 4))) return rc;
-        if ((rc = up(p->civ, c.initv.data(), c.initv.size() * 8))) return rc;
-        if ((rc = up(p->cpost, c.post.data(), c.post.size() * 4))) return rc;
-        if ((rc = up(p->cpre, c.pre.data(), c.pre.size() * 4))) return rc;
-        if ((rc = up(p->cvsel, c.vsel.data(), c.vsel.size() * 4))) return rc;
+    if (p->t_ok) {
+        const auto &t = p->tprog;
+        if ((rc = up(p->tpass, t.passes.data(), t.passes.size() * sizeof(JtTPass)))) return rc;
+        if ((rc = up(p->ttab, t.tab.data(), t.tab.size() * 4))) return rc;
+        if ((rc = up(p->tiv, t.initv.data(), t.initv.size() * 8))) return rc;
     }
     return FBN_OK;
 }
@@ -575,21 +569,34 @@ int fbn_jt_plan_create(const fbn_network *net, int device, fbn_jt_plan **out) {
     if (!net || !out) return SetError(FBN_ERR_ARG, "null pointer");
     auto p = std::unique_ptr<fbn_jt_plan>(new (std::nothrow) fbn_jt_plan());
     if (!p) return SetError(FBN_ERR_NOMEM, "out of memory");
+    static const bool ptime = getenv("FBN_PLAN_TIMING") != nullptr;  // diagnostic: plan phases
+    auto tp0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char *what) {
+        if (!ptime) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "plan %s: %.1f ms\n", what, std::chrono::duration<double, std::milli>(t - tp0).count());
+        tp0 = t;
+    };
     int rc = fbn::BuildJTPlan(net->net, p->host);
     if (rc) return rc;
+    lap("structure");
     rc = fbn::CompileJTProgram(p->host, p->prog);
     if (rc) return rc;
     rc = fbn::CompileJTProgramLDS(p->host, p->lprog);
     if (rc) return rc;
+    lap("interpreter programs");
     rc = fbn::CompileJTProgramV(p->host, p->vprog);
     if (rc && rc != FBN_ERR_LIMIT) return rc;
     p->v_ok = rc == FBN_OK;
     if (!p->v_ok) p->vprog = fbn::JTProgramV();
-    rc = fbn::CompileJTProgramC(p->host, p->cprog);
+    lap("streamed program");
+    // tiled variant: factors of a clique phase staged in LDS up to this many bytes per wave
+    static const int t_lds = getenv("FBN_JT_TLDS") ? atoi(getenv("FBN_JT_TLDS")) : 16384;  // (tuning knob)
+    rc = fbn::CompileJTProgramT(p->host, p->tprog, t_lds);
     if (rc && rc != FBN_ERR_LIMIT) return rc;
-    p->c_ok = rc == FBN_OK;
-    for (int d : p->host.dom) p->c_ok = p->c_ok && d <= 64;
-    if (!p->c_ok) p->cprog = fbn::JTProgramC();
+    p->t_ok = rc == FBN_OK;
+    if (!p->t_ok) p->tprog = fbn::JTProgramT();
+    lap("tiled program");
     p->gen_eligible = fbn::JTCodegenEligible(p->host, nullptr);
     p->device = device;
     if (device >= 0) {  // device < 0: host-only plan (info / dump), runs fail with FBN_ERR_NODEV
@@ -624,6 +631,11 @@ int fbn_jt_plan_info_get(const fbn_jt_plan *p, fbn_jt_plan_info *info) {
     info->streamed_eligible = p->v_ok ? 1 : 0;
     info->streamed_waves = JT_V_WAVES;
     info->streamed_split_efficiency = p->v_ok ? p->vprog.split_efficiency : 0.0;
+    info->tiled_eligible = p->t_ok ? 1 : 0;
+    info->tiled_passes = (int32_t)p->tprog.passes.size();
+    info->tiled_entry_visits = p->tprog.entry_visits;
+    info->tiled_lds_bytes = p->tprog.lds_bytes;
+    info->tiled_table_bytes = (int64_t)p->tprog.tab.size() * 4;
     return FBN_OK;
 }
 
@@ -641,6 +653,22 @@ int fbn_jt_stream_schedule(const fbn_jt_plan *p, int32_t *order, int64_t order_c
     if (sched) {
         if (sched_cap < (int64_t)v.sched.size()) return SetError(FBN_ERR_ARG, "sched buffer too small");
         std::copy(v.sched.begin(), v.sched.end(), sched);
+    }
+    return FBN_OK;
+}
+
+int fbn_jt_tile_program(const fbn_jt_plan *p, int32_t *passes, int32_t *tab, double *initv, int64_t *geometry) {
+    if (!p) return SetError(FBN_ERR_ARG, "null pointer");
+    if (!p->t_ok) return SetError(FBN_ERR_LIMIT, "plan not eligible for the tiled kernel");
+    static_assert(sizeof(JtTPass) == 26 * 4, "JtTPass = 26 int32");
+    const auto &t = p->tprog;
+    if (passes) memcpy(passes, t.passes.data(), t.passes.size() * sizeof(JtTPass));
+    if (tab) memcpy(tab, t.tab.data(), t.tab.size() * 4);
+    if (initv) memcpy(initv, t.initv.data(), t.initv.size() * 8);
+    if (geometry) {
+        const int64_t g[8] = {(int64_t)t.passes.size(), (int64_t)t.tab.size(), (int64_t)t.initv.size(), t.scr_row,
+                              t.red_row, t.store_rows, JT_T_C, JT_T_L};
+        memcpy(geometry, g, sizeof g);
     }
     return FBN_OK;
 }
@@ -697,10 +725,10 @@ int fbn_jt_set_waves_per_cu(fbn_jt_plan *p, int waves) {
 int fbn_jt_set_variant(fbn_jt_plan *p, int variant) {
     if (!p || variant < -1 || variant > 5)
         return SetError(FBN_ERR_ARG, "variant must be -1 (auto), 0 (LDS), 1 (global), 2 (LDS, IEEE division), "
-                                     "3 (specialized), 4 (streamed) or 5 (per-case)");
+                                     "3 (specialized), 4 (streamed) or 5 (tiled)");
     if (variant == 3 && !p->gen_eligible) return SetError(FBN_ERR_ARG, "plan not eligible for the specialized kernel");
     if (variant == 4 && !p->v_ok) return SetError(FBN_ERR_ARG, "plan not eligible for the streamed kernel");
-    if (variant == 5 && !p->c_ok) return SetError(FBN_ERR_ARG, "plan not eligible for the per-case kernel");
+    if (variant == 5 && !p->t_ok) return SetError(FBN_ERR_ARG, "plan not eligible for the tiled kernel");
     p->variant = variant;
     return FBN_OK;
 }
@@ -922,6 +950,7 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
         // specialized kernel when eligible; else the streamed kernel (1.5-2x the interpreters on
         // ALARM and the Munin-like network); the interpreters only for plans it cannot take
         if (p->gen_eligible && GenEnsure(p) == FBN_OK) variant = 3;
+        else if (p->t_ok && JtFast(p)) variant = 5;  // (fast arithmetic order only)
         else if (p->v_ok) variant = 4;
         else variant = (p->lprog.max_table * 64 * 8 * 2 <= (int64_t)kLdsBytes) ? 0 : 1;
     }
@@ -982,41 +1011,30 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
             (rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s)))
             return rc;
     } else if (variant == 5) {
-        // one wave per case (persistent, striding over the cases); per wave: the case's messages
-        // plus a global bin area for bin sets beyond the LDS budget
-        const auto &c = p->cprog;
-        const int lds_env = getenv("FBN_JT_CLDS") ? atoi(getenv("FBN_JT_CLDS")) : 1024;  // (tuning / testing knob)
-        const int lds_bins = std::max(64, std::min(lds_env, 16384));
+        // JT_T_C cases per wave, one wave per workgroup (persistent); per wave: its message store
+        // (messages, partial and reduced bins of the pass in flight) and its LDS factor stage
+        const auto &t = p->tprog;
+        const int64_t ncg = (ncases + JT_T_C - 1) / JT_T_C;
         const int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 8;
-        int grid = (int)std::min<int64_t>(ncases, (int64_t)p->num_cu * wpc);
-        const size_t per_wave = (size_t)(c.msg_doubles + c.max_bins) * 8;
-        const size_t lds = (size_t)lds_bins * 8 + (size_t)((V + 7) & ~7) + (size_t)((c.num_cliques + 7) & ~7) + (size_t)V * 2;
-        if (lds > kLdsBytes) return SetError(FBN_ERR_LIMIT, "per-case kernel: %zu B of LDS per wave", lds);
+        int grid = (int)std::min<int64_t>(ncg, (int64_t)p->num_cu * wpc);
+        const size_t per_wave = (size_t)t.store_rows * JT_T_C * 8;
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+            const size_t have = free_b / 10 * 8 + p->ws.bytes;
+            grid = (int)std::max<int64_t>(1, std::min<int64_t>(grid, (int64_t)(have / per_wave)));
+        }
         if ((rc = p->ws.ensure((size_t)grid * per_wave))) return rc;
         if ((rc = p->flags.ensure((size_t)nblk * 4))) return rc;
         FBN_HIP(hipMemsetAsync(p->flags.p, 0, (size_t)nblk * 4, s));
-        // diagnostics: bits 1/2/4 skip work (wrong results), 8 = per-phase cycle totals
-        // (fbn_jt_debug_op_cycles reads them)
-        const int cdbg = getenv("FBN_JT_CDEBUG") ? atoi(getenv("FBN_JT_CDEBUG")) : 0;
-        if (cdbg & 8) {
-            if ((rc = p->prof.ensure(16 * 8))) return rc;
-            FBN_HIP(hipMemsetAsync(p->prof.p, 0, 16 * 8, s));
-            p->last_grid = 1;
-        }
         FBN_HIP(hipEventRecord(p->ev0, s));
-        hipError_t e = fbn_jt_case_launch(p->ccl.as<JtCClique>(), p->cvrec.as<int32_t>(), p->caux.as<int32_t>(),
-                                          p->civ.as<double>(), p->cpost.as<int32_t>(), p->cpre.as<int32_t>(),
-                                          p->cvsel.as<int32_t>(), d_evidence, marg, labels, p->ws.as<double>(),
-                                          p->flags.as<int>(), ncases, c.msg_doubles, c.max_bins, nc, V, SD, lds_bins,
-                                          grid,
-                                          // diagnostic ablation only (tools/): skip work, wrong results
-                                          cdbg, cdbg & 8 ? p->prof.as<unsigned long long>() : nullptr, s);
+        hipError_t e = fbn_jt_tile_launch(p->tpass.as<JtTPass>(), (int)t.passes.size(), p->ttab.as<int32_t>(),
+                                          p->tiv.as<double>(), d_evidence, marg, labels, p->ws.as<double>(),
+                                          p->flags.as<int>(), ncases, t.store_rows, t.scr_row, t.red_row, V, SD,
+                                          (int)t.lds_bytes, grid, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt kernel launch: %s", hipGetErrorString(e));
         if (p->force_fixup) FBN_HIP(hipMemsetAsync(p->flags.p, 1, (size_t)nblk * 4, s));  // testing only
-        // exact recomputation of the blocks holding a case whose sums left the checked range
-        if (!(cdbg & 7) &&
-            (rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s)))
-            return rc;
+        // exact recomputation of the blocks holding a case group whose pass totals left the checked range
+        if ((rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s))) return rc;
     } else if (variant == 3) {
         // one wave (64 cases) per SIMD: the clique in flight occupies the register file (+ LDS tail)
         int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 4;

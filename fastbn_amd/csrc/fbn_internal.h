@@ -118,21 +118,21 @@ struct JTProgramV {
 // more than 8 * JT_MAX_DIG_WORDS variables, or tables beyond int32 indexing)
 int CompileJTProgramV(const JTPlanHost &plan, JTProgramV &prog);
 
-// per-case variant (jt_case.hip), see jt_program.h
-struct JTProgramC {
-    std::vector<JtCClique> cl;
-    std::vector<int32_t> vrec;   // JT_C_VREC int32 per clique variable
-    std::vector<int32_t> aux;    // child records {Ts, col, dis}, then candidate clique lists
+// tiled variant (jt_tile.hip), see jt_program.h
+struct JTProgramT {
+    std::vector<JtTPass> passes;  // Collect (post-order), then Distribute (pre-order)
+    std::vector<int32_t> tab;     // G / R / outer / bin-digit / marginal / variable / staging records
     std::vector<double> initv;
-    std::vector<int32_t> post, pre;  // Collect (DFS post-order, root excluded) / Distribute (pre-order)
-    std::vector<int32_t> vsel;       // per variable {cand_off, ncand, out_off, dim}
-    int64_t msg_doubles = 0;         // per-wave message slice: Collect messages, then Distribute ones
-    int32_t max_bins = 0;            // largest bin set of any pass (fp64 values)
+    int64_t scr_row = 0;          // wave store rows (JT_T_C fp64 each): messages, then partial bins,
+    int64_t red_row = 0;          // then reduced bins
+    int64_t store_rows = 0;
+    int64_t lds_bytes = 0;        // per wave: the largest set of factors staged at once
+    int64_t entry_visits = 0;     // clique entries summed over all passes (one case)
     int num_cliques = 0, sum_dom = 0;
 };
-// FBN_ERR_LIMIT when the plan does not fit (> JT_C_MAX_CHILDREN children, > 64 variables in a
-// clique, > 65535 cliques, tables beyond int32 indexing)
-int CompileJTProgramC(const JTPlanHost &plan, JTProgramC &prog);
+// FBN_ERR_LIMIT when the plan does not fit (a domain > JT_T_MAXDIM states, > JT_T_MAXF - 1 children,
+// > 32 digit bits in a clique, tables beyond int32 indexing).  lds_budget: bytes of factors per wave.
+int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget);
 
 // plan-specialized kernel source (jt_codegen.cpp): eligibility and generation.  The generated
 // kernel's per-wave workspace holds wave_entries rows of 64 fp64 lanes; initv is its constant input.

@@ -89,28 +89,41 @@ struct JtVClique {
 #define JT_V_MAX_CHILDREN 6
 #define JT_V_WAVES 2  // waves sharing one 64-case block (disjoint subtrees in parallel)
 
-// ---- per-case variant, jt_case.hip (fast arithmetic order only): one wave = ONE evidence case,
-// lanes over that case's evidence-reduced clique entries (the reference's TableReduction,
-// src/PotentialTable.cpp:309-396, as an index space instead of a copied table: observed digits are
-// fixed, only the consistent entries are visited).  A pass over a clique forms every entry as
-//     init(e) * M_1(s_1(e)) * ... * M_k(s_k(e)) [* M_parent(s_up(e))]
-// (child Collect messages, then the parent's Distribute message) and accumulates the normalization
-// sum and the separator / marginal bins of that product; the per-step normalizations of the
-// reference cancel in the normalized result, so every message equals the reference's up to
-// rounding (one pass per clique and direction, no table is stored).  Messages of one case live in
-// the wave's slice of a global workspace as plain fp64 vectors (one 8-byte slot per separator
-// entry, not a 512-byte 64-case row).
-#define JT_C_MAX_CHILDREN 6
-#define JT_C_VREC 12  // per clique variable: {var, dim, cum, up-separator stride, child separator
-                      // strides [JT_C_MAX_CHILDREN], output offset of the variable, division magic}
-struct JtCClique {
-    int32_t T, nv, k, root;          // entries, variables, children, is the root
+// ---- tiled variant, jt_tile.hip (fast arithmetic order; the Munin-class default): one wave = JT_T_C
+// evidence cases x JT_T_L entry slots.  A pass over a clique splits the clique's variables into G
+// (lane variables: slot s of a round takes G-configuration round * JT_T_L + s) and R (a stream of
+// configurations every lane walks in the same order: outer R-configurations over the output's
+// remaining variables, inner ones over the rest).  Entry e = G-part + R-part, so every index map is
+// one per-lane constant plus one wave-uniform offset (scalar loads of the R table); an entry is
+//     init(e) * M_1(s_1(e)) * ... * M_F(s_F(e))   (0 if it contradicts the case's evidence)
+// with the factors = the child Collect messages [+ the parent's Distribute message].  A lane sums
+// its entries over the inner stream in a register and stores the sum once per outer configuration
+// into the output's bin (distinct per lane: G holds output variables, or extra variables E whose
+// partial bins the post sweep adds up), so no atomics and a fixed summation order.  Messages are
+// 64-byte rows [separator entry][JT_T_C cases]: the factors of a clique fit LDS, the per-case
+// normalizations of the reference cancel in the normalized results (fast order, within 1e-12).
+#define JT_T_C 8            // cases per wave
+#define JT_T_L 8            // entry slots per case (JT_T_C * JT_T_L = 64 lanes)
+#define JT_T_MAXF 7         // factors per pass: <= 6 child messages + the parent message
+#define JT_T_MAXDIM 8       // state counts the marginal sweep handles (one slot per value)
+enum JtTKind : int32_t { JT_T_COL = 0, JT_T_DIS = 1, JT_T_MARG = 2 };
+struct JtTPass {
+    int32_t kind, clique, nf, mode;  // mode: 0 every factor in LDS, 1 every factor global, 2 all but the
+                                     // last (the parent message) in LDS
+    int32_t nG, rounds, nRo, nRi;    // G-configurations, rounds of JT_T_L, outer / inner R stream
+    int32_t g_off, r_off, o_off;     // tab: G records (4 + nf ints: e, digit word, bin, pad, factor
+                                     // byte offsets), R records (2 + nf ints: e, digit word, factor
+                                     // byte offsets), outer records (1 int: bin offset)
+    int32_t nE, nbins;               // partial bins per output bin (E configurations), output bins
+    int32_t dest_row, col_row;       // output message rows (-1: MARG), the child's Collect message (DIS)
+    int32_t bdig_off;                // tab: packed digits of every output bin (marginal sweep)
+    int32_t nmv, mv_off;             // marginals taken from this pass's bins: {var, out_off, dim, shift, mask}
     int32_t iv_off;                  // initial potentials (fp64 index)
-    int32_t var_off;                 // first of nv JT_C_VREC records
-    int32_t up_Ts, up_col, up_dis;   // upstream separator: entries, Collect / Distribute message
-                                     // offsets (fp64 index into the wave's message slice)
-    int32_t child_off;               // aux: k records {Ts, col, dis}
-    int32_t id, dbins;               // clique id; bins of its Distribute pass (sum child Ts + 4 * max dim)
+    int32_t nv, vars_off;            // clique variables {var, shift, mask} (evidence digit fields)
+    uint32_t gfields;                // digit fields of the G variables
+    int32_t first;                   // first pass of a clique phase: the lanes' evidence words, then the
+    int32_t nstage, stage_off;       // factors staged into LDS ({src row, rows, lds byte offset} records)
+    int32_t pad1;
 };
 
 #endif

@@ -1,0 +1,435 @@
+// jt_tile_plan.cpp -- compiles the host plan into the passes of the tiled kernel (jt_tile.hip,
+// descriptor JtTPass in jt_program.h).
+//
+// Per clique and direction (Collect in DFS post-order, Distribute in DFS pre-order, children in
+// clique_down order = the reference's multiplication order, src/JunctionTree.cpp:1282-1302):
+//   Collect      one pass, output = the upstream separator (SeparatorLevelCollectionOptimized,
+//                src/JunctionTree.cpp:1056-1148), factors = the children's Collect messages;
+//   Distribute   one pass per child, output = that child's separator (SeparatorLevelDistribution,
+//                :700-816), factors = the children's Collect messages + the parent's Distribute
+//                message; one more pass for the clique's private variables (in no separator) when
+//                their marginals are needed.
+// Marginals (GetProbabilitiesOneNode, :1392-1454): after Distribute every clique holding a variable
+// has the same marginal of it (a calibrated tree), so each variable's marginal is summed from the
+// bins of the smallest Distribute output that contains it -- no pass of its own unless private.
+//
+// G / R split of a pass: G = output variables whose state product fills the JT_T_L slots of a round
+// best (plus extra variables E when the output has fewer than JT_T_L bins: their partial bins are
+// added by the post sweep), R outer = the remaining output variables, R inner = the rest.  Every
+// index map is linear in the digits (entry = sum d_v cum_v, separator index = sum d_v stride_v),
+// so a G record and an R record hold the two halves of each map.
+#include <algorithm>
+#include <climits>
+#include <cstdlib>
+#include <functional>
+
+#include "fbn_internal.h"
+
+namespace fbn {
+
+namespace {
+
+int PosIn(const std::vector<int> &vars, int v) {
+    for (size_t i = 0; i < vars.size(); ++i)
+        if (vars[i] == v) return (int)i;
+    return -1;
+}
+
+struct Factor {
+    const Table *sep;
+    int64_t row;   // first row of the message in the wave store
+    int lds_off;   // byte offset in the wave's LDS, -1: read from the wave store
+};
+
+// Cartesian enumeration of the digits of `pos` (positions into the clique's variables), last fastest
+void ForEachConfig(const Table &t, const std::vector<int> &pos, const std::function<void(const std::vector<int> &)> &fn) {
+    std::vector<int> d(pos.size(), 0);
+    while (true) {
+        fn(d);
+        int j = (int)pos.size() - 1;
+        while (j >= 0 && ++d[j] == t.dims[pos[j]]) d[j--] = 0;
+        if (j < 0) break;
+    }
+}
+
+int64_t Prod(const Table &t, const std::vector<int> &pos) {
+    int64_t p = 1;
+    for (int i : pos) p *= t.dims[i];
+    return p;
+}
+
+// slots used / slots occupied over the rounds of a G of `n` configurations
+double SlotEfficiency(int64_t n) { return (double)n / (double)(JT_T_L * ((n + JT_T_L - 1) / JT_T_L)); }
+
+// best subset of `cand` (positions) by slot efficiency, ties -> fewer configurations; `base` always in
+std::vector<int> BestSubset(const Table &t, const std::vector<int> &base, const std::vector<int> &cand, bool need_full) {
+    const int m = (int)cand.size();
+    std::vector<int> best = base;
+    double be = -1.0;
+    int64_t bn = INT64_MAX;
+    for (int mask = 0; mask < (1 << m); ++mask) {
+        std::vector<int> g = base;
+        for (int i = 0; i < m; ++i)
+            if (mask >> i & 1) g.push_back(cand[i]);
+        if (g.empty()) continue;
+        const int64_t n = Prod(t, g);
+        if (need_full && n < JT_T_L && mask != (1 << m) - 1) continue;  // fill a round when possible
+        const double e = SlotEfficiency(n);
+        if (e > be + 1e-9 || (e > be - 1e-9 && n < bn)) be = e, bn = n, best = g;
+    }
+    return best;
+}
+
+}  // namespace
+
+int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) {
+    prog = JTProgramT();
+    const int nc = (int)plan.cliques.size(), ns = (int)plan.seps.size(), V = plan.num_nodes;
+    for (int d : plan.dom)
+        if (d < 1 || d > JT_T_MAXDIM) return SetError(FBN_ERR_LIMIT, "a domain of %d states (tiled variant: 1..%d)", d, JT_T_MAXDIM);
+    for (int c = 0; c < nc; ++c) {
+        const Table &t = plan.cliques[c];
+        if ((int)plan.clique_down[c].size() + 1 > JT_T_MAXF)
+            return SetError(FBN_ERR_LIMIT, "clique %d has %zu children (tiled variant: max %d)", c,
+                            plan.clique_down[c].size(), JT_T_MAXF - 1);
+        int bits = 0;
+        for (int d : t.dims) {
+            int w = 1;
+            while ((1 << w) < d) ++w;
+            bits += w;
+        }
+        if (bits > 32) return SetError(FBN_ERR_LIMIT, "clique %d: %d digit bits (tiled variant: max 32)", c, bits);
+        if (t.size() >= ((int64_t)1 << 26)) return SetError(FBN_ERR_LIMIT, "clique table of %lld entries", (long long)t.size());
+    }
+    prog.num_cliques = nc;
+    std::vector<int64_t> out_off(V);
+    for (int v = 0; v < V; ++v) out_off[v] = prog.sum_dom, prog.sum_dom += plan.dom[v];
+    // wave store rows (JT_T_C doubles each): Collect messages, Distribute messages, partial bins of the
+    // pass in flight, its reduced bins
+    std::vector<int64_t> col(ns), dis(ns);
+    int64_t rows = 0;
+    for (int s = 0; s < ns; ++s) col[s] = rows, rows += plan.seps[s].size();
+    for (int s = 0; s < ns; ++s) dis[s] = rows, rows += plan.seps[s].size();
+    prog.scr_row = rows;
+
+    // clique digit fields (evidence masks), initial potentials
+    std::vector<std::vector<int>> sh(nc), fm(nc);
+    std::vector<int32_t> iv_off(nc), vars_off(nc);
+    for (int c = 0; c < nc; ++c) {
+        const Table &t = plan.cliques[c];
+        int bits = 0;
+        vars_off[c] = (int32_t)prog.tab.size();
+        for (size_t j = 0; j < t.vars.size(); ++j) {
+            int w = 1;
+            while ((1 << w) < t.dims[j]) ++w;
+            sh[c].push_back(bits), fm[c].push_back((1 << w) - 1);
+            prog.tab.push_back(t.vars[j]);
+            prog.tab.push_back(bits);
+            prog.tab.push_back((1 << w) - 1);
+            bits += w;
+        }
+        iv_off[c] = (int32_t)prog.initv.size();
+        prog.initv.insert(prog.initv.end(), t.pot.begin(), t.pot.end());
+    }
+    if (prog.initv.size() > (size_t)INT32_MAX / 8) return SetError(FBN_ERR_LIMIT, "clique tables too large for the tiled variant");
+
+    // DFS orders
+    std::vector<int> post, pre;
+    {
+        std::vector<std::pair<int, size_t>> st{{plan.root, 0}};
+        while (!st.empty()) {
+            auto &top = st.back();
+            const int c = top.first;
+            if (top.second == 0) pre.push_back(c);
+            if (top.second < plan.clique_down[c].size()) {
+                const int ch = plan.sep_down[plan.clique_down[c][top.second++]];
+                st.push_back({ch, 0});
+            } else {
+                post.push_back(c);
+                st.pop_back();
+            }
+        }
+        if ((int)pre.size() != nc) return SetError(FBN_ERR_LIMIT, "tree traversal covers %zu of %d cliques", pre.size(), nc);
+    }
+
+    // marginal sources: the smallest separator holding the variable (its SEPDIS pass), else the
+    // private-variable pass of the only clique holding it
+    std::vector<int> src_sep(V, -1);
+    for (int s = 0; s < ns; ++s)
+        for (int v : plan.seps[s].vars)
+            if (src_sep[v] < 0 || plan.seps[s].size() < plan.seps[src_sep[v]].size()) src_sep[v] = s;
+    std::vector<std::vector<int>> priv(nc);  // positions of private variables
+    {
+        std::vector<int> holder(V, -1), count(V, 0);
+        for (int c = 0; c < nc; ++c)
+            for (int v : plan.cliques[c].vars) holder[v] = c, ++count[v];
+        for (int v = 0; v < V; ++v) {
+            if (count[v] == 0) return SetError(FBN_ERR_ARG, "variable %d appears in no clique", v);
+            if (src_sep[v] < 0) {
+                if (count[v] != 1) return SetError(FBN_ERR_ARG, "internal: variable %d in %d cliques, no separator", v, count[v]);
+                priv[holder[v]].push_back(PosIn(plan.cliques[holder[v]].vars, v));
+            }
+        }
+        for (auto &p : priv) std::sort(p.begin(), p.end());
+    }
+
+    const int budget_rows = std::max(0, lds_budget) / (JT_T_C * 8);
+    int64_t max_x = 1, max_bins = 1;
+
+    // one pass: clique c, output variables `opos` (positions) laid out by `ocum` (stride of each
+    // output variable in the output's bin index), factors, destination
+    auto build_pass = [&](int c, int kind, const std::vector<int> &opos, const std::vector<int64_t> &ocum,
+                          int64_t nbins, const std::vector<Factor> &fac, int64_t dest_row, int64_t col_row,
+                          const std::vector<int> &mvars, bool first, int nstage, int32_t stage_off) -> int {
+        const Table &t = plan.cliques[c];
+        const int nv = (int)t.vars.size(), nf = (int)fac.size();
+        JtTPass P{};
+        P.kind = kind;
+        P.clique = c;
+        P.nf = nf;
+        bool all_lds = true, all_glb = true, last_glb_only = nf > 0;
+        for (int j = 0; j < nf; ++j) {
+            all_lds = all_lds && fac[j].lds_off >= 0;
+            all_glb = all_glb && fac[j].lds_off < 0;
+            if (j < nf - 1) last_glb_only = last_glb_only && fac[j].lds_off >= 0;
+            else last_glb_only = last_glb_only && fac[j].lds_off < 0;
+        }
+        P.mode = (nf == 0 || all_lds) ? 0 : all_glb ? 1 : 2;
+        if (nf > 0 && !all_lds && !all_glb && !last_glb_only)
+            return SetError(FBN_ERR_ARG, "internal: factor placement of clique %d", c);
+        // G: output variables first (no partial bins), extra variables when the output is small
+        std::vector<int> G;
+        std::vector<int> others;
+        for (int j = 0; j < nv; ++j)
+            if (std::find(opos.begin(), opos.end(), j) == opos.end()) others.push_back(j);
+        if (Prod(t, opos) >= JT_T_L || others.empty()) G = BestSubset(t, {}, opos, false);
+        else G = BestSubset(t, opos, others, true);
+        if (G.empty()) G = opos.empty() ? std::vector<int>{} : opos;
+        std::vector<int> E, RO, RI;
+        for (int j : G)
+            if (std::find(opos.begin(), opos.end(), j) == opos.end()) E.push_back(j);
+        for (int j : opos)
+            if (std::find(G.begin(), G.end(), j) == G.end()) RO.push_back(j);
+        for (int j = 0; j < nv; ++j)
+            if (std::find(G.begin(), G.end(), j) == G.end() && std::find(RO.begin(), RO.end(), j) == RO.end())
+                RI.push_back(j);
+        const int64_t nE = Prod(t, E), nG = G.empty() ? 1 : Prod(t, G);
+        P.nG = (int32_t)nG;
+        P.rounds = (int32_t)((nG + JT_T_L - 1) / JT_T_L);
+        P.nRo = (int32_t)Prod(t, RO);
+        P.nRi = (int32_t)Prod(t, RI);
+        P.nE = (int32_t)nE;
+        P.nbins = (int32_t)nbins;
+        max_x = std::max(max_x, nbins * nE);
+        max_bins = std::max(max_bins, nbins);
+        // factor strides per clique variable
+        std::vector<std::vector<int64_t>> fs(nf, std::vector<int64_t>(nv, 0));
+        for (int j = 0; j < nf; ++j)
+            for (int i = 0; i < nv; ++i) {
+                const int l = PosIn(fac[j].sep->vars, t.vars[i]);
+                fs[j][i] = l >= 0 ? fac[j].sep->cum[l] : 0;
+            }
+        std::vector<int64_t> ecum(nv, 0), ocum_p(nv, 0);
+        {
+            int64_t m = 1;
+            for (int i = (int)E.size() - 1; i >= 0; --i) ecum[E[i]] = m, m *= t.dims[E[i]];
+            for (size_t i = 0; i < opos.size(); ++i) ocum_p[opos[i]] = ocum[i];
+        }
+        auto fbase = [&](int j) -> int64_t { return fac[j].lds_off >= 0 ? fac[j].lds_off : fac[j].row * (JT_T_C * 8); };
+        uint32_t gf = 0;
+        for (int j : G) gf |= (uint32_t)fm[c][j] << sh[c][j];
+        P.gfields = gf;
+        // G records
+        P.g_off = (int32_t)prog.tab.size();
+        ForEachConfig(t, G, [&](const std::vector<int> &d) {
+            int64_t e = 0, x = 0;
+            uint32_t dw = 0;
+            for (size_t i = 0; i < G.size(); ++i) {
+                const int j = G[i];
+                e += d[i] * t.cum[j];
+                dw |= (uint32_t)d[i] << sh[c][j];
+                x += d[i] * (ocum_p[j] * nE + ecum[j]);
+            }
+            prog.tab.push_back((int32_t)e);
+            prog.tab.push_back((int32_t)dw);
+            prog.tab.push_back((int32_t)x);
+            prog.tab.push_back(0);
+            for (int f = 0; f < nf; ++f) {
+                int64_t o = fbase(f);
+                for (size_t i = 0; i < G.size(); ++i) o += d[i] * fs[f][G[i]] * (JT_T_C * 8);
+                prog.tab.push_back((int32_t)o);
+            }
+        });
+        // R records: outer over RO, inner over RI (odometers; per-variable increments of every map)
+        P.r_off = (int32_t)prog.tab.size();
+        std::vector<int32_t> otab;
+        {
+            const int RS = 2 + nf;
+            const int64_t nR = Prod(t, RO) * Prod(t, RI);
+            std::vector<int> Rv(RO);
+            Rv.insert(Rv.end(), RI.begin(), RI.end());  // outer digits first: last RI digit fastest
+            const int nr = (int)Rv.size();
+            std::vector<int64_t> inc((size_t)nr * RS);  // per R variable: entry, digit word, factor offsets
+            for (int i = 0; i < nr; ++i) {
+                const int j = Rv[i];
+                inc[(size_t)i * RS + 0] = t.cum[j];
+                inc[(size_t)i * RS + 1] = (int64_t)1 << sh[c][j];
+                for (int f = 0; f < nf; ++f) inc[(size_t)i * RS + 2 + f] = fs[f][j] * (JT_T_C * 8);
+            }
+            const size_t base = prog.tab.size();
+            prog.tab.resize(base + (size_t)nR * RS);
+            int32_t *out = prog.tab.data() + base;
+            int64_t cur[2 + JT_T_MAXF] = {0};
+            std::vector<int> d(nr, 0);
+            for (int64_t k = 0; k < nR; ++k) {
+                for (int q = 0; q < RS; ++q) out[k * RS + q] = (int32_t)cur[q];
+                int i = nr - 1;
+                while (i >= 0) {
+                    const int j = Rv[i];
+                    if (++d[i] < t.dims[j]) {
+                        for (int q = 0; q < RS; ++q) cur[q] += inc[(size_t)i * RS + q];
+                        break;
+                    }
+                    for (int q = 0; q < RS; ++q) cur[q] -= inc[(size_t)i * RS + q] * (t.dims[j] - 1);
+                    d[i--] = 0;
+                }
+            }
+            ForEachConfig(t, RO, [&](const std::vector<int> &dout) {
+                int64_t xo = 0;
+                for (size_t i = 0; i < RO.size(); ++i) xo += dout[i] * ocum_p[RO[i]] * nE;
+                otab.push_back((int32_t)xo);
+            });
+        }
+        P.o_off = (int32_t)prog.tab.size();
+        prog.tab.insert(prog.tab.end(), otab.begin(), otab.end());
+        P.dest_row = (int32_t)dest_row;
+        P.col_row = (int32_t)col_row;
+        // packed digits of every output bin, fields of the output variables in output order
+        P.bdig_off = (int32_t)prog.tab.size();
+        std::vector<int> osh(opos.size()), ofm(opos.size());
+        {
+            int bits = 0;
+            for (size_t i = 0; i < opos.size(); ++i) {
+                int w = 1;
+                while ((1 << w) < t.dims[opos[i]]) ++w;
+                osh[i] = bits, ofm[i] = (1 << w) - 1, bits += w;
+            }
+        }
+        if (!mvars.empty()) {
+            std::vector<int32_t> bd((size_t)nbins, 0);
+            ForEachConfig(t, opos, [&](const std::vector<int> &d) {
+                int64_t b = 0;
+                uint32_t w = 0;
+                for (size_t i = 0; i < opos.size(); ++i) b += d[i] * ocum[i], w |= (uint32_t)d[i] << osh[i];
+                bd[(size_t)b] = (int32_t)w;
+            });
+            prog.tab.insert(prog.tab.end(), bd.begin(), bd.end());
+        }
+        P.nmv = (int32_t)mvars.size();
+        P.mv_off = (int32_t)prog.tab.size();
+        for (int v : mvars) {
+            const int i = PosIn(plan.cliques[c].vars, v);
+            const int oi = (int)(std::find(opos.begin(), opos.end(), i) - opos.begin());
+            prog.tab.push_back(v);
+            prog.tab.push_back((int32_t)out_off[v]);
+            prog.tab.push_back(plan.dom[v]);
+            prog.tab.push_back(osh[oi]);
+            prog.tab.push_back(ofm[oi]);
+        }
+        P.iv_off = iv_off[c];
+        P.nv = nv;
+        P.vars_off = vars_off[c];
+        P.first = first ? 1 : 0;
+        P.nstage = first ? nstage : 0;
+        P.stage_off = stage_off;
+        prog.passes.push_back(P);
+        prog.entry_visits += t.size();
+        if (prog.tab.size() > (size_t)INT32_MAX / 2) return SetError(FBN_ERR_LIMIT, "device program too large for the tiled variant");
+        return FBN_OK;
+    };
+
+    // factor placement of one clique phase: every factor in LDS if they fit, else all but the last
+    // (the parent message, Distribute) if those fit, else none; staging records for the LDS ones
+    auto place = [&](std::vector<Factor> &fac, bool parent_last, int *nstage, int32_t *stage_off) {
+        int64_t tot = 0, head = 0;
+        for (size_t j = 0; j < fac.size(); ++j) {
+            tot += fac[j].sep->size();
+            if (j + 1 < fac.size() || !parent_last) head += fac[j].sep->size();
+        }
+        size_t n_lds = 0;
+        if (tot <= budget_rows) n_lds = fac.size();
+        else if (parent_last && head <= budget_rows) n_lds = fac.size() - 1;
+        *stage_off = (int32_t)prog.tab.size();
+        *nstage = 0;
+        int64_t off = 0;
+        for (size_t j = 0; j < fac.size(); ++j) {
+            if (j < n_lds) {
+                fac[j].lds_off = (int)(off * JT_T_C * 8);
+                prog.tab.push_back((int32_t)fac[j].row);
+                prog.tab.push_back((int32_t)fac[j].sep->size());
+                prog.tab.push_back(fac[j].lds_off);
+                off += fac[j].sep->size();
+                ++*nstage;
+            } else {
+                fac[j].lds_off = -1;
+            }
+        }
+        prog.lds_bytes = std::max<int64_t>(prog.lds_bytes, off * JT_T_C * 8);
+    };
+
+    int rc;
+    // ---- Collect (post-order, the root has no upstream separator)
+    for (int c : post) {
+        if (c == plan.root) continue;
+        std::vector<Factor> fac;
+        for (int s : plan.clique_down[c]) fac.push_back({&plan.seps[s], col[s], -1});
+        int nst;
+        int32_t so;
+        place(fac, false, &nst, &so);
+        const int s = plan.clique_up[c];
+        const Table &sp = plan.seps[s];
+        std::vector<int> opos;
+        for (int v : sp.vars) opos.push_back(PosIn(plan.cliques[c].vars, v));
+        if ((rc = build_pass(c, JT_T_COL, opos, std::vector<int64_t>(sp.cum.begin(), sp.cum.end()), sp.size(), fac,
+                             col[s], -1, {}, true, nst, so)))
+            return rc;
+    }
+    // ---- Distribute (pre-order): one pass per child, then the private variables
+    for (int c : pre) {
+        const Table &t = plan.cliques[c];
+        std::vector<Factor> fac;
+        for (int s : plan.clique_down[c]) fac.push_back({&plan.seps[s], col[s], -1});
+        const bool has_parent = c != plan.root;
+        if (has_parent) fac.push_back({&plan.seps[plan.clique_up[c]], dis[plan.clique_up[c]], -1});
+        int nst;
+        int32_t so;
+        place(fac, has_parent, &nst, &so);
+        bool first = true;
+        for (int s : plan.clique_down[c]) {
+            const Table &sp = plan.seps[s];
+            std::vector<int> opos, mv;
+            for (int v : sp.vars) opos.push_back(PosIn(t.vars, v));
+            for (int v : sp.vars)
+                if (src_sep[v] == s) mv.push_back(v);
+            if ((rc = build_pass(c, JT_T_DIS, opos, std::vector<int64_t>(sp.cum.begin(), sp.cum.end()), sp.size(), fac,
+                                 dis[s], col[s], mv, first, nst, so)))
+                return rc;
+            first = false;
+        }
+        if (!priv[c].empty()) {
+            std::vector<int64_t> ocum(priv[c].size());
+            int64_t m = 1;
+            for (int i = (int)priv[c].size() - 1; i >= 0; --i) ocum[i] = m, m *= t.dims[priv[c][i]];
+            std::vector<int> mv;
+            for (int j : priv[c]) mv.push_back(t.vars[j]);
+            if ((rc = build_pass(c, JT_T_MARG, priv[c], ocum, m, fac, -1, -1, mv, first, nst, so)))
+                return rc;
+        }
+    }
+    prog.red_row = prog.scr_row + max_x;
+    prog.store_rows = prog.red_row + max_bins;
+    if (prog.store_rows * JT_T_C * 8 > INT32_MAX) return SetError(FBN_ERR_LIMIT, "junction tree too large for the tiled variant");
+    return FBN_OK;
+}
+
+}  // namespace fbn

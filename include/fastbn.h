@@ -94,6 +94,11 @@ typedef struct {
     int32_t streamed_eligible;    /* the streamed kernel (variant 4) can take the plan */
     int32_t streamed_waves;       /* waves sharing one 64-case block in variant 4 */
     double streamed_split_efficiency; /* modelled parallel efficiency of their subtree split */
+    int32_t tiled_eligible;       /* the tiled kernel (variant 5, fast order) can take the plan */
+    int32_t tiled_passes;         /* its clique passes per case group */
+    int64_t tiled_entry_visits;   /* clique entries summed over those passes (one case) */
+    int64_t tiled_lds_bytes;      /* LDS per wave for staged factors */
+    int64_t tiled_table_bytes;    /* its index tables (G / R records, ...) */
 } fbn_jt_plan_info;
 
 /* Build the case-independent schedule (JunctionTree ctor, src/JunctionTree.cpp:3-46:
@@ -174,6 +179,11 @@ int fbn_jt_kernel_cache_path(const fbn_jt_plan *p, char *buf, int64_t cap);
 int fbn_jt_kernel_build(const fbn_jt_plan *p);
 /* Compile options of the specialized kernel, '\n'-separated. */
 int fbn_jt_kernel_options(char *buf, int64_t cap);
+/* The tiled kernel's program (variant 5, jt_program.h JtTPass): passes [n_passes] (26 int32 each),
+ * index tables [n_tab], initial potentials [n_init]; geometry = {n_passes, n_tab, n_init,
+ * partial-bin row, reduced-bin row, store rows, cases per wave, slots per case}.  Buffers may be
+ * NULL (sizes only).  For tests that execute the tables on the host (tests/tile_emulator.py). */
+int fbn_jt_tile_program(const fbn_jt_plan *p, int32_t *passes, int32_t *tab, double *initv, int64_t *geometry);
 int fbn_jt_plan_destroy(fbn_jt_plan *p);
 
 /* ------------------------------------------------------------------ CI tests (G^2) */

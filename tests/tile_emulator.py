@@ -1,0 +1,92 @@
+"""TEST INFRASTRUCTURE: executes the tiled kernel's program (variant 5, fastbn_amd/csrc/jt_tile.hip,
+tables from jt_tile_plan.cpp via fbn_jt_tile_program) on the host with numpy, one case at a time,
+so that the plan compiler's G / R records, factor offsets, LDS staging records, output bins and
+marginal sources are checked against the oracle without a GPU (tests/test_host.py).  Same algebra
+as the kernel (entry = G-part + R-part; w = init * prod factors, 0 against the evidence; partial
+bins -> output bins -> messages / marginals), different summation order (numpy), so results agree
+with the oracle to ~1e-14, not bit for bit.  Never used by the product path."""
+import numpy as np
+
+# JtTPass field order (jt_program.h)
+F = ["kind", "clique", "nf", "mode", "nG", "rounds", "nRo", "nRi", "g_off", "r_off", "o_off", "nE", "nbins",
+     "dest_row", "col_row", "bdig_off", "nmv", "mv_off", "iv_off", "nv", "vars_off", "gfields", "first", "nstage",
+     "stage_off", "pad1"]
+COL, DIS, MARG = 0, 1, 2
+
+
+def run_case(prog, ev_row, sum_dom, lds_bytes=1 << 20):
+    """One evidence case (int8 [V], -1 unobserved) -> (label, marginals [sum_dom])."""
+    passes, tab, iv, geo = prog
+    C = geo["cases_per_wave"]
+    row_b = C * 8  # bytes per message row (the kernel's [entry][C cases] layout; this case is case 0)
+    store = np.zeros(geo["store_rows"])
+    lds = np.zeros(lds_bytes // 8)
+    out = np.zeros(sum_dom)
+    label = None
+    M = W = 0
+    for prow in passes:
+        P = dict(zip(F, (int(x) for x in prow)))
+        P["gfields"] &= 0xFFFFFFFF
+        nf = P["nf"]
+        if P["first"]:
+            M = W = 0
+            for j in range(P["nv"]):
+                var, sh, fm = tab[P["vars_off"] + 3 * j:P["vars_off"] + 3 * j + 3]
+                x = int(ev_row[var])
+                if x >= 0:
+                    M |= int(fm) << int(sh)
+                    W |= x << int(sh)
+            for k in range(P["nstage"]):
+                src, rows, dst = (int(v) for v in tab[P["stage_off"] + 3 * k:P["stage_off"] + 3 * k + 3])
+                lds[dst // 8:dst // 8 + rows * C:C] = store[src:src + rows]
+        mv = [tuple(int(v) for v in tab[P["mv_off"] + 5 * m:P["mv_off"] + 5 * m + 5]) for m in range(P["nmv"])]
+        if P["kind"] == MARG and all(int(ev_row[v]) >= 0 for v, *_ in mv):
+            for var, off, dim, _, _ in mv:
+                out[off:off + dim] = 0.0
+            continue
+        nG, nRo, nRi = P["nG"], P["nRo"], P["nRi"]
+        g = tab[P["g_off"]:P["g_off"] + nG * (4 + nf)].reshape(nG, 4 + nf).astype(np.int64)
+        r = tab[P["r_off"]:P["r_off"] + nRo * nRi * (2 + nf)].reshape(nRo * nRi, 2 + nf).astype(np.int64)
+        otab = tab[P["o_off"]:P["o_off"] + nRo].astype(np.int64)
+        e = g[:, 0:1] + r[None, :, 0]
+        dw = (g[:, 1:2] & 0xFFFFFFFF) | (r[None, :, 1] & 0xFFFFFFFF)
+        ok = ((dw ^ W) & M) == 0
+        x = iv[P["iv_off"] + e].copy()
+        for j in range(nf):
+            off = g[:, 4 + j:5 + j] + r[None, :, 2 + j]
+            in_lds = P["mode"] == 0 or (P["mode"] == 2 and j < nf - 1)
+            x *= lds[off // 8] if in_lds else store[off // row_b]
+        x[~ok] = 0.0
+        acc = x.reshape(nG, nRo, nRi).sum(axis=2)
+        xidx = g[:, 2:3] + otab[None, :]
+        nb, nE = P["nbins"], P["nE"]
+        part = np.zeros(nb * nE)
+        part[xidx.reshape(-1)] = acc.reshape(-1)
+        S = acc.sum()
+        v = part.reshape(nb, nE).sum(axis=1)
+        if P["kind"] == COL:
+            store[P["dest_row"]:P["dest_row"] + nb] = v / S
+        elif P["kind"] == DIS:
+            old = store[P["col_row"]:P["col_row"] + nb]
+            with np.errstate(divide="ignore", invalid="ignore"):
+                store[P["dest_row"]:P["dest_row"] + nb] = np.where(old == 0.0, 0.0, (v / S) / old)
+        bd = tab[P["bdig_off"]:P["bdig_off"] + nb].astype(np.int64) & 0xFFFFFFFF
+        for var, off, dim, sh, fm in mv:
+            if int(ev_row[var]) >= 0:
+                out[off:off + dim] = 0.0
+                continue
+            dg = (bd >> sh) & fm
+            a = np.array([v[dg == d].sum() for d in range(dim)])
+            out[off:off + dim] = a / a.sum()
+            if var == 0:
+                label = int(np.argmax(out[off:off + dim]))
+    return label, out
+
+
+def run(prog, ev, sum_dom):
+    labs, margs = [], []
+    for row in ev:
+        lab, m = run_case(prog, row, sum_dom)
+        labs.append(-1 if lab is None else lab)
+        margs.append(m)
+    return np.array(labs, np.int32), np.stack(margs)
