@@ -86,7 +86,8 @@ extern "C" hipError_t fbn_ci_bits_pairs_tiled(const uint32_t *bits, const int32_
 extern "C" hipError_t fbn_jt_tile_launch(const JtTPass *passes, int npass, const int32_t *tab, const double *iv,
                                          const int8_t *evid, double *marg, int32_t *labels, double *ws, int *flags,
                                          long long ncases, long long store_rows, long long scr_row, long long red_row,
-                                         int V, int SD, int lds_bytes, int grid, hipStream_t stream);
+                                         int V, int SD, int lds_bytes, int grid, unsigned long long *prof,
+                                         hipStream_t stream);
 extern "C" hipError_t fbn_jt_virt_launch(const JtVClique *cls, const int32_t *aux, const double *initv,
                                          const uint64_t *dig, const int32_t *order, const int32_t *sched,
                                          const int32_t *vsel, const int8_t *evid, double *marg, int32_t *labels,
@@ -591,7 +592,7 @@ int fbn_jt_plan_create(const fbn_network *net, int device, fbn_jt_plan **out) {
     if (!p->v_ok) p->vprog = fbn::JTProgramV();
     lap("streamed program");
     // tiled variant: factors of a clique phase staged in LDS up to this many bytes per wave
-    static const int t_lds = getenv("FBN_JT_TLDS") ? atoi(getenv("FBN_JT_TLDS")) : 16384;  // (tuning knob)
+    static const int t_lds = getenv("FBN_JT_TLDS") ? atoi(getenv("FBN_JT_TLDS")) : 6144;  // (tuning knob)
     rc = fbn::CompileJTProgramT(p->host, p->tprog, t_lds);
     if (rc && rc != FBN_ERR_LIMIT) return rc;
     p->t_ok = rc == FBN_OK;
@@ -660,7 +661,7 @@ int fbn_jt_stream_schedule(const fbn_jt_plan *p, int32_t *order, int64_t order_c
 int fbn_jt_tile_program(const fbn_jt_plan *p, int32_t *passes, int32_t *tab, double *initv, int64_t *geometry) {
     if (!p) return SetError(FBN_ERR_ARG, "null pointer");
     if (!p->t_ok) return SetError(FBN_ERR_LIMIT, "plan not eligible for the tiled kernel");
-    static_assert(sizeof(JtTPass) == 26 * 4, "JtTPass = 26 int32");
+    static_assert(sizeof(JtTPass) == 27 * 4, "JtTPass = 27 int32");
     const auto &t = p->tprog;
     if (passes) memcpy(passes, t.passes.data(), t.passes.size() * sizeof(JtTPass));
     if (tab) memcpy(tab, t.tab.data(), t.tab.size() * 4);
@@ -1015,7 +1016,7 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
         // (messages, partial and reduced bins of the pass in flight) and its LDS factor stage
         const auto &t = p->tprog;
         const int64_t ncg = (ncases + JT_T_C - 1) / JT_T_C;
-        const int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 8;
+        const int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 16;
         int grid = (int)std::min<int64_t>(ncg, (int64_t)p->num_cu * wpc);
         const size_t per_wave = (size_t)t.store_rows * JT_T_C * 8;
         size_t free_b = 0, total_b = 0;
@@ -1026,11 +1027,18 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
         if ((rc = p->ws.ensure((size_t)grid * per_wave))) return rc;
         if ((rc = p->flags.ensure((size_t)nblk * 4))) return rc;
         FBN_HIP(hipMemsetAsync(p->flags.p, 0, (size_t)nblk * 4, s));
+        unsigned long long *tprof = nullptr;  // diagnostic: per-phase cycles (fbn_jt_debug_op_cycles)
+        if (p->prof_on) {
+            if ((rc = p->prof.ensure(16 * 8))) return rc;
+            FBN_HIP(hipMemsetAsync(p->prof.p, 0, 16 * 8, s));
+            p->last_grid = 1;
+            tprof = p->prof.as<unsigned long long>();
+        }
         FBN_HIP(hipEventRecord(p->ev0, s));
         hipError_t e = fbn_jt_tile_launch(p->tpass.as<JtTPass>(), (int)t.passes.size(), p->ttab.as<int32_t>(),
                                           p->tiv.as<double>(), d_evidence, marg, labels, p->ws.as<double>(),
                                           p->flags.as<int>(), ncases, t.store_rows, t.scr_row, t.red_row, V, SD,
-                                          (int)t.lds_bytes, grid, s);
+                                          (int)t.lds_bytes, grid, tprof, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt kernel launch: %s", hipGetErrorString(e));
         if (p->force_fixup) FBN_HIP(hipMemsetAsync(p->flags.p, 1, (size_t)nblk * 4, s));  // testing only
         // exact recomputation of the blocks holding a case group whose pass totals left the checked range

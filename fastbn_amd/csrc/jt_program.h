@@ -100,30 +100,31 @@ struct JtVClique {
 // its entries over the inner stream in a register and stores the sum once per outer configuration
 // into the output's bin (distinct per lane: G holds output variables, or extra variables E whose
 // partial bins the post sweep adds up), so no atomics and a fixed summation order.  Messages are
-// 64-byte rows [separator entry][JT_T_C cases]: the factors of a clique fit LDS, the per-case
+// rows [separator entry][JT_T_C cases]: the factors of a clique fit LDS, the per-case
 // normalizations of the reference cancel in the normalized results (fast order, within 1e-12).
-#define JT_T_C 8            // cases per wave
-#define JT_T_L 8            // entry slots per case (JT_T_C * JT_T_L = 64 lanes)
+#define JT_T_C 16           // cases per wave: a message row is JT_T_C fp64 = 128 B, one cache line
+#define JT_T_L 4            // entry slots per case (JT_T_C * JT_T_L = 64 lanes)
 #define JT_T_MAXF 7         // factors per pass: <= 6 child messages + the parent message
-#define JT_T_MAXDIM 8       // state counts the marginal sweep handles (one slot per value)
+#define JT_T_MAXDIM 8       // state counts of the variables (marginal sweep: value d in slot d % JT_T_L)
+#define JT_T_LDS_BIN_ROWS 16  // a pass's partial bins live in LDS when they are at most this many rows
 enum JtTKind : int32_t { JT_T_COL = 0, JT_T_DIS = 1, JT_T_MARG = 2 };
 struct JtTPass {
     int32_t kind, clique, nf, mode;  // mode: 0 every factor in LDS, 1 every factor global, 2 all but the
                                      // last (the parent message) in LDS
     int32_t nG, rounds, nRo, nRi;    // G-configurations, rounds of JT_T_L, outer / inner R stream
-    int32_t g_off, r_off, o_off;     // tab: G records (4 + nf ints: e, digit word, bin, pad, factor
-                                     // byte offsets), R records (2 + nf ints: e, digit word, factor
-                                     // byte offsets), outer records (1 int: bin offset)
+    int32_t g_off, o_off, i_off;     // tab: G records and outer R records (4 + nf ints each: entry, digit
+                                     // word, bin, pad, factor byte offsets), inner R records (2 + nf
+                                     // ints: entry byte offset, digit word, factor byte offsets)
     int32_t nE, nbins;               // partial bins per output bin (E configurations), output bins
     int32_t dest_row, col_row;       // output message rows (-1: MARG), the child's Collect message (DIS)
     int32_t bdig_off;                // tab: packed digits of every output bin (marginal sweep)
     int32_t nmv, mv_off;             // marginals taken from this pass's bins: {var, out_off, dim, shift, mask}
     int32_t iv_off;                  // initial potentials (fp64 index)
     int32_t nv, vars_off;            // clique variables {var, shift, mask} (evidence digit fields)
-    uint32_t gfields;                // digit fields of the G variables
+    uint32_t gfields, ofields;       // digit fields of the G / outer R variables
     int32_t first;                   // first pass of a clique phase: the lanes' evidence words, then the
     int32_t nstage, stage_off;       // factors staged into LDS ({src row, rows, lds byte offset} records)
-    int32_t pad1;
+    int32_t et_off;                  // tab: the R part of the entry (bytes) of every flattened R step
 };
 
 #endif

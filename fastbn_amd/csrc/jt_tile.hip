@@ -14,7 +14,7 @@
 //   Distribute:  a child separator's message  (tmp / S) / old, 0 where old == 0       (:700-816)
 // and the marginals whose source is this pass (GetProbabilitiesOneNode, :1392-1454; ArgMax,
 // src/Inference.cpp:92-102).  Every sum runs in a fixed order (per lane, then a butterfly over the
-// slots), so results are run-to-run identical.  Messages are 64-byte rows [entry][JT_T_C cases] in
+// slots), so results are run-to-run identical.  Messages are rows [entry][JT_T_C cases] in
 // the wave's store; a clique's factors are staged into LDS when they fit the per-wave budget.
 // A case group whose pass totals leave [2^-900, 2^900] flags its 64-case block; the exact
 // interpreter recomputes flagged blocks.
@@ -26,9 +26,10 @@
 namespace {
 
 constexpr int C = JT_T_C, L = JT_T_L;
-constexpr int U = 4;  // R steps with their loads in flight together
 static_assert(C * L == 64, "one wave = C cases x L slots");
-static_assert(JT_T_MAXDIM <= L, "the marginal sweep gives each value one slot");
+constexpr int kValChunks = (JT_T_MAXDIM + L - 1) / L;  // marginal sweep: value d in slot d % L, chunk d / L
+constexpr int kBinRows = JT_T_LDS_BIN_ROWS;  // bin sets up to this many rows live in LDS
+constexpr int kMaxCliqueVars = 10;           // (32 digit bits of >= 2-state variables, jt_tile_plan.cpp)
 
 typedef __attribute__((ext_vector_type(2))) unsigned u2;
 
@@ -45,68 +46,143 @@ __device__ __forceinline__ double slot_sum(double x) {
     return x;
 }
 
-// the entry work of one pass: rounds of G-configurations x the R stream -> partial bins; returns
-// the lane's share of the pass total.  MODE 0: every factor in LDS, 1: every factor in the wave
-// store, 2: all but the last (the parent message) in LDS
+// lane n of every 16-lane DPP row (row_newbcast:n): the value slot s's lane n loaded, to all 16
+// lanes of the slot
+template <int N>
+__device__ __forceinline__ double row_bcast(double x) {
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x150 + N, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x150 + N, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// n is a constant after unrolling: the switch folds to one row_bcast
+__device__ __forceinline__ double row_bcast_n(double x, int n) {
+    switch (n & 15) {
+    case 0: return row_bcast<0>(x);
+    case 1: return row_bcast<1>(x);
+    case 2: return row_bcast<2>(x);
+    case 3: return row_bcast<3>(x);
+    case 4: return row_bcast<4>(x);
+    case 5: return row_bcast<5>(x);
+    case 6: return row_bcast<6>(x);
+    case 7: return row_bcast<7>(x);
+    case 8: return row_bcast<8>(x);
+    case 9: return row_bcast<9>(x);
+    case 10: return row_bcast<10>(x);
+    case 11: return row_bcast<11>(x);
+    case 12: return row_bcast<12>(x);
+    case 13: return row_bcast<13>(x);
+    case 14: return row_bcast<14>(x);
+    default: return row_bcast<15>(x);
+    }
+}
+
+// the entry work of one pass: rounds of G-configurations x the R stream (outer x inner
+// configurations, flattened) -> partial bins; returns the lane's share of the pass total.
+// The stream runs in chunks of 16 steps = the 16 lanes (cases) of a slot: lane (s, g) loads the
+// initial potential of ITS slot's entry at step k0 + g (one fully used gather per chunk instead of
+// one per step), and step k0 + u takes it from lane u of the slot's DPP row.  Per step: one digit
+// test and NF factor loads (LDS: one address add; wave store: voffset + scalar soffset), a factor
+// row is reused when the step leaves its index unchanged.  The scalar R parts = the current outer
+// record + the inner record (a small table every outer configuration and round re-reads).  The sum
+// of an inner run goes to its bin (LDS rows for small bin sets, else the wave store) when the run
+// ends.  MODE 0: every factor in LDS, 1: every factor in the wave store, 2: all but the last (the
+// parent message) in LDS
 template <int NF, int MODE>
 __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *__restrict__ tab,
-                                               const double *__restrict__ iv, __amdgpu_buffer_rsrc_t st,
-                                               const double *__restrict__ lds, int s, int g8, uint32_t M, uint32_t W,
-                                               int scr_b) {
-    constexpr int RS = 2 + NF, GS = 4 + NF;
+                                               __amdgpu_buffer_rsrc_t ivrs, __amdgpu_buffer_rsrc_t st,
+                                               char *__restrict__ ldsb, int s, int g, uint32_t M, uint32_t W,
+                                               int scr_b, int binb, bool bins_lds) {
+    static_assert(C == 16, "a chunk = the 16 lanes of a DPP row");
+    constexpr int IS = 2 + NF, GS = 4 + NF, NFA = NF > 0 ? NF : 1;
+    constexpr int U = NF <= 2 ? 8 : 4;  // steps with their loads in flight together (register budget)
+    const int g8 = g * 8;
     double tot = 0.0;
-    const uint32_t MR = M & ~(uint32_t)P.gfields, WR = W & MR;
-    const int nRi = P.nRi;
+    const uint32_t gf = (uint32_t)P.gfields;
+    const uint32_t MR = M & ~gf, WR = W & MR;  // evidence on the R digits
+    const int nRi = P.nRi, nR = P.nRo * P.nRi;
+    const int32_t *__restrict__ it = tab + P.i_off;
+    const int32_t *__restrict__ ot = tab + P.o_off;
+    const int32_t *__restrict__ et = tab + P.et_off;
     for (int r = 0; r < P.rounds; ++r) {
         const int cfg = r * L + s;
         const bool la = cfg < P.nG;
         const int32_t *__restrict__ gr = tab + P.g_off + (size_t)(la ? cfg : 0) * GS;
-        const int eG = gr[0];
+        const int ivb = (P.iv_off + gr[0]) * 8;  // this lane's G part of the entry (bytes)
         const uint32_t dwG = (uint32_t)gr[1];
         const int xG = gr[2];
-        int fG[NF > 0 ? NF : 1];
+        int fG[NFA];
 #pragma unroll
         for (int j = 0; j < NF; ++j) fG[j] = gr[4 + j] + g8;
-        const bool okG = la && (((dwG ^ W) & M & (uint32_t)P.gfields) == 0u);
-        const double *__restrict__ ivg = iv + P.iv_off + eG;
-        for (int o = 0; o < P.nRo; ++o) {
-            const int32_t *__restrict__ rr = tab + P.r_off + (size_t)o * nRi * RS;
-            double acc = 0.0;
-            int i = 0;
-            auto step = [&](const int32_t *__restrict__ q, double &w, double (&f)[NF > 0 ? NF : 1], bool &ok) {
-                w = ivg[q[0]];
-                ok = (((uint32_t)q[1]) & MR) == WR;
+        const bool okG = la && (((dwG ^ W) & M & gf) == 0u);
+        // current outer record (uniform), the inner position
+        int o = 0, i = 0;
+        int ox = ot[2];
+        uint32_t odw = (uint32_t)ot[1];
+        int of[NFA], pso[NFA];
+        double pf[NFA];
 #pragma unroll
-                for (int j = 0; j < NF; ++j) {
-                    if (MODE == 0 || (MODE == 2 && j < NF - 1)) f[j] = lds[(fG[j] + q[2 + j]) >> 3];
-                    else f[j] = bld(st, fG[j], q[2 + j]);
-                }
-            };
-            for (; i + U <= nRi; i += U) {
-                double w[U], f[U][NF > 0 ? NF : 1];
-                bool ok[U];
+        for (int j = 0; j < NF; ++j) of[j] = ot[4 + j], pso[j] = -1, pf[j] = 0.0;
+        double acc = 0.0;
+        for (int k0 = 0; k0 < nR; k0 += C) {
+            const int kk = k0 + g < nR ? k0 + g : nR - 1;
+            const double wl = bld(ivrs, ivb + et[kk], 0);  // slot s's entry at step k0 + g
 #pragma unroll
-                for (int u = 0; u < U; ++u) step(rr + (size_t)(i + u) * RS, w[u], f[u], ok[u]);
+            for (int u0 = 0; u0 < C; u0 += U) {
+                double w[U], f[U][NFA];
+                bool ok[U], fl[U], va[U];
+                int xo[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
+                    va[u] = k0 + u0 + u < nR;
+                    const int32_t *__restrict__ q = it + (size_t)i * IS;
+                    ok[u] = ((odw | (uint32_t)q[1]) & MR) == WR;
+#pragma unroll
+                    for (int j = 0; j < NF; ++j) {
+                        const int so = of[j] + q[2 + j];
+                        if (so != pso[j]) {  // (uniform) a new factor row
+                            if (MODE == 0 || (MODE == 2 && j < NF - 1))
+                                pf[j] = *reinterpret_cast<const double *>(ldsb + (fG[j] + so));  // byte offsets
+                            else pf[j] = bld(st, fG[j], so);
+                            pso[j] = so;
+                        }
+                        f[u][j] = pf[j];
+                    }
+                    fl[u] = va[u] && i == nRi - 1;
+                    xo[u] = ox;
+                    if (va[u] && ++i == nRi) {  // the next outer configuration (uniform)
+                        i = 0;
+                        if (++o < P.nRo) {
+                            const int32_t *__restrict__ oq = ot + (size_t)o * GS;
+                            odw = (uint32_t)oq[1], ox = oq[2];
+#pragma unroll
+                            for (int j = 0; j < NF; ++j) of[j] = oq[4 + j];
+                        } else {
+                            o = P.nRo - 1;  // (past the end: the remaining steps of the chunk are masked)
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) w[u] = row_bcast_n(wl, u0 + u);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (!va[u]) continue;
                     double x = w[u];
 #pragma unroll
                     for (int j = 0; j < NF; ++j) x *= f[u][j];
                     acc += ok[u] ? x : 0.0;
+                    if (fl[u]) {  // end of an inner run: its bin
+                        const double a = okG ? acc : 0.0;
+                        if (la) {
+                            const int x8 = (xG + xo[u]) * (C * 8) + g8;
+                            if (bins_lds) *reinterpret_cast<double *>(ldsb + binb + x8) = a;
+                            else bst(st, scr_b + x8, a);
+                        }
+                        tot += a;
+                        acc = 0.0;
+                    }
                 }
             }
-            for (; i < nRi; ++i) {
-                double w, f[NF > 0 ? NF : 1];
-                bool ok;
-                step(rr + (size_t)i * RS, w, f, ok);
-                double x = w;
-#pragma unroll
-                for (int j = 0; j < NF; ++j) x *= f[j];
-                acc += ok ? x : 0.0;
-            }
-            const double a = okG ? acc : 0.0;
-            if (la) bst(st, scr_b + (xG + tab[P.o_off + o]) * (C * 8) + g8, a);
-            tot += a;
         }
     }
     return tot;
@@ -114,9 +190,9 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
 
 #define FBN_TCASE(NFv)                                                                                    \
     case NFv:                                                                                             \
-        if (P.mode == 0) tot = pass_entries<NFv, 0>(P, tab, iv, st, lds, s, g8, M, W, scr_b);             \
-        else if (P.mode == 1) tot = pass_entries<NFv, 1>(P, tab, iv, st, lds, s, g8, M, W, scr_b);        \
-        else tot = pass_entries<NFv, 2>(P, tab, iv, st, lds, s, g8, M, W, scr_b);                         \
+        if (P.mode == 0) tot = pass_entries<NFv, 0>(P, tab, ivrs, st, ldsb, s, g, M, W, scr_b, binb, bins_lds);             \
+        else if (P.mode == 1) tot = pass_entries<NFv, 1>(P, tab, ivrs, st, ldsb, s, g, M, W, scr_b, binb, bins_lds);        \
+        else tot = pass_entries<NFv, 2>(P, tab, ivrs, st, ldsb, s, g, M, W, scr_b, binb, bins_lds);                         \
         break;
 
 __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__ passes, int npass,
@@ -124,13 +200,24 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
                                                      const int8_t *__restrict__ evid, double *__restrict__ marg,
                                                      int32_t *__restrict__ labels, double *__restrict__ ws,
                                                      int *__restrict__ flags, long long ncases, long long store_rows,
-                                                     long long scr_row, long long red_row, int V, int SD) {
+                                                     long long scr_row, long long red_row, int V, int SD,
+                                                     int fac_bytes, unsigned long long *__restrict__ prof) {
     extern __shared__ double lds[];
+    char *ldsb = reinterpret_cast<char *>(lds);
     const int lane = threadIdx.x & 63;
     const int s = lane / C, g = lane % C, g8 = g * 8;
     __amdgpu_buffer_rsrc_t st = __builtin_amdgcn_make_buffer_rsrc(
         ws + (size_t)blockIdx.x * (size_t)store_rows * C, 0, (int)(store_rows * C * 8), 0x00020000);
     const int scr_b = (int)(scr_row * C * 8), red_b = (int)(red_row * C * 8);
+    // LDS: [factors: fac_bytes][partial bins: kBinRows rows][reduced bins: kBinRows rows]
+    const int binb = fac_bytes, redl = fac_bytes + kBinRows * C * 8;
+    // initial potentials through a buffer resource: entry = per-lane G part (voffset) + the R
+    // record's part (soffset, scalar) -- no per-step address arithmetic
+    const __amdgpu_buffer_rsrc_t ivrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(iv), 0, 0x7FFFFFF8, 0x00020000);
+    // diagnostic (prof != nullptr): s_memtime cycles per phase, summed over the waves -- [0] staging,
+    // [1..3] entry work in factor mode 0 / 1 / 2, [4] post sweep, [5] marginal sweeps, [6] all
+    unsigned long long pc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long t_all = prof ? clock64() : 0ull;
     for (long long cg = blockIdx.x; cg * C < ncases; cg += gridDim.x) {
         const long long cs = cg * C + g;
         const bool act = cs < ncases;
@@ -141,22 +228,36 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
         bool bad = false;
         for (int p = 0; p < npass; ++p) {
             const JtTPass P = passes[p];
+            unsigned long long t0 = prof ? clock64() : 0ull;
             if (P.first) {
                 M = 0u, W = 0u;
                 const int32_t *__restrict__ vr = tab + P.vars_off;
-                for (int j = 0; j < P.nv; ++j) {
-                    const int x = ev[vr[3 * j]];
-                    if (x >= 0) M |= (uint32_t)vr[3 * j + 2] << vr[3 * j + 1], W |= (uint32_t)x << vr[3 * j + 1];
-                }
+                int xs[kMaxCliqueVars];  // every evidence byte in flight at once
+#pragma unroll
+                for (int j = 0; j < kMaxCliqueVars; ++j) xs[j] = j < P.nv ? ev[vr[3 * j]] : -1;
+#pragma unroll
+                for (int j = 0; j < kMaxCliqueVars; ++j)
+                    if (xs[j] >= 0) M |= (uint32_t)vr[3 * j + 2] << vr[3 * j + 1], W |= (uint32_t)xs[j] << vr[3 * j + 1];
                 if (P.nstage > 0) {
                     __syncthreads();  // (one wave per workgroup: orders the LDS writes after earlier reads)
                     for (int k = 0; k < P.nstage; ++k) {
                         const int32_t *__restrict__ sr = tab + P.stage_off + 3 * k;
                         const int src = sr[0] * (C * 8), n = sr[1] * C, dst = sr[2] >> 3;
-                        for (int i = lane; i < n; i += 64) lds[dst + i] = bld(st, i * 8, src);
+                        int i = lane;
+                        for (; i + 192 < n; i += 256) {  // four loads in flight
+                            const double a0 = bld(st, i * 8, src), a1 = bld(st, (i + 64) * 8, src),
+                                         a2 = bld(st, (i + 128) * 8, src), a3 = bld(st, (i + 192) * 8, src);
+                            lds[dst + i] = a0, lds[dst + i + 64] = a1, lds[dst + i + 128] = a2, lds[dst + i + 192] = a3;
+                        }
+                        for (; i < n; i += 64) lds[dst + i] = bld(st, i * 8, src);
                     }
                     __syncthreads();
                 }
+            }
+            if (prof) {
+                const unsigned long long t1 = clock64();
+                pc[0] += t1 - t0;
+                t0 = t1;
             }
             // a private-variable pass runs only if some case of the group lacks evidence on one of them
             bool need_entries = true;
@@ -166,66 +267,117 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
                 need_entries = __ballot(any) != 0ull;
             }
             double S = 1.0;
+            // partial bins (and the reduced bins of the marginal sweep) in LDS when they fit
+            const bool bins_lds = P.nbins * P.nE <= kBinRows;
             if (need_entries) {
                 double tot = 0.0;
                 switch (P.nf) {
                     FBN_TCASE(0) FBN_TCASE(1) FBN_TCASE(2) FBN_TCASE(3) FBN_TCASE(4) FBN_TCASE(5) FBN_TCASE(6)
                     default: {
-                        if (P.mode == 0) tot = pass_entries<7, 0>(P, tab, iv, st, lds, s, g8, M, W, scr_b);
-                        else if (P.mode == 1) tot = pass_entries<7, 1>(P, tab, iv, st, lds, s, g8, M, W, scr_b);
-                        else tot = pass_entries<7, 2>(P, tab, iv, st, lds, s, g8, M, W, scr_b);
+                        if (P.mode == 0) tot = pass_entries<7, 0>(P, tab, ivrs, st, ldsb, s, g, M, W, scr_b, binb, bins_lds);
+                        else if (P.mode == 1) tot = pass_entries<7, 1>(P, tab, ivrs, st, ldsb, s, g, M, W, scr_b, binb, bins_lds);
+                        else tot = pass_entries<7, 2>(P, tab, ivrs, st, ldsb, s, g, M, W, scr_b, binb, bins_lds);
                     }
+                }
+                if (prof) {
+                    const unsigned long long t1 = clock64();
+                    pc[1 + P.mode] += t1 - t0;
+                    t0 = t1;
                 }
                 S = slot_sum(tot);
                 bad |= act && !(S >= 0x1p-900 && S <= 0x1p+900);
-                __threadfence_block();  // the partial bins, stored by other lanes, become visible
-                // post sweep: output bin b = sum of its nE partial bins (in order)
-                const int nE = P.nE;
-                for (int b = s; b < P.nbins; b += L) {
-                    double v = 0.0;
-                    for (int e = 0; e < nE; ++e) v += bld(st, scr_b + (b * nE + e) * (C * 8) + g8, 0);
-                    if (P.kind == JT_T_COL) {
-                        bst(st, (P.dest_row + b) * (C * 8) + g8, v / S);
-                    } else if (P.kind == JT_T_DIS) {
-                        const double old = bld(st, (P.col_row + b) * (C * 8) + g8, 0);
-                        bst(st, (P.dest_row + b) * (C * 8) + g8, old == 0.0 ? 0.0 : (v / S) / old);
+                if (bins_lds) __syncthreads();  // the partial bins, written by other lanes, become visible
+                else __threadfence_block();
+                // post sweep: output bin b = sum of its nE partial bins (in order); four bins per lane in
+                // flight
+                const int nE = P.nE, nb = P.nbins;
+                auto part = [&](int b, int e) {
+                    const int x8 = (b * nE + e) * (C * 8) + g8;
+                    return bins_lds ? *reinterpret_cast<const double *>(ldsb + binb + x8) : bld(st, scr_b + x8, 0);
+                };
+                for (int b0 = 0; b0 < nb; b0 += 4 * L) {
+                    double v[4] = {0.0, 0.0, 0.0, 0.0}, old[4] = {1.0, 1.0, 1.0, 1.0};
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const int b = b0 + t * L + s;
+                        if (b < nb) {
+                            for (int e = 0; e < nE; ++e) v[t] += part(b, e);
+                            if (P.kind == JT_T_DIS) old[t] = bld(st, (P.col_row + b) * (C * 8) + g8, 0);
+                        }
                     }
-                    if (P.nmv > 0) bst(st, red_b + b * (C * 8) + g8, v);
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const int b = b0 + t * L + s;
+                        if (b >= nb) continue;
+                        if (P.kind == JT_T_COL) bst(st, (P.dest_row + b) * (C * 8) + g8, v[t] / S);
+                        else if (P.kind == JT_T_DIS)
+                            bst(st, (P.dest_row + b) * (C * 8) + g8, old[t] == 0.0 ? 0.0 : (v[t] / S) / old[t]);
+                        if (P.nmv > 0) {
+                            if (bins_lds) *reinterpret_cast<double *>(ldsb + redl + b * (C * 8) + g8) = v[t];
+                            else bst(st, red_b + b * (C * 8) + g8, v[t]);
+                        }
+                    }
                 }
-                __threadfence_block();
+                if (bins_lds) __syncthreads();
+                __threadfence_block();  // (the messages: read by later passes, by other lanes)
+                if (prof) {
+                    const unsigned long long t1 = clock64();
+                    pc[4] += t1 - t0;
+                    t0 = t1;
+                }
             }
-            // marginals whose source is this pass: value d of the variable in slot d, summed over the
-            // bins in bin order, normalized by their total (evidence variables: zeros)
+            // marginals whose source is this pass: value d of the variable in slot d % L (chunk d / L),
+            // summed over the bins in bin order, normalized by their total (evidence variables: zeros)
             for (int m = 0; m < P.nmv; ++m) {
                 const int32_t *__restrict__ mr = tab + P.mv_off + 5 * m;
                 const int var = mr[0], off = mr[1], dim = mr[2], sh = mr[3];
                 const uint32_t fm = (uint32_t)mr[4];
                 const bool obs = ev[var] >= 0;
                 const bool need = need_entries && __ballot(act && !obs) != 0ull;
-                double a = 0.0;
+                double a[kValChunks];
+#pragma unroll
+                for (int c = 0; c < kValChunks; ++c) a[c] = 0.0;
                 if (need) {
                     const int32_t *__restrict__ bd = tab + P.bdig_off;
                     for (int b = 0; b < P.nbins; ++b) {
                         const int dg = (int)(((uint32_t)bd[b] >> sh) & fm);
-                        const double v = bld(st, red_b + b * (C * 8) + g8, 0);
-                        a += dg == s ? v : 0.0;
+                        const double v = bins_lds ? *reinterpret_cast<const double *>(ldsb + redl + b * (C * 8) + g8)
+                                                  : bld(st, red_b + b * (C * 8) + g8, 0);
+#pragma unroll
+                        for (int c = 0; c < kValChunks; ++c) a[c] += dg == c * L + s ? v : 0.0;
                     }
                 }
-                const double tm = slot_sum(a);
-                if (act && s < dim) out[off + s] = obs ? 0.0 : a / tm;
+                double am = 0.0;  // the lane's values in chunk order, then the slot butterfly
+#pragma unroll
+                for (int c = 0; c < kValChunks; ++c) am += a[c];
+                const double tm = slot_sum(am);
+#pragma unroll
+                for (int c = 0; c < kValChunks; ++c)
+                    if (act && c * L + s < dim) out[off + c * L + s] = obs ? 0.0 : a[c] / tm;
                 if (var == 0 && need) {  // label: ArgMax, strict '>' from 0 (src/Inference.cpp:92-102)
                     int lab = 0;
                     double mx = 0.0;
                     for (int d = 0; d < dim; ++d) {
-                        const double pd = __shfl(a, d * C + g) / tm;
+                        double ad = 0.0;
+#pragma unroll
+                        for (int c = 0; c < kValChunks; ++c) {
+                            const double t = __shfl(a[c], (d % L) * C + g);
+                            ad = d / L == c ? t : ad;
+                        }
+                        const double pd = ad / tm;
                         if (pd > mx) mx = pd, lab = d;
                     }
                     if (act && !obs && s == 0) labels[cs] = lab;
                 }
             }
+            if (prof) pc[5] += clock64() - t0;
         }
         const unsigned long long fb = __ballot(bad);
         if (fb && lane == 0) atomicOr(flags + (cg * C) / 64, 1);
+    }
+    if (prof && lane == 0) {
+        pc[6] = clock64() - t_all;
+        for (int k = 0; k < 7; ++k) atomicAdd(prof + k, pc[k]);
     }
 }
 
@@ -234,8 +386,12 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
 extern "C" hipError_t fbn_jt_tile_launch(const JtTPass *passes, int npass, const int32_t *tab, const double *iv,
                                          const int8_t *evid, double *marg, int32_t *labels, double *ws, int *flags,
                                          long long ncases, long long store_rows, long long scr_row, long long red_row,
-                                         int V, int SD, int lds_bytes, int grid, hipStream_t stream) {
-    hipLaunchKernelGGL(jt_tile_kernel, dim3(grid), dim3(64), (size_t)(lds_bytes > 0 ? lds_bytes : 8), stream, passes,
-                       npass, tab, iv, evid, marg, labels, ws, flags, ncases, store_rows, scr_row, red_row, V, SD);
+                                         int V, int SD, int lds_bytes, int grid, unsigned long long *prof,
+                                         hipStream_t stream) {
+    // LDS per wave: the staged factors, then the small bin sets (partial, reduced)
+    const int fac = (lds_bytes + 15) & ~15;
+    const size_t total = (size_t)fac + 2 * (size_t)kBinRows * C * 8;
+    hipLaunchKernelGGL(jt_tile_kernel, dim3(grid), dim3(64), total, stream, passes, npass, tab, iv, evid, marg, labels,
+                       ws, flags, ncases, store_rows, scr_row, red_row, V, SD, fac, prof);
     return hipGetLastError();
 }

@@ -260,48 +260,57 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
                 prog.tab.push_back((int32_t)o);
             }
         });
-        // R records: outer over RO, inner over RI (odometers; per-variable increments of every map)
-        P.r_off = (int32_t)prog.tab.size();
-        std::vector<int32_t> otab;
-        {
-            const int RS = 2 + nf;
-            const int64_t nR = Prod(t, RO) * Prod(t, RI);
-            std::vector<int> Rv(RO);
-            Rv.insert(Rv.end(), RI.begin(), RI.end());  // outer digits first: last RI digit fastest
-            const int nr = (int)Rv.size();
-            std::vector<int64_t> inc((size_t)nr * RS);  // per R variable: entry, digit word, factor offsets
-            for (int i = 0; i < nr; ++i) {
-                const int j = Rv[i];
-                inc[(size_t)i * RS + 0] = t.cum[j];
-                inc[(size_t)i * RS + 1] = (int64_t)1 << sh[c][j];
-                for (int f = 0; f < nf; ++f) inc[(size_t)i * RS + 2 + f] = fs[f][j] * (JT_T_C * 8);
+        // the R stream = outer configurations (RO) x inner ones (RI); every map is the sum of an outer
+        // and an inner part, so the kernel reads a small inner table (reused by every outer
+        // configuration and round: it stays in the scalar cache) and one outer record per configuration
+        auto emit = [&](const std::vector<int> &vars, bool outer) {  // odometer over `vars`, last fastest
+            const int RS = outer ? 4 + nf : 2 + nf;
+            const int64_t n = Prod(t, vars);
+            const int nr = (int)vars.size();
+            std::vector<int64_t> inc((size_t)nr * RS, 0);  // per variable: increments of every field
+            for (int k = 0; k < nr; ++k) {
+                const int j = vars[k];
+                int64_t *q = &inc[(size_t)k * RS];
+                q[0] = outer ? t.cum[j] : t.cum[j] * 8;  // inner: byte offsets (buffer soffset)
+                q[1] = (int64_t)1 << sh[c][j];
+                if (outer) q[2] = ocum_p[j] * nE;
+                for (int f = 0; f < nf; ++f) q[(outer ? 4 : 2) + f] = fs[f][j] * (JT_T_C * 8);
             }
             const size_t base = prog.tab.size();
-            prog.tab.resize(base + (size_t)nR * RS);
+            prog.tab.resize(base + (size_t)n * RS);
             int32_t *out = prog.tab.data() + base;
-            int64_t cur[2 + JT_T_MAXF] = {0};
+            int64_t cur[4 + JT_T_MAXF] = {0};
             std::vector<int> d(nr, 0);
-            for (int64_t k = 0; k < nR; ++k) {
+            for (int64_t k = 0; k < n; ++k) {
                 for (int q = 0; q < RS; ++q) out[k * RS + q] = (int32_t)cur[q];
-                int i = nr - 1;
-                while (i >= 0) {
-                    const int j = Rv[i];
-                    if (++d[i] < t.dims[j]) {
-                        for (int q = 0; q < RS; ++q) cur[q] += inc[(size_t)i * RS + q];
+                int i2 = nr - 1;
+                while (i2 >= 0) {
+                    const int jv = vars[i2];
+                    if (++d[i2] < t.dims[jv]) {
+                        for (int q = 0; q < RS; ++q) cur[q] += inc[(size_t)i2 * RS + q];
                         break;
                     }
-                    for (int q = 0; q < RS; ++q) cur[q] -= inc[(size_t)i * RS + q] * (t.dims[j] - 1);
-                    d[i--] = 0;
+                    for (int q = 0; q < RS; ++q) cur[q] -= inc[(size_t)i2 * RS + q] * (t.dims[jv] - 1);
+                    d[i2--] = 0;
                 }
             }
-            ForEachConfig(t, RO, [&](const std::vector<int> &dout) {
-                int64_t xo = 0;
-                for (size_t i = 0; i < RO.size(); ++i) xo += dout[i] * ocum_p[RO[i]] * nE;
-                otab.push_back((int32_t)xo);
-            });
-        }
+        };
         P.o_off = (int32_t)prog.tab.size();
-        prog.tab.insert(prog.tab.end(), otab.begin(), otab.end());
+        emit(RO, true);
+        P.i_off = (int32_t)prog.tab.size();
+        emit(RI, false);
+        {  // flattened entry offsets of the R stream (outer x inner), bytes: the kernel's per-lane gather
+            const int64_t nRo_ = Prod(t, RO), nRi_ = Prod(t, RI);
+            const int32_t *ro = prog.tab.data() + P.o_off, *ri = prog.tab.data() + P.i_off;
+            std::vector<int32_t> et((size_t)(nRo_ * nRi_));
+            for (int64_t o = 0; o < nRo_; ++o)
+                for (int64_t i = 0; i < nRi_; ++i) et[o * nRi_ + i] = ro[o * (4 + nf)] * 8 + ri[i * (2 + nf)];
+            P.et_off = (int32_t)prog.tab.size();
+            prog.tab.insert(prog.tab.end(), et.begin(), et.end());
+        }
+        uint32_t of = 0;
+        for (int j : RO) of |= (uint32_t)fm[c][j] << sh[c][j];
+        P.ofields = of;
         P.dest_row = (int32_t)dest_row;
         P.col_row = (int32_t)col_row;
         // packed digits of every output bin, fields of the output variables in output order

@@ -38,11 +38,13 @@ def test_every_pass_covers_its_clique_once():
         for prow in passes:
             P = dict(zip(TE.F, (int(x) for x in prow)))
             nf, nG, nRo, nRi = P["nf"], P["nG"], P["nRo"], P["nRi"]
-            g = tab[P["g_off"]:P["g_off"] + nG * (4 + nf)].reshape(nG, 4 + nf)
-            r = tab[P["r_off"]:P["r_off"] + nRo * nRi * (2 + nf)].reshape(nRo * nRi, 2 + nf)
-            e = (g[:, 0:1] + r[None, :, 0]).reshape(-1)
+            g = tab[P["g_off"]:P["g_off"] + nG * (4 + nf)].reshape(nG, 4 + nf).astype(np.int64)
+            ro = tab[P["o_off"]:P["o_off"] + nRo * (4 + nf)].reshape(nRo, 4 + nf).astype(np.int64)
+            ri = tab[P["i_off"]:P["i_off"] + nRi * (2 + nf)].reshape(nRi, 2 + nf).astype(np.int64)
+            er = (ro[:, 0:1] + ri[None, :, 0] // 8).reshape(-1)
+            e = (g[:, 0:1] + er[None, :]).reshape(-1)
             assert sorted(e.tolist()) == list(range(nG * nRo * nRi))
-            x = (g[:, 2:3] + tab[P["o_off"]:P["o_off"] + nRo][None, :]).reshape(-1)
+            x = (g[:, 2:3] + ro[None, :, 2]).reshape(-1)
             assert sorted(x.tolist()) == list(range(P["nbins"] * P["nE"]))
             assert P["rounds"] * geo["slots"] >= nG
 

@@ -8,9 +8,9 @@ with the oracle to ~1e-14, not bit for bit.  Never used by the product path."""
 import numpy as np
 
 # JtTPass field order (jt_program.h)
-F = ["kind", "clique", "nf", "mode", "nG", "rounds", "nRo", "nRi", "g_off", "r_off", "o_off", "nE", "nbins",
-     "dest_row", "col_row", "bdig_off", "nmv", "mv_off", "iv_off", "nv", "vars_off", "gfields", "first", "nstage",
-     "stage_off", "pad1"]
+F = ["kind", "clique", "nf", "mode", "nG", "rounds", "nRo", "nRi", "g_off", "o_off", "i_off", "nE", "nbins",
+     "dest_row", "col_row", "bdig_off", "nmv", "mv_off", "iv_off", "nv", "vars_off", "gfields", "ofields", "first",
+     "nstage", "stage_off", "et_off"]
 COL, DIS, MARG = 0, 1, 2
 
 
@@ -27,6 +27,7 @@ def run_case(prog, ev_row, sum_dom, lds_bytes=1 << 20):
     for prow in passes:
         P = dict(zip(F, (int(x) for x in prow)))
         P["gfields"] &= 0xFFFFFFFF
+        P["ofields"] &= 0xFFFFFFFF
         nf = P["nf"]
         if P["first"]:
             M = W = 0
@@ -46,8 +47,15 @@ def run_case(prog, ev_row, sum_dom, lds_bytes=1 << 20):
             continue
         nG, nRo, nRi = P["nG"], P["nRo"], P["nRi"]
         g = tab[P["g_off"]:P["g_off"] + nG * (4 + nf)].reshape(nG, 4 + nf).astype(np.int64)
-        r = tab[P["r_off"]:P["r_off"] + nRo * nRi * (2 + nf)].reshape(nRo * nRi, 2 + nf).astype(np.int64)
-        otab = tab[P["o_off"]:P["o_off"] + nRo].astype(np.int64)
+        ro = tab[P["o_off"]:P["o_off"] + nRo * (4 + nf)].reshape(nRo, 4 + nf).astype(np.int64)
+        ri = tab[P["i_off"]:P["i_off"] + nRi * (2 + nf)].reshape(nRi, 2 + nf).astype(np.int64)
+        # R record (o, i) = outer part + inner part (inner entry offsets are in bytes)
+        r = np.zeros((nRo * nRi, 2 + nf), np.int64)
+        r[:, 0] = (ro[:, 0:1] + ri[None, :, 0] // 8).reshape(-1)
+        r[:, 1] = ((ro[:, 1:2] & 0xFFFFFFFF) | (ri[None, :, 1] & 0xFFFFFFFF)).reshape(-1)
+        for j in range(nf):
+            r[:, 2 + j] = (ro[:, 4 + j:5 + j] + ri[None, :, 2 + j]).reshape(-1)
+        otab = ro[:, 2]
         e = g[:, 0:1] + r[None, :, 0]
         dw = (g[:, 1:2] & 0xFFFFFFFF) | (r[None, :, 1] & 0xFFFFFFFF)
         ok = ((dw ^ W) & M) == 0
