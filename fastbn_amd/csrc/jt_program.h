@@ -125,6 +125,8 @@ struct JtTPass {
     int32_t first;                   // first pass of a clique phase: the lanes' evidence words, then the
     int32_t nstage, stage_off;       // factors staged into LDS ({src row, rows, lds byte offset} records)
     int32_t et_off;                  // tab: the R part of the entry (bytes) of every flattened R step
+    int32_t st_off;                  // tab: step records {factor soffsets [nf], digit word, bin offset of
+                                     //      the inner run ending at the step or -1}
 };
 
 #endif

@@ -46,6 +46,13 @@ __device__ __forceinline__ double slot_sum(double x) {
     return x;
 }
 
+// diagnostic phase clock: drains the wave's outstanding memory operations first, so a phase's
+// loads are charged to it (prof mode only: slows the kernel down)
+__device__ __forceinline__ unsigned long long dclock() {
+    __builtin_amdgcn_s_waitcnt(0);
+    return clock64();
+}
+
 // lane n of every 16-lane DPP row (row_newbcast:n): the value slot s's lane n loaded, to all 16
 // lanes of the slot
 template <int N>
@@ -77,32 +84,29 @@ __device__ __forceinline__ double row_bcast_n(double x, int n) {
     }
 }
 
-// the entry work of one pass: rounds of G-configurations x the R stream (outer x inner
-// configurations, flattened) -> partial bins; returns the lane's share of the pass total.
-// The stream runs in chunks of 16 steps = the 16 lanes (cases) of a slot: lane (s, g) loads the
-// initial potential of ITS slot's entry at step k0 + g (one fully used gather per chunk instead of
-// one per step), and step k0 + u takes it from lane u of the slot's DPP row.  Per step: one digit
-// test and NF factor loads (LDS: one address add; wave store: voffset + scalar soffset), a factor
-// row is reused when the step leaves its index unchanged.  The scalar R parts = the current outer
-// record + the inner record (a small table every outer configuration and round re-reads).  The sum
-// of an inner run goes to its bin (LDS rows for small bin sets, else the wave store) when the run
-// ends.  MODE 0: every factor in LDS, 1: every factor in the wave store, 2: all but the last (the
-// parent message) in LDS
+// the entry work of one pass: rounds of G-configurations x the flattened R stream (outer x inner
+// configurations) -> partial bins; returns the lane's share of the pass total.  The stream runs in
+// chunks of 16 steps = the 16 lanes (cases) of a slot: lane (s, g) loads the initial potential of
+// ITS slot's entry at step k0 + g (one fully used gather per chunk instead of one per step), and
+// step k0 + u takes it from lane u of the slot's DPP row.  Per step: a scalar step record (factor
+// soffsets, digit word, the bin of the inner run ending there), one digit test and NF factor loads
+// (LDS: one address add; wave store: voffset + soffset).  The sum of an inner run goes to its bin
+// (LDS rows for small bin sets, else the wave store).  MODE 0: every factor in LDS, 1: every factor
+// in the wave store, 2: all but the last (the parent message) in LDS
 template <int NF, int MODE>
 __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *__restrict__ tab,
                                                __amdgpu_buffer_rsrc_t ivrs, __amdgpu_buffer_rsrc_t st,
                                                char *__restrict__ ldsb, int s, int g, uint32_t M, uint32_t W,
                                                int scr_b, int binb, bool bins_lds) {
     static_assert(C == 16, "a chunk = the 16 lanes of a DPP row");
-    constexpr int IS = 2 + NF, GS = 4 + NF, NFA = NF > 0 ? NF : 1;
+    constexpr int RS = NF + 2, GS = 4 + NF, NFA = NF > 0 ? NF : 1;
     constexpr int U = NF <= 2 ? 8 : 4;  // steps with their loads in flight together (register budget)
     const int g8 = g * 8;
     double tot = 0.0;
     const uint32_t gf = (uint32_t)P.gfields;
     const uint32_t MR = M & ~gf, WR = W & MR;  // evidence on the R digits
-    const int nRi = P.nRi, nR = P.nRo * P.nRi;
-    const int32_t *__restrict__ it = tab + P.i_off;
-    const int32_t *__restrict__ ot = tab + P.o_off;
+    const int nR = P.nRo * P.nRi;
+    const int32_t *__restrict__ sr = tab + P.st_off;
     const int32_t *__restrict__ et = tab + P.et_off;
     for (int r = 0; r < P.rounds; ++r) {
         const int cfg = r * L + s;
@@ -115,66 +119,43 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
 #pragma unroll
         for (int j = 0; j < NF; ++j) fG[j] = gr[4 + j] + g8;
         const bool okG = la && (((dwG ^ W) & M & gf) == 0u);
-        // current outer record (uniform), the inner position
-        int o = 0, i = 0;
-        int ox = ot[2];
-        uint32_t odw = (uint32_t)ot[1];
-        int of[NFA], pso[NFA];
-        double pf[NFA];
-#pragma unroll
-        for (int j = 0; j < NF; ++j) of[j] = ot[4 + j], pso[j] = -1, pf[j] = 0.0;
         double acc = 0.0;
+        // slot s's entry at step k0 + g, one chunk ahead (the tables are padded by one chunk)
+        double wn = bld(ivrs, ivb + et[g], 0);
         for (int k0 = 0; k0 < nR; k0 += C) {
-            const int kk = k0 + g < nR ? k0 + g : nR - 1;
-            const double wl = bld(ivrs, ivb + et[kk], 0);  // slot s's entry at step k0 + g
+            const double wl = wn;
+            if (k0 + C < nR) wn = bld(ivrs, ivb + et[k0 + C + g], 0);
 #pragma unroll
             for (int u0 = 0; u0 < C; u0 += U) {
+                if (k0 + u0 >= nR) break;  // (uniform)
                 double w[U], f[U][NFA];
-                bool ok[U], fl[U], va[U];
-                int xo[U];
+                bool ok[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    va[u] = k0 + u0 + u < nR;
-                    const int32_t *__restrict__ q = it + (size_t)i * IS;
-                    ok[u] = ((odw | (uint32_t)q[1]) & MR) == WR;
+                    const int32_t *__restrict__ q = sr + (size_t)(k0 + u0 + u) * RS;  // (steps >= nR: padding)
+                    ok[u] = (((uint32_t)q[NF]) & MR) == WR;
 #pragma unroll
                     for (int j = 0; j < NF; ++j) {
-                        const int so = of[j] + q[2 + j];
-                        if (so != pso[j]) {  // (uniform) a new factor row
-                            if (MODE == 0 || (MODE == 2 && j < NF - 1))
-                                pf[j] = *reinterpret_cast<const double *>(ldsb + (fG[j] + so));  // byte offsets
-                            else pf[j] = bld(st, fG[j], so);
-                            pso[j] = so;
-                        }
-                        f[u][j] = pf[j];
-                    }
-                    fl[u] = va[u] && i == nRi - 1;
-                    xo[u] = ox;
-                    if (va[u] && ++i == nRi) {  // the next outer configuration (uniform)
-                        i = 0;
-                        if (++o < P.nRo) {
-                            const int32_t *__restrict__ oq = ot + (size_t)o * GS;
-                            odw = (uint32_t)oq[1], ox = oq[2];
-#pragma unroll
-                            for (int j = 0; j < NF; ++j) of[j] = oq[4 + j];
-                        } else {
-                            o = P.nRo - 1;  // (past the end: the remaining steps of the chunk are masked)
-                        }
+                        if (MODE == 0 || (MODE == 2 && j < NF - 1))
+                            f[u][j] = *reinterpret_cast<const double *>(ldsb + (fG[j] + q[j]));  // byte offsets
+                        else f[u][j] = bld(st, fG[j], q[j]);
                     }
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u) w[u] = row_bcast_n(wl, u0 + u);
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    if (!va[u]) continue;
+                    const int k = k0 + u0 + u;
+                    if (k >= nR) break;
                     double x = w[u];
 #pragma unroll
                     for (int j = 0; j < NF; ++j) x *= f[u][j];
                     acc += ok[u] ? x : 0.0;
-                    if (fl[u]) {  // end of an inner run: its bin
+                    const int xo = sr[(size_t)k * RS + NF + 1];
+                    if (xo >= 0) {  // end of an inner run: its bin
                         const double a = okG ? acc : 0.0;
                         if (la) {
-                            const int x8 = (xG + xo[u]) * (C * 8) + g8;
+                            const int x8 = (xG + xo) * (C * 8) + g8;
                             if (bins_lds) *reinterpret_cast<double *>(ldsb + binb + x8) = a;
                             else bst(st, scr_b + x8, a);
                         }
@@ -186,6 +167,54 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
         }
     }
     return tot;
+}
+
+// the post sweep of a pass: output bin b = its nE partial bins added in order, then
+//   Collect     the upstream separator's message  tmp / S
+//   Distribute  a child separator's message  (tmp / S) / old, 0 where old == 0 (old = the child's
+//               Collect message)
+// and the reduced bins for the marginal sweep; LB: the partial / reduced bins live in LDS
+template <bool LB>
+__device__ __forceinline__ void post_sweep(const JtTPass &P, __amdgpu_buffer_rsrc_t st, char *__restrict__ ldsb,
+                                           int s, int g8, double S, int scr_b, int binb, int red_b, int redl) {
+    constexpr int T = 4;  // bins per lane in flight
+    const int nE = P.nE, nb = P.nbins;
+    const double rS = 1.0 / S;
+    auto part = [&](int x) {
+        const int x8 = x * (C * 8) + g8;
+        return LB ? *reinterpret_cast<const double *>(ldsb + binb + x8) : bld(st, scr_b + x8, 0);
+    };
+    for (int b0 = 0; b0 < nb; b0 += T * L) {
+        double v[T], old[T];
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const int b = b0 + t * L + s, bc = b < nb ? b : nb - 1;
+            v[t] = part(bc * nE);
+            old[t] = P.kind == JT_T_DIS ? bld(st, (P.col_row + bc) * (C * 8) + g8, 0) : 1.0;
+        }
+        for (int e = 1; e < nE; ++e) {
+            double w[T];
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                const int b = b0 + t * L + s, bc = b < nb ? b : nb - 1;
+                w[t] = part(bc * nE + e);
+            }
+#pragma unroll
+            for (int t = 0; t < T; ++t) v[t] += w[t];
+        }
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const int b = b0 + t * L + s;
+            if (b >= nb) continue;
+            if (P.kind == JT_T_COL) bst(st, (P.dest_row + b) * (C * 8) + g8, v[t] * rS);
+            else if (P.kind == JT_T_DIS)
+                bst(st, (P.dest_row + b) * (C * 8) + g8, old[t] == 0.0 ? 0.0 : (v[t] * rS) / old[t]);
+            if (P.nmv > 0) {
+                if (LB) *reinterpret_cast<double *>(ldsb + redl + b * (C * 8) + g8) = v[t];
+                else bst(st, red_b + b * (C * 8) + g8, v[t]);
+            }
+        }
+    }
 }
 
 #define FBN_TCASE(NFv)                                                                                    \
@@ -228,8 +257,11 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
         bool bad = false;
         for (int p = 0; p < npass; ++p) {
             const JtTPass P = passes[p];
-            unsigned long long t0 = prof ? clock64() : 0ull;
+            unsigned long long t0 = prof ? dclock() : 0ull;
             if (P.first) {
+                // the messages earlier passes stored (other lanes) become visible: one fence per clique
+                // phase (no pass of a phase reads what another pass of the same phase writes)
+                __threadfence_block();
                 M = 0u, W = 0u;
                 const int32_t *__restrict__ vr = tab + P.vars_off;
                 int xs[kMaxCliqueVars];  // every evidence byte in flight at once
@@ -255,7 +287,7 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
                 }
             }
             if (prof) {
-                const unsigned long long t1 = clock64();
+                const unsigned long long t1 = dclock();
                 pc[0] += t1 - t0;
                 t0 = t1;
             }
@@ -280,7 +312,7 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
                     }
                 }
                 if (prof) {
-                    const unsigned long long t1 = clock64();
+                    const unsigned long long t1 = dclock();
                     pc[1 + P.mode] += t1 - t0;
                     t0 = t1;
                 }
@@ -288,40 +320,21 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
                 bad |= act && !(S >= 0x1p-900 && S <= 0x1p+900);
                 if (bins_lds) __syncthreads();  // the partial bins, written by other lanes, become visible
                 else __threadfence_block();
-                // post sweep: output bin b = sum of its nE partial bins (in order); four bins per lane in
-                // flight
-                const int nE = P.nE, nb = P.nbins;
-                auto part = [&](int b, int e) {
-                    const int x8 = (b * nE + e) * (C * 8) + g8;
-                    return bins_lds ? *reinterpret_cast<const double *>(ldsb + binb + x8) : bld(st, scr_b + x8, 0);
-                };
-                for (int b0 = 0; b0 < nb; b0 += 4 * L) {
-                    double v[4] = {0.0, 0.0, 0.0, 0.0}, old[4] = {1.0, 1.0, 1.0, 1.0};
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        const int b = b0 + t * L + s;
-                        if (b < nb) {
-                            for (int e = 0; e < nE; ++e) v[t] += part(b, e);
-                            if (P.kind == JT_T_DIS) old[t] = bld(st, (P.col_row + b) * (C * 8) + g8, 0);
-                        }
-                    }
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        const int b = b0 + t * L + s;
-                        if (b >= nb) continue;
-                        if (P.kind == JT_T_COL) bst(st, (P.dest_row + b) * (C * 8) + g8, v[t] / S);
-                        else if (P.kind == JT_T_DIS)
-                            bst(st, (P.dest_row + b) * (C * 8) + g8, old[t] == 0.0 ? 0.0 : (v[t] / S) / old[t]);
-                        if (P.nmv > 0) {
-                            if (bins_lds) *reinterpret_cast<double *>(ldsb + redl + b * (C * 8) + g8) = v[t];
-                            else bst(st, red_b + b * (C * 8) + g8, v[t]);
-                        }
-                    }
-                }
-                if (bins_lds) __syncthreads();
-                __threadfence_block();  // (the messages: read by later passes, by other lanes)
                 if (prof) {
-                    const unsigned long long t1 = clock64();
+                    const unsigned long long t1 = dclock();
+                    pc[7] += t1 - t0;  // pass total + the partial bins' visibility
+                    t0 = t1;
+                }
+                // post sweep: output bin b = sum of its nE partial bins (in order); four bins per lane in
+                // flight, every load of a step issued before any use
+                if (bins_lds) post_sweep<true>(P, st, ldsb, s, g8, S, scr_b, binb, red_b, redl);
+                else post_sweep<false>(P, st, ldsb, s, g8, S, scr_b, binb, red_b, redl);
+                if (P.nmv > 0) {  // the reduced bins, for the marginal sweep (other lanes)
+                    if (bins_lds) __syncthreads();
+                    else __threadfence_block();
+                }
+                if (prof) {
+                    const unsigned long long t1 = dclock();
                     pc[4] += t1 - t0;
                     t0 = t1;
                 }
@@ -339,12 +352,22 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
                 for (int c = 0; c < kValChunks; ++c) a[c] = 0.0;
                 if (need) {
                     const int32_t *__restrict__ bd = tab + P.bdig_off;
-                    for (int b = 0; b < P.nbins; ++b) {
-                        const int dg = (int)(((uint32_t)bd[b] >> sh) & fm);
-                        const double v = bins_lds ? *reinterpret_cast<const double *>(ldsb + redl + b * (C * 8) + g8)
-                                                  : bld(st, red_b + b * (C * 8) + g8, 0);
+                    const int nb = P.nbins;
+                    for (int b0 = 0; b0 < nb; b0 += 4) {
+                        double v[4];
 #pragma unroll
-                        for (int c = 0; c < kValChunks; ++c) a[c] += dg == c * L + s ? v : 0.0;
+                        for (int t = 0; t < 4; ++t) {
+                            const int bc = b0 + t < nb ? b0 + t : nb - 1;
+                            v[t] = bins_lds ? *reinterpret_cast<const double *>(ldsb + redl + bc * (C * 8) + g8)
+                                            : bld(st, red_b + bc * (C * 8) + g8, 0);
+                        }
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            if (b0 + t >= nb) break;
+                            const int dg = (int)(((uint32_t)bd[b0 + t] >> sh) & fm);
+#pragma unroll
+                            for (int c = 0; c < kValChunks; ++c) a[c] += dg == c * L + s ? v[t] : 0.0;
+                        }
                     }
                 }
                 double am = 0.0;  // the lane's values in chunk order, then the slot butterfly
@@ -370,14 +393,14 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
                     if (act && !obs && s == 0) labels[cs] = lab;
                 }
             }
-            if (prof) pc[5] += clock64() - t0;
+            if (prof) pc[5] += dclock() - t0;
         }
         const unsigned long long fb = __ballot(bad);
         if (fb && lane == 0) atomicOr(flags + (cg * C) / 64, 1);
     }
     if (prof && lane == 0) {
         pc[6] = clock64() - t_all;
-        for (int k = 0; k < 7; ++k) atomicAdd(prof + k, pc[k]);
+        for (int k = 0; k < 8; ++k) atomicAdd(prof + k, pc[k]);
     }
 }
 

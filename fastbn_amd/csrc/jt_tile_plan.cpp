@@ -299,14 +299,33 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
         emit(RO, true);
         P.i_off = (int32_t)prog.tab.size();
         emit(RI, false);
-        {  // flattened entry offsets of the R stream (outer x inner), bytes: the kernel's per-lane gather
+        {  // the flattened R stream (outer x inner): per step the entry's R part (bytes: the kernel's
+           // per-lane gather), and a step record {factor soffsets [nf], digit word, bin offset of the
+           // inner run that ends here or -1}
             const int64_t nRo_ = Prod(t, RO), nRi_ = Prod(t, RI);
             const int32_t *ro = prog.tab.data() + P.o_off, *ri = prog.tab.data() + P.i_off;
-            std::vector<int32_t> et((size_t)(nRo_ * nRi_));
+            std::vector<int32_t> et((size_t)(nRo_ * nRi_)), sr((size_t)(nRo_ * nRi_ * (nf + 2)));
             for (int64_t o = 0; o < nRo_; ++o)
-                for (int64_t i = 0; i < nRi_; ++i) et[o * nRi_ + i] = ro[o * (4 + nf)] * 8 + ri[i * (2 + nf)];
+                for (int64_t i = 0; i < nRi_; ++i) {
+                    const int64_t k = o * nRi_ + i;
+                    const int32_t *oq = ro + o * (4 + nf), *iq = ri + i * (2 + nf);
+                    et[k] = oq[0] * 8 + iq[0];
+                    int32_t *q = &sr[k * (nf + 2)];
+                    for (int f = 0; f < nf; ++f) q[f] = oq[4 + f] + iq[2 + f];
+                    q[nf] = (int32_t)((uint32_t)oq[1] | (uint32_t)iq[1]);
+                    q[nf + 1] = i == nRi_ - 1 ? oq[2] : -1;
+                }
+            // padded by one chunk (JT_T_C steps, zero offsets, no bin): the kernel reads whole chunks
+            et.resize(et.size() + JT_T_C, 0);
+            for (int pad = 0; pad < JT_T_C; ++pad) {
+                for (int f = 0; f < nf; ++f) sr.push_back(0);
+                sr.push_back(0);
+                sr.push_back(-1);
+            }
             P.et_off = (int32_t)prog.tab.size();
             prog.tab.insert(prog.tab.end(), et.begin(), et.end());
+            P.st_off = (int32_t)prog.tab.size();
+            prog.tab.insert(prog.tab.end(), sr.begin(), sr.end());
         }
         uint32_t of = 0;
         for (int j : RO) of |= (uint32_t)fm[c][j] << sh[c][j];

@@ -12,7 +12,7 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "oracle"))
-PHASES = ["stage", "entries/lds", "entries/global", "entries/mixed", "post", "marginals", "all"]
+PHASES = ["stage", "entries/lds", "entries/global", "entries/mixed", "post sweep", "marginals", "all", "pass total"]
 
 
 def child(cases, wpcs, with_v4):
@@ -56,7 +56,7 @@ def child(cases, wpcs, with_v4):
             torch.cuda.synchronize(dev)
             F.lib.fbn_jt_debug_op_cycles(jt._h, 0, buf)
             tot = max(1, buf[6])
-            line += " | " + " ".join(f"{n} {100.0 * buf[k] / tot:.1f}%" for k, n in enumerate(PHASES[:6]))
+            line += " | " + " ".join(f"{n} {100.0 * buf[k] / tot:.1f}%" for k, n in enumerate(PHASES) if k != 6)
             line += f" | lds/wave {info['tiled_lds_bytes']}"
         print(line, flush=True)
 
