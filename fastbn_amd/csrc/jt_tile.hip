@@ -169,28 +169,29 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
     return tot;
 }
 
-// the post sweep of a pass: output bin b = its nE partial bins added in order, then
-//   Collect     the upstream separator's message  tmp / S
-//   Distribute  a child separator's message  (tmp / S) / old, 0 where old == 0 (old = the child's
-//               Collect message)
-// and the reduced bins for the marginal sweep; LB: the partial / reduced bins live in LDS
+// the post sweep of a pass: output bin b = its nE partial bins added in order (U(b)), then
+//   Collect     the upstream separator's message  U / S, S = the pass total
+//   Distribute  a child separator's message  U / S, 0 where old == 0 (old = the child's Collect
+//               message, left out of the pass's factors: it cancels), S = sum_b old(b) U(b)
+// and the reduced bins for the marginal sweep (old * U for Distribute); LB: the partial / reduced
+// bins live in LDS.  Returns S.
 template <bool LB>
-__device__ __forceinline__ void post_sweep(const JtTPass &P, __amdgpu_buffer_rsrc_t st, char *__restrict__ ldsb,
-                                           int s, int g8, double S, int scr_b, int binb, int red_b, int redl) {
+__device__ __forceinline__ double post_sweep(const JtTPass &P, __amdgpu_buffer_rsrc_t st, char *__restrict__ ldsb,
+                                             int s, int g8, double S, int scr_b, int binb, int red_b, int redl) {
     constexpr int T = 4;  // bins per lane in flight
     const int nE = P.nE, nb = P.nbins;
-    const double rS = 1.0 / S;
+    const bool dis = P.kind == JT_T_DIS;
     auto part = [&](int x) {
         const int x8 = x * (C * 8) + g8;
         return LB ? *reinterpret_cast<const double *>(ldsb + binb + x8) : bld(st, scr_b + x8, 0);
     };
-    for (int b0 = 0; b0 < nb; b0 += T * L) {
-        double v[T], old[T];
+    // T bins of this lane from b0: U and old
+    auto load = [&](int b0, double (&v)[T], double (&old)[T]) {
 #pragma unroll
         for (int t = 0; t < T; ++t) {
             const int b = b0 + t * L + s, bc = b < nb ? b : nb - 1;
             v[t] = part(bc * nE);
-            old[t] = P.kind == JT_T_DIS ? bld(st, (P.col_row + bc) * (C * 8) + g8, 0) : 1.0;
+            old[t] = dis ? bld(st, (P.col_row + bc) * (C * 8) + g8, 0) : 1.0;
         }
         for (int e = 1; e < nE; ++e) {
             double w[T];
@@ -202,19 +203,36 @@ __device__ __forceinline__ void post_sweep(const JtTPass &P, __amdgpu_buffer_rsr
 #pragma unroll
             for (int t = 0; t < T; ++t) v[t] += w[t];
         }
+    };
+    if (dis) {  // S = sum_b old(b) U(b), lane partials in bin order, then the slot butterfly
+        double sp = 0.0;
+        for (int b0 = 0; b0 < nb; b0 += T * L) {
+            double v[T], old[T];
+            load(b0, v, old);
+#pragma unroll
+            for (int t = 0; t < T; ++t)
+                if (b0 + t * L + s < nb) sp += old[t] * v[t];
+        }
+        S = slot_sum(sp);
+    }
+    const double rS = 1.0 / S;
+    for (int b0 = 0; b0 < nb; b0 += T * L) {
+        double v[T], old[T];
+        load(b0, v, old);
 #pragma unroll
         for (int t = 0; t < T; ++t) {
             const int b = b0 + t * L + s;
             if (b >= nb) continue;
             if (P.kind == JT_T_COL) bst(st, (P.dest_row + b) * (C * 8) + g8, v[t] * rS);
-            else if (P.kind == JT_T_DIS)
-                bst(st, (P.dest_row + b) * (C * 8) + g8, old[t] == 0.0 ? 0.0 : (v[t] * rS) / old[t]);
+            else if (dis) bst(st, (P.dest_row + b) * (C * 8) + g8, old[t] == 0.0 ? 0.0 : v[t] * rS);
             if (P.nmv > 0) {
-                if (LB) *reinterpret_cast<double *>(ldsb + redl + b * (C * 8) + g8) = v[t];
-                else bst(st, red_b + b * (C * 8) + g8, v[t]);
+                const double red = dis ? old[t] * v[t] : v[t];
+                if (LB) *reinterpret_cast<double *>(ldsb + redl + b * (C * 8) + g8) = red;
+                else bst(st, red_b + b * (C * 8) + g8, red);
             }
         }
     }
+    return S;
 }
 
 #define FBN_TCASE(NFv)                                                                                    \
@@ -317,7 +335,6 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
                     t0 = t1;
                 }
                 S = slot_sum(tot);
-                bad |= act && !(S >= 0x1p-900 && S <= 0x1p+900);
                 if (bins_lds) __syncthreads();  // the partial bins, written by other lanes, become visible
                 else __threadfence_block();
                 if (prof) {
@@ -327,8 +344,9 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
                 }
                 // post sweep: output bin b = sum of its nE partial bins (in order); four bins per lane in
                 // flight, every load of a step issued before any use
-                if (bins_lds) post_sweep<true>(P, st, ldsb, s, g8, S, scr_b, binb, red_b, redl);
-                else post_sweep<false>(P, st, ldsb, s, g8, S, scr_b, binb, red_b, redl);
+                if (bins_lds) S = post_sweep<true>(P, st, ldsb, s, g8, S, scr_b, binb, red_b, redl);
+                else S = post_sweep<false>(P, st, ldsb, s, g8, S, scr_b, binb, red_b, redl);
+                bad |= act && !(S >= 0x1p-900 && S <= 0x1p+900);
                 if (P.nmv > 0) {  // the reduced bins, for the marginal sweep (other lanes)
                     if (bins_lds) __syncthreads();
                     else __threadfence_block();

@@ -433,13 +433,21 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
         int32_t so;
         place(fac, has_parent, &nst, &so);
         bool first = true;
-        for (int s : plan.clique_down[c]) {
+        for (size_t ci = 0; ci < plan.clique_down[c].size(); ++ci) {
+            const int s = plan.clique_down[c][ci];
             const Table &sp = plan.seps[s];
             std::vector<int> opos, mv;
             for (int v : sp.vars) opos.push_back(PosIn(t.vars, v));
             for (int v : sp.vars)
                 if (src_sep[v] == s) mv.push_back(v);
-            if ((rc = build_pass(c, JT_T_DIS, opos, std::vector<int64_t>(sp.cum.begin(), sp.cum.end()), sp.size(), fac,
+            // the child's own Collect message M_i is constant on each output bin b and cancels in
+            // SEPDIS: tmp(b) = M_i(b) U(b) / S, dis(b) = tmp(b) / M_i(b) = U(b) / S (0 where M_i(b) = 0),
+            // S = sum_b M_i(b) U(b) -- so the pass multiplies every other factor and the post sweep
+            // forms S from the bins
+            std::vector<Factor> sub;
+            for (size_t j = 0; j < fac.size(); ++j)
+                if (j != ci) sub.push_back(fac[j]);
+            if ((rc = build_pass(c, JT_T_DIS, opos, std::vector<int64_t>(sp.cum.begin(), sp.cum.end()), sp.size(), sub,
                                  dis[s], col[s], mv, first, nst, so)))
                 return rc;
             first = false;

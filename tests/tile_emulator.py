@@ -75,9 +75,12 @@ def run_case(prog, ev_row, sum_dom, lds_bytes=1 << 20):
         if P["kind"] == COL:
             store[P["dest_row"]:P["dest_row"] + nb] = v / S
         elif P["kind"] == DIS:
+            # the child's own Collect message (not a factor of the pass) cancels: dis = U / S with
+            # S = sum old * U; the marginal bins are old * U
             old = store[P["col_row"]:P["col_row"] + nb]
-            with np.errstate(divide="ignore", invalid="ignore"):
-                store[P["dest_row"]:P["dest_row"] + nb] = np.where(old == 0.0, 0.0, (v / S) / old)
+            S = (old * v).sum()
+            store[P["dest_row"]:P["dest_row"] + nb] = np.where(old == 0.0, 0.0, v / S)
+            v = old * v
         bd = tab[P["bdig_off"]:P["bdig_off"] + nb].astype(np.int64) & 0xFFFFFFFF
         for var, off, dim, sh, fm in mv:
             if int(ev_row[var]) >= 0:
