@@ -242,12 +242,24 @@ def bench_pc(steps, warmup):
                          "frac": achieved / HBM_PEAK_GBS, "model_bytes_per_run": model_bytes,
                          "achieved_kernel_only": model_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None,
                          "kernel_ms_per_run": kernel_ms, "wall_ms_per_run": ms,
-                         "column_bytes_read_per_run": pc.device_bytes,
+                         "column_bytes_read_per_run": pc.device_bytes, **pc_small_traffic(),
                          "note": "achieved = SURVEY 8(d) byte model (N (d + 2) bytes per reference-equivalent test, "
                                  "80.3 MB per run) / C-ABI wall time.  The whole skeleton search is ONE device launch "
                                  "(pc_small.hip: five levels, one grid barrier each) over a column store that stays "
                                  "in cache (185 KB): a latency chain of five dependent levels, not bound by HBM or "
                                  "VALU, so frac is small by construction (DESIGN.md 5.4)"}}
+
+
+def pc_small_traffic():
+    """Measured L2<->fabric bytes of one device-resident search launch (rocprofv3 FETCH_SIZE +
+    WRITE_SIZE, calibrated; committed summary profiles/r04/pmc_pc_small_traffic.json from
+    tools/profile_r04.sh)."""
+    path = os.path.join(REPO, "profiles", "r04", "pmc_pc_small_traffic.json")
+    if not os.path.exists(path):
+        return {"traffic": None}
+    with open(path) as f:
+        t = json.load(f)
+    return {"traffic": t["hbm_bytes_per_launch"], "traffic_source": "profiles/r04/pmc_pc_small_traffic.json"}
 
 
 N_VARS_C5 = 1000
@@ -593,7 +605,7 @@ def bench_munin(steps, warmup, cases=125_000, rank=0, world=1, device=0, with_ba
             "wall_ms_per_step": 1e3 * wall / steps, "plan_s": plan_s,
             "kernel_variant": jt.refresh_info()["variant"],
             "arithmetic_order": "exact" if (exact or (exact is None and jt.info["specialized_eligible"]))
-                                else "fast (one-pass Collect denominators)",
+                                else "fast (normalizations cancel; labels equal, marginals within 1e-12)",
             "parity_vs_oracle_16_cases": {"labels_equal_and_marg_within_1e-12": bool(ok), "max_rel_err": rel},
             "cliques": jt.info["num_cliques"], "clique_entries": jt.info["clique_entries"],
             "roofline": {"bound": "hbm", "achieved": bpc * cases / (k * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
@@ -615,9 +627,9 @@ def munin_traffic(cases, kernel_ms):
     b = t["hbm_bytes_per_launch"] * cases / t["cases_per_launch"]
     return {"traffic": b, "traffic_rate_GBs": b / (kernel_ms * 1e-3) / 1e9,
             "traffic_frac": b / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-            "traffic_note": "the streamed kernel recomputes clique tables from separator messages instead of "
-                            "storing them; its measured traffic (message re-reads + per-wave scratch tables) "
-                            "exceeds the materialized-table bytes and is what bounds it (DESIGN.md 5.2)"}
+            "traffic_note": "the tiled kernel recomputes every clique entry from its initial potential and the "
+                            "separator messages instead of storing clique tables; its measured traffic is the "
+                            "message rows re-read from L2 misses plus the per-wave message store (DESIGN.md 5.2)"}
 
 
 VALU_PEAK_LANE_OPS = 256 * 4 * 16 * 2.4e9  # MI355X: CUs x SIMDs x lanes x clock (fp64 FMA full rate)

@@ -245,20 +245,21 @@ def test_bad_evidence_rejected_on_device_path(jt, ojt):
 
 
 def test_munin_like_full_network_vs_reference(munin_fixture):
-    """BASELINE config 4 at its real network size: the streamed kernel (default variant for the
-    1041-variable plan) on the reference's 32 fixture cases -- labels equal to the reference's,
-    marginals within 1e-12 relative (its heap-ordered tree breaks a few Prim ties differently,
-    conftest.MUNIN_REF_RTOL), and bit-identical to the restatement on our tree."""
+    """BASELINE config 4 at its real network size on the reference's 32 fixture cases: the tiled
+    kernel (default for the 1041-variable plan, fast order) -- labels equal to the reference's,
+    marginals within 1e-9 relative; the streamed kernel in exact order -- within 1e-12 relative (the
+    reference's heap-ordered tree breaks a few Prim ties differently, conftest.MUNIN_REF_RTOL) and
+    bit-identical to the restatement on our tree."""
     from conftest import MUNIN_REF_RTOL, read_ref_marg
     jt = F.JunctionTree(F.Network(munin_fixture["xml"]), device=0)
     o = O.OracleJT(munin_fixture["xml"])
     ev, _ = O.load_libsvm(munin_fixture["libsvm"], o.n)
     rlab, rmarg, _, _ = read_ref_marg(munin_fixture["marg"], o.dims)
     olab, omarg = o.infer(ev)
-    # default (auto = fast order for this plan): labels equal the reference's, marginals within 1e-9
-    # relative of the reference's own (north_star: 1e-6)
+    # default (auto = fast order for this plan, the tiled kernel): labels equal the reference's,
+    # marginals within 1e-9 relative of the reference's own (north_star: 1e-6)
     lab, marg = jt.infer(ev)
-    assert jt.refresh_info()["variant"] == 4
+    assert jt.refresh_info()["variant"] == 5
     np.testing.assert_array_equal(lab, rlab)
     np.testing.assert_allclose(marg, rmarg, rtol=1e-9, atol=1e-300)
     np.testing.assert_allclose(marg, omarg, rtol=1e-12, atol=1e-300)

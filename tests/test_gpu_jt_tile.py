@@ -1,0 +1,120 @@
+"""The tiled JT kernel (variant 5, fastbn_amd/csrc/jt_tile.hip: 16 cases x 4 entry slots per wave,
+fast arithmetic order -- the Munin-class default) against the oracle: labels equal, marginals within
+1e-12 relative (north_star allows 1e-6 on potentials), evidence variables zero, every other marginal a
+distribution; the forced exact-fixup path bit-identical to the oracle; run-to-run identical results.
+The reference's own Munin-like dump: tests/test_gpu_jt.py::test_munin_like_full_network_vs_reference."""
+import os
+
+import numpy as np
+import pytest
+from conftest import GOLD
+
+import fastbn_amd as F
+import oracle as O
+from fastbn_amd import synth
+
+pytestmark = pytest.mark.gpu
+ALARM = os.path.join(GOLD, "alarm", "alarm.xml")
+
+
+def _check(lab, marg, olab, omarg, ev, dims):
+    np.testing.assert_array_equal(lab, olab)
+    np.testing.assert_allclose(marg, omarg, rtol=1e-12, atol=1e-300)
+    off = np.concatenate([[0], np.cumsum(dims)])
+    for v in range(len(dims)):
+        s = marg[:, off[v]:off[v + 1]].sum(1)
+        obs = ev[:, v] >= 0
+        assert np.all(marg[obs, off[v]:off[v + 1]] == 0) and np.allclose(s[~obs], 1.0, atol=1e-12)
+
+
+@pytest.fixture(scope="module")
+def alarm():
+    jt = F.JunctionTree(F.Network(ALARM), device=0)
+    assert jt.info["tiled_eligible"] == 1
+    jt.set_variant(5)
+    return jt, O.OracleJT(ALARM)
+
+
+@pytest.mark.parametrize("n", [1, 15, 16, 17, 63, 64, 65, 1000])
+def test_alarm_ragged_batches(alarm, n):
+    jt, ojt = alarm
+    ev = synth.evidence_cases(synth.read_xmlbif(ALARM), n, 7, seed=100 + n)
+    lab, marg = jt.infer(ev)
+    _check(lab, marg, *ojt.infer(ev), ev, jt.network.dims)
+
+
+def test_alarm_evidence_extremes(alarm):
+    jt, ojt = alarm
+    rng = np.random.default_rng(5)
+    dims = jt.network.dims
+    ev = np.full((20, 37), -1, np.int8)
+    ev[1, 1:] = [rng.integers(0, d) for d in dims[1:]]  # everything but the query observed
+    ev[2, 1::2] = [rng.integers(0, d) for d in dims[1::2]]
+    ev[3, 36] = 0
+    for r in range(4, 20):  # many observed variables, random
+        k = rng.integers(1, 30)
+        vs = rng.choice(np.arange(1, 37), k, replace=False)
+        ev[r, vs] = [rng.integers(0, dims[v]) for v in vs]
+    lab, marg = jt.infer(ev)
+    _check(lab, marg, *ojt.infer(ev), ev, dims)
+
+
+def test_alarm_forced_fixup_is_exact(alarm):
+    """Every 64-case block through the exact interpreter pass: the oracle's bits."""
+    jt, ojt = alarm
+    ev = synth.evidence_cases(synth.read_xmlbif(ALARM), 300, 7, seed=4)
+    jt.debug_force_fixup(True)
+    try:
+        lab, marg = jt.infer(ev)
+    finally:
+        jt.debug_force_fixup(False)
+    olab, omarg = ojt.infer(ev)
+    np.testing.assert_array_equal(lab, olab)
+    np.testing.assert_array_equal(marg, omarg)
+
+
+def test_run_to_run_identical_and_waves(alarm):
+    jt, _ = alarm
+    ev = synth.evidence_cases(synth.read_xmlbif(ALARM), 5000, 7, seed=6)
+    lab, marg = jt.infer(ev)
+    for w in (4, 8, 16, 0):
+        jt.set_waves_per_cu(w)
+        lab2, marg2 = jt.infer(ev)
+        np.testing.assert_array_equal(lab2, lab)
+        np.testing.assert_array_equal(marg2, marg)
+
+
+@pytest.mark.parametrize("nodes,window,dom,k", [(200, 10, (2, 5), 40), (120, 6, (2, 8), 25), (60, 4, (5, 8), 10)])
+def test_synthetic_networks(tmp_path, nodes, window, dom, k):
+    """Random networks, state counts up to 8 (the marginal sweep's value chunks > 4 slots)."""
+    p = str(tmp_path / "syn.xml")
+    synth.random_network(nodes, seed=nodes + k, window=window, dom=dom, path=p)
+    net = synth.read_xmlbif(p)
+    ev = synth.evidence_cases(net, 333, k, seed=nodes)
+    ev[0, :] = -1  # no evidence
+    jt = F.JunctionTree(F.Network(p), device=0)
+    if not jt.info["tiled_eligible"]:
+        pytest.skip("plan outside the tiled variant's limits")
+    jt.set_variant(5)
+    lab, marg = jt.infer(ev)
+    _check(lab, marg, *O.OracleJT(p).infer(ev), ev, jt.network.dims)
+
+
+def test_munin_like_default_and_vs_oracle(tmp_path):
+    """BASELINE config 4's network: auto mode takes the tiled kernel (fast order); 136 cases incl. one
+    without evidence against the oracle; exact mode still runs the streamed kernel (variant 4)."""
+    p = str(tmp_path / "munin_like.xml")
+    synth.random_network(1041, seed=1041, window=12, path=p, name="munin_like")
+    net = synth.read_xmlbif(p)
+    ev = synth.evidence_cases(net, 136, 208, seed=20250131)
+    ev[0, :] = -1
+    jt = F.JunctionTree(F.Network(p), device=0)
+    lab, marg = jt.infer(ev)
+    assert jt.refresh_info()["variant"] == 5
+    olab, omarg = O.OracleJT(p).infer(ev)
+    _check(lab, marg, olab, omarg, ev, jt.network.dims)
+    jt.set_exact(True)
+    lab, marg = jt.infer(ev)
+    assert jt.refresh_info()["variant"] == 4
+    np.testing.assert_array_equal(lab, olab)
+    np.testing.assert_array_equal(marg, omarg)
