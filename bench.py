@@ -604,8 +604,7 @@ def bench_munin(steps, warmup, cases=125_000, rank=0, world=1, device=0, with_ba
             "unit": "cases/s", "n_gpus": world, "cases": cases * world, "cases_per_gpu": cases, "kernel_ms": k,
             "wall_ms_per_step": 1e3 * wall / steps, "plan_s": plan_s,
             "kernel_variant": jt.refresh_info()["variant"],
-            "arithmetic_order": "exact" if (exact or (exact is None and jt.info["specialized_eligible"]))
-                                else "fast (normalizations cancel; labels equal, marginals within 1e-12)",
+            "arithmetic_order": "exact" if exact else "fast (normalizations cancel; labels equal, marginals within 1e-12)",
             "parity_vs_oracle_16_cases": {"labels_equal_and_marg_within_1e-12": bool(ok), "max_rel_err": rel},
             "cliques": jt.info["num_cliques"], "clique_entries": jt.info["clique_entries"],
             "roofline": {"bound": "hbm", "achieved": bpc * cases / (k * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
@@ -788,7 +787,10 @@ def main():
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle as O
         olab, omarg = O.OracleJT(os.path.join(ALARM, "alarm.xml")).infer(ev[:256])
-        ok = (d_lab[:256].cpu().numpy() == olab).all() and (d_marg[:256].cpu().numpy() == omarg).all()
+        # default (fast) arithmetic order: labels equal, marginals within 1e-12 relative
+        gm = d_marg[:256].cpu().numpy()
+        alarm_rel = float(np.max(np.abs(gm - omarg) / np.maximum(np.abs(omarg), 1e-300)))
+        ok = (d_lab[:256].cpu().numpy() == olab).all() and alarm_rel <= 1e-12
         if not ok:
             log("ERROR: GPU results differ from the oracle")
             sys.exit(1)
@@ -819,11 +821,17 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel_ms": kernel_ms, "algorithmic_bytes_per_case": bpc,
                      "kernel_variant": jt.refresh_info()["variant"],
+                     "arithmetic_order": "fast (normalizations cancel; labels equal, marginals within 1e-12)",
+                     "parity_vs_oracle_256_cases": {"labels_equal": True,
+                                                    "max_rel_err": alarm_rel if rank == 0 else None},
                      "valu": valu_roofline("alarm", args.cases, kernel_ms),
-                     "note": "achieved = materialized-table algorithmic bytes (SURVEY 8(d)) / kernel time; the "
-                             "specialized kernel keeps tables in registers/LDS and recomputes instead of "
-                             "parking them, so measured traffic is below the algorithmic bytes and the "
-                             "kernel is fp64-VALU/latency bound (DESIGN.md)"},
+                     "traffic_frac": (traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+                     "note": "achieved = materialized-table algorithmic bytes (SURVEY 8(d): every per-case table "
+                             "written and read once) / kernel time; frac may exceed 1 and is not clipped "
+                             "(SURVEY 8(d)): the specialized kernel keeps tables in registers/LDS and "
+                             "recomputes instead of parking them, so its measured traffic (traffic, "
+                             "traffic_frac: separator rows of the per-wave workspace) is far below the model "
+                             "and the kernel is latency bound at one wave per SIMD (valu frac; DESIGN.md 5.1)"},
     }
     if world > 1 and not args.no_munin:
         # BASELINE config 4 at its real scale: 125k Munin-like cases per rank (1M on 8 GPUs)

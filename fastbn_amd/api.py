@@ -330,9 +330,9 @@ class JunctionTree:
         lib.fbn_jt_debug_force_fixup(self._h, int(enable))
 
     def set_exact(self, exact):
-        """Streamed kernel arithmetic order: True = the reference's (bit-identical), False = fast
-        (one-pass Collect denominators, within a few ulp), None = auto (exact for ALARM-class plans,
-        fast for Munin-class ones)."""
+        """Arithmetic order of the specialized / streamed kernels: True = the reference's
+        (bit-identical), False = fast (normalizations that cancel left out; labels equal, marginals
+        within 1e-12), None = auto (fast)."""
         lib.fbn_jt_set_exact(self._h, -1 if exact is None else int(bool(exact)))
 
     def build_kernel(self):

@@ -173,14 +173,14 @@ struct fbn_jt_plan {
     // plan-specialized kernel (variant 3)
     bool gen_eligible = false;
     int gen_state = 0;  // 0 not tried, 1 loaded, -1 failed
+    bool gen_fast = false;  // arithmetic order of the loaded specialized kernel
     hipModule_t gen_mod = nullptr;
     hipFunction_t gen_fn = nullptr;
     int64_t gen_we = 0, gen_lds = 0;
     DevBuf flags, ws_fix, gen_iv;
     bool force_fixup = false;
-    // arithmetic order of the streamed kernel: 1 = the reference's (bit-identical), 0 = fast (one-pass
-    // Collect denominators, results within a few ulp per operation), -1 = auto (exact for plans
-    // the specialized kernel takes -- ALARM class --, fast for the rest -- Munin class)
+    // arithmetic order of the specialized / streamed kernels: 1 = the reference's (bit-identical),
+    // 0 = fast (normalizations that cancel left out, within 1e-12), -1 = auto (fast)
     int exact = -1;
     DevBuf ops, aux, initv, dig;
     DevBuf lops, laux, linitv, ldig;
@@ -715,7 +715,8 @@ int fbn_jt_plan_dump(const fbn_jt_plan *p, const char *plan_path, const char *in
 }
 
 constexpr int kJtVFast = 1 << 12;  // jt_virt.hip kVFast
-static bool JtFast(const fbn_jt_plan *p) { return p->exact == 0 || (p->exact < 0 && !p->gen_eligible); }
+// auto (-1) = the fast arithmetic order for every kernel that has one; exact (1) on request
+static bool JtFast(const fbn_jt_plan *p) { return p->exact != 1; }
 
 int fbn_jt_set_waves_per_cu(fbn_jt_plan *p, int waves) {
     if (!p || waves < 0 || waves > 32) return SetError(FBN_ERR_ARG, "waves per CU must be 0..32");
@@ -736,12 +737,18 @@ int fbn_jt_set_variant(fbn_jt_plan *p, int variant) {
 
 // load (cache) or compile (hiprtc) the plan-specialized kernel once per plan
 static int GenEnsure(fbn_jt_plan *p) {
+    const bool fast = JtFast(p);
+    if (p->gen_state != 0 && p->gen_fast != fast) {  // the other arithmetic order was loaded (or failed)
+        if (p->gen_mod) (void)hipModuleUnload(p->gen_mod);
+        p->gen_mod = nullptr, p->gen_fn = nullptr, p->gen_state = 0;
+    }
     if (p->gen_state == 1) return FBN_OK;
     if (p->gen_state == -1) return FBN_ERR_HIP;
     p->gen_state = -1;
+    p->gen_fast = fast;
     std::string src;
     std::vector<double> iv;
-    int rc = fbn::GenerateJTKernel(p->host, src, &p->gen_we, iv, &p->gen_lds);
+    int rc = fbn::GenerateJTKernel(p->host, src, &p->gen_we, iv, &p->gen_lds, fast);
     if (rc) return rc;
     std::vector<char> code;
     if ((rc = fbn::JitCodeObject(src, code))) return rc;
@@ -775,7 +782,7 @@ int fbn_jt_kernel_source(const fbn_jt_plan *p, char *buf, int64_t cap, int64_t *
     std::string src;
     std::vector<double> iv;
     int64_t we = 0;
-    int rc = fbn::GenerateJTKernel(p->host, src, &we, iv);
+    int rc = fbn::GenerateJTKernel(p->host, src, &we, iv, nullptr, JtFast(p));
     if (rc) return rc;
     if (len) *len = (int64_t)src.size() + 1;
     if (buf && cap > 0) {
@@ -792,7 +799,7 @@ int fbn_jt_kernel_cache_path(const fbn_jt_plan *p, char *buf, int64_t cap) {
     std::string src;
     std::vector<double> iv;
     int64_t we = 0;
-    int rc = fbn::GenerateJTKernel(p->host, src, &we, iv);
+    int rc = fbn::GenerateJTKernel(p->host, src, &we, iv, nullptr, JtFast(p));
     if (rc) return rc;
     snprintf(buf, (size_t)cap, "%s", fbn::JitCachePath(src).c_str());
     return FBN_OK;
@@ -816,7 +823,7 @@ int fbn_jt_kernel_build(const fbn_jt_plan *p) {
     std::string src;
     std::vector<double> iv;
     int64_t we = 0;
-    int rc = fbn::GenerateJTKernel(p->host, src, &we, iv);
+    int rc = fbn::GenerateJTKernel(p->host, src, &we, iv, nullptr, JtFast(p));
     if (rc) return rc;
     std::vector<char> code;
     return fbn::JitCodeObject(src, code);

@@ -137,8 +137,10 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget);
 // plan-specialized kernel source (jt_codegen.cpp): eligibility and generation.  The generated
 // kernel's per-wave workspace holds wave_entries rows of 64 fp64 lanes; initv is its constant input.
 bool JTCodegenEligible(const JTPlanHost &plan, int64_t *entry_ops);
+// fast: the fast arithmetic order (normalizations that cancel are left out; results within 1e-12 of
+// the exact order, which repeats the reference's every multiply + Normalize)
 int GenerateJTKernel(const JTPlanHost &plan, std::string &src, int64_t *wave_entries, std::vector<double> &initv,
-                     int64_t *lds_bytes = nullptr);
+                     int64_t *lds_bytes = nullptr, bool fast = false);
 
 }  // namespace fbn
 

@@ -67,12 +67,16 @@ namespace {
 
 class JTGen {
   public:
-    explicit JTGen(const JTPlanHost &p) : plan(p) {}
+    JTGen(const JTPlanHost &p, bool fast_order) : plan(p), fast(fast_order) {}
     int Run(std::string &src, int64_t *wave_entries, std::vector<double> &initv);
     int64_t lds_rows = 0;  // LDS rows (64 lanes x fp64) per wave
 
   private:
     const JTPlanHost &plan;
+    // fast arithmetic order: a clique's table is init * (product of its messages), never normalized
+    // in between (the reference's per-step normalizations cancel in every normalized result);
+    // messages are normalized once, marginals from a statically chosen clique
+    const bool fast;
     std::ostringstream o;
     std::vector<int> okw_word, okw_pos, out_off;
     std::vector<int64_t> sep_row, init_off;
@@ -134,7 +138,14 @@ class JTGen {
     // table has been normalized eagerly (Normalize) since its last update
     bool normed = false;
     std::string Val(const std::string &P, int c, int64_t e) const {
-        return normed ? N(P, c, e) : "dv(" + N(P, c, e) + ", den, y)";
+        return (normed || fast) ? N(P, c, e) : "dv(" + N(P, c, e) + ", den, y)";
+    }
+    // fast order: the clique total (den, y) the Distribute messages are scaled by
+    void Total(const std::string &P, int c) {
+        const Table &t = plan.cliques[c];
+        o << "        { double sm = 0.0;";
+        for (int64_t e = 0; e < t.size(); ++e) o << " sm += " << N(P, c, e) << ";";
+        o << " den = sm; y = 1.0 / den; bad |= den_bad(den); }\n" << B(6);
     }
     void Normalize(const std::string &P, int c) {
         const Table &t = plan.cliques[c];
@@ -156,7 +167,7 @@ void JTGen::Init(const std::string &P, int c) {
               << okw_pos[v] + d << ") & 1u;";
         o << "\n";
     }
-    o << "        double s_" << P << c << " = 0.0;\n";
+    if (!fast) o << "        double s_" << P << c << " = 0.0;\n";
     // software-pipelined in batches: the LDS reads of batch b+1 are issued before batch b computes
     const int64_t kB = 16, T = t.size();
     auto loads = [&](int64_t b0) {
@@ -178,11 +189,14 @@ void JTGen::Init(const std::string &P, int c) {
                 cond << (j ? " && " : "") << "k" << P << c << "_" << j << "_" << dgt;
             }
             o << "        " << (e < kRegEntries ? "double " : "") << N(P, c, e) << " = sel(" << cond.str() << ", w" << P
-              << c << "_" << e << "); s_" << P << c << " += " << N(P, c, e) << ";\n";
+              << c << "_" << e << ");";
+            if (!fast) o << " s_" << P << c << " += " << N(P, c, e) << ";";
+            o << "\n";
         }
         o << "        __builtin_amdgcn_sched_barrier(0);\n";
     }
-    o << "        den = s_" << P << c << "; y = 1.0 / den; bad |= den_bad(den);\n" << B(2);
+    if (!fast) o << "        den = s_" << P << c << "; y = 1.0 / den; bad |= den_bad(den);\n";
+    o << B(2);
     normed = false;
 }
 
@@ -196,9 +210,12 @@ void JTGen::Mul(const std::string &P, int c, int s, const std::string &M) {
         for (int64_t e : inv[j]) o << " " << N(P, c, e) << " = " << Val(P, c, e) << " * " << M << s << "_" << j << ";";
         o << "\n";
     }
-    o << "        { double sm = 0.0;";
-    for (int64_t e = 0; e < t.size(); ++e) o << " sm += " << N(P, c, e) << ";";
-    o << " den = sm; y = 1.0 / den; bad |= den_bad(den); }\n" << B(3);
+    if (!fast) {
+        o << "        { double sm = 0.0;";
+        for (int64_t e = 0; e < t.size(); ++e) o << " sm += " << N(P, c, e) << ";";
+        o << " den = sm; y = 1.0 / den; bad |= den_bad(den); }\n";
+    }
+    o << B(3);
     normed = false;
 }
 
@@ -206,6 +223,23 @@ void JTGen::Mul(const std::string &P, int c, int s, const std::string &M) {
 void JTGen::SepCol(const std::string &P, int c, int s, bool store) {
     const Table &t = plan.cliques[c];
     const int64_t Ts = plan.seps[s].size(), Q = t.size() / Ts;
+    if (fast) {  // message = bin sums / their total (= the normalized table's sums)
+        for (int64_t j = 0; j < Ts; ++j) {
+            o << "        const double mr" << s << "_" << j << " = " << N(P, c, j);
+            for (int64_t q = 1; q < Q; ++q) o << " + " << N(P, c, q * Ts + j);
+            o << ";\n";
+        }
+        o << "        double ys" << s << "; { double sm = mr" << s << "_0;";
+        for (int64_t j = 1; j < Ts; ++j) o << " sm += mr" << s << "_" << j << ";";
+        o << " ys" << s << " = 1.0 / sm; bad |= den_bad(sm); }\n";
+        for (int64_t j = 0; j < Ts; ++j) {
+            o << "        const double mc" << s << "_" << j << " = mr" << s << "_" << j << " * ys" << s << ";";
+            if (store) o << " W(" << sep_row[s] + j << "LL) = mc" << s << "_" << j << ";";
+            o << "\n";
+        }
+        o << B(4);
+        return;
+    }
     for (int64_t j = 0; j < Ts; ++j) {
         o << "        const double mc" << s << "_" << j << " = " << Val(P, c, j);
         for (int64_t q = 1; q < Q; ++q) o << " + " << Val(P, c, q * Ts + j);
@@ -226,9 +260,12 @@ void JTGen::DMul(const std::string &P, int c, int s, const std::string &M) {
             o << " " << N(P, c, e) << " = " << Val(P, c, e) << " * " << M << s << "_" << j << ";";
         o << "\n";
     }
-    o << "        { double sm = 0.0;";
-    for (int64_t e = 0; e < t.size(); ++e) o << " sm += " << N(P, c, e) << ";";
-    o << " den = sm; y = 1.0 / den; bad |= den_bad(den); }\n" << B(5);
+    if (!fast) {
+        o << "        { double sm = 0.0;";
+        for (int64_t e = 0; e < t.size(); ++e) o << " sm += " << N(P, c, e) << ";";
+        o << " den = sm; y = 1.0 / den; bad |= den_bad(den); }\n";
+    }
+    o << B(5);
     normed = false;
 }
 
@@ -241,6 +278,7 @@ void JTGen::SepDis(const std::string &P, int c, int s, const std::string &old, b
         o << "        double md" << s << "_" << j << ";";
         o << " { double a = " << Val(P, c, lists[j][0]) << ";";
         for (size_t q = 1; q < lists[j].size(); ++q) o << " a += " << Val(P, c, lists[j][q]) << ";";
+        if (fast) o << " a *= y;";  // the clique total (Total)
         o << " const double od = " << old << s << "_" << j << "; md" << s << "_" << j << " = (od == 0.0) ? 0.0 : a / od; }";
         if (store) o << " W(" << sep_row[s] + j << "LL) = md" << s << "_" << j << ";";
         o << "\n";
@@ -256,11 +294,19 @@ void JTGen::Marg(const std::string &P, int c) {
         const int v = t.vars[j];
         const int dim = plan.dom[v];
         const int64_t cum = t.cum[j], bw = dim * cum, nhi = t.size() / bw;
-        // selection: first candidate clique with the fewest reduced variables (recomputed here)
-        o << "        { int b = " << R(cand[v][0]) << ", sl = " << cand[v][0] << ";";
-        for (size_t k = 1; k < cand[v].size(); ++k)
-            o << " { const int r = " << R(cand[v][k]) << "; if (r < b) { b = r; sl = " << cand[v][k] << "; } }";
-        o << "\n        if (sl == " << c << " && !" << observed(v) << ") { // marginal of var " << v << "\n";
+        if (fast) {  // the smallest clique holding the variable (a calibrated tree: any gives the marginal)
+            int sel = cand[v][0];
+            for (int q : cand[v])
+                if (plan.cliques[q].size() < plan.cliques[sel].size()) sel = q;
+            if (sel != c) continue;
+            o << "        { const int b = 0;\n        if (!" << observed(v) << ") { // marginal of var " << v << "\n";
+        } else {
+            // selection: first candidate clique with the fewest reduced variables (recomputed here)
+            o << "        { int b = " << R(cand[v][0]) << ", sl = " << cand[v][0] << ";";
+            for (size_t k = 1; k < cand[v].size(); ++k)
+                o << " { const int r = " << R(cand[v][k]) << "; if (r < b) { b = r; sl = " << cand[v][k] << "; } }";
+            o << "\n        if (sl == " << c << " && !" << observed(v) << ") { // marginal of var " << v << "\n";
+        }
         o << "          double tot = 0.0;";
         for (int d = 0; d < dim; ++d) o << " double p" << d << ";";
         o << "\n";
@@ -334,7 +380,8 @@ int JTGen::Run(std::string &src, int64_t *wave_entries, std::vector<double> &ini
     }
     if ((int)post.size() != nc) return SetError(FBN_ERR_LIMIT, "codegen: tree traversal covers %zu of %d cliques", post.size(), nc);
 
-    o << "// generated by libfastbn (jt_codegen.cpp): " << nc << " cliques, " << ns << " separators\n";
+    o << "// generated by libfastbn (jt_codegen.cpp): " << nc << " cliques, " << ns << " separators, "
+      << (fast ? "fast" : "exact") << " arithmetic order\n";
     o << "#define FBN_V " << V << "\n#define FBN_SD " << SD << "\n#define FBN_WE " << *wave_entries << "LL\n";
     o << "#define FBN_IV_BASE " << lds_rows * 64 << "\n#define FBN_NIV " << initv.size() << "\n";
     o << "#define FBN_IV_LDS " << (iv_lds ? 1 : 0) << "\n#define FBN_MIN_WAVES " << min_waves << "\n";
@@ -541,7 +588,9 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
         }
         const auto &down = plan.clique_down[c];
         // consumers of the normalized table: one SepDis per child, one marginal per variable
-        if (down.size() + plan.cliques[c].vars.size() >= 2) Normalize(P, c);
+        if (fast) {
+            if (!down.empty()) Total(P, c);
+        } else if (down.size() + plan.cliques[c].vars.size() >= 2) Normalize(P, c);
         for (size_t i = 0; i < down.size(); ++i) {
             if (!early) Load("lc", down[i]), o << B(1);
             SepDis(P, c, down[i], early ? "lb" : "lc", !md_reg[down[i]]);
@@ -567,8 +616,8 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
 }  // namespace
 
 int GenerateJTKernel(const JTPlanHost &plan, std::string &src, int64_t *wave_entries, std::vector<double> &initv,
-                     int64_t *lds_bytes) {
-    JTGen g(plan);
+                     int64_t *lds_bytes, bool fast) {
+    JTGen g(plan, fast);
     int rc = g.Run(src, wave_entries, initv);
     const bool iv_lds = !getenv("FBN_JT_IV_LDS") || atoi(getenv("FBN_JT_IV_LDS")) != 0;
     if (lds_bytes) *lds_bytes = (g.lds_rows * 64 + (iv_lds ? (int64_t)initv.size() : 0)) * 8;

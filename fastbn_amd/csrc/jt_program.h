@@ -109,8 +109,8 @@ struct JtVClique {
 #define JT_T_LDS_BIN_ROWS 16  // a pass's partial bins live in LDS when they are at most this many rows
 enum JtTKind : int32_t { JT_T_COL = 0, JT_T_DIS = 1, JT_T_MARG = 2 };
 struct JtTPass {
-    int32_t kind, clique, nf, mode;  // mode: 0 every factor in LDS, 1 every factor global, 2 all but the
-                                     // last (the parent message) in LDS
+    int32_t kind, clique, nf, nl;    // factors; factors 0 .. nl-1 are staged in LDS, the rest are read
+                                     // from the wave store
     int32_t nG, rounds, nRo, nRi;    // G-configurations, rounds of JT_T_L, outer / inner R stream
     int32_t g_off, o_off, i_off;     // tab: G records and outer R records (4 + nf ints each: entry, digit
                                      // word, bin, pad, factor byte offsets), inner R records (2 + nf
@@ -125,8 +125,9 @@ struct JtTPass {
     int32_t first;                   // first pass of a clique phase: the lanes' evidence words, then the
     int32_t nstage, stage_off;       // factors staged into LDS ({src row, rows, lds byte offset} records)
     int32_t et_off;                  // tab: the R part of the entry (bytes) of every flattened R step
-    int32_t st_off;                  // tab: step records {factor soffsets [nf], digit word, bin offset of
-                                     //      the inner run ending at the step or -1}
+    int32_t st_off;                  // tab: step records {factor soffsets [nf] (bit 0: the same row as the
+                                     //      step before), digit word, bin offset of the inner run ending
+                                     //      at the step or -1}
 };
 
 #endif

@@ -91,9 +91,10 @@ __device__ __forceinline__ double row_bcast_n(double x, int n) {
 // step k0 + u takes it from lane u of the slot's DPP row.  Per step: a scalar step record (factor
 // soffsets, digit word, the bin of the inner run ending there), one digit test and NF factor loads
 // (LDS: one address add; wave store: voffset + soffset).  The sum of an inner run goes to its bin
-// (LDS rows for small bin sets, else the wave store).  MODE 0: every factor in LDS, 1: every factor
-// in the wave store, 2: all but the last (the parent message) in LDS
-template <int NF, int MODE>
+// (LDS rows for small bin sets, else the wave store).  Factors 0 .. NL-1 are in LDS, the rest in the
+// wave store.  A factor whose row is the one of the step before (bit 0 of its soffset, set by the
+// plan, which orders the R stream to make that common) is not loaded again: the lane keeps the value
+template <int NF, int NL>
 __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *__restrict__ tab,
                                                __amdgpu_buffer_rsrc_t ivrs, __amdgpu_buffer_rsrc_t st,
                                                char *__restrict__ ldsb, int s, int g, uint32_t M, uint32_t W,
@@ -120,6 +121,9 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
         for (int j = 0; j < NF; ++j) fG[j] = gr[4 + j] + g8;
         const bool okG = la && (((dwG ^ W) & M & gf) == 0u);
         double acc = 0.0;
+        double fe[NFA];  // the factor values of the step before
+#pragma unroll
+        for (int j = 0; j < NFA; ++j) fe[j] = 0.0;
         // slot s's entry at step k0 + g, one chunk ahead (the tables are padded by one chunk)
         double wn = bld(ivrs, ivb + et[g], 0);
         for (int k0 = 0; k0 < nR; k0 += C) {
@@ -136,8 +140,8 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
                     ok[u] = (((uint32_t)q[NF]) & MR) == WR;
 #pragma unroll
                     for (int j = 0; j < NF; ++j) {
-                        if (MODE == 0 || (MODE == 2 && j < NF - 1))
-                            f[u][j] = *reinterpret_cast<const double *>(ldsb + (fG[j] + q[j]));  // byte offsets
+                        if (q[j] & 1) continue;  // (uniform) the row of the step before
+                        if (j < NL) f[u][j] = *reinterpret_cast<const double *>(ldsb + (fG[j] + q[j]));  // bytes
                         else f[u][j] = bld(st, fG[j], q[j]);
                     }
                 }
@@ -148,10 +152,14 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
                     const int k = k0 + u0 + u;
                     if (k >= nR) break;
                     double x = w[u];
+                    const int32_t *__restrict__ q = sr + (size_t)k * RS;
 #pragma unroll
-                    for (int j = 0; j < NF; ++j) x *= f[u][j];
+                    for (int j = 0; j < NF; ++j) {
+                        if (!(q[j] & 1)) fe[j] = f[u][j];
+                        x *= fe[j];
+                    }
                     acc += ok[u] ? x : 0.0;
-                    const int xo = sr[(size_t)k * RS + NF + 1];
+                    const int xo = q[NF + 1];
                     if (xo >= 0) {  // end of an inner run: its bin
                         const double a = okG ? acc : 0.0;
                         if (la) {
@@ -235,12 +243,21 @@ __device__ __forceinline__ double post_sweep(const JtTPass &P, __amdgpu_buffer_r
     return S;
 }
 
-#define FBN_TCASE(NFv)                                                                                    \
-    case NFv:                                                                                             \
-        if (P.mode == 0) tot = pass_entries<NFv, 0>(P, tab, ivrs, st, ldsb, s, g, M, W, scr_b, binb, bins_lds);             \
-        else if (P.mode == 1) tot = pass_entries<NFv, 1>(P, tab, ivrs, st, ldsb, s, g, M, W, scr_b, binb, bins_lds);        \
-        else tot = pass_entries<NFv, 2>(P, tab, ivrs, st, ldsb, s, g, M, W, scr_b, binb, bins_lds);                         \
-        break;
+template <int NF>
+__device__ __forceinline__ double pass_entries_nl(const JtTPass &P, const int32_t *__restrict__ tab,
+                                                  __amdgpu_buffer_rsrc_t ivrs, __amdgpu_buffer_rsrc_t st,
+                                                  char *__restrict__ ldsb, int s, int g, uint32_t M, uint32_t W,
+                                                  int scr_b, int binb, bool bins_lds) {
+#define FBN_TNL(n)                                                                                        \
+    case n:                                                                                               \
+        if constexpr (n <= NF) return pass_entries<NF, n>(P, tab, ivrs, st, ldsb, s, g, M, W, scr_b, binb, bins_lds); \
+        else return 0.0;
+    switch (P.nl) {
+        FBN_TNL(1) FBN_TNL(2) FBN_TNL(3) FBN_TNL(4) FBN_TNL(5) FBN_TNL(6) FBN_TNL(7)
+    default: return pass_entries<NF, 0>(P, tab, ivrs, st, ldsb, s, g, M, W, scr_b, binb, bins_lds);
+    }
+#undef FBN_TNL
+}
 
 __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__ passes, int npass,
                                                      const int32_t *__restrict__ tab, const double *__restrict__ iv,
@@ -262,7 +279,8 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
     // record's part (soffset, scalar) -- no per-step address arithmetic
     const __amdgpu_buffer_rsrc_t ivrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(iv), 0, 0x7FFFFFF8, 0x00020000);
     // diagnostic (prof != nullptr): s_memtime cycles per phase, summed over the waves -- [0] staging,
-    // [1..3] entry work in factor mode 0 / 1 / 2, [4] post sweep, [5] marginal sweeps, [6] all
+    // [1..3] entry work with every factor in LDS / in the wave store / mixed, [4] post sweep,
+    // [5] marginal sweeps, [6] all, [7] pass totals
     unsigned long long pc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long t_all = prof ? clock64() : 0ull;
     for (long long cg = blockIdx.x; cg * C < ncases; cg += gridDim.x) {
@@ -321,17 +339,16 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
             const bool bins_lds = P.nbins * P.nE <= kBinRows;
             if (need_entries) {
                 double tot = 0.0;
+#define FBN_TNF(n) \
+    case n: tot = pass_entries_nl<n>(P, tab, ivrs, st, ldsb, s, g, M, W, scr_b, binb, bins_lds); break;
                 switch (P.nf) {
-                    FBN_TCASE(0) FBN_TCASE(1) FBN_TCASE(2) FBN_TCASE(3) FBN_TCASE(4) FBN_TCASE(5) FBN_TCASE(6)
-                    default: {
-                        if (P.mode == 0) tot = pass_entries<7, 0>(P, tab, ivrs, st, ldsb, s, g, M, W, scr_b, binb, bins_lds);
-                        else if (P.mode == 1) tot = pass_entries<7, 1>(P, tab, ivrs, st, ldsb, s, g, M, W, scr_b, binb, bins_lds);
-                        else tot = pass_entries<7, 2>(P, tab, ivrs, st, ldsb, s, g, M, W, scr_b, binb, bins_lds);
-                    }
+                    FBN_TNF(0) FBN_TNF(1) FBN_TNF(2) FBN_TNF(3) FBN_TNF(4) FBN_TNF(5) FBN_TNF(6)
+                    default: tot = pass_entries_nl<7>(P, tab, ivrs, st, ldsb, s, g, M, W, scr_b, binb, bins_lds);
                 }
+#undef FBN_TNF
                 if (prof) {
                     const unsigned long long t1 = dclock();
-                    pc[1 + P.mode] += t1 - t0;
+                    pc[P.nl == P.nf ? 1 : P.nl == 0 ? 2 : 3] += t1 - t0;
                     t0 = t1;
                 }
                 S = slot_sum(tot);

@@ -179,24 +179,19 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
     // one pass: clique c, output variables `opos` (positions) laid out by `ocum` (stride of each
     // output variable in the output's bin index), factors, destination
     auto build_pass = [&](int c, int kind, const std::vector<int> &opos, const std::vector<int64_t> &ocum,
-                          int64_t nbins, const std::vector<Factor> &fac, int64_t dest_row, int64_t col_row,
+                          int64_t nbins, const std::vector<Factor> &fac_in, int64_t dest_row, int64_t col_row,
                           const std::vector<int> &mvars, bool first, int nstage, int32_t stage_off) -> int {
         const Table &t = plan.cliques[c];
-        const int nv = (int)t.vars.size(), nf = (int)fac.size();
+        const int nv = (int)t.vars.size(), nf = (int)fac_in.size();
         JtTPass P{};
         P.kind = kind;
         P.clique = c;
         P.nf = nf;
-        bool all_lds = true, all_glb = true, last_glb_only = nf > 0;
-        for (int j = 0; j < nf; ++j) {
-            all_lds = all_lds && fac[j].lds_off >= 0;
-            all_glb = all_glb && fac[j].lds_off < 0;
-            if (j < nf - 1) last_glb_only = last_glb_only && fac[j].lds_off >= 0;
-            else last_glb_only = last_glb_only && fac[j].lds_off < 0;
-        }
-        P.mode = (nf == 0 || all_lds) ? 0 : all_glb ? 1 : 2;
-        if (nf > 0 && !all_lds && !all_glb && !last_glb_only)
-            return SetError(FBN_ERR_ARG, "internal: factor placement of clique %d", c);
+        // the LDS-resident factors first (the kernel reads factors 0 .. nl-1 from LDS)
+        std::vector<Factor> fac(fac_in);
+        std::stable_partition(fac.begin(), fac.end(), [](const Factor &f) { return f.lds_off >= 0; });
+        P.nl = 0;
+        for (const Factor &f : fac) P.nl += f.lds_off >= 0 ? 1 : 0;
         // G: output variables first (no partial bins), extra variables when the output is small
         std::vector<int> G;
         std::vector<int> others;
@@ -229,6 +224,51 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
                 const int l = PosIn(fac[j].sep->vars, t.vars[i]);
                 fs[j][i] = l >= 0 ? fac[j].sep->cum[l] : 0;
             }
+        // R order (outer, then inner; slowest first): a factor's row changes only when one of its
+        // variables does, and the kernel reuses the row it loaded at the previous step, so the order
+        // that minimizes the row changes of the wave-store factors (weight 1; LDS ones 1/8) is taken
+        // -- exhaustively for small R, else by sorting (variables of many/large factors slowest)
+        {
+            auto changes = [&](const std::vector<int> &ord) {
+                double cst = 0.0;
+                for (int j = 0; j < nf; ++j) {
+                    int64_t n = 1, seg = 1;
+                    for (int i : ord) {
+                        n *= t.dims[i];
+                        if (fs[j][i] != 0) seg = n;
+                    }
+                    cst += (j < P.nl ? 0.125 : 1.0) * (double)seg;
+                }
+                return cst;
+            };
+            auto fact = [](size_t n) { size_t f = 1; for (size_t i = 2; i <= n; ++i) f *= i; return f; };
+            if (nf > 0 && fact(RO.size()) * fact(RI.size()) <= 20000) {
+                std::vector<int> ro = RO, ri = RI, best;
+                std::sort(ro.begin(), ro.end());
+                double bc = 1e300;
+                do {
+                    std::sort(ri.begin(), ri.end());
+                    do {
+                        std::vector<int> ord = ro;
+                        ord.insert(ord.end(), ri.begin(), ri.end());
+                        const double cst = changes(ord);
+                        if (cst < bc - 1e-9) bc = cst, best = ord;
+                    } while (std::next_permutation(ri.begin(), ri.end()));
+                } while (std::next_permutation(ro.begin(), ro.end()));
+                std::copy(best.begin(), best.begin() + RO.size(), RO.begin());
+                std::copy(best.begin() + RO.size(), best.end(), RI.begin());
+            } else if (nf > 0) {
+                auto key = [&](int i) {
+                    double k = 0.0;
+                    for (int j = 0; j < nf; ++j)
+                        if (fs[j][i] != 0) k += j < P.nl ? 0.125 : 1.0;
+                    return k;
+                };
+                auto by = [&](int a, int b) { return key(a) > key(b); };
+                std::stable_sort(RO.begin(), RO.end(), by);
+                std::stable_sort(RI.begin(), RI.end(), by);
+            }
+        }
         std::vector<int64_t> ecum(nv, 0), ocum_p(nv, 0);
         {
             int64_t m = 1;
@@ -311,7 +351,12 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
                     const int32_t *oq = ro + o * (4 + nf), *iq = ri + i * (2 + nf);
                     et[k] = oq[0] * 8 + iq[0];
                     int32_t *q = &sr[k * (nf + 2)];
-                    for (int f = 0; f < nf; ++f) q[f] = oq[4 + f] + iq[2 + f];
+                    for (int f = 0; f < nf; ++f) {
+                        q[f] = oq[4 + f] + iq[2 + f];
+                        // bit 0 (offsets are multiples of a 128-byte row): the same row as the step
+                        // before -- the kernel keeps the value it loaded then
+                        if (k > 0 && q[f] == (sr[(k - 1) * (nf + 2) + f] & ~1)) q[f] |= 1;
+                    }
                     q[nf] = (int32_t)((uint32_t)oq[1] | (uint32_t)iq[1]);
                     q[nf + 1] = i == nRi_ - 1 ? oq[2] : -1;
                 }
@@ -376,22 +421,17 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
         return FBN_OK;
     };
 
-    // factor placement of one clique phase: every factor in LDS if they fit, else all but the last
-    // (the parent message, Distribute) if those fit, else none; staging records for the LDS ones
-    auto place = [&](std::vector<Factor> &fac, bool parent_last, int *nstage, int32_t *stage_off) {
-        int64_t tot = 0, head = 0;
-        for (size_t j = 0; j < fac.size(); ++j) {
-            tot += fac[j].sep->size();
-            if (j + 1 < fac.size() || !parent_last) head += fac[j].sep->size();
-        }
-        size_t n_lds = 0;
-        if (tot <= budget_rows) n_lds = fac.size();
-        else if (parent_last && head <= budget_rows) n_lds = fac.size() - 1;
+    // factor placement of one clique phase: the smallest factors in LDS while they fit the per-wave
+    // budget, the rest read from the wave store; staging records for the LDS ones
+    auto place = [&](std::vector<Factor> &fac, int *nstage, int32_t *stage_off) {
+        std::vector<size_t> idx(fac.size());
+        for (size_t j = 0; j < fac.size(); ++j) idx[j] = j;
+        std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return fac[a].sep->size() < fac[b].sep->size(); });
         *stage_off = (int32_t)prog.tab.size();
         *nstage = 0;
         int64_t off = 0;
-        for (size_t j = 0; j < fac.size(); ++j) {
-            if (j < n_lds) {
+        for (size_t j : idx) {
+            if (off + fac[j].sep->size() <= budget_rows) {
                 fac[j].lds_off = (int)(off * JT_T_C * 8);
                 prog.tab.push_back((int32_t)fac[j].row);
                 prog.tab.push_back((int32_t)fac[j].sep->size());
@@ -413,7 +453,7 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
         for (int s : plan.clique_down[c]) fac.push_back({&plan.seps[s], col[s], -1});
         int nst;
         int32_t so;
-        place(fac, false, &nst, &so);
+        place(fac, &nst, &so);
         const int s = plan.clique_up[c];
         const Table &sp = plan.seps[s];
         std::vector<int> opos;
@@ -431,7 +471,7 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
         if (has_parent) fac.push_back({&plan.seps[plan.clique_up[c]], dis[plan.clique_up[c]], -1});
         int nst;
         int32_t so;
-        place(fac, has_parent, &nst, &so);
+        place(fac, &nst, &so);
         bool first = true;
         for (size_t ci = 0; ci < plan.clique_down[c].size(); ++ci) {
             const int s = plan.clique_down[c][ci];

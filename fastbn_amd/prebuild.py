@@ -26,7 +26,9 @@ def prebuild(xml_paths):
     for xml in xml_paths:
         jt = api.JunctionTree(api.Network(xml), device=-1)
         if jt.info["specialized_eligible"]:
-            out.append(jt.build_kernel())
+            for exact in (None, True):  # both arithmetic orders (default fast, exact on request)
+                jt.set_exact(exact)
+                out.append(jt.build_kernel())
     return out
 
 

@@ -143,26 +143,26 @@ int fbn_jt_score(const fbn_jt_plan *p, const double *marginals, const double *go
 int fbn_jt_last_kernel_ms(const fbn_jt_plan *p, float *ms);
 /* Tuning: persistent waves per CU (0 = default: as many as keep the largest clique in LDS). */
 int fbn_jt_set_waves_per_cu(fbn_jt_plan *p, int waves);
-/* Kernel variant: -1 = auto (default: 3 when eligible and its code object loads, else 4, else 0/1),
- * 0 = clique-in-LDS interpreter, 1 = whole case state in a global workspace interpreter,
- * 2 = variant 0 with the IEEE division sequence forced (ablation / testing),
+/* Kernel variant: -1 = auto (default: 3 when eligible and its code object loads, else 5 in the fast
+ * order, else 4, else 0/1), 0 = clique-in-LDS interpreter, 1 = whole case state in a global
+ * workspace interpreter, 2 = variant 0 with the IEEE division sequence forced (ablation / testing),
  * 3 = plan-specialized kernel (jt_codegen.cpp; hiprtc or the on-disk code-object cache) followed
  *     by an exact-path fixup of the blocks it flags.  Selecting 3 fails if the plan is not eligible.
  * 4 = streamed ("virtual table") kernel for large trees (jt_virt.hip): tables recomputed per pass
  *     from initial potentials + received messages, only messages stored; exact-path fixup as 3.
  *     Selecting 4 fails for plans it cannot take (a clique with more than 6 children, ...).
- * 5 = per-case kernel (jt_case.hip, opt-in): one wave per evidence case over its evidence-reduced
- *     clique entries, one pass per clique and direction, fast arithmetic order only (the exact
- *     setting does not apply); exact-path fixup as 3.  Fails for plans with > 6 children per clique,
- *     > 64 variables per clique or a domain > 64 states. */
+ * 5 = tiled kernel (jt_tile.hip, the Munin-class default): 16 evidence cases x 4 entry slots per
+ *     wave, every clique entry recomputed per pass from its initial potential and the messages,
+ *     fast arithmetic order only (the exact setting does not apply); exact-path fixup as 3.  Fails
+ *     for plans with > 6 children per clique, > 32 digit bits per clique or a domain > 8 states. */
 int fbn_jt_set_variant(fbn_jt_plan *p, int variant);
-/* Arithmetic order of the streamed kernel (variant 4): 1 = exact (the reference's sequential
- * Normalize after every multiply: bit-identical marginals), 0 = fast (all Collect normalization sums
- * of a clique in one pass from prefix products, D_L = P_L / (D_0 ... D_{L-1}): the same values up to a
- * few ulp per operation, inside north_star's 1e-6 relative on potentials), -1 = auto (default:
- * exact for plans the specialized kernel takes -- ALARM class --, fast for the others -- the
- * Munin class, where the bit-exact order costs most of the achievable rate).  Replaces no
- * reference interface (the reference has one arithmetic order, src/JunctionTree.cpp:829-941). */
+/* Arithmetic order of the specialized (3) and streamed (4) kernels: 1 = exact (the reference's
+ * sequential Normalize after every multiply: bit-identical marginals), 0 = fast (a clique's table is
+ * its initial potential times its messages, normalized once where a result is formed -- the
+ * reference's intermediate normalizations cancel: labels equal, marginals within 1e-12 relative,
+ * inside north_star's 1e-6), -1 = auto (default: fast).  This is a parity-relevant default: a
+ * caller that needs the reference's bits selects 1.  Replaces no reference interface (the reference
+ * has one arithmetic order, src/JunctionTree.cpp:829-941). */
 int fbn_jt_set_exact(fbn_jt_plan *p, int exact);
 /* Diagnostics (LDS variant): enable per-op-type s_memtime accounting for subsequent runs and/or
  * read the totals of the last run (cycles[10], op types JT_L_INIT..JT_L_EVZERO, summed over waves). */

@@ -1,4 +1,5 @@
-"""Junction-tree HIP path vs the oracle and the reference's own outputs (bit-exact fp64)."""
+"""Junction-tree HIP path vs the oracle and the reference's own outputs (bit-exact fp64): the exact
+arithmetic order (set_exact(True)); the default fast order is tests/test_gpu_jt_fast.py."""
 import os
 
 import numpy as np
@@ -13,7 +14,9 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def jt(alarm_paths):
-    return F.JunctionTree(F.Network(alarm_paths["xml"]), device=0)
+    j = F.JunctionTree(F.Network(alarm_paths["xml"]), device=0)
+    j.set_exact(True)  # the reference's arithmetic order: bit-identical
+    return j
 
 
 @pytest.fixture(scope="module")
@@ -112,6 +115,7 @@ def test_specialized_synthetic(tmp_path):
     net = synth.read_xmlbif(p)
     ev = synth.evidence_cases(net, 777, 15, seed=8)
     jt = F.JunctionTree(F.Network(p), device=0)
+    jt.set_exact(True)
     assert jt.info["specialized_eligible"] == 1
     olab, omarg = O.OracleJT(p).infer(ev)
     for variant in (3, 0):

@@ -1,0 +1,103 @@
+"""The default (fast) arithmetic order of the plan-specialized ALARM-class kernel (variant 3,
+jt_codegen.cpp): a clique's table is its initial potential times its messages, normalized once
+where a message or marginal is formed -- the reference's intermediate normalizations
+(src/JunctionTree.cpp:829-941, 1150-1238) cancel.  Labels equal the reference's own dumps and the
+oracle; marginals within 1e-12 relative (north_star allows 1e-6)."""
+import os
+
+import numpy as np
+import pytest
+from conftest import GOLD, read_ref_marg
+
+import fastbn_amd as F
+import oracle as O
+from fastbn_amd import synth
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-12
+
+
+def _close(marg, ref):
+    np.testing.assert_allclose(marg, ref, rtol=TOL, atol=1e-300)
+
+
+@pytest.fixture(scope="module")
+def jt(alarm_paths):
+    j = F.JunctionTree(F.Network(alarm_paths["xml"]), device=0)
+    j.set_exact(None)  # auto = fast
+    return j
+
+
+@pytest.mark.parametrize("which", ["alarm_1k", "alarm_rand"])
+def test_fast_vs_reference_fixture(jt, alarm_paths, which):
+    path = alarm_paths["test"] if which == "alarm_1k" else alarm_paths["rand"]
+    ev, _ = F.load_libsvm(path, 37)
+    lab, marg = jt.infer(ev)
+    assert jt.refresh_info()["variant"] == 3
+    rlab, rmarg, _, _ = read_ref_marg(os.path.join(GOLD, which + ".marg.gz"), jt.network.dims)
+    np.testing.assert_array_equal(lab, rlab)
+    _close(marg, rmarg)
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 20000])
+def test_fast_ragged_vs_oracle(jt, n):
+    net = synth.read_xmlbif(os.path.join(GOLD, "alarm", "alarm.xml"))
+    ev = synth.evidence_cases(net, n, 7, seed=n)
+    lab, marg = jt.infer(ev)
+    olab, omarg = O.OracleJT(os.path.join(GOLD, "alarm", "alarm.xml")).infer(ev)
+    np.testing.assert_array_equal(lab, olab)
+    _close(marg, omarg)
+
+
+def test_fast_evidence_extremes_and_fixup(jt):
+    rng = np.random.default_rng(3)
+    dims = jt.network.dims
+    ev = np.full((130, 37), -1, np.int8)
+    ev[1, 1:] = [rng.integers(0, d) for d in dims[1:]]  # everything but the query observed
+    ev[2, 1::2] = [rng.integers(0, d) for d in dims[1::2]]
+    ev[3, 36] = 0
+    ev[4:] = synth.evidence_cases(synth.read_xmlbif(os.path.join(GOLD, "alarm", "alarm.xml")), 126, 20, seed=9)
+    olab, omarg = O.OracleJT(os.path.join(GOLD, "alarm", "alarm.xml")).infer(ev)
+    for force in (False, True):  # True: every block recomputed by the exact interpreter pass
+        jt.debug_force_fixup(force)
+        lab, marg = jt.infer(ev)
+        np.testing.assert_array_equal(lab, olab)
+        _close(marg, omarg)
+    jt.debug_force_fixup(False)
+    off = np.concatenate([[0], np.cumsum(dims)])
+    for v in range(37):  # evidence nodes -> zeros; others -> a distribution
+        s = marg[:, off[v]:off[v + 1]].sum(1)
+        obs = ev[:, v] >= 0
+        assert np.all(s[obs] == 0) and np.allclose(s[~obs], 1.0, atol=1e-12)
+
+
+def test_fast_and_exact_kernels_switch(jt):
+    """Toggling the order reloads the matching code object; exact stays bit-identical."""
+    net = synth.read_xmlbif(os.path.join(GOLD, "alarm", "alarm.xml"))
+    ev = synth.evidence_cases(net, 500, 7, seed=4)
+    olab, omarg = O.OracleJT(os.path.join(GOLD, "alarm", "alarm.xml")).infer(ev)
+    try:
+        for exact in (True, False, True):
+            jt.set_exact(exact)
+            lab, marg = jt.infer(ev)
+            assert jt.refresh_info()["variant"] == 3
+            np.testing.assert_array_equal(lab, olab)
+            if exact:
+                np.testing.assert_array_equal(marg, omarg)
+            else:
+                _close(marg, omarg)
+    finally:
+        jt.set_exact(None)
+
+
+def test_fast_specialized_synthetic(tmp_path):
+    from fastbn_amd import prebuild
+    p = prebuild.synth_small_xml(str(tmp_path))
+    ev = synth.evidence_cases(synth.read_xmlbif(p), 777, 15, seed=8)
+    jt = F.JunctionTree(F.Network(p), device=0)
+    assert jt.info["specialized_eligible"] == 1
+    jt.set_variant(3)
+    lab, marg = jt.infer(ev)
+    olab, omarg = O.OracleJT(p).infer(ev)
+    np.testing.assert_array_equal(lab, olab)
+    _close(marg, omarg)

@@ -61,3 +61,41 @@ def test_munin_like_fixture_vs_reference(munin_fixture):
     lab, marg = TE.run(prog, ev[:n], jt.info["sum_dom"])
     np.testing.assert_array_equal(lab, rlab[:n])
     np.testing.assert_allclose(marg, rmarg[:n], rtol=1e-9, atol=1e-300)
+
+
+def _check_steps(passes, tab, geo):
+    """The flattened step records the kernel reads equal the outer x inner composition, with bit 0 of a
+    factor soffset set exactly where the row equals the step before's; chunk padding present."""
+    C = geo["cases_per_wave"]
+    for prow in passes:
+        P = dict(zip(TE.F, (int(x) for x in prow)))
+        nf, nRo, nRi = P["nf"], P["nRo"], P["nRi"]
+        nR = nRo * nRi
+        assert 0 <= P["nl"] <= nf
+        ro = tab[P["o_off"]:P["o_off"] + nRo * (4 + nf)].reshape(nRo, 4 + nf).astype(np.int64)
+        ri = tab[P["i_off"]:P["i_off"] + nRi * (2 + nf)].reshape(nRi, 2 + nf).astype(np.int64)
+        et = tab[P["et_off"]:P["et_off"] + nR + C].astype(np.int64)
+        st = tab[P["st_off"]:P["st_off"] + (nR + C) * (nf + 2)].reshape(nR + C, nf + 2).astype(np.int64)
+        np.testing.assert_array_equal(et[:nR], (ro[:, 0:1] * 8 + ri[None, :, 0]).reshape(-1))
+        assert (et[nR:] == 0).all() and (st[nR:, nf + 1] == -1).all()
+        for j in range(nf):
+            off = (ro[:, 4 + j:5 + j] + ri[None, :, 2 + j]).reshape(-1)
+            assert (off % (C * 8) == 0).all()
+            np.testing.assert_array_equal(st[:nR, j] & ~1, off)
+            same = np.concatenate([[False], off[1:] == off[:-1]])
+            np.testing.assert_array_equal((st[:nR, j] & 1) == 1, same)
+        dw = ((ro[:, 1:2] & 0xFFFFFFFF) | (ri[None, :, 1] & 0xFFFFFFFF)).reshape(-1)
+        np.testing.assert_array_equal(st[:nR, nf] & 0xFFFFFFFF, dw)
+        last = np.full((nRo, nRi), -1, np.int64)
+        last[:, -1] = ro[:, 2]
+        np.testing.assert_array_equal(st[:nR, nf + 1], last.reshape(-1))
+
+
+def test_step_records_alarm():
+    _, (passes, tab, iv, geo) = _prog(ALARM)
+    _check_steps(passes, tab, geo)
+
+
+def test_step_records_munin_like(munin_fixture):
+    _, (passes, tab, iv, geo) = _prog(munin_fixture["xml"])
+    _check_steps(passes, tab, geo)

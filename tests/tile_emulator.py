@@ -8,7 +8,7 @@ with the oracle to ~1e-14, not bit for bit.  Never used by the product path."""
 import numpy as np
 
 # JtTPass field order (jt_program.h)
-F = ["kind", "clique", "nf", "mode", "nG", "rounds", "nRo", "nRi", "g_off", "o_off", "i_off", "nE", "nbins",
+F = ["kind", "clique", "nf", "nl", "nG", "rounds", "nRo", "nRi", "g_off", "o_off", "i_off", "nE", "nbins",
      "dest_row", "col_row", "bdig_off", "nmv", "mv_off", "iv_off", "nv", "vars_off", "gfields", "ofields", "first",
      "nstage", "stage_off", "et_off", "st_off"]
 COL, DIS, MARG = 0, 1, 2
@@ -62,7 +62,7 @@ def run_case(prog, ev_row, sum_dom, lds_bytes=1 << 20):
         x = iv[P["iv_off"] + e].copy()
         for j in range(nf):
             off = g[:, 4 + j:5 + j] + r[None, :, 2 + j]
-            in_lds = P["mode"] == 0 or (P["mode"] == 2 and j < nf - 1)
+            in_lds = j < P["nl"]
             x *= lds[off // 8] if in_lds else store[off // row_b]
         x[~ok] = 0.0
         acc = x.reshape(nG, nRo, nRi).sum(axis=2)
