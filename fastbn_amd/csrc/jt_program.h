@@ -128,6 +128,10 @@ struct JtTPass {
     int32_t st_off;                  // tab: step records {factor soffsets [nf] (bit 0: the same row as the
                                      //      step before), digit word, bin offset of the inner run ending
                                      //      at the step or -1}
+    // messages are stored un-normalized with a per-case scale row (normalized = values / scale):
+    int32_t fsc_off;                 // tab: the nf factors' scale rows
+    int32_t dest_sc, col_sc;         // scale rows of the output message and of the child's Collect message (DIS)
+    int32_t pad_;
 };
 
 #endif

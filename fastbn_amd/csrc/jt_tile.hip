@@ -7,17 +7,23 @@
 //     w(e) = init(e) * prod_j M_j(s_j(e))        (0 if e contradicts the lane's case's evidence)
 // -- the clique's table after all its child multiplications [and the parent's], up to the
 // normalizations, which cancel (fast order; the reference multiplies and normalizes step by step,
-// src/JunctionTree.cpp:829-941, 1150-1238).  The inner R stream sums into one register, stored once
-// per outer configuration into the pass's partial-bin rows; the post sweep adds the E partials of
-// every output bin in order, normalizes by the pass total S and writes
-//   Collect:     the upstream separator's message  tmp / S          (src/JunctionTree.cpp:1056-1148)
-//   Distribute:  a child separator's message  (tmp / S) / old, 0 where old == 0       (:700-816)
-// and the marginals whose source is this pass (GetProbabilitiesOneNode, :1392-1454; ArgMax,
-// src/Inference.cpp:92-102).  Every sum runs in a fixed order (per lane, then a butterfly over the
-// slots), so results are run-to-run identical.  Messages are rows [entry][JT_T_C cases] in
-// the wave's store; a clique's factors are staged into LDS when they fit the per-wave budget.
-// A case group whose pass totals leave [2^-900, 2^900] flags its 64-case block; the exact
-// interpreter recomputes flagged blocks.
+// src/JunctionTree.cpp:829-941, 1150-1238).  Messages are stored un-normalized, each with a per-case
+// scale row (normalized message = values / scale); a pass multiplies its lanes' sums by
+// sigma = 1 / (product of its factors' scales).  The inner R stream sums into one register, and at
+// the end of every inner run the sum (times sigma) is written straight to its output bin U(b):
+//   Collect:     the upstream separator's message U, scale S = sum_b U(b)  (src/JunctionTree.cpp:1056-1148)
+//   Distribute:  a child separator's message U, scale sum_b U(b)                       (:700-816)
+// The reference's Distribute message is (U / S') / old, 0 where old == 0, S' = sum_b old U: the
+// child's own Collect message `old` cancels in it (it is left out of the pass's factors), S' is a
+// per-case constant that cancels in every normalized result, and where old(b) == 0 every entry of
+// the child that b reaches is 0 already -- so U / sum U serves.  Marginals whose source is this pass
+// (GetProbabilitiesOneNode, :1392-1454; ArgMax, src/Inference.cpp:92-102) sum old(b) U(b) by value.
+// Outputs with fewer than JT_T_L bins take extra lane variables: their partial bins are added by a
+// post sweep first.  Every sum runs in a fixed order (per lane, then a butterfly over the slots), so
+// results are run-to-run identical.  Messages are rows [entry][JT_T_C cases] in the wave's store; a
+// clique's factors are staged into LDS when they fit the per-wave budget.  A case group whose pass
+// totals or factor scales leave [2^-900, 2^900] flags its 64-case block; the exact interpreter
+// recomputes flagged blocks.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -84,6 +90,15 @@ __device__ __forceinline__ double row_bcast_n(double x, int n) {
     }
 }
 
+// where a pass's inner-run sums go: straight to the output bins (direct: one bin per run, times
+// sigma; LDS for a small private-variable output) or to the partial bins of the post sweep
+struct PassOut {
+    bool direct, out_lds, bins_lds;
+    int out_b;   // output rows (bytes: wave store, or LDS for out_lds)
+    int part_b;  // partial bins (bytes: LDS for bins_lds, else the wave store)
+    double sig;
+};
+
 // the entry work of one pass: rounds of G-configurations x the flattened R stream (outer x inner
 // configurations) -> partial bins; returns the lane's share of the pass total.  The stream runs in
 // chunks of 16 steps = the 16 lanes (cases) of a slot: lane (s, g) loads the initial potential of
@@ -98,7 +113,7 @@ template <int NF, int NL>
 __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *__restrict__ tab,
                                                __amdgpu_buffer_rsrc_t ivrs, __amdgpu_buffer_rsrc_t st,
                                                char *__restrict__ ldsb, int s, int g, uint32_t M, uint32_t W,
-                                               int scr_b, int binb, bool bins_lds) {
+                                               const PassOut &O) {
     static_assert(C == 16, "a chunk = the 16 lanes of a DPP row");
     constexpr int RS = NF + 2, GS = 4 + NF, NFA = NF > 0 ? NF : 1;
     constexpr int U = NF <= 2 ? 8 : 4;  // steps with their loads in flight together (register budget)
@@ -164,10 +179,17 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
                         const double a = okG ? acc : 0.0;
                         if (la) {
                             const int x8 = (xG + xo) * (C * 8) + g8;
-                            if (bins_lds) *reinterpret_cast<double *>(ldsb + binb + x8) = a;
-                            else bst(st, scr_b + x8, a);
+                            if (O.direct) {
+                                const double v = a * O.sig;
+                                if (O.out_lds) *reinterpret_cast<double *>(ldsb + O.out_b + x8) = v;
+                                else bst(st, O.out_b + x8, v);
+                                tot += v;
+                            } else if (O.bins_lds) {
+                                *reinterpret_cast<double *>(ldsb + O.part_b + x8) = a;
+                            } else {
+                                bst(st, O.part_b + x8, a);
+                            }
                         }
-                        tot += a;
                         acc = 0.0;
                     }
                 }
@@ -177,84 +199,40 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
     return tot;
 }
 
-// the post sweep of a pass: output bin b = its nE partial bins added in order (U(b)), then
-//   Collect     the upstream separator's message  U / S, S = the pass total
-//   Distribute  a child separator's message  U / S, 0 where old == 0 (old = the child's Collect
-//               message, left out of the pass's factors: it cancels), S = sum_b old(b) U(b)
-// and the reduced bins for the marginal sweep (old * U for Distribute); LB: the partial / reduced
-// bins live in LDS.  Returns S.
-template <bool LB>
+// the post sweep of a pass whose output has fewer than JT_T_L bins (extra lane variables E):
+// output bin b = its nE partial bins added in order, times sigma, written like a direct pass's bin.
+// Returns the pass total S (lane partials in bin order, then the slot butterfly).
 __device__ __forceinline__ double post_sweep(const JtTPass &P, __amdgpu_buffer_rsrc_t st, char *__restrict__ ldsb,
-                                             int s, int g8, double S, int scr_b, int binb, int red_b, int redl) {
-    constexpr int T = 4;  // bins per lane in flight
+                                             int s, int g8, const PassOut &O) {
     const int nE = P.nE, nb = P.nbins;
-    const bool dis = P.kind == JT_T_DIS;
-    auto part = [&](int x) {
-        const int x8 = x * (C * 8) + g8;
-        return LB ? *reinterpret_cast<const double *>(ldsb + binb + x8) : bld(st, scr_b + x8, 0);
-    };
-    // T bins of this lane from b0: U and old
-    auto load = [&](int b0, double (&v)[T], double (&old)[T]) {
-#pragma unroll
-        for (int t = 0; t < T; ++t) {
-            const int b = b0 + t * L + s, bc = b < nb ? b : nb - 1;
-            v[t] = part(bc * nE);
-            old[t] = dis ? bld(st, (P.col_row + bc) * (C * 8) + g8, 0) : 1.0;
+    double tot = 0.0;
+    for (int b = s; b < nb; b += L) {
+        double v = 0.0;
+        for (int e = 0; e < nE; ++e) {
+            const int x8 = (b * nE + e) * (C * 8) + g8;
+            v += O.bins_lds ? *reinterpret_cast<const double *>(ldsb + O.part_b + x8) : bld(st, O.part_b + x8, 0);
         }
-        for (int e = 1; e < nE; ++e) {
-            double w[T];
-#pragma unroll
-            for (int t = 0; t < T; ++t) {
-                const int b = b0 + t * L + s, bc = b < nb ? b : nb - 1;
-                w[t] = part(bc * nE + e);
-            }
-#pragma unroll
-            for (int t = 0; t < T; ++t) v[t] += w[t];
-        }
-    };
-    if (dis) {  // S = sum_b old(b) U(b), lane partials in bin order, then the slot butterfly
-        double sp = 0.0;
-        for (int b0 = 0; b0 < nb; b0 += T * L) {
-            double v[T], old[T];
-            load(b0, v, old);
-#pragma unroll
-            for (int t = 0; t < T; ++t)
-                if (b0 + t * L + s < nb) sp += old[t] * v[t];
-        }
-        S = slot_sum(sp);
+        v *= O.sig;
+        const int o8 = b * (C * 8) + g8;
+        if (O.out_lds) *reinterpret_cast<double *>(ldsb + O.out_b + o8) = v;
+        else bst(st, O.out_b + o8, v);
+        tot += v;
     }
-    const double rS = 1.0 / S;
-    for (int b0 = 0; b0 < nb; b0 += T * L) {
-        double v[T], old[T];
-        load(b0, v, old);
-#pragma unroll
-        for (int t = 0; t < T; ++t) {
-            const int b = b0 + t * L + s;
-            if (b >= nb) continue;
-            if (P.kind == JT_T_COL) bst(st, (P.dest_row + b) * (C * 8) + g8, v[t] * rS);
-            else if (dis) bst(st, (P.dest_row + b) * (C * 8) + g8, old[t] == 0.0 ? 0.0 : v[t] * rS);
-            if (P.nmv > 0) {
-                const double red = dis ? old[t] * v[t] : v[t];
-                if (LB) *reinterpret_cast<double *>(ldsb + redl + b * (C * 8) + g8) = red;
-                else bst(st, red_b + b * (C * 8) + g8, red);
-            }
-        }
-    }
-    return S;
+    return slot_sum(tot);
 }
 
 template <int NF>
 __device__ __forceinline__ double pass_entries_nl(const JtTPass &P, const int32_t *__restrict__ tab,
                                                   __amdgpu_buffer_rsrc_t ivrs, __amdgpu_buffer_rsrc_t st,
                                                   char *__restrict__ ldsb, int s, int g, uint32_t M, uint32_t W,
-                                                  int scr_b, int binb, bool bins_lds) {
+                                                  const PassOut &O) {
 #define FBN_TNL(n)                                                                                        \
     case n:                                                                                               \
-        if constexpr (n <= NF) return pass_entries<NF, n>(P, tab, ivrs, st, ldsb, s, g, M, W, scr_b, binb, bins_lds); \
+        if constexpr (n <= NF) return pass_entries<NF, n>(P, tab, ivrs, st, ldsb, s, g, M, W, O);     \
         else return 0.0;
     switch (P.nl) {
         FBN_TNL(1) FBN_TNL(2) FBN_TNL(3) FBN_TNL(4) FBN_TNL(5) FBN_TNL(6) FBN_TNL(7)
-    default: return pass_entries<NF, 0>(P, tab, ivrs, st, ldsb, s, g, M, W, scr_b, binb, bins_lds);
+    default: return pass_entries<NF, 0>(P, tab, ivrs, st, ldsb, s, g, M, W, O);
     }
 #undef FBN_TNL
 }
@@ -279,8 +257,8 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
     // record's part (soffset, scalar) -- no per-step address arithmetic
     const __amdgpu_buffer_rsrc_t ivrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(iv), 0, 0x7FFFFFF8, 0x00020000);
     // diagnostic (prof != nullptr): s_memtime cycles per phase, summed over the waves -- [0] staging,
-    // [1..3] entry work with every factor in LDS / in the wave store / mixed, [4] post sweep,
-    // [5] marginal sweeps, [6] all, [7] pass totals
+    // [1..3] entry work with every factor in LDS / in the wave store / mixed, [4] pass totals, scales
+    // and the post sweep, [5] marginal sweeps, [6] all
     unsigned long long pc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long t_all = prof ? clock64() : 0ull;
     for (long long cg = blockIdx.x; cg * C < ncases; cg += gridDim.x) {
@@ -334,16 +312,28 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
                 for (int m = 0; m < P.nmv; ++m) any |= act && ev[tab[P.mv_off + 5 * m]] < 0;
                 need_entries = __ballot(any) != 0ull;
             }
-            double S = 1.0;
-            // partial bins (and the reduced bins of the marginal sweep) in LDS when they fit
-            const bool bins_lds = P.nbins * P.nE <= kBinRows;
+            // output: Collect / Distribute -> the message rows (wave store); private variables -> the
+            // reduced rows (LDS when they fit); partial bins (outputs with extra lane variables) in LDS
+            // when they fit
+            const bool marg_pass = P.kind == JT_T_MARG;
+            PassOut O;
+            O.direct = P.nE == 1;
+            O.bins_lds = P.nbins * P.nE <= kBinRows;
+            O.part_b = O.bins_lds ? binb : scr_b;
+            O.out_lds = marg_pass && P.nbins <= kBinRows;
+            O.out_b = marg_pass ? (O.out_lds ? redl : red_b) : P.dest_row * (C * 8);
             if (need_entries) {
+                // sigma = 1 / product of the factors' scales (this lane's case)
+                double prod = 1.0;
+                for (int j = 0; j < P.nf; ++j) prod *= bld(st, tab[P.fsc_off + j] * (C * 8) + g8, 0);
+                bad |= act && !(prod >= 0x1p-900 && prod <= 0x1p+900);
+                O.sig = 1.0 / prod;
                 double tot = 0.0;
 #define FBN_TNF(n) \
-    case n: tot = pass_entries_nl<n>(P, tab, ivrs, st, ldsb, s, g, M, W, scr_b, binb, bins_lds); break;
+    case n: tot = pass_entries_nl<n>(P, tab, ivrs, st, ldsb, s, g, M, W, O); break;
                 switch (P.nf) {
                     FBN_TNF(0) FBN_TNF(1) FBN_TNF(2) FBN_TNF(3) FBN_TNF(4) FBN_TNF(5) FBN_TNF(6)
-                    default: tot = pass_entries_nl<7>(P, tab, ivrs, st, ldsb, s, g, M, W, scr_b, binb, bins_lds);
+                    default: tot = pass_entries_nl<7>(P, tab, ivrs, st, ldsb, s, g, M, W, O);
                 }
 #undef FBN_TNF
                 if (prof) {
@@ -351,21 +341,18 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
                     pc[P.nl == P.nf ? 1 : P.nl == 0 ? 2 : 3] += t1 - t0;
                     t0 = t1;
                 }
-                S = slot_sum(tot);
-                if (bins_lds) __syncthreads();  // the partial bins, written by other lanes, become visible
-                else __threadfence_block();
-                if (prof) {
-                    const unsigned long long t1 = dclock();
-                    pc[7] += t1 - t0;  // pass total + the partial bins' visibility
-                    t0 = t1;
+                double S;
+                if (O.direct) {
+                    S = slot_sum(tot);
+                } else {  // the partial bins, written by other lanes, become visible; then the post sweep
+                    if (O.bins_lds) __syncthreads();
+                    else __threadfence_block();
+                    S = post_sweep(P, st, ldsb, s, g8, O);
                 }
-                // post sweep: output bin b = sum of its nE partial bins (in order); four bins per lane in
-                // flight, every load of a step issued before any use
-                if (bins_lds) S = post_sweep<true>(P, st, ldsb, s, g8, S, scr_b, binb, red_b, redl);
-                else S = post_sweep<false>(P, st, ldsb, s, g8, S, scr_b, binb, red_b, redl);
                 bad |= act && !(S >= 0x1p-900 && S <= 0x1p+900);
-                if (P.nmv > 0) {  // the reduced bins, for the marginal sweep (other lanes)
-                    if (bins_lds) __syncthreads();
+                if (!marg_pass && s == 0) bst(st, P.dest_sc * (C * 8) + g8, S);  // the message's scale
+                if (P.nmv > 0) {  // the output bins, for the marginal sweep (other lanes)
+                    if (O.out_lds) __syncthreads();
                     else __threadfence_block();
                 }
                 if (prof) {
@@ -386,6 +373,8 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
 #pragma unroll
                 for (int c = 0; c < kValChunks; ++c) a[c] = 0.0;
                 if (need) {
+                    // bin values: old(b) U(b) (Distribute: the calibrated separator up to a per-case
+                    // constant), U(b) (private variables)
                     const int32_t *__restrict__ bd = tab + P.bdig_off;
                     const int nb = P.nbins;
                     for (int b0 = 0; b0 < nb; b0 += 4) {
@@ -393,8 +382,10 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
 #pragma unroll
                         for (int t = 0; t < 4; ++t) {
                             const int bc = b0 + t < nb ? b0 + t : nb - 1;
-                            v[t] = bins_lds ? *reinterpret_cast<const double *>(ldsb + redl + bc * (C * 8) + g8)
-                                            : bld(st, red_b + bc * (C * 8) + g8, 0);
+                            const int o8 = bc * (C * 8) + g8;
+                            if (marg_pass) v[t] = O.out_lds ? *reinterpret_cast<const double *>(ldsb + O.out_b + o8)
+                                                            : bld(st, O.out_b + o8, 0);
+                            else v[t] = bld(st, P.col_row * (C * 8) + o8, 0) * bld(st, O.out_b + o8, 0);
                         }
 #pragma unroll
                         for (int t = 0; t < 4; ++t) {

@@ -38,6 +38,7 @@ int PosIn(const std::vector<int> &vars, int v) {
 struct Factor {
     const Table *sep;
     int64_t row;   // first row of the message in the wave store
+    int64_t srow;  // its scale row (the message is stored un-normalized: values / scale)
     int lds_off;   // byte offset in the wave's LDS, -1: read from the wave store
 };
 
@@ -106,10 +107,13 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
     for (int v = 0; v < V; ++v) out_off[v] = prog.sum_dom, prog.sum_dom += plan.dom[v];
     // wave store rows (JT_T_C doubles each): Collect messages, Distribute messages, partial bins of the
     // pass in flight, its reduced bins
-    std::vector<int64_t> col(ns), dis(ns);
+    // messages are stored un-normalized, each with a scale row (per case: the normalized message =
+    // row values / scale), so a pass writes its output bins once, straight from the entry sweep
+    std::vector<int64_t> col(ns), dis(ns), col_sc(ns), dis_sc(ns);
     int64_t rows = 0;
     for (int s = 0; s < ns; ++s) col[s] = rows, rows += plan.seps[s].size();
     for (int s = 0; s < ns; ++s) dis[s] = rows, rows += plan.seps[s].size();
+    for (int s = 0; s < ns; ++s) col_sc[s] = rows++, dis_sc[s] = rows++;
     prog.scr_row = rows;
 
     // clique digit fields (evidence masks), initial potentials
@@ -180,7 +184,8 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
     // output variable in the output's bin index), factors, destination
     auto build_pass = [&](int c, int kind, const std::vector<int> &opos, const std::vector<int64_t> &ocum,
                           int64_t nbins, const std::vector<Factor> &fac_in, int64_t dest_row, int64_t col_row,
-                          const std::vector<int> &mvars, bool first, int nstage, int32_t stage_off) -> int {
+                          int64_t dest_sc, int64_t col_sc_row, const std::vector<int> &mvars, bool first, int nstage,
+                          int32_t stage_off) -> int {
         const Table &t = plan.cliques[c];
         const int nv = (int)t.vars.size(), nf = (int)fac_in.size();
         JtTPass P{};
@@ -377,6 +382,10 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
         P.ofields = of;
         P.dest_row = (int32_t)dest_row;
         P.col_row = (int32_t)col_row;
+        P.dest_sc = (int32_t)dest_sc;
+        P.col_sc = (int32_t)col_sc_row;
+        P.fsc_off = (int32_t)prog.tab.size();  // the factors' scale rows, in factor order
+        for (int j = 0; j < nf; ++j) prog.tab.push_back((int32_t)fac[j].srow);
         // packed digits of every output bin, fields of the output variables in output order
         P.bdig_off = (int32_t)prog.tab.size();
         std::vector<int> osh(opos.size()), ofm(opos.size());
@@ -450,7 +459,7 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
     for (int c : post) {
         if (c == plan.root) continue;
         std::vector<Factor> fac;
-        for (int s : plan.clique_down[c]) fac.push_back({&plan.seps[s], col[s], -1});
+        for (int s : plan.clique_down[c]) fac.push_back({&plan.seps[s], col[s], col_sc[s], -1});
         int nst;
         int32_t so;
         place(fac, &nst, &so);
@@ -459,16 +468,17 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
         std::vector<int> opos;
         for (int v : sp.vars) opos.push_back(PosIn(plan.cliques[c].vars, v));
         if ((rc = build_pass(c, JT_T_COL, opos, std::vector<int64_t>(sp.cum.begin(), sp.cum.end()), sp.size(), fac,
-                             col[s], -1, {}, true, nst, so)))
+                             col[s], -1, col_sc[s], -1, {}, true, nst, so)))
             return rc;
     }
     // ---- Distribute (pre-order): one pass per child, then the private variables
     for (int c : pre) {
         const Table &t = plan.cliques[c];
         std::vector<Factor> fac;
-        for (int s : plan.clique_down[c]) fac.push_back({&plan.seps[s], col[s], -1});
+        for (int s : plan.clique_down[c]) fac.push_back({&plan.seps[s], col[s], col_sc[s], -1});
         const bool has_parent = c != plan.root;
-        if (has_parent) fac.push_back({&plan.seps[plan.clique_up[c]], dis[plan.clique_up[c]], -1});
+        if (has_parent)
+            fac.push_back({&plan.seps[plan.clique_up[c]], dis[plan.clique_up[c]], dis_sc[plan.clique_up[c]], -1});
         int nst;
         int32_t so;
         place(fac, &nst, &so);
@@ -488,7 +498,7 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
             for (size_t j = 0; j < fac.size(); ++j)
                 if (j != ci) sub.push_back(fac[j]);
             if ((rc = build_pass(c, JT_T_DIS, opos, std::vector<int64_t>(sp.cum.begin(), sp.cum.end()), sp.size(), sub,
-                                 dis[s], col[s], mv, first, nst, so)))
+                                 dis[s], col[s], dis_sc[s], col_sc[s], mv, first, nst, so)))
                 return rc;
             first = false;
         }
@@ -498,7 +508,7 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
             for (int i = (int)priv[c].size() - 1; i >= 0; --i) ocum[i] = m, m *= t.dims[priv[c][i]];
             std::vector<int> mv;
             for (int j : priv[c]) mv.push_back(t.vars[j]);
-            if ((rc = build_pass(c, JT_T_MARG, priv[c], ocum, m, fac, -1, -1, mv, first, nst, so)))
+            if ((rc = build_pass(c, JT_T_MARG, priv[c], ocum, m, fac, -1, -1, -1, -1, mv, first, nst, so)))
                 return rc;
         }
     }

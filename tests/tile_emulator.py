@@ -2,15 +2,16 @@
 tables from jt_tile_plan.cpp via fbn_jt_tile_program) on the host with numpy, one case at a time,
 so that the plan compiler's G / R records, factor offsets, LDS staging records, output bins and
 marginal sources are checked against the oracle without a GPU (tests/test_host.py).  Same algebra
-as the kernel (entry = G-part + R-part; w = init * prod factors, 0 against the evidence; partial
-bins -> output bins -> messages / marginals), different summation order (numpy), so results agree
-with the oracle to ~1e-14, not bit for bit.  Never used by the product path."""
+as the kernel (entry = G-part + R-part; w = init * prod factors, 0 against the evidence; output
+bins U times sigma = 1 / prod of the factors' scales -> un-normalized messages with a scale row,
+marginals from old * U), different summation order (numpy), so results agree with the oracle to
+~1e-14, not bit for bit.  Never used by the product path."""
 import numpy as np
 
 # JtTPass field order (jt_program.h)
 F = ["kind", "clique", "nf", "nl", "nG", "rounds", "nRo", "nRi", "g_off", "o_off", "i_off", "nE", "nbins",
      "dest_row", "col_row", "bdig_off", "nmv", "mv_off", "iv_off", "nv", "vars_off", "gfields", "ofields", "first",
-     "nstage", "stage_off", "et_off", "st_off"]
+     "nstage", "stage_off", "et_off", "st_off", "fsc_off", "dest_sc", "col_sc", "pad_"]
 COL, DIS, MARG = 0, 1, 2
 
 
@@ -41,6 +42,7 @@ def run_case(prog, ev_row, sum_dom, lds_bytes=1 << 20):
                 src, rows, dst = (int(v) for v in tab[P["stage_off"] + 3 * k:P["stage_off"] + 3 * k + 3])
                 lds[dst // 8:dst // 8 + rows * C:C] = store[src:src + rows]
         mv = [tuple(int(v) for v in tab[P["mv_off"] + 5 * m:P["mv_off"] + 5 * m + 5]) for m in range(P["nmv"])]
+        sig = 1.0 / np.prod([store[int(r)] for r in tab[P["fsc_off"]:P["fsc_off"] + nf]])
         if P["kind"] == MARG and all(int(ev_row[v]) >= 0 for v, *_ in mv):
             for var, off, dim, _, _ in mv:
                 out[off:off + dim] = 0.0
@@ -70,17 +72,14 @@ def run_case(prog, ev_row, sum_dom, lds_bytes=1 << 20):
         nb, nE = P["nbins"], P["nE"]
         part = np.zeros(nb * nE)
         part[xidx.reshape(-1)] = acc.reshape(-1)
-        S = acc.sum()
-        v = part.reshape(nb, nE).sum(axis=1)
-        if P["kind"] == COL:
-            store[P["dest_row"]:P["dest_row"] + nb] = v / S
-        elif P["kind"] == DIS:
-            # the child's own Collect message (not a factor of the pass) cancels: dis = U / S with
-            # S = sum old * U; the marginal bins are old * U
-            old = store[P["col_row"]:P["col_row"] + nb]
-            S = (old * v).sum()
-            store[P["dest_row"]:P["dest_row"] + nb] = np.where(old == 0.0, 0.0, v / S)
-            v = old * v
+        v = part.reshape(nb, nE).sum(axis=1) * sig
+        if P["kind"] != MARG:  # un-normalized message U, scale sum U
+            store[P["dest_row"]:P["dest_row"] + nb] = v
+            store[P["dest_sc"]] = v.sum()
+        if P["kind"] == DIS:
+            # the child's own Collect message `old` (not a factor of the pass) cancels in the
+            # reference's (U / S') / old; the marginal bins are old * U
+            v = store[P["col_row"]:P["col_row"] + nb] * v
         bd = tab[P["bdig_off"]:P["bdig_off"] + nb].astype(np.int64) & 0xFFFFFFFF
         for var, off, dim, sh, fm in mv:
             if int(ev_row[var]) >= 0:
