@@ -48,6 +48,7 @@ _SIGS = {
     "fbn_jt_kernel_options": [C.c_char_p, C.c_int64],
     "fbn_jt_kernel_build": [_vp],
     "fbn_jt_debug_force_fixup": [_vp, C.c_int],
+    "fbn_jt_debug_flagged_blocks": [_vp, _vp],
     "fbn_jt_set_exact": [_vp, C.c_int],
     "fbn_jt_plan_destroy": [_vp],
     "fbn_ci_dataset_upload": [_vp, C.c_int, _i64, _vp, C.c_int, _pp],
@@ -328,6 +329,12 @@ class JunctionTree:
 
     def debug_force_fixup(self, enable):
         lib.fbn_jt_debug_force_fixup(self._h, int(enable))
+
+    def debug_flagged_blocks(self):
+        """64-case blocks the last run flagged for the exact fixup (variants 3-5)."""
+        n = C.c_int64()
+        lib.fbn_jt_debug_flagged_blocks(self._h, C.byref(n))
+        return n.value
 
     def set_exact(self, exact):
         """Arithmetic order of the specialized / streamed kernels: True = the reference's

@@ -60,16 +60,17 @@ extern "C" hipError_t fbn_ci_onehot_build(const uint8_t *cols, const int32_t *di
 extern "C" size_t fbn_ci_l1_edge_bytes(void);
 extern "C" hipError_t fbn_ci_l1_setup(const int32_t *pairs, int E, const int32_t *adj, const int32_t *adj_off,
                                       void *ed, int32_t *pos, uint8_t *st, int32_t *sep, long long *counted,
-                                      int chunk0, int32_t *len, unsigned *ring, hipStream_t s);
+                                      int chunk0, int32_t *len, int32_t *off, unsigned *ring,
+                                      unsigned long long *sstat, long long cap, long long *scal, int num_cu,
+                                      hipStream_t s);
 extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims, const int32_t *row0, long long W,
                                       const int32_t *adj, const int32_t *pairtab, int nvars, void *edv, int32_t *pos,
                                       uint8_t *st, int32_t *sep, long long *counted, int32_t *len, int32_t *off,
-                                      int E, int chunk, long long cap, long long *total, long long *launched,
-                                      int32_t *items, int32_t *counts, int32_t *df, uint8_t *indep, double alpha,
-                                      unsigned long long *stats, const double *band, int nband, unsigned *open_cnt,
-                                      unsigned long long *rows_read, void *scan_tmp, size_t scan_tmp_bytes,
-                                      int num_cu, unsigned *open_next, int next_chunk, hipStream_t s);
-extern "C" size_t fbn_ci_l1_scan_bytes(int E);
+                                      int E, long long cap, long long *scal, int32_t *items, int32_t *counts,
+                                      int32_t *df, uint8_t *indep, double alpha, unsigned long long *stats,
+                                      const double *band, int nband, unsigned *open_cnt, int num_cu,
+                                      unsigned *open_next, int next_chunk, unsigned long long *sstat, unsigned epoch,
+                                      hipStream_t s);
 extern "C" hipError_t fbn_ci_gram(const uint32_t *bits, long long W, const int32_t *rl, const int32_t *tasks,
                                   long long ntasks, int masked, int32_t *out, int num_cu, hipStream_t s);
 extern "C" hipError_t fbn_ci_gram_pairs(const int32_t *G, long long ld, const int32_t *lead0, const int32_t *dims,
@@ -174,6 +175,7 @@ struct fbn_jt_plan {
     bool gen_eligible = false;
     int gen_state = 0;  // 0 not tried, 1 loaded, -1 failed
     bool gen_fast = false;  // arithmetic order of the loaded specialized kernel
+    int64_t last_nblk = 0;  // 64-case blocks of the last run (flags of variants 3-5)
     hipModule_t gen_mod = nullptr;
     hipFunction_t gen_fn = nullptr;
     int64_t gen_we = 0, gen_lds = 0;
@@ -254,7 +256,7 @@ struct fbn_ci_ctx {
     // device-resident level-1 search (CiLevel1Device): edge state, round buffers, per-round open
     // counts (pinned mirror), round events
     DevBuf l1pairs, l1adj, l1adjoff, l1ed, l1pos, l1st, l1sep, l1cnt, l1len, l1off, l1scal, l1open;
-    DevBuf l1items, l1counts, l1df, l1indep, l1tmp;
+    DevBuf l1items, l1counts, l1df, l1indep, l1sstat;  // l1sstat: the offset scan's per-tile status words
     DevBuf keptidx, kepttmp;  // level-0 kept pair indices (CiAllPairsKept)
     // level-0 Gram on the matrix cores (ci_gram_mfma.hip): FP4 one-hot store (Rp x Kb bytes, built
     // once, stage-major), the tile list of row range [g4_r0, g4_r1), split-K slabs
@@ -592,7 +594,8 @@ int fbn_jt_plan_create(const fbn_network *net, int device, fbn_jt_plan **out) {
     if (!p->v_ok) p->vprog = fbn::JTProgramV();
     lap("streamed program");
     // tiled variant: factors of a clique phase staged in LDS up to this many bytes per wave
-    static const int t_lds = getenv("FBN_JT_TLDS") ? atoi(getenv("FBN_JT_TLDS")) : 6144;  // (tuning knob)
+    // LDS factor budget per workgroup (JT_T_W waves share it; tuning knob)
+    static const int t_lds = getenv("FBN_JT_TLDS") ? atoi(getenv("FBN_JT_TLDS")) : 24576;
     rc = fbn::CompileJTProgramT(p->host, p->tprog, t_lds);
     if (rc && rc != FBN_ERR_LIMIT) return rc;
     p->t_ok = rc == FBN_OK;
@@ -817,6 +820,17 @@ int fbn_jt_debug_force_fixup(fbn_jt_plan *p, int enable) {
     return FBN_OK;
 }
 
+int fbn_jt_debug_flagged_blocks(fbn_jt_plan *p, int64_t *count) {
+    if (!p || !count) return SetError(FBN_ERR_ARG, "null pointer");
+    *count = 0;
+    if (p->last_nblk <= 0 || !p->flags.p) return FBN_OK;
+    std::vector<int> h((size_t)p->last_nblk);
+    FBN_HIP(hipDeviceSynchronize());
+    FBN_HIP(hipMemcpy(h.data(), p->flags.p, h.size() * 4, hipMemcpyDeviceToHost));
+    for (int f : h) *count += f != 0;
+    return FBN_OK;
+}
+
 int fbn_jt_kernel_build(const fbn_jt_plan *p) {
     if (!p) return SetError(FBN_ERR_ARG, "null pointer");
     if (!p->gen_eligible) return SetError(FBN_ERR_ARG, "plan not eligible for codegen");
@@ -964,6 +978,7 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
     }
     else if (variant == 3 && (rc = GenEnsure(p))) return rc;
     p->last_variant = variant;
+    p->last_nblk = variant >= 3 ? nblk : 0;
 
     if (variant == 1) {
         const int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 8;
@@ -1019,19 +1034,19 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
             (rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s)))
             return rc;
     } else if (variant == 5) {
-        // JT_T_C cases per wave, one wave per workgroup (persistent); per wave: its message store
-        // (messages, partial and reduced bins of the pass in flight) and its LDS factor stage
         const auto &t = p->tprog;
+        // workgroups of JT_T_W waves, one case group (JT_T_C cases) each, persistent; per workgroup
+        // its message store
         const int64_t ncg = (ncases + JT_T_C - 1) / JT_T_C;
         const int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 16;
-        int grid = (int)std::min<int64_t>(ncg, (int64_t)p->num_cu * wpc);
-        const size_t per_wave = (size_t)t.store_rows * JT_T_C * 8;
+        int grid = (int)std::min<int64_t>(ncg, std::max<int64_t>(1, (int64_t)p->num_cu * wpc / JT_T_W));
+        const size_t per_wg = (size_t)t.store_rows * JT_T_C * 8;
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
             const size_t have = free_b / 10 * 8 + p->ws.bytes;
-            grid = (int)std::max<int64_t>(1, std::min<int64_t>(grid, (int64_t)(have / per_wave)));
+            grid = (int)std::max<int64_t>(1, std::min<int64_t>(grid, (int64_t)(have / per_wg)));
         }
-        if ((rc = p->ws.ensure((size_t)grid * per_wave))) return rc;
+        if ((rc = p->ws.ensure((size_t)grid * per_wg))) return rc;
         if ((rc = p->flags.ensure((size_t)nblk * 4))) return rc;
         FBN_HIP(hipMemsetAsync(p->flags.p, 0, (size_t)nblk * 4, s));
         unsigned long long *tprof = nullptr;  // diagnostic: per-phase cycles (fbn_jt_debug_op_cycles)
@@ -1049,7 +1064,10 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt kernel launch: %s", hipGetErrorString(e));
         if (p->force_fixup) FBN_HIP(hipMemsetAsync(p->flags.p, 1, (size_t)nblk * 4, s));  // testing only
         // exact recomputation of the blocks holding a case group whose pass totals left the checked range
-        if ((rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s))) return rc;
+        // (FBN_JT_NO_FIXUP: diagnostic only -- flagged blocks keep the tiled kernel's values)
+        static const bool no_fix = getenv("FBN_JT_NO_FIXUP") != nullptr;
+        if (!no_fix && (rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s)))
+            return rc;
     } else if (variant == 3) {
         // one wave (64 cases) per SIMD: the clique in flight occupies the register file (+ LDS tail)
         int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 4;
@@ -2242,12 +2260,11 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
         (rc = c->l1pos.ensure((size_t)E * 4)) || (rc = c->l1st.ensure((size_t)E)) ||
         (rc = c->l1sep.ensure((size_t)E * 4)) || (rc = c->l1cnt.ensure((size_t)E * 8)) ||
         (rc = c->l1len.ensure((size_t)E * 4)) || (rc = c->l1off.ensure((size_t)E * 4)) ||
-        (rc = c->l1scal.ensure(32)) || (rc = c->l1open.ensure(kL1Ring * 4)) ||
+        (rc = c->l1scal.ensure(48)) || (rc = c->l1open.ensure(kL1Ring * 4)) ||
+        (rc = c->l1sstat.ensure((size_t)((E + 255) / 256) * 8)) ||
         (rc = c->l1items.ensure((size_t)cap * 12)) || (rc = c->l1counts.ensure((size_t)cap * 256)) ||
         (rc = c->l1df.ensure((size_t)cap * 4)) || (rc = c->l1indep.ensure((size_t)cap)))
         return rc;
-    const size_t scan_bytes = std::max<size_t>(fbn_ci_l1_scan_bytes(E), 16);
-    if ((rc = c->l1tmp.ensure(scan_bytes))) return rc;
     if (!c->h_open) {
         hipError_t e = hipHostMalloc((void **)&c->h_open, kL1Ring * 4, hipHostMallocDefault);
         if (e != hipSuccess) return SetError(FBN_ERR_NOMEM, "hipHostMalloc: %s", hipGetErrorString(e));
@@ -2260,14 +2277,16 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
     FBN_HIP(hipMemcpyAsync(c->l1pairs.p, edges.data() + e_begin, (size_t)E * 8, hipMemcpyHostToDevice, s));
     if (!adjf.empty()) FBN_HIP(hipMemcpyAsync(c->l1adj.p, adjf.data(), adjf.size() * 4, hipMemcpyHostToDevice, s));
     FBN_HIP(hipMemcpyAsync(c->l1adjoff.p, adj_off.data(), (size_t)(nv + 1) * 4, hipMemcpyHostToDevice, s));
-    FBN_HIP(hipMemsetAsync(c->l1scal.p, 0, 32, s));
+    // scalars (total, launched, rows read, scan flag, tickets) and the tile scan's status words (epoch 0)
+    FBN_HIP(hipMemsetAsync(c->l1scal.p, 0, 48, s));
+    FBN_HIP(hipMemsetAsync(c->l1sstat.p, 0, (size_t)((E + 255) / 256) * 8, s));
 
     if (ptiming)
         fprintf(stderr, "  level 1 device setup (host): %.3f ms\n",
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
     CiSlot &S = c->slot[0];
     if (c->timing) FBN_HIP(hipEventRecord(S.ev0, s));
-    long long *scal = c->l1scal.as<long long>();  // total, launched, rows read
+    long long *scal = c->l1scal.as<long long>();  // total, launched, rows read, scan flag, tickets
     int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(32, EnvOr0("FBN_PC_ROUND0", 8192) / E));
     // chunk x2 per round: rounds here cost a few launches, speculation costs counted tests (config 5:
     // x4 launches 430k tests for 294k counted, x2 345k)
@@ -2276,10 +2295,11 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
     chunk = std::min(chunk, max_chunk);
     // the setup writes round 0's lengths and zeroes the open-count ring; each round's resolve writes
     // the next round's lengths and zeroes the other ring slot (no length kernel or memset per round)
+    unsigned long long *sstat = c->l1sstat.as<unsigned long long>();
     hipError_t e = fbn_ci_l1_setup(c->l1pairs.as<int32_t>(), E, c->l1adj.as<int32_t>(), c->l1adjoff.as<int32_t>(),
                                    c->l1ed.p, c->l1pos.as<int32_t>(), c->l1st.as<uint8_t>(), c->l1sep.as<int32_t>(),
                                    c->l1cnt.as<long long>(), (int)chunk, c->l1len.as<int32_t>(),
-                                   c->l1open.as<unsigned>(), s);
+                                   c->l1off.as<int32_t>(), c->l1open.as<unsigned>(), sstat, cap, scal, c->num_cu, s);
     if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci level-1 setup: %s", hipGetErrorString(e));
     for (int r = 0;; ++r) {
         unsigned *open_r = c->l1open.as<unsigned>() + (r & 1);
@@ -2287,12 +2307,10 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
         e = fbn_ci_l1_round(c->bits.as<uint32_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(), c->bits_W,
                             c->l1adj.as<int32_t>(), c->pairtab.as<int32_t>(), nv, c->l1ed.p, c->l1pos.as<int32_t>(),
                             c->l1st.as<uint8_t>(), c->l1sep.as<int32_t>(), c->l1cnt.as<long long>(),
-                            c->l1len.as<int32_t>(), c->l1off.as<int32_t>(), E, (int)chunk, cap, scal, scal + 1,
-                            c->l1items.as<int32_t>(), c->l1counts.as<int32_t>(), c->l1df.as<int32_t>(),
-                            c->l1indep.as<uint8_t>(), alpha, c->stats.as<unsigned long long>(), band, nband,
-                            open_r, reinterpret_cast<unsigned long long *>(scal + 2),
-                            c->l1tmp.p, scan_bytes, c->num_cu, c->l1open.as<unsigned>() + ((r + 1) & 1),
-                            (int)next_chunk, s);
+                            c->l1len.as<int32_t>(), c->l1off.as<int32_t>(), E, cap, scal, c->l1items.as<int32_t>(),
+                            c->l1counts.as<int32_t>(), c->l1df.as<int32_t>(), c->l1indep.as<uint8_t>(), alpha,
+                            c->stats.as<unsigned long long>(), band, nband, open_r, c->num_cu,
+                            c->l1open.as<unsigned>() + ((r + 1) & 1), (int)next_chunk, sstat, (unsigned)(r + 2), s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci level-1 round: %s", hipGetErrorString(e));
         FBN_HIP(hipMemcpyAsync(c->h_open + (r & 1), open_r, 4, hipMemcpyDeviceToHost, s));
         FBN_HIP(hipEventRecord(c->l1ev[r & 1], s));
@@ -2305,17 +2323,18 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
     if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
     // read-back through one pinned staging buffer (DMA, no pageable staging copies):
     // [counters 8E | scalars 24 | sepsets 4E | status E] (each part aligned to its type)
-    if ((rc = PinnedEnsure(c->h_xfer, c->h_xfer_bytes, (size_t)E * 13 + 32))) return rc;
+    if ((rc = PinnedEnsure(c->h_xfer, c->h_xfer_bytes, (size_t)E * 13 + 40))) return rc;
     char *hx = static_cast<char *>(c->h_xfer);
     const long long *cnt = reinterpret_cast<const long long *>(hx);
     const long long *sc = reinterpret_cast<const long long *>(hx + (size_t)E * 8);
-    const int32_t *hsep = reinterpret_cast<const int32_t *>(hx + (size_t)E * 8 + 24);
-    const uint8_t *st = reinterpret_cast<const uint8_t *>(hx + (size_t)E * 12 + 24);
+    const int32_t *hsep = reinterpret_cast<const int32_t *>(hx + (size_t)E * 8 + 32);
+    const uint8_t *st = reinterpret_cast<const uint8_t *>(hx + (size_t)E * 12 + 32);
     FBN_HIP(hipMemcpyAsync(hx, c->l1cnt.p, (size_t)E * 8, hipMemcpyDeviceToHost, s));
-    FBN_HIP(hipMemcpyAsync(hx + (size_t)E * 8, scal, 24, hipMemcpyDeviceToHost, s));
-    FBN_HIP(hipMemcpyAsync(hx + (size_t)E * 8 + 24, c->l1sep.p, (size_t)E * 4, hipMemcpyDeviceToHost, s));
-    FBN_HIP(hipMemcpyAsync(hx + (size_t)E * 12 + 24, c->l1st.p, (size_t)E, hipMemcpyDeviceToHost, s));
+    FBN_HIP(hipMemcpyAsync(hx + (size_t)E * 8, scal, 32, hipMemcpyDeviceToHost, s));
+    FBN_HIP(hipMemcpyAsync(hx + (size_t)E * 8 + 32, c->l1sep.p, (size_t)E * 4, hipMemcpyDeviceToHost, s));
+    FBN_HIP(hipMemcpyAsync(hx + (size_t)E * 12 + 32, c->l1st.p, (size_t)E, hipMemcpyDeviceToHost, s));
     FBN_HIP(hipStreamSynchronize(s));
+    if (sc[3]) return SetError(FBN_ERR_HIP, "level-1 offset scan: look-back timed out");
     std::memcpy(out.sep.data(), hsep, (size_t)E * 4);
     for (int i = 0; i < E; ++i) {
         out.removed[i] = st[i] == 1;

@@ -17,11 +17,12 @@
 // bit for bit).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <algorithm>
 #include <stdlib.h>
 
 #include "ci_chisq.h"
 
-#include <hipcub/hipcub.hpp>
 
 namespace {
 
@@ -1035,54 +1036,118 @@ struct L1Edge {
     int32_t x, y, m0, L, skx, sky, ax, ay;  // ax / ay: adjacency offsets, skx / sky: position of y / x
 };
 
-// (also the first round's lengths, chunk0 candidates per edge, and both open-count ring slots zeroed)
+// The rounds' test offsets: a single-pass exclusive scan of the edges' lengths inside the kernel
+// that computes them (ci_l1_setup for round 0, ci_l1_resolve for the next round), 256-edge tiles
+// taken in ticket order (so every earlier tile belongs to a running workgroup) with a decoupled
+// look-back over the earlier tiles' published aggregates / prefixes, then the round's clip at cap
+// (edges past it continue next round).  Status word per tile: epoch << 34 | flag << 32 | value
+// (flag 1 = tile aggregate, 2 = inclusive prefix); the epoch (1 = setup, r + 2 = round r's resolve)
+// makes stale words of earlier kernels invisible without a memset.  scal: [0] total, [1] launched,
+// [2] rows read, [3] scan-timeout flag, then two ticket counters (kernel of epoch k uses k & 1 and
+// zeroes the other for the next kernel).
+constexpr long long kScanSpin = 1ll << 24;  // look-back spins before giving up (never reached)
+
+__device__ __forceinline__ int l1_ticket(unsigned *tickets, unsigned epoch) {
+    __shared__ int t_sh;
+    if (threadIdx.x == 0) t_sh = (int)atomicAdd(tickets + (epoch & 1u), 1u);
+    __syncthreads();
+    const int t = t_sh;
+    __syncthreads();
+    return t;
+}
+
+// exclusive offset of this thread's edge (len: this round's length, clipped in place)
+__device__ __forceinline__ int32_t l1_tile_scan(int tile, int ntiles, int32_t &len, unsigned long long *sstat,
+                                                unsigned epoch, long long cap, long long *scal) {
+    __shared__ int wsum[4];
+    __shared__ long long ex_sh;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int v = len;
+    int inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(inc, o);
+        if (lane >= o) inc += t;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    int wbase = 0, agg = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) wbase += k < w ? wsum[k] : 0, agg += wsum[k];
+    if (tid == 0) {
+        const unsigned long long tag = (unsigned long long)epoch << 34;
+        long long ex = 0;
+        if (tile > 0) {
+            __hip_atomic_store(sstat + tile, tag | (1ull << 32) | (unsigned)agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            long long spins = 0;
+            for (int j = tile - 1; j >= 0;) {
+                const unsigned long long st = __hip_atomic_load(sstat + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                if ((st >> 34) != epoch) {
+                    if (++spins > kScanSpin) {  // cannot happen (tiles are taken in order by running
+                        scal[3] = 1;            // workgroups); reported instead of hanging
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                ex += (long long)(st & 0xFFFFFFFFull);
+                if (((st >> 32) & 3ull) == 2ull) break;
+                --j;
+            }
+        }
+        __hip_atomic_store(sstat + tile, tag | (2ull << 32) | (unsigned long long)(ex + agg), __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        ex_sh = ex;
+        if (tile == ntiles - 1) {
+            const long long t = ex + agg < cap ? ex + agg : cap;
+            scal[0] = t;
+            scal[1] += t;
+        }
+    }
+    __syncthreads();
+    long long run = ex_sh + wbase + inc - v;
+    if (run + v > cap) {  // the clip: this round holds at most cap tests
+        len = (int32_t)(run >= cap ? 0 : cap - run);
+        run = run < cap ? run : cap;
+    }
+    return (int32_t)run;
+}
+
+// (also the first round's lengths, chunk0 candidates per edge, and their offsets; both open-count
+// ring slots zeroed)
 __global__ __launch_bounds__(256) void ci_l1_setup(const int32_t *__restrict__ pairs, int E,
                                                    const int32_t *__restrict__ adj,
                                                    const int32_t *__restrict__ adj_off, L1Edge *__restrict__ ed,
                                                    int32_t *__restrict__ pos, uint8_t *__restrict__ st,
                                                    int32_t *__restrict__ sep, long long *__restrict__ counted,
-                                                   int chunk0, int32_t *__restrict__ len, unsigned *__restrict__ ring) {
+                                                   int chunk0, int32_t *__restrict__ len, int32_t *__restrict__ off,
+                                                   unsigned *__restrict__ ring, unsigned long long *__restrict__ sstat,
+                                                   long long cap, long long *__restrict__ scal) {
+    constexpr unsigned epoch = 1;
+    unsigned *tickets = reinterpret_cast<unsigned *>(scal + 4);
     if (blockIdx.x == 0 && threadIdx.x < 2) ring[threadIdx.x] = 0u;
-    for (int e = blockIdx.x * 256 + threadIdx.x; e < E; e += gridDim.x * 256) {
-        const int x = pairs[2 * e], y = pairs[2 * e + 1];
-        const int ax = adj_off[x], nx = adj_off[x + 1] - ax, ay = adj_off[y], ny = adj_off[y + 1] - ay;
-        int skx = find_sorted(adj + ax, nx, y), sky = find_sorted(adj + ay, ny, x);
-        const int m0 = skx >= 0 ? nx - 1 : nx, m1 = sky >= 0 ? ny - 1 : ny;
-        skx = skx >= 0 ? skx : nx + 1, sky = sky >= 0 ? sky : ny + 1;
-        ed[e] = L1Edge{x, y, m0, m0 + m1, skx, sky, ax, ay};
-        pos[e] = 0;
-        st[e] = m0 + m1 == 0 ? 2 : 0;  // no candidate on either side: kept
-        sep[e] = -1;
-        counted[e] = 0;
-        len[e] = m0 + m1 == 0 ? 0 : (m0 + m1 < chunk0 ? m0 + m1 : chunk0);
-    }
-}
-
-__global__ __launch_bounds__(256) void ci_l1_len(const L1Edge *__restrict__ ed, const int32_t *__restrict__ pos,
-                                                 const uint8_t *__restrict__ st, int E, int chunk,
-                                                 int32_t *__restrict__ len) {
-    for (int e = blockIdx.x * 256 + threadIdx.x; e < E; e += gridDim.x * 256) {
-        const int left = ed[e].L - pos[e];
-        len[e] = st[e] == 0 ? (left < chunk ? left : chunk) : 0;
-    }
-}
-
-// after the exclusive scan of len (off, hipcub): lengths clipped so the round holds at most cap
-// tests (the clipped edges continue next round); *total = the round's tests, *launched += *total
-__global__ __launch_bounds__(256) void ci_l1_clip(int32_t *__restrict__ len, int32_t *__restrict__ off, int E,
-                                                  long long cap, long long *__restrict__ total,
-                                                  long long *__restrict__ launched) {
-    for (int e = blockIdx.x * 256 + threadIdx.x; e < E; e += gridDim.x * 256) {
-        const long long run = off[e], l = len[e];
-        if (e == E - 1) {
-            const long long t = run + l < cap ? run + l : cap;
-            *total = t;
-            *launched += t;
+    if (blockIdx.x == 0 && threadIdx.x == 0) tickets[(epoch + 1) & 1u] = 0u;
+    const int ntiles = (E + 255) / 256;
+    for (;;) {
+        const int tile = l1_ticket(tickets, epoch);
+        if (tile >= ntiles) break;
+        const int e = tile * 256 + threadIdx.x;
+        int32_t l = 0;
+        if (e < E) {
+            const int x = pairs[2 * e], y = pairs[2 * e + 1];
+            const int ax = adj_off[x], nx = adj_off[x + 1] - ax, ay = adj_off[y], ny = adj_off[y + 1] - ay;
+            int skx = find_sorted(adj + ax, nx, y), sky = find_sorted(adj + ay, ny, x);
+            const int m0 = skx >= 0 ? nx - 1 : nx, m1 = sky >= 0 ? ny - 1 : ny;
+            skx = skx >= 0 ? skx : nx + 1, sky = sky >= 0 ? sky : ny + 1;
+            ed[e] = L1Edge{x, y, m0, m0 + m1, skx, sky, ax, ay};
+            pos[e] = 0;
+            st[e] = m0 + m1 == 0 ? 2 : 0;  // no candidate on either side: kept
+            sep[e] = -1;
+            counted[e] = 0;
+            l = m0 + m1 == 0 ? 0 : (m0 + m1 < chunk0 ? m0 + m1 : chunk0);
         }
-        if (run + l > cap) {
-            len[e] = (int32_t)(run >= cap ? 0 : cap - run);
-            off[e] = (int32_t)(run < cap ? run : cap);
-        }
+        const int32_t o = l1_tile_scan(tile, ntiles, l, sstat, epoch, cap, scal);
+        if (e < E) len[e] = l, off[e] = o;
     }
 }
 
@@ -1121,17 +1186,22 @@ __global__ __launch_bounds__(256) void ci_l1_gen(const L1Edge *__restrict__ ed, 
 }
 
 __global__ __launch_bounds__(256) void ci_l1_resolve(const L1Edge *__restrict__ ed, int32_t *__restrict__ pos,
-                                                     const int32_t *__restrict__ len,
-                                                     const int32_t *__restrict__ off, uint8_t *__restrict__ st,
-                                                     int32_t *__restrict__ sep, long long *__restrict__ counted,
-                                                     const uint8_t *__restrict__ indep,
+                                                     int32_t *__restrict__ len, int32_t *__restrict__ off,
+                                                     uint8_t *__restrict__ st, int32_t *__restrict__ sep,
+                                                     long long *__restrict__ counted, const uint8_t *__restrict__ indep,
                                                      const int32_t *__restrict__ items, int E,
                                                      unsigned *__restrict__ open_cnt, unsigned *__restrict__ open_next,
-                                                     int next_chunk, int32_t *__restrict__ len_next) {
-    // the next round's open-count slot (its previous value went to the host before this round)
-    if (blockIdx.x == 0 && threadIdx.x == 0) *open_next = 0u;
-    for (int e0 = blockIdx.x * 256 + (threadIdx.x & ~63); e0 < E; e0 += gridDim.x * 256) {
-        const int e = e0 + (threadIdx.x & 63);
+                                                     int next_chunk, unsigned long long *__restrict__ sstat,
+                                                     unsigned epoch, long long cap, long long *__restrict__ scal) {
+    unsigned *tickets = reinterpret_cast<unsigned *>(scal + 4);
+    // the next round's open-count slot (its previous value went to the host before this round) and
+    // the next kernel's ticket counter
+    if (blockIdx.x == 0 && threadIdx.x == 0) *open_next = 0u, tickets[(epoch + 1) & 1u] = 0u;
+    const int ntiles = (E + 255) / 256;
+    for (;;) {
+        const int tile = l1_ticket(tickets, epoch);
+        if (tile >= ntiles) break;
+        const int e = tile * 256 + threadIdx.x;
         bool open = false;
         if (e < E && st[e] == 0) {
             const int n = len[e], o = off[e];
@@ -1152,11 +1222,14 @@ __global__ __launch_bounds__(256) void ci_l1_resolve(const L1Edge *__restrict__ 
                 else open = true;
             }
         }
-        // the next round's length of this edge (what ci_l1_len computed as a kernel of its own)
-        if (e < E) {
+        // the next round's length of this edge and, through the tile scan, its offset
+        int32_t l = 0;
+        if (e < E && open) {
             const int left = ed[e].L - pos[e];
-            len_next[e] = open ? (left < next_chunk ? left : next_chunk) : 0;
+            l = left < next_chunk ? left : next_chunk;
         }
+        const int32_t o = l1_tile_scan(tile, ntiles, l, sstat, epoch, cap, scal);
+        if (e < E) len[e] = l, off[e] = o;
         const unsigned nopen = (unsigned)__popcll(__ballot(open));  // one atomic per wave
         if ((threadIdx.x & 63) == 0 && nopen) atomicAdd(open_cnt, nopen);
     }
@@ -1233,55 +1306,48 @@ extern "C" hipError_t fbn_ci_bits_pairs_tiled(const uint32_t *bits, const int32_
 
 extern "C" size_t fbn_ci_l1_edge_bytes(void) { return sizeof(L1Edge); }
 
-// temporary storage of the round's length scan for E edges
-extern "C" size_t fbn_ci_l1_scan_bytes(int E) {
-    size_t b = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const int32_t *)nullptr, (int32_t *)nullptr, E);
-    return b;
-}
-
 extern "C" hipError_t fbn_ci_l1_setup(const int32_t *pairs, int E, const int32_t *adj, const int32_t *adj_off,
                                       void *ed, int32_t *pos, uint8_t *st, int32_t *sep, long long *counted,
-                                      int chunk0, int32_t *len, unsigned *ring, hipStream_t s) {
+                                      int chunk0, int32_t *len, int32_t *off, unsigned *ring,
+                                      unsigned long long *sstat, long long cap, long long *scal, int num_cu,
+                                      hipStream_t s) {
+    const int ntiles = (E + 255) / 256;
     if (E > 0)
-        hipLaunchKernelGGL(ci_l1_setup, dim3((E + 255) / 256), dim3(256), 0, s, pairs, E, adj, adj_off,
-                           (L1Edge *)ed, pos, st, sep, counted, chunk0, len, ring);
+        hipLaunchKernelGGL(ci_l1_setup, dim3((unsigned)std::min(ntiles, num_cu * 4)), dim3(256), 0, s, pairs, E, adj,
+                           adj_off, (L1Edge *)ed, pos, st, sep, counted, chunk0, len, off, ring, sstat, cap, scal);
     return hipGetLastError();
 }
 
-// one round: scan of the lengths (from ci_l1_setup or the previous round's resolve), clip,
-// generation, counting, G^2 / decisions, resolution (+ the next round's lengths for next_chunk);
-// `total` = the round's test count (device), `open_cnt` += edges still open after it, *open_next = 0
+// one round (its lengths and offsets come from ci_l1_setup or the previous round's resolve):
+// generation, counting, G^2 / decisions, resolution + the next round's lengths and offsets for
+// next_chunk; scal[0] = the round's test count (device), open_cnt += edges still open after it,
+// *open_next = 0; epoch = round + 2
 extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims, const int32_t *row0, long long W,
                                       const int32_t *adj, const int32_t *pairtab, int nvars, void *edv, int32_t *pos,
                                       uint8_t *st, int32_t *sep, long long *counted, int32_t *len, int32_t *off,
-                                      int E, int chunk, long long cap, long long *total, long long *launched,
-                                      int32_t *items, int32_t *counts, int32_t *df, uint8_t *indep, double alpha,
-                                      unsigned long long *stats, const double *band, int nband, unsigned *open_cnt,
-                                      unsigned long long *rows_read, void *scan_tmp, size_t scan_tmp_bytes,
-                                      int num_cu, unsigned *open_next, int next_chunk, hipStream_t s) {
+                                      int E, long long cap, long long *scal, int32_t *items, int32_t *counts,
+                                      int32_t *df, uint8_t *indep, double alpha, unsigned long long *stats,
+                                      const double *band, int nband, unsigned *open_cnt, int num_cu,
+                                      unsigned *open_next, int next_chunk, unsigned long long *sstat, unsigned epoch,
+                                      hipStream_t s) {
     const L1Edge *ed = (const L1Edge *)edv;
-    const long long ge = ((long long)E + 255) / 256, gcap = (long long)num_cu * 8;
-    const dim3 gE((unsigned)(ge < gcap ? ge : gcap));
+    const long long gcap = (long long)num_cu * 8;
     const long long gt = (cap + 255) / 256;
     const dim3 gT((unsigned)(gt < gcap ? gt : gcap));
     const long long gw = (cap + 3) / 4;
     const dim3 gW((unsigned)(gw < gcap ? gw : gcap));
-    (void)chunk;  // (this round's lengths came from ci_l1_setup or the previous round's resolve)
-    size_t tmp_bytes = scan_tmp_bytes;
-    hipError_t e = hipcub::DeviceScan::ExclusiveSum(scan_tmp, tmp_bytes, len, off, E, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(ci_l1_clip, gE, dim3(256), 0, s, len, off, E, cap, total, launched);
-    hipLaunchKernelGGL(ci_l1_gen, gT, dim3(256), 0, s, ed, pos, off, E, (const long long *)total, adj, items, dims,
-                       rows_read);
+    const int ntiles = (E + 255) / 256;
+    const long long *total = scal;
+    unsigned long long *rows_read = reinterpret_cast<unsigned long long *>(scal + 2);
+    hipLaunchKernelGGL(ci_l1_gen, gT, dim3(256), 0, s, ed, pos, off, E, total, adj, items, dims, rows_read);
     hipLaunchKernelGGL(ci_bits_count_derived, gW, dim3(256), 0, s, bits, dims, row0, (const int32_t *)items, W, cap,
-                       counts, pairtab, nvars, 1, (const long long *)total);
+                       counts, pairtab, nvars, 1, total);
     hipLaunchKernelGGL(ci_bits_g2<1>, gT, dim3(256), 0, s, (const int32_t *)counts, dims, (const int32_t *)items, cap,
                        alpha, (double *)nullptr, df, (double *)nullptr, indep, (int32_t *)nullptr, stats, nvars, 0ll,
-                       band, nband, (const long long *)total);
-    hipLaunchKernelGGL(ci_l1_resolve, gE, dim3(256), 0, s, ed, pos, (const int32_t *)len, (const int32_t *)off, st,
-                       sep, counted, (const uint8_t *)indep, (const int32_t *)items, E, open_cnt, open_next,
-                       next_chunk, len);
+                       band, nband, total);
+    hipLaunchKernelGGL(ci_l1_resolve, dim3((unsigned)std::min(ntiles, num_cu * 4)), dim3(256), 0, s, ed, pos, len,
+                       off, st, sep, counted, (const uint8_t *)indep, (const int32_t *)items, E, open_cnt, open_next,
+                       next_chunk, sstat, epoch, cap, scal);
     return hipGetLastError();
 }
 

@@ -90,7 +90,7 @@ struct JtVClique {
 #define JT_V_WAVES 2  // waves sharing one 64-case block (disjoint subtrees in parallel)
 
 // ---- tiled variant, jt_tile.hip (fast arithmetic order; the Munin-class default): one wave = JT_T_C
-// evidence cases x JT_T_L entry slots.  A pass over a clique splits the clique's variables into G
+// evidence cases x JT_T_L entry slots; JT_T_W waves work on the same case group.  A pass over a clique splits the clique's variables into G
 // (lane variables: slot s of a round takes G-configuration round * JT_T_L + s) and R (a stream of
 // configurations every lane walks in the same order: outer R-configurations over the output's
 // remaining variables, inner ones over the rest).  Entry e = G-part + R-part, so every index map is
@@ -107,6 +107,8 @@ struct JtVClique {
 #define JT_T_MAXF 7         // factors per pass: <= 6 child messages + the parent message
 #define JT_T_MAXDIM 8       // state counts of the variables (marginal sweep: value d in slot d % JT_T_L)
 #define JT_T_LDS_BIN_ROWS 16  // a pass's partial bins live in LDS when they are at most this many rows
+#define JT_T_W 4            // waves per workgroup: they share one case group, its message store and its
+                            // LDS factor stage, and split every pass (rounds or outer configurations)
 enum JtTKind : int32_t { JT_T_COL = 0, JT_T_DIS = 1, JT_T_MARG = 2 };
 struct JtTPass {
     int32_t kind, clique, nf, nl;    // factors; factors 0 .. nl-1 are staged in LDS, the rest are read
@@ -131,7 +133,8 @@ struct JtTPass {
     // messages are stored un-normalized with a per-case scale row (normalized = values / scale):
     int32_t fsc_off;                 // tab: the nf factors' scale rows
     int32_t dest_sc, col_sc;         // scale rows of the output message and of the child's Collect message (DIS)
-    int32_t pad_;
+    int32_t split;                   // work of the JT_T_W waves: 0 = rounds (round r -> wave r % JT_T_W),
+                                     // 1 = outer configurations (contiguous blocks, every round)
 };
 
 #endif

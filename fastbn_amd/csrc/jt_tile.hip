@@ -31,7 +31,7 @@
 
 namespace {
 
-constexpr int C = JT_T_C, L = JT_T_L;
+constexpr int C = JT_T_C, L = JT_T_L, W = JT_T_W;
 static_assert(C * L == 64, "one wave = C cases x L slots");
 constexpr int kValChunks = (JT_T_MAXDIM + L - 1) / L;  // marginal sweep: value d in slot d % L, chunk d / L
 constexpr int kBinRows = JT_T_LDS_BIN_ROWS;  // bin sets up to this many rows live in LDS
@@ -97,6 +97,8 @@ struct PassOut {
     int out_b;   // output rows (bytes: wave store, or LDS for out_lds)
     int part_b;  // partial bins (bytes: LDS for bins_lds, else the wave store)
     double sig;
+    int r0, rs;  // this wave's rounds: r0, r0 + rs, ...
+    int kb, ke;  // and its steps of each round's R stream [kb, ke) (whole inner runs)
 };
 
 // the entry work of one pass: rounds of G-configurations x the flattened R stream (outer x inner
@@ -112,7 +114,7 @@ struct PassOut {
 template <int NF, int NL>
 __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *__restrict__ tab,
                                                __amdgpu_buffer_rsrc_t ivrs, __amdgpu_buffer_rsrc_t st,
-                                               char *__restrict__ ldsb, int s, int g, uint32_t M, uint32_t W,
+                                               char *__restrict__ ldsb, int s, int g, uint32_t M, uint32_t Wd,
                                                const PassOut &O) {
     static_assert(C == 16, "a chunk = the 16 lanes of a DPP row");
     constexpr int RS = NF + 2, GS = 4 + NF, NFA = NF > 0 ? NF : 1;
@@ -120,11 +122,11 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
     const int g8 = g * 8;
     double tot = 0.0;
     const uint32_t gf = (uint32_t)P.gfields;
-    const uint32_t MR = M & ~gf, WR = W & MR;  // evidence on the R digits
-    const int nR = P.nRo * P.nRi;
+    const uint32_t MR = M & ~gf, WR = Wd & MR;  // evidence on the R digits
+    const int kb = O.kb, ke = O.ke;
     const int32_t *__restrict__ sr = tab + P.st_off;
     const int32_t *__restrict__ et = tab + P.et_off;
-    for (int r = 0; r < P.rounds; ++r) {
+    for (int r = O.r0; r < P.rounds; r += O.rs) {
         const int cfg = r * L + s;
         const bool la = cfg < P.nG;
         const int32_t *__restrict__ gr = tab + P.g_off + (size_t)(la ? cfg : 0) * GS;
@@ -134,24 +136,24 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
         int fG[NFA];
 #pragma unroll
         for (int j = 0; j < NF; ++j) fG[j] = gr[4 + j] + g8;
-        const bool okG = la && (((dwG ^ W) & M & gf) == 0u);
+        const bool okG = la && (((dwG ^ Wd) & M & gf) == 0u);
         double acc = 0.0;
         double fe[NFA];  // the factor values of the step before
 #pragma unroll
         for (int j = 0; j < NFA; ++j) fe[j] = 0.0;
         // slot s's entry at step k0 + g, one chunk ahead (the tables are padded by one chunk)
-        double wn = bld(ivrs, ivb + et[g], 0);
-        for (int k0 = 0; k0 < nR; k0 += C) {
+        double wn = bld(ivrs, ivb + et[kb + g], 0);
+        for (int k0 = kb; k0 < ke; k0 += C) {
             const double wl = wn;
-            if (k0 + C < nR) wn = bld(ivrs, ivb + et[k0 + C + g], 0);
+            if (k0 + C < ke) wn = bld(ivrs, ivb + et[k0 + C + g], 0);
 #pragma unroll
             for (int u0 = 0; u0 < C; u0 += U) {
-                if (k0 + u0 >= nR) break;  // (uniform)
+                if (k0 + u0 >= ke) break;  // (uniform)
                 double w[U], f[U][NFA];
                 bool ok[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    const int32_t *__restrict__ q = sr + (size_t)(k0 + u0 + u) * RS;  // (steps >= nR: padding)
+                    const int32_t *__restrict__ q = sr + (size_t)(k0 + u0 + u) * RS;  // (< ke + C: padded)
                     ok[u] = (((uint32_t)q[NF]) & MR) == WR;
 #pragma unroll
                     for (int j = 0; j < NF; ++j) {
@@ -165,7 +167,7 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const int k = k0 + u0 + u;
-                    if (k >= nR) break;
+                    if (k >= ke) break;
                     double x = w[u];
                     const int32_t *__restrict__ q = sr + (size_t)k * RS;
 #pragma unroll
@@ -201,12 +203,12 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
 
 // the post sweep of a pass whose output has fewer than JT_T_L bins (extra lane variables E):
 // output bin b = its nE partial bins added in order, times sigma, written like a direct pass's bin.
-// Returns the pass total S (lane partials in bin order, then the slot butterfly).
+// Returns the wave's share of the pass total (lane partials in bin order, then the slot butterfly).
 __device__ __forceinline__ double post_sweep(const JtTPass &P, __amdgpu_buffer_rsrc_t st, char *__restrict__ ldsb,
-                                             int s, int g8, const PassOut &O) {
+                                             int wv, int s, int g8, const PassOut &O) {
     const int nE = P.nE, nb = P.nbins;
     double tot = 0.0;
-    for (int b = s; b < nb; b += L) {
+    for (int b = wv * L + s; b < nb; b += W * L) {  // bins over the workgroup's slots
         double v = 0.0;
         for (int e = 0; e < nE; ++e) {
             const int x8 = (b * nE + e) * (C * 8) + g8;
@@ -224,81 +226,84 @@ __device__ __forceinline__ double post_sweep(const JtTPass &P, __amdgpu_buffer_r
 template <int NF>
 __device__ __forceinline__ double pass_entries_nl(const JtTPass &P, const int32_t *__restrict__ tab,
                                                   __amdgpu_buffer_rsrc_t ivrs, __amdgpu_buffer_rsrc_t st,
-                                                  char *__restrict__ ldsb, int s, int g, uint32_t M, uint32_t W,
+                                                  char *__restrict__ ldsb, int s, int g, uint32_t M, uint32_t Wd,
                                                   const PassOut &O) {
 #define FBN_TNL(n)                                                                                        \
     case n:                                                                                               \
-        if constexpr (n <= NF) return pass_entries<NF, n>(P, tab, ivrs, st, ldsb, s, g, M, W, O);     \
+        if constexpr (n <= NF) return pass_entries<NF, n>(P, tab, ivrs, st, ldsb, s, g, M, Wd, O);    \
         else return 0.0;
     switch (P.nl) {
         FBN_TNL(1) FBN_TNL(2) FBN_TNL(3) FBN_TNL(4) FBN_TNL(5) FBN_TNL(6) FBN_TNL(7)
-    default: return pass_entries<NF, 0>(P, tab, ivrs, st, ldsb, s, g, M, W, O);
+    default: return pass_entries<NF, 0>(P, tab, ivrs, st, ldsb, s, g, M, Wd, O);
     }
 #undef FBN_TNL
 }
 
-__global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__ passes, int npass,
-                                                     const int32_t *__restrict__ tab, const double *__restrict__ iv,
-                                                     const int8_t *__restrict__ evid, double *__restrict__ marg,
-                                                     int32_t *__restrict__ labels, double *__restrict__ ws,
-                                                     int *__restrict__ flags, long long ncases, long long store_rows,
-                                                     long long scr_row, long long red_row, int V, int SD,
-                                                     int fac_bytes, unsigned long long *__restrict__ prof) {
+__global__ __launch_bounds__(64 * W, 16 / W) void jt_tile_kernel(const JtTPass *__restrict__ passes, int npass,
+                                                         const int32_t *__restrict__ tab, const double *__restrict__ iv,
+                                                         const int8_t *__restrict__ evid, double *__restrict__ marg,
+                                                         int32_t *__restrict__ labels, double *__restrict__ ws,
+                                                         int *__restrict__ flags, long long ncases, long long store_rows,
+                                                         long long scr_row, long long red_row, int V, int SD,
+                                                         int fac_bytes, unsigned long long *__restrict__ prof) {
     extern __shared__ double lds[];
     char *ldsb = reinterpret_cast<char *>(lds);
-    const int lane = threadIdx.x & 63;
+    const int tid = threadIdx.x, wv = tid / 64, lane = tid & 63;
     const int s = lane / C, g = lane % C, g8 = g * 8;
+    // the workgroup's message store (its case group's messages, partial and reduced bins)
     __amdgpu_buffer_rsrc_t st = __builtin_amdgcn_make_buffer_rsrc(
         ws + (size_t)blockIdx.x * (size_t)store_rows * C, 0, (int)(store_rows * C * 8), 0x00020000);
     const int scr_b = (int)(scr_row * C * 8), red_b = (int)(red_row * C * 8);
-    // LDS: [factors: fac_bytes][partial bins: kBinRows rows][reduced bins: kBinRows rows]
-    const int binb = fac_bytes, redl = fac_bytes + kBinRows * C * 8;
+    // LDS: [factors: fac_bytes][partial bins x 2][reduced bins x 2][wave totals x 2] -- the bin and
+    // total regions alternate with the parity of the pass barrier, so a wave one pass ahead never
+    // writes what a slower wave still reads
+    constexpr int kBinBytes = kBinRows * C * 8;
+    const int bin0 = fac_bytes, red0 = fac_bytes + 2 * kBinBytes, tot0 = fac_bytes + 4 * kBinBytes;
     // initial potentials through a buffer resource: entry = per-lane G part (voffset) + the R
     // record's part (soffset, scalar) -- no per-step address arithmetic
     const __amdgpu_buffer_rsrc_t ivrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(iv), 0, 0x7FFFFFF8, 0x00020000);
     // diagnostic (prof != nullptr): s_memtime cycles per phase, summed over the waves -- [0] staging,
     // [1..3] entry work with every factor in LDS / in the wave store / mixed, [4] pass totals, scales
-    // and the post sweep, [5] marginal sweeps, [6] all
+    // and the post sweep (incl. the barrier wait), [5] marginal sweeps, [6] all
     unsigned long long pc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long t_all = prof ? clock64() : 0ull;
+    int par = 0;  // parity of the pass barriers so far (uniform over the workgroup)
     for (long long cg = blockIdx.x; cg * C < ncases; cg += gridDim.x) {
         const long long cs = cg * C + g;
         const bool act = cs < ncases;
         const long long csr = act ? cs : ncases - 1;
         const int8_t *__restrict__ ev = evid + csr * V;
         double *__restrict__ out = marg + csr * SD;
-        uint32_t M = 0u, W = 0u;  // the case's evidence in the clique's digit fields
+        uint32_t M = 0u, Wd = 0u;  // the case's evidence in the clique's digit fields
         bool bad = false;
         for (int p = 0; p < npass; ++p) {
             const JtTPass P = passes[p];
             unsigned long long t0 = prof ? dclock() : 0ull;
             if (P.first) {
-                // the messages earlier passes stored (other lanes) become visible: one fence per clique
-                // phase (no pass of a phase reads what another pass of the same phase writes)
-                __threadfence_block();
-                M = 0u, W = 0u;
+                M = 0u, Wd = 0u;
                 const int32_t *__restrict__ vr = tab + P.vars_off;
                 int xs[kMaxCliqueVars];  // every evidence byte in flight at once
 #pragma unroll
                 for (int j = 0; j < kMaxCliqueVars; ++j) xs[j] = j < P.nv ? ev[vr[3 * j]] : -1;
 #pragma unroll
                 for (int j = 0; j < kMaxCliqueVars; ++j)
-                    if (xs[j] >= 0) M |= (uint32_t)vr[3 * j + 2] << vr[3 * j + 1], W |= (uint32_t)xs[j] << vr[3 * j + 1];
-                if (P.nstage > 0) {
-                    __syncthreads();  // (one wave per workgroup: orders the LDS writes after earlier reads)
-                    for (int k = 0; k < P.nstage; ++k) {
-                        const int32_t *__restrict__ sr = tab + P.stage_off + 3 * k;
-                        const int src = sr[0] * (C * 8), n = sr[1] * C, dst = sr[2] >> 3;
-                        int i = lane;
-                        for (; i + 192 < n; i += 256) {  // four loads in flight
-                            const double a0 = bld(st, i * 8, src), a1 = bld(st, (i + 64) * 8, src),
-                                         a2 = bld(st, (i + 128) * 8, src), a3 = bld(st, (i + 192) * 8, src);
-                            lds[dst + i] = a0, lds[dst + i + 64] = a1, lds[dst + i + 128] = a2, lds[dst + i + 192] = a3;
-                        }
-                        for (; i < n; i += 64) lds[dst + i] = bld(st, i * 8, src);
+                    if (xs[j] >= 0) M |= (uint32_t)vr[3 * j + 2] << vr[3 * j + 1], Wd |= (uint32_t)xs[j] << vr[3 * j + 1];
+                // the clique's LDS factors, staged by the whole workgroup (every wave is past the last
+                // pass barrier, after which no wave reads the previous phase's factors)
+                for (int k = 0; k < P.nstage; ++k) {
+                    const int32_t *__restrict__ sg = tab + P.stage_off + 3 * k;
+                    const int src = sg[0] * (C * 8), n = sg[1] * C, dst = sg[2] >> 3;
+                    int i = tid;
+                    for (; i + 3 * 64 * W < n; i += 4 * 64 * W) {  // four loads in flight
+                        const double a0 = bld(st, i * 8, src), a1 = bld(st, (i + 64 * W) * 8, src),
+                                     a2 = bld(st, (i + 128 * W) * 8, src), a3 = bld(st, (i + 192 * W) * 8, src);
+                        lds[dst + i] = a0, lds[dst + i + 64 * W] = a1, lds[dst + i + 128 * W] = a2, lds[dst + i + 192 * W] = a3;
                     }
-                    __syncthreads();
+                    for (; i < n; i += 64 * W) lds[dst + i] = bld(st, i * 8, src);
                 }
+                // the staged factors, and the messages / scales the previous phase wrote (other waves),
+                // become visible
+                __syncthreads();
             }
             if (prof) {
                 const unsigned long long t1 = dclock();
@@ -310,7 +315,7 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
             if (P.kind == JT_T_MARG) {
                 bool any = false;
                 for (int m = 0; m < P.nmv; ++m) any |= act && ev[tab[P.mv_off + 5 * m]] < 0;
-                need_entries = __ballot(any) != 0ull;
+                need_entries = __ballot(any) != 0ull;  // (the same cases in every wave)
             }
             // output: Collect / Distribute -> the message rows (wave store); private variables -> the
             // reduced rows (LDS when they fit); partial bins (outputs with extra lane variables) in LDS
@@ -319,10 +324,17 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
             PassOut O;
             O.direct = P.nE == 1;
             O.bins_lds = P.nbins * P.nE <= kBinRows;
-            O.part_b = O.bins_lds ? binb : scr_b;
+            O.part_b = O.bins_lds ? bin0 + par * kBinBytes : scr_b;
             O.out_lds = marg_pass && P.nbins <= kBinRows;
-            O.out_b = marg_pass ? (O.out_lds ? redl : red_b) : P.dest_row * (C * 8);
+            O.out_b = marg_pass ? (O.out_lds ? red0 + par * kBinBytes : red_b) : P.dest_row * (C * 8);
             if (need_entries) {
+                // this wave's share: rounds r = wv (mod W), or a contiguous block of outer configurations
+                const int nRi = P.nRi;
+                if (P.split == 0) {
+                    O.r0 = wv, O.rs = W, O.kb = 0, O.ke = P.nRo * nRi;
+                } else {
+                    O.r0 = 0, O.rs = 1, O.kb = (P.nRo * wv) / W * nRi, O.ke = (P.nRo * (wv + 1)) / W * nRi;
+                }
                 // sigma = 1 / product of the factors' scales (this lane's case)
                 double prod = 1.0;
                 for (int j = 0; j < P.nf; ++j) prod *= bld(st, tab[P.fsc_off + j] * (C * 8) + g8, 0);
@@ -330,10 +342,10 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
                 O.sig = 1.0 / prod;
                 double tot = 0.0;
 #define FBN_TNF(n) \
-    case n: tot = pass_entries_nl<n>(P, tab, ivrs, st, ldsb, s, g, M, W, O); break;
+    case n: tot = pass_entries_nl<n>(P, tab, ivrs, st, ldsb, s, g, M, Wd, O); break;
                 switch (P.nf) {
                     FBN_TNF(0) FBN_TNF(1) FBN_TNF(2) FBN_TNF(3) FBN_TNF(4) FBN_TNF(5) FBN_TNF(6)
-                    default: tot = pass_entries_nl<7>(P, tab, ivrs, st, ldsb, s, g, M, W, O);
+                    default: tot = pass_entries_nl<7>(P, tab, ivrs, st, ldsb, s, g, M, Wd, O);
                 }
 #undef FBN_TNF
                 if (prof) {
@@ -341,29 +353,34 @@ __global__ __launch_bounds__(64) void jt_tile_kernel(const JtTPass *__restrict__
                     pc[P.nl == P.nf ? 1 : P.nl == 0 ? 2 : 3] += t1 - t0;
                     t0 = t1;
                 }
-                double S;
+                double Sw;
                 if (O.direct) {
-                    S = slot_sum(tot);
-                } else {  // the partial bins, written by other lanes, become visible; then the post sweep
-                    if (O.bins_lds) __syncthreads();
-                    else __threadfence_block();
-                    S = post_sweep(P, st, ldsb, s, g8, O);
+                    Sw = slot_sum(tot);
+                } else {  // the partial bins (every wave's) become visible; then the post sweep
+                    __syncthreads();
+                    Sw = post_sweep(P, st, ldsb, wv, s, g8, O);
                 }
+                // pass total = the waves' shares in wave order; the barrier also makes the output bins
+                // visible to the marginal sweep
+                double *tw = reinterpret_cast<double *>(ldsb + tot0 + par * (W * C * 8));
+                if (s == 0) tw[wv * C + g] = Sw;
+                __syncthreads();
+                double S = tw[g];
+#pragma unroll
+                for (int w = 1; w < W; ++w) S += tw[w * C + g];
                 bad |= act && !(S >= 0x1p-900 && S <= 0x1p+900);
-                if (!marg_pass && s == 0) bst(st, P.dest_sc * (C * 8) + g8, S);  // the message's scale
-                if (P.nmv > 0) {  // the output bins, for the marginal sweep (other lanes)
-                    if (O.out_lds) __syncthreads();
-                    else __threadfence_block();
-                }
+                if (!marg_pass && wv == 0 && s == 0) bst(st, P.dest_sc * (C * 8) + g8, S);  // the message's scale
+                par ^= 1;
                 if (prof) {
                     const unsigned long long t1 = dclock();
                     pc[4] += t1 - t0;
                     t0 = t1;
                 }
             }
-            // marginals whose source is this pass: value d of the variable in slot d % L (chunk d / L),
-            // summed over the bins in bin order, normalized by their total (evidence variables: zeros)
-            for (int m = 0; m < P.nmv; ++m) {
+            // marginals whose source is this pass (wave m % W): value d of the variable in slot d % L
+            // (chunk d / L), summed over the bins in bin order, normalized by their total (evidence
+            // variables: zeros)
+            for (int m = wv; m < P.nmv; m += W) {
                 const int32_t *__restrict__ mr = tab + P.mv_off + 5 * m;
                 const int var = mr[0], off = mr[1], dim = mr[2], sh = mr[3];
                 const uint32_t fm = (uint32_t)mr[4];
@@ -437,10 +454,11 @@ extern "C" hipError_t fbn_jt_tile_launch(const JtTPass *passes, int npass, const
                                          long long ncases, long long store_rows, long long scr_row, long long red_row,
                                          int V, int SD, int lds_bytes, int grid, unsigned long long *prof,
                                          hipStream_t stream) {
-    // LDS per wave: the staged factors, then the small bin sets (partial, reduced)
+    // workgroups of JT_T_W waves (one case group each); LDS per workgroup: the staged factors, the
+    // small bin sets (partial, reduced; two parities each), the waves' pass totals (two parities)
     const int fac = (lds_bytes + 15) & ~15;
-    const size_t total = (size_t)fac + 2 * (size_t)kBinRows * C * 8;
-    hipLaunchKernelGGL(jt_tile_kernel, dim3(grid), dim3(64), total, stream, passes, npass, tab, iv, evid, marg, labels,
-                       ws, flags, ncases, store_rows, scr_row, red_row, V, SD, fac, prof);
+    const size_t total = (size_t)fac + 4 * (size_t)kBinRows * C * 8 + 2 * (size_t)W * C * 8;
+    hipLaunchKernelGGL(jt_tile_kernel, dim3(grid), dim3(64 * W), total, stream, passes, npass, tab, iv, evid, marg,
+                       labels, ws, flags, ncases, store_rows, scr_row, red_row, V, SD, fac, prof);
     return hipGetLastError();
 }

@@ -220,6 +220,11 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
         P.nRi = (int32_t)Prod(t, RI);
         P.nE = (int32_t)nE;
         P.nbins = (int32_t)nbins;
+        {  // split the pass over the JT_T_W waves by rounds or by outer configurations, whichever is shorter
+            const int64_t by_rounds = (P.rounds + JT_T_W - 1) / JT_T_W * (int64_t)P.nRo;
+            const int64_t by_outer = (int64_t)P.rounds * ((P.nRo + JT_T_W - 1) / JT_T_W);
+            P.split = by_outer < by_rounds ? 1 : 0;
+        }
         max_x = std::max(max_x, nbins * nE);
         max_bins = std::max(max_bins, nbins);
         // factor strides per clique variable
@@ -356,11 +361,15 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
                     const int32_t *oq = ro + o * (4 + nf), *iq = ri + i * (2 + nf);
                     et[k] = oq[0] * 8 + iq[0];
                     int32_t *q = &sr[k * (nf + 2)];
+                    // a wave's first step (outer-configuration split) loads every factor
+                    bool wave_start = k == 0;
+                    if (P.split == 1)
+                        for (int w = 1; w < JT_T_W; ++w) wave_start |= k == (int64_t)P.nRo * w / JT_T_W * nRi_;
                     for (int f = 0; f < nf; ++f) {
                         q[f] = oq[4 + f] + iq[2 + f];
                         // bit 0 (offsets are multiples of a 128-byte row): the same row as the step
                         // before -- the kernel keeps the value it loaded then
-                        if (k > 0 && q[f] == (sr[(k - 1) * (nf + 2) + f] & ~1)) q[f] |= 1;
+                        if (!wave_start && q[f] == (sr[(k - 1) * (nf + 2) + f] & ~1)) q[f] |= 1;
                     }
                     q[nf] = (int32_t)((uint32_t)oq[1] | (uint32_t)iq[1]);
                     q[nf + 1] = i == nRi_ - 1 ? oq[2] : -1;

@@ -172,6 +172,9 @@ int fbn_jt_debug_op_cycles(fbn_jt_plan *p, int enable, unsigned long long *cycle
 int fbn_jt_kernel_source(const fbn_jt_plan *p, char *buf, int64_t cap, int64_t *len);
 /* Testing: variant 3 marks every block for the exact fixup pass (exercises the fixup path). */
 int fbn_jt_debug_force_fixup(fbn_jt_plan *p, int enable);
+/* Testing: number of 64-case blocks the last run of variant 3 / 4 / 5 flagged for the exact fixup
+ * (0 for other variants); synchronizes the device. */
+int fbn_jt_debug_flagged_blocks(fbn_jt_plan *p, int64_t *count);
 /* Path of the specialized kernel's code object in the on-disk cache (whether or not it exists);
  * a build step may compile fbn_jt_kernel_source() there with the options of fbn_jt_kernel_options. */
 int fbn_jt_kernel_cache_path(const fbn_jt_plan *p, char *buf, int64_t cap);

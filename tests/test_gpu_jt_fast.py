@@ -44,6 +44,7 @@ def test_fast_ragged_vs_oracle(jt, n):
     net = synth.read_xmlbif(os.path.join(GOLD, "alarm", "alarm.xml"))
     ev = synth.evidence_cases(net, n, 7, seed=n)
     lab, marg = jt.infer(ev)
+    assert jt.debug_flagged_blocks() == 0  # the specialized kernel's own results
     olab, omarg = O.OracleJT(os.path.join(GOLD, "alarm", "alarm.xml")).infer(ev)
     np.testing.assert_array_equal(lab, olab)
     _close(marg, omarg)

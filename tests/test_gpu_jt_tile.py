@@ -40,6 +40,7 @@ def test_alarm_ragged_batches(alarm, n):
     jt, ojt = alarm
     ev = synth.evidence_cases(synth.read_xmlbif(ALARM), n, 7, seed=100 + n)
     lab, marg = jt.infer(ev)
+    assert jt.debug_flagged_blocks() == 0  # the tiled kernel's own results (no exact recomputation)
     _check(lab, marg, *ojt.infer(ev), ev, jt.network.dims)
 
 
@@ -97,6 +98,7 @@ def test_synthetic_networks(tmp_path, nodes, window, dom, k):
         pytest.skip("plan outside the tiled variant's limits")
     jt.set_variant(5)
     lab, marg = jt.infer(ev)
+    assert jt.debug_flagged_blocks() == 0
     _check(lab, marg, *O.OracleJT(p).infer(ev), ev, jt.network.dims)
 
 
@@ -111,6 +113,7 @@ def test_munin_like_default_and_vs_oracle(tmp_path):
     jt = F.JunctionTree(F.Network(p), device=0)
     lab, marg = jt.infer(ev)
     assert jt.refresh_info()["variant"] == 5
+    assert jt.debug_flagged_blocks() == 0
     olab, omarg = O.OracleJT(p).infer(ev)
     _check(lab, marg, olab, omarg, ev, jt.network.dims)
     jt.set_exact(True)

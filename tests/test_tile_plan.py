@@ -78,11 +78,14 @@ def _check_steps(passes, tab, geo):
         st = tab[P["st_off"]:P["st_off"] + (nR + C) * (nf + 2)].reshape(nR + C, nf + 2).astype(np.int64)
         np.testing.assert_array_equal(et[:nR], (ro[:, 0:1] * 8 + ri[None, :, 0]).reshape(-1))
         assert (et[nR:] == 0).all() and (st[nR:, nf + 1] == -1).all()
+        W = 4  # JT_T_W: with the outer-configuration split every wave's first step loads its factors
+        starts = [0] + ([nRo * w // W * nRi for w in range(1, W)] if P["split"] == 1 else [])
         for j in range(nf):
             off = (ro[:, 4 + j:5 + j] + ri[None, :, 2 + j]).reshape(-1)
             assert (off % (C * 8) == 0).all()
             np.testing.assert_array_equal(st[:nR, j] & ~1, off)
             same = np.concatenate([[False], off[1:] == off[:-1]])
+            same[[k for k in starts if k < nR]] = False
             np.testing.assert_array_equal((st[:nR, j] & 1) == 1, same)
         dw = ((ro[:, 1:2] & 0xFFFFFFFF) | (ri[None, :, 1] & 0xFFFFFFFF)).reshape(-1)
         np.testing.assert_array_equal(st[:nR, nf] & 0xFFFFFFFF, dw)
