@@ -87,8 +87,8 @@ extern "C" hipError_t fbn_ci_bits_pairs_tiled(const uint32_t *bits, const int32_
 extern "C" hipError_t fbn_jt_tile_launch(const JtTPass *passes, int npass, const int32_t *tab, const double *iv,
                                          const int8_t *evid, double *marg, int32_t *labels, double *ws, int *flags,
                                          long long ncases, long long store_rows, long long scr_row, long long red_row,
-                                         int V, int SD, int lds_bytes, int grid, unsigned long long *prof,
-                                         hipStream_t stream);
+                                         int V, int SD, int lds_bytes, int grid, int waves,
+                                         unsigned long long *prof, hipStream_t stream);
 extern "C" hipError_t fbn_jt_virt_launch(const JtVClique *cls, const int32_t *aux, const double *initv,
                                          const uint64_t *dig, const int32_t *order, const int32_t *sched,
                                          const int32_t *vsel, const int8_t *evid, double *marg, int32_t *labels,
@@ -594,8 +594,9 @@ int fbn_jt_plan_create(const fbn_network *net, int device, fbn_jt_plan **out) {
     if (!p->v_ok) p->vprog = fbn::JTProgramV();
     lap("streamed program");
     // tiled variant: factors of a clique phase staged in LDS up to this many bytes per wave
-    // LDS factor budget per workgroup (JT_T_W waves share it; tuning knob)
-    static const int t_lds = getenv("FBN_JT_TLDS") ? atoi(getenv("FBN_JT_TLDS")) : 24576;
+    // LDS factor budget per workgroup (tuning knob): 6016 B + the bin and total rows = 10 KB, so 16
+    // one-wave workgroups fit a CU's 160 KB
+    static const int t_lds = getenv("FBN_JT_TLDS") ? atoi(getenv("FBN_JT_TLDS")) : 6016;
     rc = fbn::CompileJTProgramT(p->host, p->tprog, t_lds);
     if (rc && rc != FBN_ERR_LIMIT) return rc;
     p->t_ok = rc == FBN_OK;
@@ -1039,7 +1040,7 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
         // its message store
         const int64_t ncg = (ncases + JT_T_C - 1) / JT_T_C;
         const int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 16;
-        int grid = (int)std::min<int64_t>(ncg, std::max<int64_t>(1, (int64_t)p->num_cu * wpc / JT_T_W));
+        int grid = (int)std::min<int64_t>(ncg, std::max<int64_t>(1, (int64_t)p->num_cu * wpc / t.waves));
         const size_t per_wg = (size_t)t.store_rows * JT_T_C * 8;
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
@@ -1060,7 +1061,7 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
         hipError_t e = fbn_jt_tile_launch(p->tpass.as<JtTPass>(), (int)t.passes.size(), p->ttab.as<int32_t>(),
                                           p->tiv.as<double>(), d_evidence, marg, labels, p->ws.as<double>(),
                                           p->flags.as<int>(), ncases, t.store_rows, t.scr_row, t.red_row, V, SD,
-                                          (int)t.lds_bytes, grid, tprof, s);
+                                          (int)t.lds_bytes, grid, t.waves, tprof, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt kernel launch: %s", hipGetErrorString(e));
         if (p->force_fixup) FBN_HIP(hipMemsetAsync(p->flags.p, 1, (size_t)nblk * 4, s));  // testing only
         // exact recomputation of the blocks holding a case group whose pass totals left the checked range

@@ -1074,34 +1074,47 @@ __device__ __forceinline__ int32_t l1_tile_scan(int tile, int ntiles, int32_t &l
     int wbase = 0, agg = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) wbase += k < w ? wsum[k] : 0, agg += wsum[k];
-    if (tid == 0) {
+    if (w == 0) {  // wave 0: publish the aggregate, then look back 64 tiles at a time
         const unsigned long long tag = (unsigned long long)epoch << 34;
         long long ex = 0;
         if (tile > 0) {
-            __hip_atomic_store(sstat + tile, tag | (1ull << 32) | (unsigned)agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0)
+                __hip_atomic_store(sstat + tile, tag | (1ull << 32) | (unsigned)agg, __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_AGENT);
             long long spins = 0;
-            for (int j = tile - 1; j >= 0;) {
-                const unsigned long long st = __hip_atomic_load(sstat + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                if ((st >> 34) != epoch) {
+            for (int j0 = tile - 1; j0 >= 0; j0 -= 64) {
+                const int j = j0 - lane;  // lane l looks at tile j0 - l
+                unsigned long long st = 0;
+                for (;;) {  // until every looked-at tile has published
+                    st = j >= 0 ? __hip_atomic_load(sstat + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)
+                                : tag | (2ull << 32);
+                    if (__ballot((st >> 34) != epoch) == 0ull) break;
                     if (++spins > kScanSpin) {  // cannot happen (tiles are taken in order by running
                         scal[3] = 1;            // workgroups); reported instead of hanging
                         break;
                     }
                     __builtin_amdgcn_s_sleep(1);
-                    continue;
                 }
-                ex += (long long)(st & 0xFFFFFFFFull);
-                if (((st >> 32) & 3ull) == 2ull) break;
-                --j;
+                // the nearest inclusive prefix among them ends the look-back: add the values of the
+                // lanes up to and including it
+                const unsigned long long pre = __ballot(((st >> 32) & 3ull) == 2ull && j >= 0);
+                const int stop = pre ? __builtin_ctzll(pre) : 64;
+                long long val = (lane <= stop && j >= 0) ? (long long)(st & 0xFFFFFFFFull) : 0;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) val += __shfl_xor(val, o);
+                ex += val;
+                if (pre || spins > kScanSpin) break;
             }
         }
-        __hip_atomic_store(sstat + tile, tag | (2ull << 32) | (unsigned long long)(ex + agg), __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        ex_sh = ex;
-        if (tile == ntiles - 1) {
-            const long long t = ex + agg < cap ? ex + agg : cap;
-            scal[0] = t;
-            scal[1] += t;
+        if (lane == 0) {
+            __hip_atomic_store(sstat + tile, tag | (2ull << 32) | (unsigned long long)(ex + agg), __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            ex_sh = ex;
+            if (tile == ntiles - 1) {
+                const long long t = ex + agg < cap ? ex + agg : cap;
+                scal[0] = t;
+                scal[1] += t;
+            }
         }
     }
     __syncthreads();

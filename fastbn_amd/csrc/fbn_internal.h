@@ -129,6 +129,7 @@ struct JTProgramT {
     int64_t lds_bytes = 0;        // per wave: the largest set of factors staged at once
     int64_t entry_visits = 0;     // clique entries summed over all passes (one case)
     int num_cliques = 0, sum_dom = 0;
+    int waves = 1;                // waves per workgroup (one case group each) the passes' splits assume
 };
 // FBN_ERR_LIMIT when the plan does not fit (a domain > JT_T_MAXDIM states, > JT_T_MAXF - 1 children,
 // > 32 digit bits in a clique, tables beyond int32 indexing).  lds_budget: bytes of factors per wave.

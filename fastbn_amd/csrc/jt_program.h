@@ -107,8 +107,9 @@ struct JtVClique {
 #define JT_T_MAXF 7         // factors per pass: <= 6 child messages + the parent message
 #define JT_T_MAXDIM 8       // state counts of the variables (marginal sweep: value d in slot d % JT_T_L)
 #define JT_T_LDS_BIN_ROWS 16  // a pass's partial bins live in LDS when they are at most this many rows
-#define JT_T_W 4            // waves per workgroup: they share one case group, its message store and its
-                            // LDS factor stage, and split every pass (rounds or outer configurations)
+#define JT_T_W 4            // most waves per workgroup: they share one case group, its message store and
+                            // its LDS factor stage, and split every pass (rounds or outer configurations);
+                            // the plan's choice (FBN_JT_TW, default 1: measured fastest)
 enum JtTKind : int32_t { JT_T_COL = 0, JT_T_DIS = 1, JT_T_MARG = 2 };
 struct JtTPass {
     int32_t kind, clique, nf, nl;    // factors; factors 0 .. nl-1 are staged in LDS, the rest are read

@@ -31,7 +31,7 @@
 
 namespace {
 
-constexpr int C = JT_T_C, L = JT_T_L, W = JT_T_W;
+constexpr int C = JT_T_C, L = JT_T_L, kMaxW = JT_T_W;
 static_assert(C * L == 64, "one wave = C cases x L slots");
 constexpr int kValChunks = (JT_T_MAXDIM + L - 1) / L;  // marginal sweep: value d in slot d % L, chunk d / L
 constexpr int kBinRows = JT_T_LDS_BIN_ROWS;  // bin sets up to this many rows live in LDS
@@ -205,7 +205,7 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
 // output bin b = its nE partial bins added in order, times sigma, written like a direct pass's bin.
 // Returns the wave's share of the pass total (lane partials in bin order, then the slot butterfly).
 __device__ __forceinline__ double post_sweep(const JtTPass &P, __amdgpu_buffer_rsrc_t st, char *__restrict__ ldsb,
-                                             int wv, int s, int g8, const PassOut &O) {
+                                             int wv, int W, int s, int g8, const PassOut &O) {
     const int nE = P.nE, nb = P.nbins;
     double tot = 0.0;
     for (int b = wv * L + s; b < nb; b += W * L) {  // bins over the workgroup's slots
@@ -239,7 +239,7 @@ __device__ __forceinline__ double pass_entries_nl(const JtTPass &P, const int32_
 #undef FBN_TNL
 }
 
-__global__ __launch_bounds__(64 * W, 16 / W) void jt_tile_kernel(const JtTPass *__restrict__ passes, int npass,
+__global__ __launch_bounds__(64 * kMaxW, 16 / kMaxW) void jt_tile_kernel(const JtTPass *__restrict__ passes, int npass,
                                                          const int32_t *__restrict__ tab, const double *__restrict__ iv,
                                                          const int8_t *__restrict__ evid, double *__restrict__ marg,
                                                          int32_t *__restrict__ labels, double *__restrict__ ws,
@@ -248,17 +248,21 @@ __global__ __launch_bounds__(64 * W, 16 / W) void jt_tile_kernel(const JtTPass *
                                                          int fac_bytes, unsigned long long *__restrict__ prof) {
     extern __shared__ double lds[];
     char *ldsb = reinterpret_cast<char *>(lds);
-    const int tid = threadIdx.x, wv = tid / 64, lane = tid & 63;
+    // (wv through readfirstlane: the compiler then knows it is wave-uniform, so the step records of
+    // every wave's share stay scalar loads)
+    const int tid = threadIdx.x, wv = __builtin_amdgcn_readfirstlane(tid / 64), lane = tid & 63;
+    const int W = blockDim.x / 64;  // waves sharing the case group (the plan's split assumes this many)
     const int s = lane / C, g = lane % C, g8 = g * 8;
     // the workgroup's message store (its case group's messages, partial and reduced bins)
     __amdgpu_buffer_rsrc_t st = __builtin_amdgcn_make_buffer_rsrc(
         ws + (size_t)blockIdx.x * (size_t)store_rows * C, 0, (int)(store_rows * C * 8), 0x00020000);
     const int scr_b = (int)(scr_row * C * 8), red_b = (int)(red_row * C * 8);
-    // LDS: [factors: fac_bytes][partial bins x 2][reduced bins x 2][wave totals x 2] -- the bin and
-    // total regions alternate with the parity of the pass barrier, so a wave one pass ahead never
-    // writes what a slower wave still reads
+    // LDS: [factors: fac_bytes][partial bins x nbuf][reduced bins x nbuf][wave totals x nbuf] -- with
+    // several waves the bin and total regions alternate with the parity of the pass barrier, so a
+    // wave one pass ahead never writes what a slower wave still reads
     constexpr int kBinBytes = kBinRows * C * 8;
-    const int bin0 = fac_bytes, red0 = fac_bytes + 2 * kBinBytes, tot0 = fac_bytes + 4 * kBinBytes;
+    const int nbuf = W > 1 ? 2 : 1;
+    const int bin0 = fac_bytes, red0 = fac_bytes + nbuf * kBinBytes, tot0 = fac_bytes + 2 * nbuf * kBinBytes;
     // initial potentials through a buffer resource: entry = per-lane G part (voffset) + the R
     // record's part (soffset, scalar) -- no per-step address arithmetic
     const __amdgpu_buffer_rsrc_t ivrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(iv), 0, 0x7FFFFFF8, 0x00020000);
@@ -301,9 +305,10 @@ __global__ __launch_bounds__(64 * W, 16 / W) void jt_tile_kernel(const JtTPass *
                     }
                     for (; i < n; i += 64 * W) lds[dst + i] = bld(st, i * 8, src);
                 }
-                // the staged factors, and the messages / scales the previous phase wrote (other waves),
-                // become visible
-                __syncthreads();
+                // the staged factors, and the messages / scales the previous phase wrote (other lanes /
+                // waves), become visible
+                if (W > 1 || P.nstage > 0) __syncthreads();
+                else __threadfence_block();
             }
             if (prof) {
                 const unsigned long long t1 = dclock();
@@ -358,19 +363,24 @@ __global__ __launch_bounds__(64 * W, 16 / W) void jt_tile_kernel(const JtTPass *
                     Sw = slot_sum(tot);
                 } else {  // the partial bins (every wave's) become visible; then the post sweep
                     __syncthreads();
-                    Sw = post_sweep(P, st, ldsb, wv, s, g8, O);
+                    Sw = post_sweep(P, st, ldsb, wv, W, s, g8, O);
                 }
                 // pass total = the waves' shares in wave order; the barrier also makes the output bins
                 // visible to the marginal sweep
-                double *tw = reinterpret_cast<double *>(ldsb + tot0 + par * (W * C * 8));
-                if (s == 0) tw[wv * C + g] = Sw;
-                __syncthreads();
-                double S = tw[g];
-#pragma unroll
-                for (int w = 1; w < W; ++w) S += tw[w * C + g];
+                double S = Sw;
+                if (W > 1) {
+                    double *tw = reinterpret_cast<double *>(ldsb + tot0 + par * (W * C * 8));
+                    if (s == 0) tw[wv * C + g] = Sw;
+                    __syncthreads();
+                    S = tw[g];
+                    for (int w = 1; w < W; ++w) S += tw[w * C + g];
+                } else if (P.nmv > 0) {  // one wave: the output bins (other lanes) become visible
+                    if (O.out_lds) __syncthreads();
+                    else __threadfence_block();
+                }
                 bad |= act && !(S >= 0x1p-900 && S <= 0x1p+900);
                 if (!marg_pass && wv == 0 && s == 0) bst(st, P.dest_sc * (C * 8) + g8, S);  // the message's scale
-                par ^= 1;
+                par ^= nbuf - 1;
                 if (prof) {
                     const unsigned long long t1 = dclock();
                     pc[4] += t1 - t0;
@@ -452,13 +462,14 @@ __global__ __launch_bounds__(64 * W, 16 / W) void jt_tile_kernel(const JtTPass *
 extern "C" hipError_t fbn_jt_tile_launch(const JtTPass *passes, int npass, const int32_t *tab, const double *iv,
                                          const int8_t *evid, double *marg, int32_t *labels, double *ws, int *flags,
                                          long long ncases, long long store_rows, long long scr_row, long long red_row,
-                                         int V, int SD, int lds_bytes, int grid, unsigned long long *prof,
-                                         hipStream_t stream) {
+                                         int V, int SD, int lds_bytes, int grid, int waves,
+                                         unsigned long long *prof, hipStream_t stream) {
     // workgroups of JT_T_W waves (one case group each); LDS per workgroup: the staged factors, the
     // small bin sets (partial, reduced; two parities each), the waves' pass totals (two parities)
     const int fac = (lds_bytes + 15) & ~15;
-    const size_t total = (size_t)fac + 4 * (size_t)kBinRows * C * 8 + 2 * (size_t)W * C * 8;
-    hipLaunchKernelGGL(jt_tile_kernel, dim3(grid), dim3(64 * W), total, stream, passes, npass, tab, iv, evid, marg,
+    const size_t nbuf = waves > 1 ? 2 : 1;
+    const size_t total = (size_t)fac + 2 * nbuf * (size_t)kBinRows * C * 8 + nbuf * (size_t)waves * C * 8;
+    hipLaunchKernelGGL(jt_tile_kernel, dim3(grid), dim3(64 * waves), total, stream, passes, npass, tab, iv, evid, marg,
                        labels, ws, flags, ncases, store_rows, scr_row, red_row, V, SD, fac, prof);
     return hipGetLastError();
 }

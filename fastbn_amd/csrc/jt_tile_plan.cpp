@@ -178,6 +178,11 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
     }
 
     const int budget_rows = std::max(0, lds_budget) / (JT_T_C * 8);
+    // waves per workgroup sharing a case group (1 .. JT_T_W; FBN_JT_TW: tuning knob).  Default 1:
+    // on the Munin-like tree 2 / 4 waves per case group measured 235 / 291 ms against 211 ms --
+    // the passes' per-pass latency chain and imbalance outweigh the larger shared LDS stage
+    const int TW = std::max(1, std::min(JT_T_W, getenv("FBN_JT_TW") ? atoi(getenv("FBN_JT_TW")) : 1));
+    prog.waves = TW;
     int64_t max_x = 1, max_bins = 1;
 
     // one pass: clique c, output variables `opos` (positions) laid out by `ocum` (stride of each
@@ -220,9 +225,9 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
         P.nRi = (int32_t)Prod(t, RI);
         P.nE = (int32_t)nE;
         P.nbins = (int32_t)nbins;
-        {  // split the pass over the JT_T_W waves by rounds or by outer configurations, whichever is shorter
-            const int64_t by_rounds = (P.rounds + JT_T_W - 1) / JT_T_W * (int64_t)P.nRo;
-            const int64_t by_outer = (int64_t)P.rounds * ((P.nRo + JT_T_W - 1) / JT_T_W);
+        {  // split the pass over the workgroup's waves by rounds or by outer configurations, whichever is shorter
+            const int64_t by_rounds = (P.rounds + TW - 1) / TW * (int64_t)P.nRo;
+            const int64_t by_outer = (int64_t)P.rounds * ((P.nRo + TW - 1) / TW);
             P.split = by_outer < by_rounds ? 1 : 0;
         }
         max_x = std::max(max_x, nbins * nE);
@@ -239,6 +244,12 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
         // that minimizes the row changes of the wave-store factors (weight 1; LDS ones 1/8) is taken
         // -- exhaustively for small R, else by sorting (variables of many/large factors slowest)
         {
+            // weight of a row change: an LDS factor 1/8; a wave-store factor that stays in the
+            // wave's share of L2 (<= kCacheRows rows) 1/4; a larger one (its next row misses) 1
+            static const int64_t kCacheRows = getenv("FBN_JT_ORDER_ROWS") ? atoll(getenv("FBN_JT_ORDER_ROWS")) : 64;
+            auto wgt = [&](int j) {
+                return j < P.nl ? 0.125 : fac[j].sep->size() <= kCacheRows ? 0.25 : 1.0;
+            };
             auto changes = [&](const std::vector<int> &ord) {
                 double cst = 0.0;
                 for (int j = 0; j < nf; ++j) {
@@ -247,7 +258,7 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
                         n *= t.dims[i];
                         if (fs[j][i] != 0) seg = n;
                     }
-                    cst += (j < P.nl ? 0.125 : 1.0) * (double)seg;
+                    cst += wgt(j) * (double)seg;
                 }
                 return cst;
             };
@@ -271,7 +282,7 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
                 auto key = [&](int i) {
                     double k = 0.0;
                     for (int j = 0; j < nf; ++j)
-                        if (fs[j][i] != 0) k += j < P.nl ? 0.125 : 1.0;
+                        if (fs[j][i] != 0) k += wgt(j);
                     return k;
                 };
                 auto by = [&](int a, int b) { return key(a) > key(b); };
@@ -364,7 +375,7 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
                     // a wave's first step (outer-configuration split) loads every factor
                     bool wave_start = k == 0;
                     if (P.split == 1)
-                        for (int w = 1; w < JT_T_W; ++w) wave_start |= k == (int64_t)P.nRo * w / JT_T_W * nRi_;
+                        for (int w = 1; w < TW; ++w) wave_start |= k == (int64_t)P.nRo * w / TW * nRi_;
                     for (int f = 0; f < nf; ++f) {
                         q[f] = oq[4 + f] + iq[2 + f];
                         // bit 0 (offsets are multiples of a 128-byte row): the same row as the step

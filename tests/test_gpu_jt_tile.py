@@ -121,3 +121,25 @@ def test_munin_like_default_and_vs_oracle(tmp_path):
     assert jt.refresh_info()["variant"] == 4
     np.testing.assert_array_equal(lab, olab)
     np.testing.assert_array_equal(marg, omarg)
+
+
+@pytest.mark.parametrize("tw", [2, 4])
+def test_multi_wave_case_groups(alarm, tmp_path, monkeypatch, tw):
+    """FBN_JT_TW = 2 / 4 waves per case group (opt-in: passes split over the waves, one LDS stage
+    per case group): ALARM and a synthetic network against the oracle, nothing flagged."""
+    monkeypatch.setenv("FBN_JT_TW", str(tw))
+    _, ojt = alarm
+    jt = F.JunctionTree(F.Network(ALARM), device=0)
+    jt.set_variant(5)
+    ev = synth.evidence_cases(synth.read_xmlbif(ALARM), 777, 7, seed=tw)
+    lab, marg = jt.infer(ev)
+    assert jt.debug_flagged_blocks() == 0
+    _check(lab, marg, *ojt.infer(ev), ev, jt.network.dims)
+    p = str(tmp_path / "syn.xml")
+    synth.random_network(200, seed=200 + tw, window=10, path=p)
+    ev = synth.evidence_cases(synth.read_xmlbif(p), 333, 40, seed=tw)
+    jt = F.JunctionTree(F.Network(p), device=0)
+    jt.set_variant(5)
+    lab, marg = jt.infer(ev)
+    assert jt.debug_flagged_blocks() == 0
+    _check(lab, marg, *O.OracleJT(p).infer(ev), ev, jt.network.dims)

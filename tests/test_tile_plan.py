@@ -78,7 +78,7 @@ def _check_steps(passes, tab, geo):
         st = tab[P["st_off"]:P["st_off"] + (nR + C) * (nf + 2)].reshape(nR + C, nf + 2).astype(np.int64)
         np.testing.assert_array_equal(et[:nR], (ro[:, 0:1] * 8 + ri[None, :, 0]).reshape(-1))
         assert (et[nR:] == 0).all() and (st[nR:, nf + 1] == -1).all()
-        W = 4  # JT_T_W: with the outer-configuration split every wave's first step loads its factors
+        W = int(os.environ.get("FBN_JT_TW", "1"))  # with the outer split every wave's first step loads
         starts = [0] + ([nRo * w // W * nRi for w in range(1, W)] if P["split"] == 1 else [])
         for j in range(nf):
             off = (ro[:, 4 + j:5 + j] + ri[None, :, 2 + j]).reshape(-1)
@@ -101,4 +101,13 @@ def test_step_records_alarm():
 
 def test_step_records_munin_like(munin_fixture):
     _, (passes, tab, iv, geo) = _prog(munin_fixture["xml"])
+    _check_steps(passes, tab, geo)
+
+
+def test_step_records_four_wave_split(munin_fixture, monkeypatch):
+    """FBN_JT_TW = 4 (four waves per case group): split passes, reuse bits cleared at every wave's
+    first step."""
+    monkeypatch.setenv("FBN_JT_TW", "4")
+    _, (passes, tab, iv, geo) = _prog(munin_fixture["xml"])
+    assert any(int(p[TE.F.index("split")]) == 1 for p in passes)
     _check_steps(passes, tab, geo)

@@ -1,6 +1,7 @@
 """Tiled JT kernel (variant 5) on the GPU: parity against the oracle on ALARM and the Munin-like
 network, Munin-like timing (125k cases) and per-phase cycles, for a sweep of the LDS factor budget
-(FBN_JT_TLDS, per process) and waves per CU.  Usage: python tools/tile_probe.py [cases] [tlds:wpc ...]"""
+(FBN_JT_TLDS, per process), waves per CU and waves per workgroup (FBN_JT_TW).
+Usage: python tools/tile_probe.py [cases] [tlds:wpc[:tw] ...]"""
 import ctypes
 import os
 import subprocess
@@ -47,7 +48,8 @@ def child(cases, wpcs, with_v4):
         gm = d_marg[:16].cpu().numpy()
         rel = float(np.max(np.abs(gm - omarg) / np.maximum(np.abs(omarg), 1e-300)))
         ok = bool((d_lab[:16].cpu().numpy() == olab).all())
-        line = (f"TLDS {os.environ.get('FBN_JT_TLDS', 'default')} v{v} wpc {w}: kernel ms "
+        line = (f"TLDS {os.environ.get('FBN_JT_TLDS', 'default')} TW {os.environ.get('FBN_JT_TW', 'default')} "
+                f"v{v} wpc {w}: kernel ms "
                 f"{min(ms):.1f} -> {cases / (min(ms) * 1e-3):.4g} cases/s; labels equal {ok} max rel {rel:.2e}")
         if v == 5:
             buf = (ctypes.c_ulonglong * 10)()
@@ -79,8 +81,10 @@ def main():
     print(f"alarm v5: labels equal {bool((lab == olab).all())} max rel {rel:.3e}", flush=True)
     specs = sys.argv[2:] or ["16384:8", "8192:16,12", "32768:4"]
     for i, sp in enumerate(specs):
-        tl, w = sp.split(":")
+        tl, w, *tw = sp.split(":")  # LDS factor bytes per workgroup : waves per CU [: waves per workgroup]
         env = dict(os.environ, _TP_CHILD="1", FBN_JT_TLDS=tl, _TP_WPC=w, _TP_V4="1" if i == 0 else "0")
+        if tw:
+            env["FBN_JT_TW"] = tw[0]
         subprocess.run([sys.executable, __file__, str(cases)], check=True, env=env)
 
 
