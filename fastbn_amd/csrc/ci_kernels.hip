@@ -360,7 +360,8 @@ __global__ __launch_bounds__(BS) void ci_g2_kernel(CiArgs A) {
         // decision-only batches (no G^2 / p returned, band present): the terms summed as a block tree
         // first.  Tree and in-order sums of the same terms differ by at most (cells + 64) u sum|t|, so
         // a tree sum that clears the band [lo, hi] by that much decides exactly as the reference's
-        // ordered sum would; only the rest (near the band, or df past it) add in order below.
+        // ordered sum would (past the band's df range: p at both ends of that interval); only the
+        // rest (near alpha) add in order below.
         auto term_of = [&](int c) {
             const int k = c / dxy, i = (c / dy) % dx, j = c % dy;
             const long total = nk[k], sum_row = ni[k * dx + i], sum_col = nj[k * dy + j], observed = hist[c];
@@ -398,11 +399,21 @@ __global__ __launch_bounds__(BS) void ci_g2_kernel(CiArgs A) {
                 for (int w = 4; w < NW; ++w) gs += sred[2 * w], ga += sred[2 * w + 1], df += sdf[w];
                 const double err = (cells + 64) * 2.3e-16 * ga;
                 int dec = -1;  // 0 dependent, 1 independent, -1 in-order sum
+                double pd = -1.0;  // p of a decision past the band's df range
                 if (df == 0) dec = 1;  // src/IndependenceTest.cpp:140-142
                 else if (df <= A.nband && gs + err < A.band[2 * df - 2]) dec = 1;
                 else if (df <= A.nband && gs - err > A.band[2 * df - 1]) dec = 0;
+                else if (df > A.nband) {
+                    // p decreases in G^2 and the in-order sum lies in [gs - err, gs + err]: p at
+                    // both ends on the same side of alpha (by a relative 1e-12 more than the
+                    // evaluation's own rounding) decides as the in-order sum would
+                    const double phi = fbn_chisq_pvalue(gs - err > 0.0 ? gs - err : 0.0, df), plo = fbn_chisq_pvalue(gs + err, df);
+                    if (plo > A.alpha * (1.0 + 1e-12)) dec = 1, pd = plo;
+                    else if (phi < A.alpha * (1.0 - 1e-12)) dec = 0, pd = phi;
+                }
                 if (dec >= 0) {
-                    const double p = df == 0 ? 1.0 : dec ? A.alpha + A.band[2 * A.nband] : A.alpha - A.band[2 * A.nband];
+                    const double p = df == 0 ? 1.0 : pd >= 0.0 ? pd
+                                                 : dec ? A.alpha + A.band[2 * A.nband] : A.alpha - A.band[2 * A.nband];
                     if (A.df) A.df[it] = df;
                     if (A.indep) A.indep[it] = dec;
                     if (A.stats) {
