@@ -118,7 +118,7 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
                                                const PassOut &O) {
     static_assert(C == 16, "a chunk = the 16 lanes of a DPP row");
     constexpr int RS = NF + 2, GS = 4 + NF, NFA = NF > 0 ? NF : 1;
-    constexpr int U = NF <= 2 ? 8 : 4;  // steps with their loads in flight together (register budget)
+    constexpr int U = 4;  // steps with their loads in flight together
     const int g8 = g * 8;
     double tot = 0.0;
     const uint32_t gf = (uint32_t)P.gfields;
