@@ -2607,7 +2607,12 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
     // FBN_PC_SMALL_FAIL (test knob): "launch" = treat the launch as refused, "timeout" = a barrier
     // limit of one tick, so the first level's barrier times out in the kernel itself
     const char *force = getenv("FBN_PC_SMALL_FAIL");  // (read per call: tests set it)
-    static const bool plain = getenv("FBN_PC_SMALL_PLAIN") != nullptr;  // (diagnostic: non-cooperative launch)
+    // launch: plain by default -- the grid (one workgroup per CU, occupancy checked above) is resident
+    // unless other work holds CUs, and then a barrier times out (bounded spin) and the host driver
+    // takes over; hipLaunchCooperativeKernel (FBN_PC_SMALL_COOP=1, read per call) refuses such a grid
+    // up front but measured 12-15 us more kernel time per call (0.140 vs 0.126 ms on ALARM-5000)
+    const char *coop_env = getenv("FBN_PC_SMALL_COOP");
+    const bool plain = !(coop_env && atoi(coop_env) != 0);
     const bool force_launch = force && !strcmp(force, "launch");
     const long long spin = (force && !strcmp(force, "timeout")) ? 1 : 0;
     {

@@ -124,7 +124,7 @@ def test_repeated_runs_and_context_margin_log(alarm):
 
 @pytest.mark.parametrize("mode", ["launch", "timeout"])
 def test_fallback_to_host_levels(alarm, mode, monkeypatch):
-    """A refused cooperative launch, or a grid barrier that times out inside the kernel (a barrier
+    """A refused launch, or a grid barrier that times out inside the kernel (a barrier
     limit of one tick), hands the whole search to the host-driven levels: the same tests per level,
     skeleton, sepsets, orientation and SHD as the device-resident path, and a fresh margin log."""
     ds, od = alarm
@@ -142,3 +142,16 @@ def test_fallback_to_host_levels(alarm, mode, monkeypatch):
     # and the device path works again afterwards (barrier words zeroed again)
     again = F.PCStable(0.05, 1000).StructLearnCompData(ds)
     assert again.path == 1 and again.edges == dev.edges and again.sepset == dev.sepset
+
+
+def test_cooperative_launch_option(alarm, monkeypatch):
+    """FBN_PC_SMALL_COOP=1: the same search through hipLaunchCooperativeKernel (refuses a grid that
+    cannot be resident at once); default = plain launch with the bounded-spin fallback."""
+    ds, od = alarm
+    plain = F.PCStable(0.05, 1000).StructLearnCompData(ds)
+    monkeypatch.setenv("FBN_PC_SMALL_COOP", "1")
+    coop = F.PCStable(0.05, 1000).StructLearnCompData(ds)
+    monkeypatch.delenv("FBN_PC_SMALL_COOP")
+    assert plain.path == coop.path == 1
+    assert coop.tests_per_level.tolist() == plain.tests_per_level.tolist() == [666, 3579, 828, 118, 15]
+    assert coop.edges == plain.edges and coop.sepset == plain.sepset and coop.oriented == plain.oriented

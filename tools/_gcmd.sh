@@ -1,11 +1,9 @@
-# scratch GPU command (gpurun): round-4 -- full GPU suite, bench, kernel-trace stats
+# scratch GPU command (gpurun): round-4 -- pc_small plain launch default
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-o=gpurun_out/r04z; mkdir -p $o
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $o/gpu_tests.log 2>&1 || { tail -30 $o/gpu_tests.log; exit 1; }
-tail -2 $o/gpu_tests.log
-timeout -k 10 600 python bench.py > $o/bench.json 2> $o/bench.err || { tail -20 $o/bench.err; exit 1; }
-python -c "import json;d=json.loads(open('$o/bench.json').read().strip().splitlines()[-1]);print(json.dumps(d['summary']))"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/ktrace -o kt --output-format csv -- python bench.py --steps 5 --no-baseline --no-loaders > $o/kt_bench.json 2> $o/kt_bench.err || { tail -5 $o/kt_bench.err; exit 1; }
-ls $o/ktrace
+o=gpurun_out/r04h2; mkdir -p $o
+timeout -k 10 300 python -u -m pytest tests/test_gpu_pc_small.py tests/test_gpu_pc_dist.py tests/test_gpu_cli.py -x -v --timeout 120 --timeout-method thread > $o/t.log 2>&1 || { tail -30 $o/t.log; exit 1; }
+tail -1 $o/t.log
+timeout -k 10 300 python -u tools/pc_small_timing.py 400 > $o/tm.log 2>&1 || { tail -20 $o/tm.log; exit 1; }
+grep median $o/tm.log

@@ -30,7 +30,7 @@ def run(reps):
         t.append(time.perf_counter() - t0)
         F.lib.fbn_pc_result_destroy(h)
     mode = ("host-driven" if os.environ.get("FBN_PC_NO_SMALL") else
-            "device-resident (plain launch)" if os.environ.get("FBN_PC_SMALL_PLAIN") else "device-resident (cooperative)")
+            "device-resident (cooperative)" if os.environ.get("FBN_PC_SMALL_COOP") else "device-resident (plain launch)")
     print(f"{mode}: "
           f"median {1e3 * np.median(t):.4f} ms  min {1e3 * np.min(t):.4f} ms  kernel {kernel_ms:.4f} ms  "
           f"tests {pc.tests_per_level.tolist()} launched {pc.launched_per_level.tolist()} edges {len(pc.edges)}",
@@ -42,7 +42,7 @@ if __name__ == "__main__":
     if os.environ.get("_PCST_CHILD"):
         run(reps)
     else:
-        for extra in ({}, {"FBN_PC_SMALL_PLAIN": "1"}, {}, {"FBN_PC_SMALL_PLAIN": "1"}, {"FBN_PC_NO_SMALL": "1"}):
+        for extra in ({}, {"FBN_PC_SMALL_COOP": "1"}, {}, {"FBN_PC_SMALL_COOP": "1"}, {"FBN_PC_NO_SMALL": "1"}):
             env = dict(os.environ, _PCST_CHILD="1", **extra)
             subprocess.run([sys.executable, __file__, str(reps)], check=True, env=env)
         env = dict(os.environ, _PCST_CHILD="1", FBN_PC_TIMING="1")
