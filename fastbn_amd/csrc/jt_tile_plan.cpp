@@ -289,6 +289,104 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget) 
                 std::stable_sort(RO.begin(), RO.end(), by);
                 std::stable_sort(RI.begin(), RI.end(), by);
             }
+            // LRU refinement, for passes whose wave-store factors exceed the wave's share of L2
+            // (kCacheRows rows): round 0's row stream (every slot's rows of every wave-store factor,
+            // reused rows skipped as the kernel does) through a kCacheRows-row LRU, for candidate
+            // orders -- all when few, else the order above, its adjacent swaps and seeded random
+            // ones; the fewest misses wins (ties keep the order above).  FBN_JT_NO_LRU_ORDER: off.
+            int64_t glob_rows = 0;
+            for (int j = P.nl; j < nf; ++j) glob_rows += fac[j].sep->size();
+            const int64_t nR_ = Prod(t, RO) * Prod(t, RI);
+            static const bool no_lru = getenv("FBN_JT_NO_LRU_ORDER") != nullptr;
+            if (!no_lru && nf > P.nl && glob_rows > kCacheRows && nR_ * P.rounds * (nf - P.nl) >= 8192) {
+                std::vector<std::vector<int>> gd;
+                ForEachConfig(t, G, [&](const std::vector<int> &d) {
+                    if (gd.size() < (size_t)JT_T_L) gd.push_back(d);
+                });
+                if (G.empty()) gd.assign(1, {});
+                std::vector<std::vector<int64_t>> gpart(nf, std::vector<int64_t>(gd.size(), 0));
+                for (int j = P.nl; j < nf; ++j)
+                    for (size_t sl = 0; sl < gd.size(); ++sl)
+                        for (size_t i = 0; i < G.size(); ++i) gpart[j][sl] += gd[sl][i] * fs[j][G[i]];
+                const int K = (int)std::min<int64_t>(256, kCacheRows);
+                static const int64_t kLruSteps = getenv("FBN_JT_LRU_STEPS") ? atoll(getenv("FBN_JT_LRU_STEPS")) : 1024;
+                auto misses = [&](const std::vector<int> &ord) -> int64_t {
+                    const int nr = (int)ord.size();
+                    std::vector<int> d(nr, 0);
+                    std::vector<int64_t> prev(nf, -1);
+                    int64_t keys[256];
+                    uint64_t stamp[256];
+                    int used = 0;
+                    uint64_t clk = 0;
+                    int64_t miss = 0;
+                    for (int64_t k = 0; k < std::min<int64_t>(nR_, kLruSteps); ++k) {  // (a prefix: the
+                        for (int j = P.nl; j < nf; ++j) {                              // stream is periodic)
+                            int64_t r = 0;
+                            for (int i = 0; i < nr; ++i) r += d[i] * fs[j][ord[i]];
+                            if (r == prev[j]) continue;  // the kernel keeps the row it has
+                            prev[j] = r;
+                            for (size_t sl = 0; sl < gd.size(); ++sl) {
+                                const int64_t key = ((int64_t)j << 40) | (gpart[j][sl] + r);
+                                ++clk;
+                                int hit = -1, lru = 0;
+                                for (int q = 0; q < used; ++q) {
+                                    if (keys[q] == key) { hit = q; break; }
+                                    if (stamp[q] < stamp[lru]) lru = q;
+                                }
+                                if (hit >= 0) { stamp[hit] = clk; continue; }
+                                ++miss;
+                                if (used < K) keys[used] = key, stamp[used++] = clk;
+                                else keys[lru] = key, stamp[lru] = clk;
+                            }
+                        }
+                        for (int i = nr - 1; i >= 0; --i) {  // odometer, last fastest
+                            if (++d[i] < t.dims[ord[i]]) break;
+                            d[i] = 0;
+                        }
+                    }
+                    return miss;
+                };
+                std::vector<std::pair<std::vector<int>, std::vector<int>>> cand;
+                cand.push_back({RO, RI});
+                if (fact(RO.size()) * fact(RI.size()) <= 48) {
+                    std::vector<int> ro = RO, ri = RI;
+                    std::sort(ro.begin(), ro.end());
+                    do {
+                        std::sort(ri.begin(), ri.end());
+                        do cand.push_back({ro, ri});
+                        while (std::next_permutation(ri.begin(), ri.end()));
+                    } while (std::next_permutation(ro.begin(), ro.end()));
+                } else {
+                    for (size_t i = 0; i + 1 < RI.size(); ++i) {
+                        auto ri = RI;
+                        std::swap(ri[i], ri[i + 1]);
+                        cand.push_back({RO, ri});
+                    }
+                    for (size_t i = 0; i + 1 < RO.size(); ++i) {
+                        auto ro = RO;
+                        std::swap(ro[i], ro[i + 1]);
+                        cand.push_back({ro, RI});
+                    }
+                    uint64_t rs = 0x9E3779B97F4A7C15ull ^ (uint64_t)prog.passes.size();
+                    auto rnd = [&]() { rs ^= rs << 13, rs ^= rs >> 7, rs ^= rs << 17; return rs; };
+                    for (int q = 0; q < 24; ++q) {
+                        auto ro = RO, ri = RI;
+                        for (size_t i = ro.size(); i > 1; --i) std::swap(ro[i - 1], ro[rnd() % i]);
+                        for (size_t i = ri.size(); i > 1; --i) std::swap(ri[i - 1], ri[rnd() % i]);
+                        cand.push_back({ro, ri});
+                    }
+                }
+                int64_t bm = -1;
+                size_t bi = 0;
+                for (size_t q = 0; q < cand.size(); ++q) {
+                    std::vector<int> ord = cand[q].first;
+                    ord.insert(ord.end(), cand[q].second.begin(), cand[q].second.end());
+                    const int64_t m = misses(ord);
+                    if (bm < 0 || m < bm) bm = m, bi = q;
+                }
+                RO = cand[bi].first;
+                RI = cand[bi].second;
+            }
         }
         std::vector<int64_t> ecum(nv, 0), ocum_p(nv, 0);
         {
