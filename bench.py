@@ -709,8 +709,9 @@ def main():
     backend = os.environ.get("FBN_BENCH_BACKEND", "nccl")
     if backend != "nccl":
         local = local % max(1, torch.cuda.device_count())
-    if world > 1:
+    if world > 1 or os.environ.get("FBN_BENCH_FORCE_GATHER") == "1":
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
@@ -739,28 +740,34 @@ def main():
     jt.validate_device(d_ev.data_ptr(), args.cases, stream.cuda_stream)
     jt.set_evidence_check(False)
 
-    def step():
-        jt.run_device(d_ev.data_ptr(), args.cases, d_lab.data_ptr(), d_marg.data_ptr(), stream.cuda_stream)
+    # N > 1: north_star's "final gather" -- every step's labels (4 B per case) stay on the device
+    # (one slice per timed step) and ONE all-gather at the end of the timed region sends every
+    # rank's labels of every step to every rank (RCCL on the device; the gloo rehearsal stages
+    # through the host).  Marginals stay on the device; there is no golden table for
+    # synthetic cases, so no MSE / HD sum to reduce.  (A per-step all-gather measured +24 us per
+    # step at world size 1 even asynchronous: the collective's call overhead.)
+    # (FBN_BENCH_FORCE_GATHER=1: the gather at world size 1 too -- a test of the RCCL path)
+    gathering = world > 1 or (os.environ.get("FBN_BENCH_FORCE_GATHER") == "1" and dist.is_initialized())
+    step_labs = torch.empty((max(1, args.steps), args.cases), dtype=torch.int32, device=dev)
+    all_labs = torch.empty(world * step_labs.numel(), dtype=torch.int32, device=dev) if gathering else None
 
-    # N > 1: the step ends with north_star's "final gather" -- every rank's labels (4 B per case) to
-    # every rank in one all-gather (RCCL on the device; the gloo rehearsal stages through the host).
-    # Marginals stay on the device; there is no golden table for synthetic cases, so
-    # no MSE / HD sum to reduce.
-    all_lab = torch.empty(world * args.cases, dtype=torch.int32, device=dev) if world > 1 else None
+    def step(i=0):
+        lab = step_labs[i % step_labs.shape[0]]
+        jt.run_device(d_ev.data_ptr(), args.cases, lab.data_ptr(), d_marg.data_ptr(), stream.cuda_stream)
 
-    def gather():
-        if world == 1:
+    def final_gather():
+        if not gathering:
             return
         if backend == "nccl":
-            dist.all_gather_into_tensor(all_lab, d_lab)
+            dist.all_gather_into_tensor(all_labs, step_labs.view(-1))
         else:
-            parts = [torch.empty(args.cases, dtype=torch.int32) for _ in range(world)]
-            dist.all_gather(parts, d_lab.cpu())
-            all_lab.copy_(torch.cat(parts))
+            parts = [torch.empty(step_labs.numel(), dtype=torch.int32) for _ in range(world)]
+            dist.all_gather(parts, step_labs.view(-1).cpu())
+            all_labs.copy_(torch.cat(parts))
 
-    for _ in range(args.warmup):
-        step()
-        gather()
+    for i in range(args.warmup):
+        step(i)
+    final_gather()
     torch.cuda.synchronize(dev)
     ev_pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 for _ in range(args.steps)]
@@ -770,9 +777,9 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         ev_pairs[i][0].record(stream)
-        step()
+        step(i)
         ev_pairs[i][1].record(stream)
-        gather()
+    final_gather()  # part of the timed region
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -780,8 +787,10 @@ def main():
     elapsed = shard.max_over_ranks(elapsed, dev)  # identity at N = 1
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_pairs]))
 
-    if world > 1:  # the gathered labels hold every rank's shard in rank order
-        assert torch.equal(all_lab[rank * args.cases:(rank + 1) * args.cases], d_lab), "label all-gather"
+    d_lab = step_labs[(args.steps - 1) % step_labs.shape[0]]  # the last step's labels (checked below)
+    if gathering:  # the gathered labels hold every rank's labels of every step, in rank order
+        n1 = step_labs.numel()
+        assert torch.equal(all_labs[rank * n1:(rank + 1) * n1], step_labs.view(-1)), "label all-gather"
     # sanity: labels of the last step agree with a CPU recomputation on a few cases (not timed)
     if rank == 0:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -816,7 +825,8 @@ def main():
         "config": {"workload": "ALARM (37 vars) JT inference, 100k synthetic cases per GPU @ 7 evidence vars "
                                "(BASELINE config 2)", "cases_per_gpu": args.cases,
                    "evidence_per_case": EVIDENCE_PER_CASE,
-                   "parallelism": f"case-sharded x{world}" + (" + labels all-gather per step" if world > 1 else "")},
+                   "parallelism": f"case-sharded x{world}" + (" + one labels all-gather of every step (final gather)"
+                                                              if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel_ms": kernel_ms, "algorithmic_bytes_per_case": bpc,
