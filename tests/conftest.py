@@ -185,7 +185,12 @@ def munin_fixture(tmp_path_factory):
     plan = str(d / "ref.plan")
     with gzip.open(os.path.join(MUNIN, "ref.plan.gz"), "rb") as f, open(plan, "wb") as g:
         g.write(f.read())
-    return {"xml": xml, "libsvm": lib, "plan": plan, "marg": os.path.join(MUNIN, "ref.marg.gz")}
+    extra = str(d / "extra_ev.libsvm")
+    with gzip.open(os.path.join(MUNIN, "extra_ev.libsvm.gz"), "rb") as f, open(extra, "wb") as g:
+        g.write(f.read())
+    return {"xml": xml, "libsvm": lib, "plan": plan, "marg": os.path.join(MUNIN, "ref.marg.gz"),
+            # 64 more cases at 0 / 52 / 208 / 520 observed variables (make_golden_synth.py munin_extra)
+            "extra_libsvm": extra, "extra_marg": os.path.join(MUNIN, "extra_ref.marg.gz")}
 
 
 def parse_plan(path):

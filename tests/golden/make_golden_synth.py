@@ -64,6 +64,35 @@ def munin_like():
         gz_write(os.path.join(out, "ref.plan.gz"), open(pre + ".plan", "rb").read())
 
 
+MUNIN_EXTRA = (16, 0), (16, 52), (16, 208), (16, 520)  # (cases, observed variables): 64 cases
+
+
+def munin_like_extra():
+    """munin_like/extra_*: 64 more cases of the same network at 0 / 52 / 208 / 520 observed variables
+    (seed 7), with the reference's labels and 17-digit marginals -- the fast-order tiled kernel (the
+    Munin-class default) against the reference beyond the 32 base cases."""
+    import numpy as np
+    from fastbn_amd import synth
+    out = os.path.join(HERE, "munin_like")
+    ref_dump = os.path.join(REPO, "oracle", "_ref", "ref_dump")
+    if not os.path.exists(ref_dump):
+        subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref"], check=True)
+    with tempfile.TemporaryDirectory() as td:
+        xml = os.path.join(td, "munin_like.xml")
+        synth.random_network(1041, seed=1041, window=12, path=xml, name="munin_like")
+        net = synth.read_xmlbif(xml)
+        ev = np.concatenate([synth.evidence_cases(net, n, k, seed=7 + k) for n, k in MUNIN_EXTRA])
+        n = ev.shape[0]
+        lib = os.path.join(td, "ev.libsvm")
+        with open(lib, "w") as f:
+            for r in ev:
+                f.write("0 " + " ".join(f"{v}:{r[v]}" for v in range(r.size) if r[v] >= 0) + " \n")
+        pre = os.path.join(td, "ref")
+        subprocess.run([ref_dump, "jt", xml, lib, "-", pre, str(n)], check=True, stdout=subprocess.DEVNULL)
+        gz_write(os.path.join(out, "extra_ev.libsvm.gz"), open(lib, "rb").read())
+        gz_write(os.path.join(out, "extra_ref.marg.gz"), open(pre + ".marg", "rb").read())
+
+
 def pc_c5():
     import numpy as np
     import oracle as O
@@ -176,9 +205,11 @@ def gram_ragged():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["munin", "c5", "c5ci", "gram"]
+    which = sys.argv[1:] or ["munin", "munin_extra", "c5", "c5ci", "gram"]
     if "munin" in which:
         munin_like()
+    if "munin_extra" in which:
+        munin_like_extra()
     if "c5" in which:
         pc_c5()
     if "c5ci" in which:

@@ -274,3 +274,18 @@ def test_munin_like_full_network_vs_reference(munin_fixture):
     np.testing.assert_allclose(marg, rmarg, rtol=MUNIN_REF_RTOL, atol=1e-300)
     np.testing.assert_array_equal(lab, olab)
     np.testing.assert_array_equal(marg, omarg)
+
+
+def test_munin_like_extra_cases_vs_reference(munin_fixture):
+    """The default Munin-class path (tiled kernel, fast order) on 64 more reference cases at 0 / 52 /
+    208 / 520 observed variables: labels equal the reference's, marginals within 1e-9 relative,
+    nothing handed to the exact fixup."""
+    from conftest import read_ref_marg
+    jt = F.JunctionTree(F.Network(munin_fixture["xml"]), device=0)
+    o = O.OracleJT(munin_fixture["xml"])
+    ev, _ = O.load_libsvm(munin_fixture["extra_libsvm"], o.n)
+    rlab, rmarg, _, _ = read_ref_marg(munin_fixture["extra_marg"], o.dims)
+    lab, marg = jt.infer(ev)
+    assert jt.refresh_info()["variant"] == 5 and jt.debug_flagged_blocks() == 0
+    np.testing.assert_array_equal(lab, rlab)
+    np.testing.assert_allclose(marg, rmarg, rtol=1e-9, atol=1e-300)

@@ -111,3 +111,16 @@ def test_step_records_four_wave_split(munin_fixture, monkeypatch):
     _, (passes, tab, iv, geo) = _prog(munin_fixture["xml"])
     assert any(int(p[TE.F.index("split")]) == 1 for p in passes)
     _check_steps(passes, tab, geo)
+
+
+def test_munin_like_extra_cases_vs_reference(munin_fixture):
+    """The tiled program on one reference case per evidence level (0 / 52 / 208 / 520 observed)."""
+    from conftest import read_ref_marg
+    jt, prog = _prog(munin_fixture["xml"])
+    o = O.OracleJT(munin_fixture["xml"])
+    ev, _ = O.load_libsvm(munin_fixture["extra_libsvm"], o.n)
+    rlab, rmarg, _, _ = read_ref_marg(munin_fixture["extra_marg"], o.dims)
+    pick = [0, 16, 32, 48]
+    lab, marg = TE.run(prog, ev[pick], jt.info["sum_dom"])
+    np.testing.assert_array_equal(lab, rlab[pick])
+    np.testing.assert_allclose(marg, rmarg[pick], rtol=1e-9, atol=1e-300)
