@@ -143,6 +143,14 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
         for (int j = 0; j < NFA; ++j) fe[j] = 0.0;
         // slot s's entry at step k0 + g, one chunk ahead (the tables are padded by one chunk)
         double wn = bld(ivrs, ivb + et[kb + g], 0);
+        // the step records of the batch in flight (qc) and of the next one (qn): the next batch's
+        // scalar loads are issued before this batch computes, so a scalar-cache miss is not on the
+        // batch's critical path (the records are padded past every wave's last step)
+        int32_t qc[U][RS];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int i = 0; i < RS; ++i) qc[u][i] = sr[(size_t)(kb + u) * RS + i];
         for (int k0 = kb; k0 < ke; k0 += C) {
             const double wl = wn;
             if (k0 + C < ke) wn = bld(ivrs, ivb + et[k0 + C + g], 0);
@@ -153,15 +161,19 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
                 bool ok[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    const int32_t *__restrict__ q = sr + (size_t)(k0 + u0 + u) * RS;  // (< ke + C: padded)
-                    ok[u] = (((uint32_t)q[NF]) & MR) == WR;
+                    ok[u] = (((uint32_t)qc[u][NF]) & MR) == WR;
 #pragma unroll
                     for (int j = 0; j < NF; ++j) {
-                        if (q[j] & 1) continue;  // (uniform) the row of the step before
-                        if (j < NL) f[u][j] = *reinterpret_cast<const double *>(ldsb + (fG[j] + q[j]));  // bytes
-                        else f[u][j] = bld(st, fG[j], q[j]);
+                        if (qc[u][j] & 1) continue;  // (uniform) the row of the step before
+                        if (j < NL) f[u][j] = *reinterpret_cast<const double *>(ldsb + (fG[j] + qc[u][j]));  // bytes
+                        else f[u][j] = bld(st, fG[j], qc[u][j]);
                     }
                 }
+                int32_t qn[U][RS];
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int i = 0; i < RS; ++i) qn[u][i] = sr[(size_t)(k0 + u0 + U + u) * RS + i];
 #pragma unroll
                 for (int u = 0; u < U; ++u) w[u] = row_bcast_n(wl, u0 + u);
 #pragma unroll
@@ -169,14 +181,13 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
                     const int k = k0 + u0 + u;
                     if (k >= ke) break;
                     double x = w[u];
-                    const int32_t *__restrict__ q = sr + (size_t)k * RS;
 #pragma unroll
                     for (int j = 0; j < NF; ++j) {
-                        if (!(q[j] & 1)) fe[j] = f[u][j];
+                        if (!(qc[u][j] & 1)) fe[j] = f[u][j];
                         x *= fe[j];
                     }
                     acc += ok[u] ? x : 0.0;
-                    const int xo = q[NF + 1];
+                    const int xo = qc[u][NF + 1];
                     if (xo >= 0) {  // end of an inner run: its bin
                         const double a = okG ? acc : 0.0;
                         if (la) {
@@ -195,6 +206,10 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
                         acc = 0.0;
                     }
                 }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int i = 0; i < RS; ++i) qc[u][i] = qn[u][i];
             }
         }
     }
