@@ -2,7 +2,9 @@
 // default.  Passes and tables: jt_tile_plan.cpp; layout: jt_program.h (JtTPass).
 //
 // One wave = JT_T_C evidence cases x JT_T_L entry slots (lane = slot * JT_T_C + case), persistent
-// over groups of JT_T_C cases.  A pass walks one clique: slot s of round r takes G-configuration
+// over groups of JT_T_C cases (one wave per workgroup by default; FBN_JT_TW = 2 / 4 lets that many
+// waves share a case group, its store and its LDS stage, splitting every pass by rounds or by
+// blocks of outer configurations).  A pass walks one clique: slot s of round r takes G-configuration
 // r * JT_T_L + s, every lane walks the same R stream, and entry e = G-part + R-part gives
 //     w(e) = init(e) * prod_j M_j(s_j(e))        (0 if e contradicts the lane's case's evidence)
 // -- the clique's table after all its child multiplications [and the parent's], up to the
