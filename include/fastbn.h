@@ -182,7 +182,7 @@ int fbn_jt_kernel_cache_path(const fbn_jt_plan *p, char *buf, int64_t cap);
 int fbn_jt_kernel_build(const fbn_jt_plan *p);
 /* Compile options of the specialized kernel, '\n'-separated. */
 int fbn_jt_kernel_options(char *buf, int64_t cap);
-/* The tiled kernel's program (variant 5, jt_program.h JtTPass): passes [n_passes] (28 int32 each),
+/* The tiled kernel's program (variant 5, jt_program.h JtTPass): passes [n_passes] (32 int32 each),
  * index tables [n_tab], initial potentials [n_init]; geometry = {n_passes, n_tab, n_init,
  * partial-bin row, reduced-bin row, store rows, cases per wave, slots per case}.  Buffers may be
  * NULL (sizes only).  For tests that execute the tables on the host (tests/tile_emulator.py). */
@@ -215,16 +215,16 @@ int fbn_ci_run(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alp
 int fbn_ci_counts(fbn_ci_ctx *c, int x, int y, const int32_t *z, int d, int32_t *counts, int64_t cap,
                   int64_t *cells);
 int fbn_ci_last_kernel_ms(const fbn_ci_ctx *c, float *ms);
-/* Decision-margin log (SURVEY §8(c)): the p-value CDF (stats::pchisq, src/IndependenceTest.cpp:146,
- * 268,355) is not pinned by any reference fixture, so every test records min |p - alpha| and counts
- * tests with |p - alpha| < 1e-9 (a decision a different-but-accurate CDF could flip).  Covers every
- * test run on `c` since the last reset (creation resets; `reset` != 0 resets after reading). */
 /* Parity pinning of the production paths: counts of n tests (items [n][2+d], level-0 pairs x < y)
  * through the kernels a PC run uses at level d -- d = 0 the complete-graph level-0 batch (Gram of
  * the leading bit-sliced rows, every pair's table recorded), d = 1 the derived counting from those
  * recorded pair tables, d >= 2 the histogram kernel (2-bit packed columns at >= 64k samples) over
  * one batch.  counts [n][cap], Counts3D cell order (src/CellTable.cpp:277-281). */
 int fbn_ci_debug_counts(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, int32_t *counts, int64_t cap);
+/* Decision-margin log (SURVEY §8(c)): the p-value CDF (stats::pchisq, src/IndependenceTest.cpp:146,
+ * 268,355) is not pinned by any reference fixture, so every test records min |p - alpha| and counts
+ * tests with |p - alpha| < 1e-9 (a decision a different-but-accurate CDF could flip).  Covers every
+ * test run on `c` since the last reset (creation resets; `reset` != 0 resets after reading). */
 int fbn_ci_decision_margin(fbn_ci_ctx *c, double *min_margin, int64_t *near_alpha, int reset);
 int fbn_ci_ctx_destroy(fbn_ci_ctx *c);
 
@@ -246,9 +246,6 @@ int fbn_pc_num_edges(const fbn_pc_result *r, int *n);
 int fbn_pc_edges(const fbn_pc_result *r, int32_t *pairs /* [n][2], vec_edges order */);
 /* sepsets flattened as (x, y, k, z_0..z_{k-1})*, key x < y; returns total int count in *len */
 int fbn_pc_sepsets(const fbn_pc_result *r, int32_t *buf, int64_t cap, int64_t *len);
-/* After the skeleton, fbn_pc_stable orients like StructLearnByPCStable steps 2-3
- * (OrientVStructure / OrientImplied, src/PCStable.cpp:576-843): triples [n][3] =
- * (from, to, 1) for arcs, (min, max, 0) for undirected edges, in the reference's vec_edges order. */
 /* One skeleton level for the edge range [e_begin, e_end) of the current skeleton `edges`
  * ([nedges][2], x < y, lexicographic = the reference's vec_edges order): level 0 = one marginal test
  * per edge (src/PCStable.cpp:73-157), level d >= 1 = SearchAtDepth/CheckEdge over the adjacency
@@ -263,6 +260,9 @@ int fbn_pc_level(fbn_ci_ctx *c, double alpha, int d, int group_size, const int32
  * (records (x, y, m, z_0..z_{m-1}) as fbn_pc_sepsets writes them) into a new result. */
 int fbn_pc_orient_skeleton(int nvars, const int32_t *pairs, int nedges, const int32_t *sepsets, int64_t len,
                            fbn_pc_result **out);
+/* After the skeleton, fbn_pc_stable orients like StructLearnByPCStable steps 2-3
+ * (OrientVStructure / OrientImplied, src/PCStable.cpp:576-843): triples [n][3] =
+ * (from, to, 1) for arcs, (min, max, 0) for undirected edges, in the reference's vec_edges order. */
 int fbn_pc_num_oriented_edges(const fbn_pc_result *r, int *n);
 int fbn_pc_oriented_edges(const fbn_pc_result *r, int32_t *triples);
 /* SHD against the CPDAG of the DAG in a BIF file (BNSLComparison::GetSHD, src/BNSLComparison.cpp:12-121,
