@@ -87,16 +87,16 @@ class SepsetMap {
     // the entries near the last hit instead of a cold binary search over the whole run
     // (orientation's v-structure pass: ~1.7k lookups on a 1000-variable run)
     void find_many(const std::pair<int, int> *keys, size_t n, View *v, char *found) const {
-        std::vector<uint32_t> open(n);
-        for (size_t i = 0; i < n; ++i) open[i] = (uint32_t)i;
-        std::sort(open.begin(), open.end(), [&](uint32_t a, uint32_t b) { return keys[a] < keys[b]; });
-        size_t k = 0;
-        for (uint32_t q : open) {
+        // the level-0 flags first (most keys of a PC run end there), then only the rest sorted
+        std::vector<uint32_t> open;
+        open.reserve(n);
+        for (size_t q = 0; q < n; ++q) {
             found[q] = l0_hit(keys[q]);
             if (found[q]) v[q] = View{pool_.data(), 0};
-            else open[k++] = q;
+            else open.push_back((uint32_t)q);
         }
-        open.resize(k);
+        std::sort(open.begin(), open.end(), [&](uint32_t a, uint32_t b) { return keys[a] < keys[b]; });
+        size_t k;
         size_t end = e_.size();
         for (size_t r = runs_.size() + 1; r-- > 0 && !open.empty();) {  // last run first, as find()
             const size_t begin = r ? runs_[r - 1] : 0;

@@ -129,14 +129,15 @@ def test_orientation_alarm_known_answer():
 
 
 def test_orientation_random_skeletons():
-    """Random skeletons and sepsets (cycles, conflicting v-structures, Rule 3's position indexing)."""
+    """Random skeletons and sepsets (cycles, conflicting v-structures, Rule 3's position indexing);
+    the dense trials give nodes more neighbours / parents than the node sets hold inline (6)."""
     import random
     import orient
     rng = random.Random(7)
-    for trial in range(60):
-        n = rng.randint(4, 14)
+    for trial in range(80):
+        n = rng.randint(4, 14) if trial < 60 else rng.randint(12, 16)
         pairs = [(a, b) for a in range(n) for b in range(a + 1, n)]
-        edges = [p for p in pairs if rng.random() < 0.35]
+        edges = [p for p in pairs if rng.random() < (0.35 if trial < 60 else 0.75)]
         sep = {}
         for p in pairs:
             if p not in edges:
