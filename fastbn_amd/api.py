@@ -1,5 +1,7 @@
 """ctypes binding of include/fastbn.h and the reference-shaped Python classes."""
+import atexit
 import ctypes as C
+import weakref
 import os
 
 import numpy as np
@@ -144,6 +146,49 @@ class _Lib:
 
 lib = _Lib()
 
+# Every live handle (networks, datasets, plans, CI contexts, results, sessions) is destroyed by an
+# atexit hook, before the interpreter's module teardown and before the HIP runtime's own exit
+# handlers: no fbn_* destroy ever runs from a finalizer racing those (or after `lib` is gone).
+# Destroy order: results and sessions, then plans and contexts (they drain their device work),
+# then host-only handles.
+_LIVE = weakref.WeakSet()
+_CLOSE_ORDER = {"PCResult": 0, "PCDistSession": 1, "JunctionTree": 2, "IndependenceTest": 3, "Dataset": 4,
+                "Network": 5}
+
+
+def _register(obj):
+    _LIVE.add(obj)
+
+
+def close_all():
+    """Destroy every live handle now (also run at interpreter exit)."""
+    objs = sorted(list(_LIVE), key=lambda o: _CLOSE_ORDER.get(type(o).__name__, 9))
+    for o in objs:
+        try:
+            o.close()
+        except Exception:  # noqa: BLE001 (exit path: keep closing the rest)
+            pass
+
+
+atexit.register(close_all)
+
+
+class _Handle:
+    """A libfastbn handle: `_h`, destroyed once by close() (explicitly, by __del__, or at exit)."""
+    _destroy = None
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._h = None
+            getattr(lib, self._destroy)(h)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 (finalizer)
+            pass
+
 
 def _p(a):
     return None if a is None else a.ctypes.data
@@ -167,13 +212,15 @@ class _PlanInfo(C.Structure):
                 ("tiled_table_bytes", C.c_int64)]
 
 
-class Network:
+class Network(_Handle):
+    _destroy = "fbn_network_destroy"
     """Discrete BN loaded from XMLBIF (CustomNetwork::GetNetFromXMLBIFFile)."""
 
     def __init__(self, path):
         h = C.c_void_p()
         lib.fbn_network_load_xmlbif(os.fsencode(path), C.byref(h))
         self._h = h
+        _register(self)
         n = C.c_int()
         lib.fbn_network_num_nodes(h, C.byref(n))
         self.num_nodes = n.value
@@ -198,10 +245,6 @@ class Network:
         lib.fbn_synth_evidence(self._h, int(n), int(k), int(seed), int(query), _p(ev))
         return ev
 
-    def __del__(self):
-        if getattr(self, "_h", None):
-            lib.fbn_network_destroy(self._h)
-            self._h = None
 
 
 def write_csv(path, columns, network=None):
@@ -268,7 +311,8 @@ class Dataset:
         return self.columns.shape[1]
 
 
-class JunctionTree:
+class JunctionTree(_Handle):
+    _destroy = "fbn_jt_plan_destroy"
     """Batched JT inference on one device (JunctionTree ctor + PredictUseJTInfer over all cases)."""
 
     def __init__(self, network, device=0):
@@ -276,6 +320,7 @@ class JunctionTree:
         h = C.c_void_p()
         lib.fbn_jt_plan_create(network._h, device, C.byref(h))
         self._h = h
+        _register(self)
         info = _PlanInfo()
         lib.fbn_jt_plan_info_get(h, C.byref(info))
         self.info = {k: getattr(info, k) for k, _ in _PlanInfo._fields_}
@@ -410,13 +455,10 @@ class JunctionTree:
         mse, hd = self.score(marg, golden)
         return acc, mse / len(labels), hd / len(labels)
 
-    def __del__(self):
-        if getattr(self, "_h", None):
-            lib.fbn_jt_plan_destroy(self._h)
-            self._h = None
 
 
-class IndependenceTest:
+class IndependenceTest(_Handle):
+    _destroy = "fbn_ci_ctx_destroy"
     """G^2 tests on the device (IndependenceTest::IndependenceResult, batched)."""
 
     def __init__(self, dataset, alpha=0.05, device=0):
@@ -426,6 +468,7 @@ class IndependenceTest:
         lib.fbn_ci_dataset_upload(_p(dataset.columns), dataset.num_vars, dataset.num_instance,
                                   _p(dataset.dims), device, C.byref(h))
         self._h = h
+        _register(self)
 
     @classmethod
     def from_device(cls, d_cols_ptr, nvars, nsamples, dims, alpha=0.05, device=0):
@@ -439,6 +482,7 @@ class IndependenceTest:
         lib.fbn_ci_dataset_from_device(C.c_void_p(d_cols_ptr), int(nvars), int(nsamples), _p(dims), device,
                                        C.byref(h))
         self._h = h
+        _register(self)
         return self
 
     def set_kernel_timing(self, enable):
@@ -505,17 +549,15 @@ class IndependenceTest:
         lib.fbn_ci_last_kernel_ms(self._h, C.byref(ms))
         return ms.value
 
-    def __del__(self):
-        if getattr(self, "_h", None):
-            lib.fbn_ci_ctx_destroy(self._h)
-            self._h = None
 
 
-class PCResult:
+class PCResult(_Handle):
+    _destroy = "fbn_pc_result_destroy"
     """A PC-stable result handle: skeleton, sepsets, orientation, SHD (fbn_pc_*)."""
 
     def __init__(self, handle):
         self._h = handle
+        _register(self)
         self._edges = self._sepset = self._oriented = None
         m, near = C.c_double(), C.c_int64()
         lib.fbn_pc_decision_margin(handle, C.byref(m), C.byref(near))
@@ -590,10 +632,6 @@ class PCResult:
         lib.fbn_pc_shd_bif(self._h, os.fsencode(bif_path), C.byref(shd))
         return shd.value
 
-    def __del__(self):
-        if getattr(self, "_h", None):
-            lib.fbn_pc_result_destroy(self._h)
-            self._h = None
 
 
 def shd_bif(bif_path, nvars, oriented):

@@ -173,13 +173,17 @@ struct fbn_jt_plan {
     int device = 0, num_cu = 0, waves_per_cu = 0, variant = -1, last_variant = -1;
     // plan-specialized kernel (variant 3)
     bool gen_eligible = false;
-    int gen_state = 0;  // 0 not tried, 1 loaded, -1 failed
-    bool gen_fast = false;  // arithmetic order of the loaded specialized kernel
+    // one loaded module (and initial-potential buffer) per arithmetic order, [0] exact, [1] fast:
+    // switching the order never unloads a module or rewrites a buffer a queued run may still use
+    struct GenKernel {
+        int state = 0;  // 0 not tried, 1 loaded, -1 failed
+        hipModule_t mod = nullptr;
+        hipFunction_t fn = nullptr;
+        int64_t we = 0, lds = 0;
+        DevBuf iv;
+    } gen[2];
     int64_t last_nblk = 0;  // 64-case blocks of the last run (flags of variants 3-5)
-    hipModule_t gen_mod = nullptr;
-    hipFunction_t gen_fn = nullptr;
-    int64_t gen_we = 0, gen_lds = 0;
-    DevBuf flags, ws_fix, gen_iv;
+    DevBuf flags, ws_fix;
     bool force_fixup = false;
     // arithmetic order of the specialized / streamed kernels: 1 = the reference's (bit-identical),
     // 0 = fast (normalizations that cancel left out, within 1e-12), -1 = auto (fast)
@@ -195,7 +199,8 @@ struct fbn_jt_plan {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     ~fbn_jt_plan() {
-        if (gen_mod) (void)hipModuleUnload(gen_mod);
+        for (auto &k : gen)
+            if (k.mod) (void)hipModuleUnload(k.mod);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
     }
@@ -739,28 +744,26 @@ int fbn_jt_set_variant(fbn_jt_plan *p, int variant) {
     return FBN_OK;
 }
 
-// load (cache) or compile (hiprtc) the plan-specialized kernel once per plan
+// the plan-specialized kernel of the current arithmetic order, loaded (cache) or compiled (hiprtc)
+// once per plan and order; both orders stay loaded
+static fbn_jt_plan::GenKernel &GenCur(fbn_jt_plan *p) { return p->gen[JtFast(p) ? 1 : 0]; }
 static int GenEnsure(fbn_jt_plan *p) {
     const bool fast = JtFast(p);
-    if (p->gen_state != 0 && p->gen_fast != fast) {  // the other arithmetic order was loaded (or failed)
-        if (p->gen_mod) (void)hipModuleUnload(p->gen_mod);
-        p->gen_mod = nullptr, p->gen_fn = nullptr, p->gen_state = 0;
-    }
-    if (p->gen_state == 1) return FBN_OK;
-    if (p->gen_state == -1) return FBN_ERR_HIP;
-    p->gen_state = -1;
-    p->gen_fast = fast;
+    auto &k = GenCur(p);
+    if (k.state == 1) return FBN_OK;
+    if (k.state == -1) return FBN_ERR_HIP;
+    k.state = -1;
     std::string src;
     std::vector<double> iv;
-    int rc = fbn::GenerateJTKernel(p->host, src, &p->gen_we, iv, &p->gen_lds, fast);
+    int rc = fbn::GenerateJTKernel(p->host, src, &k.we, iv, &k.lds, fast);
     if (rc) return rc;
     std::vector<char> code;
     if ((rc = fbn::JitCodeObject(src, code))) return rc;
-    FBN_HIP(hipModuleLoadData(&p->gen_mod, code.data()));
-    FBN_HIP(hipModuleGetFunction(&p->gen_fn, p->gen_mod, "fbn_jt_gen"));
-    if ((rc = p->gen_iv.ensure(std::max<size_t>(iv.size() * 8, 8)))) return rc;
-    FBN_HIP(hipMemcpy(p->gen_iv.p, iv.data(), iv.size() * 8, hipMemcpyHostToDevice));
-    p->gen_state = 1;
+    FBN_HIP(hipModuleLoadData(&k.mod, code.data()));
+    FBN_HIP(hipModuleGetFunction(&k.fn, k.mod, "fbn_jt_gen"));
+    if ((rc = k.iv.ensure(std::max<size_t>(iv.size() * 8, 8)))) return rc;
+    FBN_HIP(hipMemcpy(k.iv.p, iv.data(), iv.size() * 8, hipMemcpyHostToDevice));  // (a new buffer: no run uses it yet)
+    k.state = 1;
     return FBN_OK;
 }
 
@@ -1071,10 +1074,11 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
             return rc;
     } else if (variant == 3) {
         // one wave (64 cases) per SIMD: the clique in flight occupies the register file (+ LDS tail)
+        const auto &gk = GenCur(p);
         int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 4;
-        if (p->gen_lds > 0) wpc = std::max<int>(1, std::min<int64_t>(wpc, (int64_t)kLdsBytes / p->gen_lds));
+        if (gk.lds > 0) wpc = std::max<int>(1, std::min<int64_t>(wpc, (int64_t)kLdsBytes / gk.lds));
         const int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * wpc);
-        if ((rc = p->ws.ensure((size_t)grid * p->gen_we * 64 * 8))) return rc;
+        if ((rc = p->ws.ensure((size_t)grid * gk.we * 64 * 8))) return rc;
         if ((rc = p->flags.ensure((size_t)nblk * 4))) return rc;
         FBN_HIP(hipEventRecord(p->ev0, s));
 
@@ -1082,7 +1086,7 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
         double *a_marg = marg, *a_ws = p->ws.as<double>();
         int32_t *a_lab = labels;
         int *a_flags = p->flags.as<int>();
-        const double *a_iv = p->gen_iv.as<double>();
+        const double *a_iv = gk.iv.as<double>();
         long long a_n = ncases;
         unsigned long long *a_prof = nullptr;
         if (p->prof_on) {  // diagnostic: only kernels generated with FBN_JT_PROFILE=1 write it
@@ -1092,7 +1096,7 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
             a_prof = p->prof.as<unsigned long long>();
         }
         void *args[] = {&a_ev, &a_marg, &a_lab, &a_ws, &a_flags, &a_iv, &a_n, &a_prof};
-        FBN_HIP(hipModuleLaunchKernel(p->gen_fn, grid, 1, 1, 64, 1, 1, (unsigned)p->gen_lds, s, args, nullptr));
+        FBN_HIP(hipModuleLaunchKernel(gk.fn, grid, 1, 1, 64, 1, 1, (unsigned)gk.lds, s, args, nullptr));
         if (p->force_fixup) FBN_HIP(hipMemsetAsync(p->flags.p, 1, (size_t)nblk * 4, s));  // testing only
         // exact recomputation of the blocks whose denominators left the fast-division range
         if ((rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s))) return rc;
@@ -1173,7 +1177,11 @@ int fbn_jt_last_kernel_ms(const fbn_jt_plan *p, float *ms) {
 }
 
 int fbn_jt_plan_destroy(fbn_jt_plan *p) {
-    if (p && p->device >= 0) (void)hipSetDevice(p->device);
+    if (!p) return FBN_OK;
+    if (p->device >= 0) {  // runs are queued on caller streams: drain them before the buffers go
+        (void)hipSetDevice(p->device);
+        (void)hipDeviceSynchronize();
+    }
     delete p;
     return FBN_OK;
 }
@@ -1899,7 +1907,12 @@ int fbn_ci_last_kernel_ms(const fbn_ci_ctx *c, float *ms) {
 }
 
 int fbn_ci_ctx_destroy(fbn_ci_ctx *c) {
-    if (c) (void)hipSetDevice(c->device);
+    if (!c) return FBN_OK;
+    // nothing of this ctx may still run when its buffers, pinned records and stream go: the device-
+    // resident search returns on its completion word, and batches may be queued on caller streams
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    (void)hipDeviceSynchronize();
     delete c;
     return FBN_OK;
 }

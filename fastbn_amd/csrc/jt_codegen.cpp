@@ -323,11 +323,13 @@ void JTGen::Marg(const std::string &P, int c) {
         }
         o << "          const double yt = 1.0 / tot; bad |= den_bad(tot);\n";
         if (v == 0) {
-            o << "          if (ACT) { int lab = 0; double mp = 0.0;";
+            // (fast order: a near-tie, top two within 1e-12 relative, may break differently from the
+            // reference's exact values -- the block is flagged for the exact pass)
+            o << "          if (ACT) { int lab = 0; double mp = 0.0, m2 = 0.0;";
             for (int d = 0; d < dim; ++d)
-                o << " { const double q = (b == 1) ? p" << d << " : dv(p" << d << ", tot, yt); if (q > mp) { mp = q; lab = " << d
-                  << "; } }";
-            o << " labels[CS] = lab; }\n";
+                o << " { const double q = (b == 1) ? p" << d << " : dv(p" << d << ", tot, yt); if (q > mp) { m2 = mp; mp = q; lab = " << d
+                  << "; } else if (q > m2) m2 = q; }";
+            o << " labels[CS] = lab;" << (fast ? " bad |= (mp - m2 <= 1e-12 * mp) ? 1u : 0u;" : "") << " }\n";
         }
         o << "          if (ACT) {";
         for (int d = 0; d < dim; ++d) o << " OUT(" << out_off[v] + d << ") = dv(p" << d << ", tot, yt);";

@@ -105,7 +105,8 @@ struct JtVClique {
 #define JT_T_C 16           // cases per wave: a message row is JT_T_C fp64 = 128 B, one cache line
 #define JT_T_L 4            // entry slots per case (JT_T_C * JT_T_L = 64 lanes)
 #define JT_T_MAXF 7         // factors per pass: <= 6 child messages + the parent message
-#define JT_T_MAXDIM 8       // state counts of the variables (marginal sweep: value d in slot d % JT_T_L)
+#define JT_T_MAXDIM 128     // state counts of the variables (int8 evidence codes; marginal sweep in
+                            // groups of 8 values, value d in slot d % JT_T_L)
 #define JT_T_LDS_BIN_ROWS 16  // a pass's partial bins live in LDS when they are at most this many rows
 #define JT_T_W 4            // most waves per workgroup: they share one case group, its message store and
                             // its LDS factor stage, and split every pass (rounds or outer configurations);

@@ -35,9 +35,11 @@ namespace {
 
 constexpr int C = JT_T_C, L = JT_T_L, kMaxW = JT_T_W;
 static_assert(C * L == 64, "one wave = C cases x L slots");
-constexpr int kValChunks = (JT_T_MAXDIM + L - 1) / L;  // marginal sweep: value d in slot d % L, chunk d / L
+constexpr int kValChunks = 2;  // marginal sweep: value d in slot d % L, chunk (d % kGrp) / L
+constexpr int kGrp = kValChunks * L;  // values per bin sweep (more states: one sweep per group)
 constexpr int kBinRows = JT_T_LDS_BIN_ROWS;  // bin sets up to this many rows live in LDS
-constexpr int kMaxCliqueVars = 10;           // (32 digit bits of >= 2-state variables, jt_tile_plan.cpp)
+constexpr int kMaxCliqueVars = 10;           // evidence bytes loaded together; wider cliques (up to 32
+                                             // digit bits, jt_tile_plan.cpp) take the rest in a loop
 
 typedef __attribute__((ext_vector_type(2))) unsigned u2;
 
@@ -309,6 +311,10 @@ __global__ __launch_bounds__(64 * kMaxW, 16 / kMaxW) void jt_tile_kernel(const J
 #pragma unroll
                 for (int j = 0; j < kMaxCliqueVars; ++j)
                     if (xs[j] >= 0) M |= (uint32_t)vr[3 * j + 2] << vr[3 * j + 1], Wd |= (uint32_t)xs[j] << vr[3 * j + 1];
+                for (int j = kMaxCliqueVars; j < P.nv; ++j) {  // (wider cliques: the rest one at a time)
+                    const int x = ev[vr[3 * j]];
+                    if (x >= 0) M |= (uint32_t)vr[3 * j + 2] << vr[3 * j + 1], Wd |= (uint32_t)x << vr[3 * j + 1];
+                }
                 // the clique's LDS factors, staged by the whole workgroup (every wave is past the last
                 // pass barrier, after which no wave reads the previous phase's factors)
                 for (int k = 0; k < P.nstage; ++k) {
@@ -406,61 +412,83 @@ __global__ __launch_bounds__(64 * kMaxW, 16 / kMaxW) void jt_tile_kernel(const J
             }
             // marginals whose source is this pass (wave m % W): value d of the variable in slot d % L
             // (chunk d / L), summed over the bins in bin order, normalized by their total (evidence
-            // variables: zeros)
+            // variables: zeros).  Variables of more than kGrp states: one bin sweep per group of kGrp
+            // values, the total from a first sweep over all bins
             for (int m = wv; m < P.nmv; m += W) {
                 const int32_t *__restrict__ mr = tab + P.mv_off + 5 * m;
                 const int var = mr[0], off = mr[1], dim = mr[2], sh = mr[3];
                 const uint32_t fm = (uint32_t)mr[4];
                 const bool obs = ev[var] >= 0;
                 const bool need = need_entries && __ballot(act && !obs) != 0ull;
-                double a[kValChunks];
+                const int32_t *__restrict__ bd = tab + P.bdig_off;
+                const int nb = P.nbins;
+                // bin values: old(b) U(b) (Distribute: the calibrated separator up to a per-case
+                // constant), U(b) (private variables)
+                auto bins4 = [&](int b0, double *v) {
 #pragma unroll
-                for (int c = 0; c < kValChunks; ++c) a[c] = 0.0;
-                if (need) {
-                    // bin values: old(b) U(b) (Distribute: the calibrated separator up to a per-case
-                    // constant), U(b) (private variables)
-                    const int32_t *__restrict__ bd = tab + P.bdig_off;
-                    const int nb = P.nbins;
+                    for (int t = 0; t < 4; ++t) {
+                        const int bc = b0 + t < nb ? b0 + t : nb - 1;
+                        const int o8 = bc * (C * 8) + g8;
+                        if (marg_pass) v[t] = O.out_lds ? *reinterpret_cast<const double *>(ldsb + O.out_b + o8)
+                                                        : bld(st, O.out_b + o8, 0);
+                        else v[t] = bld(st, P.col_row * (C * 8) + o8, 0) * bld(st, O.out_b + o8, 0);
+                    }
+                };
+                double tm = 0.0;
+                if (need && dim > kGrp)
                     for (int b0 = 0; b0 < nb; b0 += 4) {
                         double v[4];
+                        bins4(b0, v);
 #pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            const int bc = b0 + t < nb ? b0 + t : nb - 1;
-                            const int o8 = bc * (C * 8) + g8;
-                            if (marg_pass) v[t] = O.out_lds ? *reinterpret_cast<const double *>(ldsb + O.out_b + o8)
-                                                            : bld(st, O.out_b + o8, 0);
-                            else v[t] = bld(st, P.col_row * (C * 8) + o8, 0) * bld(st, O.out_b + o8, 0);
-                        }
+                        for (int t = 0; t < 4; ++t)
+                            if (b0 + t < nb) tm += v[t];
+                    }
+                int lab = 0;
+                double mx = 0.0, m2 = 0.0;
+                for (int q0 = 0; q0 < dim; q0 += kGrp) {
+                    double a[kValChunks];
 #pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            if (b0 + t >= nb) break;
-                            const int dg = (int)(((uint32_t)bd[b0 + t] >> sh) & fm);
+                    for (int c = 0; c < kValChunks; ++c) a[c] = 0.0;
+                    if (need) {
+                        for (int b0 = 0; b0 < nb; b0 += 4) {
+                            double v[4];
+                            bins4(b0, v);
 #pragma unroll
-                            for (int c = 0; c < kValChunks; ++c) a[c] += dg == c * L + s ? v[t] : 0.0;
+                            for (int t = 0; t < 4; ++t) {
+                                if (b0 + t >= nb) break;
+                                const int dg = (int)(((uint32_t)bd[b0 + t] >> sh) & fm) - q0;
+#pragma unroll
+                                for (int c = 0; c < kValChunks; ++c) a[c] += dg == c * L + s ? v[t] : 0.0;
+                            }
                         }
                     }
+                    if (dim <= kGrp) {  // the lane's values in chunk order, then the slot butterfly
+                        double am = 0.0;
+#pragma unroll
+                        for (int c = 0; c < kValChunks; ++c) am += a[c];
+                        tm = slot_sum(am);
+                    }
+#pragma unroll
+                    for (int c = 0; c < kValChunks; ++c)
+                        if (act && q0 + c * L + s < dim) out[off + q0 + c * L + s] = obs ? 0.0 : a[c] / tm;
+                    if (var == 0 && need)  // label: ArgMax, strict '>' from 0 (src/Inference.cpp:92-102)
+                        for (int d = q0; d < dim && d < q0 + kGrp; ++d) {
+                            double ad = 0.0;
+#pragma unroll
+                            for (int c = 0; c < kValChunks; ++c) {
+                                const double t = __shfl(a[c], (d % L) * C + g);
+                                ad = (d - q0) / L == c ? t : ad;
+                            }
+                            const double pd = ad / tm;
+                            if (pd > mx) m2 = mx, mx = pd, lab = d;
+                            else if (pd > m2) m2 = pd;
+                        }
                 }
-                double am = 0.0;  // the lane's values in chunk order, then the slot butterfly
-#pragma unroll
-                for (int c = 0; c < kValChunks; ++c) am += a[c];
-                const double tm = slot_sum(am);
-#pragma unroll
-                for (int c = 0; c < kValChunks; ++c)
-                    if (act && c * L + s < dim) out[off + c * L + s] = obs ? 0.0 : a[c] / tm;
-                if (var == 0 && need) {  // label: ArgMax, strict '>' from 0 (src/Inference.cpp:92-102)
-                    int lab = 0;
-                    double mx = 0.0;
-                    for (int d = 0; d < dim; ++d) {
-                        double ad = 0.0;
-#pragma unroll
-                        for (int c = 0; c < kValChunks; ++c) {
-                            const double t = __shfl(a[c], (d % L) * C + g);
-                            ad = d / L == c ? t : ad;
-                        }
-                        const double pd = ad / tm;
-                        if (pd > mx) mx = pd, lab = d;
-                    }
+                if (var == 0 && need) {
                     if (act && !obs && s == 0) labels[cs] = lab;
+                    // a near-tie (top two within 1e-12 relative) may break differently from the
+                    // reference's exact values: the block goes to the exact pass
+                    bad |= act && !obs && mx - m2 <= 1e-12 * mx;
                 }
             }
             if (prof) pc[5] += dclock() - t0;

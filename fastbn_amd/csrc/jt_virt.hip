@@ -38,6 +38,10 @@ struct Den {
     double den, y;
 };
 constexpr int kVFast = 1 << 12;  // launch flag (dbg word): one-pass Collect denominators (vsum_all)
+// fast order: a label whose top two normalized values are within 1e-12 (relative) of each other
+// may differ from the reference's ArgMax (strict '>' from 0, src/Inference.cpp:92-102), so its
+// block is flagged and recomputed by the exact pass
+__device__ __forceinline__ bool near_tie(double mx, double m2) { return mx - m2 <= 1e-12 * mx; }
 __device__ __forceinline__ double mdiv(double x, const Den &d) {
     const double q = x * d.y;
     const double r = __builtin_fma(-d.den, q, x);
@@ -714,12 +718,14 @@ void jt_virt_kernel(
                 if (wr) {
                     if (var == 0) {  // label: ArgMax, strict '>' from 0 (src/Inference.cpp:92-102)
                         int lab = 0;
-                        double mx = 0.0;
+                        double mx = 0.0, m2 = 0.0;
                         for (int d = 0; d < dim; ++d) {
                             const double p = (best == 1) ? o[d] : o[d] / tot;
-                            if (p > mx) mx = p, lab = d;
+                            if (p > mx) m2 = mx, mx = p, lab = d;
+                            else if (p > m2) m2 = p;
                         }
                         labels[cs] = lab;
+                        bad |= fast && near_tie(mx, m2);
                     }
                     for (int d = 0; d < dim; ++d) o[d] = o[d] / tot;
                 }
@@ -758,12 +764,14 @@ void jt_virt_kernel(
                 if (wr) {
                     if (var == 0) {  // label: ArgMax, strict '>' from 0 (src/Inference.cpp:92-102)
                         int lab = 0;
-                        double mx = 0.0;
+                        double mx = 0.0, m2 = 0.0;
                         for (int d = 0; d < dim; ++d) {
                             const double p = (best == 1) ? o[d] : o[d] / tot;
-                            if (p > mx) mx = p, lab = d;
+                            if (p > mx) m2 = mx, mx = p, lab = d;
+                            else if (p > m2) m2 = p;
                         }
                         labels[cs] = lab;
+                        bad |= fast && near_tie(mx, m2);
                     }
                     for (int d = 0; d < dim; ++d) o[d] = o[d] / tot;
                 }

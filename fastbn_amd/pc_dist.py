@@ -17,13 +17,15 @@ import numpy as np
 from . import api
 
 
-class PCDistSession:
+class PCDistSession(api._Handle):
     """One rank's view of a distributed PC-stable skeleton search (fbn_pc_dist_*)."""
+    _destroy = "fbn_pc_dist_destroy"
 
     def __init__(self, nvars, alpha=0.05, depth=1000, group_size=1):
         h = C.c_void_p()
         api.lib.fbn_pc_dist_create(int(nvars), float(alpha), int(depth), int(group_size), C.byref(h))
         self._h, self.nvars = h, int(nvars)
+        api._register(self)
 
     def level(self, world, rank):
         """Partition of the current level -> (d, e_begin, e_end, record_len), or None when done."""
@@ -78,11 +80,6 @@ class PCDistSession:
         r = C.c_void_p()
         api.lib.fbn_pc_dist_result(self._h, C.byref(r))
         return api.PCResult.with_levels(r)
-
-    def __del__(self):
-        if getattr(self, "_h", None):
-            api.lib.fbn_pc_dist_destroy(self._h)
-            self._h = None
 
 
 def _world_rank():

@@ -32,6 +32,26 @@ def prebuild(xml_paths):
     return out
 
 
-def prebuild_default():
+def fixture_xmls(dirname):
+    """The XMLBIF fixtures of the GPU tests (tests/golden/synth_nets/*.xml.gz), unpacked."""
+    import glob
+    import gzip
+    out = []
+    for gz in sorted(glob.glob(os.path.join(REPO, "tests", "golden", "synth_nets", "*.xml.gz"))):
+        path = os.path.join(dirname, os.path.basename(gz)[:-3])
+        with gzip.open(gz, "rb") as f, open(path, "wb") as g:
+            g.write(f.read())
+        out.append(path)
+    return out
+
+
+def prebuild_default(clean=True):
+    """Every eligible benchmark / test network, both orders; clean: drop code objects of older
+    generator versions first (their source hash no longer matches any plan)."""
+    if clean:
+        kdir = os.path.join(REPO, "fastbn_amd", "kcache")
+        for f in os.listdir(kdir) if os.path.isdir(kdir) else []:
+            if f.endswith(".hsaco"):
+                os.remove(os.path.join(kdir, f))
     with tempfile.TemporaryDirectory() as d:
-        return prebuild([ALARM_XML, synth_small_xml(d)])
+        return prebuild([ALARM_XML, synth_small_xml(d)] + fixture_xmls(d))

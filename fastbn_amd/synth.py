@@ -103,12 +103,14 @@ def evidence_cases(net, n, k, seed, query=0):
 
 
 def random_network(n_nodes, seed, window=12, parent_probs=(0.8, 0.15, 0.05), dom=(2, 5), path=None,
-                   name="synthetic", k_min=1):
+                   name="synthetic", k_min=1, fan_in=None):
     """Random DAG over nodes 0..n-1: node i > 0 draws k parents from the previous `window` nodes,
     P(k = k_min, k_min + 1, ...) = parent_probs (default: k >= 1, mean 1.25 parents per node, i.e.
     ~1300 arcs at 1041 nodes like Munin3).  k_min = 1 keeps the DAG connected, which the JT path
     needs: the reference's Prim step has no junction-forest support
-    (src/JunctionTreeStructure.cpp:262-281); the PC datasets use k_min = 0."""
+    (src/JunctionTreeStructure.cpp:262-281); the PC datasets use k_min = 0.
+    fan_in = {node: k}: those nodes draw exactly k parents (wide cliques for tests; every other
+    node's draw is unchanged)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     dims = rng.integers(dom[0], dom[1] + 1, size=n_nodes)
     pp = np.asarray(parent_probs, float) / np.sum(parent_probs)
@@ -116,6 +118,8 @@ def random_network(n_nodes, seed, window=12, parent_probs=(0.8, 0.15, 0.05), dom
     for i in range(n_nodes):
         lo = max(0, i - window)
         k = min(int(rng.choice(np.arange(k_min, k_min + pp.size), p=pp)), i - lo) if i > 0 else 0
+        if fan_in and i in fan_in:
+            k = min(int(fan_in[i]), i - lo)
         ps = sorted(rng.choice(np.arange(lo, i), size=k, replace=False).tolist()) if k else []
         parents.append(ps)
     cpts = []

@@ -217,3 +217,90 @@ def parse_plan(path):
 # maximum-weight spanning trees over the same cliques; message order then differs on the tied
 # branches, so the marginals agree to a few ulp, labels exactly.
 MUNIN_REF_RTOL = 1e-12
+
+
+# ---- seeded networks beyond ALARM / Munin-like: state counts up to 21 (the reference's own networks
+# -- Hailfinder, Diabetes, Munin -- have such variables), a 12-variable clique, and symmetric CPTs
+# whose query marginals tie.  Fixtures: tests/golden/make_golden_synth.py synth_nets (the reference's
+# own labels and marginals, oracle/_ref/ref_dump jt).
+SYNTH_NETS = os.path.join(GOLD, "synth_nets")
+SYNTH_NET_SPECS = {
+    "bigdom": dict(n_nodes=120, seed=21, window=6, parent_probs=(0.75, 0.25), dom=(2, 21)),
+    "wide": dict(n_nodes=48, seed=11, window=12, parent_probs=(0.85, 0.15), dom=(2, 2), fan_in={14: 11, 30: 6}),
+}
+# evidence cases per fixture: (cases, observed variables, seed) blocks
+SYNTH_NET_CASES = {"bigdom": [(16, 0, 5), (16, 24, 6), (16, 60, 7)],
+                   "wide": [(24, 10, 8), (24, 30, 9), (16, 47, 10)],
+                   "tie": [(32, 4, 11), (32, 8, 12)]}
+
+
+def tie_network(path, n_sym=8, n_extra=40, seed=3):
+    """Query X0 (binary, 0.5 / 0.5) with n_sym binary children whose CPTs are symmetric under
+    swapping X0's values (P(c | X0 = 0) = (a, b), P(c | X0 = 1) = (b, a)), so X0's posterior ties
+    exactly whenever as many observed children are 0 as 1 (and with none observed); plus n_extra
+    seeded nodes hanging off the children (a larger tree).  Written as XMLBIF (node-major TABLE)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    n = 1 + n_sym + n_extra
+    parents, tables = [[]], [[0.5, 0.5]]
+    for i in range(1, 1 + n_sym):
+        parents.append([0])
+        tables.append([0.3, 0.7, 0.7, 0.3])  # node-major: [value][X0]
+    for i in range(1 + n_sym, n):
+        p = int(rng.integers(1, i))
+        parents.append([p])
+        rows = np.round(rng.dirichlet(np.ones(2), size=2), 4)  # [parent value][value]
+        tables.append(rows.T.reshape(-1).tolist())
+    with open(path, "w") as f:
+        f.write('<?xml version="1.0" encoding="UTF-8"?>\n<BIF>\n<NETWORK>\n<NAME>tie</NAME>\n')
+        for i in range(n):
+            f.write("<VARIABLE>\n<NAME>X%d</NAME>\n<TYPE>discrete</TYPE>\n<VALUE>s0</VALUE>\n<VALUE>s1</VALUE>\n"
+                    "</VARIABLE>\n" % i)
+        for i in range(n):
+            f.write("<PROBABILITY>\n<FOR>X%d</FOR>\n" % i)
+            for q in parents[i]:
+                f.write("<GIVEN>X%d</GIVEN>\n" % q)
+            f.write("<TABLE>%s </TABLE>\n</PROBABILITY>\n" % " ".join("%.4f" % x for x in tables[i]))
+        f.write("</NETWORK>\n</BIF>\n")
+    return path
+
+
+def synth_net_xml(name, path):
+    from fastbn_amd import synth
+    if name == "tie":
+        return tie_network(path)
+    synth.random_network(path=path, name=name, **SYNTH_NET_SPECS[name])
+    return path
+
+
+def synth_net_cases(name, xml):
+    """The fixture's evidence cases (int8 [n][V]); tie: only X1..X8 observed (balanced counts tie)."""
+    from fastbn_amd import synth
+    net = synth.read_xmlbif(xml)
+    if name == "tie":
+        rng = np.random.Generator(np.random.PCG64(77))
+        blocks = []
+        for n, k, seed in SYNTH_NET_CASES[name]:
+            ev = np.full((n, len(net[1])), -1, np.int8)
+            for r in range(n):
+                vs = rng.choice(np.arange(1, 9), size=min(k, 8) if r % 4 else r % 3 * 2, replace=False)
+                ev[r, vs] = rng.integers(0, 2, size=vs.size)
+            blocks.append(ev)
+        return np.concatenate(blocks)
+    return np.concatenate([synth.evidence_cases(net, n, k, seed=seed) for n, k, seed in SYNTH_NET_CASES[name]])
+
+
+@pytest.fixture(scope="session")
+def synth_nets(tmp_path_factory):
+    """name -> {xml, ev, labels, marg} of the reference's own outputs (tests/golden/synth_nets)."""
+    d = tmp_path_factory.mktemp("synth_nets")
+    out = {}
+    for name in ("bigdom", "wide", "tie"):
+        xml = str(d / (name + ".xml"))
+        with gzip.open(os.path.join(SYNTH_NETS, name + ".xml.gz"), "rb") as f, open(xml, "wb") as g:
+            g.write(f.read())
+        ev = np.load(os.path.join(SYNTH_NETS, name + ".ev.npy"))
+        from fastbn_amd import synth
+        dims = synth.read_xmlbif(xml)[1]
+        lab, marg, _, _ = read_ref_marg(os.path.join(SYNTH_NETS, name + ".ref.marg.gz"), dims)
+        out[name] = {"xml": xml, "ev": ev, "labels": lab, "marg": marg, "dims": dims}
+    return out

@@ -9,6 +9,9 @@ TEST INFRASTRUCTURE -- runs in the build container.
                 reference JunctionTree compiled in place): per-case label + 17-digit marginals
                 (ref.marg.gz) and the reference's junction-tree plan (ref.plan.gz).
   pc_c5.ci.gz   config 5: the reference's own Counts2D / Counts3D tables (pc_c5_ci below)
+  synth_nets/   networks beyond ALARM / Munin-like (tests/conftest.py SYNTH_NET_SPECS, tie_network):
+                state counts up to 21, a 12-variable clique, symmetric CPTs whose query marginals
+                tie; seeded evidence cases (.ev.npy) and the reference's own labels + marginals
   pc_c5.json    config 5: PC-stable (depth 6, alpha 0.05) on the seeded 1000-variable x 100k-sample
                 dataset, run by the CPU restatement (oracle/pc_oracle.cpp; the reference's
                 PCStable/IndependenceTest cannot be compiled here: stats/gcem absent): tests per
@@ -204,8 +207,35 @@ def gram_ragged():
     print("gram_ragged.ci.gz: %d shapes x %d pairs" % (len(GRAM_SHAPES), GRAM_PAIRS))
 
 
+def synth_nets():
+    """synth_nets/<name>.{xml.gz, ev.npy, ref.marg.gz} for name in bigdom / wide / tie: the XMLBIF,
+    the evidence cases (conftest.synth_net_cases) and the UNMODIFIED reference's labels and 17-digit
+    marginals on them (oracle/_ref/ref_dump jt)."""
+    import numpy as np
+    from conftest import SYNTH_NETS, synth_net_cases, synth_net_xml
+    ref_dump = os.path.join(REPO, "oracle", "_ref", "ref_dump")
+    if not os.path.exists(ref_dump):
+        subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref"], check=True)
+    os.makedirs(SYNTH_NETS, exist_ok=True)
+    for name in ("bigdom", "wide", "tie"):
+        with tempfile.TemporaryDirectory() as td:
+            xml = synth_net_xml(name, os.path.join(td, name + ".xml"))
+            ev = synth_net_cases(name, xml)
+            lib = os.path.join(td, "ev.libsvm")
+            with open(lib, "w") as f:
+                for r in ev:
+                    f.write("0 " + " ".join(f"{v}:{r[v]}" for v in range(r.size) if r[v] >= 0) + " \n")
+            pre = os.path.join(td, "ref")
+            t0 = time.time()
+            subprocess.run([ref_dump, "jt", xml, lib, "-", pre, str(len(ev))], check=True, stdout=subprocess.DEVNULL)
+            gz_write(os.path.join(SYNTH_NETS, name + ".xml.gz"), open(xml, "rb").read())
+            np.save(os.path.join(SYNTH_NETS, name + ".ev.npy"), ev)
+            gz_write(os.path.join(SYNTH_NETS, name + ".ref.marg.gz"), open(pre + ".marg", "rb").read())
+            print("synth_nets/%s: %d cases, reference %.1f s" % (name, len(ev), time.time() - t0))
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["munin", "munin_extra", "c5", "c5ci", "gram"]
+    which = sys.argv[1:] or ["munin", "munin_extra", "c5", "c5ci", "gram", "synth_nets"]
     if "munin" in which:
         munin_like()
     if "munin_extra" in which:
@@ -216,3 +246,5 @@ if __name__ == "__main__":
         pc_c5_ci()
     if "gram" in which:
         gram_ragged()
+    if "synth_nets" in which:
+        synth_nets()

@@ -143,3 +143,42 @@ def test_multi_wave_case_groups(alarm, tmp_path, monkeypatch, tw):
     lab, marg = jt.infer(ev)
     assert jt.debug_flagged_blocks() == 0
     _check(lab, marg, *O.OracleJT(p).infer(ev), ev, jt.network.dims)
+
+
+@pytest.mark.parametrize("name", ["bigdom", "wide"])
+def test_synth_nets_default_path_vs_reference(synth_nets, name):
+    """Through the default path (auto: the tiled kernel, fast order): a network with state counts up
+    to 21 and one with a 12-variable clique (evidence on clique variables past the 10th), against the
+    reference's own labels and marginals (tests/golden/synth_nets; 1e-9 as for the Munin-like dumps:
+    bigdom's tree breaks Prim ties differently) and the oracle (1e-12); nothing flagged for the exact
+    pass unless a query marginal is a near-tie."""
+    fx = synth_nets[name]
+    jt = F.JunctionTree(F.Network(fx["xml"]), device=0)
+    lab, marg = jt.infer(fx["ev"])
+    assert jt.refresh_info()["variant"] == 5
+    np.testing.assert_array_equal(lab, fx["labels"])
+    np.testing.assert_allclose(marg, fx["marg"], rtol=1e-9, atol=1e-300)
+    _check(lab, marg, *O.OracleJT(fx["xml"]).infer(fx["ev"]), fx["ev"], fx["dims"])
+    # more cases, random evidence incl. every variable of the wide clique observed
+    net = synth.read_xmlbif(fx["xml"])
+    ev = synth.evidence_cases(net, 300, len(fx["dims"]) // 3, seed=99)
+    ev[:8] = synth.evidence_cases(net, 8, len(fx["dims"]) - 1, seed=98)
+    lab, marg = jt.infer(ev)
+    _check(lab, marg, *O.OracleJT(fx["xml"]).infer(ev), ev, fx["dims"])
+
+
+@pytest.mark.parametrize("variant", [None, 5, 4])
+def test_tied_query_marginals_label_like_reference(synth_nets, variant):
+    """Symmetric CPTs: X0's posterior ties exactly in 24 of the 64 fixture cases.  The fast arithmetic
+    order (default; kernels 3 / 5 / 4) flags a block whose top two query values are within 1e-12 and
+    the exact pass recomputes it, so labels equal the reference's ArgMax (strict '>' from 0) on every
+    tie (near-tie label stability)."""
+    fx = synth_nets["tie"]
+    jt = F.JunctionTree(F.Network(fx["xml"]), device=0)
+    if variant is not None:
+        jt.set_variant(variant)
+    lab, marg = jt.infer(fx["ev"])
+    assert jt.refresh_info()["variant"] == (variant if variant is not None else 3)
+    np.testing.assert_array_equal(lab, fx["labels"])
+    np.testing.assert_allclose(marg, fx["marg"], rtol=1e-12, atol=1e-300)
+    assert jt.debug_flagged_blocks() >= 1  # the ties went through the exact pass

@@ -124,3 +124,16 @@ def test_munin_like_extra_cases_vs_reference(munin_fixture):
     lab, marg = TE.run(prog, ev[pick], jt.info["sum_dom"])
     np.testing.assert_array_equal(lab, rlab[pick])
     np.testing.assert_allclose(marg, rmarg[pick], rtol=1e-9, atol=1e-300)
+
+
+def test_synth_nets_emulated_vs_reference(synth_nets):
+    """The tiled program of a network with state counts up to 21 (plan limit was 8) and of one with
+    a 12-variable clique (evidence on every clique variable, kernel loads past the 10th in a loop),
+    emulated on the host, against the reference's own labels and marginals (tests/golden/synth_nets)."""
+    for name, pick in (("bigdom", [0, 17, 40]), ("wide", list(range(0, 64, 5)))):
+        fx = synth_nets[name]
+        jt, prog = _prog(fx["xml"])
+        lab, marg = TE.run(prog, fx["ev"][pick], jt.info["sum_dom"])
+        np.testing.assert_array_equal(lab, fx["labels"][pick])
+        np.testing.assert_allclose(marg, fx["marg"][pick], rtol=1e-9, atol=1e-300)
+    assert max(synth_nets["bigdom"]["dims"]) == 21
