@@ -276,7 +276,11 @@ def pc_roofline(kernel_s, device_bytes, byte_column_bytes):
     the kernel time measured live (HIP events around every CI batch of a run)."""
     path = os.path.join(REPO, "profiles", "pc5_kernels.json")
     out = {"kernel_ms_per_run": 1e3 * kernel_s, "column_bytes_read_per_run": device_bytes,
-           "byte_column_model_bytes": byte_column_bytes}
+           "model": {"bytes_per_run": byte_column_bytes,
+                     "model_frac": byte_column_bytes / kernel_s / (HBM_PEAK_GBS * 1e9),
+                     "note": "informational: SURVEY 8(d)'s byte-column model (every test streams N (d + 2) "
+                             "uint8 bytes); the bit-sliced / FP4 kernels read packed masks from L2 instead, so "
+                             "this ratio is not a bound (it exceeds 1)"}}
     if not os.path.exists(path):
         return {"bound": None, **out}
     with open(path) as f:
@@ -635,25 +639,40 @@ VALU_PEAK_LANE_OPS = 256 * 4 * 16 * 2.4e9  # MI355X: CUs x SIMDs x lanes x clock
 
 
 def valu_roofline(which, cases, kernel_ms):
-    """Second roofline of a JT kernel: measured VALU instructions per launch (rocprofv3
-    SQ_INSTS_VALU, committed summary profiles/jt_valu.json from tools/pmc_valu.sh) scaled to this
-    launch, as wave64 lane-ops per second against the fp64 vector peak."""
-    path = os.path.join(REPO, "profiles", "jt_valu.json")
-    if not os.path.exists(path):
+    """The VALU roofline of a JT kernel: measured fp64 VALU instructions per launch (rocprofv3
+    SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64, committed summary profiles/r05/jt_valu.json from
+    tools/profile_r05.sh) scaled to this launch, as wave64 lane-ops per second against the fp64
+    vector peak (a wave64 fp64 instruction holds its SIMD 4 cycles, so frac <= 1 by construction);
+    all VALU instructions (SQ_INSTS_VALU, incl. 32-bit selects / integer ops) beside it."""
+    for path in (os.path.join(REPO, "profiles", "r05", "jt_valu.json"), os.path.join(REPO, "profiles", "jt_valu.json")):
+        if os.path.exists(path):
+            break
+    else:
         return None
     with open(path) as f:
         t = json.load(f)[which]
-    insts = t["valu_insts_per_launch"] * cases / t["cases_per_launch"]
-    ach = insts * 64 / (kernel_ms * 1e-3)
-    return {"bound": "valu", "achieved": ach / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12, "unit": "Tlane-op/s",
-            "frac": ach / VALU_PEAK_LANE_OPS, "valu_insts": insts}
+    sc = cases / t["cases_per_launch"]
+    insts = t["valu_insts_per_launch"] * sc
+    f64 = t.get("f64_insts_per_launch")
+    if f64 is None:  # (older profile: total VALU only)
+        ach = insts * 64 / (kernel_ms * 1e-3)
+        return {"bound": "valu", "achieved": ach / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12, "unit": "Tlane-op/s",
+                "frac": ach / VALU_PEAK_LANE_OPS, "valu_insts": insts, "source": os.path.relpath(path, REPO)}
+    f64 *= sc
+    ach = f64 * 64 / (kernel_ms * 1e-3)
+    return {"bound": "valu_f64", "achieved": ach / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12, "unit": "Tlane-op/s",
+            "frac": ach / VALU_PEAK_LANE_OPS, "f64_insts": f64, "valu_insts": insts,
+            "all_valu_frac": insts * 64 / (kernel_ms * 1e-3) / VALU_PEAK_LANE_OPS,
+            "source": os.path.relpath(path, REPO)}
 
 
 def load_traffic(cases):
     """Measured HBM bytes per launch (rocprofv3 FETCH_SIZE + WRITE_SIZE, calibrated; committed
-    summary profiles/jt_traffic.json from tools/pmc_traffic.sh), scaled to this launch's cases."""
-    path = os.path.join(REPO, "profiles", "jt_traffic.json")
-    if not os.path.exists(path):
+    summary profiles/r05/jt_traffic.json, else profiles/jt_traffic.json), scaled to this launch's cases."""
+    for path in (os.path.join(REPO, "profiles", "r05", "jt_traffic.json"), os.path.join(REPO, "profiles", "jt_traffic.json")):
+        if os.path.exists(path):
+            break
+    else:
         return None
     with open(path) as f:
         t = json.load(f)
@@ -661,12 +680,38 @@ def load_traffic(cases):
     return None if b is None else b * cases / t.get("cases_per_launch", CASES_PER_GPU)
 
 
+def alarm_roofline(info, cases, kernel_ms, traffic):
+    """The ALARM kernel's (fbn_jt_gen, variant 3) roofline against the bound it has:
+    it keeps every clique table in registers / LDS, so it moves only the compulsory bytes (evidence
+    in, marginals + labels out: V + 8 sum_dom + 4 B per case) plus the separator rows its per-wave
+    workspace spills past L2 (`traffic`, calibrated PMC), and at one wave per SIMD it is bound by the
+    issue of its fp64 VALU instructions: `frac` = fp64 VALU lane-ops / fp64 vector peak (<= 1 by
+    construction).  SURVEY 8(d)'s materialized-table bytes (every table written and read once) are
+    kept as `model`, informational: this design does not move them, so that ratio may exceed 1."""
+    comp = info["num_nodes"] + 8 * info["sum_dom"] + 4
+    t = kernel_ms * 1e-3
+    hbm = {"compulsory_bytes_per_case": comp, "achieved": comp * cases / t / 1e9, "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": comp * cases / t / 1e9 / HBM_PEAK_GBS, "traffic": traffic,
+           "traffic_achieved": traffic / t / 1e9 if traffic else None,
+           "traffic_frac": traffic / t / 1e9 / HBM_PEAK_GBS if traffic else None}
+    bpc = info["algorithmic_bytes_per_case"]
+    model = {"bytes_per_case": bpc, "achieved": bpc * cases / t / 1e9, "model_frac": bpc * cases / t / 1e9 / HBM_PEAK_GBS,
+             "note": "informational: SURVEY 8(d)'s materialized-table bytes, which this kernel does not move"}
+    v = valu_roofline("alarm", cases, kernel_ms)
+    base = {"kernel_ms": kernel_ms, "traffic": traffic, "hbm": hbm, "model": model}
+    if v is None:
+        return {"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": hbm["frac"], **base}
+    return {**v, **base, "note": "fp64 VALU issue at one wave per SIMD binds this kernel (DESIGN.md 5.1); "
+                                 "hbm: compulsory bytes and measured L2<->fabric traffic; model: informational"}
+
+
 def summary(out):
     """Every workload's headline number in a few hundred bytes (the end of the JSON line)."""
     def r(x, n=4):
         return None if x is None else float(f"{x:.{n}g}")
     sm = {"alarm_jt": {"cases_s": r(out["value"]), "kernel_ms": r(out["roofline"]["kernel_ms"]),
-                       "frac": r(out["roofline"]["frac"], 3)}}
+                       "frac": r(out["roofline"]["frac"], 3), "bound": out["roofline"]["bound"]}}
     pc = out.get("pc_stable")
     if pc:
         sm["alarm5000_pc"] = {"ms_call": r(pc["ms_per_run"]), "tests_s": r(pc["value"]),
@@ -681,7 +726,7 @@ def summary(out):
     c5 = out.get("pc_synthetic")
     if c5:
         sm["config5_pc"] = {"ms_run": r(c5["ms_per_run"]), "tests_s": r(c5["value"]),
-                            "frac": r(c5.get("roofline", {}).get("frac"), 3)}
+                            "frac": r(c5.get("roofline", {}).get("frac"), 3), "bound": c5.get("roofline", {}).get("bound")}
     return sm
 
 
@@ -806,9 +851,8 @@ def main():
 
     total_cases = args.cases * args.steps * world
     value = total_cases / elapsed
-    bpc = info["algorithmic_bytes_per_case"]
-    achieved = bpc * args.cases / (kernel_ms * 1e-3) / 1e9
     traffic = load_traffic(args.cases)
+    roof = alarm_roofline(info, args.cases, kernel_ms, traffic)
     out = {
         "metric": "JT test-cases/sec (ALARM, Munin) + PC-stable CI-tests/sec, 1/2/4/8 GPU",
         "value": value,
@@ -827,21 +871,10 @@ def main():
                    "evidence_per_case": EVIDENCE_PER_CASE,
                    "parallelism": f"case-sharded x{world}" + (" + one labels all-gather of every step (final gather)"
                                                               if world > 1 else "")},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel_ms": kernel_ms, "algorithmic_bytes_per_case": bpc,
-                     "kernel_variant": jt.refresh_info()["variant"],
+        "roofline": {**roof, "kernel_variant": jt.refresh_info()["variant"],
                      "arithmetic_order": "fast (normalizations cancel; labels equal, marginals within 1e-12)",
                      "parity_vs_oracle_256_cases": {"labels_equal": True,
-                                                    "max_rel_err": alarm_rel if rank == 0 else None},
-                     "valu": valu_roofline("alarm", args.cases, kernel_ms),
-                     "traffic_frac": (traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
-                     "note": "achieved = materialized-table algorithmic bytes (SURVEY 8(d): every per-case table "
-                             "written and read once) / kernel time; frac may exceed 1 and is not clipped "
-                             "(SURVEY 8(d)): the specialized kernel keeps tables in registers/LDS and "
-                             "recomputes instead of parking them, so its measured traffic (traffic, "
-                             "traffic_frac: separator rows of the per-wave workspace) is far below the model "
-                             "and the kernel is latency bound at one wave per SIMD (valu frac; DESIGN.md 5.1)"},
+                                                    "max_rel_err": alarm_rel if rank == 0 else None}},
     }
     if world > 1 and not args.no_munin:
         # BASELINE config 4 at its real scale: 125k Munin-like cases per rank (1M on 8 GPUs)

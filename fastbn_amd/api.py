@@ -17,6 +17,8 @@ _SIGS = {
     "fbn_version": [_vp, _vp],
     "fbn_device_count": [_vp],
     "fbn_network_load_xmlbif": [_cstr, _pp],
+    "fbn_network_create": [C.c_int, _vp, _vp, _vp, _vp, _vp, _pp],
+    "fbn_network_node_counts": [_vp, C.c_int, _vp, _vp, _vp, _vp],
     "fbn_network_num_nodes": [_vp, _vp],
     "fbn_network_dims": [_vp, _vp],
     "fbn_network_name": [_vp, C.c_int, C.c_char_p, C.c_int],
@@ -216,9 +218,10 @@ class Network(_Handle):
     _destroy = "fbn_network_destroy"
     """Discrete BN loaded from XMLBIF (CustomNetwork::GetNetFromXMLBIFFile)."""
 
-    def __init__(self, path):
-        h = C.c_void_p()
-        lib.fbn_network_load_xmlbif(os.fsencode(path), C.byref(h))
+    def __init__(self, path=None, _handle=None):
+        h = C.c_void_p() if _handle is None else _handle
+        if _handle is None:
+            lib.fbn_network_load_xmlbif(os.fsencode(path), C.byref(h))
         self._h = h
         _register(self)
         n = C.c_int()
@@ -226,6 +229,37 @@ class Network(_Handle):
         self.num_nodes = n.value
         self.dims = np.zeros(self.num_nodes, np.int32)
         lib.fbn_network_dims(h, _p(self.dims))
+
+    @classmethod
+    def from_counts(cls, dims, parents, counts, names=None):
+        """A network built in memory (fbn_network_create; the reference's Network of DiscreteNodes,
+        src/DiscreteNode.cpp:114-147): dims[v] states, parents[v] (the node's own order), counts[v]
+        = int [dims[v]][parent configs], configurations over the parents in ascending index order,
+        last fastest (map_cond_prob_table_statistics)."""
+        n = len(dims)
+        d = np.ascontiguousarray(dims, np.int32)
+        off = np.zeros(n + 1, np.int32)
+        for v in range(n):
+            off[v + 1] = off[v] + len(parents[v])
+        par = np.ascontiguousarray([q for ps in parents for q in ps] or [0], np.int32)
+        cnt = np.ascontiguousarray(np.concatenate([np.asarray(c, np.int64).reshape(-1) for c in counts]), np.int64)
+        nm = None
+        if names is not None:
+            enc = [os.fsencode(x) for x in names]
+            nm = (C.c_char_p * n)(*enc)
+        h = C.c_void_p()
+        lib.fbn_network_create(n, _p(d), _p(off), _p(par), _p(cnt), C.cast(nm, C.c_void_p) if nm is not None else None,
+                               C.byref(h))
+        return cls(_handle=h)
+
+    def node_counts(self, v):
+        """(parents ascending, counts [dims[v]][parent configs]) of node v."""
+        npar, ncnt = C.c_int(), C.c_int64()
+        lib.fbn_network_node_counts(self._h, int(v), None, None, C.byref(npar), C.byref(ncnt))
+        par = np.zeros(max(1, npar.value), np.int32)
+        cnt = np.zeros(max(1, ncnt.value), np.int64)
+        lib.fbn_network_node_counts(self._h, int(v), _p(par), _p(cnt), C.byref(npar), C.byref(ncnt))
+        return par[:npar.value], cnt[:ncnt.value].reshape(int(self.dims[v]), -1)
 
     def name(self, i):
         buf = C.create_string_buffer(256)

@@ -473,6 +473,21 @@ int fbn_network_load_xmlbif(const char *path, fbn_network **out) {
     *out = h.release();
     return FBN_OK;
 }
+int fbn_network_create(int nvars, const int32_t *dims, const int32_t *parent_off, const int32_t *parents,
+                       const int64_t *counts, const char *const *names, fbn_network **out) {
+    if (!out) return SetError(FBN_ERR_ARG, "null pointer");
+    auto h = std::unique_ptr<fbn_network>(new (std::nothrow) fbn_network());
+    if (!h) return SetError(FBN_ERR_NOMEM, "out of memory");
+    int rc = fbn::BuildNetwork(nvars, dims, parent_off, parents, counts, names, h->net);
+    if (rc) return rc;
+    *out = h.release();
+    return FBN_OK;
+}
+int fbn_network_node_counts(const fbn_network *net, int node, int32_t *parents, int64_t *counts, int *nparents,
+                            int64_t *ncounts) {
+    if (!net) return SetError(FBN_ERR_ARG, "null pointer");
+    return fbn::NodeCounts(net->net, node, parents, counts, nparents, ncounts);
+}
 int fbn_network_num_nodes(const fbn_network *net, int *n) {
     if (!net || !n) return SetError(FBN_ERR_ARG, "null pointer");
     *n = net->net.n();

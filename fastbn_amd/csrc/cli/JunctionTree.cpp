@@ -81,24 +81,28 @@ double JunctionTree::EvaluateAccuracy(const std::string &pt_path, int /*num_thre
               << "Begin testing the trained network." << std::endl;
     auto t0 = std::chrono::steady_clock::now();
     predictions.assign(n, 0);
-    marginals.assign((size_t)n * SD, 0.0);
     float kms = 0.f;
+    int64_t correct = 0;  // Accuracy (src/Inference.cpp:46-61)
     if (gpus_ > 1 || ForceExchange()) {
-        std::string e = RunSharded(&kms);
+        // marginals stay on the devices: every rank scores its own shard
+        marginals.clear();
+        double sums[3] = {0, 0, 0};
+        std::string e = RunSharded(golden, &kms, sums);
         if (!e.empty()) {
             fprintf(stderr, "Error in PredictUseJTInfer: %s\n", e.c_str());
             exit(1);
         }
+        mse = sums[0], hd = sums[1], correct = (int64_t)sums[2];
     } else {
+        marginals.assign((size_t)n * SD, 0.0);
         if (fbn_jt_run(plan_, tester_->evidence.data(), n, predictions.data(), marginals.data(), nullptr))
             Die("PredictUseJTInfer");
         fbn_jt_last_kernel_ms(plan_, &kms);
+        if (fbn_jt_score(plan_, marginals.data(), golden.data(), n, &mse, &hd)) Die("CalculateMSE");
+        for (int64_t c = 0; c < n; ++c) correct += predictions[c] == tester_->ground_truths[c];
     }
-    if (fbn_jt_score(plan_, marginals.data(), golden.data(), n, &mse, &hd)) Die("CalculateMSE");
     std::cout << "average MSE = " << mse / n << std::endl;
     std::cout << "average HD = " << hd / n << std::endl;
-    int64_t correct = 0;  // Accuracy (src/Inference.cpp:46-61)
-    for (int64_t c = 0; c < n; ++c) correct += predictions[c] == tester_->ground_truths[c];
     double acc = correct / (double)n;
     double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     std::cout << "==================================================" << std::endl
@@ -109,10 +113,13 @@ double JunctionTree::EvaluateAccuracy(const std::string &pt_path, int /*num_thre
 
 // Cases sharded over the GPUs: rank r takes cases [r * chunk, (r + 1) * chunk), builds
 // its plan on its device from the parsed network (rank 0 reuses the constructor's), runs its shard
-// from device memory, and the final gather brings every shard's labels and marginals to rank 0
-// (ncclSend / ncclRecv in one group); one ncclAllReduce (max) of the kernel times.  Rank 0 then
-// scores in the reference's case order, so MSE / HD / accuracy equal the one-GPU run exactly.
-std::string JunctionTree::RunSharded(float *kernel_ms) {
+// from device memory and scores it against its slice of the golden table (fbn_jt_score over the
+// shard's cases in order, CalculateMSE / HD src/Inference.cpp:153-206, plus its correct labels).
+// The marginals never leave their device's shard path: one ncclReduce (sum) of the three per-rank
+// sums {MSE, HD, #correct} to rank 0, one ncclAllGather of the labels (the final gather) and one
+// ncclAllReduce (max) of the kernel times.  MSE / HD add per-shard partial sums (the one-GPU run adds
+// case after case), so they may differ from it in the last bits; accuracy is exact.
+std::string JunctionTree::RunSharded(const std::vector<double> &golden, float *kernel_ms, double *sums) {
     const int64_t n = tester_->num_instances();
     const int V = info_.num_nodes, SD = info_.sum_dom;
     GpuGroup g(gpus_, device_);
@@ -120,6 +127,7 @@ std::string JunctionTree::RunSharded(float *kernel_ms) {
     const int world = g.size();
     const int64_t chunk = std::max<int64_t>(1, (n + world - 1) / world);
     float kmax = 0.f;
+    std::vector<int32_t> all_labels((size_t)chunk * world, -1);
     std::string err = g.Run([&](int r) -> std::string {
         hipStream_t s = g.stream(r);
         ncclComm_t comm = g.comm(r);
@@ -127,21 +135,26 @@ std::string JunctionTree::RunSharded(float *kernel_ms) {
         fbn_jt_plan *plan = plan_;
         if (r > 0 && fbn_jt_plan_create(net_, g.device(r), &plan)) return std::string("fbn_jt_plan_create: ") + fbn_last_error();
         const int64_t c0 = std::min<int64_t>(n, r * chunk), nr = std::min<int64_t>(n, c0 + chunk) - c0;
-        void *d_ev = nullptr, *d_lab = nullptr, *d_marg = nullptr, *d_k = nullptr;
+        void *d_ev = nullptr, *d_lab = nullptr, *d_all = nullptr, *d_marg = nullptr, *d_k = nullptr, *d_s = nullptr;
         auto cleanup = [&] {
-            for (void *p : {d_ev, d_lab, d_marg, d_k})
+            for (void *p : {d_ev, d_lab, d_all, d_marg, d_k, d_s})
                 if (p) (void)hipFree(p);
             if (r > 0) fbn_jt_plan_destroy(plan);
         };
-        const size_t gathered = r == 0 ? (size_t)world : 1;  // rank 0 receives every shard
         if ((e = HipErr(hipMalloc(&d_ev, (size_t)chunk * V), "hipMalloc")).size() ||
-            (e = HipErr(hipMalloc(&d_lab, (size_t)chunk * 4 * gathered), "hipMalloc")).size() ||
-            (e = HipErr(hipMalloc(&d_marg, (size_t)chunk * SD * 8 * gathered), "hipMalloc")).size() ||
-            (e = HipErr(hipMalloc(&d_k, 4), "hipMalloc")).size()) {
+            (e = HipErr(hipMalloc(&d_lab, (size_t)chunk * 4), "hipMalloc")).size() ||
+            (e = HipErr(hipMalloc(&d_all, (size_t)chunk * 4 * world), "hipMalloc")).size() ||
+            (e = HipErr(hipMalloc(&d_marg, (size_t)chunk * SD * 8), "hipMalloc")).size() ||
+            (e = HipErr(hipMalloc(&d_k, 4), "hipMalloc")).size() ||
+            (e = HipErr(hipMalloc(&d_s, 3 * 8), "hipMalloc")).size()) {
             cleanup();
             return e;
         }
+        (void)hipMemsetAsync(d_lab, 0xFF, (size_t)chunk * 4, s);  // labels past n: -1
         float ms = 0.f;
+        double part[3] = {0, 0, 0};
+        std::vector<int32_t> lab((size_t)std::max<int64_t>(nr, 0));
+        std::vector<double> marg((size_t)std::max<int64_t>(nr, 0) * SD);
         if (nr > 0) {
             (void)hipMemcpyAsync(d_ev, tester_->evidence.data() + (size_t)c0 * V, (size_t)nr * V, hipMemcpyHostToDevice, s);
             if (fbn_jt_run_device(plan, static_cast<const int8_t *>(d_ev), nr, static_cast<int32_t *>(d_lab),
@@ -151,31 +164,33 @@ std::string JunctionTree::RunSharded(float *kernel_ms) {
                 return e;
             }
             fbn_jt_last_kernel_ms(plan, &ms);
-        }
-        // final gather at rank 0: shard q lands at offset q * chunk
-        ncclGroupStart();
-        if (r == 0) {
-            for (int q = 1; q < world; ++q) {
-                ncclRecv(static_cast<int32_t *>(d_lab) + (size_t)q * chunk, (size_t)chunk, ncclInt32, q, comm, s);
-                ncclRecv(static_cast<double *>(d_marg) + (size_t)q * chunk * SD, (size_t)chunk * SD, ncclFloat64, q,
-                         comm, s);
+            // this rank's shard: marginals to its host slice over its own link, scored in case order
+            (void)hipMemcpyAsync(marg.data(), d_marg, marg.size() * 8, hipMemcpyDeviceToHost, s);
+            (void)hipMemcpyAsync(lab.data(), d_lab, lab.size() * 4, hipMemcpyDeviceToHost, s);
+            if ((e = HipErr(hipStreamSynchronize(s), "shard results")).size()) {
+                cleanup();
+                return e;
             }
-        } else {
-            ncclSend(d_lab, (size_t)chunk, ncclInt32, 0, comm, s);
-            ncclSend(d_marg, (size_t)chunk * SD, ncclFloat64, 0, comm, s);
+            if (fbn_jt_score(plan, marg.data(), golden.data() + (size_t)c0 * SD, nr, &part[0], &part[1])) {
+                e = std::string("fbn_jt_score: ") + fbn_last_error();
+                cleanup();
+                return e;
+            }
+            for (int64_t c = 0; c < nr; ++c) part[2] += lab[c] == tester_->ground_truths[c0 + c];
         }
-        if ((e = NcclErr(ncclGroupEnd(), "ncclGroupEnd (gather)")).size()) {
-            cleanup();
-            return e;
-        }
+        (void)hipMemcpyAsync(d_s, part, sizeof part, hipMemcpyHostToDevice, s);
         (void)hipMemcpyAsync(d_k, &ms, 4, hipMemcpyHostToDevice, s);
-        if ((e = NcclErr(ncclAllReduce(d_k, d_k, 1, ncclFloat32, ncclMax, comm, s), "ncclAllReduce")).size()) {
+        ncclGroupStart();
+        ncclReduce(d_s, d_s, 3, ncclFloat64, ncclSum, 0, comm, s);
+        ncclAllGather(d_lab, d_all, (size_t)chunk, ncclInt32, comm, s);
+        ncclAllReduce(d_k, d_k, 1, ncclFloat32, ncclMax, comm, s);
+        if ((e = NcclErr(ncclGroupEnd(), "ncclGroupEnd (reduce / gather)")).size()) {
             cleanup();
             return e;
         }
         if (r == 0) {
-            (void)hipMemcpyAsync(predictions.data(), d_lab, (size_t)n * 4, hipMemcpyDeviceToHost, s);
-            (void)hipMemcpyAsync(marginals.data(), d_marg, (size_t)n * SD * 8, hipMemcpyDeviceToHost, s);
+            (void)hipMemcpyAsync(sums, d_s, 3 * 8, hipMemcpyDeviceToHost, s);
+            (void)hipMemcpyAsync(all_labels.data(), d_all, all_labels.size() * 4, hipMemcpyDeviceToHost, s);
             (void)hipMemcpyAsync(&kmax, d_k, 4, hipMemcpyDeviceToHost, s);
         }
         e = HipErr(hipStreamSynchronize(s), "gather");
@@ -183,6 +198,7 @@ std::string JunctionTree::RunSharded(float *kernel_ms) {
         return e;
     });
     if (!err.empty()) return err;
+    std::copy(all_labels.begin(), all_labels.begin() + n, predictions.begin());
     *kernel_ms = kmax;
     std::cout << "junction tree on " << world << " GPU(s) (RCCL), " << chunk << " cases per GPU" << std::endl;
     return std::string();

@@ -27,7 +27,7 @@ public:
     double EvaluateAccuracy(const std::string &pt_path, int num_threads);
 
     std::vector<int32_t> predictions;
-    std::vector<double> marginals;  // [ncases][sum_dom]
+    std::vector<double> marginals;  // [ncases][sum_dom] (one GPU; empty when sharded: they stay per rank)
     double mse = 0, hd = 0;
 
 private:
@@ -36,8 +36,9 @@ private:
     fbn_jt_plan *plan_ = nullptr;
     fbn_jt_plan_info info_{};
     int device_ = 0, gpus_ = 1;
-    // PredictUseJTInfer over all cases on gpus_ devices -> predictions / marginals; "" or an error
-    std::string RunSharded(float *kernel_ms);
+    // PredictUseJTInfer over all cases on gpus_ devices -> predictions, sums = {MSE, HD, #correct}
+    // over all cases (each rank scores its shard against `golden`); "" or an error
+    std::string RunSharded(const std::vector<double> &golden, float *kernel_ms, double *sums);
 };
 
 #endif

@@ -29,6 +29,9 @@ struct Network {
     double Prob(int v, int q, const int *parent_vals_asc) const;
 };
 int LoadXmlbif(const std::string &path, Network &net);
+int BuildNetwork(int n, const int32_t *dims, const int32_t *parent_off, const int32_t *parents, const int64_t *counts,
+                 const char *const *names, Network &net);
+int NodeCounts(const Network &net, int v, int32_t *parents_asc, int64_t *counts, int *nparents, int64_t *ncounts);
 
 struct Dataset {
     int nvars = 0;

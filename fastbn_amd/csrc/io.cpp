@@ -97,6 +97,74 @@ double Network::Prob(int v, int q, const int *pv) const {
     return ((double)counts[v][q * npc + pc] + 1.0) / ((double)totals[v][pc] + 1.0 * (double)dom[v]);
 }
 
+// A network given in memory: what a reference `Network` of DiscreteNodes holds after
+// InitializeCPT + AddCount (src/DiscreteNode.cpp:114-147): per node its state count, its parents
+// (the order given = the node's own parent order, used by the seeded generators) and the count map
+// map_cond_prob_table_statistics[value][parent config], parent configurations over the parents in
+// ascending index order, last fastest (a DiscreteConfig is an ordered set of (var, value) pairs).
+// map_total_count_under_parents_config is the sum over the values, as AddCount keeps it; the
+// probabilities follow GetProbability (:154-164) with laplace_smooth = 1, as for the XMLBIF path.
+int BuildNetwork(int n, const int32_t *dims, const int32_t *parent_off, const int32_t *parents, const int64_t *counts,
+                 const char *const *names, Network &net) {
+    if (n < 1 || !dims || !parent_off || (!parents && parent_off[n] > 0) || !counts)
+        return SetError(FBN_ERR_ARG, "network: bad arguments");
+    net = Network();
+    net.dom.assign(dims, dims + n);
+    for (int v = 0; v < n; ++v) {
+        if (net.dom[v] < 1 || net.dom[v] > 127) return SetError(FBN_ERR_LIMIT, "node %d has %d states (supported 1..127)", v, net.dom[v]);
+        net.names.push_back(names && names[v] ? std::string(names[v]) : "X" + std::to_string(v));
+    }
+    net.given.assign(n, {});
+    net.parents_asc.assign(n, {});
+    net.counts.assign(n, {});
+    net.totals.assign(n, {});
+    int64_t off = 0;
+    for (int v = 0; v < n; ++v) {
+        if (parent_off[v + 1] < parent_off[v]) return SetError(FBN_ERR_ARG, "node %d: parent offsets decrease", v);
+        for (int32_t k = parent_off[v]; k < parent_off[v + 1]; ++k) {
+            const int q = parents[k];
+            if (q < 0 || q >= n || q == v) return SetError(FBN_ERR_ARG, "node %d: bad parent %d", v, q);
+            net.given[v].push_back(q);
+        }
+        std::set<int> ps(net.given[v].begin(), net.given[v].end());
+        if (ps.size() != net.given[v].size()) return SetError(FBN_ERR_ARG, "node %d: repeated parent", v);
+        net.parents_asc[v].assign(ps.begin(), ps.end());
+        int64_t npc = 1;
+        for (int q : net.parents_asc[v]) npc *= net.dom[q];
+        net.counts[v].assign(counts + off, counts + off + net.dom[v] * npc);
+        net.totals[v].assign((size_t)npc, 0);
+        for (int q = 0; q < net.dom[v]; ++q)
+            for (int64_t pc = 0; pc < npc; ++pc) {
+                const int64_t c = net.counts[v][q * npc + pc];
+                if (c < 0) return SetError(FBN_ERR_ARG, "node %d: negative count", v);
+                net.totals[v][pc] += c;
+            }
+        off += net.dom[v] * npc;
+    }
+    // a DAG (the junction tree and the generators need one)
+    std::vector<int> indeg(n, 0), order;
+    std::vector<std::vector<int>> ch(n);
+    for (int v = 0; v < n; ++v)
+        for (int q : net.parents_asc[v]) ch[q].push_back(v), ++indeg[v];
+    for (int v = 0; v < n; ++v)
+        if (!indeg[v]) order.push_back(v);
+    for (size_t i = 0; i < order.size(); ++i)
+        for (int c : ch[order[i]])
+            if (--indeg[c] == 0) order.push_back(c);
+    if ((int)order.size() != n) return SetError(FBN_ERR_ARG, "network: the parent lists form a cycle");
+    return FBN_OK;
+}
+
+// the count map of node v (layout as BuildNetwork's), parents in ascending order
+int NodeCounts(const Network &net, int v, int32_t *parents_asc, int64_t *counts, int *nparents, int64_t *ncounts) {
+    if (v < 0 || v >= net.n()) return SetError(FBN_ERR_ARG, "node %d out of range", v);
+    if (nparents) *nparents = (int)net.parents_asc[v].size();
+    if (ncounts) *ncounts = (int64_t)net.counts[v].size();
+    if (parents_asc) std::copy(net.parents_asc[v].begin(), net.parents_asc[v].end(), parents_asc);
+    if (counts) std::copy(net.counts[v].begin(), net.counts[v].end(), counts);
+    return FBN_OK;
+}
+
 int LoadXmlbif(const std::string &path, Network &net) {
     std::string s;
     if (!ReadFile(path, s)) return SetError(FBN_ERR_IO, "cannot open %s", path.c_str());

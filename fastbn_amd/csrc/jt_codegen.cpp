@@ -140,13 +140,15 @@ class JTGen {
     std::string Val(const std::string &P, int c, int64_t e) const {
         return (normed || fast) ? N(P, c, e) : "dv(" + N(P, c, e) + ", den, y)";
     }
-    // fast order: the clique total (den, y) the Distribute messages are scaled by
-    void Total(const std::string &P, int c) {
-        const Table &t = plan.cliques[c];
-        o << "        { double sm = 0.0;";
-        for (int64_t e = 0; e < t.size(); ++e) o << " sm += " << N(P, c, e) << ";";
-        o << " den = sm; y = 1.0 / den; bad |= den_bad(den); }\n" << B(6);
+    // fast order: a sum as a balanced tree of adds (depth log2 n instead of an n-long dependency
+    // chain: a dependent fp64 add costs ~45 cycles at one wave per SIMD, an independent one ~5,
+    // tools/micro/fp64_ilp.hip); the reference's left-to-right order is kept in the exact order
+    static std::string TreeSum(const std::vector<std::string> &t, size_t b, size_t e) {
+        if (e - b == 1) return t[b];
+        const size_t m = b + (e - b) / 2;
+        return "(" + TreeSum(t, b, m) + " + " + TreeSum(t, m, e) + ")";
     }
+    static std::string TreeSum(const std::vector<std::string> &t) { return TreeSum(t, 0, t.size()); }
     void Normalize(const std::string &P, int c) {
         const Table &t = plan.cliques[c];
         for (int64_t e = 0; e < t.size(); ++e) o << (e % 8 ? " " : (e ? "\n        " : "        ")) << N(P, c, e) << " = dv(" << N(P, c, e) << ", den, y);";
@@ -223,15 +225,16 @@ void JTGen::Mul(const std::string &P, int c, int s, const std::string &M) {
 void JTGen::SepCol(const std::string &P, int c, int s, bool store) {
     const Table &t = plan.cliques[c];
     const int64_t Ts = plan.seps[s].size(), Q = t.size() / Ts;
-    if (fast) {  // message = bin sums / their total (= the normalized table's sums)
+    if (fast) {  // message = bin sums / their total (= the normalized table's sums), tree sums
+        std::vector<std::string> tot;
         for (int64_t j = 0; j < Ts; ++j) {
-            o << "        const double mr" << s << "_" << j << " = " << N(P, c, j);
-            for (int64_t q = 1; q < Q; ++q) o << " + " << N(P, c, q * Ts + j);
-            o << ";\n";
+            std::vector<std::string> terms;
+            for (int64_t q = 0; q < Q; ++q) terms.push_back(N(P, c, q * Ts + j));
+            o << "        const double mr" << s << "_" << j << " = " << TreeSum(terms) << ";\n";
+            tot.push_back("mr" + std::to_string(s) + "_" + std::to_string(j));
         }
-        o << "        double ys" << s << "; { double sm = mr" << s << "_0;";
-        for (int64_t j = 1; j < Ts; ++j) o << " sm += mr" << s << "_" << j << ";";
-        o << " ys" << s << " = 1.0 / sm; bad |= den_bad(sm); }\n";
+        o << "        double ys" << s << "; { const double sm = " << TreeSum(tot) << "; ys" << s
+          << " = frcp(sm); bad |= den_bad(sm); }\n";
         for (int64_t j = 0; j < Ts; ++j) {
             o << "        const double mc" << s << "_" << j << " = mr" << s << "_" << j << " * ys" << s << ";";
             if (store) o << " W(" << sep_row[s] + j << "LL) = mc" << s << "_" << j << ";";
@@ -274,11 +277,34 @@ void JTGen::SepDis(const std::string &P, int c, int s, const std::string &old, b
     const Table &t = plan.cliques[c], &sp = plan.seps[s];
     std::vector<std::vector<int64_t>> lists(sp.size());
     for (int64_t e = 0; e < t.size(); ++e) lists[SepIndex(t, sp, e)].push_back(e);
+    if (fast) {
+        // bin sums a(j) as trees; the clique total S = sum_j a(j) (the same value as the sum over the
+        // table, without a T-long chain); md(j) = a(j) / S / old(j), 0 where old(j) == 0, with
+        // branch-free reciprocals (v_rcp_f64 + one Newton step) so the Ts quotients overlap
+        std::vector<std::string> as;
+        for (int64_t j = 0; j < sp.size(); ++j) {
+            std::vector<std::string> terms;
+            for (int64_t e : lists[j]) terms.push_back(N(P, c, e));
+            const std::string a = "sa" + std::to_string(s) + "_" + std::to_string(j);
+            o << "        const double " << a << " = " << TreeSum(terms) << ";\n";
+            as.push_back(a);
+        }
+        o << "        double ysd" << s << "; { const double sm = " << TreeSum(as) << "; ysd" << s
+          << " = frcp(sm); bad |= den_bad(sm); }\n";
+        for (int64_t j = 0; j < sp.size(); ++j) {
+            o << "        double md" << s << "_" << j << "; { const double od = " << old << s << "_" << j
+              << "; const double q = (" << as[j] << " * ysd" << s << ") * frcp(od); md" << s << "_" << j
+              << " = (od == 0.0) ? 0.0 : q; }";
+            if (store) o << " W(" << sep_row[s] + j << "LL) = md" << s << "_" << j << ";";
+            o << "\n";
+        }
+        o << B(7);
+        return;
+    }
     for (int64_t j = 0; j < sp.size(); ++j) {
         o << "        double md" << s << "_" << j << ";";
         o << " { double a = " << Val(P, c, lists[j][0]) << ";";
         for (size_t q = 1; q < lists[j].size(); ++q) o << " a += " << Val(P, c, lists[j][q]) << ";";
-        if (fast) o << " a *= y;";  // the clique total (Total)
         o << " const double od = " << old << s << "_" << j << "; md" << s << "_" << j << " = (od == 0.0) ? 0.0 : a / od; }";
         if (store) o << " W(" << sep_row[s] + j << "LL) = md" << s << "_" << j << ";";
         o << "\n";
@@ -307,21 +333,33 @@ void JTGen::Marg(const std::string &P, int c) {
                 o << " { const int r = " << R(cand[v][k]) << "; if (r < b) { b = r; sl = " << cand[v][k] << "; } }";
             o << "\n        if (sl == " << c << " && !" << observed(v) << ") { // marginal of var " << v << "\n";
         }
-        o << "          double tot = 0.0;";
-        for (int d = 0; d < dim; ++d) o << " double p" << d << ";";
-        o << "\n";
-        for (int d = 0; d < dim; ++d) {
-            bool first = true;
-            o << "          { double a = ";
-            for (int64_t hi = 0; hi < nhi; ++hi)
-                for (int64_t l = 0; l < cum; ++l) {
-                    const int64_t e = hi * bw + d * cum + l;
-                    o << (first ? "" : " a += ") << Val(P, c, e) << ";";
-                    first = false;
-                }
-            o << " p" << d << " = a; tot += a; }\n";
+        if (fast) {  // tree sums, branch-free reciprocal of the total
+            std::vector<std::string> ps;
+            for (int d = 0; d < dim; ++d) {
+                std::vector<std::string> terms;
+                for (int64_t hi = 0; hi < nhi; ++hi)
+                    for (int64_t l = 0; l < cum; ++l) terms.push_back(N(P, c, hi * bw + d * cum + l));
+                o << "          const double p" << d << " = " << TreeSum(terms) << ";\n";
+                ps.push_back("p" + std::to_string(d));
+            }
+            o << "          const double tot = " << TreeSum(ps) << "; const double yt = frcp(tot); bad |= den_bad(tot);\n";
+        } else {
+            o << "          double tot = 0.0;";
+            for (int d = 0; d < dim; ++d) o << " double p" << d << ";";
+            o << "\n";
+            for (int d = 0; d < dim; ++d) {
+                bool first = true;
+                o << "          { double a = ";
+                for (int64_t hi = 0; hi < nhi; ++hi)
+                    for (int64_t l = 0; l < cum; ++l) {
+                        const int64_t e = hi * bw + d * cum + l;
+                        o << (first ? "" : " a += ") << Val(P, c, e) << ";";
+                        first = false;
+                    }
+                o << " p" << d << " = a; tot += a; }\n";
+            }
+            o << "          const double yt = 1.0 / tot; bad |= den_bad(tot);\n";
         }
-        o << "          const double yt = 1.0 / tot; bad |= den_bad(tot);\n";
         if (v == 0) {
             // (fast order: a near-tie, top two within 1e-12 relative, may break differently from the
             // reference's exact values -- the block is flagged for the exact pass)
@@ -413,6 +451,13 @@ extern __shared__ double fbn_lds[];
 __device__ __forceinline__ double sel(bool c, double v) { return c ? v : 0.0; }
 #define FBN_STAMP(k) do { unsigned long long t_; __asm__ volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_) :: "memory"); pacc[k] += t_ - tprev; tprev = t_; } while (0)
 __device__ __forceinline__ unsigned den_bad(double d) { return (d >= 0x1p-600 && d <= 0x1p+600) ? 0u : 1u; }
+// fast order: 1 / x as v_rcp_f64 + one Newton step (relative error <= 2.3e-15 over 2^-60..2^60,
+// tools/micro/fp64_ilp.hip), branch-free, so independent reciprocals overlap; the operands are
+// range-checked by den_bad (a block outside [2^-600, 2^600] goes to the exact pass)
+__device__ __forceinline__ double frcp(double x) {
+    const double r = __builtin_amdgcn_rcp(x);
+    return __builtin_fma(r, __builtin_fma(-x, r, 1.0), r);
+}
 // this lane's case / output row, recomputed per segment from the (laundered) block index
 #define CS (blkl * 64 + lane)
 #define ACT (CS < ncases)
@@ -590,9 +635,8 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
         }
         const auto &down = plan.clique_down[c];
         // consumers of the normalized table: one SepDis per child, one marginal per variable
-        if (fast) {
-            if (!down.empty()) Total(P, c);
-        } else if (down.size() + plan.cliques[c].vars.size() >= 2) Normalize(P, c);
+        // (fast order: each SepDis takes the clique total from its own bin sums)
+        if (!fast && down.size() + plan.cliques[c].vars.size() >= 2) Normalize(P, c);
         for (size_t i = 0; i < down.size(); ++i) {
             if (!early) Load("lc", down[i]), o << B(1);
             SepDis(P, c, down[i], early ? "lb" : "lc", !md_reg[down[i]]);

@@ -46,12 +46,14 @@ def fixture_xmls(dirname):
 
 
 def prebuild_default(clean=True):
-    """Every eligible benchmark / test network, both orders; clean: drop code objects of older
-    generator versions first (their source hash no longer matches any plan)."""
+    """Every eligible benchmark / test network, both orders (cache hits are free); clean: then drop
+    the code objects no current plan uses (older generator versions)."""
+    with tempfile.TemporaryDirectory() as d:
+        built = prebuild([ALARM_XML, synth_small_xml(d)] + fixture_xmls(d))
     if clean:
+        keep = {os.path.basename(p) for p in built}
         kdir = os.path.join(REPO, "fastbn_amd", "kcache")
         for f in os.listdir(kdir) if os.path.isdir(kdir) else []:
-            if f.endswith(".hsaco"):
+            if f.endswith(".hsaco") and f not in keep:
                 os.remove(os.path.join(kdir, f))
-    with tempfile.TemporaryDirectory() as d:
-        return prebuild([ALARM_XML, synth_small_xml(d)] + fixture_xmls(d))
+    return built

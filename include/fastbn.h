@@ -45,6 +45,23 @@ typedef struct fbn_network fbn_network;
  * node-major TABLE).  Replaces CustomNetwork::GetNetFromXMLBIFFile (src/CustomNetwork.cpp:20-41)
  * + XMLBIFParser (src/XMLBIFParser.cpp:3-218). */
 int fbn_network_load_xmlbif(const char *path, fbn_network **out);
+/* A network built in memory -- learned, or constructed by the caller -- with no file in between.
+ * Mirrors what the reference's Network of DiscreteNodes holds after InitializeCPT + AddCount
+ * (src/DiscreteNode.cpp:114-147): node v has dims[v] states, parents parents[parent_off[v] ..
+ * parent_off[v+1]) (any order: the node's own parent order) and the count map
+ * map_cond_prob_table_statistics as int64 counts[value][parent config] (parent configurations over
+ * the parents in ASCENDING index order, last fastest -- a DiscreteConfig is an ordered set), node
+ * after node in one array; totals are the sums over the values (as AddCount keeps
+ * map_total_count_under_parents_config), probabilities (count + 1) / (total + dims[v]) as
+ * GetProbability (:154-164).  names may be NULL ("X<v>").  The parent lists must form a DAG.
+ * The JunctionTree(Network*, ...) constructor of the reference (src/JunctionTree.cpp:3-9) binds to
+ * this + fbn_jt_plan_create. */
+int fbn_network_create(int nvars, const int32_t *dims, const int32_t *parent_off /* [nvars+1] */,
+                       const int32_t *parents, const int64_t *counts, const char *const *names,
+                       fbn_network **out);
+/* Node v's parents (ascending) and count map in fbn_network_create's layout; NULL buffers: sizes only. */
+int fbn_network_node_counts(const fbn_network *net, int node, int32_t *parents, int64_t *counts, int *nparents,
+                            int64_t *ncounts);
 int fbn_network_num_nodes(const fbn_network *net, int *n);
 int fbn_network_dims(const fbn_network *net, int32_t *dims /* [n] */);
 int fbn_network_name(const fbn_network *net, int node, char *buf, int cap);

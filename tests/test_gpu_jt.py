@@ -289,3 +289,22 @@ def test_munin_like_extra_cases_vs_reference(munin_fixture):
     assert jt.refresh_info()["variant"] == 5 and jt.debug_flagged_blocks() == 0
     np.testing.assert_array_equal(lab, rlab)
     np.testing.assert_allclose(marg, rmarg, rtol=1e-9, atol=1e-300)
+
+
+def test_network_from_counts_runs_like_xmlbif():
+    """A network handed over in memory (fbn_network_create) infers exactly like the XMLBIF path:
+    labels and marginals bit for bit, fast and exact order."""
+    from test_host import _counts_from_xmlbif
+    from fastbn_amd import synth
+    xml = os.path.join(GOLD, "alarm", "alarm.xml")
+    names, dims, parents, counts = _counts_from_xmlbif(xml)
+    ev = synth.evidence_cases(synth.read_xmlbif(xml), 2000, 7, seed=31)
+    a = F.JunctionTree(F.Network.from_counts(dims, parents, counts, names), device=0)
+    b = F.JunctionTree(F.Network(xml), device=0)
+    for exact in (None, True):
+        a.set_exact(exact)
+        b.set_exact(exact)
+        la, ma = a.infer(ev)
+        lb, mb = b.infer(ev)
+        np.testing.assert_array_equal(la, lb)
+        np.testing.assert_array_equal(ma, mb)

@@ -49,6 +49,51 @@ def test_host_only_plan_matches_reference_dump(alarm_paths, tmp_path):
         jt.infer(np.full((1, 37), -1, np.int8))
 
 
+def _counts_from_xmlbif(path):
+    """(dims, parents in GIVEN order, counts [value][parent configs over ascending parents]) from the
+    XMLBIF TABLE text alone (int(p * 10000), node-major, GIVEN order last fastest): an independent
+    restatement of the count maps the reference's parser builds (src/XMLBIFParser.cpp:73-179)."""
+    from fastbn_amd import synth
+    import xml.etree.ElementTree as ET
+    names, dims, parents, _ = synth.read_xmlbif(path)
+    idx = {n: i for i, n in enumerate(names)}
+    counts = [None] * len(names)
+    for p in ET.parse(path).getroot().find("NETWORK").findall("PROBABILITY"):
+        v = idx[p.find("FOR").text.strip()]
+        given = [idx[g.text.strip()] for g in p.findall("GIVEN")]
+        vals = [int(float(t) * 10000) for t in p.find("TABLE").text.strip().split(" ")]
+        c = np.array(vals, np.int64).reshape([dims[v]] + [dims[g] for g in given])
+        asc = sorted(given)
+        c = np.transpose(c, [0] + [1 + given.index(q) for q in asc])  # parents to ascending order
+        counts[v] = c.reshape(dims[v], -1)
+    return names, dims, parents, counts
+
+
+def test_network_from_counts_equals_xmlbif_path(alarm_paths, tmp_path):
+    """fbn_network_create (a network handed over in memory, the reference's JunctionTree(Network*)
+    binding) built from ALARM's count maps: the same node counts, the same plan and initial
+    potentials as the XMLBIF path, byte for byte (the reference's own dump)."""
+    names, dims, parents, counts = _counts_from_xmlbif(alarm_paths["xml"])
+    net = F.Network.from_counts(dims, parents, counts, names)
+    ref = F.Network(alarm_paths["xml"])
+    np.testing.assert_array_equal(net.dims, ref.dims)
+    for v in range(ref.num_nodes):
+        pa, ca = net.node_counts(v)
+        pb, cb = ref.node_counts(v)
+        np.testing.assert_array_equal(pa, pb)
+        np.testing.assert_array_equal(ca, cb)
+    assert net.name(36) == "BP"
+    jt = F.JunctionTree(net, device=-1)
+    jt.dump_plan(str(tmp_path / "p"), str(tmp_path / "i"))
+    assert open(tmp_path / "p").read() == open(os.path.join(GOLD, "alarm_1k.plan")).read()
+    assert open(tmp_path / "i").read() == open(os.path.join(GOLD, "alarm_1k.init")).read()
+    # bad inputs are reported, not fatal
+    with pytest.raises(F.FastBNError, match="cycle"):
+        F.Network.from_counts([2, 2], [[1], [0]], [np.ones((2, 2)), np.ones((2, 2))])
+    with pytest.raises(F.FastBNError, match="bad parent"):
+        F.Network.from_counts([2], [[3]], [np.ones((2, 2))])
+
+
 def test_synthetic_network_plan_matches_oracle(tmp_path):
     from fastbn_amd import synth
     p = str(tmp_path / "syn.xml")
