@@ -28,7 +28,8 @@ extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, co
                                     int32_t *gscratch, unsigned long long *stats, const uint32_t *bits,
                                     const int32_t *row0, long long W, const double *band, int nband,
                                     const uint32_t *pk, long long PW, long long cstride, int32_t *tab,
-                                    long long tstride, int split, int split_grid, hipStream_t stream);
+                                    long long tstride, int split, int split_grid, const int32_t *pairtab,
+                                    int nvars, hipStream_t stream);
 extern "C" hipError_t fbn_ci_pack2_build(const uint8_t *cols, int nvars, long long N, long long PW, uint32_t *pk,
                                          hipStream_t stream);
 extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy);
@@ -1738,7 +1739,13 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
     // (ci_kernels.hip) when it is built.  Opt-in: every z-configuration re-reads the x / y value rows,
     // so config 5 level 2 moves more bytes than the byte columns (0.79 vs 0.76 ms) and levels 3-5
     // are several times slower (up to 4^5 configurations per test)
-    const bool bitsn = d >= 2 && c->bits_ready && maxdim <= 4 && getenv("FBN_CI_BITSN");
+    const bool bitsn0 = d >= 2 && c->bits_ready && maxdim <= 4 && getenv("FBN_CI_BITSN");
+    // d = 2 within a PC run (level-0 pair tables recorded), every state count <= 4, the bit-sliced
+    // store built: derived counting of the leading cells (ci_kernels.hip MODE 3; FBN_CI_NO_DER2 = 1
+    // takes the 2-bit packed histogram kernel instead)
+    const bool der2 = d == 2 && c->bits_ready && maxdim <= 4 && c->pair_mode == 2 && c->pairs_recorded &&
+                      !global_tables && !getenv("FBN_CI_NO_DER2");
+    const bool bitsn = bitsn0 || der2;
     // decisions only: the decision band up to this batch's largest df ((maxdim-1)^2 maxdim^d)
     const double *hband = nullptr;
     int hnband = 0;
@@ -1790,7 +1797,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
                                  counts_dev, lds, grid, gscratch, c->stats.as<unsigned long long>(),
                                  bitsn ? c->bits.as<uint32_t>() : nullptr, c->brow.as<int32_t>(), c->bits_W, hband,
                                  hnband, pk ? c->pack2.as<uint32_t>() : nullptr, c->pack2_W, c->counts_stride, tab,
-                                 tstride, split, split_grid, s);
+                                 tstride, split, split_grid, der2 ? c->pairtab.as<int32_t>() : nullptr, c->nvars, s);
     if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci kernel launch: %s", hipGetErrorString(e));
     if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
     return FBN_OK;
@@ -1888,6 +1895,12 @@ int fbn_ci_debug_counts(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, i
             std::copy(rec.begin() + t * 64, rec.begin() + t * 64 + std::min<int64_t>(cells, cap), counts + t * cap);
         }
         return FBN_OK;
+    }
+    if (d == 2) {  // a PC run's level 2 has its level-0 pair tables (derived counting, ci_kernels.hip MODE 3)
+        fbn::CiBatchStats st{0, 0};
+        for (int v = 0; v < nv; ++v) st.maxdim = std::max(st.maxdim, (int)c->dims[v]);
+        if (!c->pairs_recorded && st.maxdim <= 4 && c->N >= 4096 && (rc = level0())) return rc;
+        if (c->pairs_recorded) fbn::CiSetPairMode(c, 2);
     }
     if ((rc = c->counts.ensure((size_t)n * cap * 4))) return rc;
     FBN_HIP(hipMemsetAsync(c->counts.p, 0, (size_t)n * cap * 4, c->stream));  // cells beyond a table: 0

@@ -26,6 +26,7 @@ namespace {
 // G^2 terms buffered per chunk of cells (LDS doubles) before the in-order sum
 constexpr int kTermChunk = 1024;
 constexpr long long kWideTests = 512;  // batches up to this size: 1024-thread workgroups
+constexpr int kDerivedInts = 256;      // MODE 3: the four full 3-way tables (4 x 64 ints) after the terms
 
 // sub-histogram copies per wave for a table of `cells` > 16 cells (0: one shared table, beyond
 // 64 KB of LDS for the 4 waves' copies): 4 for small tables (config-5 level 2, <= 256 cells:
@@ -72,7 +73,239 @@ struct CiArgs {
     int32_t *tab;
     long long tstride;
     int split;
+    // MODE 3 (d = 2, bit-sliced, derived): the pair tables of this PC run's level 0 (every pair u < v
+    // of the nvars variables, [value of u][value of v], ci_bits.hip pair_table)
+    const int32_t *pairtab;
+    int nvars;
 };
+
+// ---- MODE 3: tests with two conditioning variables (z1, z2), every state count <= 4, from the
+// bit-sliced store, counting only LEADING cells (values 0 .. d-2 of each variable; the masks of a
+// variable partition the samples, so the last value of any variable follows by subtraction):
+//   L4[c1][c2][a][b] = sum popcount(x_a & y_b & z1_c1 & z2_c2)      the 4-way table's leading cells
+//   the leading cells of the four 3-way tables (x, y | z1), (x, y | z2), (z1, z2, x), (z1, z2, y)
+// then every 3-way table is completed from its leading cells and the pair tables level 0 recorded
+// (full 2-way tables), and the 4-way table from its leading cells and the four 3-way tables --
+// each step fills the cells whose last index is at its last value from cells already known:
+//   G[i][j][MK] = P_ij - sum_k<MK G[i][j][k];  G[i][MJ][k] = P_ik - sum_j<MJ;  G[MI][j][k] = P_jk - sum_i<MI
+// Exact integers: the table is Counts3D's (src/CellTable.cpp:268-291, z = c1 * dz2 + c2) cell for
+// cell, so the G^2 epilogue is the histogram kernel's own.  Per 32 samples: <= 54 AND + popcount
+// pairs per wave (wave c1 < 3: the 4-way and three 3-way tables of its z1 value; wave 3: (x, y | z2))
+// instead of 32 LDS-atomic binnings.
+__device__ __forceinline__ int pair_at(const int32_t *__restrict__ pairtab, int nvars, const int32_t *__restrict__ dims,
+                                       int u, int a, int v, int b) {
+    const int i = u < v ? u : v, j = u < v ? v : u;
+    const int32_t *T = pairtab + 16 * ((long long)i * nvars - (long long)i * (i + 1) / 2 + (j - i - 1));
+    return u < v ? T[a * dims[v] + b] : T[b * dims[u] + a];
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// hist: the test's table (zeroed); F: 4 x 64 ints of LDS for the 3-way tables
+__device__ __forceinline__ void derived4(const CiArgs &A, int x, int y, int z1, int z2, int dx, int dy,
+                                      int32_t *__restrict__ hist, int32_t *__restrict__ F, int tid) {
+    typedef __attribute__((ext_vector_type(4))) unsigned u4;
+    const long long W = A.W;
+    const int32_t *dims = A.dims;
+    const int d1 = dims[z1], d2 = dims[z2];
+    const int MX = dx - 1, MY = dy - 1, M1 = d1 - 1, M2 = d2 - 1;
+    const int wv = tid >> 6, lane = tid & 63;
+    const uint32_t *px = A.bits + (size_t)A.row0[x] * W, *py = A.bits + (size_t)A.row0[y] * W,
+                   *p1 = A.bits + (size_t)A.row0[z1] * W, *p2 = A.bits + (size_t)A.row0[z2] * W;
+    // F[0] = (z1, x, y), F[1] = (z2, x, y), F[2] = (z1, z2, x), F[3] = (z1, z2, y): [i][j][k] at
+    // (i * 4 + j) * 4 + k; the 4-way table in hist at ((c1 * d2 + c2) * dx + a) * dy + b
+    int32_t *Fxy1 = F, *Fxy2 = F + 64, *F12x = F + 128, *F12y = F + 192;
+    auto H = [&](int c1, int c2, int a, int b) -> int32_t & { return hist[((c1 * d2 + c2) * dx + a) * dy + b]; };
+    auto I3 = [](int i, int j, int k) { return (i * 4 + j) * 4 + k; };
+    uint32_t k4[3][3][3], ka[3][3], kc[3][3], kd[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            ka[i][j] = kc[i][j] = kd[i][j] = 0u;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) k4[i][j][k] = 0u;
+        }
+    const bool c1wave = wv < M1, ywave = wv == 3;  // (uniform per wave)
+    if (c1wave || ywave) {
+        const uint32_t *pz1 = p1 + (size_t)(c1wave ? wv : 0) * W;
+        for (long long w4 = lane; 4 * w4 < W; w4 += 64) {
+            u4 X[3], Y[3], Z[3], Z1 = {~0u, ~0u, ~0u, ~0u};
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+                if (a < MX) X[a] = *reinterpret_cast<const u4 *>(px + a * W + 4 * w4);
+#pragma unroll
+            for (int b = 0; b < 3; ++b)
+                if (b < MY) Y[b] = *reinterpret_cast<const u4 *>(py + b * W + 4 * w4);
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                if (c < M2) Z[c] = *reinterpret_cast<const u4 *>(p2 + c * W + 4 * w4);
+            if (c1wave) Z1 = *reinterpret_cast<const u4 *>(pz1 + 4 * w4);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (c1wave) {
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) {
+                        if (a >= MX) continue;
+                        const uint32_t xm = X[a][q] & Z1[q];
+#pragma unroll
+                        for (int c = 0; c < 3; ++c)
+                            if (c < M2) kc[c][a] += __builtin_popcount(xm & Z[c][q]);
+#pragma unroll
+                        for (int b = 0; b < 3; ++b) {
+                            if (b >= MY) continue;
+                            const uint32_t xy = xm & Y[b][q];
+                            ka[a][b] += __builtin_popcount(xy);
+#pragma unroll
+                            for (int c = 0; c < 3; ++c)
+                                if (c < M2) k4[c][a][b] += __builtin_popcount(xy & Z[c][q]);
+                        }
+                    }
+#pragma unroll
+                    for (int b = 0; b < 3; ++b) {
+                        if (b >= MY) continue;
+                        const uint32_t ym = Y[b][q] & Z1[q];
+#pragma unroll
+                        for (int c = 0; c < 3; ++c)
+                            if (c < M2) kd[c][b] += __builtin_popcount(ym & Z[c][q]);
+                    }
+                } else {  // wave 3: (x, y | z2)'s leading cells
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) {
+                        if (a >= MX) continue;
+#pragma unroll
+                        for (int b = 0; b < 3; ++b) {
+                            if (b >= MY) continue;
+                            const uint32_t xy = X[a][q] & Y[b][q];
+#pragma unroll
+                            for (int c = 0; c < 3; ++c)
+                                if (c < M2) k4[c][a][b] += __builtin_popcount(xy & Z[c][q]);
+                        }
+                    }
+                }
+            }
+        }
+        // wave totals of the leading cells into the tables
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    if (c >= M2 || a >= MX || b >= MY) continue;
+                    const uint32_t v = wave_sum(k4[c][a][b]);
+                    if (lane == 0) {
+                        if (c1wave) H(wv, c, a, b) = (int32_t)v;
+                        else Fxy2[I3(c, a, b)] = (int32_t)v;
+                    }
+                }
+        if (c1wave) {
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int b = 0; b < 3; ++b)
+                    if (a < MX && b < MY) {
+                        const uint32_t v = wave_sum(ka[a][b]);
+                        if (lane == 0) Fxy1[I3(wv, a, b)] = (int32_t)v;
+                    }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+#pragma unroll
+                for (int a = 0; a < 3; ++a)
+                    if (c < M2 && a < MX) {
+                        const uint32_t v = wave_sum(kc[c][a]);
+                        if (lane == 0) F12x[I3(wv, c, a)] = (int32_t)v;
+                    }
+#pragma unroll
+                for (int b = 0; b < 3; ++b)
+                    if (c < M2 && b < MY) {
+                        const uint32_t v = wave_sum(kd[c][b]);
+                        if (lane == 0) F12y[I3(wv, c, b)] = (int32_t)v;
+                    }
+            }
+        }
+    }
+    __syncthreads();
+    // the four 3-way tables, one per wave: G[i][j][k] over (vi, vj, vk) with dims (DI, DJ, DK)
+    {
+        const int t = wv;
+        int vi, vj, vk;
+        int32_t *G;
+        if (t == 0) vi = z1, vj = x, vk = y, G = Fxy1;
+        else if (t == 1) vi = z2, vj = x, vk = y, G = Fxy2;
+        else if (t == 2) vi = z1, vj = z2, vk = x, G = F12x;
+        else vi = z1, vj = z2, vk = y, G = F12y;
+        const int DI = dims[vi], DJ = dims[vj], DK = dims[vk], MI = DI - 1, MJ = DJ - 1, MK = DK - 1;
+        auto P = [&](int u, int a, int v, int b) { return pair_at(A.pairtab, A.nvars, dims, u, a, v, b); };
+        // step 1: G[i][j][MK], i < MI, j < MJ
+        if (lane < MI * MJ) {
+            const int i = lane / MJ, j = lane % MJ;
+            int32_t r = P(vi, i, vj, j);
+            for (int k = 0; k < MK; ++k) r -= G[I3(i, j, k)];
+            G[I3(i, j, MK)] = r;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes done (one wave per table)
+        __builtin_amdgcn_wave_barrier();
+        // step 2: G[i][MJ][k], i < MI, every k
+        if (lane < MI * DK) {
+            const int i = lane / DK, k = lane % DK;
+            int32_t r = P(vi, i, vk, k);
+            for (int j = 0; j < MJ; ++j) r -= G[I3(i, j, k)];
+            G[I3(i, MJ, k)] = r;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        // step 3: G[MI][j][k], every j, k
+        if (lane < DJ * DK) {
+            const int j = lane / DK, k = lane % DK;
+            int32_t r = P(vj, j, vk, k);
+            for (int i = 0; i < MI; ++i) r -= G[I3(i, j, k)];
+            G[I3(MI, j, k)] = r;
+        }
+    }
+    __syncthreads();
+    // the 4-way table T[c1][c2][a][b] from its leading cells and the 3-way tables (wave 0)
+    if (wv == 0) {
+        // step 1: T[c1][c2][a][MY] = F12x[c1][c2][a] - sum_b<MY
+        if (lane < M1 * M2 * MX) {
+            const int c1 = lane / (M2 * MX), c2 = (lane / MX) % M2, a = lane % MX;
+            int32_t r = F12x[I3(c1, c2, a)];
+            for (int b = 0; b < MY; ++b) r -= H(c1, c2, a, b);
+            H(c1, c2, a, MY) = r;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        // step 2: T[c1][c2][MX][b] = F12y[c1][c2][b] - sum_a<MX (every b)
+        if (lane < M1 * M2 * dy) {
+            const int c1 = lane / (M2 * dy), c2 = (lane / dy) % M2, b = lane % dy;
+            int32_t r = F12y[I3(c1, c2, b)];
+            for (int a = 0; a < MX; ++a) r -= H(c1, c2, a, b);
+            H(c1, c2, MX, b) = r;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        // step 3: T[c1][M2][a][b] = Fxy1[c1][a][b] - sum_c2<M2 (every a, b)
+        if (lane < M1 * dx * dy) {
+            const int c1 = lane / (dx * dy), a = (lane / dy) % dx, b = lane % dy;
+            int32_t r = Fxy1[I3(c1, a, b)];
+            for (int c2 = 0; c2 < M2; ++c2) r -= H(c1, c2, a, b);
+            H(c1, M2, a, b) = r;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        // step 4: T[M1][c2][a][b] = Fxy2[c2][a][b] - sum_c1<M1 (every c2, a, b: up to 64 cells)
+        if (lane < d2 * dx * dy) {
+            const int c2 = lane / (dx * dy), a = (lane / dy) % dx, b = lane % dy;
+            int32_t r = Fxy2[I3(c2, a, b)];
+            for (int c1 = 0; c1 < M1; ++c1) r -= H(c1, c2, a, b);
+            H(M1, c2, a, b) = r;
+        }
+    }
+}
 
 // BITS: count from the bit-sliced store (A.bits); a separate instantiation, so the byte-column
 // kernel keeps its register budget (74 VGPRs vs 178 with the bit-sliced counters compiled in).
@@ -132,7 +365,9 @@ __global__ __launch_bounds__(BS) void ci_g2_kernel(CiArgs A) {
         if (nsub > 1 && !BITS && MODE != 2)
             for (int c = tid; c < nsub * sstr; c += BS) sub[c] = 0;
         __syncthreads();
-        if (BITS) {
+        if (BITS && MODE == 3) {
+            if constexpr (D == 2) derived4(A, x, y, zv[0], zv[1], dx, dy, hist, smem + term_off + 2 * tc, tid);
+        } else if (BITS) {
             // bit-sliced counting: wave w takes the prefixes p = w, w + 4, ... of the z-configuration
             // (values of z_1 .. z_{d-1}; the last conditioning variable is the fastest digit, so
             // configuration k = p * dl + c for its value c).  Per 4-word step: m = AND of the prefix's
@@ -492,7 +727,7 @@ extern "C" size_t fbn_ci_lds_bytes(int dimz, int dx, int dy) {
     const size_t nsub = 4 * kl;
     size_t ints = ((cells + 3) & ~(size_t)3) + nsub * (cells | 1) + (size_t)dimz * (dx + dy + 2);
     ints = (ints + 1) & ~(size_t)1;
-    return ints * 4 + std::min<size_t>(cells, kTermChunk) * 8;
+    return ints * 4 + std::min<size_t>(cells, kTermChunk) * 8 + kDerivedInts * 4;
 }
 
 extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, const int32_t *items, long long N,
@@ -501,10 +736,15 @@ extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, co
                                     int32_t *gscratch, unsigned long long *stats, const uint32_t *bits,
                                     const int32_t *row0, long long W, const double *band, int nband,
                                     const uint32_t *pk, long long PW, long long cstride, int32_t *tab,
-                                    long long tstride, int split, int split_grid, hipStream_t stream) {
+                                    long long tstride, int split, int split_grid, const int32_t *pairtab, int nvars,
+                                    hipStream_t stream) {
     CiArgs a{cols, dims, items, N, n, alpha, g2, df, p, indep, counts, gscratch, (long long)(lds_bytes / 4 + 1) & ~1ll,
-             stats, bits, row0, W, band, nband, pk, PW, cstride, tab, tstride, split};
+             stats, bits, row0, W, band, nband, pk, PW, cstride, tab, tstride, split, pairtab, nvars};
     if (gscratch) lds_bytes = 0;
+    if (pairtab && bits && d == 2) {  // MODE 3: derived bit-sliced counting (every state count <= 4)
+        hipLaunchKernelGGL((ci_g2_kernel<2, true, false, 256, 3>), dim3(grid), dim3(256), lds_bytes, stream, a);
+        return hipGetLastError();
+    }
     if (split > 1 && pk && !bits && !gscratch) {  // small batch: count in parts, then decide
         hipError_t e = hipMemsetAsync(tab, 0, (size_t)n * tstride * 4, stream);
         if (e != hipSuccess) return e;

@@ -26,6 +26,7 @@
 #include <map>
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
 #include <sstream>
 #include <string>
 
@@ -65,6 +66,8 @@ bool JTCodegenEligible(const JTPlanHost &plan, int64_t *entry_ops) {
 
 namespace {
 
+constexpr int kDefaultMerge = 0;  // FBN_JT_MERGE default (fast order)
+
 class JTGen {
   public:
     JTGen(const JTPlanHost &p, bool fast_order) : plan(p), fast(fast_order) {}
@@ -81,9 +84,19 @@ class JTGen {
     std::vector<int> okw_word, okw_pos, out_off;
     std::vector<int64_t> sep_row, init_off;
     std::vector<std::vector<int>> cand;
+    // fast order: the one clique each variable's evidence is entered in (its smallest holder): the
+    // indicator of an observed value multiplies the joint once, so every calibrated clique still
+    // holds P(clique, evidence) -- the other holders receive the zeros through their messages
+    // (running intersection: the path to the home clique carries the variable)
+    std::vector<int> home;
     int nobs = 0;
     // op boundary (+ diagnostic cycle stamp of op category k when FBN_JT_PROFILE is set)
     bool profile = false;
+    // fast order, op regions merged (FBN_JT_MERGE bits): 1 = a clique's SepDis ops and marginals in
+    // one region (independent of each other: their latencies overlap), 2 = a Collect message's
+    // sums in one region with the next clique's product (small cliques)
+    int merge = 0;
+    bool in_merged = false;  // the current op's closing boundary is left out
     int min_waves = 1;
     bool iv_lds = true;
     std::string B(int k) const {
@@ -118,6 +131,10 @@ class JTGen {
         return idx;
     }
     void Init(const std::string &P, int c);
+    // fast order: Init and every multiplication of the clique fused into one op (per entry the
+    // initial potential x the home-evidence indicators x each message), ILP over all entries
+    void InitProd(const std::string &P, int c, const std::vector<std::pair<int, std::string>> &kids, int up,
+                  const std::string &upM);
     void Mul(const std::string &P, int c, int s, const std::string &M);
     void SepCol(const std::string &P, int c, int s, bool store);
     void DMul(const std::string &P, int c, int s, const std::string &M);
@@ -162,8 +179,11 @@ void JTGen::Init(const std::string &P, int c) {
     const Table &t = plan.cliques[c];
     const int nv = (int)t.vars.size();
     // per (variable, value) "allowed by the evidence" lane masks, then one AND chain per entry
+    std::vector<bool> ev_here(nv, true);  // variables whose evidence this table carries
+    for (int j = 0; j < nv; ++j) ev_here[j] = !fast || home[t.vars[j]] == c;
     for (int j = 0; j < nv; ++j) {
         const int v = t.vars[j];
+        if (!ev_here[j]) continue;
         for (int d = 0; d < plan.dom[v]; ++d)
             o << (d ? " " : "        ") << "const bool k" << P << c << "_" << j << "_" << d << " = (okw" << okw_word[v] << " >> "
               << okw_pos[v] + d << ") & 1u;";
@@ -185,19 +205,81 @@ void JTGen::Init(const std::string &P, int c) {
         for (int64_t e = b0; e < std::min(T, b0 + kB); ++e) {
             std::ostringstream cond;
             int64_t r = e;
+            bool any = false;
             for (int j = 0; j < nv; ++j) {
                 const int64_t dgt = r / t.cum[j];
                 r %= t.cum[j];
-                cond << (j ? " && " : "") << "k" << P << c << "_" << j << "_" << dgt;
+                if (!ev_here[j]) continue;
+                cond << (any ? " && " : "") << "k" << P << c << "_" << j << "_" << dgt;
+                any = true;
             }
-            o << "        " << (e < kRegEntries ? "double " : "") << N(P, c, e) << " = sel(" << cond.str() << ", w" << P
-              << c << "_" << e << ");";
+            o << "        " << (e < kRegEntries ? "double " : "") << N(P, c, e) << " = ";
+            if (any) o << "sel(" << cond.str() << ", w" << P << c << "_" << e << ");";
+            else o << "w" << P << c << "_" << e << ";";
             if (!fast) o << " s_" << P << c << " += " << N(P, c, e) << ";";
             o << "\n";
         }
         o << "        __builtin_amdgcn_sched_barrier(0);\n";
     }
     if (!fast) o << "        den = s_" << P << c << "; y = 1.0 / den; bad |= den_bad(den);\n";
+    o << B(2);
+    normed = false;
+}
+
+void JTGen::InitProd(const std::string &P, int c, const std::vector<std::pair<int, std::string>> &kids, int up,
+                     const std::string &upM) {
+    const Table &t = plan.cliques[c];
+    const int nv = (int)t.vars.size();
+    // 0.0 / 1.0 indicators of the home variables' allowed values (x * 1.0 == x, x * 0.0 == 0 for the
+    // finite potentials: the masking of the reference's reduction, one multiply instead of a select)
+    std::vector<bool> ev_here(nv, false);
+    for (int j = 0; j < nv; ++j) ev_here[j] = home[t.vars[j]] == c;
+    for (int j = 0; j < nv; ++j) {
+        if (!ev_here[j]) continue;
+        const int v = t.vars[j];
+        for (int d = 0; d < plan.dom[v]; ++d)
+            o << (d ? " " : "        ") << "const double i" << P << c << "_" << j << "_" << d << " = (double)((okw"
+              << okw_word[v] << " >> " << okw_pos[v] + d << ") & 1u);";
+        o << "\n";
+    }
+    std::vector<std::vector<int64_t>> kidx(kids.size());
+    for (size_t i = 0; i < kids.size(); ++i) {
+        const Table &sp = plan.seps[kids[i].first];
+        for (int64_t e = 0; e < t.size(); ++e) kidx[i].push_back(SepIndex(t, sp, e));
+    }
+    const int64_t Tup = up >= 0 ? plan.seps[up].size() : 0;
+    const int64_t kB = 16, T = t.size();
+    auto loads = [&](int64_t b0) {
+        if (b0 >= T) return;
+        o << "       ";
+        for (int64_t e = b0; e < std::min(T, b0 + kB); ++e)
+            o << " const double w" << P << c << "_" << e << " = IV(" << init_off[c] + e << ");";
+        o << "\n        __builtin_amdgcn_sched_barrier(0);\n";
+    };
+    loads(0);
+    for (int64_t b0 = 0; b0 < T; b0 += kB) {
+        loads(b0 + kB);
+        for (int64_t e = b0; e < std::min(T, b0 + kB); ++e) {
+            std::vector<std::string> f{"w" + P + std::to_string(c) + "_" + std::to_string(e)};
+            int64_t r = e;
+            for (int j = 0; j < nv; ++j) {
+                const int64_t dgt = r / t.cum[j];
+                r %= t.cum[j];
+                if (ev_here[j]) f.push_back("i" + P + std::to_string(c) + "_" + std::to_string(j) + "_" + std::to_string(dgt));
+            }
+            for (size_t i = 0; i < kids.size(); ++i)
+                f.push_back(kids[i].second + std::to_string(kids[i].first) + "_" + std::to_string(kidx[i][e]));
+            if (up >= 0) f.push_back(upM + std::to_string(up) + "_" + std::to_string(e % Tup));
+            // a balanced product tree (depth log2 of the factor count)
+            std::function<std::string(size_t, size_t)> prod = [&](size_t lo, size_t hi) -> std::string {
+                if (hi - lo == 1) return f[lo];
+                const size_t m = lo + (hi - lo) / 2;
+                return "(" + prod(lo, m) + " * " + prod(m, hi) + ")";
+            };
+            o << "        " << (e < kRegEntries ? "double " : "") << N(P, c, e) << " = " << prod(0, f.size()) << ";\n";
+        }
+        o << "        __builtin_amdgcn_sched_barrier(0);\n";
+    }
     o << B(2);
     normed = false;
 }
@@ -225,22 +307,18 @@ void JTGen::Mul(const std::string &P, int c, int s, const std::string &M) {
 void JTGen::SepCol(const std::string &P, int c, int s, bool store) {
     const Table &t = plan.cliques[c];
     const int64_t Ts = plan.seps[s].size(), Q = t.size() / Ts;
-    if (fast) {  // message = bin sums / their total (= the normalized table's sums), tree sums
-        std::vector<std::string> tot;
+    if (fast) {
+        // message = the raw bin sums (tree sums), never normalized: every later use is invariant to
+        // a per-case scale of it (the Distribute ratio a / old, the normalized marginals), and its
+        // values are likelihoods of the evidence below (<= 1); Marg range-checks the products
         for (int64_t j = 0; j < Ts; ++j) {
             std::vector<std::string> terms;
             for (int64_t q = 0; q < Q; ++q) terms.push_back(N(P, c, q * Ts + j));
-            o << "        const double mr" << s << "_" << j << " = " << TreeSum(terms) << ";\n";
-            tot.push_back("mr" + std::to_string(s) + "_" + std::to_string(j));
-        }
-        o << "        double ys" << s << "; { const double sm = " << TreeSum(tot) << "; ys" << s
-          << " = frcp(sm); bad |= den_bad(sm); }\n";
-        for (int64_t j = 0; j < Ts; ++j) {
-            o << "        const double mc" << s << "_" << j << " = mr" << s << "_" << j << " * ys" << s << ";";
+            o << "        const double mc" << s << "_" << j << " = " << TreeSum(terms) << ";";
             if (store) o << " W(" << sep_row[s] + j << "LL) = mc" << s << "_" << j << ";";
             o << "\n";
         }
-        o << B(4);
+        if (!in_merged) o << B(4);
         return;
     }
     for (int64_t j = 0; j < Ts; ++j) {
@@ -278,27 +356,19 @@ void JTGen::SepDis(const std::string &P, int c, int s, const std::string &old, b
     std::vector<std::vector<int64_t>> lists(sp.size());
     for (int64_t e = 0; e < t.size(); ++e) lists[SepIndex(t, sp, e)].push_back(e);
     if (fast) {
-        // bin sums a(j) as trees; the clique total S = sum_j a(j) (the same value as the sum over the
-        // table, without a T-long chain); md(j) = a(j) / S / old(j), 0 where old(j) == 0, with
-        // branch-free reciprocals (v_rcp_f64 + one Newton step) so the Ts quotients overlap
-        std::vector<std::string> as;
+        // bin sums a(j) as trees; md(j) = a(j) / old(j), 0 where old(j) == 0, with branch-free
+        // reciprocals (v_rcp_f64 + one Newton step) so the Ts quotients overlap; no normalization
+        // (the child's marginals are normalized at the end; values stay likelihoods <= 1)
         for (int64_t j = 0; j < sp.size(); ++j) {
             std::vector<std::string> terms;
             for (int64_t e : lists[j]) terms.push_back(N(P, c, e));
-            const std::string a = "sa" + std::to_string(s) + "_" + std::to_string(j);
-            o << "        const double " << a << " = " << TreeSum(terms) << ";\n";
-            as.push_back(a);
-        }
-        o << "        double ysd" << s << "; { const double sm = " << TreeSum(as) << "; ysd" << s
-          << " = frcp(sm); bad |= den_bad(sm); }\n";
-        for (int64_t j = 0; j < sp.size(); ++j) {
             o << "        double md" << s << "_" << j << "; { const double od = " << old << s << "_" << j
-              << "; const double q = (" << as[j] << " * ysd" << s << ") * frcp(od); md" << s << "_" << j
+              << "; const double q = " << TreeSum(terms) << " * frcp(od); md" << s << "_" << j
               << " = (od == 0.0) ? 0.0 : q; }";
             if (store) o << " W(" << sep_row[s] + j << "LL) = md" << s << "_" << j << ";";
             o << "\n";
         }
-        o << B(7);
+        if (!in_merged) o << B(7);
         return;
     }
     for (int64_t j = 0; j < sp.size(); ++j) {
@@ -371,7 +441,7 @@ void JTGen::Marg(const std::string &P, int c) {
         }
         o << "          if (ACT) {";
         for (int d = 0; d < dim; ++d) o << " OUT(" << out_off[v] + d << ") = dv(p" << d << ", tot, yt);";
-        o << " }\n        } }\n" << B(8);
+        o << " }\n        } }\n" << (in_merged ? std::string() : B(8));
     }
 }
 
@@ -379,6 +449,7 @@ int JTGen::Run(std::string &src, int64_t *wave_entries, std::vector<double> &ini
     const int nc = (int)plan.cliques.size(), ns = (int)plan.seps.size(), V = plan.num_nodes;
     if (const char *e = getenv("FBN_JT_REG_ENTRIES")) kRegEntries = std::max<int64_t>(1, atoll(e));  // tuning
     profile = getenv("FBN_JT_PROFILE") && atoi(getenv("FBN_JT_PROFILE")) != 0;  // diagnostic build
+    merge = fast ? (getenv("FBN_JT_MERGE") ? atoi(getenv("FBN_JT_MERGE")) : kDefaultMerge) : 0;  // (tuning)
     // occupancy: waves per SIMD the register allocation must allow (1: up to 512 registers)
     min_waves = getenv("FBN_JT_MIN_WAVES") ? std::max(1, atoi(getenv("FBN_JT_MIN_WAVES"))) : min_waves;
     // initial potentials: LDS copy per wave (1) or scalar loads from the constant buffer (0)
@@ -403,6 +474,10 @@ int JTGen::Run(std::string &src, int64_t *wave_entries, std::vector<double> &ini
     cand.assign(V, {});
     for (int c = 0; c < nc; ++c)
         for (int v : plan.cliques[c].vars) cand[v].push_back(c);
+    home.assign(V, -1);
+    for (int v = 0; v < V; ++v)
+        for (int q : cand[v])
+            if (home[v] < 0 || plan.cliques[q].size() < plan.cliques[home[v]].size()) home[v] = q;
     // traversal orders
     std::vector<int> post, pre;
     std::vector<std::pair<int, size_t>> st{{plan.root, 0}};
@@ -559,15 +634,25 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
                 for (int s : next)
                     if (!loaded_a[s]) Load("la", s), loaded_a[s] = true;
         }
-        o << B(1);
-        Init("t", c);
+        if (!in_merged) o << B(1);
+        in_merged = false;
         const auto &down = plan.clique_down[c];
-        for (size_t i = 0; i < down.size(); ++i) {
-            const int s = down[i];
-            Mul("t", c, s, loaded_a[s] ? "la" : "mc");
+        if (fast) {
+            std::vector<std::pair<int, std::string>> kids;
+            for (int s : down) kids.push_back({s, loaded_a[s] ? "la" : "mc"});
+            InitProd("t", c, kids, -1, "");
+        } else {
+            Init("t", c);
+            for (size_t i = 0; i < down.size(); ++i) {
+                const int s = down[i];
+                Mul("t", c, s, loaded_a[s] ? "la" : "mc");
+            }
         }
+        // merge the message's sums with the next clique's product when both are small
+        in_merged = fast && (merge & 2) && c != plan.root && k + 1 < post.size() && tsize(c) + tsize(post[k + 1]) <= 96;
         if (c != plan.root) SepCol("t", c, plan.clique_up[c], true);
     }
+    in_merged = false;
     // ---------------- Distribute, DFS pre-order (root continues from its Collect registers)
     // Register policy (kBudget fp64 values per lane):
     //  * the message to a first child stays in registers if that child's table, the message and
@@ -623,7 +708,13 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
         }
         o << B(1);
         std::string P = "t";
-        if (c != plan.root) {
+        if (c != plan.root && fast && early) {  // all messages in registers: one fused op
+            P = "u";
+            if (!md_reg[up] && !loaded_d[up]) Load("ld", up), loaded_d[up] = true, o << B(1);
+            std::vector<std::pair<int, std::string>> kids;
+            for (int s : plan.clique_down[c]) kids.push_back({s, "lb"});
+            InitProd(P, c, kids, up, md_reg[up] ? "md" : "ld");
+        } else if (c != plan.root) {
             P = "u";  // recompute the Collect table (same ops, same order -> same bits)
             Init(P, c);
             for (int s : plan.clique_down[c]) {
@@ -637,11 +728,14 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
         // consumers of the normalized table: one SepDis per child, one marginal per variable
         // (fast order: each SepDis takes the clique total from its own bin sums)
         if (!fast && down.size() + plan.cliques[c].vars.size() >= 2) Normalize(P, c);
+        in_merged = fast && (merge & 1) && early;
         for (size_t i = 0; i < down.size(); ++i) {
             if (!early) Load("lc", down[i]), o << B(1);
             SepDis(P, c, down[i], early ? "lb" : "lc", !md_reg[down[i]]);
         }
         Marg(P, c);
+        if (in_merged) o << B(8);
+        in_merged = false;
     }
     for (int v = 0; v < V; ++v) {
         o << "        if (ACT && " << observed(v) << ") {";

@@ -440,3 +440,37 @@ def test_pc_stable_config5_full_size_vs_fixture():
     assert len(pc.edges) == ref["num_edges"] and len(pc.sepset) == ref["num_sepsets"]
     assert pc_digest(pc.edges, pc.sepset) == {k: ref[k] for k in ("edges_sha256", "sepsets_sha256")}
     assert pc.near_alpha == 0
+
+
+@pytest.mark.parametrize("ns", [4096, 5000, 100003])
+def test_level2_derived_counting_matches_histogram(ns, monkeypatch):
+    """d = 2 tests inside a PC run (level-0 pair tables recorded), every state count <= 4: the
+    derived bit-sliced counting (ci_kernels.hip MODE 3: leading 4-way and 3-way cells by popcount,
+    the rest by subtraction from the pair tables) gives the histogram kernel's tables exactly
+    (FBN_CI_NO_DER2), hence the same df, G^2, p and decisions bit for bit, and the oracle's."""
+    rng = np.random.default_rng(ns + 29)
+    dims = np.array([2, 3, 4, 1, 4, 3, 2, 4, 3, 4, 2], np.int32)
+    cols = np.stack([rng.integers(0, d, ns) for d in dims]).astype(np.uint8)
+    cols[4] = (cols[2] + cols[1]) % 4
+    cols[9] = (cols[7] * cols[0] + cols[5]) % 4
+    ci = F.IndependenceTest(F.Dataset(columns=cols, dims=dims), 0.05, device=0)
+    od = O.OracleDataset(columns=cols, dims=dims)
+    nv = len(dims)
+    items = np.array([[x, y, a, b] for x in range(nv) for y in range(x + 1, nv) for a in range(nv)
+                      for b in range(a + 1, nv) if len({x, y, a, b}) == 4][::7], np.int32)
+    cap = 256
+    got = ci.production_counts(items, 2, cap)  # records level 0's pair tables first
+    g2, df, p, ind = ci.run(items, 2)
+    monkeypatch.setenv("FBN_CI_NO_DER2", "1")
+    ref = ci.production_counts(items, 2, cap)
+    g2b, dfb, pb, indb = ci.run(items, 2)
+    np.testing.assert_array_equal(got, ref)
+    np.testing.assert_array_equal(df, dfb)
+    np.testing.assert_array_equal(g2, g2b)
+    np.testing.assert_array_equal(p, pb)
+    np.testing.assert_array_equal(ind, indb)
+    for k in range(0, len(items), max(1, len(items) // 12)):
+        it = [int(v) for v in items[k]]
+        r = od.ci_test(it[0], it[1], it[2:])
+        assert df[k] == r["df"] and ind[k] == r["is_independent"]
+        assert abs(g2[k] - r["g2"]) <= G2_TOL * max(1.0, abs(r["g2"]))
