@@ -77,6 +77,7 @@ struct CiArgs {
     // of the nvars variables, [value of u][value of v], ci_bits.hip pair_table)
     const int32_t *pairtab;
     int nvars;
+    int dbg;  // diagnostic ablations (FBN_CI_DER2_DBG): bit 0 = MODE 3 skips its counting
 };
 
 // ---- MODE 3: tests with two conditioning variables (z1, z2), every state count <= 4, from the
@@ -105,10 +106,135 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
+// the leading cells of one test (see above) for MX = dx - 1, MY = dy - 1, M2 = dz2 - 1 values: wave
+// c1 < M1 counts the 4-way cells and three 3-way tables of its z1 value, wave 3 the (x, y | z2)
+// table; wave totals into the 4-way table (hist) and the 3-way tables (F..., [i][j][k] at (4i+j)4+k)
+template <int MX, int MY, int M2>
+__device__ __forceinline__ void lead4(const uint32_t *__restrict__ px, const uint32_t *__restrict__ py,
+                                      const uint32_t *__restrict__ p1, const uint32_t *__restrict__ p2, long long W,
+                                      int M1, int wv, int lane, int32_t *__restrict__ hist, int d2, int dx, int dy,
+                                      int32_t *__restrict__ Fxy1, int32_t *__restrict__ Fxy2,
+                                      int32_t *__restrict__ F12x, int32_t *__restrict__ F12y) {
+    typedef __attribute__((ext_vector_type(4))) unsigned u4;
+    constexpr int AX = MX > 0 ? MX : 1, AY = MY > 0 ? MY : 1, A2 = M2 > 0 ? M2 : 1;
+    // waves 0-2: (z1 value c1, word part) units -- with fewer than 3 z1 leading values the words are
+    // split between waves (M1 = 1: 3 parts), so a binary z1 does not leave two waves idle; wave 3
+    // counts (x, y | z2) over all words.  Parts add into the (zeroed) LDS tables atomically.
+    const int P = M1 > 0 ? 3 / M1 : 0;
+    const bool c1wave = wv < M1 * P, ywave = wv == 3;  // (uniform per wave)
+    if (!c1wave && !ywave) return;
+    const int c1 = c1wave ? wv % M1 : 0, part = c1wave ? wv / M1 : 0, nparts = c1wave ? P : 1;
+    uint32_t k4[A2][AX][AY], ka[AX][AY], kc[A2][AX], kd[A2][AY];
+#pragma unroll
+    for (int a = 0; a < AX; ++a) {
+#pragma unroll
+        for (int b = 0; b < AY; ++b) {
+            ka[a][b] = 0u;
+#pragma unroll
+            for (int c = 0; c < A2; ++c) k4[c][a][b] = 0u;
+        }
+#pragma unroll
+        for (int c = 0; c < A2; ++c) kc[c][a] = 0u;
+    }
+#pragma unroll
+    for (int c = 0; c < A2; ++c)
+#pragma unroll
+        for (int b = 0; b < AY; ++b) kd[c][b] = 0u;
+    if (c1wave) {
+        const uint32_t *pz1 = p1 + (size_t)c1 * W;
+        for (long long w4 = lane + 64 * part; 4 * w4 < W; w4 += 64 * nparts) {
+            u4 X[AX], Y[AY], Z[A2];
+#pragma unroll
+            for (int a = 0; a < MX; ++a) X[a] = *reinterpret_cast<const u4 *>(px + a * W + 4 * w4);
+#pragma unroll
+            for (int b = 0; b < MY; ++b) Y[b] = *reinterpret_cast<const u4 *>(py + b * W + 4 * w4);
+#pragma unroll
+            for (int c = 0; c < M2; ++c) Z[c] = *reinterpret_cast<const u4 *>(p2 + c * W + 4 * w4);
+            const u4 Z1 = *reinterpret_cast<const u4 *>(pz1 + 4 * w4);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                for (int a = 0; a < MX; ++a) {
+                    const uint32_t xm = X[a][q] & Z1[q];
+#pragma unroll
+                    for (int c = 0; c < M2; ++c) kc[c][a] += __builtin_popcount(xm & Z[c][q]);
+#pragma unroll
+                    for (int b = 0; b < MY; ++b) {
+                        const uint32_t xy = xm & Y[b][q];
+                        ka[a][b] += __builtin_popcount(xy);
+#pragma unroll
+                        for (int c = 0; c < M2; ++c) k4[c][a][b] += __builtin_popcount(xy & Z[c][q]);
+                    }
+                }
+#pragma unroll
+                for (int b = 0; b < MY; ++b) {
+                    const uint32_t ym = Y[b][q] & Z1[q];
+#pragma unroll
+                    for (int c = 0; c < M2; ++c) kd[c][b] += __builtin_popcount(ym & Z[c][q]);
+                }
+            }
+        }
+    } else {  // wave 3: (x, y | z2)'s leading cells
+        for (long long w4 = lane; 4 * w4 < W; w4 += 64) {
+            u4 X[AX], Y[AY], Z[A2];
+#pragma unroll
+            for (int a = 0; a < MX; ++a) X[a] = *reinterpret_cast<const u4 *>(px + a * W + 4 * w4);
+#pragma unroll
+            for (int b = 0; b < MY; ++b) Y[b] = *reinterpret_cast<const u4 *>(py + b * W + 4 * w4);
+#pragma unroll
+            for (int c = 0; c < M2; ++c) Z[c] = *reinterpret_cast<const u4 *>(p2 + c * W + 4 * w4);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int a = 0; a < MX; ++a)
+#pragma unroll
+                    for (int b = 0; b < MY; ++b) {
+                        const uint32_t xy = X[a][q] & Y[b][q];
+#pragma unroll
+                        for (int c = 0; c < M2; ++c) k4[c][a][b] += __builtin_popcount(xy & Z[c][q]);
+                    }
+        }
+    }
+    auto I3 = [](int i, int j, int k) { return (i * 4 + j) * 4 + k; };
+#pragma unroll
+    for (int c = 0; c < M2; ++c)
+#pragma unroll
+        for (int a = 0; a < MX; ++a)
+#pragma unroll
+            for (int b = 0; b < MY; ++b) {
+                const uint32_t v = wave_sum(k4[c][a][b]);
+                if (lane == 0) {
+                    if (c1wave) atomicAdd(&hist[((c1 * d2 + c) * dx + a) * dy + b], (int32_t)v);
+                    else Fxy2[I3(c, a, b)] = (int32_t)v;
+                }
+            }
+    if (c1wave) {
+#pragma unroll
+        for (int a = 0; a < MX; ++a)
+#pragma unroll
+            for (int b = 0; b < MY; ++b) {
+                const uint32_t v = wave_sum(ka[a][b]);
+                if (lane == 0) atomicAdd(&Fxy1[I3(c1, a, b)], (int32_t)v);
+            }
+#pragma unroll
+        for (int c = 0; c < M2; ++c) {
+#pragma unroll
+            for (int a = 0; a < MX; ++a) {
+                const uint32_t v = wave_sum(kc[c][a]);
+                if (lane == 0) atomicAdd(&F12x[I3(c1, c, a)], (int32_t)v);
+            }
+#pragma unroll
+            for (int b = 0; b < MY; ++b) {
+                const uint32_t v = wave_sum(kd[c][b]);
+                if (lane == 0) atomicAdd(&F12y[I3(c1, c, b)], (int32_t)v);
+            }
+        }
+    }
+}
+
 // hist: the test's table (zeroed); F: 4 x 64 ints of LDS for the 3-way tables
 __device__ __forceinline__ void derived4(const CiArgs &A, int x, int y, int z1, int z2, int dx, int dy,
                                       int32_t *__restrict__ hist, int32_t *__restrict__ F, int tid) {
-    typedef __attribute__((ext_vector_type(4))) unsigned u4;
     const long long W = A.W;
     const int32_t *dims = A.dims;
     const int d1 = dims[z1], d2 = dims[z2];
@@ -121,113 +247,22 @@ __device__ __forceinline__ void derived4(const CiArgs &A, int x, int y, int z1, 
     int32_t *Fxy1 = F, *Fxy2 = F + 64, *F12x = F + 128, *F12y = F + 192;
     auto H = [&](int c1, int c2, int a, int b) -> int32_t & { return hist[((c1 * d2 + c2) * dx + a) * dy + b]; };
     auto I3 = [](int i, int j, int k) { return (i * 4 + j) * 4 + k; };
-    uint32_t k4[3][3][3], ka[3][3], kc[3][3], kd[3][3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            ka[i][j] = kc[i][j] = kd[i][j] = 0u;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) k4[i][j][k] = 0u;
-        }
-    const bool c1wave = wv < M1, ywave = wv == 3;  // (uniform per wave)
-    if (c1wave || ywave) {
-        const uint32_t *pz1 = p1 + (size_t)(c1wave ? wv : 0) * W;
-        for (long long w4 = lane; 4 * w4 < W; w4 += 64) {
-            u4 X[3], Y[3], Z[3], Z1 = {~0u, ~0u, ~0u, ~0u};
-#pragma unroll
-            for (int a = 0; a < 3; ++a)
-                if (a < MX) X[a] = *reinterpret_cast<const u4 *>(px + a * W + 4 * w4);
-#pragma unroll
-            for (int b = 0; b < 3; ++b)
-                if (b < MY) Y[b] = *reinterpret_cast<const u4 *>(py + b * W + 4 * w4);
-#pragma unroll
-            for (int c = 0; c < 3; ++c)
-                if (c < M2) Z[c] = *reinterpret_cast<const u4 *>(p2 + c * W + 4 * w4);
-            if (c1wave) Z1 = *reinterpret_cast<const u4 *>(pz1 + 4 * w4);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (c1wave) {
-#pragma unroll
-                    for (int a = 0; a < 3; ++a) {
-                        if (a >= MX) continue;
-                        const uint32_t xm = X[a][q] & Z1[q];
-#pragma unroll
-                        for (int c = 0; c < 3; ++c)
-                            if (c < M2) kc[c][a] += __builtin_popcount(xm & Z[c][q]);
-#pragma unroll
-                        for (int b = 0; b < 3; ++b) {
-                            if (b >= MY) continue;
-                            const uint32_t xy = xm & Y[b][q];
-                            ka[a][b] += __builtin_popcount(xy);
-#pragma unroll
-                            for (int c = 0; c < 3; ++c)
-                                if (c < M2) k4[c][a][b] += __builtin_popcount(xy & Z[c][q]);
-                        }
-                    }
-#pragma unroll
-                    for (int b = 0; b < 3; ++b) {
-                        if (b >= MY) continue;
-                        const uint32_t ym = Y[b][q] & Z1[q];
-#pragma unroll
-                        for (int c = 0; c < 3; ++c)
-                            if (c < M2) kd[c][b] += __builtin_popcount(ym & Z[c][q]);
-                    }
-                } else {  // wave 3: (x, y | z2)'s leading cells
-#pragma unroll
-                    for (int a = 0; a < 3; ++a) {
-                        if (a >= MX) continue;
-#pragma unroll
-                        for (int b = 0; b < 3; ++b) {
-                            if (b >= MY) continue;
-                            const uint32_t xy = X[a][q] & Y[b][q];
-#pragma unroll
-                            for (int c = 0; c < 3; ++c)
-                                if (c < M2) k4[c][a][b] += __builtin_popcount(xy & Z[c][q]);
-                        }
-                    }
-                }
-            }
-        }
-        // wave totals of the leading cells into the tables
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-#pragma unroll
-            for (int a = 0; a < 3; ++a)
-#pragma unroll
-                for (int b = 0; b < 3; ++b) {
-                    if (c >= M2 || a >= MX || b >= MY) continue;
-                    const uint32_t v = wave_sum(k4[c][a][b]);
-                    if (lane == 0) {
-                        if (c1wave) H(wv, c, a, b) = (int32_t)v;
-                        else Fxy2[I3(c, a, b)] = (int32_t)v;
-                    }
-                }
-        if (c1wave) {
-#pragma unroll
-            for (int a = 0; a < 3; ++a)
-#pragma unroll
-                for (int b = 0; b < 3; ++b)
-                    if (a < MX && b < MY) {
-                        const uint32_t v = wave_sum(ka[a][b]);
-                        if (lane == 0) Fxy1[I3(wv, a, b)] = (int32_t)v;
-                    }
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-#pragma unroll
-                for (int a = 0; a < 3; ++a)
-                    if (c < M2 && a < MX) {
-                        const uint32_t v = wave_sum(kc[c][a]);
-                        if (lane == 0) F12x[I3(wv, c, a)] = (int32_t)v;
-                    }
-#pragma unroll
-                for (int b = 0; b < 3; ++b)
-                    if (c < M2 && b < MY) {
-                        const uint32_t v = wave_sum(kd[c][b]);
-                        if (lane == 0) F12y[I3(wv, c, b)] = (int32_t)v;
-                    }
-            }
-        }
+    for (int i = tid; i < 256; i += 256) F[i] = 0;  // (parts of the 3-way tables add atomically)
+    __syncthreads();
+    // the leading cells by popcount: static loops per (MX, MY, M2) (runtime guards inside unrolled
+    // loops measured no faster than the histogram kernel: a branch per cell and word)
+    switch (A.dbg & 1 ? -1 : MX * 16 + MY * 4 + M2) {  // (dbg bit 0: counting skipped, diagnostic)
+#define FBN_L4(A_, B_, C_) \
+    case A_ * 16 + B_ * 4 + C_: \
+        lead4<A_, B_, C_>(px, py, p1, p2, W, M1, wv, lane, hist, d2, dx, dy, Fxy1, Fxy2, F12x, F12y); \
+        break;
+#define FBN_L4B(A_, B_) FBN_L4(A_, B_, 0) FBN_L4(A_, B_, 1) FBN_L4(A_, B_, 2) FBN_L4(A_, B_, 3)
+#define FBN_L4A(A_) FBN_L4B(A_, 0) FBN_L4B(A_, 1) FBN_L4B(A_, 2) FBN_L4B(A_, 3)
+        FBN_L4A(0) FBN_L4A(1) FBN_L4A(2) FBN_L4A(3)
+#undef FBN_L4A
+#undef FBN_L4B
+#undef FBN_L4
+    default: break;
     }
     __syncthreads();
     // the four 3-way tables, one per wave: G[i][j][k] over (vi, vj, vk) with dims (DI, DJ, DK)
@@ -739,7 +774,8 @@ extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, co
                                     long long tstride, int split, int split_grid, const int32_t *pairtab, int nvars,
                                     hipStream_t stream) {
     CiArgs a{cols, dims, items, N, n, alpha, g2, df, p, indep, counts, gscratch, (long long)(lds_bytes / 4 + 1) & ~1ll,
-             stats, bits, row0, W, band, nband, pk, PW, cstride, tab, tstride, split, pairtab, nvars};
+             stats, bits, row0, W, band, nband, pk, PW, cstride, tab, tstride, split, pairtab, nvars,
+             getenv("FBN_CI_DER2_DBG") ? atoi(getenv("FBN_CI_DER2_DBG")) : 0};
     if (gscratch) lds_bytes = 0;
     if (pairtab && bits && d == 2) {  // MODE 3: derived bit-sliced counting (every state count <= 4)
         hipLaunchKernelGGL((ci_g2_kernel<2, true, false, 256, 3>), dim3(grid), dim3(256), lds_bytes, stream, a);

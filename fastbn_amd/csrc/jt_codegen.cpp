@@ -66,7 +66,7 @@ bool JTCodegenEligible(const JTPlanHost &plan, int64_t *entry_ops) {
 
 namespace {
 
-constexpr int kDefaultMerge = 0;  // FBN_JT_MERGE default (fast order)
+constexpr int kDefaultMerge = 1;  // FBN_JT_MERGE default (fast order; round 5 sweep: -1..3 %)
 
 class JTGen {
   public:
@@ -89,6 +89,12 @@ class JTGen {
     // holds P(clique, evidence) -- the other holders receive the zeros through their messages
     // (running intersection: the path to the home clique carries the variable)
     std::vector<int> home;
+    // fast order: the separator a variable's marginal is summed from (its smallest holder when that
+    // is smaller than its smallest clique; -1: the clique): the calibrated separator belief is the
+    // parent's bin sums of its SepDis, P(separator, evidence) up to a per-case constant
+    std::vector<int> msep;
+    // fast order: a marginal (and the label of variable 0) from the terms of each value
+    void MargTerms(int v, const std::vector<std::vector<std::string>> &terms);
     int nobs = 0;
     // op boundary (+ diagnostic cycle stamp of op category k when FBN_JT_PROFILE is set)
     bool profile = false;
@@ -96,6 +102,7 @@ class JTGen {
     // one region (independent of each other: their latencies overlap), 2 = a Collect message's
     // sums in one region with the next clique's product (small cliques)
     int merge = 0;
+    int64_t init_batch = 16;  // fast order: entries per software-pipelined batch of the fused product
     bool in_merged = false;  // the current op's closing boundary is left out
     int min_waves = 1;
     bool iv_lds = true;
@@ -248,7 +255,7 @@ void JTGen::InitProd(const std::string &P, int c, const std::vector<std::pair<in
         for (int64_t e = 0; e < t.size(); ++e) kidx[i].push_back(SepIndex(t, sp, e));
     }
     const int64_t Tup = up >= 0 ? plan.seps[up].size() : 0;
-    const int64_t kB = 16, T = t.size();
+    const int64_t kB = init_batch, T = t.size();  // (FBN_JT_INIT_BATCH: tuning)
     auto loads = [&](int64_t b0) {
         if (b0 >= T) return;
         o << "       ";
@@ -362,11 +369,21 @@ void JTGen::SepDis(const std::string &P, int c, int s, const std::string &old, b
         for (int64_t j = 0; j < sp.size(); ++j) {
             std::vector<std::string> terms;
             for (int64_t e : lists[j]) terms.push_back(N(P, c, e));
-            o << "        double md" << s << "_" << j << "; { const double od = " << old << s << "_" << j
-              << "; const double q = " << TreeSum(terms) << " * frcp(od); md" << s << "_" << j
-              << " = (od == 0.0) ? 0.0 : q; }";
+            const std::string sa = "sa" + std::to_string(s) + "_" + std::to_string(j);
+            o << "        const double " << sa << " = " << TreeSum(terms) << ";";
+            o << " double md" << s << "_" << j << "; { const double od = " << old << s << "_" << j
+              << "; const double q = " << sa << " * frcp(od); md" << s << "_" << j << " = (od == 0.0) ? 0.0 : q; }";
             if (store) o << " W(" << sep_row[s] + j << "LL) = md" << s << "_" << j << ";";
             o << "\n";
+        }
+        // the marginals summed from this separator's calibrated belief (its bin sums)
+        for (size_t l = 0; l < sp.vars.size(); ++l) {
+            const int v = sp.vars[l];
+            if (msep[v] != s) continue;
+            std::vector<std::vector<std::string>> terms(plan.dom[v]);
+            for (int64_t j = 0; j < sp.size(); ++j)
+                terms[(j / sp.cum[l]) % sp.dims[l]].push_back("sa" + std::to_string(s) + "_" + std::to_string(j));
+            MargTerms(v, terms);
         }
         if (!in_merged) o << B(7);
         return;
@@ -382,6 +399,29 @@ void JTGen::SepDis(const std::string &P, int c, int s, const std::string &old, b
     o << B(7);
 }
 
+void JTGen::MargTerms(int v, const std::vector<std::vector<std::string>> &terms) {
+    const int dim = plan.dom[v];
+    o << "        if (!" << observed(v) << ") { // marginal of var " << v << "\n";
+    std::vector<std::string> ps;
+    for (int d = 0; d < dim; ++d) {
+        o << "          const double p" << d << " = " << TreeSum(terms[d]) << ";\n";
+        ps.push_back("p" + std::to_string(d));
+    }
+    o << "          const double tot = " << TreeSum(ps) << "; const double yt = frcp(tot); bad |= den_bad(tot);\n";
+    if (v == 0) {
+        // a near-tie (top two within 1e-12 relative) may break differently from the reference's exact
+        // values: the block is flagged for the exact pass
+        o << "          if (ACT) { int lab = 0; double mp = 0.0, m2 = 0.0;";
+        for (int d = 0; d < dim; ++d)
+            o << " { const double q = dv(p" << d << ", tot, yt); if (q > mp) { m2 = mp; mp = q; lab = " << d
+              << "; } else if (q > m2) m2 = q; }";
+        o << " labels[CS] = lab; bad |= (mp - m2 <= 1e-12 * mp) ? 1u : 0u; }\n";
+    }
+    o << "          if (ACT) {";
+    for (int d = 0; d < dim; ++d) o << " OUT(" << out_off[v] + d << ") = dv(p" << d << ", tot, yt);";
+    o << " }\n        }\n";
+}
+
 // GetProbabilitiesOneNode for every variable whose selected clique (first with the fewest reduced
 // variables) is c, and the label (ArgMax, strict '>' from 0; un-normalized if c reduces to one var)
 void JTGen::Marg(const std::string &P, int c) {
@@ -391,11 +431,14 @@ void JTGen::Marg(const std::string &P, int c) {
         const int dim = plan.dom[v];
         const int64_t cum = t.cum[j], bw = dim * cum, nhi = t.size() / bw;
         if (fast) {  // the smallest clique holding the variable (a calibrated tree: any gives the marginal)
-            int sel = cand[v][0];
-            for (int q : cand[v])
-                if (plan.cliques[q].size() < plan.cliques[sel].size()) sel = q;
-            if (sel != c) continue;
-            o << "        { const int b = 0;\n        if (!" << observed(v) << ") { // marginal of var " << v << "\n";
+            if (home[v] != c || msep[v] >= 0) continue;
+            std::vector<std::vector<std::string>> terms(dim);
+            for (int d = 0; d < dim; ++d)
+                for (int64_t hi = 0; hi < nhi; ++hi)
+                    for (int64_t l = 0; l < cum; ++l) terms[d].push_back(N(P, c, hi * bw + d * cum + l));
+            MargTerms(v, terms);
+            if (!in_merged) o << B(8);
+            continue;
         } else {
             // selection: first candidate clique with the fewest reduced variables (recomputed here)
             o << "        { int b = " << R(cand[v][0]) << ", sl = " << cand[v][0] << ";";
@@ -450,6 +493,7 @@ int JTGen::Run(std::string &src, int64_t *wave_entries, std::vector<double> &ini
     if (const char *e = getenv("FBN_JT_REG_ENTRIES")) kRegEntries = std::max<int64_t>(1, atoll(e));  // tuning
     profile = getenv("FBN_JT_PROFILE") && atoi(getenv("FBN_JT_PROFILE")) != 0;  // diagnostic build
     merge = fast ? (getenv("FBN_JT_MERGE") ? atoi(getenv("FBN_JT_MERGE")) : kDefaultMerge) : 0;  // (tuning)
+    init_batch = getenv("FBN_JT_INIT_BATCH") ? std::max<int64_t>(1, atoll(getenv("FBN_JT_INIT_BATCH"))) : 16;
     // occupancy: waves per SIMD the register allocation must allow (1: up to 512 registers)
     min_waves = getenv("FBN_JT_MIN_WAVES") ? std::max(1, atoi(getenv("FBN_JT_MIN_WAVES"))) : min_waves;
     // initial potentials: LDS copy per wave (1) or scalar loads from the constant buffer (0)
@@ -478,6 +522,13 @@ int JTGen::Run(std::string &src, int64_t *wave_entries, std::vector<double> &ini
     for (int v = 0; v < V; ++v)
         for (int q : cand[v])
             if (home[v] < 0 || plan.cliques[q].size() < plan.cliques[home[v]].size()) home[v] = q;
+    msep.assign(V, -1);
+    if (fast && !getenv("FBN_JT_NO_SEPMARG"))  // (diagnostic: marginals from cliques only)
+        for (int sp = 0; sp < ns; ++sp)
+            for (int v : plan.seps[sp].vars) {
+                const int64_t have = msep[v] >= 0 ? plan.seps[msep[v]].size() : plan.cliques[home[v]].size();
+                if (plan.seps[sp].size() < have) msep[v] = sp;
+            }
     // traversal orders
     std::vector<int> post, pre;
     std::vector<std::pair<int, size_t>> st{{plan.root, 0}};
@@ -602,7 +653,8 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
     o << B(0);
 
     // fp64 values per lane: table in flight + prefetched rows (FBN_JT_PREFETCH_BUDGET: tuning)
-    const int64_t kBudget = getenv("FBN_JT_PREFETCH_BUDGET") ? atoll(getenv("FBN_JT_PREFETCH_BUDGET")) : 200;
+    // (fast order: 260 -- round 5 sweep 150 / 200 / 260 / 320: 0.171 / 0.169 / 0.165 / 0.166 ms)
+    const int64_t kBudget = getenv("FBN_JT_PREFETCH_BUDGET") ? atoll(getenv("FBN_JT_PREFETCH_BUDGET")) : fast ? 260 : 200;
     auto tsize = [&](int c) { return plan.cliques[c].size(); };
     // ---------------- Collect, DFS post-order
     // loads of clique post[k]: its children's messages except a last child that is post[k-1]
