@@ -364,7 +364,7 @@ class JunctionTree(_Handle):
         geometry dict) -- for host-side checks of its tables (tests/tile_emulator.py)."""
         g = np.zeros(8, np.int64)
         lib.fbn_jt_tile_program(self._h, None, None, None, _p(g))
-        passes = np.zeros((int(g[0]), 32), np.int32)
+        passes = np.zeros((int(g[0]), 33), np.int32)
         tab = np.zeros(max(int(g[1]), 1), np.int32)
         iv = np.zeros(max(int(g[2]), 1), np.float64)
         lib.fbn_jt_tile_program(self._h, _p(passes), _p(tab), _p(iv), _p(g))

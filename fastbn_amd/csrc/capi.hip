@@ -686,7 +686,7 @@ int fbn_jt_stream_schedule(const fbn_jt_plan *p, int32_t *order, int64_t order_c
 int fbn_jt_tile_program(const fbn_jt_plan *p, int32_t *passes, int32_t *tab, double *initv, int64_t *geometry) {
     if (!p) return SetError(FBN_ERR_ARG, "null pointer");
     if (!p->t_ok) return SetError(FBN_ERR_LIMIT, "plan not eligible for the tiled kernel");
-    static_assert(sizeof(JtTPass) == 32 * 4, "JtTPass = 32 int32");
+    static_assert(sizeof(JtTPass) == 33 * 4, "JtTPass = 33 int32");
     const auto &t = p->tprog;
     if (passes) memcpy(passes, t.passes.data(), t.passes.size() * sizeof(JtTPass));
     if (tab) memcpy(tab, t.tab.data(), t.tab.size() * 4);

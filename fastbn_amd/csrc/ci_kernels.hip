@@ -27,6 +27,9 @@ namespace {
 constexpr int kTermChunk = 1024;
 constexpr long long kWideTests = 512;  // batches up to this size: 1024-thread workgroups
 constexpr int kDerivedInts = 256;      // MODE 3: the four full 3-way tables (4 x 64 ints) after the terms
+// MODE 3 / 4: the derived d = 2 counting with the register allocation unconstrained (2 waves per
+// SIMD) / allowing 3 waves per SIMD (the default; only the widest state-count instantiations spill)
+__host__ __device__ constexpr int der2_waves(int mode) { return mode == 4 ? 3 : 1; }
 
 // sub-histogram copies per wave for a table of `cells` > 16 cells (0: one shared table, beyond
 // 64 KB of LDS for the 4 waves' copies): 4 for small tables (config-5 level 2, <= 256 cells:
@@ -117,6 +120,7 @@ __device__ __forceinline__ void lead4(const uint32_t *__restrict__ px, const uin
                                       int32_t *__restrict__ F12x, int32_t *__restrict__ F12y) {
     typedef __attribute__((ext_vector_type(4))) unsigned u4;
     constexpr int AX = MX > 0 ? MX : 1, AY = MY > 0 ? MY : 1, A2 = M2 > 0 ? M2 : 1;
+    constexpr int kQU = MX * MY * A2 > 8 ? 1 : 4;  // sub-words unrolled (see the word loop)
     // waves 0-2: (z1 value c1, word part) units -- with fewer than 3 z1 leading values the words are
     // split between waves (M1 = 1: 3 parts), so a binary z1 does not leave two waves idle; wave 3
     // counts (x, y | z2) over all words.  Parts add into the (zeroed) LDS tables atomically.
@@ -151,7 +155,9 @@ __device__ __forceinline__ void lead4(const uint32_t *__restrict__ px, const uin
 #pragma unroll
             for (int c = 0; c < M2; ++c) Z[c] = *reinterpret_cast<const u4 *>(p2 + c * W + 4 * w4);
             const u4 Z1 = *reinterpret_cast<const u4 *>(pz1 + 4 * w4);
-#pragma unroll
+            // (the four sub-words one after the other for the wide tables: all four in flight
+            // needed 238 VGPRs, i.e. 2 waves per SIMD)
+#pragma unroll kQU
             for (int q = 0; q < 4; ++q) {
 #pragma unroll
                 for (int a = 0; a < MX; ++a) {
@@ -352,7 +358,7 @@ __device__ __forceinline__ void derived4(const CiArgs &A, int x, int y, int z1, 
 // config 5: 30-1056 tests of 100k samples each, one workgroup per test leaves most CUs idle) run as
 // 1 then 2.  Counts are integers: the same in any order.
 template <int D, bool BITS, bool PK = false, int BS = 256, int MODE = 0>
-__global__ __launch_bounds__(BS) void ci_g2_kernel(CiArgs A) {
+__global__ __launch_bounds__(BS, der2_waves(MODE)) void ci_g2_kernel(CiArgs A) {
     constexpr int NW = BS / 64;  // waves per workgroup (sub-histogram copies exist for 4 of them)
     extern __shared__ __align__(16) int32_t lds_base[];
     int32_t *smem = A.gscratch ? A.gscratch + (size_t)blockIdx.x * A.gstride : lds_base;
@@ -400,7 +406,7 @@ __global__ __launch_bounds__(BS) void ci_g2_kernel(CiArgs A) {
         if (nsub > 1 && !BITS && MODE != 2)
             for (int c = tid; c < nsub * sstr; c += BS) sub[c] = 0;
         __syncthreads();
-        if (BITS && MODE == 3) {
+        if (BITS && MODE >= 3) {
             if constexpr (D == 2) derived4(A, x, y, zv[0], zv[1], dx, dy, hist, smem + term_off + 2 * tc, tid);
         } else if (BITS) {
             // bit-sliced counting: wave w takes the prefixes p = w, w + 4, ... of the z-configuration
@@ -778,7 +784,11 @@ extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, co
              getenv("FBN_CI_DER2_DBG") ? atoi(getenv("FBN_CI_DER2_DBG")) : 0};
     if (gscratch) lds_bytes = 0;
     if (pairtab && bits && d == 2) {  // MODE 3: derived bit-sliced counting (every state count <= 4)
-        hipLaunchKernelGGL((ci_g2_kernel<2, true, false, 256, 3>), dim3(grid), dim3(256), lds_bytes, stream, a);
+        // registers for 3 waves per SIMD (config-5 level 2: 0.47 / 0.42 / 0.49 ms at 2 / 3 / 4 waves;
+        // FBN_CI_DER2_WAVES = 2 selects the unconstrained allocation)
+        static const int w = getenv("FBN_CI_DER2_WAVES") ? atoi(getenv("FBN_CI_DER2_WAVES")) : 3;
+        if (w == 2) hipLaunchKernelGGL((ci_g2_kernel<2, true, false, 256, 3>), dim3(grid), dim3(256), lds_bytes, stream, a);
+        else hipLaunchKernelGGL((ci_g2_kernel<2, true, false, 256, 4>), dim3(grid), dim3(256), lds_bytes, stream, a);
         return hipGetLastError();
     }
     if (split > 1 && pk && !bits && !gscratch) {  // small batch: count in parts, then decide

@@ -45,33 +45,48 @@ std::string BroadcastCtx(const std::vector<uint8_t> &cols, const std::vector<int
 
 // Small graphs (fbn_pc_small_eligible: the one-launch device-resident search) on g.size() GPUs:
 // REPLICAS -- every rank runs the whole search on its own copy of the broadcast column store, then
-// ONE ncclBroadcast of rank 0's result record (fbn_pc_result_record, fixed capacity) and every
+// ncclBroadcasts of rank 0's result record (fbn_pc_result_record: its length, then the record) and every
 // rank checks its own result against it.  Five dependent levels in one 0.14 ms launch do not
 // shard: cutting them over ranks would add an all-gather per level.
 std::string PcReplicas(const std::vector<uint8_t> &cols, const std::vector<int32_t> &dims, int nvars,
                        int64_t nsamples, double alpha, int depth, GpuGroup &g, fbn_pc_result **out) {
     const int world = g.size();
-    const int64_t P = (int64_t)nvars * (nvars - 1) / 2;
-    const int64_t cap = 3 + 2 * 8 + 1 + 2 * P + 1 + P * (3 + 8);  // (pc_dist.record_cap)
     std::vector<fbn_pc_result *> res(world, nullptr);
     std::string err = g.Run([&](int r) -> std::string {
         hipStream_t s = g.stream(r);
         fbn_ci_ctx *ctx = nullptr;
         std::string e = BroadcastCtx(cols, dims, nvars, nsamples, g, r, &ctx);
         if (e.empty()) e = FbnErr(fbn_pc_stable(ctx, alpha, depth, 1, &res[r]), "fbn_pc_stable");
-        std::vector<int32_t> mine((size_t)cap, 0), got((size_t)cap, 0);
-        if (e.empty()) e = FbnErr(fbn_pc_result_record(res[r], mine.data(), cap, nullptr), "fbn_pc_result_record");
+        // the record is sized by the result: rank 0's length goes out first (one int64), then the
+        // record at that length.  (Every rank reaches both broadcasts, even after an error, so no
+        // rank waits forever; a rank with an error sends / receives zeros and reports its own error.)
+        int64_t len = 0;
+        if (e.empty()) e = FbnErr(fbn_pc_result_record(res[r], nullptr, 0, &len), "fbn_pc_result_record");
+        DevMem d_len;
+        std::string e2 = d_len.alloc(8);
+        if (e2.empty()) e2 = HipErr(hipMemcpyAsync(d_len.p, &len, 8, hipMemcpyHostToDevice, s), "hipMemcpyAsync");
+        const std::string e3 = NcclErr(ncclBroadcast(d_len.p, d_len.p, 1, ncclInt64, 0, g.comm(r), s), "ncclBroadcast");
+        if (e2.empty()) e2 = e3;
+        int64_t len0 = 0;
+        if (e2.empty()) e2 = HipErr(hipMemcpyAsync(&len0, d_len.p, 8, hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+        if (e2.empty()) e2 = HipErr(hipStreamSynchronize(s), "record length");
+        if (e.empty()) e = e2;
+        const int64_t cap = std::max<int64_t>(len0, 1);
+        std::vector<int32_t> mine((size_t)std::max(cap, len), 0), got((size_t)cap, 0);
+        if (e.empty()) e = FbnErr(fbn_pc_result_record(res[r], mine.data(), (int64_t)mine.size(), nullptr),
+                                  "fbn_pc_result_record");
         DevMem d_rec;
-        if (e.empty()) e = d_rec.alloc((size_t)cap * 4);
-        if (e.empty()) e = HipErr(hipMemcpyAsync(d_rec.p, mine.data(), (size_t)cap * 4, hipMemcpyHostToDevice, s),
-                                  "hipMemcpyAsync");
-        // (every rank reaches the broadcast, even after an error, so no rank waits forever; a rank
-        // with an error broadcasts / receives zeros and reports its own error)
-        std::string e2 = NcclErr(ncclBroadcast(d_rec.p, d_rec.p, (size_t)cap, ncclInt32, 0, g.comm(r), s), "ncclBroadcast");
+        e2 = d_rec.alloc((size_t)cap * 4);
+        if (e2.empty())
+            e2 = HipErr(hipMemcpyAsync(d_rec.p, mine.data(), (size_t)cap * 4, hipMemcpyHostToDevice, s), "hipMemcpyAsync");
+        const std::string e4 = NcclErr(ncclBroadcast(d_rec.p, d_rec.p, (size_t)cap, ncclInt32, 0, g.comm(r), s), "ncclBroadcast");
+        if (e2.empty()) e2 = e4;
         if (e.empty()) e = e2;
         if (e.empty()) e = HipErr(hipMemcpyAsync(got.data(), d_rec.p, (size_t)cap * 4, hipMemcpyDeviceToHost, s),
                                   "hipMemcpyAsync");
         if (e.empty()) e = HipErr(hipStreamSynchronize(s), "record");
+        if (e.empty() && len != len0) e = "PC replicas disagree with rank 0's result record (length)";
+        mine.resize((size_t)cap);
         if (e.empty() && got != mine) e = "PC replicas disagree with rank 0's result record";
         if (ctx) fbn_ci_ctx_destroy(ctx);
         return e;

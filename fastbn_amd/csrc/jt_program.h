@@ -137,6 +137,10 @@ struct JtTPass {
     int32_t dest_sc, col_sc;         // scale rows of the output message and of the child's Collect message (DIS)
     int32_t split;                   // work of the JT_T_W waves: 0 = rounds (round r -> wave r % JT_T_W),
                                      // 1 = outer configurations (contiguous blocks, every round)
+    int32_t chunk;                   // inner steps per run: nRi, or (loop-tiled R stream) fewer -- the
+                                     // stream is then chunk-major (for each chunk of the inner range, every
+                                     // outer configuration), a run's sum writes its bin in the first chunk
+                                     // and adds into it after (step record bin field -(bin + 2))
 };
 
 #endif

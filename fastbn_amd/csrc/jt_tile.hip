@@ -192,19 +192,26 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
                     }
                     acc += ok[u] ? x : 0.0;
                     const int xo = qc[u][NF + 1];
-                    if (xo >= 0) {  // end of an inner run: its bin
+                    if (xo != -1) {  // end of an inner run (or of its chunk, loop-tiled): its bin
+                        const bool add = xo < -1;  // (a later chunk: add into the bin, which this
+                        const int xb = add ? -xo - 2 : xo;  // lane wrote in an earlier chunk)
                         const double a = okG ? acc : 0.0;
                         if (la) {
-                            const int x8 = (xG + xo) * (C * 8) + g8;
+                            const int x8 = (xG + xb) * (C * 8) + g8;
                             if (O.direct) {
                                 const double v = a * O.sig;
-                                if (O.out_lds) *reinterpret_cast<double *>(ldsb + O.out_b + x8) = v;
-                                else bst(st, O.out_b + x8, v);
+                                if (O.out_lds) {
+                                    double *p = reinterpret_cast<double *>(ldsb + O.out_b + x8);
+                                    *p = add ? *p + v : v;
+                                } else {
+                                    bst(st, O.out_b + x8, add ? bld(st, O.out_b + x8, 0) + v : v);
+                                }
                                 tot += v;
                             } else if (O.bins_lds) {
-                                *reinterpret_cast<double *>(ldsb + O.part_b + x8) = a;
+                                double *p = reinterpret_cast<double *>(ldsb + O.part_b + x8);
+                                *p = add ? *p + a : a;
                             } else {
-                                bst(st, O.part_b + x8, a);
+                                bst(st, O.part_b + x8, add ? bld(st, O.part_b + x8, 0) + a : a);
                             }
                         }
                         acc = 0.0;

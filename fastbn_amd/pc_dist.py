@@ -207,23 +207,26 @@ def independence_test_broadcast(cols, dims, shape, alpha=0.05, device=0, src=0):
 RECORD_MAGIC = 0x52504246
 
 
-def record_cap(nvars, max_levels=8, max_d=8):
-    """Upper bound of fbn_pc_result_record's length for a graph of `nvars` variables."""
-    P = nvars * (nvars - 1) // 2
-    return 3 + 2 * max_levels + 1 + 2 * P + 1 + P * (3 + max_d)
-
-
 def small_eligible(ci, group_size=1):
     e = C.c_int()
     api.lib.fbn_pc_small_eligible(ci._h, int(group_size), C.byref(e))
     return bool(e.value)
 
 
-def result_record(handle, cap):
-    """fbn_pc_result_record of a result handle into a zero-padded int32 array of length `cap`."""
+def record_len(handle):
+    """Length (int32 words) of fbn_pc_result_record for a result handle."""
+    n = C.c_int64()
+    api.lib.fbn_pc_result_record(handle, None, 0, C.byref(n))
+    return int(n.value)
+
+
+def result_record(handle, cap=None):
+    """fbn_pc_result_record of a result handle: an int32 array of exactly its length (cap=None), or
+    zero-padded to `cap` (FastBNError when the record needs more)."""
+    cap = record_len(handle) if cap is None else int(cap)
     rec = np.zeros(cap, np.int32)
     n = C.c_int64()
-    api.lib.fbn_pc_result_record(handle, rec.ctypes.data, int(cap), C.byref(n))
+    api.lib.fbn_pc_result_record(handle, rec.ctypes.data, cap, C.byref(n))  # (raises when short)
     return rec
 
 
@@ -271,8 +274,13 @@ def pc_stable_replicas(ci, alpha=0.05, depth=1000, device=None, check=True):
     h = C.c_void_p()
     api.lib.fbn_pc_stable(ci._h, float(alpha), int(depth), 1, C.byref(h))
     res = api.PCResult(h)
-    mine = result_record(h, record_cap(len(ci.dims)))
-    got = broadcast_record(mine, device)
-    if check and not np.array_equal(got, mine):
+    mine = result_record(h)
+    # rank 0's record length first (records are sized by the result, not by a fixed bound), then
+    # the record; a rank whose own length differs still takes part in both broadcasts
+    n0 = int(broadcast_record(np.array([len(mine)], np.int32), device)[0])
+    buf = np.zeros(n0, np.int32)
+    buf[:min(n0, len(mine))] = mine[:n0]
+    got = broadcast_record(buf, device)
+    if check and not (len(mine) == n0 and np.array_equal(got, mine)):
         raise RuntimeError("PC replicas disagree with rank 0's result record")
     return res, unpack_record(got)

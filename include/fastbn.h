@@ -199,7 +199,7 @@ int fbn_jt_kernel_cache_path(const fbn_jt_plan *p, char *buf, int64_t cap);
 int fbn_jt_kernel_build(const fbn_jt_plan *p);
 /* Compile options of the specialized kernel, '\n'-separated. */
 int fbn_jt_kernel_options(char *buf, int64_t cap);
-/* The tiled kernel's program (variant 5, jt_program.h JtTPass): passes [n_passes] (32 int32 each),
+/* The tiled kernel's program (variant 5, jt_program.h JtTPass): passes [n_passes] (33 int32 each),
  * index tables [n_tab], initial potentials [n_init]; geometry = {n_passes, n_tab, n_init,
  * partial-bin row, reduced-bin row, store rows, cases per wave, slots per case}.  Buffers may be
  * NULL (sizes only).  For tests that execute the tables on the host (tests/tile_emulator.py). */

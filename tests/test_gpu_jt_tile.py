@@ -123,6 +123,22 @@ def test_munin_like_default_and_vs_oracle(tmp_path):
     np.testing.assert_array_equal(marg, omarg)
 
 
+def test_loop_tiled_munin_like_vs_reference(munin_fixture, monkeypatch):
+    """FBN_JT_TILING = 1 (opt-in loop tiling: chunk-major R streams, bins written by a run's first
+    chunk and added into by the later ones) on the reference's own Munin-like fixture cases."""
+    from conftest import read_ref_marg
+    monkeypatch.setenv("FBN_JT_TILING", "1")
+    jt = F.JunctionTree(F.Network(munin_fixture["xml"]), device=0)
+    o = O.OracleJT(munin_fixture["xml"])
+    ev, _ = O.load_libsvm(munin_fixture["libsvm"], o.n)
+    rlab, rmarg, _, _ = read_ref_marg(munin_fixture["marg"], o.dims)
+    lab, marg = jt.infer(ev)
+    assert jt.refresh_info()["variant"] == 5
+    np.testing.assert_array_equal(lab, rlab)
+    np.testing.assert_allclose(marg, rmarg, rtol=1e-9, atol=1e-300)
+    np.testing.assert_allclose(marg, o.infer(ev)[1], rtol=1e-12, atol=1e-300)
+
+
 @pytest.mark.parametrize("tw", [2, 4])
 def test_multi_wave_case_groups(alarm, tmp_path, monkeypatch, tw):
     """FBN_JT_TW = 2 / 4 waves per case group (opt-in: passes split over the waves, one LDS stage

@@ -237,7 +237,7 @@ def _replica_worker(rank, world, port, csv, out_path):
     from fastbn_amd import pc_dist
     ref = O.OracleDataset(csv=csv).pc_stable(0.05, 1000, 1)
     res = F.orient_skeleton(37, ref["edges"], {tuple(k): tuple(v) for k, v in ref["sepset"].items()})
-    mine = pc_dist.result_record(res._h, pc_dist.record_cap(37))
+    mine = pc_dist.result_record(res._h)
     got = pc_dist.broadcast_record(mine)
     out = pc_dist.unpack_record(got)
     np.save(f"{out_path}.{rank}.npy", np.array([out["edges"], sorted(out["sepset"].items()),

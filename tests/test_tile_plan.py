@@ -76,22 +76,34 @@ def _check_steps(passes, tab, geo):
         ri = tab[P["i_off"]:P["i_off"] + nRi * (2 + nf)].reshape(nRi, 2 + nf).astype(np.int64)
         et = tab[P["et_off"]:P["et_off"] + nR + C].astype(np.int64)
         st = tab[P["st_off"]:P["st_off"] + (nR + C) * (nf + 2)].reshape(nR + C, nf + 2).astype(np.int64)
-        np.testing.assert_array_equal(et[:nR], (ro[:, 0:1] * 8 + ri[None, :, 0]).reshape(-1))
+        # stream order: (outer, inner) pairs, chunk-major when the plan loop-tiled the inner range
+        q = P["chunk"]
+        assert 1 <= q <= nRi and (q == nRi or (W_env() == 1 and P["split"] == 0))
+        order = [(o, i) for c0 in range(0, nRi, q) for o in range(nRo) for i in range(c0, min(nRi, c0 + q))]
+        oi = np.array(order, np.int64).reshape(-1, 2)
+        oo, ii = oi[:, 0], oi[:, 1]
+        np.testing.assert_array_equal(et[:nR], ro[oo, 0] * 8 + ri[ii, 0])
         assert (et[nR:] == 0).all() and (st[nR:, nf + 1] == -1).all()
-        W = int(os.environ.get("FBN_JT_TW", "1"))  # with the outer split every wave's first step loads
+        W = W_env()  # with the outer split every wave's first step loads
         starts = [0] + ([nRo * w // W * nRi for w in range(1, W)] if P["split"] == 1 else [])
         for j in range(nf):
-            off = (ro[:, 4 + j:5 + j] + ri[None, :, 2 + j]).reshape(-1)
+            off = ro[oo, 4 + j] + ri[ii, 2 + j]
             assert (off % (C * 8) == 0).all()
             np.testing.assert_array_equal(st[:nR, j] & ~1, off)
             same = np.concatenate([[False], off[1:] == off[:-1]])
             same[[k for k in starts if k < nR]] = False
             np.testing.assert_array_equal((st[:nR, j] & 1) == 1, same)
-        dw = ((ro[:, 1:2] & 0xFFFFFFFF) | (ri[None, :, 1] & 0xFFFFFFFF)).reshape(-1)
+        dw = (ro[oo, 1] & 0xFFFFFFFF) | (ri[ii, 1] & 0xFFFFFFFF)
         np.testing.assert_array_equal(st[:nR, nf] & 0xFFFFFFFF, dw)
-        last = np.full((nRo, nRi), -1, np.int64)
-        last[:, -1] = ro[:, 2]
-        np.testing.assert_array_equal(st[:nR, nf + 1], last.reshape(-1))
+        # a run's chunk end writes its bin (first chunk) or adds into it (-(bin + 2))
+        end = (ii == np.minimum(nRi, (ii // q) * q + q) - 1)
+        want = np.where(end, np.where(ii < q, ro[oo, 2], -(ro[oo, 2] + 2)), -1)
+        np.testing.assert_array_equal(st[:nR, nf + 1], want)
+    return [int(p[TE.F.index("chunk")]) for p in passes]
+
+
+def W_env():
+    return int(os.environ.get("FBN_JT_TW", "1"))
 
 
 def test_step_records_alarm():
@@ -102,6 +114,24 @@ def test_step_records_alarm():
 def test_step_records_munin_like(munin_fixture):
     _, (passes, tab, iv, geo) = _prog(munin_fixture["xml"])
     _check_steps(passes, tab, geo)
+
+
+def test_step_records_loop_tiled(munin_fixture, monkeypatch):
+    """FBN_JT_TILING = 1 (opt-in loop tiling of the inner range): chunk-major step order, a run's
+    first chunk writes its bin and later chunks add into it; the emulated program still matches the
+    reference's own Munin-like labels / marginals."""
+    from conftest import read_ref_marg
+    monkeypatch.setenv("FBN_JT_TILING", "1")
+    jt, (passes, tab, iv, geo) = _prog(munin_fixture["xml"])
+    chunks = _check_steps(passes, tab, geo)
+    nri = [int(p[TE.F.index("nRi")]) for p in passes]
+    assert sum(c < n for c, n in zip(chunks, nri)) > 50
+    o = O.OracleJT(munin_fixture["xml"])
+    ev, _ = O.load_libsvm(munin_fixture["libsvm"], o.n)
+    rlab, rmarg, _, _ = read_ref_marg(munin_fixture["marg"], o.dims)
+    lab, marg = TE.run((passes, tab, iv, geo), ev[:2], jt.info["sum_dom"])
+    np.testing.assert_array_equal(lab, rlab[:2])
+    np.testing.assert_allclose(marg, rmarg[:2], rtol=1e-9, atol=1e-300)
 
 
 def test_step_records_four_wave_split(munin_fixture, monkeypatch):

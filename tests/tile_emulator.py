@@ -11,7 +11,7 @@ import numpy as np
 # JtTPass field order (jt_program.h)
 F = ["kind", "clique", "nf", "nl", "nG", "rounds", "nRo", "nRi", "g_off", "o_off", "i_off", "nE", "nbins",
      "dest_row", "col_row", "bdig_off", "nmv", "mv_off", "iv_off", "nv", "vars_off", "gfields", "ofields", "first",
-     "nstage", "stage_off", "et_off", "st_off", "fsc_off", "dest_sc", "col_sc", "split"]
+     "nstage", "stage_off", "et_off", "st_off", "fsc_off", "dest_sc", "col_sc", "split", "chunk"]
 COL, DIS, MARG = 0, 1, 2
 
 
