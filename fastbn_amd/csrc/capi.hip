@@ -1115,7 +1115,10 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
         FBN_HIP(hipModuleLaunchKernel(gk.fn, grid, 1, 1, 64, 1, 1, (unsigned)gk.lds, s, args, nullptr));
         if (p->force_fixup) FBN_HIP(hipMemsetAsync(p->flags.p, 1, (size_t)nblk * 4, s));  // testing only
         // exact recomputation of the blocks whose denominators left the fast-division range
-        if ((rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s))) return rc;
+        // (FBN_JT_NO_FIXUP: diagnostic only, as above)
+        static const bool no_fix3 = getenv("FBN_JT_NO_FIXUP") != nullptr;
+        if (!no_fix3 && (rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s)))
+            return rc;
     } else {
         FBN_HIP(hipEventRecord(p->ev0, s));
         if ((rc = LaunchLds(p, p->ws, d_evidence, ncases, labels, marg, nullptr, variant == 2, s))) return rc;

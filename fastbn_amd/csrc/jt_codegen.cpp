@@ -551,6 +551,9 @@ int JTGen::Run(std::string &src, int64_t *wave_entries, std::vector<double> &ini
     o << "#define FBN_V " << V << "\n#define FBN_SD " << SD << "\n#define FBN_WE " << *wave_entries << "LL\n";
     o << "#define FBN_IV_BASE " << lds_rows * 64 << "\n#define FBN_NIV " << initv.size() << "\n";
     o << "#define FBN_IV_LDS " << (iv_lds ? 1 : 0) << "\n#define FBN_MIN_WAVES " << min_waves << "\n";
+    // diagnostic only (FBN_JT_WS_FOLD=K, wrong results): K workspaces shared by all waves, so the
+    // workspace stays in L2 -- times the kernel without its workspace's fabric traffic
+    if (const char *e = getenv("FBN_JT_WS_FOLD")) o << "#define FBN_WS_FOLD " << atoi(e) << "\n";
     o << R"FBN(typedef signed char i8;
 __device__ __forceinline__ double dv(double x, double den, double y) {  // x / den (Markstein, see jt_kernels.hip)
     const double q = x * y;
@@ -605,7 +608,11 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
     ldouble *ivl = (ldouble *)fbn_lds;  // unused (laundered at op boundaries)
 #endif
     unsigned long long pacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tprev = __builtin_amdgcn_s_memtime();
+#ifdef FBN_WS_FOLD
+    gdouble *Wb = (gdouble *)ws + (unsigned long long)(blockIdx.x % FBN_WS_FOLD) * FBN_WE * 64;
+#else
     gdouble *Wb = (gdouble *)ws + (unsigned long long)blockIdx.x * FBN_WE * 64;
+#endif
     unsigned lo = (unsigned)lane * 8;
     for (long long blk = blockIdx.x; blk * 64 < ncases; blk += gridDim.x) {
         long long blkl = blk;

@@ -29,8 +29,10 @@
 // counter, every workgroup polls relaxed with s_sleep; the data crossing workgroups moves through
 // agent-coherent accesses, so the barrier carries no cache-maintenance fence (see grid_barrier);
 // every spin bounded (a timed-out launch reports status 1 and exits; the host then runs the search
-// on its level loop).  The launch is cooperative: a grid that cannot be co-resident fails at launch
-// (and the host falls back) instead of spinning.
+// on its level loop).  The launch is plain by default: the host checks first that the grid fits
+// the occupancy (hipOccupancyMaxActiveBlocksPerMultiprocessor) and falls back to its level loop if
+// not, and the bounded spin covers a grid that is still not co-resident; FBN_PC_SMALL_COOP=1 selects
+// hipLaunchCooperativeKernel, which refuses such a grid at launch.
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>

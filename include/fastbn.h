@@ -289,7 +289,8 @@ int fbn_pc_shd_bif(const fbn_pc_result *r, const char *bif_path, int *shd);
 int fbn_shd_bif(const char *bif_path, int nvars, const int32_t *triples, int n, int *shd);
 int fbn_pc_timing(const fbn_pc_result *r, double *total_s, double *kernel_s);
 /* Which skeleton path ran: 0 host-driven levels, 1 the device-resident search (small graphs, one
- * cooperative launch), 2 the device-resident search was refused at launch or timed out at a grid
+ * launch: plain by default after an occupancy check, cooperative with FBN_PC_SMALL_COOP=1), 2 the
+ * device-resident search was refused at launch or timed out at a grid
  * barrier and the host-driven levels ran instead (same answer). */
 int fbn_pc_path(const fbn_pc_result *r, int *path);
 /* The result as one flat int32 record (for moving it between ranks): magic 0x52504246, n_levels,

@@ -1,4 +1,4 @@
-"""Run the JT kernel a few times (for rocprofv3 PMC passes): jt_once.py [variant] [waves] [reps]."""
+"""Run the JT kernel a few times (for rocprofv3 PMC passes): jt_once.py [variant] [waves] [reps] [cases]."""
 import os
 import sys
 
@@ -13,7 +13,7 @@ variant = int(sys.argv[1]) if len(sys.argv) > 1 else 0
 waves = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 xml = os.path.join(REPO, "tests", "golden", "alarm", "alarm.xml")
-n = 100000
+n = int(sys.argv[4]) if len(sys.argv) > 4 else 100000
 ev = synth.evidence_cases(synth.read_xmlbif(xml), n, 7, seed=1)
 jt = F.JunctionTree(F.Network(xml), device=0)
 jt.set_variant(variant)
