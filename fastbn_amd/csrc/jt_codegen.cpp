@@ -3,20 +3,22 @@
 // For trees whose cliques are small (ALARM-class), the case-independent schedule is emitted as
 // straight-line code: every table entry of the clique in flight is a named fp64 register value
 // (lane = evidence case), every index map / digit / stride and every initial potential is a
-// compile-time constant; the initial potentials are copied into LDS once per wave and read with
-// wave-uniform (broadcast) addresses.
-// No op dispatch, no index arrays, no LDS.
+// compile-time constant; the initial potentials are read with wave-uniform scalar loads from a
+// constant buffer (or, FBN_JT_IV_LDS=1, from an LDS copy per wave).  No op dispatch, no index arrays;
+// LDS holds the entries of a large clique past the register-resident ones and a pool of message
+// rows (PlaceMessages).
 //
 // Schedule (values identical to the reference's level order -- a clique's Collect result depends
 // only on its subtree and the fixed order of its child messages, its Distribute result only on its
 // parent's -- so any children-first / parent-first traversal gives the same bits):
 //  * Collect in DFS post-order: the last child's message stays in registers for its parent; other
-//    messages go to the per-wave separator rows in global memory (they are needed again anyway as
-//    the "old" separator of Distribute).
+//    messages are stored (they are needed again anyway as the "old" separator of Distribute) --
+//    in LDS pool rows when their live interval fits, else in the per-wave rows in global memory.
 //  * Distribute in DFS pre-order: a clique's Collect table is not parked and reloaded but
 //    recomputed from its initial potential and its children's stored messages (which Distribute
 //    loads anyway) -- ALU is cheap here, HBM round trips are not.  The message to the first child
-//    stays in registers; the others overwrite their (now dead) Collect message rows.
+//    stays in registers; the others go to LDS pool rows or overwrite their (now dead) Collect
+//    message's global rows.
 //  * Loads for the next clique are issued at the start of the current one (register budget
 //    permitting) so their latency hides behind its arithmetic.
 // Operation order per entry is exactly the interpreter's (= the reference's), so results are
@@ -72,7 +74,11 @@ class JTGen {
   public:
     JTGen(const JTPlanHost &p, bool fast_order) : plan(p), fast(fast_order) {}
     int Run(std::string &src, int64_t *wave_entries, std::vector<double> &initv);
-    int64_t lds_rows = 0;  // LDS rows (64 lanes x fp64) per wave
+    int64_t lds_rows = 0;  // LDS rows (64 lanes x fp64) per wave: the clique tail
+    int64_t pool_rows = 0;  // + LDS rows of the message pool (after the tail, before the initial potentials)
+    // initial potentials: scalar loads from the constant buffer (round 5 default; 1 = an LDS copy per
+    // wave, which takes LDS from the message pool: ALARM 0.163 vs 0.141 ms)
+    bool iv_lds = false;
 
   private:
     const JTPlanHost &plan;
@@ -105,7 +111,12 @@ class JTGen {
     int64_t init_batch = 16;  // fast order: entries per software-pipelined batch of the fused product
     bool in_merged = false;  // the current op's closing boundary is left out
     int min_waves = 1;
-    bool iv_lds = true;
+    // where each stored message lives, per separator entry: "W(row)" (the per-wave workspace in
+    // global memory) or "LP(row)" (the LDS message pool); the Collect message (child -> parent) and
+    // the Distribute message (parent -> child) of a separator are placed separately
+    std::vector<std::vector<std::string>> col_loc, dis_loc;
+    std::vector<bool> md_reg;  // Distribute messages kept in registers (first child, if it fits)
+    void PlaceMessages(const std::vector<int> &post, const std::vector<int> &pre, int64_t budget);
     std::string B(int k) const {
         return profile ? "        FBN_OP_BOUNDARY(); FBN_STAMP(" + std::to_string(k) + ");\n" : "        FBN_OP_BOUNDARY();\n";
     }
@@ -147,13 +158,17 @@ class JTGen {
     void DMul(const std::string &P, int c, int s, const std::string &M);
     void SepDis(const std::string &P, int c, int s, const std::string &old, bool store);
     void Marg(const std::string &P, int c);
-    void Load(const std::string &name, int s) {
+    void Load(const std::string &name, int s) {  // "ld": the Distribute message, else the Collect one
+        const auto &loc = name == "ld" ? dis_loc[s] : col_loc[s];
         for (int64_t j = 0; j < plan.seps[s].size(); ++j)
-            o << "        const double " << name << s << "_" << j << " = W(" << sep_row[s] + j << "LL);\n";
+            o << "        const double " << name << s << "_" << j << " = " << loc[j] << ";\n";
     }
     // entry e of clique c's table: a register value, or (entries >= kRegEntries of a large table)
     // an LDS row [row][64 lanes] -- only one clique is in flight, so every table starts at row 0
-    int64_t kRegEntries = 96;
+    // (round 5: 144 -- with the initial potentials as scalar loads, the LDS this frees holds the
+    // message pool: ALARM 0.165 -> 0.138 ms per 100k cases; 96 / 112 / 128 / 136 / 144 measured
+    // 0.151 / 0.142 / 0.141 / 0.140 / 0.138 ms, gpurun_out/r05l, r05m)
+    int64_t kRegEntries = 144;
     std::string N(const std::string &P, int c, int64_t e) const {
         if (e >= kRegEntries) return "L(" + std::to_string(e - kRegEntries) + ")";
         return P + std::to_string(c) + "_" + std::to_string(e);
@@ -322,7 +337,7 @@ void JTGen::SepCol(const std::string &P, int c, int s, bool store) {
             std::vector<std::string> terms;
             for (int64_t q = 0; q < Q; ++q) terms.push_back(N(P, c, q * Ts + j));
             o << "        const double mc" << s << "_" << j << " = " << TreeSum(terms) << ";";
-            if (store) o << " W(" << sep_row[s] + j << "LL) = mc" << s << "_" << j << ";";
+            if (store) o << " " << col_loc[s][j] << " = mc" << s << "_" << j << ";";
             o << "\n";
         }
         if (!in_merged) o << B(4);
@@ -332,7 +347,7 @@ void JTGen::SepCol(const std::string &P, int c, int s, bool store) {
         o << "        const double mc" << s << "_" << j << " = " << Val(P, c, j);
         for (int64_t q = 1; q < Q; ++q) o << " + " << Val(P, c, q * Ts + j);
         o << ";";
-        if (store) o << " W(" << sep_row[s] + j << "LL) = mc" << s << "_" << j << ";";
+        if (store) o << " " << col_loc[s][j] << " = mc" << s << "_" << j << ";";
         o << "\n";
     }
     o << B(4);
@@ -373,7 +388,7 @@ void JTGen::SepDis(const std::string &P, int c, int s, const std::string &old, b
             o << "        const double " << sa << " = " << TreeSum(terms) << ";";
             o << " double md" << s << "_" << j << "; { const double od = " << old << s << "_" << j
               << "; const double q = " << sa << " * frcp(od); md" << s << "_" << j << " = (od == 0.0) ? 0.0 : q; }";
-            if (store) o << " W(" << sep_row[s] + j << "LL) = md" << s << "_" << j << ";";
+            if (store) o << " " << dis_loc[s][j] << " = md" << s << "_" << j << ";";
             o << "\n";
         }
         // the marginals summed from this separator's calibrated belief (its bin sums)
@@ -393,7 +408,7 @@ void JTGen::SepDis(const std::string &P, int c, int s, const std::string &old, b
         o << " { double a = " << Val(P, c, lists[j][0]) << ";";
         for (size_t q = 1; q < lists[j].size(); ++q) o << " a += " << Val(P, c, lists[j][q]) << ";";
         o << " const double od = " << old << s << "_" << j << "; md" << s << "_" << j << " = (od == 0.0) ? 0.0 : a / od; }";
-        if (store) o << " W(" << sep_row[s] + j << "LL) = md" << s << "_" << j << ";";
+        if (store) o << " " << dis_loc[s][j] << " = md" << s << "_" << j << ";";
         o << "\n";
     }
     o << B(7);
@@ -418,7 +433,7 @@ void JTGen::MargTerms(int v, const std::vector<std::vector<std::string>> &terms)
         o << " labels[CS] = lab; bad |= (mp - m2 <= 1e-12 * mp) ? 1u : 0u; }\n";
     }
     o << "          if (ACT) {";
-    for (int d = 0; d < dim; ++d) o << " OUT(" << out_off[v] + d << ") = dv(p" << d << ", tot, yt);";
+    for (int d = 0; d < dim; ++d) o << " OUTS(" << out_off[v] + d << ", dv(p" << d << ", tot, yt));";
     o << " }\n        }\n";
 }
 
@@ -483,8 +498,127 @@ void JTGen::Marg(const std::string &P, int c) {
             o << " labels[CS] = lab;" << (fast ? " bad |= (mp - m2 <= 1e-12 * mp) ? 1u : 0u;" : "") << " }\n";
         }
         o << "          if (ACT) {";
-        for (int d = 0; d < dim; ++d) o << " OUT(" << out_off[v] + d << ") = dv(p" << d << ", tot, yt);";
+        for (int d = 0; d < dim; ++d) o << " OUTS(" << out_off[v] + d << ", dv(p" << d << ", tot, yt));";
         o << " }\n        } }\n" << (in_merged ? std::string() : B(8));
+    }
+}
+
+// Message placement.  Every stored message has a live interval on the schedule's clock (Collect
+// clique k of the post-order at time k, Distribute clique k of the pre-order at time nc + k): the
+// Collect message of separator s from its child's Collect to its parent's Distribute, the
+// Distribute message from the parent's Distribute to the child's.  The per-wave workspace of all
+// of them (ALARM: 265 rows = 136 KB per wave, 139 MB for 1,024 waves) does not stay in L2, and each
+// row written twice per block left L2 twice (PMC, round 5: 0.49 GB written per 100k cases, the
+// kernel 20 % slower than with the workspace L2-resident).  So the LDS left over by the clique tail
+// and the initial potentials (the budget of four waves per CU) holds a pool of rows, and messages
+// get pool rows by interval: shortest intervals first while the pool has room at every time of
+// the interval, rows then assigned in start order (an interval graph: the room suffices).  The
+// rest keep global rows (Collect and Distribute message of a separator in the same rows, as
+// before).  FBN_JT_LDS_POOL=n caps the pool at n rows (0: off).
+void JTGen::PlaceMessages(const std::vector<int> &post, const std::vector<int> &pre, int64_t budget) {
+    const int nc = (int)plan.cliques.size(), ns = (int)plan.seps.size();
+    auto tsize = [&](int c) { return plan.cliques[c].size(); };
+    md_reg.assign(ns, false);
+    for (int c : pre)
+        if (!plan.clique_down[c].empty()) {
+            const int s = plan.clique_down[c][0], q = child(s);
+            int64_t mk = 0;
+            for (int s2 : plan.clique_down[q]) mk = std::max<int64_t>(mk, plan.seps[s2].size());
+            md_reg[s] = tsize(q) + plan.seps[s].size() + mk <= budget;
+        }
+    std::vector<int> pi(nc), qi(nc);
+    for (int k = 0; k < nc; ++k) qi[post[k]] = k, pi[pre[k]] = k;
+    struct Item {
+        int s;
+        bool dist;
+        int a, b;  // live interval [a, b]
+        int64_t n;
+    };
+    std::vector<Item> items;
+    for (int s = 0; s < ns; ++s) {
+        const int c = plan.sep_down[s], p = plan.sep_up[s];
+        items.push_back({s, false, qi[c], nc + pi[p], plan.seps[s].size()});
+        if (!md_reg[s]) items.push_back({s, true, nc + pi[p], nc + pi[c], plan.seps[s].size()});
+    }
+    // room: the LDS of four waves per CU (160 KB) less the clique tail and the initial potentials
+    const int64_t per_wave = 160 * 1024 / 4 / 8;  // fp64 values
+    int64_t ivn = 0;
+    for (const auto &t : plan.cliques) ivn += t.size();
+    int64_t cap = std::max<int64_t>(0, (per_wave - lds_rows * 64 - (iv_lds ? ivn : 0)) / 64);
+    if (const char *e = getenv("FBN_JT_LDS_POOL")) cap = std::min<int64_t>(cap, std::max(0, atoi(e)));
+    std::vector<int> order(items.size());
+    for (size_t i = 0; i < items.size(); ++i) order[i] = (int)i;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+        return items[x].b - items[x].a < items[y].b - items[y].a;
+    });
+    std::vector<int64_t> use(2 * nc + 1, 0);
+    std::vector<bool> in_lds(items.size(), false);
+    for (int i : order) {
+        const Item &it = items[i];
+        if (it.n > cap) continue;
+        int64_t mx = 0;
+        for (int t = it.a; t <= it.b; ++t) mx = std::max(mx, use[t]);
+        if (mx + it.n > cap) continue;
+        for (int t = it.a; t <= it.b; ++t) use[t] += it.n;
+        in_lds[i] = true;
+    }
+    // concrete pool rows, in start order
+    std::vector<int> byst;
+    for (size_t i = 0; i < items.size(); ++i)
+        if (in_lds[i]) byst.push_back((int)i);
+    std::stable_sort(byst.begin(), byst.end(), [&](int x, int y) { return items[x].a < items[y].a; });
+    std::vector<std::vector<int64_t>> rows_of(items.size());
+    std::vector<int64_t> free_rows;
+    for (int64_t r = cap - 1; r >= 0; --r) free_rows.push_back(r);  // (pop_back takes the lowest)
+    std::vector<int> active;
+    pool_rows = 0;
+    for (int i : byst) {
+        const Item &it = items[i];
+        for (size_t k = 0; k < active.size();) {  // release intervals that ended before this one
+            if (items[active[k]].b < it.a) {
+                for (int64_t r : rows_of[active[k]]) free_rows.push_back(r);
+                std::sort(free_rows.rbegin(), free_rows.rend());
+                active.erase(active.begin() + k);
+            } else {
+                ++k;
+            }
+        }
+        for (int64_t j = 0; j < it.n; ++j) {
+            rows_of[i].push_back(free_rows.back());
+            pool_rows = std::max<int64_t>(pool_rows, free_rows.back() + 1);
+            free_rows.pop_back();
+        }
+        active.push_back(i);
+    }
+    col_loc.assign(ns, {});
+    dis_loc.assign(ns, {});
+    sep_row.assign(ns, -1);
+    int64_t grow = 0;
+    for (size_t i = 0; i < items.size(); ++i) {
+        const Item &it = items[i];
+        auto &loc = it.dist ? dis_loc[it.s] : col_loc[it.s];
+        loc.assign(it.n, std::string());
+        if (in_lds[i]) {
+            for (int64_t j = 0; j < it.n; ++j) loc[j] = "LP(" + std::to_string(rows_of[i][j]) + ")";
+            continue;
+        }
+        if (sep_row[it.s] < 0) sep_row[it.s] = grow, grow += it.n;  // (shared by both messages)
+        for (int64_t j = 0; j < it.n; ++j) loc[j] = "W(" + std::to_string(sep_row[it.s] + j) + "LL)";
+    }
+    for (int s = 0; s < ns; ++s) {
+        if (sep_row[s] < 0) sep_row[s] = 0;
+        if (dis_loc[s].empty()) dis_loc[s].assign(plan.seps[s].size(), "0.0");  // (in registers: never read)
+    }
+    if (getenv("FBN_JT_PLACE_DEBUG")) {  // diagnostic: the placement's summary
+        int64_t lc = 0, ld = 0, gc = 0, gd = 0, leaf = 0;
+        for (size_t i = 0; i < items.size(); ++i)
+            (items[i].dist ? (in_lds[i] ? ld : gd) : (in_lds[i] ? lc : gc)) += items[i].n;
+        for (int s = 0; s < ns; ++s)
+            if (plan.clique_down[plan.sep_down[s]].empty()) leaf += plan.seps[s].size();
+        fprintf(stderr, "placement: pool %lld of %lld rows; Collect rows LDS %lld global %lld; Distribute rows LDS %lld "
+                        "global %lld (registers: the rest); global rows %lld; leaf-separator rows %lld\n",
+                (long long)pool_rows, (long long)cap, (long long)lc, (long long)gc, (long long)ld, (long long)gd,
+                (long long)grow, (long long)leaf);
     }
 }
 
@@ -507,11 +641,6 @@ int JTGen::Run(std::string &src, int64_t *wave_entries, std::vector<double> &ini
         init_off[c] = (int64_t)initv.size();
         initv.insert(initv.end(), plan.cliques[c].pot.begin(), plan.cliques[c].pot.end());
     }
-    // per-wave workspace: one row (64 lanes x fp64) per separator entry
-    sep_row.assign(ns, 0);
-    int64_t rows = 0;
-    for (int s = 0; s < ns; ++s) sep_row[s] = rows, rows += plan.seps[s].size();
-    *wave_entries = std::max<int64_t>(rows, 1);
     int SD = 0;
     out_off.assign(V, 0);
     for (int v = 0; v < V; ++v) out_off[v] = SD, SD += plan.dom[v];
@@ -545,11 +674,19 @@ int JTGen::Run(std::string &src, int64_t *wave_entries, std::vector<double> &ini
         }
     }
     if ((int)post.size() != nc) return SetError(FBN_ERR_LIMIT, "codegen: tree traversal covers %zu of %d cliques", post.size(), nc);
+    // fp64 values per lane: table in flight + prefetched rows (FBN_JT_PREFETCH_BUDGET: tuning)
+    // (fast order: 260 -- round 5 sweep 150 / 200 / 260 / 320: 0.171 / 0.169 / 0.165 / 0.166 ms)
+    const int64_t kBudget = getenv("FBN_JT_PREFETCH_BUDGET") ? atoll(getenv("FBN_JT_PREFETCH_BUDGET")) : fast ? 260 : 200;
+    PlaceMessages(post, pre, kBudget);
+    int64_t rows = 0;
+    for (int s = 0; s < ns; ++s) rows = std::max<int64_t>(rows, sep_row[s] + plan.seps[s].size());
+    *wave_entries = std::max<int64_t>(rows, 1);
 
     o << "// generated by libfastbn (jt_codegen.cpp): " << nc << " cliques, " << ns << " separators, "
       << (fast ? "fast" : "exact") << " arithmetic order\n";
     o << "#define FBN_V " << V << "\n#define FBN_SD " << SD << "\n#define FBN_WE " << *wave_entries << "LL\n";
-    o << "#define FBN_IV_BASE " << lds_rows * 64 << "\n#define FBN_NIV " << initv.size() << "\n";
+    o << "#define FBN_LP_BASE " << lds_rows << "\n";
+    o << "#define FBN_IV_BASE " << (lds_rows + pool_rows) * 64 << "\n#define FBN_NIV " << initv.size() << "\n";
     o << "#define FBN_IV_LDS " << (iv_lds ? 1 : 0) << "\n#define FBN_MIN_WAVES " << min_waves << "\n";
     // diagnostic only (FBN_JT_WS_FOLD=K, wrong results): K workspaces shared by all waves, so the
     // workspace stays in L2 -- times the kernel without its workspace's fabric traffic
@@ -569,6 +706,8 @@ typedef __attribute__((address_space(4))) const double cdouble;
 typedef __attribute__((address_space(3))) double ldouble;
 extern __shared__ double fbn_lds[];
 #define L(row) (ltail[(row) * 64])
+// LDS message pool row (after the clique tail)
+#define LP(row) (ltail[(FBN_LP_BASE + (row)) * 64])
 // initial potentials: copied into LDS once per wave (wave-uniform address: broadcast reads), or
 // read with scalar loads from the constant buffer
 #if FBN_IV_LDS
@@ -591,6 +730,7 @@ __device__ __forceinline__ double frcp(double x) {
 #define CS (blkl * 64 + lane)
 #define ACT (CS < ncases)
 #define OUT(k) (marg[CS * FBN_SD + (k)])
+#define OUTS(k, v) (OUT(k) = (v))  // (non-temporal stores measured 2.1x slower: partial lines)
 extern "C" __global__ void __launch_bounds__(64, FBN_MIN_WAVES)
 fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restrict__ labels,
            double *__restrict__ ws, int *__restrict__ flags, const double *ivp, long long ncases,
@@ -659,9 +799,6 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
     }
     o << B(0);
 
-    // fp64 values per lane: table in flight + prefetched rows (FBN_JT_PREFETCH_BUDGET: tuning)
-    // (fast order: 260 -- round 5 sweep 150 / 200 / 260 / 320: 0.171 / 0.169 / 0.165 / 0.166 ms)
-    const int64_t kBudget = getenv("FBN_JT_PREFETCH_BUDGET") ? atoll(getenv("FBN_JT_PREFETCH_BUDGET")) : fast ? 260 : 200;
     auto tsize = [&](int c) { return plan.cliques[c].size(); };
     // ---------------- Collect, DFS post-order
     // loads of clique post[k]: its children's messages except a last child that is post[k-1]
@@ -724,17 +861,6 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
         for (int s : plan.clique_down[c]) r += plan.seps[s].size();
         return r;
     };
-    auto max_kid = [&](int c) {
-        int64_t r = 0;
-        for (int s : plan.clique_down[c]) r = std::max<int64_t>(r, plan.seps[s].size());
-        return r;
-    };
-    std::vector<bool> md_reg(ns, false);
-    for (int c : pre)
-        if (!plan.clique_down[c].empty()) {
-            const int s = plan.clique_down[c][0], q = child(s);
-            md_reg[s] = tsize(q) + plan.seps[s].size() + max_kid(q) <= kBudget;
-        }
     auto early_lb = [&](int c) {
         const int up = plan.clique_up[c];
         const int64_t held = (c != plan.root) ? plan.seps[up].size() : 0;  // in registers at DMul either way
@@ -798,7 +924,7 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
     }
     for (int v = 0; v < V; ++v) {
         o << "        if (ACT && " << observed(v) << ") {";
-        for (int d = 0; d < plan.dom[v]; ++d) o << " OUT(" << out_off[v] + d << ") = 0.0;";
+        for (int d = 0; d < plan.dom[v]; ++d) o << " OUTS(" << out_off[v] + d << ", 0.0);";
         o << " }\n";
     }
     o << R"(        const bool any_bad = __builtin_amdgcn_ballot_w64(bad != 0u) != 0ull;
@@ -818,8 +944,7 @@ int GenerateJTKernel(const JTPlanHost &plan, std::string &src, int64_t *wave_ent
                      int64_t *lds_bytes, bool fast) {
     JTGen g(plan, fast);
     int rc = g.Run(src, wave_entries, initv);
-    const bool iv_lds = !getenv("FBN_JT_IV_LDS") || atoi(getenv("FBN_JT_IV_LDS")) != 0;
-    if (lds_bytes) *lds_bytes = (g.lds_rows * 64 + (iv_lds ? (int64_t)initv.size() : 0)) * 8;
+    if (lds_bytes) *lds_bytes = ((g.lds_rows + g.pool_rows) * 64 + (g.iv_lds ? (int64_t)initv.size() : 0)) * 8;
     return rc;
 }
 

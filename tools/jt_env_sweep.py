@@ -32,7 +32,15 @@ def child(wpc):
     for _ in range(20):
         jt.run_device(d_ev.data_ptr(), n, d_lab.data_ptr(), d_marg.data_ptr(), s)
         ms.append(jt.last_kernel_ms())
-    print(json.dumps({"ms": float(np.median(ms[3:])), "min": float(min(ms))}))
+    # parity of the last run's first 256 cases against the oracle (labels, max relative error)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    torch.cuda.synchronize()
+    olab, omarg = O.OracleJT(xml).infer(ev[:256])
+    lab, marg = d_lab[:256].cpu().numpy(), d_marg[:256].cpu().numpy()
+    err = float(np.max(np.abs(marg - omarg) / np.maximum(np.abs(omarg), 1e-300)))
+    print(json.dumps({"ms": float(np.median(ms[3:])), "min": float(min(ms)), "labels_equal": bool((lab == olab).all()),
+                      "max_rel_err": err, "flagged": jt.debug_flagged_blocks()}))
 
 
 if __name__ == "__main__":
