@@ -252,14 +252,23 @@ def bench_pc(steps, warmup):
 
 def pc_small_traffic():
     """Measured L2<->fabric bytes of one device-resident search launch (rocprofv3 FETCH_SIZE +
-    WRITE_SIZE, calibrated; committed summary profiles/r04/pmc_pc_small_traffic.json from
-    tools/profile_r04.sh)."""
-    path = os.path.join(REPO, "profiles", "r04", "pmc_pc_small_traffic.json")
-    if not os.path.exists(path):
+    WRITE_SIZE, calibrated; committed summary profiles/r05/pmc_pc_small_traffic.json from
+    tools/profile_r05_final.sh)."""
+    path = _first_profile("r05/pmc_pc_small_traffic.json", "r04/pmc_pc_small_traffic.json")
+    if path is None:
         return {"traffic": None}
     with open(path) as f:
         t = json.load(f)
-    return {"traffic": t["hbm_bytes_per_launch"], "traffic_source": "profiles/r04/pmc_pc_small_traffic.json"}
+    return {"traffic": t["hbm_bytes_per_launch"], "traffic_source": os.path.relpath(path, REPO)}
+
+
+def _first_profile(*names):
+    """The first existing committed profile summary under profiles/ (this round's before older ones)."""
+    for n in names:
+        p = os.path.join(REPO, "profiles", n)
+        if os.path.exists(p):
+            return p
+    return None
 
 
 N_VARS_C5 = 1000
@@ -272,16 +281,16 @@ def pc_roofline(kernel_s, device_bytes, byte_column_bytes):
     """Config 5's CI kernels against the bounds they can hit: 32-bit VALU issue (popcount / AND
     for the bit-sliced kernels, the binning for the histogram kernel) and L2<->fabric traffic, per
     PC run; VALU instructions and fabric bytes per run from the committed PMC profile
-    (profiles/pc5_kernels.json: rocprofv3 --pmc SQ_INSTS_VALU / FETCH_SIZE / WRITE_SIZE, calibrated),
+    (profiles/r05/pc5_kernels.json: rocprofv3 --pmc SQ_INSTS_VALU / FETCH_SIZE / WRITE_SIZE, calibrated),
     the kernel time measured live (HIP events around every CI batch of a run)."""
-    path = os.path.join(REPO, "profiles", "pc5_kernels.json")
+    path = _first_profile("r05/pc5_kernels.json", "pc5_kernels.json")
     out = {"kernel_ms_per_run": 1e3 * kernel_s, "column_bytes_read_per_run": device_bytes,
            "model": {"bytes_per_run": byte_column_bytes,
                      "model_frac": byte_column_bytes / kernel_s / (HBM_PEAK_GBS * 1e9),
                      "note": "informational: SURVEY 8(d)'s byte-column model (every test streams N (d + 2) "
                              "uint8 bytes); the bit-sliced / FP4 kernels read packed masks from L2 instead, so "
                              "this ratio is not a bound (it exceeds 1)"}}
-    if not os.path.exists(path):
+    if path is None:
         return {"bound": None, **out}
     with open(path) as f:
         prof = json.load(f)
@@ -298,7 +307,7 @@ def pc_roofline(kernel_s, device_bytes, byte_column_bytes):
     else:
         r = {"bound": "hbm", "achieved": fab / kernel_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": fabric}
     return {**r, "traffic": fab, "valu_frac": valu, "fabric_frac": fabric, **out,
-            "dominant_kernel": {top: ks[top]}, "source": "profiles/pc5_kernels.json",
+            "dominant_kernel": {top: ks[top]}, "source": os.path.relpath(path, REPO),
             "note": "all CI kernels of one run: PMC VALU lane-ops and calibrated L2<->fabric bytes per run over the "
                     "live kernel time; neither bound is reached: the popcount kernels are bound by v_bcnt issue "
                     "(half rate on gfx950, tools/micro/valu_rate.hip) and latency, the level-0 Gram is a hand-written "
@@ -620,10 +629,10 @@ def bench_munin(steps, warmup, cases=125_000, rank=0, world=1, device=0, with_ba
 
 def munin_traffic(cases, kernel_ms):
     """Measured L2<->fabric bytes of the streamed kernel (rocprofv3 FETCH_SIZE + WRITE_SIZE, calibrated;
-    committed summary profiles/munin_traffic.json from tools/profile_round.sh), scaled to this launch,
+    committed summary profiles/r05/munin_traffic.json from tools/profile_r05_final.sh), scaled to this launch,
     and the rate they imply at this launch's kernel time."""
-    path = os.path.join(REPO, "profiles", "munin_traffic.json")
-    if not os.path.exists(path):
+    path = _first_profile("r05/munin_traffic.json", "munin_traffic.json")
+    if path is None:
         return {"traffic": None}
     with open(path) as f:
         t = json.load(f)

@@ -111,11 +111,35 @@ class JTGen {
     int64_t init_batch = 16;  // fast order: entries per software-pipelined batch of the fused product
     bool in_merged = false;  // the current op's closing boundary is left out
     int min_waves = 1;
+    // fast order: unbranched marginals with observed lanes stored as 0.0 (FBN_JT_MARG_V2, default 1)
+    // and 16-byte stores of adjacent values (FBN_JT_MARG_PAIR, default 1)
+    bool marg_v2 = true, marg_pair = true;
     // where each stored message lives, per separator entry: "W(row)" (the per-wave workspace in
     // global memory) or "LP(row)" (the LDS message pool); the Collect message (child -> parent) and
     // the Distribute message (parent -> child) of a separator are placed separately
     std::vector<std::vector<std::string>> col_loc, dis_loc;
     std::vector<bool> md_reg;  // Distribute messages kept in registers (first child, if it fits)
+    // fast order, opt-in (FBN_JT_LEAF_RC=1): Collect messages of small leaf cliques recomputed in the
+    // parent's Distribute (initial potential x home indicators, bin sums: the same expression as in
+    // Collect) instead of being parked from Collect to Distribute, stored only while the parent's
+    // Collect needs them.  ALARM: 195 -> 151 global rows, but 0.137 -> 0.155 ms -- the recomputation
+    // sits on the parent's critical path (gpurun_out/r05o), so it is off by default
+    std::vector<bool> leaf_rc, col_store;
+    void LoadCol(const std::string &name, int s) {
+        if (!leaf_rc[s]) return Load(name, s);
+        const int c = plan.sep_down[s];
+        const int64_t Ts = plan.seps[s].size(), Q = plan.cliques[c].size() / Ts;
+        for (int64_t j = 0; j < Ts; ++j) o << "        double " << name << s << "_" << j << ";\n";
+        o << "        { // recompute the Collect message of leaf clique " << c << "\n";
+        const std::string P = "r" + name;
+        InitProd(P, c, {}, -1, "");
+        for (int64_t j = 0; j < Ts; ++j) {
+            std::vector<std::string> terms;
+            for (int64_t q = 0; q < Q; ++q) terms.push_back(N(P, c, q * Ts + j));
+            o << "        " << name << s << "_" << j << " = " << TreeSum(terms) << ";\n";
+        }
+        o << "        }\n";
+    }
     void PlaceMessages(const std::vector<int> &post, const std::vector<int> &pre, int64_t budget);
     std::string B(int k) const {
         return profile ? "        FBN_OP_BOUNDARY(); FBN_STAMP(" + std::to_string(k) + ");\n" : "        FBN_OP_BOUNDARY();\n";
@@ -416,6 +440,38 @@ void JTGen::SepDis(const std::string &P, int c, int s, const std::string &old, b
 
 void JTGen::MargTerms(int v, const std::vector<std::vector<std::string>> &terms) {
     const int dim = plan.dom[v];
+    if (marg_v2) {
+        // unbranched: computed for every lane, observed lanes store 0.0 (the reference's marginal of
+        // an observed variable) in the same stores -- no divergent branch, no second store pass
+        // (ALARM 0.137 -> 0.130 ms); adjacent values go out as one 16-byte store per lane (neutral).
+        // (Measured and dropped: staging groups of 8 / 16 output values in LDS pool rows and writing
+        // them out coalesced, 0.205 / 0.223 ms -- gpurun_out/r05q.)
+        o << "        { // marginal of var " << v << "\n          const bool ob = " << observed(v) << " != 0u;\n";
+        std::vector<std::string> ps;
+        for (int d = 0; d < dim; ++d) {
+            o << "          const double p" << d << " = " << TreeSum(terms[d]) << ";\n";
+            ps.push_back("p" + std::to_string(d));
+        }
+        o << "          const double tot = " << TreeSum(ps) << "; const double yt = frcp(tot); bad |= ob ? 0u : den_bad(tot);\n";
+        if (v == 0) {
+            o << "          if (ACT && !ob) { int lab = 0; double mp = 0.0, m2 = 0.0;";
+            for (int d = 0; d < dim; ++d)
+                o << " { const double q = dv(p" << d << ", tot, yt); if (q > mp) { m2 = mp; mp = q; lab = " << d
+                  << "; } else if (q > m2) m2 = q; }";
+            o << " labels[CS] = lab; bad |= (mp - m2 <= 1e-12 * mp) ? 1u : 0u; }\n";
+        }
+        for (int d = 0; d < dim; ++d) {
+            const int64_t k = out_off[v] + d;
+            if (marg_pair && d + 1 < dim) {
+                o << "          if (ACT) OUTS2(" << k << ", ob ? 0.0 : dv(p" << d << ", tot, yt), ob ? 0.0 : dv(p" << d + 1 << ", tot, yt));\n";
+                ++d;
+            } else {
+                o << "          if (ACT) OUTS(" << k << ", ob ? 0.0 : dv(p" << d << ", tot, yt));\n";
+            }
+        }
+        o << "        }\n";
+        return;
+    }
     o << "        if (!" << observed(v) << ") { // marginal of var " << v << "\n";
     std::vector<std::string> ps;
     for (int d = 0; d < dim; ++d) {
@@ -528,6 +584,18 @@ void JTGen::PlaceMessages(const std::vector<int> &post, const std::vector<int> &
         }
     std::vector<int> pi(nc), qi(nc);
     for (int k = 0; k < nc; ++k) qi[post[k]] = k, pi[pre[k]] = k;
+    const bool no_leaf_rc = !getenv("FBN_JT_LEAF_RC") || atoi(getenv("FBN_JT_LEAF_RC")) == 0;  // (tuning)
+    leaf_rc.assign(ns, false);
+    col_store.assign(ns, true);
+    for (int s = 0; s < ns; ++s) {
+        const int c = plan.sep_down[s], p = plan.sep_up[s];
+        if (!fast || no_leaf_rc || !plan.clique_down[c].empty() || tsize(c) > 64) continue;
+        leaf_rc[s] = true;
+        // the parent's Collect takes the last child's message from registers when that child ran
+        // just before it (Run's collect_loads)
+        const auto &down = plan.clique_down[p];
+        col_store[s] = !(down.back() == s && qi[p] > 0 && post[qi[p] - 1] == c);
+    }
     struct Item {
         int s;
         bool dist;
@@ -537,7 +605,8 @@ void JTGen::PlaceMessages(const std::vector<int> &post, const std::vector<int> &
     std::vector<Item> items;
     for (int s = 0; s < ns; ++s) {
         const int c = plan.sep_down[s], p = plan.sep_up[s];
-        items.push_back({s, false, qi[c], nc + pi[p], plan.seps[s].size()});
+        if (!leaf_rc[s]) items.push_back({s, false, qi[c], nc + pi[p], plan.seps[s].size()});
+        else if (col_store[s]) items.push_back({s, false, qi[c], qi[p], plan.seps[s].size()});
         if (!md_reg[s]) items.push_back({s, true, nc + pi[p], nc + pi[c], plan.seps[s].size()});
     }
     // room: the LDS of four waves per CU (160 KB) less the clique tail and the initial potentials
@@ -608,6 +677,7 @@ void JTGen::PlaceMessages(const std::vector<int> &post, const std::vector<int> &
     for (int s = 0; s < ns; ++s) {
         if (sep_row[s] < 0) sep_row[s] = 0;
         if (dis_loc[s].empty()) dis_loc[s].assign(plan.seps[s].size(), "0.0");  // (in registers: never read)
+        if (col_loc[s].empty()) col_loc[s].assign(plan.seps[s].size(), "0.0");  // (recomputed: never read)
     }
     if (getenv("FBN_JT_PLACE_DEBUG")) {  // diagnostic: the placement's summary
         int64_t lc = 0, ld = 0, gc = 0, gd = 0, leaf = 0;
@@ -619,6 +689,17 @@ void JTGen::PlaceMessages(const std::vector<int> &post, const std::vector<int> &
                         "global %lld (registers: the rest); global rows %lld; leaf-separator rows %lld\n",
                 (long long)pool_rows, (long long)cap, (long long)lc, (long long)gc, (long long)ld, (long long)gd,
                 (long long)grow, (long long)leaf);
+        std::string u;
+        for (int t = 0; t <= 2 * nc; ++t) u += std::to_string(use[t]) + (t == nc - 1 ? " | " : " ");
+        fprintf(stderr, "pool rows in use by time (Collect | Distribute): %s\n", u.c_str());
+        if (fast) {
+            std::string m;
+            for (int v = 0; v < (int)plan.dom.size(); ++v) {
+                const int t = msep[v] >= 0 ? nc + pi[plan.sep_up[msep[v]]] : nc + pi[home[v]];
+                m += std::to_string(v) + ":" + std::to_string(t) + " ";
+            }
+            fprintf(stderr, "marginal time per variable: %s\n", m.c_str());
+        }
     }
 }
 
@@ -628,6 +709,8 @@ int JTGen::Run(std::string &src, int64_t *wave_entries, std::vector<double> &ini
     profile = getenv("FBN_JT_PROFILE") && atoi(getenv("FBN_JT_PROFILE")) != 0;  // diagnostic build
     merge = fast ? (getenv("FBN_JT_MERGE") ? atoi(getenv("FBN_JT_MERGE")) : kDefaultMerge) : 0;  // (tuning)
     init_batch = getenv("FBN_JT_INIT_BATCH") ? std::max<int64_t>(1, atoll(getenv("FBN_JT_INIT_BATCH"))) : 16;
+    marg_v2 = fast && (!getenv("FBN_JT_MARG_V2") || atoi(getenv("FBN_JT_MARG_V2")) != 0);  // (tuning)
+    marg_pair = marg_v2 && (!getenv("FBN_JT_MARG_PAIR") || atoi(getenv("FBN_JT_MARG_PAIR")) != 0);  // (tuning)
     // occupancy: waves per SIMD the register allocation must allow (1: up to 512 registers)
     min_waves = getenv("FBN_JT_MIN_WAVES") ? std::max(1, atoi(getenv("FBN_JT_MIN_WAVES"))) : min_waves;
     // initial potentials: LDS copy per wave (1) or scalar loads from the constant buffer (0)
@@ -691,6 +774,7 @@ int JTGen::Run(std::string &src, int64_t *wave_entries, std::vector<double> &ini
     // diagnostic only (FBN_JT_WS_FOLD=K, wrong results): K workspaces shared by all waves, so the
     // workspace stays in L2 -- times the kernel without its workspace's fabric traffic
     if (const char *e = getenv("FBN_JT_WS_FOLD")) o << "#define FBN_WS_FOLD " << atoi(e) << "\n";
+    if (getenv("FBN_JT_NO_OUT") && atoi(getenv("FBN_JT_NO_OUT")) != 0) o << "#define FBN_NO_OUT 1\n";
     o << R"FBN(typedef signed char i8;
 __device__ __forceinline__ double dv(double x, double den, double y) {  // x / den (Markstein, see jt_kernels.hip)
     const double q = x * y;
@@ -730,7 +814,18 @@ __device__ __forceinline__ double frcp(double x) {
 #define CS (blkl * 64 + lane)
 #define ACT (CS < ncases)
 #define OUT(k) (marg[CS * FBN_SD + (k)])
+#ifdef FBN_NO_OUT  // diagnostic only (FBN_JT_NO_OUT=1): marginals computed, never stored
+#define OUTS(k, v) do { if (ncases < 0) OUT(k) = (v); } while (0)
+#else
 #define OUTS(k, v) (OUT(k) = (v))  // (non-temporal stores measured 2.1x slower: partial lines)
+#endif
+// two adjacent output values in one 16-byte store (8-byte aligned: the rows are 8 * FBN_SD bytes)
+typedef double fbn_d2u __attribute__((ext_vector_type(2), aligned(8)));
+#ifdef FBN_NO_OUT
+#define OUTS2(k, a, b) do { if (ncases < 0) *(fbn_d2u *)&OUT(k) = (fbn_d2u){(a), (b)}; } while (0)
+#else
+#define OUTS2(k, a, b) (*(fbn_d2u *)&OUT(k) = (fbn_d2u){(a), (b)})
+#endif
 extern "C" __global__ void __launch_bounds__(64, FBN_MIN_WAVES)
 fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restrict__ labels,
            double *__restrict__ ws, int *__restrict__ flags, const double *ivp, long long ncases,
@@ -846,7 +941,7 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
         }
         // merge the message's sums with the next clique's product when both are small
         in_merged = fast && (merge & 2) && c != plan.root && k + 1 < post.size() && tsize(c) + tsize(post[k + 1]) <= 96;
-        if (c != plan.root) SepCol("t", c, plan.clique_up[c], true);
+        if (c != plan.root) SepCol("t", c, plan.clique_up[c], col_store[plan.clique_up[c]]);
     }
     in_merged = false;
     // ---------------- Distribute, DFS pre-order (root continues from its Collect registers)
@@ -875,7 +970,7 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
         int64_t pend = 0;
         if (early)
             for (int s : plan.clique_down[c]) {
-                if (!loaded_b[s]) Load("lb", s), loaded_b[s] = true;
+                if (!loaded_b[s]) LoadCol("lb", s), loaded_b[s] = true;
                 pend += plan.seps[s].size();
             }
         if (c != plan.root && md_reg[up]) pend += plan.seps[up].size();
@@ -887,7 +982,7 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
             if (tsize(c) + pend + nrows <= kBudget) {
                 if (early_lb(nx))
                     for (int s : plan.clique_down[nx])
-                        if (!loaded_b[s]) Load("lb", s), loaded_b[s] = true;
+                        if (!loaded_b[s] && !leaf_rc[s]) Load("lb", s), loaded_b[s] = true;
                 if (ld_next && !loaded_d[nup]) Load("ld", nup), loaded_d[nup] = true;
             }
         }
@@ -903,7 +998,7 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
             P = "u";  // recompute the Collect table (same ops, same order -> same bits)
             Init(P, c);
             for (int s : plan.clique_down[c]) {
-                if (!early) Load("lb", s), o << B(1);
+                if (!early) LoadCol("lb", s), o << B(1);
                 Mul(P, c, s, "lb");
             }
             if (!md_reg[up] && !loaded_d[up]) Load("ld", up), loaded_d[up] = true, o << B(1);
@@ -915,14 +1010,14 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
         if (!fast && down.size() + plan.cliques[c].vars.size() >= 2) Normalize(P, c);
         in_merged = fast && (merge & 1) && early;
         for (size_t i = 0; i < down.size(); ++i) {
-            if (!early) Load("lc", down[i]), o << B(1);
+            if (!early) LoadCol("lc", down[i]), o << B(1);
             SepDis(P, c, down[i], early ? "lb" : "lc", !md_reg[down[i]]);
         }
         Marg(P, c);
         if (in_merged) o << B(8);
         in_merged = false;
     }
-    for (int v = 0; v < V; ++v) {
+    for (int v = 0; v < V && !marg_v2; ++v) {  // (unbranched marginals store the zeros themselves)
         o << "        if (ACT && " << observed(v) << ") {";
         for (int d = 0; d < plan.dom[v]; ++d) o << " OUTS(" << out_off[v] + d << ", 0.0);";
         o << " }\n";
