@@ -169,6 +169,12 @@ __device__ __forceinline__ void count_pair(const uint32_t *__restrict__ bx, cons
 // exactly -- N[c][a][DY-1] = N_xz[a][c] - sum_b, N[c][DX-1][b] = N_yz[b][c] - sum_a,
 // N[DZ-1][a][b] = N_xy[a][b] - sum_c; only DX-1, DY-1, DZ-1 mask rows are read
 template <int DX, int DY, int DZ>
+__device__ __forceinline__ void derived_finish(uint32_t (&cnt)[(DX - 1) * (DY - 1) * (DZ - 1) > 0 ? (DX - 1) * (DY - 1) * (DZ - 1) : 1],
+                                               const int32_t *__restrict__ Txy, bool txy,
+                                               const int32_t *__restrict__ Txz, bool txz,
+                                               const int32_t *__restrict__ Tyz, bool tyz,
+                                               int32_t (&full)[DZ * DX * DY]);
+template <int DX, int DY, int DZ>
 __device__ __forceinline__ void count_test_derived_full(const uint32_t *__restrict__ bx,
                                                         const uint32_t *__restrict__ by,
                                                         const uint32_t *__restrict__ bz, long long W, int lane,
@@ -201,6 +207,19 @@ __device__ __forceinline__ void count_test_derived_full(const uint32_t *__restri
                         for (int c = 0; c < MZ; ++c) cnt[(c * MX + a) * MY + b] += __builtin_popcount(xy & z[c][k]);
                     }
         }
+    }
+    derived_finish<DX, DY, DZ>(cnt, Txy, txy, Txz, txz, Tyz, tyz, full);
+}
+
+// the wave totals of the leading cells (butterfly) and the derived rest of the table
+template <int DX, int DY, int DZ>
+__device__ __forceinline__ void derived_finish(uint32_t (&cnt)[(DX - 1) * (DY - 1) * (DZ - 1) > 0 ? (DX - 1) * (DY - 1) * (DZ - 1) : 1],
+                                               const int32_t *__restrict__ Txy, bool txy,
+                                               const int32_t *__restrict__ Txz, bool txz,
+                                               const int32_t *__restrict__ Tyz, bool tyz,
+                                               int32_t (&full)[DZ * DX * DY]) {
+    constexpr int MX = DX - 1, MY = DY - 1, MZ = DZ - 1, M = MX * MY * MZ, NC = M > 0 ? M : 1;
+    if (M > 0) {
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             uint32_t v = cnt[c];
@@ -521,6 +540,7 @@ __global__ __launch_bounds__(256) void ci_bits_count_derived(const uint32_t *__r
                                                              const long long *__restrict__ n_dev) {
     count_derived_items(bits, dims, row0, items, W, n_dev ? *n_dev : n, counts, pairtab, nvars, xcd);
 }
+
 
 
 // ---- row Gram matrices (levels 0 and 1 of a PC run on the bit-sliced store)
