@@ -41,6 +41,7 @@ _SIGS = {
     "fbn_jt_run_device": [_vp, _vp, _i64, _vp, _vp, _vp],
     "fbn_jt_evidence_validate": [_vp, _vp, _i64, _vp],
     "fbn_jt_set_evidence_check": [_vp, C.c_int],
+    "fbn_jt_set_kernel_timing": [_vp, C.c_int],
     "fbn_jt_score": [_vp, _vp, _vp, _i64, _vp, _vp],
     "fbn_jt_last_kernel_ms": [_vp, _vp],
     "fbn_jt_stream_schedule": [_vp, _vp, C.c_int64, _vp, C.c_int64, _vp, _vp],
@@ -456,6 +457,11 @@ class JunctionTree(_Handle):
         """Device-side evidence range check of a device buffer; raises FastBNError if a code is out
         of its node's domain."""
         lib.fbn_jt_evidence_validate(self._h, d_evidence_ptr, ncases, stream_ptr)
+
+    def set_kernel_timing(self, enable):
+        """fbn_jt_set_kernel_timing: enable = False records no timing events per run (last_kernel_ms
+        then raises); for callers that time with their own events."""
+        lib.fbn_jt_set_kernel_timing(self._h, int(bool(enable)))
 
     def set_evidence_check(self, enable):
         """run_device's per-call evidence check (default on); off = fully asynchronous runs of a

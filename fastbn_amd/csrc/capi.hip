@@ -198,7 +198,7 @@ struct fbn_jt_plan {
     DevBuf ddom, evcheck;  // device-side evidence range check (fbn_jt_run, fbn_jt_run_device)
     bool ev_check = true;  // fbn_jt_set_evidence_check
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    bool timed = false;
+    bool timed = false, ktiming = true;
     ~fbn_jt_plan() {
         for (auto &k : gen)
             if (k.mod) (void)hipModuleUnload(k.mod);
@@ -892,8 +892,11 @@ static int LaunchLds(fbn_jt_plan *p, DevBuf &ws, const int8_t *d_evidence, int64
     int wpc, cap, rc;
     LdsGeometry(p, &wpc, &cap);
     const bool spill = cap < l.max_table;
-    // fixup mode: flagged blocks are rare, one wave per CU scans the flags
-    int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * (flags ? 1 : wpc));
+    // fixup mode: flagged blocks are rare; one wave per CU scans the flags 64 at a time (the launch
+    // follows every specialized / tiled launch: ~3 us per call on ALARM, grids of 4 / 16 / 256 waves
+    // measured alike; FBN_JT_FIX_GRID: tuning)
+    static const int fix_grid = getenv("FBN_JT_FIX_GRID") ? std::max(1, atoi(getenv("FBN_JT_FIX_GRID"))) : 0;
+    int grid = (int)std::min<int64_t>(nblk, flags ? (int64_t)(fix_grid > 0 ? fix_grid : p->num_cu) : (int64_t)p->num_cu * wpc);
     const int64_t store_off = 0, den_off = l.store_entries, sep_off = den_off + nc, spill_off = sep_off + l.sep_entries;
     const int64_t wave_entries = spill_off + (spill ? l.max_table - cap : 0);
     if (flags)  // fixup mode: at most ~2 GiB of workspace (large trees need ~100 MB per wave)
@@ -948,6 +951,12 @@ int fbn_jt_evidence_validate(fbn_jt_plan *p, const int8_t *d_evidence, int64_t n
     if (p->device < 0) return SetError(FBN_ERR_NODEV, "host-only plan (created with device < 0)");
     FBN_HIP(hipSetDevice(p->device));
     return JtCheckEvidence(p, d_evidence, ncases, static_cast<hipStream_t>(hip_stream));
+}
+
+int fbn_jt_set_kernel_timing(fbn_jt_plan *p, int enable) {
+    if (!p) return SetError(FBN_ERR_ARG, "null pointer");
+    p->ktiming = enable != 0;
+    return FBN_OK;
 }
 
 int fbn_jt_set_evidence_check(fbn_jt_plan *p, int enable) {
@@ -1014,7 +1023,7 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
         const size_t ws_d = (size_t)grid * g.state_entries * 64 * 8;
         const size_t ws_i = (size_t)grid * nc * 64 * 4;
         if ((rc = p->ws.ensure(ws_d + ws_i))) return rc;
-        FBN_HIP(hipEventRecord(p->ev0, s));
+        if (p->ktiming) FBN_HIP(hipEventRecord(p->ev0, s));
         hipError_t e = fbn_jt_launch(p->ops.as<JtOp>(), (int)g.ops.size(), p->aux.as<int32_t>(), p->initv.as<double>(),
                                      p->dig.as<uint64_t>(), d_evidence, V, ncases, SD, marg, labels,
                                      p->ws.as<double>(), reinterpret_cast<int32_t *>(p->ws.as<char>() + ws_d),
@@ -1037,7 +1046,7 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
         const size_t ws_d = (size_t)grid * per_blk_d;
         if ((rc = p->ws.ensure(ws_d + (size_t)grid * per_blk_i))) return rc;
         if ((rc = p->flags.ensure((size_t)nblk * 4))) return rc;
-        FBN_HIP(hipEventRecord(p->ev0, s));
+        if (p->ktiming) FBN_HIP(hipEventRecord(p->ev0, s));
         hipError_t e = fbn_jt_virt_launch(p->vcl.as<JtVClique>(), p->vaux.as<int32_t>(), p->viv.as<double>(),
                                           p->vdig.as<uint64_t>(), p->vorder.as<int32_t>(), p->vsched.as<int32_t>(),
                                           p->vsel.as<int32_t>(), d_evidence, marg, labels, p->ws.as<double>(),
@@ -1076,7 +1085,7 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
             p->last_grid = 1;
             tprof = p->prof.as<unsigned long long>();
         }
-        FBN_HIP(hipEventRecord(p->ev0, s));
+        if (p->ktiming) FBN_HIP(hipEventRecord(p->ev0, s));
         hipError_t e = fbn_jt_tile_launch(p->tpass.as<JtTPass>(), (int)t.passes.size(), p->ttab.as<int32_t>(),
                                           p->tiv.as<double>(), d_evidence, marg, labels, p->ws.as<double>(),
                                           p->flags.as<int>(), ncases, t.store_rows, t.scr_row, t.red_row, V, SD,
@@ -1096,7 +1105,7 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
         const int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * wpc);
         if ((rc = p->ws.ensure((size_t)grid * gk.we * 64 * 8))) return rc;
         if ((rc = p->flags.ensure((size_t)nblk * 4))) return rc;
-        FBN_HIP(hipEventRecord(p->ev0, s));
+        if (p->ktiming) FBN_HIP(hipEventRecord(p->ev0, s));
 
         const int8_t *a_ev = d_evidence;
         double *a_marg = marg, *a_ws = p->ws.as<double>();
@@ -1120,11 +1129,11 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
         if (!no_fix3 && (rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s)))
             return rc;
     } else {
-        FBN_HIP(hipEventRecord(p->ev0, s));
+        if (p->ktiming) FBN_HIP(hipEventRecord(p->ev0, s));
         if ((rc = LaunchLds(p, p->ws, d_evidence, ncases, labels, marg, nullptr, variant == 2, s))) return rc;
     }
-    FBN_HIP(hipEventRecord(p->ev1, s));
-    p->timed = true;
+    if (p->ktiming) FBN_HIP(hipEventRecord(p->ev1, s));
+    p->timed = p->ktiming;
     return FBN_OK;
 }
 

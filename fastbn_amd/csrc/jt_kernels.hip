@@ -451,8 +451,26 @@ __global__ __launch_bounds__(64) void jt_lds_kernel(const JtOp *__restrict__ ops
     int32_t *__restrict__ red = wsi + (size_t)blockIdx.x * (size_t)A.nc * 64 + lane;
     const Tab<SPILL> T{lds + lane, W + (size_t)A.spill_off * 64, A.cap};
 
-    for (long long blk = blockIdx.x; blk * 64 < A.ncases; blk += gridDim.x) {
-        if (A.flags && A.flags[blk] == 0) continue;
+    // blocks: grid stride; fixup mode (flags): each wave scans 64 flags per step (one load per lane +
+    // a ballot) and runs only the flagged blocks -- a one-flag-per-step scan is a chain of dependent
+    // scalar loads, ~80 ns each, which made a small fixup grid cost more than the kernel it checks
+    long long blk = -1, cbase = (long long)blockIdx.x * 64 - (long long)gridDim.x * 64;
+    unsigned long long pend = 0ull;
+    for (;;) {
+        if (A.flags) {
+            while (pend == 0ull) {
+                cbase += (long long)gridDim.x * 64;
+                if (cbase * 64 >= A.ncases) break;
+                const long long b = cbase + lane;
+                pend = __ballot(b * 64 < A.ncases && A.flags[b] != 0);
+            }
+            if (pend == 0ull) break;
+            blk = cbase + __builtin_ctzll(pend);
+            pend &= pend - 1ull;
+        } else {
+            blk = blk < 0 ? (long long)blockIdx.x : blk + gridDim.x;
+            if (blk * 64 >= A.ncases) break;
+        }
         const long long cs = blk * 64 + lane;
         const bool act = cs < A.ncases;
         const long long csr = act ? cs : A.ncases - 1;

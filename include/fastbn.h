@@ -158,6 +158,9 @@ int fbn_jt_score(const fbn_jt_plan *p, const double *marginals, const double *go
                  double *mse_sum, double *hd_sum);
 /* Device kernel time (ms, hipEvent) of the last fbn_jt_run*; launches of the main kernel. */
 int fbn_jt_last_kernel_ms(const fbn_jt_plan *p, float *ms);
+/* enable = 0: fbn_jt_run* records no timing events (two fewer stream markers per call; callers that
+ * time with their own events); fbn_jt_last_kernel_ms then fails.  Default 1. */
+int fbn_jt_set_kernel_timing(fbn_jt_plan *p, int enable);
 /* Tuning: persistent waves per CU (0 = default: as many as keep the largest clique in LDS). */
 int fbn_jt_set_waves_per_cu(fbn_jt_plan *p, int waves);
 /* Kernel variant: -1 = auto (default: 3 when eligible and its code object loads, else 5 in the fast
