@@ -45,11 +45,32 @@ def fixture_xmls(dirname):
     return out
 
 
+# code-generation options the GPU tests run ALARM under (tests/test_gpu_jt_fast.py)
+ALARM_TEST_OPTIONS = ({"FBN_JT_LEAF_RC": "1"}, {"FBN_JT_LDS_POOL": "0"}, {"FBN_JT_MARG_V2": "0"})
+
+
+def prebuild_options(xml, options):
+    """The fast-order kernel of `xml` under each set of generator environment options (read when
+    the kernel is generated), built in a child process per set."""
+    import subprocess
+    import sys
+    out = []
+    for opt in options:
+        env = dict(os.environ, **opt)
+        code = ("import sys; sys.path.insert(0, %r); from fastbn_amd import api; "
+                "print(api.JunctionTree(api.Network(%r), device=-1).build_kernel())" % (REPO, xml))
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
+        out.append(r.stdout.strip().splitlines()[-1])
+    return out
+
+
 def prebuild_default(clean=True):
-    """Every eligible benchmark / test network, both orders (cache hits are free); clean: then drop
-    the code objects no current plan uses (older generator versions)."""
+    """Every eligible benchmark / test network, both orders (cache hits are free), and the ALARM
+    option variants the tests use; clean: then drop the code objects no current plan uses (older
+    generator versions)."""
     with tempfile.TemporaryDirectory() as d:
         built = prebuild([ALARM_XML, synth_small_xml(d)] + fixture_xmls(d))
+    built += prebuild_options(ALARM_XML, ALARM_TEST_OPTIONS)
     if clean:
         keep = {os.path.basename(p) for p in built}
         kdir = os.path.join(REPO, "fastbn_amd", "kcache")

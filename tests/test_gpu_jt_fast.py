@@ -11,7 +11,7 @@ from conftest import GOLD, read_ref_marg
 
 import fastbn_amd as F
 import oracle as O
-from fastbn_amd import synth
+from fastbn_amd import prebuild, synth
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-12
@@ -102,3 +102,37 @@ def test_fast_specialized_synthetic(tmp_path):
     olab, omarg = O.OracleJT(p).infer(ev)
     np.testing.assert_array_equal(lab, olab)
     _close(marg, omarg)
+
+
+@pytest.mark.parametrize("env", prebuild.ALARM_TEST_OPTIONS)
+def test_fast_codegen_options_vs_reference(alarm_paths, monkeypatch, env):
+    """Code-generation options of the fast order against the reference's own ALARM dump: leaf
+    Collect messages recomputed in the parent's Distribute (opt-in), no LDS message pool (every
+    message in the per-wave global rows), and the branched marginal stores -- each changes where a
+    message lives or how a marginal is stored, never the values (labels equal, <= 1e-12)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    j = F.JunctionTree(F.Network(alarm_paths["xml"]), device=0)
+    j.set_variant(3)
+    ev, _ = F.load_libsvm(alarm_paths["rand"], 37)
+    lab, marg = j.infer(ev)
+    assert j.debug_flagged_blocks() == 0
+    rlab, rmarg, _, _ = read_ref_marg(os.path.join(GOLD, "alarm_rand.marg.gz"), j.network.dims)
+    np.testing.assert_array_equal(lab, rlab)
+    _close(marg, rmarg)
+
+
+def test_kernel_timing_switch(jt):
+    """fbn_jt_set_kernel_timing(0): no timing events (last_kernel_ms raises), identical results."""
+    ev = synth.evidence_cases(synth.read_xmlbif(os.path.join(GOLD, "alarm", "alarm.xml")), 5000, 7, seed=11)
+    lab0, marg0 = jt.infer(ev)
+    assert jt.last_kernel_ms() > 0
+    jt.set_kernel_timing(False)
+    try:
+        lab1, marg1 = jt.infer(ev)
+        with pytest.raises(F.FastBNError):
+            jt.last_kernel_ms()
+    finally:
+        jt.set_kernel_timing(True)
+    np.testing.assert_array_equal(lab0, lab1)
+    np.testing.assert_array_equal(marg0, marg1)
