@@ -574,16 +574,17 @@ void JTGen::Marg(const std::string &P, int c) {
 void JTGen::PlaceMessages(const std::vector<int> &post, const std::vector<int> &pre, int64_t budget) {
     const int nc = (int)plan.cliques.size(), ns = (int)plan.seps.size();
     auto tsize = [&](int c) { return plan.cliques[c].size(); };
+    std::vector<int> pi(nc), qi(nc);
+    for (int k = 0; k < nc; ++k) qi[post[k]] = k, pi[pre[k]] = k;
     md_reg.assign(ns, false);
     for (int c : pre)
         if (!plan.clique_down[c].empty()) {
-            const int s = plan.clique_down[c][0], q = child(s);
+            // the child Distribute visits first (the next clique of the pre-order)
+            const int q = pre[pi[c] + 1], s = plan.clique_up[q];
             int64_t mk = 0;
             for (int s2 : plan.clique_down[q]) mk = std::max<int64_t>(mk, plan.seps[s2].size());
             md_reg[s] = tsize(q) + plan.seps[s].size() + mk <= budget;
         }
-    std::vector<int> pi(nc), qi(nc);
-    for (int k = 0; k < nc; ++k) qi[post[k]] = k, pi[pre[k]] = k;
     const bool no_leaf_rc = !getenv("FBN_JT_LEAF_RC") || atoi(getenv("FBN_JT_LEAF_RC")) == 0;  // (tuning)
     leaf_rc.assign(ns, false);
     col_store.assign(ns, true);
@@ -593,8 +594,7 @@ void JTGen::PlaceMessages(const std::vector<int> &post, const std::vector<int> &
         leaf_rc[s] = true;
         // the parent's Collect takes the last child's message from registers when that child ran
         // just before it (Run's collect_loads)
-        const auto &down = plan.clique_down[p];
-        col_store[s] = !(down.back() == s && qi[p] > 0 && post[qi[p] - 1] == c);
+        col_store[s] = !(qi[p] > 0 && post[qi[p] - 1] == c);
     }
     struct Item {
         int s;
@@ -741,21 +741,40 @@ int JTGen::Run(std::string &src, int64_t *wave_entries, std::vector<double> &ini
                 const int64_t have = msep[v] >= 0 ? plan.seps[msep[v]].size() : plan.cliques[home[v]].size();
                 if (plan.seps[sp].size() < have) msep[v] = sp;
             }
-    // traversal orders
-    std::vector<int> post, pre;
-    std::vector<std::pair<int, size_t>> st{{plan.root, 0}};
-    while (!st.empty()) {  // iterative DFS
-        auto &top = st.back();
-        const int c = top.first;
-        if (top.second == 0) pre.push_back(c);
-        if (top.second < plan.clique_down[c].size()) {
-            const int ch = child(plan.clique_down[c][top.second++]);
-            st.push_back({ch, 0});
-        } else {
-            post.push_back(c);
-            st.pop_back();
+    // traversal orders: Collect in post-order, Distribute in pre-order of a DFS.  Any child order
+    // gives the same values (schedule freedom, section 4 of DESIGN.md); the fast order may pick one
+    // per phase (FBN_JT_CHILD_ORDER bits, tuning): 1 = Collect visits children by ascending
+    // separator size (a big message is produced last, so it is parked for less of the schedule),
+    // 2 = Distribute visits them by descending size (a big message is consumed first)
+    const int child_order = fast && getenv("FBN_JT_CHILD_ORDER") ? atoi(getenv("FBN_JT_CHILD_ORDER")) : 0;
+    auto dfs = [&](bool collect, std::vector<int> &post_o, std::vector<int> &pre_o) {
+        std::vector<std::vector<int>> kids(nc);
+        for (int c = 0; c < nc; ++c) {
+            kids[c] = plan.clique_down[c];
+            const bool asc = collect && (child_order & 1), desc = !collect && (child_order & 2);
+            if (asc || desc)
+                std::stable_sort(kids[c].begin(), kids[c].end(), [&](int x, int y) {
+                    return asc ? plan.seps[x].size() < plan.seps[y].size() : plan.seps[x].size() > plan.seps[y].size();
+                });
         }
-    }
+        std::vector<std::pair<int, size_t>> st{{plan.root, 0}};
+        while (!st.empty()) {  // iterative DFS
+            auto &top = st.back();
+            const int c = top.first;
+            if (top.second == 0) pre_o.push_back(c);
+            if (top.second < kids[c].size()) {
+                const int ch = child(kids[c][top.second++]);
+                st.push_back({ch, 0});
+            } else {
+                post_o.push_back(c);
+                st.pop_back();
+            }
+        }
+    };
+    std::vector<int> post, pre, unused;
+    dfs(true, post, unused);
+    unused.clear();
+    dfs(false, unused, pre);
     if ((int)post.size() != nc) return SetError(FBN_ERR_LIMIT, "codegen: tree traversal covers %zu of %d cliques", post.size(), nc);
     // fp64 values per lane: table in flight + prefetched rows (FBN_JT_PREFETCH_BUDGET: tuning)
     // (fast order: 260 -- round 5 sweep 150 / 200 / 260 / 320: 0.171 / 0.169 / 0.165 / 0.166 ms)
@@ -902,7 +921,7 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
         const int c = post[k];
         const auto &down = plan.clique_down[c];
         for (size_t i = 0; i < down.size(); ++i)
-            if (!(i + 1 == down.size() && k > 0 && child(down[i]) == post[k - 1])) ls.push_back(down[i]);
+            if (!(k > 0 && child(down[i]) == post[k - 1])) ls.push_back(down[i]);  // (the child just collected: registers)
     };
     auto rows_of = [&](const std::vector<int> &ls) {
         int64_t r = 0;
