@@ -2302,7 +2302,9 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
     FBN_HIP(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     int rc;
-    std::vector<int32_t> adjf, adj_off(nv + 1, 0);
+    static thread_local std::vector<int32_t> adjf, adj_off;  // (capacity kept across runs)
+    adjf.clear();
+    adj_off.assign(nv + 1, 0);
     for (int u = 0; u < nv; ++u) {
         adj_off[u] = (int32_t)adjf.size();
         adjf.insert(adjf.end(), adj[u].begin(), adj[u].end());
@@ -2345,7 +2347,9 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
     // chunk x2 per round: rounds here cost a few launches, speculation costs counted tests (config 5:
     // x4 launches 430k tests for 294k counted, x2 345k)
     const int64_t growth = std::max<int64_t>(2, EnvOr0("FBN_PC_GROWTH", 2));
-    const int64_t max_chunk = std::max<int64_t>(1, std::min<int64_t>(1 << 16, (int64_t)INT32_MAX / E));
+    // (FBN_PC_L1_MAXCHUNK: tuning -- a cap on the per-edge chunk trades speculative tests for rounds)
+    const int64_t max_chunk = std::max<int64_t>(
+        1, std::min<int64_t>(std::min<int64_t>(1 << 16, EnvOr0("FBN_PC_L1_MAXCHUNK", 1 << 16)), (int64_t)INT32_MAX / E));
     chunk = std::min(chunk, max_chunk);
     // the setup writes round 0's lengths and zeroes the open-count ring; each round's resolve writes
     // the next round's lengths and zeroes the other ring slot (no length kernel or memset per round)

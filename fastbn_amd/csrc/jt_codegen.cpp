@@ -745,7 +745,9 @@ int JTGen::Run(std::string &src, int64_t *wave_entries, std::vector<double> &ini
     // gives the same values (schedule freedom, section 4 of DESIGN.md); the fast order may pick one
     // per phase (FBN_JT_CHILD_ORDER bits, tuning): 1 = Collect visits children by ascending
     // separator size (a big message is produced last, so it is parked for less of the schedule),
-    // 2 = Distribute visits them by descending size (a big message is consumed first)
+    // 2 = Distribute visits them by descending size (a big message is consumed first).  ALARM: 1
+    // changes nothing, 2 moves 85 message rows to registers and measured slower (0.127 -> 0.132 ms,
+    // gpurun_out/r05y), so the default keeps the plan's order
     const int child_order = fast && getenv("FBN_JT_CHILD_ORDER") ? atoi(getenv("FBN_JT_CHILD_ORDER")) : 0;
     auto dfs = [&](bool collect, std::vector<int> &post_o, std::vector<int> &pre_o) {
         std::vector<std::vector<int>> kids(nc);

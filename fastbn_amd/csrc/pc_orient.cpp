@@ -384,7 +384,12 @@ struct Orienter {
         }
         std::vector<SepsetMap::View> z(tri.size());
         std::vector<char> found(tri.size());
+        auto tq = std::chrono::steady_clock::now();
         sepset.find_many(keys.data(), keys.size(), z.data(), found.data());
+        auto tr = std::chrono::steady_clock::now();
+        if (getenv("FBN_PC_TIMING"))
+            fprintf(stderr, "orient: %zu unshielded triples, sepset lookups %.3f ms\n", tri.size(),
+                    std::chrono::duration<double, std::milli>(tr - tq).count());
         for (size_t t = 0; t < tri.size(); ++t) {
             const int a = tri[t].a, b = tri[t].b, c = tri[t].c;
             if (found[t] && std::find(z[t].begin(), z[t].end(), b) != z[t].end()) continue;
