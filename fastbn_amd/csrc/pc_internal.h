@@ -87,16 +87,7 @@ class SepsetMap {
     // the entries near the last hit instead of a cold binary search over the whole run
     // (orientation's v-structure pass: ~1.7k lookups on a 1000-variable run)
     void find_many(const std::pair<int, int> *keys, size_t n, View *v, char *found) const {
-        // the level-0 flags first (most keys of a PC run end there), then only the rest sorted.  The
-        // flags are one byte per pair of the complete graph (0.5 MB at 1,000 variables) and the keys
-        // hit it at random: every lookup is a cache miss, so all of them are prefetched first and
-        // the misses overlap (config 5: 1,710 lookups 0.088 ms before)
-        if (!l0_.empty())
-            for (size_t q = 0; q < n; ++q) {
-                const int i = keys[q].first, j = keys[q].second;
-                if (0 <= i && i < j && j < n0_)
-                    __builtin_prefetch(&l0_[(size_t)i * n0_ - (size_t)i * (i + 1) / 2 + (size_t)(j - i - 1)]);
-            }
+        // the level-0 flags first (most keys of a PC run end there), then only the rest sorted
         std::vector<uint32_t> open;
         open.reserve(n);
         for (size_t q = 0; q < n; ++q) {
