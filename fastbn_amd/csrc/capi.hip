@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <new>
 #include <string>
@@ -59,6 +60,8 @@ extern "C" hipError_t fbn_ci_sum_planes(const int32_t *planes, int np, long long
 extern "C" hipError_t fbn_ci_onehot_build(const uint8_t *cols, const int32_t *dims, const int32_t *lead0, long long N,
                                           long long Npad, int nvars, int8_t *out, hipStream_t s);
 extern "C" size_t fbn_ci_l1_edge_bytes(void);
+extern "C" hipError_t fbn_ci_kept_csr(const uint8_t *indep, int n, int32_t *low, int32_t *up, int32_t *off,
+                                      int32_t *upoff, int32_t *adj, int32_t *pairs, long long *scal, hipStream_t s);
 extern "C" hipError_t fbn_ci_l1_setup(const int32_t *pairs, int E, const int32_t *adj, const int32_t *adj_off,
                                       void *ed, int32_t *pos, uint8_t *st, int32_t *sep, long long *counted,
                                       int chunk0, int32_t *len, int32_t *off, unsigned *ring,
@@ -264,6 +267,13 @@ struct fbn_ci_ctx {
     DevBuf l1pairs, l1adj, l1adjoff, l1ed, l1pos, l1st, l1sep, l1cnt, l1len, l1off, l1scal, l1open;
     DevBuf l1items, l1counts, l1df, l1indep, l1sstat;  // l1sstat: the offset scan's per-tile status words
     DevBuf keptidx, kepttmp;  // level-0 kept pair indices (CiAllPairsKept)
+    // level 0 -> level 1 on the device (CiL0L1Device): per-variable kept counts, upper-part offsets,
+    // (E, candidate sets); the side stream copies the flags / edge list to the host meanwhile
+    DevBuf kcnt, kupoff, kscal;
+    hipStream_t side = nullptr;
+    hipEvent_t side_ev = nullptr, main_ev = nullptr;
+    void *h_pairs = nullptr;
+    size_t h_pairs_bytes = 0;
     // level-0 Gram on the matrix cores (ci_gram_mfma.hip): FP4 one-hot store (Rp x Kb bytes, built
     // once, stage-major), the tile list of row range [g4_r0, g4_r1), split-K slabs
     DevBuf onehot4, g4tasks, g4slab;
@@ -312,6 +322,10 @@ struct fbn_ci_ctx {
         if (h_small) (void)hipHostFree(h_small);
         for (auto &e : l1ev)
             if (e) (void)hipEventDestroy(e);
+        if (h_pairs) (void)hipHostFree(h_pairs);
+        if (side_ev) (void)hipEventDestroy(side_ev);
+        if (main_ev) (void)hipEventDestroy(main_ev);
+        if (side) (void)hipStreamDestroy(side);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -2221,7 +2235,8 @@ int CiBatchLaunch(fbn_ci_ctx *c, int k, const int32_t *items, int64_t n, int d, 
 bool CiAllPairsEligible(const fbn_ci_ctx *c, const CiBatchStats &st) {
     return st.maxdim <= 4 && !getenv("FBN_CI_NO_BITS") && (c->N >= 4096 || getenv("FBN_CI_FORCE_BITS"));
 }
-int CiBatchLaunchAllPairs(fbn_ci_ctx *c, double alpha, const CiBatchStats *pre, int64_t t0, int64_t n) {
+int CiBatchLaunchAllPairs(fbn_ci_ctx *c, double alpha, const CiBatchStats *pre, int64_t t0, int64_t n,
+                          bool copy_flags) {
     CiSlot &S = c->slot[0];
     S.n = n;
     S.want_df = false;
@@ -2232,8 +2247,82 @@ int CiBatchLaunchAllPairs(fbn_ci_ctx *c, double alpha, const CiBatchStats *pre, 
     rc = CiLaunchDevice(c, nullptr, n, 0, alpha, false, nullptr, c->stream, 0, nullptr, nullptr, nullptr, pre, true,
                         t0);
     if (rc) return rc;
-    FBN_HIP(hipMemcpyAsync(S.h_res, S.indep.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    if (copy_flags) FBN_HIP(hipMemcpyAsync(S.h_res, S.indep.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
     FBN_HIP(hipEventRecord(S.done, c->stream));
+    return FBN_OK;
+}
+
+bool CiPairsReady(const fbn_ci_ctx *c) { return c->pair_mode == 2 && c->pairs_recorded; }
+
+bool CiL0L1DeviceEligible(const fbn_ci_ctx *c, int group_size) {
+    if (group_size != 1 || !c->bits_ready || getenv("FBN_PC_HOST_L1") || getenv("FBN_PC_HOST_L0L1")) return false;
+    for (int v = 0; v < c->nvars; ++v)
+        if (c->dims[v] > 4) return false;
+    return c->nvars >= 2;
+}
+
+int CiL0L1Device(fbn_ci_ctx *c, int64_t P, int *E, int64_t *cands, PCResultHost &res) {
+    const int n = c->nvars;
+    if (P != (int64_t)n * (n - 1) / 2 || P > INT32_MAX / 2) return SetError(FBN_ERR_ARG, "level 0 -> 1 on the device: one complete-graph batch");
+    FBN_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    CiSlot &S = c->slot[0];
+    int rc;
+    if ((rc = c->kcnt.ensure((size_t)n * 8)) || (rc = c->kscal.ensure(16)) || (rc = c->l1adjoff.ensure((size_t)(n + 1) * 4)) ||
+        (rc = c->l1adj.ensure((size_t)std::max<int64_t>(2 * P, 1) * 4)) || (rc = c->l1pairs.ensure((size_t)std::max<int64_t>(P, 1) * 8)) ||
+        (rc = c->kupoff.ensure((size_t)n * 4)))
+        return rc;
+    if (!c->h_kept) {
+        hipError_t e = hipHostMalloc((void **)&c->h_kept, 16, hipHostMallocDefault);
+        if (e != hipSuccess) return SetError(FBN_ERR_NOMEM, "hipHostMalloc: %s", hipGetErrorString(e));
+    }
+    if (!c->side) {
+        FBN_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+        FBN_HIP(hipEventCreateWithFlags(&c->side_ev, hipEventDisableTiming));
+        FBN_HIP(hipEventCreateWithFlags(&c->main_ev, hipEventDisableTiming));
+    }
+    // the decision flags to the host on the side stream, behind the level-0 kernels
+    FBN_HIP(hipStreamWaitEvent(c->side, S.done, 0));
+    FBN_HIP(hipMemcpyAsync(S.h_res, S.indep.p, (size_t)P, hipMemcpyDeviceToHost, c->side));
+    int32_t *cnt = c->kcnt.as<int32_t>();
+    hipError_t e = fbn_ci_kept_csr(S.indep.as<uint8_t>(), n, cnt, cnt + n, c->l1adjoff.as<int32_t>(), c->kupoff.as<int32_t>(),
+                                   c->l1adj.as<int32_t>(), c->l1pairs.as<int32_t>(), c->kscal.as<long long>(), s);
+    if (e != hipSuccess) return SetError(FBN_ERR_HIP, "kept-pair CSR: %s", hipGetErrorString(e));
+    long long *hk = reinterpret_cast<long long *>(c->h_kept);
+    FBN_HIP(hipMemcpyAsync(hk, c->kscal.p, 16, hipMemcpyDeviceToHost, s));
+    FBN_HIP(hipEventRecord(c->main_ev, s));
+    FBN_HIP(EventWaitSpin(c->main_ev));
+    *E = (int)hk[0];
+    *cands = hk[1];
+    // the edge list to the host on the side stream (the CSR kernels are done: main_ev)
+    if ((rc = PinnedEnsure(c->h_pairs, c->h_pairs_bytes, (size_t)std::max(*E, 1) * 8))) return rc;
+    FBN_HIP(hipStreamWaitEvent(c->side, c->main_ev, 0));
+    if (*E) FBN_HIP(hipMemcpyAsync(c->h_pairs, c->l1pairs.p, (size_t)*E * 8, hipMemcpyDeviceToHost, c->side));
+    FBN_HIP(hipEventRecord(c->side_ev, c->side));
+    // the level-0 batch in the run's accounting (as CiBatchWait)
+    float ms = 0.f;
+    if (c->timing) FBN_HIP(hipEventElapsedTime(&ms, S.ev0, S.ev1));
+    res.kernel_s += ms * 1e-3;
+    res.device_bytes += S.last_bytes;
+    S.n = 0;
+    return FBN_OK;
+}
+
+int CiL0L1Host(fbn_ci_ctx *c, int64_t P, int E, std::vector<char> &removed, std::vector<std::pair<int, int>> &edges,
+               std::vector<std::vector<int>> &adj) {
+    FBN_HIP(EventWaitSpin(c->side_ev));
+    removed.resize((size_t)P);
+    memcpy(removed.data(), c->slot[0].h_res, (size_t)P);
+    static_assert(sizeof(std::pair<int, int>) == 8, "pair layout");
+    edges.resize((size_t)E);
+    if (E) memcpy(edges.data(), c->h_pairs, (size_t)E * 8);
+    const int n = c->nvars;
+    {
+        std::vector<int> deg(n, 0);
+        for (auto &e : edges) ++deg[e.first], ++deg[e.second];
+        for (int v = 0; v < n; ++v) adj[v].reserve(deg[v]);
+    }
+    for (auto &e : edges) adj[e.first].push_back(e.second), adj[e.second].push_back(e.first);
     return FBN_OK;
 }
 int CiPairTablesCopy(fbn_ci_ctx *c, int64_t p0, int64_t np, void *buf, bool buf_on_device, bool to_ctx) {
@@ -2291,12 +2380,11 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
     // a level the host driver takes in one round (full speculation, ALARM-size) stays there: one
     // launch instead of a round's seven
     if (cands <= EnvOr0("FBN_PC_FULLSPEC", 16384)) return FBN_OK;
-    out.removed.assign(E, 0);
-    out.d = 1;
-    out.sep.assign(E, -1);
-    out.counted = out.launched = 0;
-    *done = true;
-    if (E == 0) return FBN_OK;
+    if (E == 0) {
+        out.removed.clear(), out.sep.clear(), out.d = 1, out.counted = out.launched = 0;
+        *done = true;
+        return FBN_OK;
+    }
     static const bool ptiming = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic
     auto tq0 = std::chrono::steady_clock::now();
     FBN_HIP(hipSetDevice(c->device));
@@ -2310,9 +2398,36 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
         adjf.insert(adjf.end(), adj[u].begin(), adj[u].end());
     }
     adj_off[nv] = (int32_t)adjf.size();
-    const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(cands, EnvOr0("FBN_PC_L1CAP", 1 << 19)));
     if ((rc = c->l1pairs.ensure((size_t)E * 8)) || (rc = c->l1adj.ensure(std::max<size_t>(adjf.size(), 1) * 4)) ||
-        (rc = c->l1adjoff.ensure((size_t)(nv + 1) * 4)) || (rc = c->l1ed.ensure((size_t)E * fbn_ci_l1_edge_bytes())) ||
+        (rc = c->l1adjoff.ensure((size_t)(nv + 1) * 4)))
+        return rc;
+    static_assert(sizeof(std::pair<int, int>) == 8, "pair layout");
+    FBN_HIP(hipMemcpyAsync(c->l1pairs.p, edges.data() + e_begin, (size_t)E * 8, hipMemcpyHostToDevice, s));
+    if (!adjf.empty()) FBN_HIP(hipMemcpyAsync(c->l1adj.p, adjf.data(), adjf.size() * 4, hipMemcpyHostToDevice, s));
+    FBN_HIP(hipMemcpyAsync(c->l1adjoff.p, adj_off.data(), (size_t)(nv + 1) * 4, hipMemcpyHostToDevice, s));
+    if (ptiming)
+        fprintf(stderr, "  level 1 device setup (host): %.3f ms\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
+    *done = true;
+    return CiLevel1Run(c, alpha, E, cands, out, res, nullptr);
+}
+
+// The level-1 rounds over the edge list / adjacency already in c->l1pairs / l1adj / l1adjoff (E
+// edges, `cands` candidate sets in all); host_work (optional) runs once, after the first round is
+// enqueued, while the device works.
+int CiLevel1Run(fbn_ci_ctx *c, double alpha, int E, int64_t cands, LevelOut &out, PCResultHost &res,
+                const std::function<int()> &host_work) {
+    const int nv = c->nvars;
+    out.removed.assign(E, 0);
+    out.d = 1;
+    out.sep.assign(E, -1);
+    out.counted = out.launched = 0;
+    FBN_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    int rc;
+    (void)nv;
+    const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(cands, EnvOr0("FBN_PC_L1CAP", 1 << 19)));
+    if ((rc = c->l1ed.ensure((size_t)E * fbn_ci_l1_edge_bytes())) ||
         (rc = c->l1pos.ensure((size_t)E * 4)) || (rc = c->l1st.ensure((size_t)E)) ||
         (rc = c->l1sep.ensure((size_t)E * 4)) || (rc = c->l1cnt.ensure((size_t)E * 8)) ||
         (rc = c->l1len.ensure((size_t)E * 4)) || (rc = c->l1off.ensure((size_t)E * 4)) ||
@@ -2329,17 +2444,9 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
     const double *band = nullptr;
     int nband = 0;
     if ((rc = CiBand(c, alpha, s, &band, &nband))) return rc;
-    static_assert(sizeof(std::pair<int, int>) == 8, "pair layout");
-    FBN_HIP(hipMemcpyAsync(c->l1pairs.p, edges.data() + e_begin, (size_t)E * 8, hipMemcpyHostToDevice, s));
-    if (!adjf.empty()) FBN_HIP(hipMemcpyAsync(c->l1adj.p, adjf.data(), adjf.size() * 4, hipMemcpyHostToDevice, s));
-    FBN_HIP(hipMemcpyAsync(c->l1adjoff.p, adj_off.data(), (size_t)(nv + 1) * 4, hipMemcpyHostToDevice, s));
     // scalars (total, launched, rows read, scan flag, tickets) and the tile scan's status words (epoch 0)
     FBN_HIP(hipMemsetAsync(c->l1scal.p, 0, 48, s));
     FBN_HIP(hipMemsetAsync(c->l1sstat.p, 0, (size_t)((E + 255) / 256) * 8, s));
-
-    if (ptiming)
-        fprintf(stderr, "  level 1 device setup (host): %.3f ms\n",
-                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count());
     CiSlot &S = c->slot[0];
     if (c->timing) FBN_HIP(hipEventRecord(S.ev0, s));
     long long *scal = c->l1scal.as<long long>();  // total, launched, rows read, scan flag, tickets
@@ -2372,6 +2479,8 @@ int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<in
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci level-1 round: %s", hipGetErrorString(e));
         FBN_HIP(hipMemcpyAsync(c->h_open + (r & 1), open_r, 4, hipMemcpyDeviceToHost, s));
         FBN_HIP(hipEventRecord(c->l1ev[r & 1], s));
+        if (r == 0 && host_work)  // (while the first round runs)
+            if ((rc = host_work())) return rc;
         if (r >= 1) {  // round r - 1's open count, while round r runs
             FBN_HIP(EventWaitSpin(c->l1ev[(r - 1) & 1]));
             if (c->h_open[(r - 1) & 1] == 0) break;  // round r found nothing to do

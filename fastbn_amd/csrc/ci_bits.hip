@@ -1339,6 +1339,99 @@ extern "C" hipError_t fbn_ci_bits_pairs_tiled(const uint32_t *bits, const int32_
 
 extern "C" size_t fbn_ci_l1_edge_bytes(void) { return sizeof(L1Edge); }
 
+// ---- level 0 -> level 1 without the host: the pairs level 0 kept (decision flag 0 over the
+// implicit complete graph, pair (i < j) at i*n - i(i+1)/2 + j-i-1) become the level-1 edge list
+// (lexicographic, as the host's vec_edges) and the CSR adjacency (each list ascending: the lower
+// neighbours, then the upper ones -- the order the host builds from the edge list).  One wave per
+// variable, 64 flags per step with a ballot.
+__device__ __forceinline__ long long kept_pidx(int i, int j, int n) {
+    return (long long)i * n - (long long)i * (i + 1) / 2 + (j - i - 1);
+}
+__global__ __launch_bounds__(256) void ci_kept_count(const uint8_t *__restrict__ indep, int n, int32_t *__restrict__ low,
+                                                     int32_t *__restrict__ up) {
+    const int lane = threadIdx.x & 63, v = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (v >= n) return;  // (whole wave)
+    int lo = 0, hi = 0;
+    for (int u0 = 0; u0 < v; u0 += 64) {
+        const int u = u0 + lane;
+        lo += __popcll(__ballot(u < v && indep[kept_pidx(u, v, n)] == 0));
+    }
+    for (int w0 = v + 1; w0 < n; w0 += 64) {
+        const int w = w0 + lane;
+        hi += __popcll(__ballot(w < n && indep[kept_pidx(v, w, n)] == 0));
+    }
+    if (lane == 0) low[v] = lo, up[v] = hi;
+}
+// one workgroup: off = exclusive scan of the degrees (off[n] = 2E), upoff = exclusive scan of the
+// upper counts; scal[0] = E, scal[1] = the level's candidate sets sum_e (deg x + deg y - 2) =
+// sum_v deg(v)^2 - 2E
+__global__ __launch_bounds__(1024) void ci_kept_scan(const int32_t *__restrict__ low, const int32_t *__restrict__ up,
+                                                     int n, int32_t *__restrict__ off, int32_t *__restrict__ upoff,
+                                                     long long *__restrict__ scal) {
+    __shared__ long long sd[1024], su[1024];
+    __shared__ long long carry_d, carry_u, sq;
+    const int t = threadIdx.x;
+    if (t == 0) carry_d = carry_u = sq = 0;
+    __syncthreads();
+    for (int b = 0; b < n; b += 1024) {
+        const int v = b + t;
+        const long long d = v < n ? (long long)low[v] + up[v] : 0, u = v < n ? up[v] : 0;
+        sd[t] = d, su[t] = u;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
+            const long long xd = t >= o ? sd[t - o] : 0, xu = t >= o ? su[t - o] : 0;
+            __syncthreads();
+            sd[t] += xd, su[t] += xu;
+            __syncthreads();
+        }
+        if (v < n) off[v] = (int32_t)(carry_d + sd[t] - d), upoff[v] = (int32_t)(carry_u + su[t] - u);
+        if (d) atomicAdd((unsigned long long *)&sq, (unsigned long long)(d * d));
+        __syncthreads();
+        if (t == 1023) carry_d += sd[1023], carry_u += su[1023];
+        __syncthreads();
+    }
+    if (t == 0) {
+        off[n] = (int32_t)carry_d;
+        scal[0] = carry_u;
+        scal[1] = sq - 2 * carry_u;
+    }
+}
+__global__ __launch_bounds__(256) void ci_kept_fill(const uint8_t *__restrict__ indep, int n,
+                                                    const int32_t *__restrict__ off, const int32_t *__restrict__ upoff,
+                                                    int32_t *__restrict__ adj, int32_t *__restrict__ pairs) {
+    const int lane = threadIdx.x & 63, v = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (v >= n) return;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    int r = off[v], q = upoff[v];
+    for (int u0 = 0; u0 < v; u0 += 64) {
+        const int u = u0 + lane;
+        const bool k = u < v && indep[kept_pidx(u, v, n)] == 0;
+        const unsigned long long m = __ballot(k);
+        if (k) adj[r + __popcll(m & below)] = u;
+        r += __popcll(m);
+    }
+    for (int w0 = v + 1; w0 < n; w0 += 64) {
+        const int w = w0 + lane;
+        const bool k = w < n && indep[kept_pidx(v, w, n)] == 0;
+        const unsigned long long m = __ballot(k);
+        if (k) {
+            const int i = __popcll(m & below);
+            adj[r + i] = w;
+            pairs[2 * (q + i)] = v, pairs[2 * (q + i) + 1] = w;
+        }
+        r += __popcll(m), q += __popcll(m);
+    }
+}
+// low / up: n ints of scratch each; scal: 2 long longs (E, candidate sets)
+extern "C" hipError_t fbn_ci_kept_csr(const uint8_t *indep, int n, int32_t *low, int32_t *up, int32_t *off,
+                                      int32_t *upoff, int32_t *adj, int32_t *pairs, long long *scal, hipStream_t s) {
+    const dim3 g((unsigned)((n + 3) / 4));
+    hipLaunchKernelGGL(ci_kept_count, g, dim3(256), 0, s, indep, n, low, up);
+    hipLaunchKernelGGL(ci_kept_scan, dim3(1), dim3(1024), 0, s, low, up, n, off, upoff, scal);
+    hipLaunchKernelGGL(ci_kept_fill, g, dim3(256), 0, s, indep, n, off, upoff, adj, pairs);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t fbn_ci_l1_setup(const int32_t *pairs, int E, const int32_t *adj, const int32_t *adj_off,
                                       void *ed, int32_t *pos, uint8_t *st, int32_t *sep, long long *counted,
                                       int chunk0, int32_t *len, int32_t *off, unsigned *ring,

@@ -472,14 +472,58 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
     } else if (n >= 2 && CiAllPairsEligible(ctx, st_all) && !getenv("FBN_CI_NO_IMPLICIT")) {
         auto ta = std::chrono::steady_clock::now();
         const double k0 = res.kernel_s;
-        std::vector<char> removed((size_t)P);
+        std::vector<char> removed;  // (sized below on the host path only)
         static_assert(sizeof(char) == sizeof(uint8_t), "flag layout");
         // batches of at most FBN_PC_L0CHUNK pairs (per-test count records: 256 B each; a
         // 10k-variable graph has 5e7 pairs), kept pairs compacted per batch
         const int64_t chunk = std::max<int64_t>(1, EnvOr("FBN_PC_L0CHUNK", (int64_t)1 << 22));
         int rc = FBN_OK;
         double t_wait = 0, t_kept = 0;
-        for (int64_t t0 = 0; t0 < P && !rc; t0 += chunk) {
+        bool P_done = false;
+        // level 0 -> level 1 without a host round trip: one complete-graph batch, whose kept pairs
+        // become the level-1 edge list / adjacency on the device; the host reads back only (E, the
+        // level's candidate sets) and builds its own copies (flags, edges, adjacency) while the first
+        // level-1 round runs (FBN_PC_HOST_L0L1: the host path)
+        if (pairs && P <= chunk && depth > 1 && CiL0L1DeviceEligible(ctx, group_size)) {
+            if ((rc = CiBatchLaunchAllPairs(ctx, alpha, &st_all, 0, P, false))) return rc;
+            int E = 0;
+            int64_t cands = 0;
+            if ((rc = CiL0L1Device(ctx, P, &E, &cands, res))) return rc;
+            res.tests_per_level.push_back(P);
+            res.launched_per_level.push_back(P);
+            CiSetPairMode(ctx, 2);
+            bool host_done = false;
+            auto host_side = [&]() -> int {
+                std::vector<char> removed;
+                if (int r = CiL0L1Host(ctx, P, E, removed, edges, adj)) return r;
+                res.sepset.set_level0(n, std::move(removed));
+                host_done = true;
+                return FBN_OK;
+            };
+            auto tb = std::chrono::steady_clock::now();
+            if (E > 0 && CiPairsReady(ctx) && cands > EnvOr("FBN_PC_FULLSPEC", 16384)) {
+                LevelOut out;
+                const double k1 = res.kernel_s;
+                if ((rc = CiLevel1Run(ctx, alpha, E, cands, out, res, host_side))) return rc;
+                if (!host_done && (rc = host_side())) return rc;
+                res.sepset.append_level(edges.data(), out.removed.data(), out.sep.data(), edges.size(), 1);
+                res.tests_per_level.push_back(out.counted);
+                res.launched_per_level.push_back(out.launched);
+                ApplyRemovals(out.removed, edges, adj);
+                if (timing)
+                    fprintf(stderr, "pc levels 0-1 on the device: level 0 %.2f ms, level 1 %.2f ms (kernels %.2f)\n",
+                            std::chrono::duration<double, std::milli>(tb - ta).count(),
+                            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb).count(),
+                            (res.kernel_s - k1) * 1e3);
+                d0 = ContinueAfter(adj, 1) ? 2 : std::max(depth, 1);
+            } else {  // level 1 (if any) on the host path
+                if ((rc = host_side())) return rc;
+                d0 = 1;
+            }
+            P_done = true;
+        }
+        if (!P_done) removed.resize((size_t)P);
+        for (int64_t t0 = 0; t0 < P && !rc && !P_done; t0 += chunk) {
             const int64_t m = std::min(chunk, P - t0);
             auto q0 = std::chrono::steady_clock::now();
             rc = CiBatchLaunchAllPairs(ctx, alpha, &st_all, t0, m);
@@ -491,6 +535,7 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
             t_kept += std::chrono::duration<double, std::milli>(q2 - q1).count();
         }
         if (rc) return rc;
+        if (!P_done) {
         auto tb = std::chrono::steady_clock::now();
         if (timing) fprintf(stderr, "pc level 0: launch + wait %.3f ms, kept pairs %.3f ms\n", t_wait, t_kept);
         res.tests_per_level.push_back(P);
@@ -514,6 +559,7 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
                     std::chrono::duration<double, std::milli>(tb - ta).count(), (res.kernel_s - k0) * 1e3,
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb).count());
         d0 = 1;
+        }
     } else {
         edges.reserve((size_t)P);
         for (int i = 0; i < n; ++i)

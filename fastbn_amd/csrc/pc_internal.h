@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <array>
 #include <cstdint>
+#include <functional>
 #include <map>
 #include <string>
 #include <utility>
@@ -212,7 +213,8 @@ const int32_t *CiCtxDims(const fbn_ci_ctx *c);  // state count per variable
 // path (st = the batch's statistics)
 bool CiAllPairsEligible(const fbn_ci_ctx *c, const CiBatchStats &st);
 // pairs [t0, t0 + n) of that order (one rank's range of a distributed level 0)
-int CiBatchLaunchAllPairs(fbn_ci_ctx *c, double alpha, const CiBatchStats *pre, int64_t t0, int64_t n);
+int CiBatchLaunchAllPairs(fbn_ci_ctx *c, double alpha, const CiBatchStats *pre, int64_t t0, int64_t n,
+                          bool copy_flags = true);
 // copy the pair tables of pairs [p0, p0 + np) (16 int32 each) out of the ctx (to_ctx = false; they
 // must have been recorded) or into it (to_ctx = true); buf in device or host memory
 int CiPairTablesCopy(fbn_ci_ctx *c, int64_t p0, int64_t np, void *buf, bool buf_on_device, bool to_ctx);
@@ -255,6 +257,23 @@ int CiAllPairsKept(fbn_ci_ctx *c, int64_t t0, int64_t P, std::vector<std::pair<i
 int CiLevel1Device(fbn_ci_ctx *c, double alpha, const std::vector<std::vector<int>> &adj,
                    const std::vector<std::pair<int, int>> &edges, size_t e_begin, size_t e_end, LevelOut &out,
                    PCResultHost &res, bool *done);
+// the level-1 rounds over an edge list / adjacency already on the device (capi.hip); host_work runs
+// once while the first round is on the device
+int CiLevel1Run(fbn_ci_ctx *c, double alpha, int E, int64_t cands, LevelOut &out, PCResultHost &res,
+                const std::function<int()> &host_work);
+// Level 0 -> level 1 without a host round trip (capi.hip): whether the ctx qualifies (level 1 would
+// run on the device: pair tables recorded, bit-sliced store, every variable <= 4 states, group 1)
+bool CiL0L1DeviceEligible(const fbn_ci_ctx *c, int group_size);
+// level 0 recorded its pair tables and the ctx uses them (pair mode 2): level 1 can run on the device
+bool CiPairsReady(const fbn_ci_ctx *c);
+// after CiBatchLaunchAllPairs(copy_flags = false) of the whole complete graph (P pairs): the kept
+// pairs become the level-1 edge list and CSR adjacency on the device; one small read-back gives
+// *E and *cands (the level's candidate sets); the decision flags and the edge list are copied to
+// pinned host memory on a side stream (CiL0L1Host waits for them); accounts the level-0 batch in res
+int CiL0L1Device(fbn_ci_ctx *c, int64_t P, int *E, int64_t *cands, PCResultHost &res);
+// the host's copies: removed[P] (level-0 decisions), edges (lexicographic) and adj
+int CiL0L1Host(fbn_ci_ctx *c, int64_t P, int E, std::vector<char> &removed, std::vector<std::pair<int, int>> &edges,
+               std::vector<std::vector<int>> &adj);
 int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::vector<std::vector<int>> &adj,
              const std::vector<std::pair<int, int>> &edges, size_t e_begin, size_t e_end, LevelOut &out,
              PCResultHost &res);
