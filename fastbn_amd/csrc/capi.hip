@@ -60,6 +60,9 @@ extern "C" hipError_t fbn_ci_sum_planes(const int32_t *planes, int np, long long
 extern "C" hipError_t fbn_ci_onehot_build(const uint8_t *cols, const int32_t *dims, const int32_t *lead0, long long N,
                                           long long Npad, int nvars, int8_t *out, hipStream_t s);
 extern "C" size_t fbn_ci_l1_edge_bytes(void);
+extern "C" hipError_t fbn_ci_l1_results(const uint8_t *st, const int32_t *sep, const long long *cnt, int E,
+                                        const long long *scal, char *h_rm, int32_t *h_sep, long long *h_sc,
+                                        long long *part, hipStream_t s);
 extern "C" hipError_t fbn_ci_kept_csr(const uint8_t *indep, int n, int32_t *low, int32_t *up, int32_t *off,
                                       int32_t *upoff, int32_t *adj, int32_t *pairs, long long *scal, hipStream_t s);
 extern "C" hipError_t fbn_ci_l1_setup(const int32_t *pairs, int E, const int32_t *adj, const int32_t *adj_off,
@@ -269,7 +272,7 @@ struct fbn_ci_ctx {
     DevBuf keptidx, kepttmp;  // level-0 kept pair indices (CiAllPairsKept)
     // level 0 -> level 1 on the device (CiL0L1Device): per-variable kept counts, upper-part offsets,
     // (E, candidate sets); the side stream copies the flags / edge list to the host meanwhile
-    DevBuf kcnt, kupoff, kscal;
+    DevBuf kcnt, kupoff, kscal, l1part;
     hipStream_t side = nullptr;
     hipEvent_t side_ev = nullptr, main_ev = nullptr;
     void *h_pairs = nullptr;
@@ -2315,7 +2318,7 @@ int CiL0L1Host(fbn_ci_ctx *c, int64_t P, int E, std::vector<char> &removed, std:
     memcpy(removed.data(), c->slot[0].h_res, (size_t)P);
     static_assert(sizeof(std::pair<int, int>) == 8, "pair layout");
     edges.resize((size_t)E);
-    if (E) memcpy(edges.data(), c->h_pairs, (size_t)E * 8);
+    if (E) memcpy(static_cast<void *>(edges.data()), c->h_pairs, (size_t)E * 8);
     const int n = c->nvars;
     {
         std::vector<int> deg(n, 0);
@@ -2466,7 +2469,11 @@ int CiLevel1Run(fbn_ci_ctx *c, double alpha, int E, int64_t cands, LevelOut &out
                                    c->l1cnt.as<long long>(), (int)chunk, c->l1len.as<int32_t>(),
                                    c->l1off.as<int32_t>(), c->l1open.as<unsigned>(), sstat, cap, scal, c->num_cu, s);
     if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci level-1 setup: %s", hipGetErrorString(e));
+    static const bool l1timing = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic
+    const auto tl0 = std::chrono::steady_clock::now();
+    int rounds = 0;
     for (int r = 0;; ++r) {
+        rounds = r + 1;
         unsigned *open_r = c->l1open.as<unsigned>() + (r & 1);
         const int64_t next_chunk = std::min<int64_t>(chunk * growth, max_chunk);
         e = fbn_ci_l1_round(c->bits.as<uint32_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(), c->bits_W,
@@ -2488,27 +2495,28 @@ int CiLevel1Run(fbn_ci_ctx *c, double alpha, int E, int64_t cands, LevelOut &out
         chunk = next_chunk;
     }
     if (c->timing) FBN_HIP(hipEventRecord(S.ev1, s));
-    // read-back through one pinned staging buffer (DMA, no pageable staging copies):
-    // [counters 8E | scalars 24 | sepsets 4E | status E] (each part aligned to its type)
-    if ((rc = PinnedEnsure(c->h_xfer, c->h_xfer_bytes, (size_t)E * 13 + 40))) return rc;
+    const auto tl1 = std::chrono::steady_clock::now();
+    // results straight into one pinned buffer by a kernel (zero-copy writes; no DMA copies):
+    // [scalars 32 | sepsets 4E | removal flags E]
+    if ((rc = PinnedEnsure(c->h_xfer, c->h_xfer_bytes, (size_t)E * 5 + 40))) return rc;
+    if ((rc = c->l1part.ensure(256 * 8))) return rc;
     char *hx = static_cast<char *>(c->h_xfer);
-    const long long *cnt = reinterpret_cast<const long long *>(hx);
-    const long long *sc = reinterpret_cast<const long long *>(hx + (size_t)E * 8);
-    const int32_t *hsep = reinterpret_cast<const int32_t *>(hx + (size_t)E * 8 + 32);
-    const uint8_t *st = reinterpret_cast<const uint8_t *>(hx + (size_t)E * 12 + 32);
-    FBN_HIP(hipMemcpyAsync(hx, c->l1cnt.p, (size_t)E * 8, hipMemcpyDeviceToHost, s));
-    FBN_HIP(hipMemcpyAsync(hx + (size_t)E * 8, scal, 32, hipMemcpyDeviceToHost, s));
-    FBN_HIP(hipMemcpyAsync(hx + (size_t)E * 8 + 32, c->l1sep.p, (size_t)E * 4, hipMemcpyDeviceToHost, s));
-    FBN_HIP(hipMemcpyAsync(hx + (size_t)E * 12 + 32, c->l1st.p, (size_t)E, hipMemcpyDeviceToHost, s));
+    long long *sc = reinterpret_cast<long long *>(hx);
+    int32_t *hsep = reinterpret_cast<int32_t *>(hx + 32);
+    char *hrm = hx + 32 + (size_t)E * 4;
+    e = fbn_ci_l1_results(c->l1st.as<uint8_t>(), c->l1sep.as<int32_t>(), c->l1cnt.as<long long>(), E, scal, hrm, hsep, sc,
+                          c->l1part.as<long long>(), s);
+    if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci level-1 results: %s", hipGetErrorString(e));
     FBN_HIP(hipStreamSynchronize(s));
     if (sc[3]) return SetError(FBN_ERR_HIP, "level-1 offset scan: look-back timed out");
     std::memcpy(out.sep.data(), hsep, (size_t)E * 4);
-    for (int i = 0; i < E; ++i) {
-        out.removed[i] = st[i] == 1;
-        if (st[i] != 1) out.sep[i] = -1;
-        out.counted += cnt[i];
-    }
+    std::memcpy(out.removed.data(), hrm, (size_t)E);
+    out.counted = sc[0];
     out.launched = sc[1];
+    if (l1timing)
+        fprintf(stderr, "  level 1 device rounds: %d, loop %.3f ms, read-back + results %.3f ms\n", rounds,
+                std::chrono::duration<double, std::milli>(tl1 - tl0).count(),
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tl1).count());
     if (c->timing) {
         float ms = 0.f;
         FBN_HIP(hipEventElapsedTime(&ms, S.ev0, S.ev1));

@@ -1422,6 +1422,42 @@ __global__ __launch_bounds__(256) void ci_kept_fill(const uint8_t *__restrict__ 
         r += __popcll(m), q += __popcll(m);
     }
 }
+// level-1 results straight into pinned host memory (one kernel instead of four DMA copies): the
+// removal flag (status 1) and the sepset (or -1) of every edge, per-workgroup sums of the counted
+// tests in `part`; ci_l1_results_tail adds them up and copies the launched count and the scan flag
+__global__ __launch_bounds__(256) void ci_l1_results(const uint8_t *__restrict__ st, const int32_t *__restrict__ sep,
+                                                     const long long *__restrict__ cnt, int E, char *__restrict__ h_rm,
+                                                     int32_t *__restrict__ h_sep, long long *__restrict__ part) {
+    __shared__ long long ws[4];
+    long long acc = 0;
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < E; e += gridDim.x * 256) {
+        const bool rm = st[e] == 1;
+        h_rm[e] = rm ? 1 : 0;
+        h_sep[e] = rm ? sep[e] : -1;
+        acc += cnt[e];
+    }
+    for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+__global__ __launch_bounds__(64) void ci_l1_results_tail(const long long *__restrict__ part, int nparts,
+                                                         const long long *__restrict__ scal, long long *__restrict__ h_sc) {
+    long long acc = 0;
+    for (int i = threadIdx.x; i < nparts; i += 64) acc += part[i];
+    for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+    if (threadIdx.x == 0) h_sc[0] = acc, h_sc[1] = scal[1], h_sc[2] = scal[2], h_sc[3] = scal[3];
+}
+// h_sc: 4 long longs (counted, launched, rows read, scan flag); part: >= 256 long longs of scratch
+extern "C" hipError_t fbn_ci_l1_results(const uint8_t *st, const int32_t *sep, const long long *cnt, int E,
+                                        const long long *scal, char *h_rm, int32_t *h_sep, long long *h_sc,
+                                        long long *part, hipStream_t s) {
+    const int g = std::max(1, std::min(256, (E + 255) / 256));
+    hipLaunchKernelGGL(ci_l1_results, dim3(g), dim3(256), 0, s, st, sep, cnt, E, h_rm, h_sep, part);
+    hipLaunchKernelGGL(ci_l1_results_tail, dim3(1), dim3(64), 0, s, part, g, scal, h_sc);
+    return hipGetLastError();
+}
+
 // low / up: n ints of scratch each; scal: 2 long longs (E, candidate sets)
 extern "C" hipError_t fbn_ci_kept_csr(const uint8_t *indep, int n, int32_t *low, int32_t *up, int32_t *off,
                                       int32_t *upoff, int32_t *adj, int32_t *pairs, long long *scal, hipStream_t s) {

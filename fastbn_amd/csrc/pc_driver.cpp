@@ -506,10 +506,14 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
                 const double k1 = res.kernel_s;
                 if ((rc = CiLevel1Run(ctx, alpha, E, cands, out, res, host_side))) return rc;
                 if (!host_done && (rc = host_side())) return rc;
+                auto tr = std::chrono::steady_clock::now();
                 res.sepset.append_level(edges.data(), out.removed.data(), out.sep.data(), edges.size(), 1);
                 res.tests_per_level.push_back(out.counted);
                 res.launched_per_level.push_back(out.launched);
                 ApplyRemovals(out.removed, edges, adj);
+                if (timing)
+                    fprintf(stderr, "  level 1 sepsets + removals %.3f ms\n",
+                            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr).count());
                 if (timing)
                     fprintf(stderr, "pc levels 0-1 on the device: level 0 %.2f ms, level 1 %.2f ms (kernels %.2f)\n",
                             std::chrono::duration<double, std::milli>(tb - ta).count(),
