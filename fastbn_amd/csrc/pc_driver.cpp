@@ -113,7 +113,7 @@ struct Pending {  // one generated test
 // Outputs per edge of the range: removed flag and, if removed, its sepset (sorted).
 int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::vector<std::vector<int>> &adj,
              const std::vector<std::pair<int, int>> &edges, size_t e_begin, size_t e_end, LevelOut &out,
-             PCResultHost &res) {
+             PCResultHost &res, std::function<void()> *deferred) {
     const size_t E = e_end - e_begin;
     out.removed.assign(E, 0);
     out.d = d;
@@ -375,6 +375,10 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
     };
     for (int h = 0; h < nh; ++h)
         if (int rc = launch(h)) return rc;
+    if (deferred && *deferred) {  // (while the first batches run)
+        (*deferred)();
+        *deferred = nullptr;
+    }
     while (true) {
         bool any = false;
         for (int h = 0; h < nh; ++h) {
@@ -429,6 +433,7 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
     if ((int)adj.size() > n) adj.resize(n);
     for (auto &a : adj) a.clear();
     adj.resize(n);
+    std::function<void()> deferred;  // host work that waits for the next level's first batches
     const bool timing = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic: host phase times per level
     // level 0 tests every pair: its tables are recorded for the level-1 kernel (derived counting)
     // and dropped when this run ends, however it ends
@@ -507,12 +512,24 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
                 if ((rc = CiLevel1Run(ctx, alpha, E, cands, out, res, host_side))) return rc;
                 if (!host_done && (rc = host_side())) return rc;
                 auto tr = std::chrono::steady_clock::now();
-                res.sepset.append_level(edges.data(), out.removed.data(), out.sep.data(), edges.size(), 1);
                 res.tests_per_level.push_back(out.counted);
                 res.launched_per_level.push_back(out.launched);
-                ApplyRemovals(out.removed, edges, adj);
+                // the level-1 sepsets are recorded while level 2 runs (only the orientation reads
+                // them): the level-1 edge list moves aside, the kept edges (few) become `edges`
+                static thread_local std::vector<std::pair<int, int>> e1_tls;
+                static thread_local LevelOut l1_tls;
+                e1_tls.swap(edges);
+                edges.clear();
+                for (size_t i = 0; i < e1_tls.size(); ++i)
+                    if (!out.removed[i]) edges.push_back(e1_tls[i]);
+                for (auto &a : adj) a.clear();
+                for (auto &e : edges) adj[e.first].push_back(e.second), adj[e.second].push_back(e.first);
+                std::swap(l1_tls, out);
+                deferred = [&res]() {
+                    res.sepset.append_level(e1_tls.data(), l1_tls.removed.data(), l1_tls.sep.data(), e1_tls.size(), 1);
+                };
                 if (timing)
-                    fprintf(stderr, "  level 1 sepsets + removals %.3f ms\n",
+                    fprintf(stderr, "  level 1 removals %.3f ms\n",
                             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr).count());
                 if (timing)
                     fprintf(stderr, "pc levels 0-1 on the device: level 0 %.2f ms, level 1 %.2f ms (kernels %.2f)\n",
@@ -578,8 +595,9 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
         LevelOut out;
         auto ta = std::chrono::steady_clock::now();
         const double k0 = res.kernel_s;
-        int rc = RunLevel(ctx, alpha, d, group_size, adj, edges, 0, edges.size(), out, res);
+        int rc = RunLevel(ctx, alpha, d, group_size, adj, edges, 0, edges.size(), out, res, &deferred);
         if (rc) return rc;
+        if (deferred) deferred(), deferred = nullptr;
         auto tb = std::chrono::steady_clock::now();
         // (recording a level's sepsets on a worker thread while the next level runs measured slower:
         // config 5 4.3 -> 4.5 ms of driver time, the orientation then reads a map built on another core)
@@ -598,6 +616,7 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
                     std::chrono::duration<double, std::milli>(td - tc).count());
         if (d >= 1 && !ContinueAfter(adj, d)) break;
     }
+    if (deferred) deferred(), deferred = nullptr;
     res.edges = edges;
     res.total_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return FBN_OK;

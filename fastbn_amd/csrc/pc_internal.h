@@ -274,9 +274,10 @@ int CiL0L1Device(fbn_ci_ctx *c, int64_t P, int *E, int64_t *cands, PCResultHost 
 // the host's copies: removed[P] (level-0 decisions), edges (lexicographic) and adj
 int CiL0L1Host(fbn_ci_ctx *c, int64_t P, int E, std::vector<char> &removed, std::vector<std::pair<int, int>> &edges,
                std::vector<std::vector<int>> &adj);
+// deferred (optional): host work run once while the level's first batches are on the device
 int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::vector<std::vector<int>> &adj,
              const std::vector<std::pair<int, int>> &edges, size_t e_begin, size_t e_end, LevelOut &out,
-             PCResultHost &res);
+             PCResultHost &res, std::function<void()> *deferred = nullptr);
 // removals after a level in vec_edges order + adjacency rebuild; FreeDegree > d (pc_driver.cpp)
 void ApplyRemovals(const std::vector<char> &rm, std::vector<std::pair<int, int>> &edges,
                    std::vector<std::vector<int>> &adj);
