@@ -215,7 +215,8 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
                         : (open_edges < EnvOr("FBN_PC_PIPELINE_EDGES", kPipelineEdges) ? 1 : 2);
     Half H[2];
     for (int h = 0; h < nh; ++h) H[h].e0 = E * h / nh, H[h].e1 = E * (h + 1) / nh, H[h].chunk = chunk;
-    if (nh == 2) {  // cut where the candidate-set counts of the open edges reach half
+    if (nh == 2) {  // cut where the candidate-set counts of the open edges reach a fraction (the
+                    // first half's generation is on the critical path, the second's is not)
         std::vector<double> cost(E, 0.0);
         double tot = 0.0;
         for (size_t e = 0; e < E; ++e)
@@ -224,7 +225,8 @@ int RunLevel(fbn_ci_ctx *ctx, double alpha, int d, int group_size, const std::ve
                                  (double)binom((int64_t)adj[st[e].y].size() - 1, d);
         double acc = 0.0;
         size_t cut = 0;
-        while (cut < E && acc + cost[cut] <= tot / 2) acc += cost[cut++];
+        static const double first = EnvOr("FBN_PC_SPLIT_PCT", 50) / 100.0;  // (tuning)
+        while (cut < E && acc + cost[cut] <= tot * first) acc += cost[cut++];
         H[0].e1 = H[1].e0 = std::max<size_t>(1, std::min(cut, E - 1));
     }
     const int32_t *dims = CiCtxDims(ctx);

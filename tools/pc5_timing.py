@@ -18,11 +18,17 @@ cols = synth.forward_sample(synth.read_xmlbif(path), 100000, seed=1000)
 dims = (cols.max(axis=1).astype(np.int32) + 1)
 ds = F.Dataset(columns=cols, dims=dims)
 ci = F.IndependenceTest(ds)  # column store resident across runs (as bench.py)
+walls, drivers = [], []
 for r in range(runs):
     pc = F.PCStable(0.05, 6)
     t0 = time.time()
     pc.StructLearnCompData(ci)
     wall = time.time() - t0
-    print(f"run {r}: wall {wall * 1e3:.1f} ms, driver {pc.total_s * 1e3:.1f} ms, kernels {pc.kernel_s * 1e3:.1f} ms, "
+    walls.append(wall)
+    drivers.append(pc.total_s)
+    print(f"run {r}: wall {wall * 1e3:.2f} ms, driver {pc.total_s * 1e3:.2f} ms, kernels {pc.kernel_s * 1e3:.2f} ms, "
           f"tests {pc.tests_per_level.tolist()} launched {pc.launched_per_level.tolist()} edges {len(pc.edges)}",
+          file=sys.stderr, flush=True)
+if runs > 2:
+    print(f"median over runs 2..: wall {np.median(walls[2:]) * 1e3:.3f} ms, driver {np.median(drivers[2:]) * 1e3:.3f} ms",
           file=sys.stderr, flush=True)
