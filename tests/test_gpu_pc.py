@@ -474,3 +474,21 @@ def test_level2_derived_counting_matches_histogram(ns, monkeypatch):
         r = od.ci_test(it[0], it[1], it[2:])
         assert df[k] == r["df"] and ind[k] == r["is_independent"]
         assert abs(g2[k] - r["g2"]) <= G2_TOL * max(1.0, abs(r["g2"]))
+
+
+@pytest.mark.parametrize("nvars,ns", [(333, 20000), (1000, 100000)])
+def test_level0_to_level1_on_device_matches_host_path(nvars, ns, monkeypatch):
+    """Level 0 -> level 1 without the host round trip (the kept pairs become the level-1 edge list
+    and CSR adjacency on the device, ci_kept_* kernels; the host builds its copies while level 1
+    runs) against the host path (FBN_PC_HOST_L0L1=1): the same skeleton, sepsets, counted and
+    launched tests and orientation; 333 variables (ballot tails: not a multiple of 64) and config 5."""
+    from fastbn_amd import synth
+    cols, dims = synth.config5_dataset(nvars, ns)
+    ci = F.IndependenceTest(F.Dataset(columns=cols, dims=dims))
+    a = F.PCStable(0.05, 6).StructLearnCompData(ci)
+    monkeypatch.setenv("FBN_PC_HOST_L0L1", "1")
+    b = F.PCStable(0.05, 6).StructLearnCompData(ci)
+    assert a.edges == b.edges and a.sepset == b.sepset
+    assert a.tests_per_level.tolist() == b.tests_per_level.tolist()
+    assert a.launched_per_level.tolist() == b.launched_per_level.tolist()
+    assert a.oriented == b.oriented
