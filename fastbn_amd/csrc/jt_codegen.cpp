@@ -99,6 +99,13 @@ class JTGen {
     // is smaller than its smallest clique; -1: the clique): the calibrated separator belief is the
     // parent's bin sums of its SepDis, P(separator, evidence) up to a per-case constant
     std::vector<int> msep;
+    // fast order: the clique a variable's marginal is summed in when msep[v] < 0 (default: home[v])
+    std::vector<int> mclq;
+    // FBN_JT_MARG_SRC (tuning): 0 = the smallest holder (default), 1 = the holder whose Distribute
+    // op comes last, 2 = first -- the marginal stores of neighbouring output offsets then land
+    // closer together in time (fewer partial write-backs of the case-major output lines).  ALARM:
+    // 0.128 / 0.155 / 0.144 ms for 0 / 1 / 2 (gpurun_out/r05an): larger holders cost more terms
+    void ChooseMarginalSources(const std::vector<int> &pre);
     // fast order: a marginal (and the label of variable 0) from the terms of each value
     void MargTerms(int v, const std::vector<std::vector<std::string>> &terms);
     int nobs = 0;
@@ -502,7 +509,7 @@ void JTGen::Marg(const std::string &P, int c) {
         const int dim = plan.dom[v];
         const int64_t cum = t.cum[j], bw = dim * cum, nhi = t.size() / bw;
         if (fast) {  // the smallest clique holding the variable (a calibrated tree: any gives the marginal)
-            if (home[v] != c || msep[v] >= 0) continue;
+            if (mclq[v] != c || msep[v] >= 0) continue;
             std::vector<std::vector<std::string>> terms(dim);
             for (int d = 0; d < dim; ++d)
                 for (int64_t hi = 0; hi < nhi; ++hi)
@@ -556,6 +563,30 @@ void JTGen::Marg(const std::string &P, int c) {
         o << "          if (ACT) {";
         for (int d = 0; d < dim; ++d) o << " OUTS(" << out_off[v] + d << ", dv(p" << d << ", tot, yt));";
         o << " }\n        } }\n" << (in_merged ? std::string() : B(8));
+    }
+}
+
+void JTGen::ChooseMarginalSources(const std::vector<int> &pre) {
+    const int mode = getenv("FBN_JT_MARG_SRC") ? atoi(getenv("FBN_JT_MARG_SRC")) : 0;
+    if (mode == 0 || getenv("FBN_JT_NO_SEPMARG")) return;
+    const int nc = (int)plan.cliques.size(), ns = (int)plan.seps.size(), V = (int)plan.dom.size();
+    std::vector<int> pi(nc);
+    for (int k = 0; k < nc; ++k) pi[pre[k]] = k;
+    for (int v = 0; v < V; ++v) {
+        // candidates: every clique holding v (its Marg, at its Distribute) and every separator
+        // holding v (its parent's SepDis); time = the pre-order position of that op
+        int best_t = -1, bc = -1, bs = -1;
+        int64_t best_sz = 0;
+        auto consider = [&](int t, int64_t sz, int c, int sp) {
+            const bool better = best_t < 0 || (mode == 1 ? t > best_t : t < best_t) || (t == best_t && sz < best_sz);
+            if (better) best_t = t, best_sz = sz, bc = c, bs = sp;
+        };
+        for (int c : cand[v]) consider(pi[c], plan.cliques[c].size(), c, -1);
+        for (int sp = 0; sp < ns; ++sp)
+            for (int u : plan.seps[sp].vars)
+                if (u == v) consider(pi[plan.sep_up[sp]], plan.seps[sp].size(), -1, sp);
+        if (bs >= 0) msep[v] = bs;
+        else msep[v] = -1, mclq[v] = bc;
     }
 }
 
@@ -695,7 +726,7 @@ void JTGen::PlaceMessages(const std::vector<int> &post, const std::vector<int> &
         if (fast) {
             std::string m;
             for (int v = 0; v < (int)plan.dom.size(); ++v) {
-                const int t = msep[v] >= 0 ? nc + pi[plan.sep_up[msep[v]]] : nc + pi[home[v]];
+                const int t = msep[v] >= 0 ? nc + pi[plan.sep_up[msep[v]]] : nc + pi[mclq[v]];
                 m += std::to_string(v) + ":" + std::to_string(t) + " ";
             }
             fprintf(stderr, "marginal time per variable: %s\n", m.c_str());
@@ -741,6 +772,7 @@ int JTGen::Run(std::string &src, int64_t *wave_entries, std::vector<double> &ini
                 const int64_t have = msep[v] >= 0 ? plan.seps[msep[v]].size() : plan.cliques[home[v]].size();
                 if (plan.seps[sp].size() < have) msep[v] = sp;
             }
+    mclq = home;
     // traversal orders: Collect in post-order, Distribute in pre-order of a DFS.  Any child order
     // gives the same values (schedule freedom, section 4 of DESIGN.md); the fast order may pick one
     // per phase (FBN_JT_CHILD_ORDER bits, tuning): 1 = Collect visits children by ascending
@@ -781,6 +813,7 @@ int JTGen::Run(std::string &src, int64_t *wave_entries, std::vector<double> &ini
     // fp64 values per lane: table in flight + prefetched rows (FBN_JT_PREFETCH_BUDGET: tuning)
     // (fast order: 260 -- round 5 sweep 150 / 200 / 260 / 320: 0.171 / 0.169 / 0.165 / 0.166 ms)
     const int64_t kBudget = getenv("FBN_JT_PREFETCH_BUDGET") ? atoll(getenv("FBN_JT_PREFETCH_BUDGET")) : fast ? 260 : 200;
+    if (fast) ChooseMarginalSources(pre);
     PlaceMessages(post, pre, kBudget);
     int64_t rows = 0;
     for (int s = 0; s < ns; ++s) rows = std::max<int64_t>(rows, sep_row[s] + plan.seps[s].size());
