@@ -70,6 +70,31 @@ int64_t Binom(int64_t m, int k) {
 }
 
 void Put64(int32_t *p, int64_t v) { memcpy(p, &v, 8); }
+
+// 8 flag bytes (any nonzero = set) -> 8 bits, byte k -> bit k: fold each byte onto its bit 0, then
+// one multiply gathers the eight bit-0s into the top byte (terms land on distinct bits, no carries)
+inline uint32_t PackFlags8(const uint8_t *p) {
+    uint64_t x;
+    memcpy(&x, p, 8);
+    x |= x >> 4;
+    x |= x >> 2;
+    x |= x >> 1;
+    x &= 0x0101010101010101ull;
+    return (uint32_t)((x * 0x0102040810204080ull) >> 56);
+}
+
+// the inverse: bit k of a byte -> flag byte k (0 / 1), one table row per byte value
+struct FlagSpread {
+    uint64_t t[256];
+    FlagSpread() {
+        for (int b = 0; b < 256; ++b) {
+            uint64_t v = 0;
+            for (int k = 0; k < 8; ++k) v |= (uint64_t)((b >> k) & 1) << (8 * k);
+            t[b] = v;
+        }
+    }
+};
+const FlagSpread kSpread;
 int64_t Get64(const int32_t *p) {
     int64_t v;
     memcpy(&v, p, 8);
@@ -101,7 +126,9 @@ int Partition(fbn_pc_dist *s, int world) {
     const int64_t E = NumEdges(s);
     s->cuts.assign(world + 1, E);
     s->cuts[0] = 0;
-    if (s->d == 0) {
+    if (world == 1) {
+        // one range: no cost cut
+    } else if (s->d == 0) {
         const int64_t chunk = (E + world - 1) / world;
         for (int r = 1; r < world; ++r) s->cuts[r] = std::min<int64_t>(E, r * chunk);
     } else {
@@ -137,10 +164,15 @@ int Pack(fbn_pc_dist *s, const uint8_t *removed, const int32_t *sep, int64_t cou
     Put64(rec + 6, (int64_t)std::llround(kernel_s * 1e9));  // ns
     int32_t *p = rec + kHdr;
     if (d == 0) {
-        for (int64_t w = 0; w < (n + 31) / 32; ++w) {
+        const int64_t full = n / 32;
+        for (int64_t w = 0; w < full; ++w) {
+            const uint8_t *q = removed + 32 * w;
+            p[w] = (int32_t)(PackFlags8(q) | PackFlags8(q + 8) << 8 | PackFlags8(q + 16) << 16 | PackFlags8(q + 24) << 24);
+        }
+        if (n % 32) {
             uint32_t bits = 0;
-            for (int k = 0; k < 32 && 32 * w + k < n; ++k) bits |= (uint32_t)(removed[32 * w + k] != 0) << k;
-            p[w] = (int32_t)bits;
+            for (int64_t k = 0; 32 * full + k < n; ++k) bits |= (uint32_t)(removed[32 * full + k] != 0) << k;
+            p[full] = (int32_t)bits;
         }
     } else {
         for (int64_t e = 0; e < n; ++e) {
@@ -324,7 +356,10 @@ int fbn_pc_dist_apply(fbn_pc_dist *s, const int32_t *records, int *more) {
             for (int64_t w = 0; w < (n + 31) / 32; ++w) {
                 const uint32_t bits = (uint32_t)p[w];
                 const int cnt = (int)std::min<int64_t>(32, n - 32 * w);
-                for (int k = 0; k < cnt; ++k) rm[b + 32 * w + k] = (char)((bits >> k) & 1u);
+                if (cnt == 32)
+                    for (int q = 0; q < 4; ++q) memcpy(&rm[b + 32 * w + 8 * q], &kSpread.t[(bits >> (8 * q)) & 0xFFu], 8);
+                else
+                    for (int k = 0; k < cnt; ++k) rm[b + 32 * w + k] = (char)((bits >> k) & 1u);
                 uint32_t m = ~bits & (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u));
                 while (m) {
                     kept.push_back(b + 32 * w + __builtin_ctz(m));
@@ -340,7 +375,7 @@ int fbn_pc_dist_apply(fbn_pc_dist *s, const int32_t *records, int *more) {
             p += 1 + d;
         }
     }
-    if (d == 0) s->res.sepset.set_level0(s->nvars, rm.data());  // edges = the complete graph
+    if (d == 0) s->res.sepset.set_level0(s->nvars, std::move(rm));  // edges = the complete graph (flags taken over)
     else s->res.sepset.append_level(s->edges.data(), rm.data(), sep.data(), E, d);
     s->res.tests_per_level.push_back(counted);
     s->res.launched_per_level.push_back(launched);

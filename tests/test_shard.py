@@ -142,7 +142,7 @@ def test_session_partition_is_deterministic_and_balanced():
     cover of the level's edges on every rank; level 0 in equal chunks of the complete graph; after
     applying the same records, level 1 cut by candidate-set cost."""
     from fastbn_amd import pc_dist
-    n = 30
+    n = 70  # 2415 pairs: ranges start off the 32-pair record words
     for world in (1, 2, 3, 8):
         ss = [pc_dist.PCDistSession(n, 0.05, 3) for _ in range(world)]
         lv = [s.level(world, r) for r, s in enumerate(ss)]
@@ -153,12 +153,16 @@ def test_session_partition_is_deterministic_and_balanced():
         assert len({x[3] for x in lv}) == 1  # same record length everywhere
         rng = np.random.default_rng(world)
         rm_all = rng.random(P) < 0.7  # drop ~70 % of the pairs at level 0
-        recs = np.stack([s.pack(rm_all[b:e], None, e - b, e - b, L) for s, (_, b, e, L) in zip(ss, lv)])
+        # removal flags are "nonzero = removed" at the C-ABI: any byte value packs to one bit
+        flags = np.where(rm_all, rng.integers(1, 256, P), 0).astype(np.uint8)
+        recs = np.stack([s.pack(flags[b:e], None, e - b, e - b, L) for s, (_, b, e, L) in zip(ss, lv)])
         for s in ss:
             assert s.apply(recs)
         lv1 = [s.level(world, r) for r, s in enumerate(ss)]
         E = len(ss[0].edges())
         assert E == int((~rm_all).sum())
+        iu = np.triu_indices(n, 1)  # pair order of the complete graph
+        np.testing.assert_array_equal(ss[0].edges(), np.stack(iu, 1)[~rm_all])
         assert lv1[0][1] == 0 and lv1[-1][2] == E and all(a[2] == b[1] for a, b in zip(lv1, lv1[1:]))
         assert all(np.array_equal(ss[0].edges(), s.edges()) for s in ss)
         assert len({x[1:] for x in lv1}) == world or E < world
