@@ -1,7 +1,9 @@
 """Diagnostic: the multi-GPU PC session (fastbn_amd.pc_dist) at world size 1 on the config-5 dataset
 (1000 vars x 100k samples, levels 0-5), per level: fbn_pc_dist_level / _run / _apply wall times,
-then fbn_pc_dist_result; the single-GPU C-ABI call beside it.  FBN_PC_TIMING=1 adds the driver's
-per-level host phase prints."""
+then fbn_pc_dist_result; the single-GPU call beside it.  Last, medians of the raw C-ABI call
+fbn_pc_stable against pc_stable_distributed (bench.py's `session_world1`).  FBN_PC_TIMING=1 adds the
+driver's per-level host phase prints."""
+import ctypes
 import os
 import sys
 import time
@@ -49,3 +51,22 @@ for r in range(runs):
     for d, n, L, tl, tr, ta in T:
         print(f"   d={d} edges {n} rec {L}: level {tl * 1e3:.3f} run {tr * 1e3:.3f} apply {ta * 1e3:.3f} ms", flush=True)
     del res, sess, pc  # (the sepset dicts `same` built take ~10 ms to free: outside the timed windows)
+
+h = ctypes.c_void_p()
+
+
+def single_call():
+    F.lib.fbn_pc_stable(ci._h, 0.05, 6, 1, ctypes.byref(h))
+    return h
+
+
+for name, fn, done in (("fbn_pc_stable", single_call, lambda r: F.lib.fbn_pc_result_destroy(r)),
+                       ("session w1", lambda: pc_dist.pc_stable_distributed(ci, 1000, 0.05, 6), lambda r: None)):
+    t = []
+    for _ in range(9):
+        t0 = time.perf_counter()
+        out = fn()
+        t.append(time.perf_counter() - t0)
+        done(out)
+        del out
+    print(f"{name}: median {1e3 * np.median(t):.3f} ms  min {1e3 * min(t):.3f} ms", flush=True)
