@@ -548,6 +548,45 @@ def bench_loaders(munin_xml=None):
     return out
 
 
+def jt_full_batch_properties(d_ev, d_lab, d_marg, dims, chunk=16384):
+    """Size-independent checks over EVERY case of a timed JT batch (not timed; the oracle sample
+    beside it covers the values): an evidence variable's marginal row is zero, every other row sums
+    to 1 within 1e-12 with entries in [0, 1], and the label is the first strict maximum of variable
+    0's marginal, 0 when variable 0 is evidence (InferenceUsingJT / ArgMax, src/Inference.cpp:92-102;
+    oracle/jt_oracle.cpp:398-449).  A label that differs where variable 0's top two lie within 1e-12
+    relative is counted as a near-tie, any other difference as a mismatch."""
+    import torch
+    dev = d_marg.device
+    dims = np.asarray(dims, np.int64)
+    V, d0, n = len(dims), int(dims[0]), d_marg.shape[0]
+    col_var = torch.repeat_interleave(torch.arange(V, device=dev), torch.as_tensor(dims, device=dev))
+    worst, bad_ev, bad_range, mism, ties = 0.0, 0, 0, 0, 0
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        m, obs = d_marg[a:b], d_ev[a:b] >= 0
+        sums = torch.zeros((b - a, V), dtype=m.dtype, device=dev).index_add_(1, col_var, m)
+        bad_ev += int((m[obs[:, col_var]] != 0).sum())
+        if bool((~obs).any()):
+            worst = max(worst, float((sums[~obs] - 1).abs().max()))
+        bad_range += int(((m < 0) | (m > 1)).sum())
+        m0 = m[:, :d0]
+        want = torch.where(obs[:, 0], torch.zeros_like(d_lab[a:b], dtype=torch.long), torch.argmax(m0, 1))
+        diff = d_lab[a:b].long() != want
+        if bool(diff.any()):
+            top = torch.topk(m0[diff], min(2, d0), dim=1).values
+            tie = (top[:, 0] - top[:, -1]) <= 1e-12 * top[:, 0]
+            ties, mism = ties + int(tie.sum()), mism + int((~tie).sum())
+    ok = bad_ev == 0 and worst <= 1e-12 and bad_range == 0 and mism == 0
+    return {"cases": int(n), "ok": bool(ok), "evidence_rows_zero": bad_ev == 0, "max_abs_row_sum_err": worst,
+            "entries_outside_0_1": bad_range, "label_mismatches": mism, "label_near_ties": ties}
+
+
+def oracle_sample(n, head, spread):
+    """Case indices the oracle checks: the first `head` and `spread` more evenly over the batch, the
+    last case included."""
+    return np.unique(np.concatenate([np.arange(min(head, n)), np.linspace(0, n - 1, spread).astype(np.int64)]))
+
+
 def bench_munin(steps, warmup, cases=125_000, rank=0, world=1, device=0, with_baseline=False, exact=None):
     """the seeded Munin-like 1041-variable network at 20 % evidence (208
     variables per case), 125k cases per GPU -- on 8 GPUs the 1M-case job sharded by rank (seed
@@ -568,10 +607,11 @@ def bench_munin(steps, warmup, cases=125_000, rank=0, world=1, device=0, with_ba
     plan_s = time.perf_counter() - t0
     # native generator (bit-identical to synth.evidence_cases, multi-threaded)
     ev = fnet.evidence_cases(cases, 208, shard.synthetic_seed(20250131, rank))
+    pick = oracle_sample(cases, 16, 48)  # ~20 ms of the oracle per Munin-like case
     if rank == 0:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle as O
-        olab, omarg = O.OracleJT(path).infer(ev[:16])
+        olab, omarg = O.OracleJT(path).infer(ev[pick])
     d_ev = torch.from_numpy(ev).to(dev)
     d_lab = torch.empty(cases, dtype=torch.int32, device=dev)
     d_marg = torch.empty((cases, jt.info["sum_dom"]), dtype=torch.float64, device=dev)
@@ -584,9 +624,11 @@ def bench_munin(steps, warmup, cases=125_000, rank=0, world=1, device=0, with_ba
     torch.cuda.synchronize(dev)
     ok, rel = True, None
     if rank == 0:  # auto arithmetic order for this plan = fast (fbn_jt_set_exact): labels equal, marginals ~1e-15
-        gm = d_marg[:16].cpu().numpy()
+        ip = torch.from_numpy(pick).to(dev)
+        gm = d_marg[ip].cpu().numpy()
         rel = float(np.max(np.abs(gm - omarg) / np.maximum(np.abs(omarg), 1e-300)))
-        ok = bool((d_lab[:16].cpu().numpy() == olab).all() and rel <= 1e-12)
+        ok = bool((d_lab[ip].cpu().numpy() == olab).all() and rel <= 1e-12)
+    props = jt_full_batch_properties(d_ev, d_lab, d_marg, fnet.dims)
     ms = []
     all_lab = None
     if world > 1:
@@ -618,7 +660,9 @@ def bench_munin(steps, warmup, cases=125_000, rank=0, world=1, device=0, with_ba
             "wall_ms_per_step": 1e3 * wall / steps, "plan_s": plan_s,
             "kernel_variant": jt.refresh_info()["variant"],
             "arithmetic_order": "exact" if exact else "fast (normalizations cancel; labels equal, marginals within 1e-12)",
-            "parity_vs_oracle_16_cases": {"labels_equal_and_marg_within_1e-12": bool(ok), "max_rel_err": rel},
+            "parity_vs_oracle": {"cases": int(len(pick)), "sample": "first 16 + 48 spread over the batch",
+                                 "labels_equal_and_marg_within_1e-12": bool(ok), "max_rel_err": rel},
+            "full_batch_properties": props,
             "cliques": jt.info["num_cliques"], "clique_entries": jt.info["clique_entries"],
             "roofline": {"bound": "hbm", "achieved": bpc * cases / (k * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": bpc * cases / (k * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -852,14 +896,21 @@ def main():
     if rank == 0:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle as O
-        olab, omarg = O.OracleJT(os.path.join(ALARM, "alarm.xml")).infer(ev[:256])
+        pick = oracle_sample(args.cases, 256, 1792)
+        olab, omarg = O.OracleJT(os.path.join(ALARM, "alarm.xml")).infer(ev[pick])
         # default (fast) arithmetic order: labels equal, marginals within 1e-12 relative
-        gm = d_marg[:256].cpu().numpy()
+        ip = torch.from_numpy(pick).to(dev)
+        gm = d_marg[ip].cpu().numpy()
         alarm_rel = float(np.max(np.abs(gm - omarg) / np.maximum(np.abs(omarg), 1e-300)))
-        ok = (d_lab[:256].cpu().numpy() == olab).all() and alarm_rel <= 1e-12
+        ok = (d_lab[ip].cpu().numpy() == olab).all() and alarm_rel <= 1e-12
         if not ok:
             log("ERROR: GPU results differ from the oracle")
             sys.exit(1)
+    # every case of the last step: size-independent properties (each rank its own shard)
+    alarm_props = jt_full_batch_properties(d_ev, d_lab, d_marg, alarm_net.dims)
+    if not alarm_props["ok"]:
+        log(f"ERROR: full-batch properties violated: {alarm_props}")
+        sys.exit(1)
 
     total_cases = args.cases * args.steps * world
     value = total_cases / elapsed
@@ -885,8 +936,10 @@ def main():
                                                               if world > 1 else "")},
         "roofline": {**roof, "kernel_variant": jt.refresh_info()["variant"],
                      "arithmetic_order": "fast (normalizations cancel; labels equal, marginals within 1e-12)",
-                     "parity_vs_oracle_256_cases": {"labels_equal": True,
-                                                    "max_rel_err": alarm_rel if rank == 0 else None}},
+                     "parity_vs_oracle": {"cases": int(len(pick)) if rank == 0 else None,
+                                          "sample": "first 256 + 1792 spread over the batch", "labels_equal": True,
+                                          "max_rel_err": alarm_rel if rank == 0 else None},
+                     "full_batch_properties": alarm_props},
     }
     if world > 1 and not args.no_munin:
         # BASELINE config 4 at its real scale: 125k Munin-like cases per rank (1M on 8 GPUs)
