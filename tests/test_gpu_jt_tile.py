@@ -123,6 +123,31 @@ def test_munin_like_default_and_vs_oracle(tmp_path):
     np.testing.assert_array_equal(marg, omarg)
 
 
+@pytest.mark.parametrize("k", [104, 416])
+def test_munin_like_large_batch_spread_vs_oracle(tmp_path, k):
+    """16,384 Munin-like cases in one launch at 10 % / 40 % evidence (the bench's shape at full
+    occupancy: 1,024 case groups): the oracle on 160 cases spread over the batch (the last
+    included), and every case through bench.jt_full_batch_properties (rows sum to 1, evidence rows
+    zero, each label the first strict maximum of variable 0's marginal)."""
+    import sys
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    p = str(tmp_path / "munin_like.xml")
+    synth.random_network(1041, seed=1041, window=12, path=p, name="munin_like")
+    n = 16384
+    ev = synth.evidence_cases(synth.read_xmlbif(p), n, k, seed=7 + k)
+    jt = F.JunctionTree(F.Network(p), device=0)
+    lab, marg = jt.infer(ev)
+    assert jt.refresh_info()["variant"] == 5
+    pick = bench.oracle_sample(n, 1, 160)
+    olab, omarg = O.OracleJT(p).infer(ev[pick])
+    _check(lab[pick], marg[pick], olab, omarg, ev[pick], jt.network.dims)
+    props = bench.jt_full_batch_properties(torch.from_numpy(ev), torch.from_numpy(lab), torch.from_numpy(marg),
+                                           jt.network.dims)
+    assert props["ok"] and props["cases"] == n, props
+
+
 def test_loop_tiled_munin_like_vs_reference(munin_fixture, monkeypatch):
     """FBN_JT_TILING = 1 (opt-in loop tiling: chunk-major R streams, bins written by a run's first
     chunk and added into by the later ones) on the reference's own Munin-like fixture cases."""
