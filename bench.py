@@ -277,12 +277,14 @@ N_VARS_C5 = 1000
 INT_VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9  # MI355X: a wave64 32-bit VALU instruction issues in 2 cycles
 
 
-def pc_roofline(kernel_s, device_bytes, byte_column_bytes):
+def pc_roofline(kernel_s, device_bytes, byte_column_bytes, world=1):
     """Config 5's CI kernels against the bounds they can hit: 32-bit VALU issue (popcount / AND
     for the bit-sliced kernels, the binning for the histogram kernel) and L2<->fabric traffic, per
     PC run; VALU instructions and fabric bytes per run from the committed PMC profile
     (profiles/r05/pc5_kernels.json: rocprofv3 --pmc SQ_INSTS_VALU / FETCH_SIZE / WRITE_SIZE, calibrated),
-    the kernel time measured live (HIP events around every CI batch of a run)."""
+    the kernel time measured live (HIP events around every CI batch of a run).  world > 1: the run's
+    work is split over the ranks, so the whole run's instructions / bytes are taken over the slowest
+    rank's kernel time against `world` GPUs' peak."""
     path = _first_profile("r05/pc5_kernels.json", "pc5_kernels.json")
     out = {"kernel_ms_per_run": 1e3 * kernel_s, "column_bytes_read_per_run": device_bytes,
            "model": {"bytes_per_run": byte_column_bytes,
@@ -298,14 +300,17 @@ def pc_roofline(kernel_s, device_bytes, byte_column_bytes):
           if k not in ("ci_cols_check", "ci_bits_build", "ci_bits_rowcount")}  # once per dataset
     ops = sum(v["valu_lane_ops_per_run"] for v in ks.values())
     fab = sum(v["fabric_bytes_per_run"] for v in ks.values())
-    valu = ops / kernel_s / INT_VALU_PEAK_LANE_OPS
-    fabric = fab / kernel_s / (HBM_PEAK_GBS * 1e9)
+    valu = ops / kernel_s / (world * INT_VALU_PEAK_LANE_OPS)
+    fabric = fab / kernel_s / (world * HBM_PEAK_GBS * 1e9)
     top = max(ks, key=lambda k: ks[k]["time_ms_per_run"])
     if valu >= fabric:
-        r = {"bound": "valu", "achieved": ops / kernel_s / 1e12, "peak": INT_VALU_PEAK_LANE_OPS / 1e12,
+        r = {"bound": "valu", "achieved": ops / kernel_s / 1e12, "peak": world * INT_VALU_PEAK_LANE_OPS / 1e12,
              "unit": "Tlane-op/s", "frac": valu}
     else:
-        r = {"bound": "hbm", "achieved": fab / kernel_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": fabric}
+        r = {"bound": "hbm", "achieved": fab / kernel_s / 1e9, "peak": world * HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": fabric}
+    if world > 1:
+        r["per_gpu_peak_x"] = world
     return {**r, "traffic": fab, "valu_frac": valu, "fabric_frac": fabric, **out,
             "dominant_kernel": {top: ks[top]}, "source": os.path.relpath(path, REPO),
             "note": "all CI kernels of one run: PMC VALU lane-ops and calibrated L2<->fabric bytes per run over the "
@@ -393,6 +398,7 @@ def _pc_broadcast_ctx(load, rank, device):
         ci = F.IndependenceTest.from_device(t.data_ptr(), meta[0][0], meta[0][1], dims, 0.05, device)
         ci._cols_keepalive = t
         coll = None
+    ci.num_samples = int(meta[0][1])
     return ci, coll, meta[0][0]
 
 
@@ -406,8 +412,10 @@ def _pc_dist_timed(load, steps, rank, world, device, depth):
     from fastbn_amd import pc_dist
     dev = torch.device("cuda", device)
     ci, coll, nvars = _pc_broadcast_ctx(load, rank, device)
+    # warm-up, with this rank's kernel time recorded (HIP events around every CI batch of its ranges)
+    res, tests, launched = pc_dist.pc_stable_distributed(ci, nvars, 0.05, depth, device=coll)
+    kernel_s = shard.max_over_ranks(res.kernel_s, dev)
     ci.set_kernel_timing(False)
-    res, tests, launched = pc_dist.pc_stable_distributed(ci, nvars, 0.05, depth, device=coll)  # warm-up
     t = []
     for _ in range(steps):
         dist.barrier()
@@ -417,7 +425,7 @@ def _pc_dist_timed(load, steps, rank, world, device, depth):
         torch.cuda.synchronize(dev)
         dist.barrier()
         t.append(shard.max_over_ranks(time.perf_counter() - t0, dev))
-    return res, tests, launched, 1e3 * float(np.median(t))
+    return res, tests, launched, 1e3 * float(np.median(t)), kernel_s
 
 
 def bench_pc_alarm_dist(steps, rank, world, device):
@@ -441,11 +449,12 @@ def bench_pc_alarm_dist(steps, rank, world, device):
     ci.set_kernel_timing(False)
     if not pc_dist.small_eligible(ci):  # (not ALARM: a larger graph takes the partitioned session)
         del ci
-        res, tests, launched, ms = _pc_dist_timed(load, steps, rank, world, device, 1000)
+        res, tests, launched, ms, kern_s = _pc_dist_timed(load, steps, rank, world, device, 1000)
         return {"metric": "PC-stable CI-tests/sec (alarm_s5000, levels 0-4)", "value": sum(tests) / (ms * 1e-3),
                 "unit": "CI-tests/s", "n_gpus": world, "tests": int(sum(tests)), "tests_per_level": tests,
                 "launched_per_level": launched, "ms_per_run": ms, "edges": len(res.edges),
-                "parallelism": f"edge ranges per level x{world}, one all-gather per level"}
+                "parallelism": f"edge ranges per level x{world}, one all-gather per level",
+                "roofline": pc_roofline(kern_s, res.device_bytes, 0, world)}
     mode = f"replicas x{world} (one-launch device-resident search per rank) + one broadcast of rank 0's record"
     for _ in range(3):  # warm-up
         res, rec0 = pc_dist.pc_stable_replicas(ci, 0.05, 1000, device=coll)
@@ -461,12 +470,21 @@ def bench_pc_alarm_dist(steps, rank, world, device):
     res, rec0 = pc_dist.pc_stable_replicas(ci, 0.05, 1000, device=coll, check=True)  # every rank == rank 0
     ms = 1e3 * float(np.median(t))
     tests = rec0["tests_per_level"]
+    # each replica runs the whole search: the single-GPU roofline (SURVEY 8(d) byte model of the
+    # reference-equivalent tests over one rank's run time; measured launch traffic beside it)
+    model_bytes = int(ci.num_samples) * sum(int(c) * (d + 2) for d, c in enumerate(tests))
+    ach = model_bytes / (ms * 1e-3) / 1e9
+    roof = {"bound": "latency", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "model_bytes_per_run": model_bytes, "per": "one replica (every rank runs the whole search)",
+            **pc_small_traffic(),
+            "note": "one launch of five dependent levels over a cache-resident column store (DESIGN.md 5.3): "
+                    "a latency chain, frac small by construction; wall time includes the record broadcast"}
     return {"metric": "PC-stable CI-tests/sec (alarm_s5000, levels 0-4)", "value": sum(tests) / (ms * 1e-3),
             "unit": "CI-tests/s", "n_gpus": world, "tests": int(sum(tests)), "tests_per_level": tests,
             "launched_per_level": res.launched_per_level.tolist(), "ms_per_run": ms, "edges": len(rec0["edges"]),
             "parallelism": mode, "scaling": "replicas only (a small graph's search does not shard)",
             "timing": "wall clock between barriers, max over ranks, median of runs",
-            "matches_single_gpu": int(sum(tests)) == 5206 and len(rec0["edges"]) == 44,
+            "matches_single_gpu": int(sum(tests)) == 5206 and len(rec0["edges"]) == 44, "roofline": roof,
             "note": "one launch of five dependent levels (0.14 ms on one GPU): N GPUs cannot shorten it, so "
                     "each rank runs it and rank 0's result record is broadcast (DESIGN.md 6)"}
 
@@ -474,12 +492,15 @@ def bench_pc_alarm_dist(steps, rank, world, device):
 def bench_pc_synth_dist(steps, rank, world, device, depth=6):
     """BASELINE config 5 on N GPUs (`_pc_dist_timed` over the 1000 x 100k synthetic store); the
     skeleton is checked against the committed fixture (tests/golden/pc_c5.json) on rank 0."""
-    res, tests, launched, ms = _pc_dist_timed(synth_c5, steps, rank, world, device, depth)
+    res, tests, launched, ms, kern_s = _pc_dist_timed(synth_c5, steps, rank, world, device, depth)
+    N = 100_000
     out = {"metric": "PC-stable CI-tests/sec (synthetic 1000 vars x 100k samples, levels 0-5, BASELINE config 5)",
            "value": sum(tests) / (ms * 1e-3), "unit": "CI-tests/s", "n_gpus": world, "tests": int(sum(tests)),
            "tests_per_level": tests, "launched_per_level": launched, "ms_per_run": ms,
            "edges": len(res.edges), "parallelism": f"edge ranges per level x{world}, one all-gather per level",
-           "timing": "wall clock between barriers, max over ranks, median of runs"}
+           "timing": "wall clock between barriers, max over ranks, median of runs",
+           "roofline": pc_roofline(kern_s, res.device_bytes, sum(n_d * N * (d + 2) for d, n_d in enumerate(launched)),
+                                   world)}
     if rank == 0:
         import json as _json
         sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -783,6 +804,42 @@ def summary(out):
     return sm
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv):
+    """`bench.py --gpus N` started without a launcher (no WORLD_SIZE in the environment): start N
+    rank processes -- the same torch.distributed.run command the driver uses, one process per GPU,
+    rendezvous on 127.0.0.1 -- and return their exit code.  Called before this process touches torch
+    or the GPU; the ranks are children (no exec), rank 0's JSON line reaches stdout unchanged."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    log(f"bench: --gpus {n} without WORLD_SIZE: launching {n} ranks ({' '.join(cmd[1:6])} ...)")
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
+
+
+def launcher_check(world, rank):
+    """--launcher-check: the rank plumbing alone, on the CPU (gloo), no GPU and no workload -- every
+    rank joins the group, the barrier / max-over-ranks timing runs, and rank 0 prints the world size
+    the group reports and the ranks it saw (tests/test_bench_checks.py).  Not a measurement."""
+    import torch
+    import torch.distributed as dist
+    t0 = time.perf_counter()
+    dist.barrier()
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0)
+    seen = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(seen, torch.tensor([rank], dtype=torch.int64))
+    if rank == 0:
+        print(json.dumps({"launcher_check": True, "n_gpus": world, "world_size_seen": dist.get_world_size(),
+                          "ranks_seen": [int(s.item()) for s in seen], "backend": dist.get_backend(),
+                          "barrier_s": elapsed}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -794,17 +851,40 @@ def main():
     ap.add_argument("--no-pc", action="store_true")
     ap.add_argument("--no-munin", action="store_true")
     ap.add_argument("--no-loaders", action="store_true")
+    ap.add_argument("--launcher-check", action="store_true",
+                    help="CPU-only check of the rank launch (gloo, no workload); not a measurement")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+
+    # --gpus N is the number of rank processes.  Under a launcher (torchrun sets WORLD_SIZE) the two
+    # must agree; without one, N > 1 starts the ranks here, before anything touches the GPU.
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    world = int(env_world) if env_world is not None else 1
+    if world != args.gpus:
+        log(f"ERROR: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+        sys.exit(2)
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launcher_check:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        launcher_check(world, rank)
+        return
     # FBN_BENCH_BACKEND=gloo + more ranks than GPUs: a rehearsal of the N > 1 path on a small box
     # (ranks share GPUs round-robin); the measured runs use RCCL, one rank per GPU
     backend = os.environ.get("FBN_BENCH_BACKEND", "nccl")
+    if backend == "nccl" and world > torch.cuda.device_count():
+        log(f"ERROR: {world} ranks over RCCL need {world} GPUs; {torch.cuda.device_count()} visible "
+            f"(FBN_BENCH_BACKEND=gloo rehearses ranks sharing a GPU)")
+        sys.exit(2)
     if backend != "nccl":
         local = local % max(1, torch.cuda.device_count())
     if world > 1 or os.environ.get("FBN_BENCH_FORCE_GATHER") == "1":
@@ -921,6 +1001,7 @@ def main():
         "value": value,
         "unit": "cases/s",
         "n_gpus": world,
+        "world_size_seen": dist.get_world_size() if dist.is_initialized() else 1,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": 1e3 * elapsed / args.steps,

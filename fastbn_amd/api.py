@@ -216,8 +216,9 @@ class _PlanInfo(C.Structure):
 
 
 class Network(_Handle):
-    _destroy = "fbn_network_destroy"
     """Discrete BN loaded from XMLBIF (CustomNetwork::GetNetFromXMLBIFFile)."""
+
+    _destroy = "fbn_network_destroy"
 
     def __init__(self, path=None, _handle=None):
         h = C.c_void_p() if _handle is None else _handle
@@ -347,8 +348,9 @@ class Dataset:
 
 
 class JunctionTree(_Handle):
-    _destroy = "fbn_jt_plan_destroy"
     """Batched JT inference on one device (JunctionTree ctor + PredictUseJTInfer over all cases)."""
+
+    _destroy = "fbn_jt_plan_destroy"
 
     def __init__(self, network, device=0):
         self.network = network
@@ -498,8 +500,9 @@ class JunctionTree(_Handle):
 
 
 class IndependenceTest(_Handle):
-    _destroy = "fbn_ci_ctx_destroy"
     """G^2 tests on the device (IndependenceTest::IndependenceResult, batched)."""
+
+    _destroy = "fbn_ci_ctx_destroy"
 
     def __init__(self, dataset, alpha=0.05, device=0):
         self.alpha = alpha
@@ -592,8 +595,9 @@ class IndependenceTest(_Handle):
 
 
 class PCResult(_Handle):
-    _destroy = "fbn_pc_result_destroy"
     """A PC-stable result handle: skeleton, sepsets, orientation, SHD (fbn_pc_*)."""
+
+    _destroy = "fbn_pc_result_destroy"
 
     def __init__(self, handle):
         self._h = handle
@@ -718,7 +722,7 @@ class PCStable:
     edges = property(lambda self: self.result.edges)
     sepset = property(lambda self: self.result.sepset)
     oriented = property(lambda self: self.result.oriented)
-    path = property(lambda self: self.result.path)  # 0 host levels, 1 device-resident, 2 fell back
+    path = property(lambda self: self.result.path)  # 0 host levels, 1 device-resident, 2 fell back, 3 host levels after the device level 0 -> 1 hand-off
 
     def GetSHD(self, bif_path):
         return self.result.GetSHD(bif_path)

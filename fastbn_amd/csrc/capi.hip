@@ -205,6 +205,14 @@ struct fbn_jt_plan {
     bool ev_check = true;  // fbn_jt_set_evidence_check
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false, ktiming = true;
+    // the caller streams runs were queued on (fbn_jt_run_device returns before its kernels end):
+    // fbn_jt_plan_destroy drains these, not the whole device
+    std::vector<hipStream_t> streams_used;
+    void note_stream(hipStream_t s) {
+        for (hipStream_t u : streams_used)
+            if (u == s) return;
+        streams_used.push_back(s);
+    }
     ~fbn_jt_plan() {
         for (auto &k : gen)
             if (k.mod) (void)hipModuleUnload(k.mod);
@@ -314,6 +322,7 @@ struct fbn_ci_ctx {
     int64_t bits_W = 0;
     CiSlot slot[2];
     hipStream_t stream = nullptr;  // the PC driver's rounds (pinned staging, one sync per round)
+    std::vector<hipStream_t> streams_used;  // caller streams of fbn_ci_run (drained by fbn_ci_ctx_destroy)
     float last_ms = 0.f;
     bool timing = true;  // HIP events around every CI kernel (fbn_ci_set_kernel_timing)
     ~fbn_ci_ctx();
@@ -967,6 +976,7 @@ int fbn_jt_evidence_validate(fbn_jt_plan *p, const int8_t *d_evidence, int64_t n
     if (ncases == 0) return FBN_OK;
     if (p->device < 0) return SetError(FBN_ERR_NODEV, "host-only plan (created with device < 0)");
     FBN_HIP(hipSetDevice(p->device));
+    p->note_stream(static_cast<hipStream_t>(hip_stream));
     return JtCheckEvidence(p, d_evidence, ncases, static_cast<hipStream_t>(hip_stream));
 }
 
@@ -991,6 +1001,7 @@ int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, 
     if (ncases == 0) return FBN_OK;
     if (p->device < 0) return SetError(FBN_ERR_NODEV, "host-only plan (created with device < 0)");
     FBN_HIP(hipSetDevice(p->device));
+    p->note_stream(static_cast<hipStream_t>(hip_stream));
     return JtRunDevice(p, d_evidence, ncases, d_labels, d_marginals, static_cast<hipStream_t>(hip_stream),
                        p->ev_check);
 }
@@ -1223,9 +1234,9 @@ int fbn_jt_last_kernel_ms(const fbn_jt_plan *p, float *ms) {
 
 int fbn_jt_plan_destroy(fbn_jt_plan *p) {
     if (!p) return FBN_OK;
-    if (p->device >= 0) {  // runs are queued on caller streams: drain them before the buffers go
+    if (p->device >= 0) {  // runs are queued on caller streams: drain those before the buffers go
         (void)hipSetDevice(p->device);
-        (void)hipDeviceSynchronize();
+        for (hipStream_t s : p->streams_used) (void)hipStreamSynchronize(s);
     }
     delete p;
     return FBN_OK;
@@ -1838,6 +1849,8 @@ int fbn_ci_run(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, double alp
     if (n == 0) return FBN_OK;
     FBN_HIP(hipSetDevice(c->device));
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    if (std::find(c->streams_used.begin(), c->streams_used.end(), s) == c->streams_used.end())
+        c->streams_used.push_back(s);
     int rc = CiLaunchDevice(c, items, n, d, alpha, g2 || p, nullptr, s);
     if (rc) return rc;
     if (g2) FBN_HIP(hipMemcpyAsync(g2, c->g2.p, (size_t)n * 8, hipMemcpyDeviceToHost, s));
@@ -1885,6 +1898,14 @@ int fbn_ci_debug_counts(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d, i
     int rc;
     const int nv = c->nvars;
     fbn::PCResultHost scratch;
+    // a debug call must not change which path later batches on this ctx take: the pair mode (and
+    // with it the derived level-1 / level-2 counting) is restored on every exit
+    struct PairModeGuard {
+        fbn_ci_ctx *c;
+        int mode;
+        bool recorded, triples;
+        ~PairModeGuard() { c->pair_mode = mode, c->pairs_recorded = recorded, c->triples_ready = triples; }
+    } guard{c, c->pair_mode, c->pairs_recorded, c->triples_ready};
     auto level0 = [&]() -> int {  // the PC run's level 0, pair tables recorded
         fbn::CiBatchStats st{0, 0};
         for (int v = 0; v < nv; ++v) st.dim_rows += (int64_t)(nv - 1) * c->dims[v], st.maxdim = std::max(st.maxdim, (int)c->dims[v]);
@@ -1969,7 +1990,7 @@ int fbn_ci_ctx_destroy(fbn_ci_ctx *c) {
     // resident search returns on its completion word, and batches may be queued on caller streams
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    (void)hipDeviceSynchronize();
+    for (hipStream_t s : c->streams_used) (void)hipStreamSynchronize(s);
     delete c;
     return FBN_OK;
 }
@@ -2257,11 +2278,18 @@ int CiBatchLaunchAllPairs(fbn_ci_ctx *c, double alpha, const CiBatchStats *pre, 
 
 bool CiPairsReady(const fbn_ci_ctx *c) { return c->pair_mode == 2 && c->pairs_recorded; }
 
-bool CiL0L1DeviceEligible(const fbn_ci_ctx *c, int group_size) {
-    if (group_size != 1 || !c->bits_ready || getenv("FBN_PC_HOST_L1") || getenv("FBN_PC_HOST_L0L1")) return false;
+// Decided before the level-0 launch, so the bit-sliced store the device hand-off reads is built
+// here when the dataset qualifies for it (the same test as CiLaunchDevice's bits path): a fresh ctx
+// -- every one-shot CLI run -- takes the device path from its first PC run on.
+bool CiL0L1DeviceEligible(fbn_ci_ctx *c, int group_size) {
+    if (group_size != 1 || getenv("FBN_PC_HOST_L1") || getenv("FBN_PC_HOST_L0L1") || c->nvars < 2) return false;
     for (int v = 0; v < c->nvars; ++v)
         if (c->dims[v] > 4) return false;
-    return c->nvars >= 2;
+    if (!c->bits_ready) {
+        const bool bits_path = !getenv("FBN_CI_NO_BITS") && (c->N >= 4096 || getenv("FBN_CI_FORCE_BITS"));
+        if (!bits_path || CiBitsEnsure(c, c->stream) != FBN_OK) return false;
+    }
+    return true;
 }
 
 int CiL0L1Device(fbn_ci_ctx *c, int64_t P, int *E, int64_t *cands, PCResultHost &res) {

@@ -263,7 +263,7 @@ int CiLevel1Run(fbn_ci_ctx *c, double alpha, int E, int64_t cands, LevelOut &out
                 const std::function<int()> &host_work);
 // Level 0 -> level 1 without a host round trip (capi.hip): whether the ctx qualifies (level 1 would
 // run on the device: pair tables recorded, bit-sliced store, every variable <= 4 states, group 1)
-bool CiL0L1DeviceEligible(const fbn_ci_ctx *c, int group_size);
+bool CiL0L1DeviceEligible(fbn_ci_ctx *c, int group_size);
 // level 0 recorded its pair tables and the ctx uses them (pair mode 2): level 1 can run on the device
 bool CiPairsReady(const fbn_ci_ctx *c);
 // after CiBatchLaunchAllPairs(copy_flags = false) of the whole complete graph (P pairs): the kept

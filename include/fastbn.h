@@ -294,7 +294,9 @@ int fbn_pc_timing(const fbn_pc_result *r, double *total_s, double *kernel_s);
 /* Which skeleton path ran: 0 host-driven levels, 1 the device-resident search (small graphs, one
  * launch: plain by default after an occupancy check, cooperative with FBN_PC_SMALL_COOP=1), 2 the
  * device-resident search was refused at launch or timed out at a grid
- * barrier and the host-driven levels ran instead (same answer). */
+ * barrier and the host-driven levels ran instead (same answer), 3 host-driven levels whose level 0
+ * -> level 1 hand-off ran on the device (the kept pairs became the level-1 edge list / adjacency
+ * there; FBN_PC_HOST_L0L1=1 forces 0). */
 int fbn_pc_path(const fbn_pc_result *r, int *path);
 /* The result as one flat int32 record (for moving it between ranks): magic 0x52504246, n_levels,
  * n_levels (lo, hi) halves of the per-level test counts, n_edges, pairs [n_edges][2], then the

@@ -57,3 +57,33 @@ def test_oracle_sample_indices():
     assert s[0] == 0 and s[-1] == 99_999 and len(s) == len(np.unique(s)) and (np.diff(s) > 0).all()
     assert set(range(256)) <= set(s.tolist())
     assert list(bench.oracle_sample(5, 16, 48)) == [0, 1, 2, 3, 4]
+
+
+def _bench(args, env_extra=None):
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, capture_output=True, text=True,
+                       env=env, timeout=240)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r.returncode, (json.loads(lines[-1]) if lines else None), r.stderr
+
+
+def test_bench_gpus_2_launches_two_ranks():
+    """`bench.py --gpus 2` without a launcher starts two rank processes itself (torch.distributed.run,
+    gloo here: --launcher-check runs the rank plumbing only) and rank 0 reports world size 2."""
+    rc, line, err = _bench(["--gpus", "2", "--launcher-check"])
+    assert rc == 0, err[-2000:]
+    assert line["n_gpus"] == 2 and line["world_size_seen"] == 2 and line["ranks_seen"] == [0, 1]
+
+
+def test_bench_gpus_1_stays_one_process():
+    rc, line, err = _bench(["--launcher-check"])
+    assert rc == 0, err[-2000:]
+    assert line["n_gpus"] == 1 and line["world_size_seen"] == 1 and line["ranks_seen"] == [0]
+
+
+def test_bench_rejects_gpus_world_size_mismatch():
+    rc, line, err = _bench(["--gpus", "2", "--launcher-check"], {"WORLD_SIZE": "3", "RANK": "0"})
+    assert rc == 2 and line is None and "WORLD_SIZE=3" in err

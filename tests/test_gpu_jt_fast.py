@@ -136,3 +136,45 @@ def test_kernel_timing_switch(jt):
         jt.set_kernel_timing(True)
     np.testing.assert_array_equal(lab0, lab1)
     np.testing.assert_array_equal(marg0, marg1)
+
+
+def test_headline_size_100k_default_and_exact(jt):
+    """BASELINE config 2 at its real size through the bench's path: 100,000 ALARM cases (1,563
+    64-case blocks: two rounds on 1,024 SIMDs, the 539-block tail included) in device buffers
+    (fbn_jt_run_device).  Default (fast) order: labels equal and marginals within 1e-12 of the
+    oracle on 2,048+ cases spread over the batch (the last block included), and every case passes
+    bench.jt_full_batch_properties.  Exact order on the same batch: bit-identical to the oracle on
+    the sample (src/JunctionTree.cpp:1508-1534, src/Inference.cpp:92-102)."""
+    import torch
+    import bench  # (conftest puts the repo root on sys.path)
+    n = 100_000
+    xml = os.path.join(GOLD, "alarm", "alarm.xml")
+    ev = jt.network.evidence_cases(n, 7, 20250131)
+    dev = torch.device("cuda", 0)
+    d_ev = torch.from_numpy(ev).to(dev)
+    d_lab = torch.empty(n, dtype=torch.int32, device=dev)
+    d_marg = torch.empty((n, jt.info["sum_dom"]), dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    pick = bench.oracle_sample(n, 256, 1792)
+    pick = np.unique(np.concatenate([pick, np.arange(n - 64, n)]))  # the whole last block
+    olab, omarg = O.OracleJT(xml).infer(ev[pick])
+    ip = torch.from_numpy(pick).to(dev)
+    try:
+        for exact in (None, True):
+            jt.set_exact(exact)
+            d_lab.fill_(-7)
+            d_marg.fill_(np.nan)
+            jt.run_device(d_ev.data_ptr(), n, d_lab.data_ptr(), d_marg.data_ptr(), stream)
+            torch.cuda.synchronize(dev)
+            assert jt.refresh_info()["variant"] == 3
+            lab, marg = d_lab[ip].cpu().numpy(), d_marg[ip].cpu().numpy()
+            np.testing.assert_array_equal(lab, olab)
+            if exact:
+                np.testing.assert_array_equal(marg, omarg)
+            else:
+                assert jt.debug_flagged_blocks() == 0
+                _close(marg, omarg)
+            props = bench.jt_full_batch_properties(d_ev, d_lab, d_marg, jt.network.dims)
+            assert props["ok"] and props["cases"] == n and props["label_near_ties"] == 0, props
+    finally:
+        jt.set_exact(None)

@@ -484,10 +484,13 @@ def test_level0_to_level1_on_device_matches_host_path(nvars, ns, monkeypatch):
     launched tests and orientation; 333 variables (ballot tails: not a multiple of 64) and config 5."""
     from fastbn_amd import synth
     cols, dims = synth.config5_dataset(nvars, ns)
+    # a fresh context: the first run must take the device hand-off (fbn_pc_path 3), not only warm runs
     ci = F.IndependenceTest(F.Dataset(columns=cols, dims=dims))
     a = F.PCStable(0.05, 6).StructLearnCompData(ci)
+    assert a.path == 3
     monkeypatch.setenv("FBN_PC_HOST_L0L1", "1")
-    b = F.PCStable(0.05, 6).StructLearnCompData(ci)
+    b = F.PCStable(0.05, 6).StructLearnCompData(F.IndependenceTest(F.Dataset(columns=cols, dims=dims)))
+    assert b.path == 0
     assert a.edges == b.edges and a.sepset == b.sepset
     assert a.tests_per_level.tolist() == b.tests_per_level.tolist()
     assert a.launched_per_level.tolist() == b.launched_per_level.tolist()
