@@ -125,20 +125,22 @@ def cpu_baseline_jt(budget_cases=40_000):
             "sample": f"{budget_cases} ALARM cases, restatement at t=1 (oracle/_ref absent), {secs:.2f} s"}
 
 
-def cpu_baseline_munin(xml, ev, cases=96):
+def cpu_baseline_munin(xml, ev, cases=1000, other=128):
     """The reference's per-case loop on the Munin-like network (ref_dump jtbench), t swept, on the
-    first `cases` cases of the GPU workload."""
+    first `cases` cases of the GPU workload at t = 1 (its best: the reference slows down with
+    threads on this tree) and the first `other` at the other thread counts (~20 s per 1,000 cases)."""
     hi = host_info()
     if not os.path.exists(REF_DUMP):
         return None
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "ev.libsvm")
         _libsvm(path, ev[:cases])
-        best, sweep = _jt_sweep(xml, path, path, lambda t: cases, hi)
+        best, sweep = _jt_sweep(xml, path, path, lambda t: cases if t == 1 else other, hi)
     return {"value": best["value"], "unit": "cases/s", "cores": best["threads"], "kind": "reference", "cpu": hi,
             "sweep": sweep,
-            "sample": f"first {cases} Munin-like cases of the GPU shard (208 evidence vars) through the reference's "
-                      f"per-case loop, best of threads {hi['sweep']}: {best['seconds']} s at t={best['threads']}"}
+            "sample": f"first {best['cases']} Munin-like cases of the GPU shard (208 evidence vars) through the "
+                      f"reference's per-case loop, best of threads {hi['sweep']} ({cases} cases at t=1, {other} "
+                      f"at the others): {best['seconds']} s at t={best['threads']}"}
 
 
 def _pc_sweep(src, depth, reps, hi):
@@ -207,6 +209,43 @@ def cpu_baseline_pc_c5(cols, dims, depth, nvars=160, reps=1):
                       f"t={best['threads']}; the O(E^2) erase loop grows quadratically with the edge count, so "
                       f"the full 1000-variable end-to-end rate is far lower (SURVEY: 826 s for level 0 at 10k "
                       f"samples)"}
+
+
+def cpu_baseline_pc_c5_full(cols, dims, depth):
+    """Config 5 at full size (all 1000 variables, 100k samples, levels 0-5: the 801,354 tests the GPU
+    runs) through the reference's counting / edge / OpenMP code (ref_dump pcbench), with its O(E^2)
+    vec_edges.erase loops replaced by one stable compaction per level ("noerase": the same edges in
+    the same order, so the same tests) -- the reference's CI work on the measured workload.  ~20-40 s
+    per thread count on a 16-CPU share, so only the upper half of the sweep runs."""
+    import struct
+    hi = host_info()
+    if not os.path.exists(REF_DUMP):
+        return None
+    threads = sorted({t for t in hi["sweep"] if t >= max(hi["sweep"]) // 2})
+    sweep = []
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "c5.bin")
+        with open(path, "wb") as f:
+            f.write(struct.pack("<iq", cols.shape[0], cols.shape[1]))
+            f.write(np.asarray(dims, np.int32).tobytes())
+            f.write(np.ascontiguousarray(cols).tobytes())
+        for t in threads:
+            log(f"bench: reference PC baseline (config 5, all {cols.shape[0]} variables, noerase), {t} threads")
+            out = subprocess.run([REF_DUMP, "pcbench", "cols:" + path, "0.05", str(depth), "1", str(t), "noerase"],
+                                 check=True, capture_output=True, text=True, env=_ref_env(t)).stdout
+            tests = [int(v) for v in out.split("|")[0].split()[1:]]
+            kv = out.split("|")[2].split()
+            tot, ci = float(kv[1]), float(kv[3])
+            sweep.append({"threads": t, "tests": sum(tests), "tests_per_level": tests, "total_s": round(tot, 3),
+                          "ci_s": round(ci, 3), "value": sum(tests) / tot, "ci_only_value": sum(tests) / ci})
+    best = max(sweep, key=lambda r: r["value"])
+    return {"value": best["value"], "unit": "CI-tests/s", "cores": best["threads"], "kind": "reference",
+            "ci_only_value": best["ci_only_value"], "tests_per_level": best["tests_per_level"], "cpu": hi,
+            "sweep": sweep,
+            "sample": f"the whole config-5 workload (1000 variables x 100k samples, levels 0-{depth - 1}, "
+                      f"{best['tests']} tests = the GPU's) through the reference's Counts2D / Counts3D / Edge / "
+                      f"ChoiceGenerator / OpenMP code (ref_dump pcbench noerase: the O(E^2) erase loop replaced by "
+                      f"one stable compaction), best of threads {threads}: {best['total_s']} s at t={best['threads']}"}
 
 
 def bench_pc(steps, warmup):
@@ -371,9 +410,14 @@ def bench_pc_synth(steps, depth=6, cpu_vars=160, with_baseline=True):
                              "same_skeleton": res.edges == pc.edges and res.sepset == pc.sepset,
                              "note": "fbn_pc_dist_* session (the N > 1 path) at world size 1, Python level "
                                      "loop + records included"}
-    cb = cpu_baseline_pc_c5(cols, dims, depth, nvars=cpu_vars) if with_baseline else None
-    if cb is not None:
-        out["cpu_baseline"] = cb
+    if with_baseline:
+        full = cpu_baseline_pc_c5_full(cols, dims, depth)
+        if full is not None:  # the measured workload itself: the line's cpu_baseline
+            out["cpu_baseline"] = full
+            out["cpu_baseline_ratio"] = out["value"] / full["value"]
+        part = cpu_baseline_pc_c5(cols, dims, depth, nvars=cpu_vars)
+        if part is not None:  # end-to-end with the reference's erase loops, on the first cpu_vars variables
+            out["cpu_baseline_end_to_end_subset" if full is not None else "cpu_baseline"] = part
     return out
 
 
@@ -755,29 +799,36 @@ def load_traffic(cases):
 
 
 def alarm_roofline(info, cases, kernel_ms, traffic):
-    """The ALARM kernel's (fbn_jt_gen, variant 3) roofline against the bound it has:
-    it keeps every clique table in registers / LDS, so it moves only the compulsory bytes (evidence
-    in, marginals + labels out: V + 8 sum_dom + 4 B per case) plus the separator rows its per-wave
-    workspace spills past L2 (`traffic`, calibrated PMC), and at one wave per SIMD it is bound by the
-    issue of its fp64 VALU instructions: `frac` = fp64 VALU lane-ops / fp64 vector peak (<= 1 by
-    construction).  SURVEY 8(d)'s materialized-table bytes (every table written and read once) are
-    kept as `model`, informational: this design does not move them, so that ratio may exceed 1."""
+    """The ALARM kernel's (fbn_jt_gen, variant 3) roofline against the resource it uses most
+    (DESIGN.md 5.1).  It keeps every clique table in registers / LDS, so it moves the compulsory
+    bytes (evidence in, marginals + labels out: V + 8 sum_dom + 4 B per case) plus the message rows
+    its per-wave workspace sends past L2; `traffic` = those measured L2<->fabric bytes (calibrated
+    PMC FETCH + WRITE per launch, scaled to this launch).  The other candidate bound is the issue of
+    its fp64 VALU instructions (measured per launch, against the fp64 vector peak).  `bound` is
+    whichever of the two fractions is higher; the other stands beside it.  SURVEY 8(d)'s
+    materialized-table bytes (every table written and read once) are kept as `model`, informational:
+    this design does not move them, so that ratio exceeds 1."""
     comp = info["num_nodes"] + 8 * info["sum_dom"] + 4
     t = kernel_ms * 1e-3
-    hbm = {"compulsory_bytes_per_case": comp, "achieved": comp * cases / t / 1e9, "peak": HBM_PEAK_GBS,
-           "unit": "GB/s", "frac": comp * cases / t / 1e9 / HBM_PEAK_GBS, "traffic": traffic,
-           "traffic_achieved": traffic / t / 1e9 if traffic else None,
-           "traffic_frac": traffic / t / 1e9 / HBM_PEAK_GBS if traffic else None}
+    hbm = {"compulsory_bytes_per_case": comp, "compulsory_achieved": comp * cases / t / 1e9,
+           "compulsory_frac": comp * cases / t / 1e9 / HBM_PEAK_GBS, "traffic": traffic,
+           "traffic_per_case": traffic / cases if traffic else None,
+           "achieved": traffic / t / 1e9 if traffic else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": traffic / t / 1e9 / HBM_PEAK_GBS if traffic else None}
     bpc = info["algorithmic_bytes_per_case"]
     model = {"bytes_per_case": bpc, "achieved": bpc * cases / t / 1e9, "model_frac": bpc * cases / t / 1e9 / HBM_PEAK_GBS,
              "note": "informational: SURVEY 8(d)'s materialized-table bytes, which this kernel does not move"}
     v = valu_roofline("alarm", cases, kernel_ms)
-    base = {"kernel_ms": kernel_ms, "traffic": traffic, "hbm": hbm, "model": model}
+    base = {"kernel_ms": kernel_ms, "traffic": traffic, "hbm": hbm, "model": model, "valu": v}
+    if hbm["frac"] is not None and (v is None or hbm["frac"] >= v["frac"]):
+        return {"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm["frac"],
+                **base, "note": "measured L2<->fabric traffic per launch over the kernel time (the higher of the "
+                                "two fractions; fp64 VALU issue beside it in `valu`)"}
     if v is None:
-        return {"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": hbm["frac"], **base}
-    return {**v, **base, "note": "fp64 VALU issue at one wave per SIMD binds this kernel (DESIGN.md 5.1); "
-                                 "hbm: compulsory bytes and measured L2<->fabric traffic; model: informational"}
+        return {"bound": "hbm", "achieved": hbm["compulsory_achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": hbm["compulsory_frac"], **base}
+    return {**{k: v[k] for k in ("bound", "achieved", "peak", "unit", "frac")}, **base,
+            "note": "fp64 VALU issue (the higher of the two fractions; measured traffic beside it in `hbm`)"}
 
 
 def summary(out):
@@ -911,7 +962,14 @@ def main():
     dev = torch.device("cuda", local)
     d_ev = torch.from_numpy(ev).to(dev)
     d_lab = torch.empty(args.cases, dtype=torch.int32, device=dev)
-    d_marg = torch.empty((args.cases, info["sum_dom"]), dtype=torch.float64, device=dev)
+    # marginals variable-major [sum_dom][cases] on the device (fbn_jt_set_output_layout 1: every
+    # store of the kernel writes 64 consecutive cases of one value, each line written once); the
+    # checks below read them through the transposed view (case-major rows, the reference's vectors)
+    layout = 0 if os.environ.get("FBN_BENCH_CASE_MAJOR") == "1" else 1
+    jt.set_output_layout(layout)
+    d_marg_buf = torch.empty(args.cases * info["sum_dom"], dtype=torch.float64, device=dev)
+    d_marg = (d_marg_buf.view(info["sum_dom"], args.cases).t() if layout == 1
+              else d_marg_buf.view(args.cases, info["sum_dom"]))
     stream = torch.cuda.current_stream(dev)
     # the evidence buffer is validated once (device-side range check, fbn_jt_evidence_validate);
     # the timed steps reuse the unchanged buffer without the per-call check (fully asynchronous)
@@ -932,7 +990,7 @@ def main():
 
     def step(i=0):
         lab = step_labs[i % step_labs.shape[0]]
-        jt.run_device(d_ev.data_ptr(), args.cases, lab.data_ptr(), d_marg.data_ptr(), stream.cuda_stream)
+        jt.run_device(d_ev.data_ptr(), args.cases, lab.data_ptr(), d_marg_buf.data_ptr(), stream.cuda_stream)
 
     def final_gather():
         if not gathering:
@@ -1013,6 +1071,8 @@ def main():
         "config": {"workload": "ALARM (37 vars) JT inference, 100k synthetic cases per GPU @ 7 evidence vars "
                                "(BASELINE config 2)", "cases_per_gpu": args.cases,
                    "evidence_per_case": EVIDENCE_PER_CASE,
+                   "marginal_layout": ("variable-major [sum_dom][cases] (fbn_jt_set_output_layout 1)" if layout == 1
+                                       else "case-major [cases][sum_dom]"),
                    "parallelism": f"case-sharded x{world}" + (" + one labels all-gather of every step (final gather)"
                                                               if world > 1 else "")},
         "roofline": {**roof, "kernel_variant": jt.refresh_info()["variant"],

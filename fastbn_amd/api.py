@@ -43,6 +43,8 @@ _SIGS = {
     "fbn_jt_set_evidence_check": [_vp, C.c_int],
     "fbn_jt_set_kernel_timing": [_vp, C.c_int],
     "fbn_jt_score": [_vp, _vp, _vp, _i64, _vp, _vp],
+    "fbn_jt_set_output_layout": [_vp, C.c_int],
+    "fbn_jt_score_terms_device": [_vp, _vp, _vp, _i64, _vp, _vp],
     "fbn_jt_last_kernel_ms": [_vp, _vp],
     "fbn_jt_stream_schedule": [_vp, _vp, C.c_int64, _vp, C.c_int64, _vp, _vp],
     "fbn_jt_set_waves_per_cu": [_vp, C.c_int],
@@ -358,6 +360,7 @@ class JunctionTree(_Handle):
         lib.fbn_jt_plan_create(network._h, device, C.byref(h))
         self._h = h
         _register(self)
+        self.output_layout = 0
         info = _PlanInfo()
         lib.fbn_jt_plan_info_get(h, C.byref(info))
         self.info = {k: getattr(info, k) for k, _ in _PlanInfo._fields_}
@@ -470,11 +473,17 @@ class JunctionTree(_Handle):
         buffer the caller validated (validate_device)."""
         lib.fbn_jt_set_evidence_check(self._h, int(bool(enable)))
 
-    def decision_margin(self, reset=False):
-        """(min |p - alpha|, #tests with |p - alpha| < 1e-9) over the tests run since the last reset."""
-        m, near = C.c_double(), C.c_int64()
-        lib.fbn_ci_decision_margin(self._h, C.byref(m), C.byref(near), int(bool(reset)))
-        return m.value, near.value
+    def set_output_layout(self, layout):
+        """fbn_jt_set_output_layout: run_device's marginals 0 = case-major [ncases][sum_dom]
+        (default), 1 = variable-major [sum_dom][ncases] (each store writes 64 consecutive cases).
+        infer() always returns case-major."""
+        lib.fbn_jt_set_output_layout(self._h, int(layout))
+        self.output_layout = int(layout)
+
+    def score_terms_device(self, d_marg_ptr, d_golden_ptr, ncases, d_terms_ptr, stream_ptr=None):
+        """fbn_jt_score_terms_device: per-case (MSE, HD) terms [ncases][2] fp64 on the device from
+        device marginals (the plan's output layout) and a case-major device golden table."""
+        lib.fbn_jt_score_terms_device(self._h, d_marg_ptr, d_golden_ptr, ncases, d_terms_ptr, stream_ptr)
 
     def last_kernel_ms(self):
         ms = C.c_float()

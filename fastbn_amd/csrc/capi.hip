@@ -22,7 +22,10 @@
 extern "C" hipError_t fbn_jt_launch(const JtOp *ops, int nops, const int32_t *aux, const double *initv,
                                     const uint64_t *dig, const int8_t *evid, int V, long long ncases, int SD,
                                     double *marg, int32_t *labels, double *ws, int32_t *wsi, long long NE, int nc,
-                                    int grid, hipStream_t stream);
+                                    int grid, int vmajor, hipStream_t stream);
+extern "C" hipError_t fbn_jt_marg_transpose(const double *in, double *out, long long n, int SD, hipStream_t s);
+extern "C" hipError_t fbn_jt_score_terms(const double *marg, const double *golden, long long n, int SD, int vmajor,
+                                         const int32_t *dom, int V, double *terms, hipStream_t s);
 extern "C" hipError_t fbn_ci_launch(const uint8_t *cols, const int32_t *dims, const int32_t *items, long long N,
                                     long long n, int d, double alpha, double *g2, int32_t *df, double *p,
                                     uint8_t *indep, int32_t *counts, size_t lds_bytes, int grid,
@@ -65,10 +68,14 @@ extern "C" hipError_t fbn_ci_l1_results(const uint8_t *st, const int32_t *sep, c
                                         long long *part, hipStream_t s);
 extern "C" hipError_t fbn_ci_kept_csr(const uint8_t *indep, int n, int32_t *low, int32_t *up, int32_t *off,
                                       int32_t *upoff, int32_t *adj, int32_t *pairs, long long *scal, hipStream_t s);
+extern "C" hipError_t fbn_ci_pair_mi(const int32_t *pairtab, const int32_t *dims, int nv, long long P, double *mi,
+                                     hipStream_t s);
 extern "C" hipError_t fbn_ci_l1_setup(const int32_t *pairs, int E, const int32_t *adj, const int32_t *adj_off,
                                       void *ed, int32_t *pos, uint8_t *st, int32_t *sep, long long *counted,
                                       int chunk0, int32_t *len, int32_t *off, unsigned *ring,
                                       unsigned long long *sstat, long long cap, long long *scal, int num_cu,
+                                      const double *mi, const int32_t *dims, const double *band, int nband, int nv,
+                                      double two_n, int32_t *plist, unsigned long long *sstat2, long long *scal2,
                                       hipStream_t s);
 extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims, const int32_t *row0, long long W,
                                       const int32_t *adj, const int32_t *pairtab, int nvars, void *edv, int32_t *pos,
@@ -77,7 +84,7 @@ extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims,
                                       int32_t *df, uint8_t *indep, double alpha, unsigned long long *stats,
                                       const double *band, int nband, unsigned *open_cnt, int num_cu,
                                       unsigned *open_next, int next_chunk, unsigned long long *sstat, unsigned epoch,
-                                      hipStream_t s);
+                                      const int32_t *plist, hipStream_t s);
 extern "C" hipError_t fbn_ci_gram(const uint32_t *bits, long long W, const int32_t *rl, const int32_t *tasks,
                                   long long ntasks, int masked, int32_t *out, int num_cu, hipStream_t s);
 extern "C" hipError_t fbn_ci_gram_pairs(const int32_t *G, long long ld, const int32_t *lead0, const int32_t *dims,
@@ -107,7 +114,8 @@ extern "C" hipError_t fbn_jt_lds_launch(const JtOp *ops, int nops, const int32_t
                                         double *marg, int32_t *labels, double *ws, int32_t *wsi, long long wave_entries,
                                         long long store_off, long long den_off, long long sep_off,
                                         long long spill_off, int nc, int cap, bool spill, int force_exact,
-                                        const int *flags, int grid, unsigned long long *prof, hipStream_t stream);
+                                        const int *flags, int grid, unsigned long long *prof, int vmajor,
+                                        hipStream_t stream);
 
 namespace fbn {
 const char *LastError();
@@ -188,7 +196,7 @@ struct fbn_jt_plan {
         hipFunction_t fn = nullptr;
         int64_t we = 0, lds = 0;
         DevBuf iv;
-    } gen[2];
+    } gen[4];  // [fast + 2 * variable-major output]
     int64_t last_nblk = 0;  // 64-case blocks of the last run (flags of variants 3-5)
     DevBuf flags, ws_fix;
     bool force_fixup = false;
@@ -201,6 +209,10 @@ struct fbn_jt_plan {
     bool prof_on = false;
     int last_grid = 0;
     DevBuf evid, labels, marg, ws;
+    // fbn_jt_set_output_layout: 1 = d_marginals variable-major [SD][ncases]; kernels without a
+    // variable-major store path (4, 5) write case-major into mtmp, transposed into place after
+    int out_layout = 0;
+    DevBuf mtmp;
     DevBuf ddom, evcheck;  // device-side evidence range check (fbn_jt_run, fbn_jt_run_device)
     bool ev_check = true;  // fbn_jt_set_evidence_check
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -277,6 +289,9 @@ struct fbn_ci_ctx {
     // counts (pinned mirror), round events
     DevBuf l1pairs, l1adj, l1adjoff, l1ed, l1pos, l1st, l1sep, l1cnt, l1len, l1off, l1scal, l1open;
     DevBuf l1items, l1counts, l1df, l1indep, l1sstat;  // l1sstat: the offset scan's per-tile status words
+    // the level-1 information screen (ci_bits.hip): pairwise I of the complete graph, the kept
+    // candidates' positions, the screen's scan status words
+    DevBuf l1mi, l1plist, l1sstat2;
     DevBuf keptidx, kepttmp;  // level-0 kept pair indices (CiAllPairsKept)
     // level 0 -> level 1 on the device (CiL0L1Device): per-variable kept counts, upper-part offsets,
     // (E, candidate sets); the side stream copies the flags / edge list to the host meanwhile
@@ -788,16 +803,16 @@ int fbn_jt_set_variant(fbn_jt_plan *p, int variant) {
 
 // the plan-specialized kernel of the current arithmetic order, loaded (cache) or compiled (hiprtc)
 // once per plan and order; both orders stay loaded
-static fbn_jt_plan::GenKernel &GenCur(fbn_jt_plan *p) { return p->gen[JtFast(p) ? 1 : 0]; }
-static int GenEnsure(fbn_jt_plan *p) {
+static fbn_jt_plan::GenKernel &GenCur(fbn_jt_plan *p, bool vm) { return p->gen[(JtFast(p) ? 1 : 0) + (vm ? 2 : 0)]; }
+static int GenEnsure(fbn_jt_plan *p, bool vm) {
     const bool fast = JtFast(p);
-    auto &k = GenCur(p);
+    auto &k = GenCur(p, vm);
     if (k.state == 1) return FBN_OK;
     if (k.state == -1) return FBN_ERR_HIP;
     k.state = -1;
     std::string src;
     std::vector<double> iv;
-    int rc = fbn::GenerateJTKernel(p->host, src, &k.we, iv, &k.lds, fast);
+    int rc = fbn::GenerateJTKernel(p->host, src, &k.we, iv, &k.lds, fast, vm);
     if (rc) return rc;
     std::vector<char> code;
     if ((rc = fbn::JitCodeObject(src, code))) return rc;
@@ -831,7 +846,7 @@ int fbn_jt_kernel_source(const fbn_jt_plan *p, char *buf, int64_t cap, int64_t *
     std::string src;
     std::vector<double> iv;
     int64_t we = 0;
-    int rc = fbn::GenerateJTKernel(p->host, src, &we, iv, nullptr, JtFast(p));
+    int rc = fbn::GenerateJTKernel(p->host, src, &we, iv, nullptr, JtFast(p), p->out_layout == 1);
     if (rc) return rc;
     if (len) *len = (int64_t)src.size() + 1;
     if (buf && cap > 0) {
@@ -848,7 +863,7 @@ int fbn_jt_kernel_cache_path(const fbn_jt_plan *p, char *buf, int64_t cap) {
     std::string src;
     std::vector<double> iv;
     int64_t we = 0;
-    int rc = fbn::GenerateJTKernel(p->host, src, &we, iv, nullptr, JtFast(p));
+    int rc = fbn::GenerateJTKernel(p->host, src, &we, iv, nullptr, JtFast(p), p->out_layout == 1);
     if (rc) return rc;
     snprintf(buf, (size_t)cap, "%s", fbn::JitCachePath(src).c_str());
     return FBN_OK;
@@ -883,7 +898,7 @@ int fbn_jt_kernel_build(const fbn_jt_plan *p) {
     std::string src;
     std::vector<double> iv;
     int64_t we = 0;
-    int rc = fbn::GenerateJTKernel(p->host, src, &we, iv, nullptr, JtFast(p));
+    int rc = fbn::GenerateJTKernel(p->host, src, &we, iv, nullptr, JtFast(p), p->out_layout == 1);
     if (rc) return rc;
     std::vector<char> code;
     return fbn::JitCodeObject(src, code);
@@ -911,7 +926,7 @@ static void LdsGeometry(const fbn_jt_plan *p, int *waves, int *cap) {
 
 // LDS interpreter launch (variants 0/2, and the exact fixup of variant 3 when flags != NULL)
 static int LaunchLds(fbn_jt_plan *p, DevBuf &ws, const int8_t *d_evidence, int64_t ncases, int32_t *labels,
-                     double *marg, const int *flags, bool force_exact, hipStream_t s) {
+                     double *marg, const int *flags, bool force_exact, hipStream_t s, bool vm = false) {
     const auto &l = p->lprog;
     const int V = p->host.num_nodes, SD = l.sum_dom, nc = l.num_cliques;
     const int64_t nblk = (ncases + 63) / 64;
@@ -940,7 +955,7 @@ static int LaunchLds(fbn_jt_plan *p, DevBuf &ws, const int8_t *d_evidence, int64
                                      p->linitv.as<double>(), p->ldig.as<uint64_t>(), d_evidence, V, ncases, SD, marg,
                                      labels, ws.as<double>(), reinterpret_cast<int32_t *>(ws.as<char>() + ws_d),
                                      wave_entries, store_off, den_off, sep_off, spill_off, nc, cap, spill, force_exact,
-                                     flags, grid, prof ? p->prof.as<unsigned long long>() : nullptr, s);
+                                     flags, grid, prof ? p->prof.as<unsigned long long>() : nullptr, vm ? 1 : 0, s);
     if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt kernel launch: %s", hipGetErrorString(e));
     return FBN_OK;
 }
@@ -993,7 +1008,7 @@ int fbn_jt_set_evidence_check(fbn_jt_plan *p, int enable) {
 }
 
 static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, int32_t *d_labels,
-                       double *d_marginals, hipStream_t s, bool check);
+                       double *d_marginals, hipStream_t s, bool check, bool vm);
 
 int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, int32_t *d_labels,
                       double *d_marginals, void *hip_stream) {
@@ -1003,11 +1018,11 @@ int fbn_jt_run_device(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, 
     FBN_HIP(hipSetDevice(p->device));
     p->note_stream(static_cast<hipStream_t>(hip_stream));
     return JtRunDevice(p, d_evidence, ncases, d_labels, d_marginals, static_cast<hipStream_t>(hip_stream),
-                       p->ev_check);
+                       p->ev_check, p->out_layout == 1 && d_marginals);
 }
 
 static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases, int32_t *d_labels,
-                       double *d_marginals, hipStream_t s, bool check) {
+                       double *d_marginals, hipStream_t s, bool check, bool vm) {
     if (check)
         if (int rc = JtCheckEvidence(p, d_evidence, ncases, s)) return rc;
     const auto &g = p->prog;
@@ -1028,13 +1043,22 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
     if (variant == -1) {
         // specialized kernel when eligible; else the streamed kernel (1.5-2x the interpreters on
         // ALARM and the Munin-like network); the interpreters only for plans it cannot take
-        if (p->gen_eligible && GenEnsure(p) == FBN_OK) variant = 3;
+        if (p->gen_eligible && GenEnsure(p, vm) == FBN_OK) variant = 3;
         else if (p->t_ok && JtFast(p)) variant = 5;  // (fast arithmetic order only)
         else if (p->v_ok) variant = 4;
         else variant = (p->lprog.max_table * 64 * 8 * 2 <= (int64_t)kLdsBytes) ? 0 : 1;
     }
-    else if (variant == 3 && (rc = GenEnsure(p))) return rc;
+    else if (variant == 3 && (rc = GenEnsure(p, vm))) return rc;
     p->last_variant = variant;
+    // variable-major output: kernels 0-3 store it directly; 4 and 5 write case-major scratch that is
+    // transposed into the caller's buffer at the end (same values)
+    double *const marg_out = marg;
+    const bool vm_scratch = vm && (variant == 4 || variant == 5);
+    if (vm_scratch) {
+        if ((rc = p->mtmp.ensure((size_t)ncases * SD * 8))) return rc;
+        marg = p->mtmp.as<double>();
+    }
+    const bool vm_direct = vm && !vm_scratch;
     p->last_nblk = variant >= 3 ? nblk : 0;
 
     if (variant == 1) {
@@ -1055,7 +1079,7 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
         hipError_t e = fbn_jt_launch(p->ops.as<JtOp>(), (int)g.ops.size(), p->aux.as<int32_t>(), p->initv.as<double>(),
                                      p->dig.as<uint64_t>(), d_evidence, V, ncases, SD, marg, labels,
                                      p->ws.as<double>(), reinterpret_cast<int32_t *>(p->ws.as<char>() + ws_d),
-                                     g.state_entries, nc, grid, s);
+                                     g.state_entries, nc, grid, vm_direct ? 1 : 0, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt kernel launch: %s", hipGetErrorString(e));
     } else if (variant == 4) {
         // streamed tables: small register footprint, many resident waves; the per-wave store holds
@@ -1127,7 +1151,7 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
             return rc;
     } else if (variant == 3) {
         // one wave (64 cases) per SIMD: the clique in flight occupies the register file (+ LDS tail)
-        const auto &gk = GenCur(p);
+        const auto &gk = GenCur(p, vm);
         int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 4;
         if (gk.lds > 0) wpc = std::max<int>(1, std::min<int64_t>(wpc, (int64_t)kLdsBytes / gk.lds));
         const int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * wpc);
@@ -1154,11 +1178,15 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
         // exact recomputation of the blocks whose denominators left the fast-division range
         // (FBN_JT_NO_FIXUP: diagnostic only, as above)
         static const bool no_fix3 = getenv("FBN_JT_NO_FIXUP") != nullptr;
-        if (!no_fix3 && (rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s)))
+        if (!no_fix3 && (rc = LaunchLds(p, p->ws_fix, d_evidence, ncases, labels, marg, p->flags.as<int>(), false, s, vm_direct)))
             return rc;
     } else {
         if (p->ktiming) FBN_HIP(hipEventRecord(p->ev0, s));
-        if ((rc = LaunchLds(p, p->ws, d_evidence, ncases, labels, marg, nullptr, variant == 2, s))) return rc;
+        if ((rc = LaunchLds(p, p->ws, d_evidence, ncases, labels, marg, nullptr, variant == 2, s, vm_direct))) return rc;
+    }
+    if (vm_scratch) {
+        hipError_t e = fbn_jt_marg_transpose(marg, marg_out, ncases, SD, s);
+        if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt marginal transpose: %s", hipGetErrorString(e));
     }
     if (p->ktiming) FBN_HIP(hipEventRecord(p->ev1, s));
     p->timed = p->ktiming;
@@ -1179,7 +1207,7 @@ int fbn_jt_run(fbn_jt_plan *p, const int8_t *evidence, int64_t ncases, int32_t *
     if ((rc = p->labels.ensure((size_t)ncases * 4))) return rc;
     if ((rc = p->marg.ensure((size_t)ncases * SD * 8))) return rc;
     FBN_HIP(hipMemcpyAsync(p->evid.p, evidence, (size_t)ncases * V, hipMemcpyHostToDevice, s));
-    rc = JtRunDevice(p, p->evid.as<int8_t>(), ncases, p->labels.as<int32_t>(), p->marg.as<double>(), s, true);
+    rc = JtRunDevice(p, p->evid.as<int8_t>(), ncases, p->labels.as<int32_t>(), p->marg.as<double>(), s, true, false);
     if (rc) return rc;
     FBN_HIP(hipMemcpyAsync(labels_out, p->labels.p, (size_t)ncases * 4, hipMemcpyDeviceToHost, s));
     if (marginals_out)
@@ -1222,6 +1250,35 @@ int fbn_jt_score(const fbn_jt_plan *p, const double *marginals, const double *go
     }
     *mse_sum = mse;
     *hd_sum = hd;
+    return FBN_OK;
+}
+
+int fbn_jt_set_output_layout(fbn_jt_plan *p, int layout) {
+    if (!p || layout < 0 || layout > 1)
+        return SetError(FBN_ERR_ARG, "layout must be 0 (case-major) or 1 (variable-major)");
+    p->out_layout = layout;
+    return FBN_OK;
+}
+
+int fbn_jt_score_terms_device(fbn_jt_plan *p, const double *d_marginals, const double *d_golden, int64_t ncases,
+                              double *d_terms, void *hip_stream) {
+    if (!p || ncases < 0 || (ncases > 0 && (!d_marginals || !d_golden || !d_terms)))
+        return SetError(FBN_ERR_ARG, "bad argument");
+    if (ncases == 0) return FBN_OK;
+    if (p->device < 0) return SetError(FBN_ERR_NODEV, "host-only plan (created with device < 0)");
+    FBN_HIP(hipSetDevice(p->device));
+    const int V = p->host.num_nodes;
+    int rc;
+    if (!p->ddom.p) {
+        if ((rc = p->ddom.ensure((size_t)V * 4))) return rc;
+        if ((rc = p->evcheck.ensure(8))) return rc;
+        FBN_HIP(hipMemcpy(p->ddom.p, p->host.dom.data(), (size_t)V * 4, hipMemcpyHostToDevice));
+    }
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    p->note_stream(s);
+    hipError_t e = fbn_jt_score_terms(d_marginals, d_golden, ncases, p->prog.sum_dom, p->out_layout == 1 ? 1 : 0,
+                                      p->ddom.as<int32_t>(), V, d_terms, s);
+    if (e != hipSuccess) return SetError(FBN_ERR_HIP, "jt score terms: %s", hipGetErrorString(e));
     return FBN_OK;
 }
 
@@ -2456,13 +2513,12 @@ int CiLevel1Run(fbn_ci_ctx *c, double alpha, int E, int64_t cands, LevelOut &out
     FBN_HIP(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     int rc;
-    (void)nv;
     const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(cands, EnvOr0("FBN_PC_L1CAP", 1 << 19)));
     if ((rc = c->l1ed.ensure((size_t)E * fbn_ci_l1_edge_bytes())) ||
         (rc = c->l1pos.ensure((size_t)E * 4)) || (rc = c->l1st.ensure((size_t)E)) ||
         (rc = c->l1sep.ensure((size_t)E * 4)) || (rc = c->l1cnt.ensure((size_t)E * 8)) ||
         (rc = c->l1len.ensure((size_t)E * 4)) || (rc = c->l1off.ensure((size_t)E * 4)) ||
-        (rc = c->l1scal.ensure(48)) || (rc = c->l1open.ensure(kL1Ring * 4)) ||
+        (rc = c->l1scal.ensure(96)) || (rc = c->l1open.ensure(kL1Ring * 4)) ||
         (rc = c->l1sstat.ensure((size_t)((E + 255) / 256) * 8)) ||
         (rc = c->l1items.ensure((size_t)cap * 12)) || (rc = c->l1counts.ensure((size_t)cap * 256)) ||
         (rc = c->l1df.ensure((size_t)cap * 4)) || (rc = c->l1indep.ensure((size_t)cap)))
@@ -2475,9 +2531,24 @@ int CiLevel1Run(fbn_ci_ctx *c, double alpha, int E, int64_t cands, LevelOut &out
     const double *band = nullptr;
     int nband = 0;
     if ((rc = CiBand(c, alpha, s, &band, &nband))) return rc;
-    // scalars (total, launched, rows read, scan flag, tickets) and the tile scan's status words (epoch 0)
-    FBN_HIP(hipMemsetAsync(c->l1scal.p, 0, 48, s));
+    // scalars (total, launched, rows read, scan flag, tickets; the screen's scan at + 8) and the tile
+    // scan's status words (epoch 0)
+    FBN_HIP(hipMemsetAsync(c->l1scal.p, 0, 96, s));
     FBN_HIP(hipMemsetAsync(c->l1sstat.p, 0, (size_t)((E + 255) / 256) * 8, s));
+    // the information screen (exact; FBN_PC_NO_MISCREEN=1: every candidate runs): needs the band (a
+    // decision threshold per df) and the level-0 pair tables of the complete graph
+    const double *mi = nullptr;
+    if (band && !getenv("FBN_PC_NO_MISCREEN")) {
+        const long long P = (long long)nv * (nv - 1) / 2;
+        if ((rc = c->l1mi.ensure((size_t)std::max<long long>(P, 1) * 8)) ||
+            (rc = c->l1plist.ensure((size_t)std::max<int64_t>(cands, 1) * 4)) ||
+            (rc = c->l1sstat2.ensure((size_t)((E + 255) / 256) * 8)))
+            return rc;
+        FBN_HIP(hipMemsetAsync(c->l1sstat2.p, 0, (size_t)((E + 255) / 256) * 8, s));
+        hipError_t e = fbn_ci_pair_mi(c->pairtab.as<int32_t>(), c->ddims.as<int32_t>(), nv, P, c->l1mi.as<double>(), s);
+        if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci pair information: %s", hipGetErrorString(e));
+        mi = c->l1mi.as<double>();
+    }
     CiSlot &S = c->slot[0];
     if (c->timing) FBN_HIP(hipEventRecord(S.ev0, s));
     long long *scal = c->l1scal.as<long long>();  // total, launched, rows read, scan flag, tickets
@@ -2495,7 +2566,9 @@ int CiLevel1Run(fbn_ci_ctx *c, double alpha, int E, int64_t cands, LevelOut &out
     hipError_t e = fbn_ci_l1_setup(c->l1pairs.as<int32_t>(), E, c->l1adj.as<int32_t>(), c->l1adjoff.as<int32_t>(),
                                    c->l1ed.p, c->l1pos.as<int32_t>(), c->l1st.as<uint8_t>(), c->l1sep.as<int32_t>(),
                                    c->l1cnt.as<long long>(), (int)chunk, c->l1len.as<int32_t>(),
-                                   c->l1off.as<int32_t>(), c->l1open.as<unsigned>(), sstat, cap, scal, c->num_cu, s);
+                                   c->l1off.as<int32_t>(), c->l1open.as<unsigned>(), sstat, cap, scal, c->num_cu, mi,
+                                   c->ddims.as<int32_t>(), band, nband, nv, 2.0 * (double)c->N, c->l1plist.as<int32_t>(),
+                                   c->l1sstat2.as<unsigned long long>(), scal + 8, s);
     if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci level-1 setup: %s", hipGetErrorString(e));
     static const bool l1timing = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic
     const auto tl0 = std::chrono::steady_clock::now();
@@ -2510,7 +2583,8 @@ int CiLevel1Run(fbn_ci_ctx *c, double alpha, int E, int64_t cands, LevelOut &out
                             c->l1len.as<int32_t>(), c->l1off.as<int32_t>(), E, cap, scal, c->l1items.as<int32_t>(),
                             c->l1counts.as<int32_t>(), c->l1df.as<int32_t>(), c->l1indep.as<uint8_t>(), alpha,
                             c->stats.as<unsigned long long>(), band, nband, open_r, c->num_cu,
-                            c->l1open.as<unsigned>() + ((r + 1) & 1), (int)next_chunk, sstat, (unsigned)(r + 2), s);
+                            c->l1open.as<unsigned>() + ((r + 1) & 1), (int)next_chunk, sstat, (unsigned)(r + 2),
+                            mi ? c->l1plist.as<int32_t>() : nullptr, s);
         if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci level-1 round: %s", hipGetErrorString(e));
         FBN_HIP(hipMemcpyAsync(c->h_open + (r & 1), open_r, 4, hipMemcpyDeviceToHost, s));
         FBN_HIP(hipEventRecord(c->l1ev[r & 1], s));

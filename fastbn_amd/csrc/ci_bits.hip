@@ -1054,7 +1054,60 @@ __global__ __launch_bounds__(256) void ci_bits_g2q(const int32_t *__restrict__ c
 // host only enqueues rounds; nothing per test crosses PCIe.
 struct L1Edge {
     int32_t x, y, m0, L, skx, sky, ax, ay;  // ax / ay: adjacency offsets, skx / sky: position of y / x
+    // the candidates the information screen keeps (below): P of them, positions plist[pl .. pl + P)
+    // (pl = -1: no screen, every candidate k = its own position)
+    int32_t P, pl;
 };
+
+// ---- the information screen of level 1 (exact: it only skips tests whose answer is known)
+// With empirical (plug-in) mutual information I over the same N samples, the chain rule holds
+// exactly: I(X;Y) + I(X;Z|Y) = I(X;Z) + I(X;Y|Z), so I(X;Y) <= I(X;Z) + I(X;Y|Z) (and likewise for
+// Y).  G^2 of a test is 2N I(X;Y|Z) (src/IndependenceTest.cpp:94-138: the sum of 2 O log(O / E)),
+// and "independent" needs G^2 <= hi(df), the upper end of the decision band for its df (df <=
+// (dx-1)(dy-1)dz; hi grows with df).  Hence a candidate z with
+//     I(X;Z) < I(X;Y) - tau   or   I(Y;Z) < I(X;Y) - tau,   tau = hi((dx-1)(dy-1)dz) / 2N (+ margins)
+// can never be the independent one: its test is dependent whatever its counts.  Level 1 runs only
+// the other candidates; counted tests stay the reference's (every candidate up to the first
+// independent one, src/PCStable.cpp:465-551), launched tests are the ones run.  The pairwise I come
+// from the level-0 pair tables.  (The margins, 1e-9 relative on hi and 1e-9 absolute in nats, are
+// orders above the rounding of either side: a few 1e-16 relative on values <= log 4.)
+__device__ __forceinline__ long long l1_pidx(int u, int v, int nv) {
+    const int i = u < v ? u : v, j = u < v ? v : u;
+    return (long long)i * nv - (long long)i * (i + 1) / 2 + (j - i - 1);
+}
+__device__ __forceinline__ bool l1_plausible(const double *__restrict__ mi, int nv, const int32_t *__restrict__ dims,
+                                             const double *__restrict__ band, int nband, double two_n, int x, int y,
+                                             int z, double mxy) {
+    const int df = (dims[x] - 1) * (dims[y] - 1) * dims[z];
+    if (df <= 0 || df > nband) return true;
+    const double lim = mxy - (band[2 * df - 1] * (1.0 + 1e-9) / two_n + 1e-9);
+    if (lim <= 0.0) return true;
+    return mi[l1_pidx(x, z, nv)] >= lim && mi[l1_pidx(y, z, nv)] >= lim;
+}
+// I(X;Y) in nats of every pair of the complete graph from its level-0 table (pairtab, 16 counts:
+// N[a][b] at a * dy + b for the pair's x < y), one thread per pair
+__global__ __launch_bounds__(256) void ci_pair_mi(const int32_t *__restrict__ pairtab, const int32_t *__restrict__ dims,
+                                                  int nv, long long P, double *__restrict__ mi) {
+    for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t < P; t += (long long)gridDim.x * 256) {
+        int x, y;
+        pair_of(t, nv, x, y);
+        const int dx = dims[x], dy = dims[y];
+        const int32_t *T = pairtab + 16 * t;
+        double r[4] = {0, 0, 0, 0}, c[4] = {0, 0, 0, 0}, n = 0.0;
+        for (int a = 0; a < dx; ++a)
+            for (int b = 0; b < dy; ++b) {
+                const double v = T[a * dy + b];
+                r[a] += v, c[b] += v, n += v;
+            }
+        double acc = 0.0;
+        for (int a = 0; a < dx; ++a)
+            for (int b = 0; b < dy; ++b) {
+                const double v = T[a * dy + b];
+                if (v > 0.0) acc += v * log(v * n / (r[a] * c[b]));
+            }
+        mi[t] = n > 0.0 ? acc / n : 0.0;
+    }
+}
 
 // The rounds' test offsets: a single-pass exclusive scan of the edges' lengths inside the kernel
 // that computes them (ci_l1_setup for round 0, ci_l1_resolve for the next round), 256-edge tiles
@@ -1146,8 +1199,13 @@ __device__ __forceinline__ int32_t l1_tile_scan(int tile, int ntiles, int32_t &l
     return (int32_t)run;
 }
 
+// candidate k of an edge: adj(x)\{y} then adj(y)\{x}, each ascending
+__device__ __forceinline__ int l1_cand(const L1Edge &g, const int32_t *__restrict__ adj, int k) {
+    return k < g.m0 ? adj[g.ax + k + (k >= g.skx)] : adj[g.ay + (k - g.m0) + ((k - g.m0) >= g.sky)];
+}
+
 // (also the first round's lengths, chunk0 candidates per edge, and their offsets; both open-count
-// ring slots zeroed)
+// ring slots zeroed; with `mi`, the information screen's candidate lists first)
 __global__ __launch_bounds__(256) void ci_l1_setup(const int32_t *__restrict__ pairs, int E,
                                                    const int32_t *__restrict__ adj,
                                                    const int32_t *__restrict__ adj_off, L1Edge *__restrict__ ed,
@@ -1155,7 +1213,11 @@ __global__ __launch_bounds__(256) void ci_l1_setup(const int32_t *__restrict__ p
                                                    int32_t *__restrict__ sep, long long *__restrict__ counted,
                                                    int chunk0, int32_t *__restrict__ len, int32_t *__restrict__ off,
                                                    unsigned *__restrict__ ring, unsigned long long *__restrict__ sstat,
-                                                   long long cap, long long *__restrict__ scal) {
+                                                   long long cap, long long *__restrict__ scal,
+                                                   const double *__restrict__ mi, const int32_t *__restrict__ dims,
+                                                   const double *__restrict__ band, int nband, int nv, double two_n,
+                                                   int32_t *__restrict__ plist, unsigned long long *__restrict__ sstat2,
+                                                   long long *__restrict__ scal2) {
     constexpr unsigned epoch = 1;
     unsigned *tickets = reinterpret_cast<unsigned *>(scal + 4);
     if (blockIdx.x == 0 && threadIdx.x < 2) ring[threadIdx.x] = 0u;
@@ -1166,18 +1228,39 @@ __global__ __launch_bounds__(256) void ci_l1_setup(const int32_t *__restrict__ p
         if (tile >= ntiles) break;
         const int e = tile * 256 + threadIdx.x;
         int32_t l = 0;
+        L1Edge g{};
+        double mxy = 0.0;
         if (e < E) {
             const int x = pairs[2 * e], y = pairs[2 * e + 1];
             const int ax = adj_off[x], nx = adj_off[x + 1] - ax, ay = adj_off[y], ny = adj_off[y + 1] - ay;
             int skx = find_sorted(adj + ax, nx, y), sky = find_sorted(adj + ay, ny, x);
             const int m0 = skx >= 0 ? nx - 1 : nx, m1 = sky >= 0 ? ny - 1 : ny;
             skx = skx >= 0 ? skx : nx + 1, sky = sky >= 0 ? sky : ny + 1;
-            ed[e] = L1Edge{x, y, m0, m0 + m1, skx, sky, ax, ay};
+            g = L1Edge{x, y, m0, m0 + m1, skx, sky, ax, ay, m0 + m1, -1};
+            if (mi) {  // the screen: count the candidates it keeps
+                mxy = mi[l1_pidx(x, y, nv)];
+                g.P = 0;
+                for (int k = 0; k < g.L; ++k) g.P += l1_plausible(mi, nv, dims, band, nband, two_n, x, y, l1_cand(g, adj, k), mxy);
+            }
+        }
+        if (mi) {  // their positions: plist[pl .. pl + P) in candidate order
+            int32_t pcount = e < E ? g.P : 0;
+            const int32_t pl = l1_tile_scan(tile, ntiles, pcount, sstat2, epoch, 1ll << 62, scal2);
+            if (e < E) {
+                g.pl = pl;
+                int q = pl;
+                for (int k = 0; k < g.L; ++k)
+                    if (l1_plausible(mi, nv, dims, band, nband, two_n, g.x, g.y, l1_cand(g, adj, k), mxy)) plist[q++] = k;
+            }
+        }
+        if (e < E) {
+            ed[e] = g;
             pos[e] = 0;
-            st[e] = m0 + m1 == 0 ? 2 : 0;  // no candidate on either side: kept
+            // no candidate left to run: kept, every candidate counted (a dependent test each)
+            st[e] = g.P == 0 ? 2 : 0;
             sep[e] = -1;
-            counted[e] = 0;
-            l = m0 + m1 == 0 ? 0 : (m0 + m1 < chunk0 ? m0 + m1 : chunk0);
+            counted[e] = g.P == 0 ? g.L : 0;
+            l = g.P < chunk0 ? g.P : chunk0;
         }
         const int32_t o = l1_tile_scan(tile, ntiles, l, sstat, epoch, cap, scal);
         if (e < E) len[e] = l, off[e] = o;
@@ -1191,7 +1274,8 @@ __global__ __launch_bounds__(256) void ci_l1_gen(const L1Edge *__restrict__ ed, 
                                                  const long long *__restrict__ total,
                                                  const int32_t *__restrict__ adj, int32_t *__restrict__ items,
                                                  const int32_t *__restrict__ dims,
-                                                 unsigned long long *__restrict__ rows_read) {
+                                                 unsigned long long *__restrict__ rows_read,
+                                                 const int32_t *__restrict__ plist) {
     const long long n = *total;
     // wave-uniform trip count (the row tally below is reduced per wave)
     for (long long wb = (long long)blockIdx.x * 256 + (threadIdx.x & ~63); wb < n; wb += (long long)gridDim.x * 256) {
@@ -1205,10 +1289,8 @@ __global__ __launch_bounds__(256) void ci_l1_gen(const L1Edge *__restrict__ ed, 
             else hi = mid;
         }
         const L1Edge g = ed[lo];
-        const int k = pos[lo] + (int)(t - off[lo]);
-        int z;
-        if (k < g.m0) z = adj[g.ax + k + (k >= g.skx)];
-        else z = adj[g.ay + (k - g.m0) + ((k - g.m0) >= g.sky)];
+        const int j = pos[lo] + (int)(t - off[lo]);
+        const int z = l1_cand(g, adj, g.pl < 0 ? j : plist[g.pl + j]);
         items[3 * t] = g.x, items[3 * t + 1] = g.y, items[3 * t + 2] = z;
         rows = dims[g.x] + dims[g.y] + dims[z] - 3;  // mask rows the derived count reads
         }
@@ -1225,7 +1307,8 @@ __global__ __launch_bounds__(256) void ci_l1_resolve(const L1Edge *__restrict__ 
                                                      const int32_t *__restrict__ items, int E,
                                                      unsigned *__restrict__ open_cnt, unsigned *__restrict__ open_next,
                                                      int next_chunk, unsigned long long *__restrict__ sstat,
-                                                     unsigned epoch, long long cap, long long *__restrict__ scal) {
+                                                     unsigned epoch, long long cap, long long *__restrict__ scal,
+                                                     const int32_t *__restrict__ plist) {
     unsigned *tickets = reinterpret_cast<unsigned *>(scal + 4);
     // the next round's open-count slot (its previous value went to the host before this round) and
     // the next kernel's ticket counter
@@ -1244,21 +1327,22 @@ __global__ __launch_bounds__(256) void ci_l1_resolve(const L1Edge *__restrict__ 
                     found = i;
                     break;
                 }
-            if (found >= 0) {
+            const L1Edge g = ed[e];
+            if (found >= 0) {  // counted: every candidate up to its position (the screened-out ones dependent)
                 st[e] = 1;
                 sep[e] = items[3 * (o + found) + 2];
-                counted[e] += found + 1;
+                const int j = pos[e] + found;
+                counted[e] = (g.pl < 0 ? j : plist[g.pl + j]) + 1;
             } else {
-                counted[e] += n;
                 pos[e] += n;
-                if (pos[e] >= ed[e].L) st[e] = 2;
+                if (pos[e] >= g.P) st[e] = 2, counted[e] = g.L;
                 else open = true;
             }
         }
         // the next round's length of this edge and, through the tile scan, its offset
         int32_t l = 0;
         if (e < E && open) {
-            const int left = ed[e].L - pos[e];
+            const int left = ed[e].P - pos[e];
             l = left < next_chunk ? left : next_chunk;
         }
         const int32_t o = l1_tile_scan(tile, ntiles, l, sstat, epoch, cap, scal);
@@ -1446,7 +1530,8 @@ __global__ __launch_bounds__(64) void ci_l1_results_tail(const long long *__rest
     long long acc = 0;
     for (int i = threadIdx.x; i < nparts; i += 64) acc += part[i];
     for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
-    if (threadIdx.x == 0) h_sc[0] = acc, h_sc[1] = scal[1], h_sc[2] = scal[2], h_sc[3] = scal[3];
+    // (scal[11]: the information screen's scan flag, ci_l1_setup's second scan at scal + 8)
+    if (threadIdx.x == 0) h_sc[0] = acc, h_sc[1] = scal[1], h_sc[2] = scal[2], h_sc[3] = scal[3] | scal[11];
 }
 // h_sc: 4 long longs (counted, launched, rows read, scan flag); part: >= 256 long longs of scratch
 extern "C" hipError_t fbn_ci_l1_results(const uint8_t *st, const int32_t *sep, const long long *cnt, int E,
@@ -1468,15 +1553,29 @@ extern "C" hipError_t fbn_ci_kept_csr(const uint8_t *indep, int n, int32_t *low,
     return hipGetLastError();
 }
 
+// mi != nullptr: the information screen (pairwise I of the complete graph over nv variables, band
+// for the level's alpha, two_n = 2N, plist >= the level's candidate sets, sstat2 / scal2 a second
+// tile-status array (>= tiles) and 6 long longs of scratch)
 extern "C" hipError_t fbn_ci_l1_setup(const int32_t *pairs, int E, const int32_t *adj, const int32_t *adj_off,
                                       void *ed, int32_t *pos, uint8_t *st, int32_t *sep, long long *counted,
                                       int chunk0, int32_t *len, int32_t *off, unsigned *ring,
                                       unsigned long long *sstat, long long cap, long long *scal, int num_cu,
+                                      const double *mi, const int32_t *dims, const double *band, int nband, int nv,
+                                      double two_n, int32_t *plist, unsigned long long *sstat2, long long *scal2,
                                       hipStream_t s) {
     const int ntiles = (E + 255) / 256;
     if (E > 0)
         hipLaunchKernelGGL(ci_l1_setup, dim3((unsigned)std::min(ntiles, num_cu * 4)), dim3(256), 0, s, pairs, E, adj,
-                           adj_off, (L1Edge *)ed, pos, st, sep, counted, chunk0, len, off, ring, sstat, cap, scal);
+                           adj_off, (L1Edge *)ed, pos, st, sep, counted, chunk0, len, off, ring, sstat, cap, scal, mi,
+                           dims, band, nband, nv, two_n, plist, sstat2, scal2);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t fbn_ci_pair_mi(const int32_t *pairtab, const int32_t *dims, int nv, long long P, double *mi,
+                                     hipStream_t s) {
+    const long long b = (P + 255) / 256;
+    if (P > 0)
+        hipLaunchKernelGGL(ci_pair_mi, dim3((unsigned)(b < 4096 ? b : 4096)), dim3(256), 0, s, pairtab, dims, nv, P, mi);
     return hipGetLastError();
 }
 
@@ -1491,7 +1590,7 @@ extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims,
                                       int32_t *df, uint8_t *indep, double alpha, unsigned long long *stats,
                                       const double *band, int nband, unsigned *open_cnt, int num_cu,
                                       unsigned *open_next, int next_chunk, unsigned long long *sstat, unsigned epoch,
-                                      hipStream_t s) {
+                                      const int32_t *plist, hipStream_t s) {
     const L1Edge *ed = (const L1Edge *)edv;
     const long long gcap = (long long)num_cu * 8;
     const long long gt = (cap + 255) / 256;
@@ -1501,7 +1600,7 @@ extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims,
     const int ntiles = (E + 255) / 256;
     const long long *total = scal;
     unsigned long long *rows_read = reinterpret_cast<unsigned long long *>(scal + 2);
-    hipLaunchKernelGGL(ci_l1_gen, gT, dim3(256), 0, s, ed, pos, off, E, total, adj, items, dims, rows_read);
+    hipLaunchKernelGGL(ci_l1_gen, gT, dim3(256), 0, s, ed, pos, off, E, total, adj, items, dims, rows_read, plist);
     hipLaunchKernelGGL(ci_bits_count_derived, gW, dim3(256), 0, s, bits, dims, row0, (const int32_t *)items, W, cap,
                        counts, pairtab, nvars, 1, total);
     hipLaunchKernelGGL(ci_bits_g2<1>, gT, dim3(256), 0, s, (const int32_t *)counts, dims, (const int32_t *)items, cap,
@@ -1509,7 +1608,7 @@ extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims,
                        band, nband, total);
     hipLaunchKernelGGL(ci_l1_resolve, dim3((unsigned)std::min(ntiles, num_cu * 4)), dim3(256), 0, s, ed, pos, len,
                        off, st, sep, counted, (const uint8_t *)indep, (const int32_t *)items, E, open_cnt, open_next,
-                       next_chunk, sstat, epoch, cap, scal);
+                       next_chunk, sstat, epoch, cap, scal, plist);
     return hipGetLastError();
 }
 

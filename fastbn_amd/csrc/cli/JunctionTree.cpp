@@ -113,12 +113,12 @@ double JunctionTree::EvaluateAccuracy(const std::string &pt_path, int /*num_thre
 
 // Cases sharded over the GPUs: rank r takes cases [r * chunk, (r + 1) * chunk), builds
 // its plan on its device from the parsed network (rank 0 reuses the constructor's), runs its shard
-// from device memory and scores it against its slice of the golden table (fbn_jt_score over the
-// shard's cases in order, CalculateMSE / HD src/Inference.cpp:153-206, plus its correct labels).
-// The marginals never leave their device's shard path: one ncclReduce (sum) of the three per-rank
-// sums {MSE, HD, #correct} to rank 0, one ncclAllGather of the labels (the final gather) and one
-// ncclAllReduce (max) of the kernel times.  MSE / HD add per-shard partial sums (the one-GPU run adds
-// case after case), so they may differ from it in the last bits; accuracy is exact.
+// from device memory and scores it there: its slice of the golden table is uploaded once and
+// fbn_jt_score_terms_device forms every case's (MSE, HD) terms (CalculateMSE / HD,
+// src/Inference.cpp:153-206) from the marginals in place -- no [n][sum_dom] buffer leaves a device.
+// One ncclAllGather of the labels (the final gather), one of the 16-byte per-case terms and one
+// ncclAllReduce (max) of the kernel times; rank 0 then adds the terms and counts the correct labels
+// in case order, so MSE / HD / accuracy equal the one-GPU run bit for bit.
 std::string JunctionTree::RunSharded(const std::vector<double> &golden, float *kernel_ms, double *sums) {
     const int64_t n = tester_->num_instances();
     const int V = info_.num_nodes, SD = info_.sum_dom;
@@ -128,6 +128,7 @@ std::string JunctionTree::RunSharded(const std::vector<double> &golden, float *k
     const int64_t chunk = std::max<int64_t>(1, (n + world - 1) / world);
     float kmax = 0.f;
     std::vector<int32_t> all_labels((size_t)chunk * world, -1);
+    std::vector<double> all_terms((size_t)chunk * world * 2, 0.0);
     std::string err = g.Run([&](int r) -> std::string {
         hipStream_t s = g.stream(r);
         ncclComm_t comm = g.comm(r);
@@ -135,9 +136,10 @@ std::string JunctionTree::RunSharded(const std::vector<double> &golden, float *k
         fbn_jt_plan *plan = plan_;
         if (r > 0 && fbn_jt_plan_create(net_, g.device(r), &plan)) return std::string("fbn_jt_plan_create: ") + fbn_last_error();
         const int64_t c0 = std::min<int64_t>(n, r * chunk), nr = std::min<int64_t>(n, c0 + chunk) - c0;
-        void *d_ev = nullptr, *d_lab = nullptr, *d_all = nullptr, *d_marg = nullptr, *d_k = nullptr, *d_s = nullptr;
+        void *d_ev = nullptr, *d_lab = nullptr, *d_all = nullptr, *d_marg = nullptr, *d_k = nullptr, *d_gold = nullptr,
+             *d_terms = nullptr, *d_tall = nullptr;
         auto cleanup = [&] {
-            for (void *p : {d_ev, d_lab, d_all, d_marg, d_k, d_s})
+            for (void *p : {d_ev, d_lab, d_all, d_marg, d_k, d_gold, d_terms, d_tall})
                 if (p) (void)hipFree(p);
             if (r > 0) fbn_jt_plan_destroy(plan);
         };
@@ -145,58 +147,56 @@ std::string JunctionTree::RunSharded(const std::vector<double> &golden, float *k
             (e = HipErr(hipMalloc(&d_lab, (size_t)chunk * 4), "hipMalloc")).size() ||
             (e = HipErr(hipMalloc(&d_all, (size_t)chunk * 4 * world), "hipMalloc")).size() ||
             (e = HipErr(hipMalloc(&d_marg, (size_t)chunk * SD * 8), "hipMalloc")).size() ||
-            (e = HipErr(hipMalloc(&d_k, 4), "hipMalloc")).size() ||
-            (e = HipErr(hipMalloc(&d_s, 3 * 8), "hipMalloc")).size()) {
+            (e = HipErr(hipMalloc(&d_gold, (size_t)chunk * SD * 8), "hipMalloc")).size() ||
+            (e = HipErr(hipMalloc(&d_terms, (size_t)chunk * 2 * 8), "hipMalloc")).size() ||
+            (e = HipErr(hipMalloc(&d_tall, (size_t)chunk * 2 * 8 * world), "hipMalloc")).size() ||
+            (e = HipErr(hipMalloc(&d_k, 4), "hipMalloc")).size()) {
             cleanup();
             return e;
         }
         (void)hipMemsetAsync(d_lab, 0xFF, (size_t)chunk * 4, s);  // labels past n: -1
+        (void)hipMemsetAsync(d_terms, 0, (size_t)chunk * 2 * 8, s);
         float ms = 0.f;
-        double part[3] = {0, 0, 0};
-        std::vector<int32_t> lab((size_t)std::max<int64_t>(nr, 0));
-        std::vector<double> marg((size_t)std::max<int64_t>(nr, 0) * SD);
         if (nr > 0) {
             (void)hipMemcpyAsync(d_ev, tester_->evidence.data() + (size_t)c0 * V, (size_t)nr * V, hipMemcpyHostToDevice, s);
+            (void)hipMemcpyAsync(d_gold, golden.data() + (size_t)c0 * SD, (size_t)nr * SD * 8, hipMemcpyHostToDevice, s);
             if (fbn_jt_run_device(plan, static_cast<const int8_t *>(d_ev), nr, static_cast<int32_t *>(d_lab),
-                                  static_cast<double *>(d_marg), s)) {
-                e = std::string("fbn_jt_run_device: ") + fbn_last_error();
+                                  static_cast<double *>(d_marg), s) ||
+                fbn_jt_score_terms_device(plan, static_cast<const double *>(d_marg), static_cast<const double *>(d_gold),
+                                          nr, static_cast<double *>(d_terms), s)) {
+                e = std::string("fbn_jt_run_device / fbn_jt_score_terms_device: ") + fbn_last_error();
                 cleanup();
                 return e;
             }
             fbn_jt_last_kernel_ms(plan, &ms);
-            // this rank's shard: marginals to its host slice over its own link, scored in case order
-            (void)hipMemcpyAsync(marg.data(), d_marg, marg.size() * 8, hipMemcpyDeviceToHost, s);
-            (void)hipMemcpyAsync(lab.data(), d_lab, lab.size() * 4, hipMemcpyDeviceToHost, s);
-            if ((e = HipErr(hipStreamSynchronize(s), "shard results")).size()) {
-                cleanup();
-                return e;
-            }
-            if (fbn_jt_score(plan, marg.data(), golden.data() + (size_t)c0 * SD, nr, &part[0], &part[1])) {
-                e = std::string("fbn_jt_score: ") + fbn_last_error();
-                cleanup();
-                return e;
-            }
-            for (int64_t c = 0; c < nr; ++c) part[2] += lab[c] == tester_->ground_truths[c0 + c];
         }
-        (void)hipMemcpyAsync(d_s, part, sizeof part, hipMemcpyHostToDevice, s);
         (void)hipMemcpyAsync(d_k, &ms, 4, hipMemcpyHostToDevice, s);
         ncclGroupStart();
-        ncclReduce(d_s, d_s, 3, ncclFloat64, ncclSum, 0, comm, s);
         ncclAllGather(d_lab, d_all, (size_t)chunk, ncclInt32, comm, s);
+        ncclAllGather(d_terms, d_tall, (size_t)chunk * 2, ncclFloat64, comm, s);
         ncclAllReduce(d_k, d_k, 1, ncclFloat32, ncclMax, comm, s);
-        if ((e = NcclErr(ncclGroupEnd(), "ncclGroupEnd (reduce / gather)")).size()) {
+        if ((e = NcclErr(ncclGroupEnd(), "ncclGroupEnd (gathers)")).size()) {
             cleanup();
             return e;
         }
         if (r == 0) {
-            (void)hipMemcpyAsync(sums, d_s, 3 * 8, hipMemcpyDeviceToHost, s);
             (void)hipMemcpyAsync(all_labels.data(), d_all, all_labels.size() * 4, hipMemcpyDeviceToHost, s);
+            (void)hipMemcpyAsync(all_terms.data(), d_tall, all_terms.size() * 8, hipMemcpyDeviceToHost, s);
             (void)hipMemcpyAsync(&kmax, d_k, 4, hipMemcpyDeviceToHost, s);
         }
         e = HipErr(hipStreamSynchronize(s), "gather");
         cleanup();
         return e;
     });
+    if (err.empty()) {  // case order, as fbn_jt_score and the reference's EvaluateAccuracy loop
+        double mse = 0.0, hd = 0.0, correct = 0.0;
+        for (int64_t c = 0; c < n; ++c) {
+            mse += all_terms[2 * c];
+            hd += all_terms[2 * c + 1];
+            correct += all_labels[c] == tester_->ground_truths[c];
+        }
+        sums[0] = mse, sums[1] = hd, sums[2] = correct;
+    }
     if (!err.empty()) return err;
     std::copy(all_labels.begin(), all_labels.begin() + n, predictions.begin());
     *kernel_ms = kmax;

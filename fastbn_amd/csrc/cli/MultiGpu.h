@@ -4,9 +4,11 @@
 // (src/main.cpp:31-82); `--gpus N` keeps that process model and drives N devices from it.
 //
 //   JT (-a 2):  the cases are cut into N contiguous shards; each rank builds its plan on its device
-//               from the parsed network, runs its shard from device memory, and ONE all-gather of
-//               labels + marginals (RCCL) hands every case back in case order (MSE / HD / accuracy
-//               scored in the reference's case order, src/Inference.cpp:153-206).
+//               from the parsed network, runs its shard from device memory and forms every case's
+//               MSE / HD terms there (fbn_jt_score_terms_device, against its golden slice uploaded
+//               once); all-gathers (RCCL) of the labels and of the 16-byte per-case terms let rank 0
+//               add them in the reference's case order (src/Inference.cpp:153-206) -- the marginals
+//               never leave their device.
 //   PC (-a 0):  rank 0 uploads the column store, ONE broadcast (RCCL) places it in every rank's
 //               device memory, and the native session fbn_pc_dist_* cuts each level by edges; per
 //               level one all-gather of the fixed-size records (and at level 0 of the pair tables,

@@ -142,9 +142,10 @@ int CompileJTProgramT(const JTPlanHost &plan, JTProgramT &prog, int lds_budget);
 // kernel's per-wave workspace holds wave_entries rows of 64 fp64 lanes; initv is its constant input.
 bool JTCodegenEligible(const JTPlanHost &plan, int64_t *entry_ops);
 // fast: the fast arithmetic order (normalizations that cancel are left out; results within 1e-12 of
-// the exact order, which repeats the reference's every multiply + Normalize)
+// the exact order, which repeats the reference's every multiply + Normalize); var_major: marginals
+// stored variable-major [sum_dom][ncases] instead of case-major [ncases][sum_dom]
 int GenerateJTKernel(const JTPlanHost &plan, std::string &src, int64_t *wave_entries, std::vector<double> &initv,
-                     int64_t *lds_bytes = nullptr, bool fast = false);
+                     int64_t *lds_bytes = nullptr, bool fast = false, bool var_major = false);
 
 }  // namespace fbn
 

@@ -72,7 +72,7 @@ constexpr int kDefaultMerge = 1;  // FBN_JT_MERGE default (fast order; round 5 s
 
 class JTGen {
   public:
-    JTGen(const JTPlanHost &p, bool fast_order) : plan(p), fast(fast_order) {}
+    JTGen(const JTPlanHost &p, bool fast_order, bool var_major) : plan(p), fast(fast_order), vmajor(var_major) {}
     int Run(std::string &src, int64_t *wave_entries, std::vector<double> &initv);
     int64_t lds_rows = 0;  // LDS rows (64 lanes x fp64) per wave: the clique tail
     int64_t pool_rows = 0;  // + LDS rows of the message pool (after the tail, before the initial potentials)
@@ -86,6 +86,7 @@ class JTGen {
     // in between (the reference's per-step normalizations cancel in every normalized result);
     // messages are normalized once, marginals from a statically chosen clique
     const bool fast;
+    const bool vmajor;  // marginals variable-major [SD][ncases] (fbn_jt_set_output_layout)
     std::ostringstream o;
     std::vector<int> okw_word, okw_pos, out_off;
     std::vector<int64_t> sep_row, init_off;
@@ -829,6 +830,7 @@ int JTGen::Run(std::string &src, int64_t *wave_entries, std::vector<double> &ini
     // workspace stays in L2 -- times the kernel without its workspace's fabric traffic
     if (const char *e = getenv("FBN_JT_WS_FOLD")) o << "#define FBN_WS_FOLD " << atoi(e) << "\n";
     if (getenv("FBN_JT_NO_OUT") && atoi(getenv("FBN_JT_NO_OUT")) != 0) o << "#define FBN_NO_OUT 1\n";
+    if (vmajor) o << "#define FBN_VMAJOR 1\n";
     o << R"FBN(typedef signed char i8;
 __device__ __forceinline__ double dv(double x, double den, double y) {  // x / den (Markstein, see jt_kernels.hip)
     const double q = x * y;
@@ -867,18 +869,28 @@ __device__ __forceinline__ double frcp(double x) {
 // this lane's case / output row, recomputed per segment from the (laundered) block index
 #define CS (blkl * 64 + lane)
 #define ACT (CS < ncases)
+#ifdef FBN_VMAJOR
+// variable-major output [SD][ncases]: value k of every case is one column, so a store instruction
+// writes 64 consecutive cases = 512 contiguous bytes (4 full lines) instead of one value into 64 lines
+#define OUT(k) (marg[(long long)(k) * ncases + CS])
+#else
 #define OUT(k) (marg[CS * FBN_SD + (k)])
+#endif
 #ifdef FBN_NO_OUT  // diagnostic only (FBN_JT_NO_OUT=1): marginals computed, never stored
 #define OUTS(k, v) do { if (ncases < 0) OUT(k) = (v); } while (0)
 #else
 #define OUTS(k, v) (OUT(k) = (v))  // (non-temporal stores measured 2.1x slower: partial lines)
 #endif
+#ifdef FBN_VMAJOR
+#define OUTS2(k, a, b) do { OUTS(k, a); OUTS((k) + 1, b); } while (0)
+#else
 // two adjacent output values in one 16-byte store (8-byte aligned: the rows are 8 * FBN_SD bytes)
 typedef double fbn_d2u __attribute__((ext_vector_type(2), aligned(8)));
 #ifdef FBN_NO_OUT
 #define OUTS2(k, a, b) do { if (ncases < 0) *(fbn_d2u *)&OUT(k) = (fbn_d2u){(a), (b)}; } while (0)
 #else
 #define OUTS2(k, a, b) (*(fbn_d2u *)&OUT(k) = (fbn_d2u){(a), (b)})
+#endif
 #endif
 extern "C" __global__ void __launch_bounds__(64, FBN_MIN_WAVES)
 fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restrict__ labels,
@@ -1090,8 +1102,8 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
 }  // namespace
 
 int GenerateJTKernel(const JTPlanHost &plan, std::string &src, int64_t *wave_entries, std::vector<double> &initv,
-                     int64_t *lds_bytes, bool fast) {
-    JTGen g(plan, fast);
+                     int64_t *lds_bytes, bool fast, bool var_major) {
+    JTGen g(plan, fast, var_major);
     int rc = g.Run(src, wave_entries, initv);
     if (lds_bytes) *lds_bytes = ((g.lds_rows + g.pool_rows) * 64 + (g.iv_lds ? (int64_t)initv.size() : 0)) * 8;
     return rc;

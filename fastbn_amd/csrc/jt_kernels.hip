@@ -31,6 +31,16 @@ struct JtArgs {
     long long ncases;
     long long NE;
     int nops, V, SD, nc;
+    int vmajor;  // marginals variable-major [SD][ncases] (fbn_jt_set_output_layout)
+};
+
+// one case's marginal outputs: a case-major row (vs = 1) or a column stride of the variable-major
+// layout (vs = ncases); value d of the output at index k is o[d] of `out + k`
+struct MOut {
+    double *p;
+    long long vs;
+    __device__ __forceinline__ double &operator[](long long d) const { return p[d * vs]; }
+    __device__ __forceinline__ MOut operator+(long long k) const { return MOut{p + k * vs, vs}; }
 };
 
 #define AT(e) S[(size_t)(e) * 64]
@@ -180,7 +190,7 @@ __device__ __forceinline__ double g_clqdis(double *__restrict__ S, const JtOp &o
 }
 template <bool EXACT>
 __device__ __forceinline__ double g_marg(double *__restrict__ S, int toff, int dim, int cum, int T, const Den &D,
-                                         double *__restrict__ o, bool act) {
+                                         const MOut &o, bool act) {
     const int bw = dim * cum, nhi = T / bw;
     double tot = 0.0;
     for (int d = 0; d < dim; ++d) {
@@ -208,7 +218,7 @@ __global__ __launch_bounds__(64) void jt_interp_kernel(JtArgs A) {
         const bool act = cs < A.ncases;
         const long long csr = act ? cs : A.ncases - 1;
         const int8_t *__restrict__ ev = A.evid + csr * A.V;
-        double *__restrict__ out = A.marg + csr * A.SD;
+        const MOut out{A.marg + csr * (A.vmajor ? 1 : A.SD), A.vmajor ? A.ncases : 1};
 
         for (int i = 0; i < A.nops; ++i) {
             const JtOp op = ops[i];
@@ -279,7 +289,7 @@ __global__ __launch_bounds__(64) void jt_interp_kernel(JtArgs A) {
             }
             case JT_OP_MARG: {  // src/JunctionTree.cpp:1339-1454, src/Inference.cpp:92-102
                 const int dim = op.b;
-                double *__restrict__ o = out + op.a;
+                const MOut o = out + op.a;
                 if (ev[op.e] >= 0) {  // evidence node: probabilities stay 0
                     if (act)
                         for (int d = 0; d < dim; ++d) o[d] = 0.0;
@@ -330,6 +340,7 @@ struct JtLParams {
     long long store_off, den_off, sep_off, spill_off;
     int nops, V, SD, nc, cap;
     int force_exact;  // ablation/testing: always take the IEEE division path
+    int vmajor;        // marginals variable-major [SD][ncases]
     const int *flags;  // fixup mode (non-null): only the blocks the specialized kernel flagged
 };
 
@@ -416,7 +427,7 @@ __device__ void op_sepdis(const Tab<SPILL> &T, const Den &D, double *__restrict_
 
 // marginal of one variable from the clique (TableMarginalization in entry order), un-normalized
 template <bool SPILL, bool EXACT>
-__device__ void op_marg(const Tab<SPILL> &T, const Den &D, double *__restrict__ o, bool act, int dim, int cum,
+__device__ void op_marg(const Tab<SPILL> &T, const Den &D, const MOut &o, bool act, int dim, int cum,
                         int Tn, double &tot) {
     const int bw = dim * cum, nhi = Tn / bw;
     tot = 0.0;
@@ -475,7 +486,7 @@ __global__ __launch_bounds__(64) void jt_lds_kernel(const JtOp *__restrict__ ops
         const bool act = cs < A.ncases;
         const long long csr = act ? cs : A.ncases - 1;
         const int8_t *__restrict__ ev = evid + csr * A.V;
-        double *__restrict__ out = marg + csr * A.SD;
+        const MOut out{marg + csr * (A.vmajor ? 1 : A.SD), A.vmajor ? A.ncases : 1};
         Den D{1.0, 1.0};  // the clique in LDS is T[e] / D.den
         bool fast = true;
 
@@ -570,7 +581,7 @@ __global__ __launch_bounds__(64) void jt_lds_kernel(const JtOp *__restrict__ ops
                     if (r < best) best = r, sel = cd[k];
                 }
                 if (sel != op.g) break;
-                double *__restrict__ o = out + op.a;
+                const MOut o = out + op.a;
                 double tot;
                 if (fast) op_marg<SPILL, false>(T, D, o, act, op.b, op.h, op.pad, tot);
                 else op_marg<SPILL, true>(T, D, o, act, op.b, op.h, op.pad, tot);
@@ -616,9 +627,11 @@ extern "C" hipError_t fbn_jt_lds_launch(const JtOp *ops, int nops, const int32_t
                                         double *marg, int32_t *labels, double *ws, int32_t *wsi, long long wave_entries,
                                         long long store_off, long long den_off, long long sep_off,
                                         long long spill_off, int nc, int cap, bool spill, int force_exact,
-                                        const int *flags, int grid, unsigned long long *prof, hipStream_t stream) {
+                                        const int *flags, int grid, unsigned long long *prof, int vmajor,
+                                        hipStream_t stream) {
     JtLParams a;
     a.force_exact = force_exact;
+    a.vmajor = vmajor;
     a.flags = flags;
     a.ncases = ncases;
     a.wave_entries = wave_entries;
@@ -653,8 +666,9 @@ extern "C" hipError_t fbn_jt_lds_launch(const JtOp *ops, int nops, const int32_t
 extern "C" hipError_t fbn_jt_launch(const JtOp *ops, int nops, const int32_t *aux, const double *initv,
                                     const uint64_t *dig, const int8_t *evid, int V, long long ncases, int SD,
                                     double *marg, int32_t *labels, double *ws, int32_t *wsi, long long NE, int nc,
-                                    int grid, hipStream_t stream) {
+                                    int grid, int vmajor, hipStream_t stream) {
     JtArgs a;
+    a.vmajor = vmajor;
     a.ops = ops;
     a.aux = aux;
     a.initv = initv;
@@ -691,5 +705,98 @@ extern "C" hipError_t fbn_jt_evidence_check(const int8_t *ev, long long n, int V
     const long long b = (n + 255) / 256;
     hipLaunchKernelGGL(jt_evidence_check, dim3((unsigned)(b < 4096 ? (b > 0 ? b : 1) : 4096)), dim3(256), 0, s, ev, n,
                        V, dom, first);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ output layout / scoring
+// case-major [n][SD] -> variable-major [SD][n] (the kernels without a variable-major store path
+// write case-major scratch; fbn_jt_set_output_layout): 32 x 32 tiles through LDS, both sides coalesced
+static __global__ __launch_bounds__(256) void jt_marg_transpose(const double *__restrict__ in, double *__restrict__ out,
+                                                                long long n, int SD) {
+    __shared__ double tile[32][33];
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+    const long long c0 = (long long)blockIdx.y * 32;
+    const int k0 = blockIdx.x * 32;
+    for (int r = ty; r < 32; r += 8) {
+        const long long c = c0 + r;
+        const int k = k0 + tx;
+        if (c < n && k < SD) tile[r][tx] = in[c * SD + k];
+    }
+    __syncthreads();
+    for (int r = ty; r < 32; r += 8) {
+        const int k = k0 + r;
+        const long long c = c0 + tx;
+        if (c < n && k < SD) out[(long long)k * n + c] = tile[tx][r];
+    }
+}
+
+extern "C" hipError_t fbn_jt_marg_transpose(const double *in, double *out, long long n, int SD, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const long long gy = (n + 31) / 32;
+    if (gy > 65535LL * 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(jt_marg_transpose, dim3((unsigned)((SD + 31) / 32), (unsigned)gy), dim3(256), 0, s, in, out, n, SD);
+    return hipGetLastError();
+}
+
+// Round(x, 7) of src/Inference.cpp:195-206, the operations of fbn_jt_score's host lambda
+__device__ __forceinline__ double jt_round7(double number) {
+    const long long integerpart = (long long)number;
+    number -= integerpart;
+    for (int i = 0; i < 7; ++i) number *= 10;
+    number = (double)(long long)(number + 0.5);
+    for (int i = 0; i < 7; ++i) number /= 10;
+    return integerpart + number;
+}
+
+// correctly rounded sqrt (the host's sqrtsd): the device estimate and its two neighbours, the one
+// whose square is nearest x (exact fma residuals; sqrt never lands on a midpoint)
+__device__ __forceinline__ double jt_sqrt_rn(double x) {
+    if (!(x > 0.0) || __builtin_isinf(x)) return __builtin_sqrt(x);
+    const double s = __builtin_sqrt(x);
+    const long long b = __double_as_longlong(s);  // s > 0, finite: neighbours by the bit pattern
+    const double sm = __longlong_as_double(b - 1), sp = __longlong_as_double(b + 1);
+    const double r = __builtin_fabs(__builtin_fma(-s, s, x)), rm = __builtin_fabs(__builtin_fma(-sm, sm, x)),
+                 rp = __builtin_fabs(__builtin_fma(-sp, sp, x));
+    return rm < r ? (rm < rp ? sm : sp) : (rp < r ? sp : s);
+}
+
+// per-case MSE / HD terms (CalculateMSE / CalculateHellingerDistance, src/Inference.cpp:153-193),
+// one thread per case; no contraction, so every term equals the host's fbn_jt_score term bit for bit
+static __global__ __launch_bounds__(256) void jt_score_terms(const double *__restrict__ marg,
+                                                             const double *__restrict__ golden, long long n, int SD,
+                                                             long long mcs, long long mvs,
+                                                             const int32_t *__restrict__ dom, int V,
+                                                             double *__restrict__ terms) {
+#pragma clang fp contract(off)
+    for (long long c = (long long)blockIdx.x * 256 + threadIdx.x; c < n; c += (long long)gridDim.x * 256) {
+        const double *__restrict__ a = marg + c * mcs;
+        const double *__restrict__ x = golden + c * SD;
+        int num = 0, off = 0;
+        double e1 = 0.0, e2 = 0.0;
+        for (int v = 0; v < V; ++v) {
+            const int dv = dom[v];
+            if (x[off] > 0) {
+                num += dv;
+                for (int j = 0; j < dv; ++j) {
+                    const double r = jt_round7(a[(long long)(off + j) * mvs]);
+                    const double d1 = r - x[off + j];
+                    e1 += d1 * d1;
+                    const double d2 = jt_sqrt_rn(r) - jt_sqrt_rn(x[off + j]);
+                    e2 += d2 * d2;
+                }
+            }
+            off += dv;
+        }
+        terms[2 * c] = jt_sqrt_rn(e1 / num);
+        terms[2 * c + 1] = jt_sqrt_rn(e2 / num);
+    }
+}
+
+extern "C" hipError_t fbn_jt_score_terms(const double *marg, const double *golden, long long n, int SD, int vmajor,
+                                         const int32_t *dom, int V, double *terms, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const long long b = (n + 255) / 256;
+    hipLaunchKernelGGL(jt_score_terms, dim3((unsigned)(b < 8192 ? b : 8192)), dim3(256), 0, s, marg, golden, n, SD,
+                       vmajor ? 1LL : (long long)SD, vmajor ? n : 1LL, dom, V, terms);
     return hipGetLastError();
 }

@@ -21,14 +21,16 @@ def synth_small_xml(dirname):
     return path
 
 
-def prebuild(xml_paths):
+def prebuild(xml_paths, layouts=(0,)):
     out = []
     for xml in xml_paths:
         jt = api.JunctionTree(api.Network(xml), device=-1)
         if jt.info["specialized_eligible"]:
-            for exact in (None, True):  # both arithmetic orders (default fast, exact on request)
-                jt.set_exact(exact)
-                out.append(jt.build_kernel())
+            for layout in layouts:  # output layouts (0 case-major, 1 variable-major: bench.py's ALARM)
+                jt.set_output_layout(layout)
+                for exact in (None, True):  # both arithmetic orders (default fast, exact on request)
+                    jt.set_exact(exact)
+                    out.append(jt.build_kernel())
     return out
 
 
@@ -69,7 +71,7 @@ def prebuild_default(clean=True):
     option variants the tests use; clean: then drop the code objects no current plan uses (older
     generator versions)."""
     with tempfile.TemporaryDirectory() as d:
-        built = prebuild([ALARM_XML, synth_small_xml(d)] + fixture_xmls(d))
+        built = prebuild([ALARM_XML], layouts=(0, 1)) + prebuild([synth_small_xml(d)] + fixture_xmls(d))
     built += prebuild_options(ALARM_XML, ALARM_TEST_OPTIONS)
     if clean:
         keep = {os.path.basename(p) for p in built}

@@ -156,6 +156,21 @@ int fbn_jt_set_evidence_check(fbn_jt_plan *p, int enable);
  * golden[.][first state] <= 0.  Host arrays; sums accumulated in case order. */
 int fbn_jt_score(const fbn_jt_plan *p, const double *marginals, const double *golden, int64_t ncases,
                  double *mse_sum, double *hd_sum);
+/* Layout of the d_marginals buffer of fbn_jt_run_device: 0 = case-major [ncases][sum_dom] (default,
+ * the reference's per-case vectors, GetProbabilitiesAllNodes src/JunctionTree.cpp:1385-1454),
+ * 1 = variable-major [sum_dom][ncases] (value k of every case contiguous: a kernel store covers 64
+ * consecutive cases, written once per cache line).  Same values either way; fbn_jt_run (host
+ * buffers) always returns case-major. */
+int fbn_jt_set_output_layout(fbn_jt_plan *p, int layout);
+/* The per-case terms of fbn_jt_score on the device: d_terms[2 * c] = sqrt(e1 / num) (MSE) and
+ * d_terms[2 * c + 1] = sqrt(e2 / num) (HD) of case c, computed exactly as fbn_jt_score computes
+ * them (same operations, no contraction), from d_marginals in the plan's output layout and
+ * d_golden [ncases][sum_dom] (case-major, as read from the golden file).  Summing the terms in case
+ * order reproduces fbn_jt_score's sums bit for bit; asynchronous on hip_stream.  Replaces
+ * Inference::CalculateMSE / CalculateHellingerDistance (src/Inference.cpp:153-206) for marginals
+ * that stay on the device (the multi-GPU CLI: 16 bytes per case leave a rank instead of sum_dom * 8). */
+int fbn_jt_score_terms_device(fbn_jt_plan *p, const double *d_marginals, const double *d_golden, int64_t ncases,
+                              double *d_terms, void *hip_stream);
 /* Device kernel time (ms, hipEvent) of the last fbn_jt_run*; launches of the main kernel. */
 int fbn_jt_last_kernel_ms(const fbn_jt_plan *p, float *ms);
 /* enable = 0: fbn_jt_run* records no timing events (two fewer stream markers per call; callers that

@@ -33,7 +33,8 @@ def test_cli_rccl_path_at_one_gpu():
     """--gpus path of the C++ host (cli/MultiGpu.h: ncclCommInitAll, one thread per GPU) forced on
     the box's one GPU (FBN_PC_DIST_FORCE_EXCHANGE): PC through ncclBroadcast of the columns + the
     native session with ncclAllGather of the records and pair tables; JT cases through
-    fbn_jt_run_device + the ncclSend/Recv gather -- the same result lines as the one-GPU path."""
+    fbn_jt_run_device, scored on the device (fbn_jt_score_terms_device) + all-gathers of the labels
+    and the per-case terms -- the same result lines as the one-GPU path."""
     env = dict(os.environ, FBN_PC_DIST_FORCE_EXCHANGE="1")
 
     def run_env(args):

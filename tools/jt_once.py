@@ -1,4 +1,5 @@
-"""Run the JT kernel a few times (for rocprofv3 PMC passes): jt_once.py [variant] [waves] [reps] [cases]."""
+"""Run the JT kernel a few times (for rocprofv3 PMC passes): jt_once.py [variant] [waves] [reps] [cases] [layout]
+(layout 1: variable-major marginals, fbn_jt_set_output_layout)."""
 import os
 import sys
 
@@ -18,6 +19,8 @@ ev = synth.evidence_cases(synth.read_xmlbif(xml), n, 7, seed=1)
 jt = F.JunctionTree(F.Network(xml), device=0)
 jt.set_variant(variant)
 jt.set_waves_per_cu(waves)
+layout = int(sys.argv[5]) if len(sys.argv) > 5 else 0
+jt.set_output_layout(layout)
 d_ev = torch.from_numpy(ev).cuda()
 d_lab = torch.empty(n, dtype=torch.int32, device="cuda")
 d_marg = torch.empty((n, jt.info["sum_dom"]), dtype=torch.float64, device="cuda")
