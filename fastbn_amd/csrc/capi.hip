@@ -1040,20 +1040,23 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
         labels = p->labels.as<int32_t>();
     }
     int variant = p->variant;
+    // the specialized kernel stores variable-major columns with 32-bit byte offsets
+    const bool vm3 = vm && (int64_t)ncases * SD * 8 < INT32_MAX;
     if (variant == -1) {
         // specialized kernel when eligible; else the streamed kernel (1.5-2x the interpreters on
         // ALARM and the Munin-like network); the interpreters only for plans it cannot take
-        if (p->gen_eligible && GenEnsure(p, vm) == FBN_OK) variant = 3;
+        if (p->gen_eligible && GenEnsure(p, vm3) == FBN_OK) variant = 3;
         else if (p->t_ok && JtFast(p)) variant = 5;  // (fast arithmetic order only)
         else if (p->v_ok) variant = 4;
         else variant = (p->lprog.max_table * 64 * 8 * 2 <= (int64_t)kLdsBytes) ? 0 : 1;
     }
-    else if (variant == 3 && (rc = GenEnsure(p, vm))) return rc;
+    else if (variant == 3 && (rc = GenEnsure(p, vm3))) return rc;
     p->last_variant = variant;
     // variable-major output: kernels 0-3 store it directly; 4 and 5 write case-major scratch that is
     // transposed into the caller's buffer at the end (same values)
     double *const marg_out = marg;
-    const bool vm_scratch = vm && (variant == 4 || variant == 5);
+    // (the specialized kernel addresses columns with 32-bit byte offsets: larger batches transpose too)
+    const bool vm_scratch = vm && (variant == 4 || variant == 5 || (variant == 3 && !vm3));
     if (vm_scratch) {
         if ((rc = p->mtmp.ensure((size_t)ncases * SD * 8))) return rc;
         marg = p->mtmp.as<double>();
@@ -1151,7 +1154,7 @@ static int JtRunDevice(fbn_jt_plan *p, const int8_t *d_evidence, int64_t ncases,
             return rc;
     } else if (variant == 3) {
         // one wave (64 cases) per SIMD: the clique in flight occupies the register file (+ LDS tail)
-        const auto &gk = GenCur(p, vm);
+        const auto &gk = GenCur(p, vm3);
         int wpc = p->waves_per_cu > 0 ? p->waves_per_cu : 4;
         if (gk.lds > 0) wpc = std::max<int>(1, std::min<int64_t>(wpc, (int64_t)kLdsBytes / gk.lds));
         const int grid = (int)std::min<int64_t>(nblk, (int64_t)p->num_cu * wpc);
@@ -2822,7 +2825,8 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
     // scratch: [zeroed: barrier words | first-independent words] [statistics slots] [pair tables]
     const size_t acc_off = (kSmallZeroBytes + 255) & ~(size_t)255;
     const size_t pt_off = acc_off + (size_t)grid * 64;
-    const size_t dout_off = (pt_off + (size_t)kSmallMaxEdges * 16 * 4 + 255) & ~(size_t)255;
+    const size_t pg_off = (pt_off + (size_t)kSmallMaxEdges * 16 * 4 + 255) & ~(size_t)255;
+    const size_t dout_off = (pg_off + (size_t)kSmallMaxEdges * 8 + 255) & ~(size_t)255;
     const size_t bytes = dout_off + sizeof(PcSmallOut);
     if ((rc = c->small_scr.ensure(bytes))) return rc;
     if (!c->h_small) {  // coherent: the host polls its completion word while the kernel runs
@@ -2863,6 +2867,8 @@ int CiPCSmall(fbn_ci_ctx *c, double alpha, int depth, PCResultHost &res, std::ve
     a.phase_base = c->small_phase;
     a.acc = reinterpret_cast<unsigned long long *>(scr + acc_off);
     a.pairtab = reinterpret_cast<int32_t *>(scr + pt_off);
+    // the level-1 information screen (exact, see ci_bits.hip; FBN_PC_NO_MISCREEN=1: off)
+    a.pg2 = band && !getenv("FBN_PC_NO_MISCREEN") ? reinterpret_cast<unsigned long long *>(scr + pg_off) : nullptr;
     a.ctx_stats = c->stats.as<unsigned long long>();
     a.dout = reinterpret_cast<PcSmallOut *>(scr + dout_off);
     a.out = out;

@@ -871,15 +871,23 @@ __device__ __forceinline__ double frcp(double x) {
 #define ACT (CS < ncases)
 #ifdef FBN_VMAJOR
 // variable-major output [SD][ncases]: value k of every case is one column, so a store instruction
-// writes 64 consecutive cases = 512 contiguous bytes (4 full lines) instead of one value into 64 lines
-#define OUT(k) (marg[(long long)(k) * ncases + CS])
+// writes 64 consecutive cases = 512 contiguous bytes (4 full lines) instead of one value into 64
+// lines.  Through a buffer resource: voffset = the lane's case (bytes), soffset = column k (bytes,
+// one scalar multiply) -- 64-bit column addresses measured 10 % more instructions and SGPR spills.
+// (The host takes this kernel only when ncases * SD * 8 < 2^31.)
+typedef unsigned fbn_u2v __attribute__((ext_vector_type(2)));
+#ifdef FBN_NO_OUT
+#define OUTS(k, v) do { if (ncases < 0) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(fbn_u2v, (double)(v)), mrs, (int)(CS * 8), (int)(k) * mcb, 0); } while (0)
+#else
+#define OUTS(k, v) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(fbn_u2v, (double)(v)), mrs, (int)(CS * 8), (int)(k) * mcb, 0)
+#endif
 #else
 #define OUT(k) (marg[CS * FBN_SD + (k)])
-#endif
 #ifdef FBN_NO_OUT  // diagnostic only (FBN_JT_NO_OUT=1): marginals computed, never stored
 #define OUTS(k, v) do { if (ncases < 0) OUT(k) = (v); } while (0)
 #else
 #define OUTS(k, v) (OUT(k) = (v))  // (non-temporal stores measured 2.1x slower: partial lines)
+#endif
 #endif
 #ifdef FBN_VMAJOR
 #define OUTS2(k, a, b) do { OUTS(k, a); OUTS((k) + 1, b); } while (0)
@@ -915,6 +923,10 @@ fbn_jt_gen(const i8 *__restrict__ evid, double *__restrict__ marg, int *__restri
     gdouble *Wb = (gdouble *)ws + (unsigned long long)blockIdx.x * FBN_WE * 64;
 #endif
     unsigned lo = (unsigned)lane * 8;
+#ifdef FBN_VMAJOR
+    const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(marg, 0, 0x7FFFFFFF, 0x00020000);
+    const int mcb = (int)ncases * 8;  // column stride, bytes
+#endif
     for (long long blk = blockIdx.x; blk * 64 < ncases; blk += gridDim.x) {
         long long blkl = blk;
         const long long cs = blk * 64 + lane;

@@ -499,7 +499,7 @@ int RunPCStable(fbn_ci_ctx *ctx, double alpha, int depth, int group_size, PCResu
             if ((rc = CiL0L1Device(ctx, P, &E, &cands, res))) return rc;
             res.tests_per_level.push_back(P);
             res.launched_per_level.push_back(P);
-            res.path = 3;
+            if (res.path == 0) res.path = 3;  // (2 -- a refused device-resident search -- stays)
             CiSetPairMode(ctx, 2);
             bool host_done = false;
             auto host_side = [&]() -> int {

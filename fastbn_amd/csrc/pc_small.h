@@ -69,6 +69,8 @@ struct PcSmallArgs {
     unsigned phase_base;     // grid barrier phases completed by the earlier launches on this scratch
     unsigned long long *acc; // [0] margin bits (min), [1] near, [2 + d] launched at level d
     int32_t *pairtab;        // [kSmallMaxEdges][16] level-0 tables (derived level-1 counting)
+    unsigned long long *pg2; // [kSmallMaxEdges] level-0 G^2 (fp64 bits) of every pair: the level-1
+                             // information screen (nullptr: off)
     unsigned long long *ctx_stats;  // the ctx's margin log, set to this run's at the end
     PcSmallOut *dout;        // the record, built in device memory during the run
     PcSmallOut *out;         // pinned host memory: the record's used part, copied at the end

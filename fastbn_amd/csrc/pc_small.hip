@@ -496,6 +496,9 @@ __device__ __forceinline__ Decision wave_test(const PcSmallArgs &A, const Lds &L
         t = g2_term(ob, nxz(a, c), nyz(b, c), tot);
     }
     const double gs = wsum_f64(t), ga = wsum_f64(fabs(t));
+    if (D == 0 && record_pair && A.pg2 && lane == 0)  // G^2 = 2N I(X;Y): the level-1 screen's input
+        __hip_atomic_store(A.pg2 + pair_index(n, x, y), (unsigned long long)__double_as_longlong(gs), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     Decision r = decide_tree(gs, ga, df, cells, A, L.band);
     if (r.ind < 0) {  // in the band: the reference's in-order running sum, then p
         r = decide_exact(wave_inorder_add(0.0, t), df, A, L.band);  // lane l = cell l (t = 0 beyond)
@@ -506,6 +509,22 @@ __device__ __forceinline__ Decision wave_test(const PcSmallArgs &A, const Lds &L
         ph[0] += c1 - c0, ph[1] += c2 - c1, ph[2] += c3 - c2, ph[3] += 1;
     }
     return r;
+}
+
+// ---- the level-1 information screen (the argument: ci_bits.hip, l1_plausible).  In G^2 units:
+// with G^2_uv = 2N I(U;V) from level 0, the test (x, y | z) can be independent only if G^2_xz and
+// G^2_yz are both >= G^2_xy - hi(df) - margins, df = (dx-1)(dy-1)dz (hi: the decision band's upper
+// end, which every independent test's G^2 stays below).  false = certainly dependent (not run).
+__device__ __forceinline__ bool screen_plausible(const PcSmallArgs &A, const Lds &L, int x, int y, int z) {
+    if (!A.pg2 || !A.band) return true;
+    const int df = (L.dims[x] - 1) * (L.dims[y] - 1) * L.dims[z];
+    if (df <= 0 || df > A.nband) return true;
+    auto g2 = [&](int u, int v) {
+        return __longlong_as_double((long long)__hip_atomic_load(
+            A.pg2 + pair_index(A.nvars, u < v ? u : v, u < v ? v : u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    };
+    const double lim = g2(x, y) - (L.band[2 * df - 1] * (1.0 + 1e-9) + 2e-9 * (double)A.N);
+    return lim <= 0.0 || (g2(x, z) >= lim && g2(y, z) >= lim);
 }
 
 // ---- one test per wave on the 2-bit packed columns (d = 2, 3: tables of <= 4^5 = 1024 cells): the
@@ -956,6 +975,7 @@ __global__ __launch_bounds__(BS) void pc_small_kernel(PcSmallArgs Ak, Barrier B)
                 } else {
                     int zz[3];
                     unrank(L, x, y, d, k, zz);
+                    if (d == 1 && !screen_plausible(A, L, x, y, zz[0])) continue;  // dependent: not run
                     if (d == 1) r = wave_test<1>(A, L, x, y, zz[0], lane, false, L.wtab[wv], L.waux[wv], L.ph[wv]);
                     else r = wave_hist_test<2>(A, L, x, y, zz, lane, L.whist[wv], L.ph[wv]);  // (d == 2)
                 }

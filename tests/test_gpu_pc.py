@@ -495,3 +495,26 @@ def test_level0_to_level1_on_device_matches_host_path(nvars, ns, monkeypatch):
     assert a.tests_per_level.tolist() == b.tests_per_level.tolist()
     assert a.launched_per_level.tolist() == b.launched_per_level.tolist()
     assert a.oriented == b.oriented
+
+
+def test_level1_information_screen_config5(monkeypatch):
+    """The level-1 information screen (ci_bits.hip l1_plausible: a candidate z with I(X;Z) or I(Y;Z)
+    below I(X;Y) - hi(df) / 2N is certainly dependent and not run) on config 5 at full size: the same
+    counted tests, skeleton, sepsets and orientation as every candidate run (FBN_PC_NO_MISCREEN), both
+    equal to the fixture; level 1 runs far fewer tests than it counts."""
+    import json
+    from conftest import GOLD, pc_digest
+    from fastbn_amd import synth
+    cols, dims = synth.config5_dataset(1000, 100000)
+    ci = F.IndependenceTest(F.Dataset(columns=cols, dims=dims))
+    a = F.PCStable(0.05, 6).StructLearnCompData(ci)
+    monkeypatch.setenv("FBN_PC_NO_MISCREEN", "1")
+    b = F.PCStable(0.05, 6).StructLearnCompData(ci)
+    monkeypatch.delenv("FBN_PC_NO_MISCREEN")
+    ref = json.load(open(os.path.join(GOLD, "pc_c5.json")))
+    for r in (a, b):
+        assert r.tests_per_level.tolist() == ref["tests_per_level"]
+        assert pc_digest(r.edges, r.sepset) == {k: ref[k] for k in ("edges_sha256", "sepsets_sha256")}
+    assert a.oriented == b.oriented
+    la, lb = a.launched_per_level.tolist(), b.launched_per_level.tolist()
+    assert la[1] < 0.5 * a.tests_per_level.tolist()[1] and lb[1] >= b.tests_per_level.tolist()[1]

@@ -47,10 +47,17 @@ def test_alarm5000_default_is_device_resident(alarm, monkeypatch):
     ds, od = alarm
     pc = _check(ds, od, 0.05, 1000, monkeypatch)
     assert pc.tests_per_level.tolist() == [666, 3579, 828, 118, 15] and len(pc.edges) == 44
-    # levels 0, 3, 4: every candidate set once; 1, 2: full speculation minus the part-B skips
+    # levels 0, 3, 4: every candidate set once; 1, 2: full speculation minus the part-B skips; level 1
+    # also minus the candidates the information screen decides (certainly dependent: not run)
     la = pc.launched_per_level.tolist()
     assert la[0] == 666 and la[3:] == [128, 15]
-    assert 3579 <= la[1] <= 8732 and 828 <= la[2] <= 1212
+    assert 0 < la[1] < 3579 and 828 <= la[2] <= 1212
+    monkeypatch.setenv("FBN_PC_NO_MISCREEN", "1")  # the screen off: the same answer, every candidate run
+    ns = F.PCStable(0.05, 1000).StructLearnCompData(F.IndependenceTest(ds))
+    monkeypatch.delenv("FBN_PC_NO_MISCREEN")
+    assert ns.tests_per_level.tolist() == pc.tests_per_level.tolist()
+    assert ns.edges == pc.edges and ns.sepset == pc.sepset and ns.oriented == pc.oriented
+    assert 3579 <= ns.launched_per_level.tolist()[1] <= 8732
     assert pc.GetSHD(os.path.join(GOLD, "alarm", "alarm.bif")) == 5
     assert pc.near_alpha == 0 and pc.min_margin > 1e-9
 
