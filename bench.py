@@ -293,7 +293,7 @@ def pc_small_traffic():
     """Measured L2<->fabric bytes of one device-resident search launch (rocprofv3 FETCH_SIZE +
     WRITE_SIZE, calibrated; committed summary profiles/r05/pmc_pc_small_traffic.json from
     tools/profile_r05_final.sh)."""
-    path = _first_profile("r05/pmc_pc_small_traffic.json", "r04/pmc_pc_small_traffic.json")
+    path = _first_profile("r06/pmc_pc_small_traffic.json", "r05/pmc_pc_small_traffic.json", "r04/pmc_pc_small_traffic.json")
     if path is None:
         return {"traffic": None}
     with open(path) as f:
@@ -324,7 +324,7 @@ def pc_roofline(kernel_s, device_bytes, byte_column_bytes, world=1):
     the kernel time measured live (HIP events around every CI batch of a run).  world > 1: the run's
     work is split over the ranks, so the whole run's instructions / bytes are taken over the slowest
     rank's kernel time against `world` GPUs' peak."""
-    path = _first_profile("r05/pc5_kernels.json", "pc5_kernels.json")
+    path = _first_profile("r06/pc5_kernels.json", "r05/pc5_kernels.json", "pc5_kernels.json")
     out = {"kernel_ms_per_run": 1e3 * kernel_s, "column_bytes_read_per_run": device_bytes,
            "model": {"bytes_per_run": byte_column_bytes,
                      "model_frac": byte_column_bytes / kernel_s / (HBM_PEAK_GBS * 1e9),
@@ -762,7 +762,7 @@ def valu_roofline(which, cases, kernel_ms):
     tools/profile_r05.sh) scaled to this launch, as wave64 lane-ops per second against the fp64
     vector peak (a wave64 fp64 instruction holds its SIMD 4 cycles, so frac <= 1 by construction);
     all VALU instructions (SQ_INSTS_VALU, incl. 32-bit selects / integer ops) beside it."""
-    for path in (os.path.join(REPO, "profiles", "r05", "jt_valu.json"), os.path.join(REPO, "profiles", "jt_valu.json")):
+    for path in (os.path.join(REPO, "profiles", r, "jt_valu.json") for r in ("r06", "r05", ".")):
         if os.path.exists(path):
             break
     else:
@@ -787,7 +787,7 @@ def valu_roofline(which, cases, kernel_ms):
 def load_traffic(cases):
     """Measured HBM bytes per launch (rocprofv3 FETCH_SIZE + WRITE_SIZE, calibrated; committed
     summary profiles/r05/jt_traffic.json, else profiles/jt_traffic.json), scaled to this launch's cases."""
-    for path in (os.path.join(REPO, "profiles", "r05", "jt_traffic.json"), os.path.join(REPO, "profiles", "jt_traffic.json")):
+    for path in (os.path.join(REPO, "profiles", r, "jt_traffic.json") for r in ("r06", "r05", ".")):
         if os.path.exists(path):
             break
     else:

@@ -68,15 +68,13 @@ extern "C" hipError_t fbn_ci_l1_results(const uint8_t *st, const int32_t *sep, c
                                         long long *part, hipStream_t s);
 extern "C" hipError_t fbn_ci_kept_csr(const uint8_t *indep, int n, int32_t *low, int32_t *up, int32_t *off,
                                       int32_t *upoff, int32_t *adj, int32_t *pairs, long long *scal, hipStream_t s);
-extern "C" hipError_t fbn_ci_pair_mi(const int32_t *pairtab, const int32_t *dims, int nv, long long P, double *mi,
-                                     hipStream_t s);
 extern "C" hipError_t fbn_ci_l1_setup(const int32_t *pairs, int E, const int32_t *adj, const int32_t *adj_off,
                                       void *ed, int32_t *pos, uint8_t *st, int32_t *sep, long long *counted,
                                       int chunk0, int32_t *len, int32_t *off, unsigned *ring,
                                       unsigned long long *sstat, long long cap, long long *scal, int num_cu,
-                                      const double *mi, const int32_t *dims, const double *band, int nband, int nv,
-                                      double two_n, int32_t *plist, unsigned long long *sstat2, long long *scal2,
-                                      hipStream_t s);
+                                      const int32_t *pairtab, double *mi, int mi_from_tables, const int32_t *dims,
+                                      const double *band, int nband, int nv, double two_n, int32_t *pcnt,
+                                      int32_t *plist, unsigned long long *sstat2, long long *scal2, hipStream_t s);
 extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims, const int32_t *row0, long long W,
                                       const int32_t *adj, const int32_t *pairtab, int nvars, void *edv, int32_t *pos,
                                       uint8_t *st, int32_t *sep, long long *counted, int32_t *len, int32_t *off,
@@ -291,7 +289,10 @@ struct fbn_ci_ctx {
     DevBuf l1items, l1counts, l1df, l1indep, l1sstat;  // l1sstat: the offset scan's per-tile status words
     // the level-1 information screen (ci_bits.hip): pairwise I of the complete graph, the kept
     // candidates' positions, the screen's scan status words
-    DevBuf l1mi, l1plist, l1sstat2;
+    DevBuf l1mi, l1pcnt, l1plist, l1sstat2;
+    // level 0's G^2 of every pair written into l1mi by the recording batches (pairs [0, covered) in
+    // order; == all pairs: the screen needs no recomputation from the pair tables)
+    int64_t l1mi_covered = 0;
     DevBuf keptidx, kepttmp;  // level-0 kept pair indices (CiAllPairsKept)
     // level 0 -> level 1 on the device (CiL0L1Device): per-variable kept counts, upper-part offsets,
     // (E, candidate sets); the side stream copies the flags / edge list to the host meanwhile
@@ -1735,11 +1736,17 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         // all pairs of the complete graph: the kernels decode test t into its pair (no item array)
         const int32_t *ditems = all_pairs ? nullptr : zc_items ? zc_items : S.items.as<int32_t>();
         int pmode = 0;
+        double *g2rec = nullptr;  // level 0's G^2 per pair, kept for the level-1 screen
         if (c->pair_mode == 1 && d == 0) {
             const size_t np = (size_t)c->nvars * (c->nvars - 1) / 2;
             if ((rc = c->pairtab.ensure(std::max<size_t>(np, 1) * 16 * 4))) return rc;
             pmode = 1;
             c->pairs_recorded = true;
+            if (all_pairs && !want_g2p && pair0 == c->l1mi_covered) {
+                if ((rc = c->l1mi.ensure(std::max<size_t>(np, 1) * 8))) return rc;
+                g2rec = c->l1mi.as<double>() + pair0;
+                c->l1mi_covered = pair0 + n;
+            }
         } else if (c->pair_mode == 2 && d == 1 && c->pairs_recorded) {
             pmode = 2;
         }
@@ -1793,7 +1800,7 @@ static int CiLaunchDevice(fbn_ci_ctx *c, const int32_t *items, int64_t n, int d,
         }
         e = fbn_ci_bits_launch(c->bits.as<uint32_t>(), c->ddims.as<int32_t>(), c->brow.as<int32_t>(),
                                           ditems, c->bits_W, n, d, alpha,
-                                          want_g2p ? c->g2.as<double>() : nullptr, zc_df ? zc_df : S.df.as<int32_t>(),
+                                          want_g2p ? c->g2.as<double>() : g2rec, zc_df ? zc_df : S.df.as<int32_t>(),
                                           want_g2p ? c->p.as<double>() : nullptr,
                                           zc_indep ? zc_indep : S.indep.as<uint8_t>(),
                                           S.bcounts.as<int32_t>(), counts_dev, c->stats.as<unsigned long long>(),
@@ -2282,6 +2289,7 @@ constexpr size_t kZeroCopyBytes = 256 << 10;
 const int32_t *CiCtxDims(const fbn_ci_ctx *c) { return c->dims.data(); }
 void CiSetPairMode(fbn_ci_ctx *c, int mode) {
     c->pair_mode = mode;
+    if (mode == 1) c->l1mi_covered = 0;  // a new level 0 records from pair 0
     c->triples_ready = false;
     if (mode != 2) c->pairs_recorded = false;
 }
@@ -2540,16 +2548,15 @@ int CiLevel1Run(fbn_ci_ctx *c, double alpha, int E, int64_t cands, LevelOut &out
     FBN_HIP(hipMemsetAsync(c->l1sstat.p, 0, (size_t)((E + 255) / 256) * 8, s));
     // the information screen (exact; FBN_PC_NO_MISCREEN=1: every candidate runs): needs the band (a
     // decision threshold per df) and the level-0 pair tables of the complete graph
-    const double *mi = nullptr;
+    double *mi = nullptr;
+    const bool mi_from_tables = c->l1mi_covered != (int64_t)nv * (nv - 1) / 2;
     if (band && !getenv("FBN_PC_NO_MISCREEN")) {
         const long long P = (long long)nv * (nv - 1) / 2;
         if ((rc = c->l1mi.ensure((size_t)std::max<long long>(P, 1) * 8)) ||
             (rc = c->l1plist.ensure((size_t)std::max<int64_t>(cands, 1) * 4)) ||
-            (rc = c->l1sstat2.ensure((size_t)((E + 255) / 256) * 8)))
+            (rc = c->l1pcnt.ensure((size_t)E * 4)) || (rc = c->l1sstat2.ensure((size_t)((E + 255) / 256) * 8)))
             return rc;
         FBN_HIP(hipMemsetAsync(c->l1sstat2.p, 0, (size_t)((E + 255) / 256) * 8, s));
-        hipError_t e = fbn_ci_pair_mi(c->pairtab.as<int32_t>(), c->ddims.as<int32_t>(), nv, P, c->l1mi.as<double>(), s);
-        if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci pair information: %s", hipGetErrorString(e));
         mi = c->l1mi.as<double>();
     }
     CiSlot &S = c->slot[0];
@@ -2569,8 +2576,9 @@ int CiLevel1Run(fbn_ci_ctx *c, double alpha, int E, int64_t cands, LevelOut &out
     hipError_t e = fbn_ci_l1_setup(c->l1pairs.as<int32_t>(), E, c->l1adj.as<int32_t>(), c->l1adjoff.as<int32_t>(),
                                    c->l1ed.p, c->l1pos.as<int32_t>(), c->l1st.as<uint8_t>(), c->l1sep.as<int32_t>(),
                                    c->l1cnt.as<long long>(), (int)chunk, c->l1len.as<int32_t>(),
-                                   c->l1off.as<int32_t>(), c->l1open.as<unsigned>(), sstat, cap, scal, c->num_cu, mi,
-                                   c->ddims.as<int32_t>(), band, nband, nv, 2.0 * (double)c->N, c->l1plist.as<int32_t>(),
+                                   c->l1off.as<int32_t>(), c->l1open.as<unsigned>(), sstat, cap, scal, c->num_cu,
+                                   c->pairtab.as<int32_t>(), mi, mi_from_tables ? 1 : 0, c->ddims.as<int32_t>(), band, nband, nv,
+                                   2.0 * (double)c->N, c->l1pcnt.as<int32_t>(), c->l1plist.as<int32_t>(),
                                    c->l1sstat2.as<unsigned long long>(), scal + 8, s);
     if (e != hipSuccess) return SetError(FBN_ERR_HIP, "ci level-1 setup: %s", hipGetErrorString(e));
     static const bool l1timing = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic

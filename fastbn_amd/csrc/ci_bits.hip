@@ -1075,37 +1075,40 @@ __device__ __forceinline__ long long l1_pidx(int u, int v, int nv) {
     const int i = u < v ? u : v, j = u < v ? v : u;
     return (long long)i * nv - (long long)i * (i + 1) / 2 + (j - i - 1);
 }
-__device__ __forceinline__ bool l1_plausible(const double *__restrict__ mi, int nv, const int32_t *__restrict__ dims,
+// (in G^2 units: g2[pair] = 2N I of the pair's level-0 table; the margin 1e-9 nats = two_n * 1e-9)
+__device__ __forceinline__ bool l1_plausible(const double *__restrict__ g2, int nv, const int32_t *__restrict__ dims,
                                              const double *__restrict__ band, int nband, double two_n, int x, int y,
-                                             int z, double mxy) {
+                                             int z, double gxy) {
     const int df = (dims[x] - 1) * (dims[y] - 1) * dims[z];
     if (df <= 0 || df > nband) return true;
-    const double lim = mxy - (band[2 * df - 1] * (1.0 + 1e-9) / two_n + 1e-9);
+    const double lim = gxy - (band[2 * df - 1] * (1.0 + 1e-9) + two_n * 1e-9);
     if (lim <= 0.0) return true;
-    return mi[l1_pidx(x, z, nv)] >= lim && mi[l1_pidx(y, z, nv)] >= lim;
+    return g2[l1_pidx(x, z, nv)] >= lim && g2[l1_pidx(y, z, nv)] >= lim;
 }
-// I(X;Y) in nats of every pair of the complete graph from its level-0 table (pairtab, 16 counts:
-// N[a][b] at a * dy + b for the pair's x < y), one thread per pair
-__global__ __launch_bounds__(256) void ci_pair_mi(const int32_t *__restrict__ pairtab, const int32_t *__restrict__ dims,
-                                                  int nv, long long P, double *__restrict__ mi) {
+// G^2 = 2N I(X;Y) of every pair of the complete graph from its level-0 table (pairtab, 16 counts:
+// N[a][b] at a * dy + b for x < y), one thread per pair -- when level 0's own G^2 values are not all
+// on this device (a rank of the distributed session ran part of level 0 and imported the others'
+// tables).  The screen reads pairs that need not be edges: (y, z) for z a neighbour of x.
+__global__ __launch_bounds__(256) void ci_pair_g2(const int32_t *__restrict__ pairtab, const int32_t *__restrict__ dims,
+                                                  int nv, long long P, double *__restrict__ g2) {
     for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t < P; t += (long long)gridDim.x * 256) {
         int x, y;
         pair_of(t, nv, x, y);
         const int dx = dims[x], dy = dims[y];
         const int32_t *T = pairtab + 16 * t;
         double r[4] = {0, 0, 0, 0}, c[4] = {0, 0, 0, 0}, n = 0.0;
-        for (int a = 0; a < dx; ++a)
+        for (int a = 0; a < dx; ++a)  // (dims <= 4 on this path)
             for (int b = 0; b < dy; ++b) {
-                const double v = T[a * dy + b];
-                r[a] += v, c[b] += v, n += v;
+                const double w = T[a * dy + b];
+                r[a] += w, c[b] += w, n += w;
             }
         double acc = 0.0;
         for (int a = 0; a < dx; ++a)
             for (int b = 0; b < dy; ++b) {
-                const double v = T[a * dy + b];
-                if (v > 0.0) acc += v * log(v * n / (r[a] * c[b]));
+                const double w = T[a * dy + b];
+                if (w > 0.0) acc += w * log(w * n / (r[a] * c[b]));
             }
-        mi[t] = n > 0.0 ? acc / n : 0.0;
+        g2[t] = 2.0 * acc;
     }
 }
 
@@ -1204,8 +1207,58 @@ __device__ __forceinline__ int l1_cand(const L1Edge &g, const int32_t *__restric
     return k < g.m0 ? adj[g.ax + k + (k >= g.skx)] : adj[g.ay + (k - g.m0) + ((k - g.m0) >= g.sky)];
 }
 
+// the screen, one wave per edge (64 candidates per step, ballots): count the candidates it keeps ...
+__device__ __forceinline__ L1Edge l1_edge_of(const int32_t *__restrict__ pairs, const int32_t *__restrict__ adj,
+                                             const int32_t *__restrict__ adj_off, int e) {
+    const int x = pairs[2 * e], y = pairs[2 * e + 1];
+    const int ax = adj_off[x], nx = adj_off[x + 1] - ax, ay = adj_off[y], ny = adj_off[y + 1] - ay;
+    int skx = find_sorted(adj + ax, nx, y), sky = find_sorted(adj + ay, ny, x);
+    const int m0 = skx >= 0 ? nx - 1 : nx, m1 = sky >= 0 ? ny - 1 : ny;
+    skx = skx >= 0 ? skx : nx + 1, sky = sky >= 0 ? sky : ny + 1;
+    return L1Edge{x, y, m0, m0 + m1, skx, sky, ax, ay, m0 + m1, -1};
+}
+__global__ __launch_bounds__(256) void ci_l1_screen_count(const int32_t *__restrict__ pairs, int E,
+                                                          const int32_t *__restrict__ adj,
+                                                          const int32_t *__restrict__ adj_off,
+                                                          const double *__restrict__ mi, const int32_t *__restrict__ dims,
+                                                          const double *__restrict__ band, int nband, int nv,
+                                                          double two_n, int32_t *__restrict__ pcnt) {
+    const int lane = threadIdx.x & 63;
+    for (int e = blockIdx.x * 4 + (threadIdx.x >> 6); e < E; e += gridDim.x * 4) {  // (whole waves)
+        const L1Edge g = l1_edge_of(pairs, adj, adj_off, e);
+        const double gxy = mi[l1_pidx(g.x, g.y, nv)];
+        int n = 0;
+        for (int k0 = 0; k0 < g.L; k0 += 64) {
+            const int k = k0 + lane;
+            n += __popcll(__ballot(k < g.L && l1_plausible(mi, nv, dims, band, nband, two_n, g.x, g.y, l1_cand(g, adj, k), gxy)));
+        }
+        if (lane == 0) pcnt[e] = n;
+    }
+}
+// ... and, once ci_l1_setup has placed every edge's list, write the kept positions in order
+__global__ __launch_bounds__(256) void ci_l1_screen_fill(const L1Edge *__restrict__ ed, int E,
+                                                         const int32_t *__restrict__ adj, const double *__restrict__ mi,
+                                                         const int32_t *__restrict__ dims,
+                                                         const double *__restrict__ band, int nband, int nv,
+                                                         double two_n, int32_t *__restrict__ plist) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    for (int e = blockIdx.x * 4 + (threadIdx.x >> 6); e < E; e += gridDim.x * 4) {
+        const L1Edge g = ed[e];
+        const double gxy = mi[l1_pidx(g.x, g.y, nv)];
+        int q = g.pl;
+        for (int k0 = 0; k0 < g.L; k0 += 64) {
+            const int k = k0 + lane;
+            const bool keep = k < g.L && l1_plausible(mi, nv, dims, band, nband, two_n, g.x, g.y, l1_cand(g, adj, k), gxy);
+            const unsigned long long m = __ballot(keep);
+            if (keep) plist[q + __popcll(m & below)] = k;
+            q += __popcll(m);
+        }
+    }
+}
+
 // (also the first round's lengths, chunk0 candidates per edge, and their offsets; both open-count
-// ring slots zeroed; with `mi`, the information screen's candidate lists first)
+// ring slots zeroed; with pcnt -- the screen's counts -- each edge's list offset pl first)
 __global__ __launch_bounds__(256) void ci_l1_setup(const int32_t *__restrict__ pairs, int E,
                                                    const int32_t *__restrict__ adj,
                                                    const int32_t *__restrict__ adj_off, L1Edge *__restrict__ ed,
@@ -1214,10 +1267,8 @@ __global__ __launch_bounds__(256) void ci_l1_setup(const int32_t *__restrict__ p
                                                    int chunk0, int32_t *__restrict__ len, int32_t *__restrict__ off,
                                                    unsigned *__restrict__ ring, unsigned long long *__restrict__ sstat,
                                                    long long cap, long long *__restrict__ scal,
-                                                   const double *__restrict__ mi, const int32_t *__restrict__ dims,
-                                                   const double *__restrict__ band, int nband, int nv, double two_n,
-                                                   int32_t *__restrict__ plist, unsigned long long *__restrict__ sstat2,
-                                                   long long *__restrict__ scal2) {
+                                                   const int32_t *__restrict__ pcnt,
+                                                   unsigned long long *__restrict__ sstat2, long long *__restrict__ scal2) {
     constexpr unsigned epoch = 1;
     unsigned *tickets = reinterpret_cast<unsigned *>(scal + 4);
     if (blockIdx.x == 0 && threadIdx.x < 2) ring[threadIdx.x] = 0u;
@@ -1229,7 +1280,6 @@ __global__ __launch_bounds__(256) void ci_l1_setup(const int32_t *__restrict__ p
         const int e = tile * 256 + threadIdx.x;
         int32_t l = 0;
         L1Edge g{};
-        double mxy = 0.0;
         if (e < E) {
             const int x = pairs[2 * e], y = pairs[2 * e + 1];
             const int ax = adj_off[x], nx = adj_off[x + 1] - ax, ay = adj_off[y], ny = adj_off[y + 1] - ay;
@@ -1237,21 +1287,12 @@ __global__ __launch_bounds__(256) void ci_l1_setup(const int32_t *__restrict__ p
             const int m0 = skx >= 0 ? nx - 1 : nx, m1 = sky >= 0 ? ny - 1 : ny;
             skx = skx >= 0 ? skx : nx + 1, sky = sky >= 0 ? sky : ny + 1;
             g = L1Edge{x, y, m0, m0 + m1, skx, sky, ax, ay, m0 + m1, -1};
-            if (mi) {  // the screen: count the candidates it keeps
-                mxy = mi[l1_pidx(x, y, nv)];
-                g.P = 0;
-                for (int k = 0; k < g.L; ++k) g.P += l1_plausible(mi, nv, dims, band, nband, two_n, x, y, l1_cand(g, adj, k), mxy);
-            }
+            if (pcnt) g.P = pcnt[e];  // the candidates the screen keeps (ci_l1_screen_count)
         }
-        if (mi) {  // their positions: plist[pl .. pl + P) in candidate order
+        if (pcnt) {  // their positions go to plist[pl .. pl + P) (ci_l1_screen_fill, after this kernel)
             int32_t pcount = e < E ? g.P : 0;
             const int32_t pl = l1_tile_scan(tile, ntiles, pcount, sstat2, epoch, 1ll << 62, scal2);
-            if (e < E) {
-                g.pl = pl;
-                int q = pl;
-                for (int k = 0; k < g.L; ++k)
-                    if (l1_plausible(mi, nv, dims, band, nband, two_n, g.x, g.y, l1_cand(g, adj, k), mxy)) plist[q++] = k;
-            }
+            if (e < E) g.pl = pl;
         }
         if (e < E) {
             ed[e] = g;
@@ -1553,29 +1594,33 @@ extern "C" hipError_t fbn_ci_kept_csr(const uint8_t *indep, int n, int32_t *low,
     return hipGetLastError();
 }
 
-// mi != nullptr: the information screen (pairwise I of the complete graph over nv variables, band
-// for the level's alpha, two_n = 2N, plist >= the level's candidate sets, sstat2 / scal2 a second
-// tile-status array (>= tiles) and 6 long longs of scratch)
+// mi != nullptr: the information screen first over mi = every pair's level-0 G^2 (indexed by pair;
+// computed here from the pair tables when mi_from_tables), band for the level's alpha, two_n = 2N,
+// pcnt >= E ints, plist >= the level's candidate sets, sstat2 / scal2 a second tile-status array
+// (>= tiles) and 4 long longs)
 extern "C" hipError_t fbn_ci_l1_setup(const int32_t *pairs, int E, const int32_t *adj, const int32_t *adj_off,
                                       void *ed, int32_t *pos, uint8_t *st, int32_t *sep, long long *counted,
                                       int chunk0, int32_t *len, int32_t *off, unsigned *ring,
                                       unsigned long long *sstat, long long cap, long long *scal, int num_cu,
-                                      const double *mi, const int32_t *dims, const double *band, int nband, int nv,
-                                      double two_n, int32_t *plist, unsigned long long *sstat2, long long *scal2,
-                                      hipStream_t s) {
+                                      const int32_t *pairtab, double *mi, int mi_from_tables, const int32_t *dims,
+                                      const double *band, int nband, int nv, double two_n, int32_t *pcnt,
+                                      int32_t *plist, unsigned long long *sstat2, long long *scal2, hipStream_t s) {
     const int ntiles = (E + 255) / 256;
-    if (E > 0)
-        hipLaunchKernelGGL(ci_l1_setup, dim3((unsigned)std::min(ntiles, num_cu * 4)), dim3(256), 0, s, pairs, E, adj,
-                           adj_off, (L1Edge *)ed, pos, st, sep, counted, chunk0, len, off, ring, sstat, cap, scal, mi,
-                           dims, band, nband, nv, two_n, plist, sstat2, scal2);
-    return hipGetLastError();
-}
-
-extern "C" hipError_t fbn_ci_pair_mi(const int32_t *pairtab, const int32_t *dims, int nv, long long P, double *mi,
-                                     hipStream_t s) {
-    const long long b = (P + 255) / 256;
-    if (P > 0)
-        hipLaunchKernelGGL(ci_pair_mi, dim3((unsigned)(b < 4096 ? b : 4096)), dim3(256), 0, s, pairtab, dims, nv, P, mi);
+    if (E <= 0) return hipSuccess;
+    const unsigned gw = (unsigned)std::min((E + 3) / 4, num_cu * 8);  // one wave per edge
+    if (mi) {
+        const long long P = (long long)nv * (nv - 1) / 2, b = (P + 255) / 256;
+        if (mi_from_tables)
+            hipLaunchKernelGGL(ci_pair_g2, dim3((unsigned)(b < 4096 ? b : 4096)), dim3(256), 0, s, pairtab, dims, nv, P, mi);
+        hipLaunchKernelGGL(ci_l1_screen_count, dim3(gw), dim3(256), 0, s, pairs, E, adj, adj_off, (const double *)mi,
+                           dims, band, nband, nv, two_n, pcnt);
+    }
+    hipLaunchKernelGGL(ci_l1_setup, dim3((unsigned)std::min(ntiles, num_cu * 4)), dim3(256), 0, s, pairs, E, adj,
+                       adj_off, (L1Edge *)ed, pos, st, sep, counted, chunk0, len, off, ring, sstat, cap, scal,
+                       mi ? (const int32_t *)pcnt : nullptr, sstat2, scal2);
+    if (mi)
+        hipLaunchKernelGGL(ci_l1_screen_fill, dim3(gw), dim3(256), 0, s, (const L1Edge *)ed, E, adj, (const double *)mi,
+                           dims, band, nband, nv, two_n, plist);
     return hipGetLastError();
 }
 
@@ -1603,9 +1648,15 @@ extern "C" hipError_t fbn_ci_l1_round(const uint32_t *bits, const int32_t *dims,
     hipLaunchKernelGGL(ci_l1_gen, gT, dim3(256), 0, s, ed, pos, off, E, total, adj, items, dims, rows_read, plist);
     hipLaunchKernelGGL(ci_bits_count_derived, gW, dim3(256), 0, s, bits, dims, row0, (const int32_t *)items, W, cap,
                        counts, pairtab, nvars, 1, total);
-    hipLaunchKernelGGL(ci_bits_g2<1>, gT, dim3(256), 0, s, (const int32_t *)counts, dims, (const int32_t *)items, cap,
-                       alpha, (double *)nullptr, df, (double *)nullptr, indep, (int32_t *)nullptr, stats, nvars, 0ll,
-                       band, nband, total);
+    // four lanes per test: the screened rounds are small (a few thousand to ~27k tests on config 5),
+    // where the lane-per-test kernel's single latency chain per test dominated (config 5: 0.22 ->
+    // 0.13 ms of G^2 per run; FBN_PC_L1_G2Q=0: lane per test)
+    static const bool quad = !(getenv("FBN_PC_L1_G2Q") && atoi(getenv("FBN_PC_L1_G2Q")) == 0);
+    const long long gq = (cap + kG2TestsPerBlock - 1) / kG2TestsPerBlock;
+    hipLaunchKernelGGL((quad ? ci_bits_g2q<1> : ci_bits_g2<1>), quad ? dim3((unsigned)(gq < gcap ? gq : gcap)) : gT,
+                       dim3(256), 0, s, (const int32_t *)counts, dims, (const int32_t *)items, cap, alpha,
+                       (double *)nullptr, df, (double *)nullptr, indep, (int32_t *)nullptr, stats, nvars, 0ll, band,
+                       nband, total);
     hipLaunchKernelGGL(ci_l1_resolve, dim3((unsigned)std::min(ntiles, num_cu * 4)), dim3(256), 0, s, ed, pos, len,
                        off, st, sep, counted, (const uint8_t *)indep, (const int32_t *)items, E, open_cnt, open_next,
                        next_chunk, sstat, epoch, cap, scal, plist);
