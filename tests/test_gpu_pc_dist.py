@@ -212,3 +212,25 @@ def test_nccl_world1_forced_exchange_configs_3_and_5(tmp_path):
     assert got["c5"]["tests"] == ref["tests_per_level"]
     assert {k: got["c5"][k] for k in ("edges_sha256", "sepsets_sha256")} == \
         {k: ref[k] for k in ("edges_sha256", "sepsets_sha256")}
+
+
+def test_bench_gpus_2_rehearsal_on_one_gpu():
+    """`bench.py --gpus 2` with no launcher starts two ranks itself (torch.distributed.run); with
+    FBN_BENCH_BACKEND=gloo they share the box's GPU.  Rank 0's line: two ranks seen, the ALARM JT
+    shards checked, config 5 through the distributed session equal to the fixture, and a roofline
+    on every leg (the N > 1 PC legs included)."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(GOLD.rstrip("/").rsplit("/", 1)[0])
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["FBN_BENCH_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--no-munin", "--no-loaders", "--no-baseline"], capture_output=True, text=True, env=env,
+                       timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["world_size_seen"] == 2
+    assert line["roofline"]["frac"] > 0 and line["roofline"]["full_batch_properties"]["ok"]
+    assert line["pc_synthetic"]["matches_fixture"] and line["pc_synthetic"]["roofline"]["frac"] > 0
+    assert line["pc_stable"]["matches_single_gpu"] and line["pc_stable"]["roofline"]["frac"] > 0
