@@ -518,3 +518,21 @@ def test_level1_information_screen_config5(monkeypatch):
     assert a.oriented == b.oriented
     la, lb = a.launched_per_level.tolist(), b.launched_per_level.tolist()
     assert la[1] < 0.5 * a.tests_per_level.tolist()[1] and lb[1] >= b.tests_per_level.tolist()[1]
+
+
+@pytest.mark.parametrize("alpha", [0.001, 0.01, 0.2, 0.5])
+def test_level1_information_screen_alphas_vs_oracle(alpha, monkeypatch):
+    """The screen's threshold moves with alpha (the band's hi per df): on a 200-variable config-5-like
+    dataset (20k samples: the device level-1 rounds run) the screened run equals the unscreened one
+    and the restatement -- tests per level, skeleton, sepsets."""
+    from fastbn_amd import synth
+    cols, dims = synth.config5_dataset(200, 20000)
+    ci = F.IndependenceTest(F.Dataset(columns=cols, dims=dims))
+    a = F.PCStable(alpha, 6).StructLearnCompData(ci)
+    monkeypatch.setenv("FBN_PC_NO_MISCREEN", "1")
+    b = F.PCStable(alpha, 6).StructLearnCompData(F.IndependenceTest(F.Dataset(columns=cols, dims=dims)))
+    monkeypatch.delenv("FBN_PC_NO_MISCREEN")
+    o = O.OracleDataset(columns=cols, dims=dims).pc_stable(alpha, 6, 1)
+    assert a.tests_per_level.tolist() == b.tests_per_level.tolist() == o["tests_per_level"]
+    assert a.edges == b.edges == o["edges"] and a.sepset == b.sepset == o["sepset"]
+    assert a.launched_per_level.tolist()[1] <= b.launched_per_level.tolist()[1]
