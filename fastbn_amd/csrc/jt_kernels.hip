@@ -715,8 +715,8 @@ static __global__ __launch_bounds__(256) void jt_marg_transpose(const double *__
                                                                 long long n, int SD) {
     __shared__ double tile[32][33];
     const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
-    const long long c0 = (long long)blockIdx.y * 32;
-    const int k0 = blockIdx.x * 32;
+    const long long c0 = (long long)blockIdx.x * 32;  // cases on x (up to 2^31 - 1 tiles), values on y
+    const int k0 = blockIdx.y * 32;
     for (int r = ty; r < 32; r += 8) {
         const long long c = c0 + r;
         const int k = k0 + tx;
@@ -732,9 +732,9 @@ static __global__ __launch_bounds__(256) void jt_marg_transpose(const double *__
 
 extern "C" hipError_t fbn_jt_marg_transpose(const double *in, double *out, long long n, int SD, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    const long long gy = (n + 31) / 32;
-    if (gy > 65535LL * 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(jt_marg_transpose, dim3((unsigned)((SD + 31) / 32), (unsigned)gy), dim3(256), 0, s, in, out, n, SD);
+    const long long gx = (n + 31) / 32, gy = (SD + 31) / 32;
+    if (gx > 0x7FFFFFFFLL || gy > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(jt_marg_transpose, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, s, in, out, n, SD);
     return hipGetLastError();
 }
 

@@ -19,6 +19,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <new>
@@ -393,6 +395,8 @@ int fbn_pc_dist_apply(fbn_pc_dist *s, const int32_t *records, int *more) {
             p += 1 + d;
         }
     }
+    static const bool timing = getenv("FBN_PC_TIMING") != nullptr;  // diagnostic
+    auto ta = std::chrono::steady_clock::now();
     FlushSepsets(s);
     if (d == 0) s->res.sepset.set_level0(s->nvars, std::move(rm));  // edges = the complete graph (flags taken over)
     else s->pend_keys.assign(s->edges.begin(), s->edges.end());  // sepsets: FlushSepsets, below or next run
@@ -415,6 +419,10 @@ int fbn_pc_dist_apply(fbn_pc_dist *s, const int32_t *records, int *more) {
         for (int v = 0; v < n; ++v) s->adj[v].clear(), s->adj[v].reserve(deg[v]);
         for (auto &ed : s->edges) s->adj[ed.first].push_back(ed.second), s->adj[ed.second].push_back(ed.first);
         s->implicit0 = false;
+        if (timing)
+            fprintf(stderr, "pc dist apply level 0: records %.3f ms, skeleton %.3f ms\n",
+                    std::chrono::duration<double, std::milli>(ta - t0).count(),
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count());
     } else {
         fbn::ApplyRemovals(rm, s->edges, s->adj);
         s->pend_rm = std::move(rm);
