@@ -363,6 +363,7 @@ int fbn_pc_dist_apply(fbn_pc_dist *s, const int32_t *records, int *more) {
     std::vector<int> sep(d > 0 ? E * (size_t)d : 0, -1);
     int64_t counted = 0, launched = 0;
     std::vector<int64_t> kept;  // level 0: kept pair indices, ascending
+    if (d == 0) kept.reserve(E / 8 + 64);
     for (int r = 0; r < world; ++r) {
         const int32_t *rec = records + (size_t)r * s->rec_len;
         const int64_t b = s->cuts[r], n = s->cuts[r + 1] - b;
@@ -381,9 +382,26 @@ int fbn_pc_dist_apply(fbn_pc_dist *s, const int32_t *records, int *more) {
                 else
                     for (int k = 0; k < cnt; ++k) rm[b + 32 * w + k] = (char)((bits >> k) & 1u);
                 uint32_t m = ~bits & (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u));
-                while (m) {
-                    kept.push_back(b + 32 * w + __builtin_ctz(m));
-                    m &= m - 1;
+                // kept pairs are sparse (~6 % on config 5): up to four per word written without a
+                // data-dependent branch (a while-per-bit loop mispredicted ~2 branches per word:
+                // 0.25-0.4 ms per 499,500 pairs), more by the loop
+                const int c = __builtin_popcount(m);
+                const int64_t base = b + 32 * w;
+                if (c <= 4) {
+                    const size_t at = kept.size();
+                    kept.resize(at + 4);
+                    int64_t *o = kept.data() + at;
+#pragma GCC unroll 4
+                    for (int j = 0; j < 4; ++j) {
+                        o[j] = base + __builtin_ctz(m | 0x80000000u);
+                        m &= m - 1;
+                    }
+                    kept.resize(at + c);
+                } else {
+                    while (m) {
+                        kept.push_back(base + __builtin_ctz(m));
+                        m &= m - 1;
+                    }
                 }
             }
             continue;
