@@ -940,7 +940,7 @@ def main():
         local = local % max(1, torch.cuda.device_count())
     if world > 1 or os.environ.get("FBN_BENCH_FORCE_GATHER") == "1":
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29517")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))  # (world 1: no launcher set one)
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))

@@ -234,3 +234,21 @@ def test_bench_gpus_2_rehearsal_on_one_gpu():
     assert line["roofline"]["frac"] > 0 and line["roofline"]["full_batch_properties"]["ok"]
     assert line["pc_synthetic"]["matches_fixture"] and line["pc_synthetic"]["roofline"]["frac"] > 0
     assert line["pc_stable"]["matches_single_gpu"] and line["pc_stable"]["roofline"]["frac"] > 0
+
+
+def test_bench_rccl_final_gather_at_world1():
+    """The N > 1 headline's timed region over RCCL (FBN_BENCH_FORCE_GATHER=1: the process group and
+    the final all-gather of every step's labels at world size 1): the line is produced and the
+    gathered labels are checked inside bench.py."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(GOLD.rstrip("/").rsplit("/", 1)[0])
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["FBN_BENCH_FORCE_GATHER"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--steps", "3", "--warmup", "1", "--no-munin",
+                        "--no-pc", "--no-loaders", "--no-baseline"], capture_output=True, text=True, env=env,
+                       timeout=200)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 1 and line["world_size_seen"] == 1 and line["roofline"]["full_batch_properties"]["ok"]
