@@ -31,5 +31,6 @@ for _ in range(reps):
     jt.run_device(d_ev.data_ptr(), n, d_lab.data_ptr(), d_marg.data_ptr(), None)
     ms.append(jt.last_kernel_ms())
 torch.cuda.synchronize()
-print(f"{os.environ.get('FBN_JT_TPOL', '0')}: kernel ms {np.median(ms):.1f} ({' '.join(f'{m:.1f}' for m in ms)}), "
+knobs = " ".join(f"{k}={v}" for k, v in sorted(os.environ.items()) if k.startswith("FBN_JT_"))
+print(f"[{knobs}] visits={jt.info['tiled_entry_visits']}: kernel ms {np.median(ms):.1f} ({' '.join(f'{m:.1f}' for m in ms)}), "
       f"labels stable {bool(torch.equal(lab0, d_lab))}", flush=True)
