@@ -18,6 +18,8 @@ synth.random_network(1041, seed=1041, window=12, path=path, name="munin_like")
 net = F.Network(path)
 ev = net.evidence_cases(n, 208, 20250131)
 jt = F.JunctionTree(net, device=0)
+if os.environ.get("FBN_WPC"):  # waves per CU of the launch (tuning)
+    jt.set_waves_per_cu(int(os.environ["FBN_WPC"]))
 d_ev = torch.from_numpy(ev).cuda()
 d_lab = torch.empty(n, dtype=torch.int32, device="cuda")
 d_marg = torch.empty((n, jt.info["sum_dom"]), dtype=torch.float64, device="cuda")
@@ -31,6 +33,6 @@ for _ in range(reps):
     jt.run_device(d_ev.data_ptr(), n, d_lab.data_ptr(), d_marg.data_ptr(), None)
     ms.append(jt.last_kernel_ms())
 torch.cuda.synchronize()
-knobs = " ".join(f"{k}={v}" for k, v in sorted(os.environ.items()) if k.startswith("FBN_JT_"))
+knobs = " ".join(f"{k}={v}" for k, v in sorted(os.environ.items()) if k.startswith("FBN_JT_") or k == "FBN_WPC")
 print(f"[{knobs}] visits={jt.info['tiled_entry_visits']}: kernel ms {np.median(ms):.1f} ({' '.join(f'{m:.1f}' for m in ms)}), "
       f"labels stable {bool(torch.equal(lab0, d_lab))}", flush=True)
