@@ -894,8 +894,11 @@ def launcher_check(world, rank):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # defaults: 100 timed steps (12 ms at N = 1) after 100 warm-up steps -- a cold MI355X needs
+    # ~15 ms of work to reach steady clocks (tools/alarm_knob_probe.py: 0.124 ms per step over the first
+    # 50 steps, 0.117 from ~150 on); the driver's own --steps / --warmup take precedence
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--cases", type=int, default=CASES_PER_GPU)
     ap.add_argument("--waves-per-cu", type=int, default=0)
     ap.add_argument("--no-baseline", action="store_true")
