@@ -738,9 +738,9 @@ def bench_munin(steps, warmup, cases=125_000, rank=0, world=1, device=0, with_ba
 
 def munin_traffic(cases, kernel_ms):
     """Measured L2<->fabric bytes of the streamed kernel (rocprofv3 FETCH_SIZE + WRITE_SIZE, calibrated;
-    committed summary profiles/r05/munin_traffic.json from tools/profile_r05_final.sh), scaled to this launch,
+    committed summary profiles/r06/munin_traffic.json from tools/profile_r06_munin.sh), scaled to this launch,
     and the rate they imply at this launch's kernel time."""
-    path = _first_profile("r05/munin_traffic.json", "munin_traffic.json")
+    path = _first_profile("r06/munin_traffic.json", "r05/munin_traffic.json", "munin_traffic.json")
     if path is None:
         return {"traffic": None}
     with open(path) as f:

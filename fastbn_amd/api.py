@@ -7,7 +7,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfastbn.so")
+# FBN_LIB_PATH: an alternative build of the same library (A/B runs of build-time switches, tools/)
+LIB_PATH = os.environ.get("FBN_LIB_PATH") or os.path.join(_HERE, "libfastbn.so")
 
 _vp, _i32, _i64, _dbl, _cstr = C.c_void_p, C.c_int32, C.c_int64, C.c_double, C.c_char_p
 _pp = C.POINTER(C.c_void_p)

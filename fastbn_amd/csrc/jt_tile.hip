@@ -38,6 +38,18 @@ static_assert(C * L == 64, "one wave = C cases x L slots");
 constexpr int kValChunks = 2;  // marginal sweep: value d in slot d % L, chunk (d % kGrp) / L
 constexpr int kGrp = kValChunks * L;  // values per bin sweep (more states: one sweep per group)
 constexpr int kBinRows = JT_T_LDS_BIN_ROWS;  // bin sets up to this many rows live in LDS
+#ifndef FBN_TILE_REUSE
+#define FBN_TILE_REUSE 0  // 1: skip the load of a factor row equal to the step before's (bit 0 of its soffset)
+#endif
+#ifndef FBN_TILE_U
+#define FBN_TILE_U 4  // steps per load batch
+#endif
+#ifndef FBN_TILE_VREC
+#define FBN_TILE_VREC 0  // 1: step records by vector loads one chunk ahead (else scalar loads one batch ahead)
+#endif
+#ifndef FBN_TILE_STEPBRK
+#define FBN_TILE_STEPBRK 1  // leave the unrolled batch at the step range's end (else: bin ends masked)
+#endif
 constexpr int kMaxCliqueVars = 10;           // evidence bytes loaded together; wider cliques (up to 32
                                              // digit bits, jt_tile_plan.cpp) take the rest in a loop
 
@@ -113,8 +125,15 @@ struct PassOut {
 // soffsets, digit word, the bin of the inner run ending there), one digit test and NF factor loads
 // (LDS: one address add; wave store: voffset + soffset).  The sum of an inner run goes to its bin
 // (LDS rows for small bin sets, else the wave store).  Factors 0 .. NL-1 are in LDS, the rest in the
-// wave store.  A factor whose row is the one of the step before (bit 0 of its soffset, set by the
-// plan, which orders the R stream to make that common) is not loaded again: the lane keeps the value
+// wave store.  Every factor is loaded at every step (round 6): a batch's loads are then one
+// straight-line block the compiler can issue back to back and wait for one step at a time.  Bit 0 of
+// a factor's soffset (set by the plan, which orders the R stream to make it common) marks "the same
+// row as the step before"; skipping that load (FBN_TILE_REUSE=1, the round-4 form) costs a scalar
+// branch per factor and step, splits the batch into basic blocks and measured 203 ms against 181-185
+// ms for the branch-free loads (125k Munin-like cases; the repeated row is an L1 hit).  Build-time
+// switches measured the same day and not kept: FBN_TILE_VREC=1 (step records as vector loads one chunk
+// ahead, read out by v_readlane, so an LDS wait no longer waits for scalar record loads: 206 ms, VGPR
+// spills), FBN_TILE_U=2 (190 ms), FBN_TILE_STEPBRK=0 (184 vs 185 ms, noise)
 template <int NF, int NL>
 __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *__restrict__ tab,
                                                __amdgpu_buffer_rsrc_t ivrs, __amdgpu_buffer_rsrc_t st,
@@ -122,7 +141,7 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
                                                const PassOut &O) {
     static_assert(C == 16, "a chunk = the 16 lanes of a DPP row");
     constexpr int RS = NF + 2, GS = 4 + NF, NFA = NF > 0 ? NF : 1;
-    constexpr int U = 4;  // steps with their loads in flight together
+    constexpr int U = FBN_TILE_U;  // steps with their loads in flight together
     const int g8 = g * 8;
     double tot = 0.0;
     const uint32_t gf = (uint32_t)P.gfields;
@@ -147,6 +166,16 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
         for (int j = 0; j < NFA; ++j) fe[j] = 0.0;
         // slot s's entry at step k0 + g, one chunk ahead (the tables are padded by one chunk)
         double wn = bld(ivrs, ivb + et[kb + g], 0);
+#if FBN_TILE_VREC
+        // the step records of a chunk (C steps x RS words) arrive one chunk ahead as VECTOR loads (lane
+        // l holds word l + 64 v) and are read out with v_readlane per batch: vector loads complete in
+        // order, so waiting for a batch's LDS factors (lgkmcnt) no longer waits for record loads too
+        constexpr int RW = C * RS, NV = (RW + 63) / 64;
+        const int ln = s * C + g;
+        int32_t rc[NV], rn[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) rc[v] = v * 64 + ln < RW ? sr[(size_t)kb * RS + v * 64 + ln] : 0;
+#else
         // the step records of the batch in flight (qc) and of the next one (qn): the next batch's
         // scalar loads are issued before this batch computes, so a scalar-cache miss is not on the
         // batch's critical path (the records are padded past every wave's last step)
@@ -155,44 +184,75 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int i = 0; i < RS; ++i) qc[u][i] = sr[(size_t)(kb + u) * RS + i];
+#endif
         for (int k0 = kb; k0 < ke; k0 += C) {
             const double wl = wn;
             if (k0 + C < ke) wn = bld(ivrs, ivb + et[k0 + C + g], 0);
+#if FBN_TILE_VREC
+            if (k0 + C < ke) {
+#pragma unroll
+                for (int v = 0; v < NV; ++v)
+                    rn[v] = v * 64 + ln < RW ? sr[(size_t)(k0 + C) * RS + v * 64 + ln] : 0;
+            }
+#endif
 #pragma unroll
             for (int u0 = 0; u0 < C; u0 += U) {
                 if (k0 + u0 >= ke) break;  // (uniform)
                 double w[U], f[U][NFA];
                 bool ok[U];
+#if FBN_TILE_VREC
+                int32_t qc[U][RS];
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int i = 0; i < RS; ++i) {
+                        const int wi = (u0 + u) * RS + i;
+                        qc[u][i] = __builtin_amdgcn_readlane(rc[wi / 64], wi % 64);
+                    }
+#endif
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     ok[u] = (((uint32_t)qc[u][NF]) & MR) == WR;
 #pragma unroll
                     for (int j = 0; j < NF; ++j) {
+#if FBN_TILE_REUSE
                         if (qc[u][j] & 1) continue;  // (uniform) the row of the step before
-                        if (j < NL) f[u][j] = *reinterpret_cast<const double *>(ldsb + (fG[j] + qc[u][j]));  // bytes
-                        else f[u][j] = bld(st, fG[j], qc[u][j]);
+#endif
+                        const int qo = FBN_TILE_REUSE ? qc[u][j] : qc[u][j] & ~1;
+                        if (j < NL) f[u][j] = *reinterpret_cast<const double *>(ldsb + (fG[j] + qo));  // bytes
+                        else f[u][j] = bld(st, fG[j], qo);
                     }
                 }
+#if !FBN_TILE_VREC
                 int32_t qn[U][RS];
 #pragma unroll
                 for (int u = 0; u < U; ++u)
 #pragma unroll
                     for (int i = 0; i < RS; ++i) qn[u][i] = sr[(size_t)(k0 + u0 + U + u) * RS + i];
+#endif
 #pragma unroll
                 for (int u = 0; u < U; ++u) w[u] = row_bcast_n(wl, u0 + u);
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const int k = k0 + u0 + u;
+#if FBN_TILE_STEPBRK
                     if (k >= ke) break;
+#endif
                     double x = w[u];
 #pragma unroll
                     for (int j = 0; j < NF; ++j) {
+#if FBN_TILE_REUSE
                         if (!(qc[u][j] & 1)) fe[j] = f[u][j];
+#else
+                        fe[j] = f[u][j];
+#endif
                         x *= fe[j];
                     }
                     acc += ok[u] ? x : 0.0;
                     const int xo = qc[u][NF + 1];
-                    if (xo != -1) {  // end of an inner run (or of its chunk, loop-tiled): its bin
+                    // (steps past ke, up to the batch's end: padding, or the next wave's share -- summed
+                    // into acc, never written: acc restarts with the next round)
+                    if (xo != -1 && (FBN_TILE_STEPBRK || k < ke)) {  // end of an inner run (or of its chunk, loop-tiled): its bin
                         const bool add = xo < -1;  // (a later chunk: add into the bin, which this
                         const int xb = add ? -xo - 2 : xo;  // lane wrote in an earlier chunk)
                         const double a = okG ? acc : 0.0;
@@ -217,11 +277,17 @@ __device__ __forceinline__ double pass_entries(const JtTPass &P, const int32_t *
                         acc = 0.0;
                     }
                 }
+#if !FBN_TILE_VREC
 #pragma unroll
                 for (int u = 0; u < U; ++u)
 #pragma unroll
                     for (int i = 0; i < RS; ++i) qc[u][i] = qn[u][i];
+#endif
             }
+#if FBN_TILE_VREC
+#pragma unroll
+            for (int v = 0; v < NV; ++v) rc[v] = rn[v];
+#endif
         }
     }
     return tot;

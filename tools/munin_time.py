@@ -35,4 +35,5 @@ for _ in range(reps):
 torch.cuda.synchronize()
 knobs = " ".join(f"{k}={v}" for k, v in sorted(os.environ.items()) if k.startswith("FBN_JT_") or k == "FBN_WPC")
 print(f"[{knobs}] visits={jt.info['tiled_entry_visits']}: kernel ms {np.median(ms):.1f} ({' '.join(f'{m:.1f}' for m in ms)}), "
-      f"labels stable {bool(torch.equal(lab0, d_lab))}", flush=True)
+      f"labels stable {bool(torch.equal(lab0, d_lab))} labels-sum {int(d_lab.long().sum())} "
+      f"marg-sum {float(d_marg.sum()):.12f} flagged {jt.info.get('flagged_blocks', 'n/a')}", flush=True)
